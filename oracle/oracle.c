@@ -1,0 +1,393 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY (see oracle.h). Plain C restatement of
+ *   cover/cover.go            (set algebra, Canonicalize, Minimize)
+ *   prog/prio.go              (calcDynamicPrio, normalizePrio, CalculatePriorities, BuildChoiceTable)
+ *   syz-manager/manager.go    (minimizeCorpus grouping, NewInput novelty)
+ *   syz-fuzzer/fuzzer.go      (execute novelty vs maxCover/flakes)
+ * Compiled with -ffp-contract=off and without fast-math: Go on amd64 rounds every float32 op
+ * separately.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gosort.h"
+
+#define SENT 0xFFFFFFFFu /* cover/cover.go:17 */
+
+/* ---- sort.Sort instantiations ------------------------------------------------------------- */
+
+/* cover/cover.go:13-15  Cover.Less(i, j) = a[i] < a[j] */
+#define COVER_LESS(x, y) ((x) < (y))
+GOSORT_DEFINE(gosort_cover, uint32_t, COVER_LESS)
+
+/* cover/cover.go:133-143  minInput{idx, cov}; Less(i, j) = len(a[i].cov) > len(a[j].cov) */
+typedef struct {
+  int64_t idx;
+  uint64_t len;
+  const uint32_t* cov;
+} min_input;
+#define MININPUT_LESS(x, y) ((x).len > (y).len)
+GOSORT_DEFINE(gosort_mininput, min_input, MININPUT_LESS)
+
+/* ---- cover/cover.go ------------------------------------------------------------------------ */
+
+int oracle_canonicalize(uint32_t* cov, size_t n, size_t* out_n) {
+  /* cover.go:29 sort.Sort(Cover(cov)); :30-38 dedup with last = sent */
+  gosort_cover(cov, (long)n);
+  size_t i = 0;
+  uint32_t last = SENT;
+  for (size_t k = 0; k < n; k++) {
+    uint32_t pc = cov[k];
+    if (pc != last) {
+      last = pc;
+      cov[i++] = pc;
+    }
+  }
+  *out_n = i;
+  return 0;
+}
+
+static inline uint32_t apply_op(int op, uint32_t v0, uint32_t v1) {
+  switch (op) {
+    case 0: /* Difference cover.go:42-49 */
+      return v0 < v1 ? v0 : SENT;
+    case 1: /* SymmetricDifference cover.go:51-61 */
+      if (v0 < v1) return v0;
+      if (v1 < v0) return v1;
+      return SENT;
+    case 2: /* Union cover.go:63-70 */
+      return v0 <= v1 ? v0 : v1;
+    default: /* Intersection cover.go:72-79 */
+      return v0 == v1 ? v0 : SENT;
+  }
+}
+
+int oracle_setop(int op, const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out,
+                 size_t cap, size_t* out_n) {
+  if (op < 0 || op > 3) return 1;
+  /* cover.go:81-102 foreach */
+  size_t n = 0;
+  for (size_t i0 = 0, i1 = 0; i0 < na || i1 < nb;) {
+    uint32_t v0 = SENT, v1 = SENT;
+    if (i0 < na) v0 = a[i0];
+    if (i1 < nb) v1 = b[i1];
+    if (v0 <= v1) i0++;
+    if (v1 <= v0) i1++;
+    uint32_t v = apply_op(op, v0, v1);
+    if (v != SENT) {
+      if (n >= cap) return 6;
+      out[n++] = v;
+    }
+  }
+  *out_n = n;
+  return 0;
+}
+
+/* Open-addressing uint32 set standing in for Go's map[uint32]struct{} (cover.go:115). Slots hold
+ * key+1 so that every uint32 (including 0 and 0xFFFFFFFF, both legal map keys) is storable. */
+typedef struct {
+  uint64_t* slot;
+  size_t mask, count;
+} u32set;
+
+static void u32set_init(u32set* s, size_t hint) {
+  size_t cap = 64;
+  while (cap < hint * 2) cap <<= 1;
+  s->slot = (uint64_t*)calloc(cap, sizeof(uint64_t));
+  s->mask = cap - 1;
+  s->count = 0;
+}
+static inline size_t u32hash(uint32_t k) {
+  uint64_t h = (uint64_t)k * 0x9E3779B97F4A7C15ull;
+  return (size_t)(h >> 32);
+}
+static void u32set_grow(u32set* s);
+static inline int u32set_has(const u32set* s, uint32_t k) {
+  for (size_t i = u32hash(k) & s->mask;; i = (i + 1) & s->mask) {
+    uint64_t v = s->slot[i];
+    if (v == 0) return 0;
+    if (v == (uint64_t)k + 1) return 1;
+  }
+}
+static inline void u32set_add(u32set* s, uint32_t k) {
+  if ((s->count + 1) * 2 > s->mask + 1) u32set_grow(s);
+  for (size_t i = u32hash(k) & s->mask;; i = (i + 1) & s->mask) {
+    uint64_t v = s->slot[i];
+    if (v == 0) {
+      s->slot[i] = (uint64_t)k + 1;
+      s->count++;
+      return;
+    }
+    if (v == (uint64_t)k + 1) return;
+  }
+}
+static void u32set_grow(u32set* s) {
+  u32set n;
+  u32set_init(&n, (s->mask + 1));
+  for (size_t i = 0; i <= s->mask; i++)
+    if (s->slot[i]) u32set_add(&n, (uint32_t)(s->slot[i] - 1));
+  free(s->slot);
+  *s = n;
+}
+
+static int minimize_core(min_input* inputs, size_t n, int64_t* out_idx, size_t* out_n) {
+  /* cover.go:113 sort.Sort(minInputArray(inputs)) */
+  gosort_mininput(inputs, (long)n);
+  /* cover.go:114-129 greedy selection against a covered-PC map */
+  size_t total = 0;
+  for (size_t i = 0; i < n; i++) total += inputs[i].len;
+  u32set covered;
+  u32set_init(&covered, total < 1024 ? 1024 : total / 4);
+  size_t m = 0;
+  for (size_t i = 0; i < n; i++) {
+    int hit = 0;
+    const uint32_t* cov = inputs[i].cov;
+    for (uint64_t k = 0; k < inputs[i].len; k++) {
+      uint32_t pc = cov[k];
+      if (!hit) {
+        if (!u32set_has(&covered, pc)) {
+          hit = 1;
+          out_idx[m++] = inputs[i].idx;
+        }
+      }
+      if (hit) u32set_add(&covered, pc);
+    }
+  }
+  free(covered.slot);
+  *out_n = m;
+  return 0;
+}
+
+int oracle_minimize(const uint32_t* pcs, const uint64_t* off, size_t ncov, int64_t* out_idx,
+                    size_t* out_n) {
+  /* cover.go:106-112 inputs[i] = &minInput{idx: i, cov: cov} */
+  min_input* inputs = (min_input*)malloc((ncov ? ncov : 1) * sizeof(min_input));
+  for (size_t i = 0; i < ncov; i++) {
+    inputs[i].idx = (int64_t)i;
+    inputs[i].len = off[i + 1] - off[i];
+    inputs[i].cov = pcs + off[i];
+  }
+  int rc = minimize_core(inputs, ncov, out_idx, out_n);
+  free(inputs);
+  return rc;
+}
+
+int oracle_minimize_order(const uint64_t* lens, size_t n, int64_t* perm) {
+  min_input* inputs = (min_input*)malloc((n ? n : 1) * sizeof(min_input));
+  for (size_t i = 0; i < n; i++) {
+    inputs[i].idx = (int64_t)i;
+    inputs[i].len = lens[i];
+    inputs[i].cov = NULL;
+  }
+  gosort_mininput(inputs, (long)n);
+  for (size_t i = 0; i < n; i++) perm[i] = inputs[i].idx;
+  free(inputs);
+  return 0;
+}
+
+int oracle_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                            size_t n, uint32_t ngroups, int64_t* out_idx, uint64_t* group_out_off) {
+  /* manager.go:514-520: bucket inputs per call, keeping corpus order inside a bucket */
+  uint64_t* cnt = (uint64_t*)calloc((size_t)ngroups + 1, sizeof(uint64_t));
+  for (size_t i = 0; i < n; i++) {
+    if (group[i] >= ngroups) {
+      free(cnt);
+      return 1;
+    }
+    cnt[group[i] + 1]++;
+  }
+  for (uint32_t g = 0; g < ngroups; g++) cnt[g + 1] += cnt[g];
+  uint64_t* fill = (uint64_t*)malloc(((size_t)ngroups + 1) * sizeof(uint64_t));
+  memcpy(fill, cnt, ((size_t)ngroups + 1) * sizeof(uint64_t));
+  int64_t* members = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+  for (size_t i = 0; i < n; i++) members[fill[group[i]]++] = (int64_t)i;
+  min_input* inputs = (min_input*)malloc((n ? n : 1) * sizeof(min_input));
+  int64_t* sel = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+  size_t outp = 0;
+  group_out_off[0] = 0;
+  /* manager.go:522-527: Minimize each bucket, append the kept inputs */
+  for (uint32_t g = 0; g < ngroups; g++) {
+    size_t ng = (size_t)(cnt[g + 1] - cnt[g]);
+    for (size_t i = 0; i < ng; i++) {
+      int64_t e = members[cnt[g] + i];
+      inputs[i].idx = (int64_t)i;
+      inputs[i].len = off[e + 1] - off[e];
+      inputs[i].cov = pcs + off[e];
+    }
+    size_t m = 0;
+    minimize_core(inputs, ng, sel, &m);
+    for (size_t k = 0; k < m; k++) out_idx[outp++] = members[cnt[g] + sel[k]];
+    group_out_off[g + 1] = outp;
+  }
+  free(cnt);
+  free(fill);
+  free(members);
+  free(inputs);
+  free(sel);
+  return 0;
+}
+
+/* ---- prog/prio.go -------------------------------------------------------------------------- */
+
+void oracle_normalize_prio(float* prios, int32_t C) {
+  /* prio.go:158-192, every op rounded to float32 separately */
+  for (int32_t r = 0; r < C; r++) {
+    float* prio = prios + (size_t)r * C;
+    float max = 0.0f;
+    float min = 1e10f;
+    long nzero = 0;
+    for (int32_t i = 0; i < C; i++) {
+      float p = prio[i];
+      if (max < p) max = p;
+      if (p != 0 && min > p) min = p;
+      if (p == 0) nzero++;
+    }
+    if (nzero != 0) {
+      volatile float den = 2.0f * (float)nzero;
+      min /= den;
+    }
+    for (int32_t i = 0; i < C; i++) {
+      float p = prio[i];
+      if (max == 0) {
+        prio[i] = 1;
+        continue;
+      }
+      if (p == 0) p = min;
+      volatile float t1 = p - min;
+      volatile float t2 = max - min;
+      volatile float t3 = t1 / t2;
+      volatile float t4 = t3 * 0.9f;
+      p = t4 + 0.1f;
+      if (p > 1) p = 1;
+      prio[i] = p;
+    }
+  }
+}
+
+int oracle_dynamic_prio(const uint16_t* prog_len, size_t nprogs, int32_t C, float* out) {
+  if (C <= 0) return 1;
+  for (size_t p = 0; p < nprogs; p++)
+    if ((int32_t)prog_len[p] > C) return 1; /* Go: index out of range panic (prio.go:148) */
+  memset(out, 0, sizeof(float) * (size_t)C * (size_t)C);
+  /* prio.go:142-151: += 1.0 for every ordered pair of call *positions*  */
+  for (size_t p = 0; p < nprogs; p++) {
+    int32_t L = prog_len[p];
+    for (int32_t i0 = 0; i0 < L; i0++)
+      for (int32_t i1 = 0; i1 < L; i1++) {
+        if (i0 == i1) continue;
+        out[(size_t)i0 * C + i1] += 1.0f;
+      }
+  }
+  oracle_normalize_prio(out, C); /* prio.go:152 */
+  return 0;
+}
+
+int oracle_calculate_priorities(const float* static_prios, const uint16_t* prog_len, size_t nprogs,
+                                int32_t C, float* out) {
+  int rc = oracle_dynamic_prio(prog_len, nprogs, C, out); /* prio.go:31 */
+  if (rc) return rc;
+  /* prio.go:32-36 dynamic[i][j] *= static[i][j] */
+  for (size_t k = 0; k < (size_t)C * (size_t)C; k++) {
+    volatile float v = out[k] * static_prios[k];
+    out[k] = v;
+  }
+  return 0;
+}
+
+/* Go on amd64 converts float32 -> int with CVTTSS2SQ: truncation toward zero; NaN and
+ * out-of-range values give the "integer indefinite" 0x8000000000000000. */
+static inline int64_t go_f32_to_int(float x) {
+  if (x != x) return INT64_MIN;
+  if (x >= 9223372036854775808.0f || x < -9223372036854775808.0f) return INT64_MIN;
+  return (int64_t)x;
+}
+
+int oracle_build_choice_table(const float* prios, const uint8_t* enabled, int32_t C, int64_t* run,
+                              uint8_t* row_present) {
+  if (C <= 0) return 1;
+  /* prio.go:213-226 */
+  for (int32_t i = 0; i < C; i++) {
+    int64_t* row = run + (size_t)i * C;
+    if (enabled && !enabled[i]) {
+      row_present[i] = 0;
+      memset(row, 0, sizeof(int64_t) * (size_t)C);
+      continue;
+    }
+    row_present[i] = 1;
+    uint64_t sum = 0; /* Go int arithmetic wraps */
+    for (int32_t j = 0; j < C; j++) {
+      if (!enabled || enabled[j]) {
+        volatile float t = prios[(size_t)i * C + j] * 1000.0f;
+        sum += (uint64_t)go_f32_to_int(t);
+      }
+      row[j] = (int64_t)sum;
+    }
+  }
+  return 0;
+}
+
+/* ---- syz-fuzzer/fuzzer.go:446-470 execute (novelty vs maxCover/flakes) ---------------------- */
+
+int oracle_novelty(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                   uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off,
+                   const uint32_t* flakes, size_t nflakes, uint8_t* is_new, uint32_t* out_mc,
+                   uint64_t* out_mc_off, size_t out_cap) {
+  /* per-group maxCover tables as growable arrays */
+  uint32_t** tab = (uint32_t**)calloc(ngroups ? ngroups : 1, sizeof(uint32_t*));
+  size_t* tlen = (size_t*)calloc(ngroups ? ngroups : 1, sizeof(size_t));
+  int rc = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    tlen[g] = (size_t)(mc_off[g + 1] - mc_off[g]);
+    tab[g] = (uint32_t*)malloc((tlen[g] ? tlen[g] : 1) * sizeof(uint32_t));
+    memcpy(tab[g], mc + mc_off[g], tlen[g] * sizeof(uint32_t));
+  }
+  for (size_t k = 0; k < n && !rc; k++) {
+    uint32_t g = group[k];
+    if (g >= ngroups) {
+      rc = 1;
+      break;
+    }
+    const uint32_t* cov = pcs + off[k];
+    size_t L = (size_t)(off[k + 1] - off[k]);
+    is_new[k] = 0;
+    if (L == 0) continue; /* fuzzer.go:451-453 */
+    /* diff := Difference(cov, maxCover[c.CallID]); diff = Difference(diff, flakes) */
+    uint32_t* d1 = (uint32_t*)malloc(L * sizeof(uint32_t));
+    uint32_t* d2 = (uint32_t*)malloc(L * sizeof(uint32_t));
+    size_t n1 = 0, n2 = 0;
+    oracle_setop(0, cov, L, tab[g], tlen[g], d1, L, &n1);
+    oracle_setop(0, d1, n1, flakes, nflakes, d2, L, &n2);
+    if (n2 != 0) {
+      /* maxCover[c.CallID] = Union(maxCover[c.CallID], diff) */
+      uint32_t* u = (uint32_t*)malloc((tlen[g] + n2) * sizeof(uint32_t));
+      size_t nu = 0;
+      oracle_setop(2, tab[g], tlen[g], d2, n2, u, tlen[g] + n2, &nu);
+      free(tab[g]);
+      tab[g] = u;
+      tlen[g] = nu;
+      is_new[k] = 1;
+    }
+    free(d1);
+    free(d2);
+  }
+  size_t p = 0;
+  out_mc_off[0] = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    if (!rc) {
+      if (p + tlen[g] > out_cap) {
+        rc = 6;
+      } else {
+        memcpy(out_mc + p, tab[g], tlen[g] * sizeof(uint32_t));
+        p += tlen[g];
+      }
+    }
+    out_mc_off[g + 1] = p;
+    free(tab[g]);
+  }
+  free(tab);
+  free(tlen);
+  return rc;
+}

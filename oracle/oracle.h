@@ -1,0 +1,73 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded restatement of the reference's corpus-analytics path, used as the
+ * parity checker for libsyzgpu.so and as the CPU baseline ("kind": "port") in bench.py.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load liboracle.so.
+ * The product library never links it and has no CPU fallback through it.
+ *
+ * Each function cites the reference file:line it restates (paths relative to the reference root).
+ * Status codes mirror include/syzgpu.h (0 = ok, 1 = invalid argument, 6 = capacity too small).
+ */
+#ifndef SYZ_ORACLE_H
+#define SYZ_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cover/cover.go:28-40  Canonicalize: in-place Go sort.Sort + unique, sentinel 0xFFFFFFFF start. */
+int oracle_canonicalize(uint32_t* cov, size_t n, size_t* out_n);
+
+/* cover/cover.go:42-102  foreach-based set ops.  op: 0 Difference, 1 SymmetricDifference,
+ * 2 Union, 3 Intersection.  *out_n = result length (Go returns nil when 0). */
+int oracle_setop(int op, const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out,
+                 size_t cap, size_t* out_n);
+
+/* cover/cover.go:105-143  Minimize over one corpus given as CSR (off has ncov+1 entries).
+ * out_idx receives the selected indices in selection order. */
+int oracle_minimize(const uint32_t* pcs, const uint64_t* off, size_t ncov, int64_t* out_idx,
+                    size_t* out_n);
+
+/* syz-manager/manager.go:507-527 minimizeCorpus: per-group Minimize. Groups are processed in
+ * ascending group id (the reference iterates a Go map, i.e. random order — SURVEY.md F7).
+ * out_idx receives corpus entry ids, group-major; group_out_off (ngroups+1) the group offsets. */
+int oracle_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                            size_t n, uint32_t ngroups, int64_t* out_idx, uint64_t* group_out_off);
+
+/* The Go-sort permutation Minimize uses: perm[p] = index (within the group) of the input at sorted
+ * position p, for a list of cover lengths (cover/cover.go:106-113, 140-143). */
+int oracle_minimize_order(const uint64_t* lens, size_t n, int64_t* perm);
+
+/* prog/prio.go:137-154 calcDynamicPrio + :158-192 normalizePrio. prog_len[i] = len(p.Calls).
+ * out is C*C row-major float32. */
+int oracle_dynamic_prio(const uint16_t* prog_len, size_t nprogs, int32_t C, float* out);
+
+/* prog/prio.go:158-192 normalizePrio on a C*C matrix in place. */
+void oracle_normalize_prio(float* prios, int32_t C);
+
+/* prog/prio.go:29-38 CalculatePriorities with the static matrix given as input (prio.go:40-135 needs
+ * the generated sys.Calls type graph, which the reference does not ship — SURVEY.md F8). */
+int oracle_calculate_priorities(const float* static_prios, const uint16_t* prog_len, size_t nprogs,
+                                int32_t C, float* out);
+
+/* prog/prio.go:202-228 BuildChoiceTable. enabled == NULL means all calls enabled.
+ * run is C*C int64 (rows of disabled calls are zero-filled and row_present[i] = 0 ⇔ Go nil). */
+int oracle_build_choice_table(const float* prios, const uint8_t* enabled, int32_t C, int64_t* run,
+                              uint8_t* row_present);
+
+/* syz-fuzzer/fuzzer.go:446-470 execute (and syz-manager/manager.go:609-616 NewInput): process the
+ * covers in order; cover k of group g is new iff (cov \ maxCover[g]) \ flakes is non-empty, in which
+ * case maxCover[g] = Union(maxCover[g], diff).  maxcover is a CSR over ngroups (mc_off ngroups+1);
+ * the updated tables are written to out_mc / out_mc_off (capacity out_cap PCs). */
+int oracle_novelty(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                   uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off,
+                   const uint32_t* flakes, size_t nflakes, uint8_t* is_new, uint32_t* out_mc,
+                   uint64_t* out_mc_off, size_t out_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
