@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""Benchmark: corpus progs/sec of syz-manager's minimizeCorpus hot path on MI355X.
+
+One step = cover.Minimize over every call group of a device-resident corpus
+(syz-manager/manager.go:507-527 -> cover/cover.go:105-131) + CalculatePriorities over the kept
+programs (prog/prio.go:29-38, 137-192) + BuildChoiceTable (prio.go:202-228), through the C ABI of
+libsyzgpu.so. Inputs (covers, call ids, program lengths, the static priority matrix) are resident in
+HBM before the timed region; the output selection, priorities and ChoiceTable stay in HBM.
+
+Workload (BASELINE.json configs[3], per GPU): 1M programs, 2M-PC space, 289 calls, C = 1159,
+synthetic corpus from the seeded generator (SURVEY.md §8d shapes). Weak scaling: at N GPUs the
+corpus has N x 1M programs; call groups are partitioned over ranks (a group's Minimize is
+independent of every other group) and the only exchange is an RCCL all-reduce of the (C+1)-entry
+program-length histogram that feeds CalculatePriorities.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--progs-per-gpu 1000000]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "corpus progs/sec: cover.Minimize + calcDynamicPrio, 1M progs, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured copy)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--progs-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--ngroups", type=int, default=289)
+    ap.add_argument("--npcs", type=int, default=2_000_000)
+    ap.add_argument("--calls", type=int, default=1159)
+    ap.add_argument("--seed", type=int, default=0x5EED0004)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="programs in the CPU baseline sample")
+    ap.add_argument("--profile", type=int, default=1, help="per-kernel HIP event timing in the timed region")
+    return ap.parse_args()
+
+
+def lpt_assign(weights, nranks):
+    """Longest-processing-time assignment of call groups to ranks (deterministic on every rank)."""
+    owner = np.zeros(weights.size, dtype=np.int64)
+    load = np.zeros(nranks, dtype=np.float64)
+    for g in np.argsort(-weights, kind="stable"):
+        r = int(np.argmin(load))
+        owner[g] = r
+        load[r] += weights[g]
+    return owner, load
+
+
+def static_matrix(C, seed=7):
+    # calcStaticPriorities output stand-in (needs the generated sys.Calls type graph):
+    # values in [0.1, 1], self-priority = row max (prio.go:124-132)
+    rnd = np.random.default_rng(seed)
+    s = (rnd.random((C, C)) * 0.9 + 0.1).astype(np.float32)
+    np.fill_diagonal(s, s.max(axis=1))
+    return s
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("run N>1 through torch.distributed.run (one process per GPU)", file=sys.stderr)
+            sys.exit(2)
+    import torch
+    import torch.distributed as dist
+
+    from syzkaller_amd import _lib, synth
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    L = _lib.lib()
+    _lib.check(L.syzgpu_init(local))
+
+    # ---- corpus (synthetic, deterministic; generated on the host, then made resident) ----
+    t0 = time.time()
+    C, G = args.calls, args.ngroups
+    p = synth.params(args.seed, args.progs_per_gpu * world, G, args.npcs)
+    group, off, plen = synth.layout(p)
+    lens = (off[1:] - off[:-1]).astype(np.float64)
+    gw = np.bincount(group, weights=lens, minlength=G)  # work per group ~ its PCs
+    owner, load = lpt_assign(gw, world)
+    ids = np.nonzero(owner[group] == rank)[0]
+    corp = synth.subcorpus(p, ids, group, off, plen)
+    gen_s = time.time() - t0
+
+    def dt(a):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64, np.dtype(np.uint16): np.int16}
+        return torch.from_numpy(a.view(view.get(a.dtype, a.dtype))).to(dev)
+
+    d_pcs, d_off, d_grp, d_len = dt(corp.pcs), dt(corp.off), dt(corp.group), dt(corp.prog_len)
+    st = static_matrix(C)
+    d_static = torch.from_numpy(st).to(dev)
+    d_sel = torch.zeros(corp.n, dtype=torch.uint8, device=dev)
+    d_hist = torch.zeros(C + 1, dtype=torch.int64, device=dev)
+    d_prios = torch.empty((C, C), dtype=torch.float32, device=dev)
+    d_run = torch.empty((C, C), dtype=torch.int64, device=dev)
+    d_pres = torch.empty(C, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step():
+        _lib.check(L.syzgpu_minimize_grouped_dev(d_pcs.data_ptr(), d_off.data_ptr(), d_grp.data_ptr(),
+                                                 d_len.data_ptr(), corp.n, G, C, d_sel.data_ptr(),
+                                                 d_hist.data_ptr(), sptr))
+        if world > 1:
+            dist.all_reduce(d_hist, op=dist.ReduceOp.SUM)  # the one exchange: (C+1) int64
+        _lib.check(L.syzgpu_prio_choice_dev(d_static.data_ptr(), d_hist.data_ptr(), C, None, d_prios.data_ptr(),
+                                            d_run.data_ptr(), d_pres.data_ptr(), sptr))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if args.profile:
+        L.syzgpu_profile_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kern = {}
+    if args.profile:
+        cap = 4096
+        names = ctypes.create_string_buffer(48 * cap)
+        ms = np.zeros(cap, np.float32)
+        by = np.zeros(cap, np.uint64)
+        k = L.syzgpu_profile_read(names, ms.ctypes.data, by.ctypes.data, cap)
+        L.syzgpu_profile_enable(0)
+        raw = names.raw
+        for i in range(k):
+            nm = raw[48 * i:48 * (i + 1)].split(b"\0")[0].decode()
+            e = kern.setdefault(nm, {"ms": 0.0, "launches": 0, "bytes": 0})
+            e["ms"] += float(ms[i])
+            e["launches"] += 1
+            e["bytes"] += int(by[i])
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_progs = args.progs_per_gpu * world
+    sum_pcs = int(corp.off[-1])
+    if world > 1:
+        tt = torch.tensor([sum_pcs], dtype=torch.int64, device=dev)
+        dist.all_reduce(tt)
+        sum_pcs_all = int(tt.item())
+    else:
+        sum_pcs_all = sum_pcs
+    ms_step = elapsed / args.steps * 1e3
+    value = total_progs * args.steps / elapsed
+
+    out = None
+    if rank == 0:
+        # roofline of the dominant kernel: algorithmic bytes per SURVEY.md §8(d) for the units one
+        # launch processes (Minimize: 4 B per PC + 10 B per program), over its measured average time
+        roof = None
+        if kern:
+            dom = max(kern, key=lambda n: kern[n]["ms"])
+            d = kern[dom]
+            avg_ms = d["ms"] / d["launches"]
+            n_local = corp.n
+            alg = 4 * sum_pcs + 10 * n_local if dom.startswith(("bucket", "group", "ranks", "select", "gosort"))\
+                else d["bytes"] / d["launches"]
+            ach = alg / (avg_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_ms": round(avg_ms, 4),
+                    "design_bytes_per_launch": int(d["bytes"] / d["launches"]),
+                    "algorithmic_bytes_per_launch": int(alg)}
+            tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(tf):
+                try:
+                    pm = json.load(open(tf))
+                    if dom in pm.get("kernels", {}) and pm.get("workload") == "config4-1M":
+                        roof["traffic"] = pm["kernels"][dom]["hbm_bytes_per_launch"]
+                except Exception:
+                    pass
+        path_bytes = 4 * sum_pcs_all + 10 * total_progs + 16 * C * C
+        cpu = None
+        if args.cpu_baseline and world == 1:
+            cpu = cpu_baseline(corp, st, min(args.cpu_sample, corp.n))
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "progs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: seeded generator (SURVEY.md §8d shapes), device-resident before timing",
+            "config": {"workload": "config4-1M: 1M programs/GPU, 2M-PC space, 289 calls, C=1159",
+                       "progs_per_gpu": args.progs_per_gpu, "total_progs": total_progs,
+                       "sum_pcs": sum_pcs_all, "ngroups": G, "npcs": args.npcs, "calls": C,
+                       "parallelism": "call-group sharded x%d + RCCL all-reduce of the length histogram" % world,
+                       "max_rank_load_share": round(float(load.max() / load.sum()), 4)},
+            "roofline": roof,
+            "path_roofline": {"bytes_per_step": path_bytes,
+                              "achieved": round(path_bytes / (ms_step * 1e-3) / 1e9, 1),
+                              "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                              "frac": round(path_bytes / (ms_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)},
+            "kernels_ms_per_step": {k: round(v["ms"] / args.steps, 4) for k, v in
+                                    sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},
+            "cpu_baseline": cpu,
+            "gen_s": round(gen_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(corp, static, n_sample):
+    """The oracle (single-threaded C restatement of the Go path) on the first n_sample programs."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    off = np.ascontiguousarray(corp.off[: n_sample + 1])
+    pcs = corp.pcs[: int(off[-1])]
+    grp = np.ascontiguousarray(corp.group[:n_sample])
+    t = time.perf_counter()
+    kept, _ = oracle.minimize_grouped(pcs, off, grp, corp.ngroups)
+    pr = oracle.calculate_priorities(static, corp.prog_len[kept])
+    oracle.build_choice_table(pr, None)
+    dt = time.perf_counter() - t
+    return {"value": round(n_sample / dt, 1), "unit": "progs/s", "cores": 1, "kind": "port",
+            "sample": "first %d programs of the same corpus (%d PCs); oracle/liboracle.so: Minimize + "
+                      "CalculatePriorities + BuildChoiceTable, %.2f s" % (n_sample, int(off[-1]), dt),
+            "cpu": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

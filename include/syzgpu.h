@@ -1,0 +1,139 @@
+/*
+ * syzgpu — MI355X-native corpus analytics for syzkaller: the C ABI (libsyzgpu.so).
+ *
+ * Every entry point replaces one function of the reference's Go API (or the batched loop around it)
+ * and is what a cgo binding would call (see INTEGRATION.md for the Go stubs). Plain pointers and
+ * sizes only. All functions return a status (0 = SYZGPU_OK); syzgpu_last_error() explains a failure.
+ * There is no CPU fallback: without a usable gfx950 device every compute entry point returns
+ * SYZGPU_ENODEV.
+ *
+ * Host-pointer functions take caller-owned host buffers; the library never keeps a pointer after
+ * returning (cgo pointer rules). The *_dev functions take device pointers (e.g. torch tensors) and a
+ * hipStream_t passed as void*; they enqueue work and may return before it completes.
+ *
+ * Thread safety: every function may be called from several threads (Go goroutines); calls are
+ * serialised internally per device context.
+ */
+#ifndef SYZGPU_H
+#define SYZGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  SYZGPU_OK = 0,
+  SYZGPU_EINVAL = 1,    /* invalid argument (unsorted set-op input, len(p.Calls) > C, group >= G ...) */
+  SYZGPU_ENODEV = 2,    /* no usable gfx950 device */
+  SYZGPU_ENOMEM = 3,    /* device allocation failed */
+  SYZGPU_EHIP = 4,      /* HIP runtime error */
+  SYZGPU_EINTERNAL = 5, /* internal invariant violated (bug) */
+  SYZGPU_ECAPACITY = 6  /* caller-provided output capacity too small */
+};
+
+enum { SYZGPU_DIFFERENCE = 0, SYZGPU_SYMMETRIC_DIFFERENCE = 1, SYZGPU_UNION = 2, SYZGPU_INTERSECTION = 3 };
+
+/* ---- context -------------------------------------------------------------------------------- */
+int syzgpu_init(int device);                    /* optional; first call of anything does init(0) */
+int syzgpu_shutdown(void);                      /* frees device memory */
+int syzgpu_device_count(int* n);
+size_t syzgpu_last_error(char* buf, size_t cap); /* thread-local message of the last failure */
+const char* syzgpu_version(void);
+
+/* ---- cover/cover.go ------------------------------------------------------------------------- */
+/* cover/cover.go:28-40 Canonicalize: sorts cov IN PLACE and removes duplicates; the result is
+ * cov[:*out_n] (aliases the input, as in Go). A cover made only of 0xFFFFFFFF becomes empty. */
+int syzgpu_canonicalize(uint32_t* cov, size_t n, size_t* out_n);
+
+/* cover/cover.go:42-49 Difference, :51-61 SymmetricDifference, :63-70 Union, :72-79 Intersection,
+ * all through foreach (:81-102). Inputs must be sorted ascending (SYZGPU_EINVAL otherwise);
+ * multiset semantics of foreach on duplicates are kept; 0xFFFFFFFF never appears in an output.
+ * Output capacity needed: Difference na, SymmetricDifference na+nb, Union na+nb, Intersection
+ * min(na, nb). *out_n == 0 corresponds to Go's nil result. */
+int syzgpu_difference(const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out,
+                      size_t cap, size_t* out_n);
+int syzgpu_symmetric_difference(const uint32_t* a, size_t na, const uint32_t* b, size_t nb,
+                                uint32_t* out, size_t cap, size_t* out_n);
+int syzgpu_union(const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out,
+                 size_t cap, size_t* out_n);
+int syzgpu_intersection(const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out,
+                        size_t cap, size_t* out_n);
+
+/* cover/cover.go:105-131 Minimize over one corpus given as CSR (off[ncov+1], pcs[off[ncov]]).
+ * out_idx (capacity ncov) receives the kept input indices in Go's selection order. */
+int syzgpu_minimize(const uint32_t* pcs, const uint64_t* off, size_t ncov, int64_t* out_idx,
+                    size_t* out_n);
+
+/* ---- batched forms (one launch for many covers / pairs) ------------------------------------- */
+/* Canonicalize every cover of a CSR in place; out_len[i] = new length of cover i. */
+int syzgpu_canonicalize_batch(uint32_t* pcs, const uint64_t* off, size_t ncov, uint64_t* out_len);
+
+/* op(a_i, b_i) for npairs pairs of CSR covers. out_off[npairs+1] is written; out must hold
+ * out_cap PCs (sum of the per-op capacities above suffices). */
+int syzgpu_setop_batch(int op, const uint32_t* a, const uint64_t* a_off, const uint32_t* b,
+                       const uint64_t* b_off, size_t npairs, uint32_t* out, size_t out_cap,
+                       uint64_t* out_off);
+
+/* syz-manager/manager.go:507-527 minimizeCorpus: Minimize every call group in one launch.
+ * group[i] < ngroups is the call (CallName id) of corpus entry i. out_idx (capacity n) receives the
+ * kept corpus entry ids group-major (groups in ascending id — the reference iterates a Go map),
+ * each group in Go's selection order; group_out_off[ngroups+1] the group boundaries. */
+int syzgpu_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                            size_t n, uint32_t ngroups, int64_t* out_idx, uint64_t* group_out_off);
+
+/* syz-fuzzer/fuzzer.go:446-470 execute (and syz-manager/manager.go:609-616 NewInput) over a batch:
+ * covers are processed in order; cover k of group g is new iff (cov \ maxCover[g]) \ flakes != {},
+ * and then maxCover[g] = Union(maxCover[g], that difference). mc/mc_off is the CSR of the ngroups
+ * maxCover tables on entry; the updated tables are written to out_mc/out_mc_off (capacity out_cap). */
+int syzgpu_novelty_batch(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                         uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off,
+                         const uint32_t* flakes, size_t nflakes, uint8_t* is_new, uint32_t* out_mc,
+                         size_t out_cap, uint64_t* out_mc_off);
+
+/* ---- prog/prio.go --------------------------------------------------------------------------- */
+/* prog/prio.go:137-154 calcDynamicPrio + normalizePrio (:158-192). prog_len[i] = len(p.Calls) of
+ * corpus program i (the only property the reference reads). out: C*C float32. */
+int syzgpu_dynamic_prio(const uint16_t* prog_len, size_t nprogs, int32_t C, float* out);
+
+/* prog/prio.go:29-38 CalculatePriorities with calcStaticPriorities' C*C result as input. */
+int syzgpu_calculate_priorities(const float* static_prios, const uint16_t* prog_len, size_t nprogs,
+                                int32_t C, float* out);
+
+/* prog/prio.go:202-228 BuildChoiceTable. enabled: C bytes or NULL (= all enabled). run: C*C int64
+ * prefix sums of int(prios*1000) over enabled columns; row_present[i] = 0 marks a Go nil row
+ * (disabled call, read by prog/rand.go:406), whose run row is zero-filled. */
+int syzgpu_build_choice_table(const float* prios, const uint8_t* enabled, int32_t C, int64_t* run,
+                              uint8_t* row_present);
+
+/* ---- device-resident pipeline (manager-side minimizeCorpus on data already in HBM) ------------ */
+/* All pointers are device pointers; stream is a hipStream_t (NULL = the null stream).
+ * Minimize every group of a resident corpus: selected[i] = 1 iff entry i is kept.
+ * len_hist (int64[C+1], zeroed by the call) receives the histogram of prog_len over kept entries,
+ * the input of the prio stage (and the only data a multi-GPU run must all-reduce). */
+int syzgpu_minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                const uint16_t* prog_len, size_t n, uint32_t ngroups, int32_t C,
+                                uint8_t* selected, int64_t* len_hist, void* stream);
+
+/* Dynamic prio from a length histogram, normalize, multiply by static, and the ChoiceTable:
+ * prog/prio.go:29-38, 137-192, 202-228 fused. enabled may be NULL. */
+int syzgpu_prio_choice_dev(const float* static_prios, const int64_t* len_hist, int32_t C,
+                           const uint8_t* enabled, float* prios, int64_t* run,
+                           uint8_t* row_present, void* stream);
+
+/* Compact device selection flags into group-major kept entry ids in Go's selection order (the
+ * order syzgpu_minimize_grouped returns). Valid after syzgpu_minimize_grouped_dev on the same
+ * corpus and before the next call into the library on this thread's context. */
+int syzgpu_minimize_grouped_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n,
+                                  uint32_t ngroups);
+
+/* Per-kernel timing of the last *_dev call (HIP events on the call's stream), for the benchmark's
+ * roofline. names/ms arrays of capacity cap; returns the number of kernels recorded. */
+int syzgpu_profile_enable(int on);
+size_t syzgpu_profile_read(char (*names)[48], float* ms, uint64_t* bytes, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -35,6 +35,11 @@ int syzgpu_synth_layout(const syzgpu_synth_params* p, uint32_t* group, uint64_t*
 int syzgpu_synth_fill(const syzgpu_synth_params* p, const uint32_t* group, const uint64_t* off,
                       uint32_t* pcs, int nthreads);
 
+/* Fill a sub-corpus: entry k of (group, off) is global entry ids[k] of the corpus p describes
+ * (its PCs are exactly those syzgpu_synth_fill would generate for that entry). */
+int syzgpu_synth_fill_ids(const syzgpu_synth_params* p, const uint64_t* ids, const uint32_t* group,
+                          const uint64_t* off, uint64_t n, uint32_t* pcs, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

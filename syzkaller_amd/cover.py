@@ -1,0 +1,140 @@
+"""Host mirror of the reference's `cover` package (cover/cover.go) over libsyzgpu.so.
+
+Same names and argument meaning as the Go API; every compute call runs on the MI355X:
+
+    Canonicalize(cov)            cover.go:28   sorts + dedups IN PLACE, returns cov[:n] (aliases)
+    Difference(a, b)             cover.go:42
+    SymmetricDifference(a, b)    cover.go:51
+    Union(a, b)                  cover.go:63
+    Intersection(a, b)           cover.go:72
+    Minimize(corpus)             cover.go:105  -> list of kept indices in selection order
+    Copy(cov), RestorePC(pc, base)  cover.go:19-25 (trivial, host)
+
+Batched forms serve the manager/fuzzer loops that call these per input:
+    MinimizeCorpus(pcs, off, group, ngroups)   syz-manager/manager.go:507-527
+    SetOpBatch(op, a_list, b_list)             one launch for many pairs
+    CanonicalizeBatch(pcs, off)
+    NoveltyBatch(...)                          syz-fuzzer/fuzzer.go:446-470
+Covers are numpy uint32 arrays. Go's nil result is returned as an empty array.
+"""
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+SENT = 0xFFFFFFFF  # cover.go:17
+
+
+def _u32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
+
+
+def Copy(cov):
+    return _u32(cov).copy()
+
+
+def RestorePC(pc, base):
+    return (int(base) << 32) + int(pc)
+
+
+def Canonicalize(cov):
+    """In place like Go: cov must be a writable uint32 numpy array; returns cov[:n]."""
+    if not (isinstance(cov, np.ndarray) and cov.dtype == np.uint32 and cov.flags.c_contiguous):
+        cov = _u32(cov).copy()
+    n = np.zeros(1, dtype=np.uint64)
+    check(lib().syzgpu_canonicalize(ptr(cov), cov.size, ptr(n)))
+    return cov[: int(n[0])]
+
+
+def _pair(fn, cap_of, a, b):
+    a, b = _u32(a), _u32(b)
+    cap = cap_of(a.size, b.size)
+    out = np.empty(max(cap, 1), dtype=np.uint32)
+    n = np.zeros(1, dtype=np.uint64)
+    check(fn(ptr(a), a.size, ptr(b), b.size, ptr(out), cap, ptr(n)))
+    return out[: int(n[0])].copy()
+
+
+def Difference(a, b):
+    return _pair(lib().syzgpu_difference, lambda x, y: x, a, b)
+
+
+def SymmetricDifference(a, b):
+    return _pair(lib().syzgpu_symmetric_difference, lambda x, y: x + y, a, b)
+
+
+def Union(a, b):
+    return _pair(lib().syzgpu_union, lambda x, y: x + y, a, b)
+
+
+def Intersection(a, b):
+    return _pair(lib().syzgpu_intersection, lambda x, y: min(x, y), a, b)
+
+
+def to_csr(covers):
+    off = np.zeros(len(covers) + 1, dtype=np.uint64)
+    if covers:
+        np.cumsum([len(c) for c in covers], out=off[1:])
+    pcs = np.concatenate([_u32(c) for c in covers]) if covers else np.zeros(0, np.uint32)
+    return np.ascontiguousarray(pcs, dtype=np.uint32), off
+
+
+def Minimize(corpus):
+    """cover.go:105 — corpus is a list of covers; returns the kept indices in Go's order."""
+    pcs, off = to_csr(corpus)
+    n = len(corpus)
+    out = np.empty(max(n, 1), dtype=np.int64)
+    m = np.zeros(1, dtype=np.uint64)
+    check(lib().syzgpu_minimize(ptr(pcs), ptr(off), n, ptr(out), ptr(m)))
+    return [int(x) for x in out[: int(m[0])]]
+
+
+def MinimizeCorpus(pcs, off, group, ngroups):
+    """minimizeCorpus (manager.go:507-527): returns (kept entry ids group-major, group offsets)."""
+    pcs, off = _u32(pcs), np.ascontiguousarray(off, dtype=np.uint64)
+    group = _u32(group)
+    n = off.size - 1
+    out = np.empty(max(n, 1), dtype=np.int64)
+    goff = np.zeros(ngroups + 1, dtype=np.uint64)
+    check(lib().syzgpu_minimize_grouped(ptr(pcs), ptr(off), ptr(group), n, ngroups, ptr(out), ptr(goff)))
+    return out[: int(goff[-1])].copy(), goff
+
+
+_OPS = {"difference": _lib.DIFFERENCE, "symmetric_difference": _lib.SYMMETRIC_DIFFERENCE,
+        "union": _lib.UNION, "intersection": _lib.INTERSECTION}
+
+
+def SetOpBatch(op, a_list, b_list):
+    """op(a_i, b_i) for every pair in one launch; returns a list of arrays."""
+    code = _OPS[op] if isinstance(op, str) else int(op)
+    a, aoff = to_csr(list(a_list))
+    b, boff = to_csr(list(b_list))
+    npairs = len(a_list)
+    cap = {0: a.size, 1: a.size + b.size, 2: a.size + b.size, 3: min(a.size, b.size)}[code]
+    out = np.empty(max(cap, 1), dtype=np.uint32)
+    ooff = np.zeros(npairs + 1, dtype=np.uint64)
+    check(lib().syzgpu_setop_batch(code, ptr(a), ptr(aoff), ptr(b), ptr(boff), npairs, ptr(out), cap, ptr(ooff)))
+    return [out[int(ooff[i]):int(ooff[i + 1])].copy() for i in range(npairs)]
+
+
+def CanonicalizeBatch(pcs, off):
+    """Canonicalize every cover of a CSR in place; returns the new lengths."""
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    n = off.size - 1
+    lens = np.zeros(max(n, 1), dtype=np.uint64)
+    check(lib().syzgpu_canonicalize_batch(ptr(pcs), ptr(off), n, ptr(lens)))
+    return lens[:n]
+
+
+def NoveltyBatch(pcs, off, group, ngroups, maxcover_pcs, maxcover_off, flakes):
+    """fuzzer.go:446-470 over a batch: returns (is_new u8[n], new maxCover CSR pcs, offsets)."""
+    pcs, off, group = _u32(pcs), np.ascontiguousarray(off, dtype=np.uint64), _u32(group)
+    mc, mco, fl = _u32(maxcover_pcs), np.ascontiguousarray(maxcover_off, dtype=np.uint64), _u32(flakes)
+    n = off.size - 1
+    is_new = np.zeros(max(n, 1), dtype=np.uint8)
+    cap = int(mc.size + pcs.size + 1)
+    out = np.empty(cap, dtype=np.uint32)
+    ooff = np.zeros(ngroups + 1, dtype=np.uint64)
+    check(lib().syzgpu_novelty_batch(ptr(pcs), ptr(off), ptr(group), n, ngroups, ptr(mc), ptr(mco), ptr(fl),
+                                     fl.size, ptr(is_new), ptr(out), cap, ptr(ooff)))
+    return is_new[:n].copy(), out[: int(ooff[-1])].copy(), ooff

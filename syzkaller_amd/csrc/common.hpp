@@ -1,0 +1,270 @@
+// Shared runtime pieces of libsyzgpu.so: error handling, the per-device context with grow-only
+// scratch buffers, and wave64 / workgroup primitives used by every kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/syzgpu.h"
+
+namespace syz {
+
+constexpr uint32_t SENT = 0xFFFFFFFFu;  // cover/cover.go:17
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string& msg);
+void set_last_error(const std::string& msg);
+
+#define SYZ_HIP(expr)                                                                            \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      ::syz::fail(e_ == hipErrorOutOfMemory ? SYZGPU_ENOMEM : SYZGPU_EHIP,                       \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                            \
+  } while (0)
+
+#define SYZ_LAUNCHED() SYZ_HIP(hipGetLastError())
+
+// Grow-only device scratch, keyed by name. Never shrinks within a context; freed at shutdown.
+class Scratch {
+ public:
+  void* get(const std::string& name, size_t bytes);
+  template <class T>
+  T* get(const std::string& name, size_t count) {
+    return static_cast<T*>(get(name, count * sizeof(T) + 16));
+  }
+  void release();
+  ~Scratch() { release(); }
+
+ private:
+  struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::map<std::string, Buf> bufs_;
+};
+
+// Pinned host staging for small D2H readbacks.
+class Pinned {
+ public:
+  void* get(size_t bytes);
+  template <class T>
+  T* get(size_t count) {
+    return static_cast<T*>(get(count * sizeof(T) + 16));
+  }
+  ~Pinned();
+
+ private:
+  void* p_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+struct Context {
+  int device = -1;
+  hipStream_t stream = nullptr;  // library-owned stream for host-pointer entry points
+  Scratch scratch;
+  Pinned pinned;
+  std::recursive_mutex mu;
+  // last minimize_grouped_dev state (for syzgpu_minimize_grouped_fetch)
+  size_t last_n = 0;
+  uint32_t last_groups = 0;
+  bool have_last = false;
+};
+
+// Returns the initialised context of the current device (lazily init(0)); throws ENODEV.
+Context& ctx();
+
+// Kernel timing (bench roofline). Records named events around launches when enabled.
+struct Prof {
+  bool on = false;
+  struct Rec {
+    std::string name;
+    hipEvent_t a, b;
+    uint64_t bytes;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  void reset();
+  void begin(const char* name, hipStream_t s, uint64_t bytes);
+  void end(hipStream_t s);
+};
+Prof& prof();
+
+struct ProfScope {
+  hipStream_t s;
+  bool on;
+  ProfScope(const char* name, hipStream_t st, uint64_t bytes) : s(st), on(prof().on) {
+    if (on) prof().begin(name, s, bytes);
+  }
+  ~ProfScope() {
+    if (on) prof().end(s);
+  }
+};
+
+// ---- device-wide scans (scan.hip) ----------------------------------------------------------
+// out[i] = sum(in[0..i)), out[n] = total. in may be uint8_t / uint32_t / uint64_t.
+void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s);
+void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s);
+void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s);
+
+inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {
+  size_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// ---- device primitives ---------------------------------------------------------------------
+__device__ __forceinline__ unsigned lane64() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const unsigned l = __lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// Compiler + LDS ordering point between lanes of one wave (ds ops of a wave retire in order).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T x) {
+  const unsigned l = __lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    T y = __shfl_up(x, d, 64);
+    if (l >= (unsigned)d) x += y;
+  }
+  return x;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_min(T x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    T y = __shfl_xor(x, d, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+// Exclusive scan across a workgroup of BLOCK threads. lds needs BLOCK/64 + 1 slots.
+template <int BLOCK, class T>
+__device__ __forceinline__ T block_excl_scan(T v, T* lds, T* total) {
+  const int w = threadIdx.x >> 6;
+  const unsigned l = __lane_id();
+  T x = wave_incl_scan(v);
+  if (l == 63) lds[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T s = 0;
+#pragma unroll
+    for (int i = 0; i < BLOCK / 64; i++) {
+      T t = lds[i];
+      lds[i] = s;
+      s += t;
+    }
+    lds[BLOCK / 64] = s;
+  }
+  __syncthreads();
+  T r = x - v + lds[w];
+  *total = lds[BLOCK / 64];
+  __syncthreads();
+  return r;
+}
+
+template <int BLOCK, class T>
+__device__ __forceinline__ T block_sum(T v, T* lds) {
+  T tot;
+  block_excl_scan<BLOCK>(v, lds, &tot);
+  return tot;
+}
+
+template <int BLOCK, class T>
+__device__ __forceinline__ T block_min(T v, T* lds) {
+  const int w = threadIdx.x >> 6;
+  T x = wave_min(v);
+  if (__lane_id() == 0) lds[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T m = lds[0];
+    for (int i = 1; i < BLOCK / 64; i++) m = lds[i] < m ? lds[i] : m;
+    lds[BLOCK / 64] = m;
+  }
+  __syncthreads();
+  T r = lds[BLOCK / 64];
+  __syncthreads();
+  return r;
+}
+
+// First index in [lo, hi) with a[i] >= v / > v.
+template <class T>
+__device__ __forceinline__ uint64_t lower_bound_dev(const T* a, uint64_t lo, uint64_t hi, T v) {
+  while (lo < hi) {
+    uint64_t m = lo + ((hi - lo) >> 1);
+    if (a[m] < v)
+      lo = m + 1;
+    else
+      hi = m;
+  }
+  return lo;
+}
+template <class T>
+__device__ __forceinline__ uint64_t upper_bound_dev(const T* a, uint64_t lo, uint64_t hi, T v) {
+  while (lo < hi) {
+    uint64_t m = lo + ((hi - lo) >> 1);
+    if (a[m] <= v)
+      lo = m + 1;
+    else
+      hi = m;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+}  // namespace syz
+
+// Entry-point wrapper: runs body under the context lock, converts exceptions to status codes.
+#define SYZ_API_BODY(...)                                                                        \
+  try {                                                                                          \
+    ::syz::Context& C_ = ::syz::ctx();                                                           \
+    std::lock_guard<std::recursive_mutex> lk_(C_.mu);                                            \
+    __VA_ARGS__;                                                                                 \
+    return SYZGPU_OK;                                                                            \
+  } catch (const ::syz::Error& e) {                                                              \
+    ::syz::set_last_error(e.msg);                                                                \
+    return e.code;                                                                               \
+  } catch (const std::bad_alloc&) {                                                              \
+    ::syz::set_last_error("host allocation failed");                                             \
+    return SYZGPU_ENOMEM;                                                                        \
+  } catch (const std::exception& e) {                                                            \
+    ::syz::set_last_error(e.what());                                                             \
+    return SYZGPU_EINTERNAL;                                                                     \
+  }

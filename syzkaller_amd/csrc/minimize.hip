@@ -1,0 +1,523 @@
+// cover.Minimize for every call group of a corpus (cover/cover.go:105-131 driven by
+// syz-manager/manager.go:507-527 minimizeCorpus), on the GPU.
+//
+// Exact reformulation: Minimize keeps input k (at Go-sort position k of its group)
+// iff some PC of cov_k does not occur in any earlier-positioned input of the group — an input that
+// is skipped adds nothing to the covered map, so covered after step k is the union of ALL inputs up
+// to k. Minimize is therefore a first-occurrence problem over (group, pc) keys:
+//   1. stable partition of entries by group (corpus order inside a group = Go's inputs[] order);
+//   2. Go sort.Sort permutation of every group (gosort.hip) -> rank R of each entry;
+//   3. bucket pass: each (pc, R) pair goes to a bucket of its group chosen by hash(pc), so that all
+//      occurrences of a key meet in one bucket and a bucket's keys fit a workgroup's LDS;
+//   4. hash pass: per bucket, an LDS open-addressing table computes min R per pc; the winning R of
+//      every key marks its entry selected;
+//   5. selected ranks in increasing order per group = Go's selection order.
+// Everything is integer work: bit-exact by construction.
+#include <algorithm>
+#include <numeric>
+
+#include "pipeline.hpp"
+
+namespace syz {
+
+// ---- 1. stable partition by group -------------------------------------------------------------
+constexpr int PW_ITEMS = 1024;  // entries per wave chunk (16 rounds of 64)
+
+constexpr uint32_t MAX_GROUPS = 4096;  // calls (CallName ids) per corpus; len(sys.Calls) ~ 1.2k
+
+// One wave per chunk of PW_ITEMS entries; per-wave group counters live in LDS (dynamic, 4*G u32).
+__global__ __launch_bounds__(256) void k_grp_count(const uint32_t* group, size_t n, uint32_t G, uint32_t nchunks,
+                                                   uint32_t* cnt, int* err) {
+  extern __shared__ uint32_t run[];  // [4][G]
+  const int w = threadIdx.x >> 6;
+  uint32_t* mine = run + (size_t)w * G;
+  for (uint32_t g = __lane_id(); g < G; g += 64) mine[g] = 0;
+  wave_sync();
+  const uint32_t chunk = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (chunk >= nchunks) return;
+  const size_t beg = (size_t)chunk * PW_ITEMS;
+  const size_t end = std::min(n, beg + PW_ITEMS);
+  for (size_t i = beg + __lane_id(); i < end; i += 64) {
+    uint32_t g = group[i];
+    if (g >= G) {
+      atomicOr(err, 1);
+      g = 0;
+    }
+    atomicAdd(&mine[g], 1u);
+  }
+  wave_sync();
+  // cnt is group-major: cnt[g * nchunks + chunk]
+  for (uint32_t g = __lane_id(); g < G; g += 64) cnt[(size_t)g * nchunks + chunk] = mine[g];
+}
+
+__global__ __launch_bounds__(256) void k_grp_sumlen(const uint32_t* group, const uint64_t* off, size_t n,
+                                                    uint32_t G, uint64_t* gpcs) {
+  extern __shared__ unsigned long long lsum[];
+  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) lsum[g] = 0;
+  __syncthreads();
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t g = group[i];
+    if (g < G) atomicAdd(&lsum[g], (unsigned long long)(off[i + 1] - off[i]));
+  }
+  __syncthreads();
+  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+    if (lsum[g]) atomicAdd((unsigned long long*)&gpcs[g], lsum[g]);
+}
+
+// Stable placement: each wave walks its chunk in order; lanes of one group inside a 64-entry round
+// are ranked with a ballot, the per-group running slot is kept in LDS.
+__global__ __launch_bounds__(256) void k_grp_scatter(const uint32_t* group, const uint64_t* off, size_t n,
+                                                     uint32_t G, uint32_t nchunks, const uint64_t* cnt_scan,
+                                                     uint32_t* members, uint64_t* el) {
+  extern __shared__ uint32_t run[];  // [4][G]
+  const int w = threadIdx.x >> 6;
+  uint32_t* mine = run + (size_t)w * G;
+  const uint32_t chunk = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (chunk >= nchunks) return;
+  for (uint32_t g = __lane_id(); g < G; g += 64) mine[g] = (uint32_t)cnt_scan[(size_t)g * nchunks + chunk];
+  wave_sync();
+  const size_t beg = (size_t)chunk * PW_ITEMS;
+  const size_t end = std::min(n, beg + PW_ITEMS);
+  for (size_t base = beg; base < end; base += 64) {
+    const size_t i = base + __lane_id();
+    const bool valid = i < end;
+    const uint32_t g = valid ? std::min(group[i], G - 1) : 0;
+    uint64_t todo = __ballot(valid);
+    while (todo) {
+      const int leader = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t gl = __shfl(g, leader, 64);
+      const uint64_t mask = __ballot(valid && g == gl);
+      const uint32_t b0 = mine[gl];
+      if (valid && g == gl) {
+        const uint32_t pos = b0 + __popcll(mask & lanemask_lt());
+        members[pos] = (uint32_t)i;
+        const uint64_t len = off[i + 1] - off[i];
+        el[pos] = (len << 32) | pos;
+      }
+      wave_sync();
+      if (__lane_id() == (unsigned)leader) mine[gl] = b0 + __popcll(mask);
+      wave_sync();
+      todo &= ~mask;
+    }
+  }
+}
+
+__global__ void k_grp_starts(const uint64_t* cnt_scan, uint32_t G, uint32_t nchunks, size_t n, uint64_t* gstart) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x)
+    gstart[g] = g < G ? cnt_scan[(size_t)g * nchunks] : (uint64_t)n;
+}
+
+// ---- 2. ranks ------------------------------------------------------------------------------------
+__global__ void k_ranks(const uint64_t* el, size_t n, const uint32_t* members, uint32_t* rank_of_member,
+                        uint32_t* ent_of_rank) {
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t gidx = (uint32_t)el[r];
+    rank_of_member[gidx] = (uint32_t)r;
+    ent_of_rank[r] = members[gidx];
+  }
+}
+
+// ---- 3. bucket passes ------------------------------------------------------------------------------
+struct Chunk {
+  uint32_t g, mbeg, mend, pad;
+};
+struct GBucket {
+  uint32_t base;  // first bucket id of the group
+  uint32_t bits;  // log2(number of buckets of the group)
+};
+
+constexpr int BK_BLOCK = 256;
+constexpr uint32_t HIST_LDS = 16384;  // buckets per group histogrammed in LDS
+
+__device__ __forceinline__ uint32_t bucket_local(uint32_t pc, uint32_t bits) {
+  return bits ? (hash32(pc) >> (32 - bits)) : 0u;
+}
+
+__global__ __launch_bounds__(BK_BLOCK) void k_bucket_count(const Chunk* chunks, const GBucket* gb, const uint32_t* members,
+                                                           const uint64_t* off, const uint32_t* pcs, uint32_t* bcount) {
+  __shared__ uint32_t hist[HIST_LDS];
+  const Chunk ch = chunks[blockIdx.x];
+  const GBucket b = gb[ch.g];
+  const uint32_t nb = 1u << b.bits;
+  const bool lds = nb <= HIST_LDS;
+  if (lds) {
+    for (uint32_t i = threadIdx.x; i < nb; i += BK_BLOCK) hist[i] = 0;
+    __syncthreads();
+  }
+  for (uint32_t m = ch.mbeg; m < ch.mend; m++) {
+    const uint32_t e = members[m];
+    const uint64_t beg = off[e], end = off[e + 1];
+    for (uint64_t k = beg + threadIdx.x; k < end; k += BK_BLOCK) {
+      const uint32_t lb = bucket_local(pcs[k], b.bits);
+      if (lds)
+        atomicAdd(&hist[lb], 1u);
+      else
+        atomicAdd(&bcount[b.base + lb], 1u);
+    }
+  }
+  if (lds) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += BK_BLOCK)
+      if (hist[i]) atomicAdd(&bcount[b.base + i], hist[i]);
+  }
+}
+
+__global__ __launch_bounds__(BK_BLOCK) void k_bucket_scatter(const Chunk* chunks, const GBucket* gb,
+                                                             const uint32_t* members, const uint64_t* off,
+                                                             const uint32_t* pcs, const uint32_t* rank_of_member,
+                                                             const uint64_t* boff, uint32_t* bcursor, uint2* items) {
+  __shared__ uint32_t hist[HIST_LDS];
+  const Chunk ch = chunks[blockIdx.x];
+  const GBucket b = gb[ch.g];
+  const uint32_t nb = 1u << b.bits;
+  const bool lds = nb <= HIST_LDS;
+  if (lds) {
+    for (uint32_t i = threadIdx.x; i < nb; i += BK_BLOCK) hist[i] = 0;
+    __syncthreads();
+    for (uint32_t m = ch.mbeg; m < ch.mend; m++) {
+      const uint32_t e = members[m];
+      for (uint64_t k = off[e] + threadIdx.x; k < off[e + 1]; k += BK_BLOCK)
+        atomicAdd(&hist[bucket_local(pcs[k], b.bits)], 1u);
+    }
+    __syncthreads();
+    // reserve this chunk's slice of every touched bucket; hist becomes the running cursor
+    for (uint32_t i = threadIdx.x; i < nb; i += BK_BLOCK)
+      if (hist[i]) hist[i] = atomicAdd(&bcursor[b.base + i], hist[i]);
+    __syncthreads();
+  }
+  for (uint32_t m = ch.mbeg; m < ch.mend; m++) {
+    const uint32_t e = members[m];
+    const uint32_t R = rank_of_member[m];
+    for (uint64_t k = off[e] + threadIdx.x; k < off[e + 1]; k += BK_BLOCK) {
+      const uint32_t pc = pcs[k];
+      const uint32_t lb = bucket_local(pc, b.bits);
+      const uint32_t slot = lds ? atomicAdd(&hist[lb], 1u) : atomicAdd(&bcursor[b.base + lb], 1u);
+      items[boff[b.base + lb] + slot] = make_uint2(pc, R);
+    }
+  }
+}
+
+// ---- 4. hash pass: min rank per pc inside one bucket -------------------------------------------
+constexpr int HT_BLOCK = 512;
+constexpr uint32_t HT_SLOTS = 16384;
+constexpr uint32_t HT_EMPTY = 0xFFFFFFFFu;  // pc == 0xFFFFFFFF is handled out of table
+constexpr uint32_t HT_ROUND_ITEMS = 12288;
+
+__device__ __forceinline__ uint32_t hslot(uint32_t pc) { return (pc * 0x9E3779B1u) >> 18; }  // 14 bits
+
+__global__ __launch_bounds__(HT_BLOCK) void k_bucket_hash(const uint64_t* boff, uint32_t nbuckets, const uint2* items,
+                                                          uint8_t* sel_rank) {
+  __shared__ uint32_t keys[HT_SLOTS];
+  __shared__ uint32_t vals[HT_SLOTS];
+  __shared__ uint32_t sent_min;
+  __shared__ int full;
+  for (uint32_t bk = blockIdx.x; bk < nbuckets; bk += gridDim.x) {
+    const uint64_t beg = boff[bk], end = boff[bk + 1];
+    const uint64_t cnt = end - beg;
+    if (cnt == 0) continue;
+    uint32_t rounds = (uint32_t)((cnt + HT_ROUND_ITEMS - 1) / HT_ROUND_ITEMS);
+    for (;;) {
+      bool restart = false;
+      for (uint32_t r = 0; r < rounds && !restart; r++) {
+        for (uint32_t i = threadIdx.x; i < HT_SLOTS; i += HT_BLOCK) {
+          keys[i] = HT_EMPTY;
+          vals[i] = 0xFFFFFFFFu;
+        }
+        if (threadIdx.x == 0) {
+          sent_min = 0xFFFFFFFFu;
+          full = 0;
+        }
+        __syncthreads();
+        for (uint64_t k = beg + threadIdx.x; k < end; k += HT_BLOCK) {
+          const uint2 it = items[k];
+          const uint32_t pc = it.x, R = it.y;
+          if (rounds > 1 && (hash32(pc ^ 0x5bd1e995u) % rounds) != r) continue;
+          if (pc == HT_EMPTY) {
+            atomicMin(&sent_min, R);
+            continue;
+          }
+          uint32_t h = hslot(pc);
+          uint32_t probes = 0;
+          for (;;) {
+            const uint32_t cur = keys[h];
+            if (cur == pc || (cur == HT_EMPTY && atomicCAS(&keys[h], HT_EMPTY, pc) == HT_EMPTY) ||
+                keys[h] == pc) {
+              if (vals[h] > R) atomicMin(&vals[h], R);
+              break;
+            }
+            h = (h + 1) & (HT_SLOTS - 1);
+            if (++probes >= HT_SLOTS) {
+              full = 1;
+              break;
+            }
+          }
+        }
+        __syncthreads();
+        if (full) {
+          restart = true;
+        } else {
+          for (uint32_t i = threadIdx.x; i < HT_SLOTS; i += HT_BLOCK)
+            if (keys[i] != HT_EMPTY) sel_rank[vals[i]] = 1;
+          if (threadIdx.x == 0 && sent_min != 0xFFFFFFFFu) sel_rank[sent_min] = 1;
+        }
+        __syncthreads();
+      }
+      if (!restart) break;
+      rounds *= 2;  // completed rounds' marks are exact, re-marking is idempotent
+    }
+  }
+}
+
+// ---- 5. selection outputs --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_select_out(const uint8_t* sel_rank, const uint32_t* ent_of_rank, size_t n,
+                                                    const uint16_t* prog_len, int32_t C, uint8_t* selected,
+                                                    int64_t* hist, int* err) {
+  extern __shared__ unsigned long long lh[];
+  const bool do_hist = prog_len != nullptr;
+  if (do_hist) {
+    for (int32_t i = threadIdx.x; i <= C; i += blockDim.x) lh[i] = 0;
+    __syncthreads();
+  }
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t e = ent_of_rank[r];
+    const uint8_t s = sel_rank[r];
+    if (selected) selected[e] = s;
+    if (do_hist && s) {
+      const uint32_t L = prog_len[e];
+      if ((int32_t)L > C)
+        atomicOr(err, 2);
+      else
+        atomicAdd(&lh[L], 1ull);
+    }
+  }
+  if (do_hist) {
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i <= C; i += blockDim.x)
+      if (lh[i]) atomicAdd((unsigned long long*)&hist[i], lh[i]);
+  }
+}
+
+__global__ void k_compact_ranks(const uint8_t* sel_rank, const uint64_t* pos, const uint32_t* ent_of_rank, size_t n,
+                                int64_t* out) {
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
+    if (sel_rank[r]) out[pos[r]] = (int64_t)ent_of_rank[r];
+}
+
+__global__ void k_group_out_off(const uint64_t* pos, const uint64_t* gstart, uint32_t G, uint64_t* goff) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x)
+    goff[g] = pos[gstart[g]];
+}
+
+// ---- host orchestration ------------------------------------------------------------------------------
+
+struct MinState {
+  uint64_t* gstart = nullptr;
+  uint8_t* sel_rank = nullptr;
+  uint32_t* ent_of_rank = nullptr;
+};
+static MinState g_min;
+
+void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
+                          size_t n, uint32_t G, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s) {
+  Context& c = ctx();
+  if (G == 0 || G > MAX_GROUPS) fail(SYZGPU_EINVAL, "ngroups out of range (1..4096)");
+  if (n >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
+  Scratch& sc = c.scratch;
+  const uint32_t nchunks = (uint32_t)((n + PW_ITEMS - 1) / PW_ITEMS);
+  int* err = sc.get<int>("mz_err", 2);
+  uint32_t* cnt = sc.get<uint32_t>("mz_cnt", (size_t)G * nchunks + 1);
+  uint64_t* cnt_scan = sc.get<uint64_t>("mz_cnt_scan", (size_t)G * nchunks + 1);
+  uint64_t* gpcs = sc.get<uint64_t>("mz_gpcs", G + 1);
+  uint64_t* gstart = sc.get<uint64_t>("mz_gstart", G + 1);
+  uint32_t* members = sc.get<uint32_t>("mz_members", n + 1);
+  uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
+  uint32_t* rank_of_member = sc.get<uint32_t>("mz_rom", n + 1);
+  uint32_t* ent_of_rank = sc.get<uint32_t>("mz_eor", n + 1);
+  uint8_t* sel_rank = sc.get<uint8_t>("mz_sel", n + 1);
+  SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
+  SYZ_HIP(hipMemsetAsync(cnt, 0, ((size_t)G * nchunks + 1) * 4, s));
+  SYZ_HIP(hipMemsetAsync(gpcs, 0, (G + 1) * 8, s));
+  SYZ_HIP(hipMemsetAsync(sel_rank, 0, n + 1, s));
+  if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
+  {
+    ProfScope ps("group_partition", s, (uint64_t)n * 28);
+    if (n) {
+      const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
+      k_grp_count<<<wg, 256, 4 * G * 4, s>>>(group, n, G, nchunks, cnt, err);
+      SYZ_LAUNCHED();
+      k_grp_sumlen<<<grid_for(n, 256, 2048), 256, G * 8, s>>>(group, off, n, G, gpcs);
+      SYZ_LAUNCHED();
+    }
+    exclusive_scan_u32(cnt, cnt_scan, (size_t)G * nchunks, s);
+    k_grp_starts<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(cnt_scan, G, nchunks, n, gstart);
+    SYZ_LAUNCHED();
+    if (n) {
+      const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
+      k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, cnt_scan, members, el);
+      SYZ_LAUNCHED();
+    }
+  }
+  // host needs the group layout to plan the sort roots and the bucket layout
+  uint64_t* hbuf = c.pinned.get<uint64_t>(2 * (size_t)G + 4);
+  int* herr = reinterpret_cast<int*>(hbuf + 2 * (size_t)G + 2);
+  SYZ_HIP(hipMemcpyAsync(hbuf, gstart, (G + 1) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hbuf + G + 1, gpcs, G * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(herr, err, 4, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (*herr) fail(SYZGPU_EINVAL, "group id >= ngroups");
+  std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
+
+  if (n) gosort_groups(el, n, gstart, G, s);
+  {
+    ProfScope ps("ranks", s, (uint64_t)n * 16);
+    if (n) {
+      k_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(el, n, members, rank_of_member, ent_of_rank);
+      SYZ_LAUNCHED();
+    }
+  }
+
+  // bucket layout: ~HT_ROUND_ITEMS occurrences per bucket, power-of-two buckets per group
+  std::vector<GBucket> hgb(G);
+  std::vector<Chunk> hch;
+  uint32_t nbuckets = 0;
+  uint64_t total_pcs = 0;
+  for (uint32_t g = 0; g < G; g++) {
+    const uint64_t np = hpcs[g];
+    total_pcs += np;
+    uint32_t bits = 0;
+    while (bits < 24 && ((uint64_t)HT_ROUND_ITEMS << bits) < np) bits++;
+    hgb[g] = GBucket{nbuckets, bits};
+    nbuckets += 1u << bits;
+    const uint64_t ng = hstart[g + 1] - hstart[g];
+    if (ng == 0) continue;
+    const uint64_t avg = std::max<uint64_t>(1, np / ng);
+    const uint64_t target = std::max<uint64_t>(32768, 4ull << bits);
+    const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ng, target / avg));
+    for (uint64_t m = hstart[g]; m < hstart[g + 1]; m += per)
+      hch.push_back(Chunk{g, (uint32_t)m, (uint32_t)std::min<uint64_t>(hstart[g + 1], m + per), 0});
+  }
+  GBucket* dgb = sc.get<GBucket>("mz_gb", G);
+  Chunk* dch = sc.get<Chunk>("mz_chunks", hch.size() + 1);
+  uint32_t* bcount = sc.get<uint32_t>("mz_bcount", nbuckets + 1);
+  uint64_t* boff = sc.get<uint64_t>("mz_boff", nbuckets + 1);
+  uint32_t* bcursor = sc.get<uint32_t>("mz_bcursor", nbuckets + 1);
+  uint2* items = sc.get<uint2>("mz_items", total_pcs + 1);
+  SYZ_HIP(hipMemcpyAsync(dgb, hgb.data(), G * sizeof(GBucket), hipMemcpyHostToDevice, s));
+  if (!hch.empty()) SYZ_HIP(hipMemcpyAsync(dch, hch.data(), hch.size() * sizeof(Chunk), hipMemcpyHostToDevice, s));
+  SYZ_HIP(hipMemsetAsync(bcount, 0, (nbuckets + 1) * 4, s));
+  SYZ_HIP(hipMemsetAsync(bcursor, 0, (nbuckets + 1) * 4, s));
+  if (!hch.empty()) {
+    {
+      ProfScope ps("bucket_count", s, total_pcs * 4 + n * 16);
+      k_bucket_count<<<(unsigned)hch.size(), BK_BLOCK, 0, s>>>(dch, dgb, members, off, pcs, bcount);
+      SYZ_LAUNCHED();
+    }
+    exclusive_scan_u32(bcount, boff, nbuckets, s);
+    {
+      ProfScope ps("bucket_scatter", s, total_pcs * 12 + n * 20);
+      k_bucket_scatter<<<(unsigned)hch.size(), BK_BLOCK, 0, s>>>(dch, dgb, members, off, pcs, rank_of_member, boff,
+                                                                 bcursor, items);
+      SYZ_LAUNCHED();
+    }
+    {
+      ProfScope ps("bucket_hash", s, total_pcs * 8);
+      k_bucket_hash<<<std::min<uint32_t>(nbuckets, 65536), HT_BLOCK, 0, s>>>(boff, nbuckets, items, sel_rank);
+      SYZ_LAUNCHED();
+    }
+  }
+  {
+    ProfScope ps("select_out", s, (uint64_t)n * 8);
+    if (n) {
+      k_select_out<<<grid_for(n, 256, 2048), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
+          sel_rank, ent_of_rank, n, len_hist ? prog_len : nullptr, C, selected, len_hist, err);
+      SYZ_LAUNCHED();
+    }
+  }
+  if (len_hist) {
+    int* h = c.pinned.get<int>(4);
+    SYZ_HIP(hipMemcpyAsync(h, err, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (h[0] & 2) fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
+  }
+  g_min.gstart = gstart;
+  g_min.sel_rank = sel_rank;
+  g_min.ent_of_rank = ent_of_rank;
+  c.last_n = n;
+  c.last_groups = G;
+  c.have_last = true;
+}
+
+void minimize_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n, uint32_t G, hipStream_t s) {
+  Context& c = ctx();
+  if (!c.have_last || c.last_n != n || c.last_groups != G) fail(SYZGPU_EINVAL, "no matching minimize result");
+  uint64_t* pos = c.scratch.get<uint64_t>("mz_pos", n + 1);
+  int64_t* dout = c.scratch.get<int64_t>("mz_out", n + 1);
+  uint64_t* dgoff = c.scratch.get<uint64_t>("mz_goff", G + 1);
+  exclusive_scan_u8(g_min.sel_rank, pos, n, s);
+  if (n) {
+    k_compact_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(g_min.sel_rank, pos, g_min.ent_of_rank, n, dout);
+    SYZ_LAUNCHED();
+  }
+  k_group_out_off<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(pos, g_min.gstart, G, dgoff);
+  SYZ_LAUNCHED();
+  SYZ_HIP(hipMemcpyAsync(group_out_off, dgoff, (G + 1) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  const uint64_t m = group_out_off[G];
+  if (m) SYZ_HIP(hipMemcpyAsync(out_idx, dout, m * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+}
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" {
+
+int syzgpu_minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                const uint16_t* prog_len, size_t n, uint32_t ngroups, int32_t C, uint8_t* selected,
+                                int64_t* len_hist, void* stream) {
+  SYZ_API_BODY({
+    if (len_hist && (C <= 0 || !prog_len)) fail(SYZGPU_EINVAL, "len_hist needs prog_len and C > 0");
+    minimize_grouped_dev(pcs, off, group, prog_len, n, ngroups, C, selected, len_hist, (hipStream_t)stream);
+  })
+}
+
+int syzgpu_minimize_grouped_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n, uint32_t ngroups) {
+  SYZ_API_BODY({ minimize_fetch(out_idx, group_out_off, n, ngroups, C_.stream); })
+}
+
+int syzgpu_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                            uint32_t ngroups, int64_t* out_idx, uint64_t* group_out_off) {
+  SYZ_API_BODY({
+    if (!off || !group_out_off || (n && (!group || !out_idx))) fail(SYZGPU_EINVAL, "null pointer");
+    if (off[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
+    hipStream_t s = C_.stream;
+    const uint64_t tot = off[n];
+    uint32_t* dp = C_.scratch.get<uint32_t>("mg_pcs", tot + 1);
+    uint64_t* doff = C_.scratch.get<uint64_t>("mg_off", n + 1);
+    uint32_t* dg = C_.scratch.get<uint32_t>("mg_grp", n + 1);
+    if (tot) SYZ_HIP(hipMemcpyAsync(dp, pcs, tot * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (n) SYZ_HIP(hipMemcpyAsync(dg, group, n * 4, hipMemcpyHostToDevice, s));
+    minimize_grouped_dev(dp, doff, dg, nullptr, n, ngroups, 0, nullptr, nullptr, s);
+    minimize_fetch(out_idx, group_out_off, n, ngroups, s);
+  })
+}
+
+int syzgpu_minimize(const uint32_t* pcs, const uint64_t* off, size_t ncov, int64_t* out_idx, size_t* out_n) {
+  SYZ_API_BODY({
+    if (!off || !out_n) fail(SYZGPU_EINVAL, "null pointer");
+    std::vector<uint32_t> grp(ncov, 0);
+    uint64_t goff[2] = {0, 0};
+    if (ncov == 0) {
+      *out_n = 0;
+      return SYZGPU_OK;
+    }
+    int rc = syzgpu_minimize_grouped(pcs, off, grp.data(), ncov, 1, out_idx, goff);
+    if (rc) return rc;
+    *out_n = (size_t)goff[1];
+  })
+}
+
+}  // extern "C"
+

@@ -1,0 +1,31 @@
+// Internal interfaces between the kernels of libsyzgpu.so.
+#pragma once
+#include "common.hpp"
+
+namespace syz {
+
+struct Seg {
+  uint32_t lo, hi;
+  int32_t depth;  // remaining sort.Sort maxDepth budget at this recursion node
+  uint32_t pad;
+};
+
+constexpr uint32_t FIN_MAX = 1024;  // segments up to this size are finished by one wave in LDS
+
+// gosort.hip
+void gosort_groups(uint64_t* el, size_t n, const uint64_t* gstart_dev, uint32_t ngroups, hipStream_t s);
+
+// setops.hip
+uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64_t na, const uint32_t* b,
+                         const uint64_t* boff, uint64_t nb, uint32_t npairs, uint32_t* out, uint64_t out_cap,
+                         uint64_t* out_off_dev, hipStream_t s);
+void canonicalize_batch_dev(uint32_t* pcs, const uint64_t* off, const uint64_t* host_off, size_t ncov,
+                            uint64_t* out_len, hipStream_t s);
+
+// prio.hip
+void len_hist_dev(const uint16_t* prog_len, const uint8_t* sel, size_t n, int32_t C, int64_t* hist, int* err,
+                  hipStream_t s);
+void prio_choice_dev(const float* static_prios, const int64_t* len_hist, const float* prios_in, int32_t C,
+                     const uint8_t* enabled, float* prios_out, int64_t* run, uint8_t* present, hipStream_t s);
+
+}  // namespace syz

@@ -1,0 +1,249 @@
+// Context, error state, scratch memory, profiling and the device-wide scans.
+#include <cstdio>
+
+#include "common.hpp"
+
+namespace syz {
+
+static thread_local std::string g_last_error;
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+[[noreturn]] void fail(int code, const std::string& msg) { throw Error{code, msg}; }
+
+void* Scratch::get(const std::string& name, size_t bytes) {
+  Buf& b = bufs_[name];
+  if (b.bytes >= bytes && b.p) return b.p;
+  if (b.p) SYZ_HIP(hipFree(b.p));
+  b.p = nullptr;
+  b.bytes = 0;
+  size_t want = bytes < 256 ? 256 : bytes;
+  want += want / 8;  // headroom for slightly larger next calls
+  SYZ_HIP(hipMalloc(&b.p, want));
+  b.bytes = want;
+  return b.p;
+}
+
+void Scratch::release() {
+  for (auto& kv : bufs_)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  bufs_.clear();
+}
+
+void* Pinned::get(size_t bytes) {
+  if (bytes_ >= bytes && p_) return p_;
+  if (p_) (void)hipHostFree(p_);
+  p_ = nullptr;
+  SYZ_HIP(hipHostMalloc(&p_, bytes, hipHostMallocDefault));
+  bytes_ = bytes;
+  return p_;
+}
+
+Pinned::~Pinned() {
+  if (p_) (void)hipHostFree(p_);
+}
+
+static std::mutex g_ctx_mu;
+static Context* g_ctx = nullptr;
+
+static void init_device(int dev) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) fail(SYZGPU_ENODEV, "no HIP device available");
+  if (dev < 0 || dev >= n) fail(SYZGPU_ENODEV, "device index out of range");
+  hipDeviceProp_t prop;
+  SYZ_HIP(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    fail(SYZGPU_ENODEV, std::string("libsyzgpu is built for gfx950 only, found ") + prop.gcnArchName);
+  SYZ_HIP(hipSetDevice(dev));
+  Context* c = new Context();
+  c->device = dev;
+  SYZ_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  g_ctx = c;
+}
+
+Context& ctx() {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if (!g_ctx) init_device(0);
+  SYZ_HIP(hipSetDevice(g_ctx->device));
+  return *g_ctx;
+}
+
+Prof& prof() {
+  static Prof p;
+  return p;
+}
+
+void Prof::reset() {
+  recs.clear();
+  used = 0;
+}
+
+void Prof::begin(const char* name, hipStream_t s, uint64_t bytes) {
+  if (used + 2 > pool.size()) {
+    for (int i = 0; i < 64; i++) {
+      hipEvent_t e;
+      SYZ_HIP(hipEventCreate(&e));
+      pool.push_back(e);
+    }
+  }
+  Rec r{name, pool[used], pool[used + 1], bytes};
+  used += 2;
+  SYZ_HIP(hipEventRecord(r.a, s));
+  recs.push_back(r);
+}
+
+void Prof::end(hipStream_t s) { SYZ_HIP(hipEventRecord(recs.back().b, s)); }
+
+// ---- device-wide exclusive scan: reduce tiles, scan tile sums (recursively), add back ----------
+constexpr int SCAN_BLOCK = 256;
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+template <class T>
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const T* in, size_t n, uint64_t* sums) {
+  __shared__ uint64_t lds[SCAN_BLOCK / 64 + 1];
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    size_t i = base + (size_t)k * SCAN_BLOCK + threadIdx.x;
+    if (i < n) s += (uint64_t)in[i];
+  }
+  uint64_t tot = block_sum<SCAN_BLOCK>(s, lds);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+template <class T>
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const T* in, size_t n, const uint64_t* offs,
+                                                           uint64_t* out, int write_total) {
+  __shared__ uint64_t lds[SCAN_BLOCK / 64 + 1];
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+  uint64_t v[SCAN_ITEMS];
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    size_t i = base + k;
+    v[k] = i < n ? (uint64_t)in[i] : 0;
+    s += v[k];
+  }
+  uint64_t tot;
+  uint64_t pre = block_excl_scan<SCAN_BLOCK>(s, lds, &tot) + offs[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    size_t i = base + k;
+    if (i < n) out[i] = pre;
+    pre += v[k];
+  }
+  if (write_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) out[n] = pre;
+}
+
+__global__ void k_zero_total(uint64_t* out) { out[0] = 0; }
+
+template <class T>
+static void scan_impl(const T* in, uint64_t* out, size_t n, hipStream_t s, int depth) {
+  if (n == 0) {
+    k_zero_total<<<1, 1, 0, s>>>(out);
+    SYZ_LAUNCHED();
+    return;
+  }
+  const size_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  Scratch& sc = ctx().scratch;
+  uint64_t* sums = sc.get<uint64_t>("scan_sums" + std::to_string(depth), tiles + 1);
+  uint64_t* offs = sc.get<uint64_t>("scan_offs" + std::to_string(depth), tiles + 1);
+  if (tiles == 1) {
+    SYZ_HIP(hipMemsetAsync(offs, 0, sizeof(uint64_t), s));
+  } else {
+    k_scan_reduce<T><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, sums);
+    SYZ_LAUNCHED();
+    scan_impl<uint64_t>(sums, offs, tiles, s, depth + 1);
+  }
+  k_scan_apply<T><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, offs, out, 1);
+  SYZ_LAUNCHED();
+}
+
+void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s) {
+  scan_impl<uint8_t>(in, out, n, s, 0);
+}
+void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s) {
+  scan_impl<uint32_t>(in, out, n, s, 0);
+}
+void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) {
+  scan_impl<uint64_t>(in, out, n, s, 0);
+}
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" {
+
+int syzgpu_init(int device) {
+  try {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    if (g_ctx) {
+      if (g_ctx->device == device) return SYZGPU_OK;
+      fail(SYZGPU_EINVAL, "already initialised on another device");
+    }
+    init_device(device);
+    return SYZGPU_OK;
+  } catch (const Error& e) {
+    set_last_error(e.msg);
+    return e.code;
+  }
+}
+
+int syzgpu_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if (g_ctx) {
+    g_ctx->scratch.release();
+    if (g_ctx->stream) (void)hipStreamDestroy(g_ctx->stream);
+    delete g_ctx;
+    g_ctx = nullptr;
+  }
+  return SYZGPU_OK;
+}
+
+int syzgpu_device_count(int* n) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return SYZGPU_OK;
+}
+
+size_t syzgpu_last_error(char* buf, size_t cap) {
+  const std::string& m = g_last_error;
+  if (buf && cap) {
+    size_t k = m.size() < cap - 1 ? m.size() : cap - 1;
+    std::memcpy(buf, m.data(), k);
+    buf[k] = 0;
+  }
+  return m.size();
+}
+
+const char* syzgpu_version(void) { return "syzgpu 0.1 gfx950"; }
+
+int syzgpu_profile_enable(int on) {
+  prof().on = on != 0;
+  prof().reset();
+  return SYZGPU_OK;
+}
+
+size_t syzgpu_profile_read(char (*names)[48], float* ms, uint64_t* bytes, size_t cap) {
+  Prof& p = prof();
+  size_t k = 0;
+  for (auto& r : p.recs) {
+    if (k >= cap) break;
+    float t = 0;
+    if (hipEventSynchronize(r.b) != hipSuccess) continue;
+    if (hipEventElapsedTime(&t, r.a, r.b) != hipSuccess) continue;
+    std::snprintf(names[k], 48, "%s", r.name.c_str());
+    ms[k] = t;
+    bytes[k] = r.bytes;
+    k++;
+  }
+  p.reset();
+  return k;
+}
+
+}  // extern "C"

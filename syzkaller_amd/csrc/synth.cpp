@@ -156,15 +156,16 @@ extern "C" int syzgpu_synth_layout(const syzgpu_synth_params* p, uint32_t* group
   return 0;
 }
 
-extern "C" int syzgpu_synth_fill(const syzgpu_synth_params* p, const uint32_t* group,
-                                 const uint64_t* off, uint32_t* pcs, int nthreads) {
+extern "C" int syzgpu_synth_fill_ids(const syzgpu_synth_params* p, const uint64_t* ids, const uint32_t* group,
+                                     const uint64_t* off, uint64_t n, uint32_t* pcs, int nthreads) {
   Layout L;
   if (!make_layout(p, &L)) return 1;
-  parallel_for(p->n, nthreads, [&](uint64_t lo, uint64_t hi) {
+  parallel_for(n, nthreads, [&](uint64_t lo, uint64_t hi) {
     std::vector<uint32_t> buf;
-    for (uint64_t e = lo; e < hi; e++) {
-      const uint32_t g = group[e];
-      const uint64_t len = off[e + 1] - off[e];
+    for (uint64_t k = lo; k < hi; k++) {
+      const uint64_t e = ids ? ids[k] : k;  // global entry id: seeds the draws
+      const uint32_t g = group[k];
+      const uint64_t len = off[k + 1] - off[k];
       Rng r(splitmix((p->seed ^ 0x5EED5EEDull) * 0x100000001B3ull + e));
       buf.clear();
       uint64_t attempts = 0;
@@ -193,8 +194,13 @@ extern "C" int syzgpu_synth_fill(const syzgpu_synth_params* p, const uint32_t* g
           buf.insert(std::upper_bound(buf.begin(), buf.end(), pc), pc);
         }
       }
-      std::memcpy(pcs + off[e], buf.data(), len * sizeof(uint32_t));
+      std::memcpy(pcs + off[k], buf.data(), len * sizeof(uint32_t));
     }
   });
   return 0;
+}
+
+extern "C" int syzgpu_synth_fill(const syzgpu_synth_params* p, const uint32_t* group,
+                                 const uint64_t* off, uint32_t* pcs, int nthreads) {
+  return syzgpu_synth_fill_ids(p, nullptr, group, off, p->n, pcs, nthreads);
 }

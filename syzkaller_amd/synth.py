@@ -41,6 +41,8 @@ def _lib():
                                           ctypes.c_void_p]
         L.syzgpu_synth_fill.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_int]
+        L.syzgpu_synth_fill_ids.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
         _LIB = L
     return _LIB
 
@@ -85,3 +87,30 @@ def corpus(seed, n, ngroups=289, npcs=50_000, nthreads=None, **kw):
     if rc:
         raise ValueError("bad synth params")
     return Corpus(pcs, off, group, plen, ngroups)
+
+
+def layout(p):
+    """(group u32[n], off u64[n+1], prog_len u16[n]) of the corpus described by params p."""
+    n = int(p.n)
+    group = np.empty(n, dtype=np.uint32)
+    off = np.empty(n + 1, dtype=np.uint64)
+    plen = np.empty(n, dtype=np.uint16)
+    if _lib().syzgpu_synth_layout(ctypes.byref(p), group.ctypes.data, off.ctypes.data, plen.ctypes.data):
+        raise ValueError("bad synth params")
+    return group, off, plen
+
+
+def subcorpus(p, ids, group, off, plen, nthreads=None):
+    """The entries `ids` (ascending global ids) of the corpus p, as a Corpus of their own."""
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    lens = (off[1:] - off[:-1])[ids]
+    soff = np.zeros(ids.size + 1, dtype=np.uint64)
+    np.cumsum(lens, out=soff[1:])
+    sgroup = np.ascontiguousarray(group[ids])
+    pcs = np.empty(int(soff[-1]), dtype=np.uint32)
+    if nthreads is None:
+        nthreads = min(16, os.cpu_count() or 1)
+    if _lib().syzgpu_synth_fill_ids(ctypes.byref(p), ids.ctypes.data, sgroup.ctypes.data, soff.ctypes.data,
+                                    ids.size, pcs.ctypes.data, nthreads):
+        raise ValueError("bad synth params")
+    return Corpus(pcs, soff, sgroup, np.ascontiguousarray(plen[ids]), int(p.ngroups))

@@ -1,0 +1,302 @@
+"""Parity of the MI355X path (libsyzgpu.so, through the C ABI) with the CPU oracle.
+
+Bit-exact for every integer result (set ops, Canonicalize, Minimize selection and order, ChoiceTable)
+and bit-exact for float32 priorities too (the north star allows 1e-6 relative; the kernels reproduce
+Go's per-op float32 rounding, so the test demands identical bits). Layout mirrors
+cover/cover_test.go: the known-answer tables first, then seeded random/property cases, then the
+BASELINE.json configs at sizes the oracle finishes in seconds.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle  # noqa: E402
+
+from syzkaller_amd import _lib, cover, prog, synth  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+SETOPS = {
+    "difference": cover.Difference,
+    "symmetric_difference": cover.SymmetricDifference,
+    "union": cover.Union,
+    "intersection": cover.Intersection,
+}
+
+
+@pytest.fixture(scope="session", autouse=True)
+def device():
+    n = np.zeros(1, np.int32)
+    _lib.lib().syzgpu_device_count(_lib.ptr(n))
+    assert n[0] >= 1, "GPU tests need a device (no CPU fallback exists)"
+    _lib.check(_lib.lib().syzgpu_init(0))
+    yield
+
+
+# ---- cover_test.go tables ------------------------------------------------------------------------
+@pytest.mark.parametrize("op", list(SETOPS))
+def test_setop_golden(golden, op):
+    for t in golden[op]:
+        res = SETOPS[op](t["v0"], t["v1"])
+        assert list(res) == t["r"], (op, t)
+
+
+def test_canonicalize_golden(golden):
+    for t in golden["canonicalize"]:
+        buf = np.array(t["v0"], dtype=np.uint32)
+        res = cover.Canonicalize(buf)
+        assert list(res) == t["r"]
+        if res.size:
+            assert np.shares_memory(res, buf)  # Go returns cov[:i], aliasing the input (F6)
+
+
+def test_minimize_golden(golden):
+    for t in golden["minimize"]:
+        assert cover.Minimize(t["inp"]) == t["out"], t
+
+
+# ---- set operations ------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(4))
+def test_setops_random_vs_oracle(seed):
+    rnd = np.random.default_rng(seed)
+    a_list, b_list = [], []
+    for _ in range(400):
+        na, nb = int(rnd.integers(0, 50)), int(rnd.integers(0, 50))
+        hi = int(rnd.choice([8, 100, 1 << 32]))
+        a = np.sort(rnd.integers(0, hi, size=na, dtype=np.uint64)).astype(np.uint32)
+        b = np.sort(rnd.integers(0, hi, size=nb, dtype=np.uint64)).astype(np.uint32)
+        if rnd.random() < 0.15:
+            a = np.append(a, np.uint32(0xFFFFFFFF))
+        if rnd.random() < 0.15:
+            b = np.append(b, np.uint32(0xFFFFFFFF))
+        a_list.append(a)
+        b_list.append(b)
+    for op, fn in SETOPS.items():
+        batch = cover.SetOpBatch(op, a_list, b_list)
+        for a, b, got in zip(a_list, b_list, batch):
+            want = oracle.setop(op, a, b)
+            assert np.array_equal(got, want), (op, a, b)
+        for a, b in list(zip(a_list, b_list))[:40]:
+            assert np.array_equal(fn(a, b), oracle.setop(op, a, b))
+
+
+def test_setops_large_lists():
+    # maxCover-sized tables against execution covers (config 3 shape)
+    rnd = np.random.default_rng(9)
+    big = np.unique(rnd.integers(0, 1 << 24, size=300_000)).astype(np.uint32)
+    covs = [np.unique(rnd.integers(0, 1 << 24, size=int(rnd.integers(1, 2000)))).astype(np.uint32)
+            for _ in range(64)]
+    for op in SETOPS:
+        got = cover.SetOpBatch(op, covs, [big] * len(covs))
+        for c, g in zip(covs, got):
+            assert np.array_equal(g, oracle.setop(op, c, big)), op
+
+
+def test_setop_rejects_unsorted():
+    with pytest.raises(_lib.SyzGpuError) as e:
+        cover.Union([3, 1], [2])
+    assert e.value.code == _lib.EINVAL
+
+
+# ---- Canonicalize -----------------------------------------------------------------------------------
+def test_canonicalize_random_vs_oracle():
+    rnd = np.random.default_rng(1)
+    covs = []
+    for size in [0, 1, 2, 12, 13, 100, 1023, 1024, 1025, 16383, 16384, 16385, 40000]:
+        covs.append(rnd.integers(0, max(2, size // 2), size=size, dtype=np.uint64).astype(np.uint32))
+    covs.append(np.full(7, 0xFFFFFFFF, np.uint32))                       # only the sentinel -> empty
+    covs.append(np.array([5, 0xFFFFFFFF, 5, 0xFFFFFFFF, 1], np.uint32))    # sentinel kept after others
+    covs.append(rnd.integers(0, 1 << 32, size=5000, dtype=np.uint64).astype(np.uint32))
+    pcs, off = cover.to_csr(covs)
+    work = pcs.copy()
+    lens = cover.CanonicalizeBatch(work, off)
+    for i, c in enumerate(covs):
+        want = oracle.canonicalize(c)
+        got = work[int(off[i]):int(off[i]) + int(lens[i])]
+        assert np.array_equal(got, want), i
+        one = cover.Canonicalize(c.copy())
+        assert np.array_equal(one, want), i
+
+
+# ---- Minimize -----------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(4))
+def test_minimize_random_property(seed):
+    # cover_test.go:170-205 with fixed seeds, plus exact equality with the oracle
+    rnd = np.random.default_rng(seed)
+    for _ in range(60):
+        n = int(rnd.integers(0, 20))
+        covs = [oracle.canonicalize(rnd.integers(0, 100, size=int(rnd.integers(0, 10)))) for _ in range(n)]
+        got = cover.Minimize(covs)
+        assert got == list(oracle.minimize(covs)) if n else got == []
+        total = np.unique(np.concatenate(covs)) if n else np.zeros(0)
+        mini = np.unique(np.concatenate([covs[i] for i in got])) if got else np.zeros(0)
+        assert np.array_equal(total, mini)
+
+
+@pytest.mark.parametrize("n,lenmax", [(13, 3), (41, 2), (200, 4), (1500, 3), (5000, 6), (30000, 5), (120000, 9)])
+def test_minimize_tie_heavy_vs_oracle(n, lenmax):
+    # many equal lengths: exercises every branch of the sort.Sort simulation (ninther, protect
+    # pass, shell+insertion), across the finisher (<= 1024) and the level kernel (> 1024)
+    rnd = np.random.default_rng(n)
+    lens = rnd.integers(1, lenmax + 1, size=n)
+    covs = [np.sort(rnd.choice(4 * lenmax + 40, size=int(l), replace=False)).astype(np.uint32) for l in lens]
+    pcs, off = cover.to_csr(covs)
+    assert np.array_equal(oracle.minimize(pcs=pcs, off=off), np.array(cover.Minimize(covs), dtype=np.int64))
+
+
+def test_minimize_sort_permutation_distinct_and_sorted_lengths():
+    for lens in [np.arange(3000), np.arange(3000)[::-1], np.zeros(3000, int) + 7]:
+        covs = [np.arange(int(l) + 1, dtype=np.uint32) * 0 + np.uint32(i) for i, l in enumerate(lens)]
+        pcs, off = cover.to_csr(covs)
+        assert np.array_equal(oracle.minimize(pcs=pcs, off=off), np.array(cover.Minimize(covs), dtype=np.int64))
+
+
+def _grouped_parity(c):
+    want, wgoff = oracle.minimize_grouped(c.pcs, c.off, c.group, c.ngroups)
+    got, ggoff = cover.MinimizeCorpus(c.pcs, c.off, c.group, c.ngroups)
+    assert np.array_equal(wgoff, ggoff)
+    assert np.array_equal(want, got)
+    return got
+
+
+def test_minimize_corpus_config1_vs_oracle():
+    # BASELINE.json configs[0]: 10k programs, ~50k PCs, 289 calls
+    c = synth.corpus(0x5EED0001, 10_000, 289, 50_000)
+    _grouped_parity(c)
+
+
+def test_minimize_corpus_config2_vs_oracle():
+    # BASELINE.json configs[1]: 100k programs, 500k PCs
+    c = synth.corpus(0x5EED0002, 100_000, 289, 500_000)
+    _grouped_parity(c)
+
+
+def test_minimize_corpus_few_big_groups():
+    # groups far above FIN_MAX (level kernel), short covers -> heavy ties, with 0xFFFFFFFF PCs
+    c = synth.corpus(77, 60_000, 3, 3000, len_median=3.0, len_sigma=0.5)
+    c.pcs[c.off[1:-1][::97].astype(np.int64) - 1] = 0xFFFFFFFF  # last PC of some covers
+    _grouped_parity(c)
+
+
+def test_minimize_corpus_property_full_size():
+    # size-independent property at the bench scale: per group, union(kept) == union(all)
+    c = synth.corpus(0x5EED0004, 300_000, 289, 2_000_000)
+    kept, goff = cover.MinimizeCorpus(c.pcs, c.off, c.group, c.ngroups)
+    lens = np.diff(c.off).astype(np.int64)
+    ent = np.repeat(np.arange(c.n), lens)
+    key_all = (c.group[ent].astype(np.uint64) << np.uint64(32)) | c.pcs.astype(np.uint64)
+    mask = np.zeros(c.n, bool)
+    mask[kept] = True
+    key_kept = key_all[mask[ent]]
+    assert np.array_equal(np.unique(key_all), np.unique(key_kept))
+    # selection order: within each group, kept entries have non-increasing cover length
+    for g in range(c.ngroups):
+        k = kept[int(goff[g]):int(goff[g + 1])]
+        assert np.all(np.diff(lens[k]) <= 0)
+        assert np.all(c.group[k] == g)
+
+
+def test_minimize_rejects_bad_group():
+    with pytest.raises(_lib.SyzGpuError) as e:
+        cover.MinimizeCorpus(np.array([1, 2], np.uint32), np.array([0, 1, 2], np.uint64),
+                             np.array([0, 5], np.uint32), 2)
+    assert e.value.code == _lib.EINVAL
+
+
+# ---- priorities / ChoiceTable ---------------------------------------------------------------------
+def _static(C, seed):
+    rnd = np.random.default_rng(seed)
+    s = (rnd.random((C, C)) * 0.9 + 0.1).astype(np.float32)
+    s[rnd.random((C, C)) < 0.1] = 0
+    np.fill_diagonal(s, s.max(axis=1))
+    return s
+
+
+@pytest.mark.parametrize("C,nprogs", [(1, 5), (8, 0), (8, 50), (64, 3000), (1159, 100_000), (1536, 20_000)])
+def test_priorities_bit_exact(C, nprogs):
+    rnd = np.random.default_rng(C + nprogs)
+    plen = rnd.integers(0, min(C, 40) + 1, size=nprogs).astype(np.uint16)
+    st = _static(C, C)
+    dyn_want = oracle.dynamic_prio(plen, C)
+    dyn_got = prog.calcDynamicPrio(plen, C)
+    assert np.array_equal(dyn_want.view(np.uint32), dyn_got.view(np.uint32))
+    want = oracle.calculate_priorities(st, plen)
+    got = prog.CalculatePriorities(st, plen)
+    assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
+    for en in [None, (rnd.random(C) < 0.8).astype(np.uint8)]:
+        wrun, wpres = oracle.build_choice_table(got, en)
+        ct = prog.BuildChoiceTable(got, en)
+        assert np.array_equal(wpres, ct.present)
+        assert np.array_equal(wrun[wpres == 1], ct.run_matrix[wpres == 1])
+
+
+def test_choice_table_special_values():
+    C = 16
+    p = np.random.default_rng(3).random((C, C)).astype(np.float32)
+    p[0, 3] = np.nan
+    p[1, 1] = np.inf
+    p[2, 5] = -np.inf
+    p[3, 7] = 3e16        # int(p*1000) overflows int64 -> Go amd64 gives INT64_MIN
+    p[4, :] = -0.7        # negative truncation toward zero
+    wrun, wpres = oracle.build_choice_table(p, None)
+    ct = prog.BuildChoiceTable(p, None)
+    assert np.array_equal(wrun, ct.run_matrix)
+
+
+def test_priorities_saturating_counts():
+    # H(k) above 2^24: float32 += 1.0 sticks at 16777216 (the reference's accumulator)
+    C = 4
+    nprogs = (1 << 24) + 5000
+    plen = np.full(nprogs, 3, np.uint16)
+    got = prog.calcDynamicPrio(plen, C)
+    raw = np.array([[0, 2**24, 2**24, 0], [2**24, 0, 2**24, 0], [2**24, 2**24, 0, 0], [0, 0, 0, 0]], np.float32)
+    assert np.array_equal(oracle.normalize_prio(raw).view(np.uint32), got.view(np.uint32))
+
+
+def test_priorities_reject_long_programs():
+    with pytest.raises(_lib.SyzGpuError) as e:
+        prog.calcDynamicPrio(np.array([3, 9], np.uint16), 8)
+    assert e.value.code == _lib.EINVAL
+
+
+# ---- device-resident pipeline (what bench.py times) -------------------------------------------------
+def test_resident_pipeline_matches_oracle():
+    import torch
+    C = 1159
+    c = synth.corpus(0x5EED0003, 20_000, 289, 100_000)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else
+                                   (a.view(np.int64) if a.dtype == np.uint64 else
+                                    (a.view(np.int16) if a.dtype == np.uint16 else a))).to(dev)
+    d_pcs, d_off, d_grp, d_len = t(c.pcs), t(c.off), t(c.group), t(c.prog_len)
+    sel = torch.zeros(c.n, dtype=torch.uint8, device=dev)
+    hist = torch.zeros(C + 1, dtype=torch.int64, device=dev)
+    st = _static(C, 5)
+    d_st = torch.from_numpy(st).to(dev)
+    prios = torch.empty((C, C), dtype=torch.float32, device=dev)
+    run = torch.empty((C, C), dtype=torch.int64, device=dev)
+    pres = torch.empty(C, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    L = _lib.lib()
+    _lib.check(L.syzgpu_minimize_grouped_dev(d_pcs.data_ptr(), d_off.data_ptr(), d_grp.data_ptr(), d_len.data_ptr(),
+                                             c.n, c.ngroups, C, sel.data_ptr(), hist.data_ptr(), stream))
+    _lib.check(L.syzgpu_prio_choice_dev(d_st.data_ptr(), hist.data_ptr(), C, None, prios.data_ptr(),
+                                        run.data_ptr(), pres.data_ptr(), stream))
+    torch.cuda.synchronize()
+    want_idx, _ = oracle.minimize_grouped(c.pcs, c.off, c.group, c.ngroups)
+    want_sel = np.zeros(c.n, np.uint8)
+    want_sel[want_idx] = 1
+    assert np.array_equal(sel.cpu().numpy(), want_sel)
+    # minimizeCorpus then CalculatePriorities(corpus) over the kept programs (manager.go:530-539)
+    want_prios = oracle.calculate_priorities(st, c.prog_len[want_sel == 1])
+    assert np.array_equal(want_prios.view(np.uint32), prios.cpu().numpy().view(np.uint32))
+    wrun, _ = oracle.build_choice_table(want_prios, None)
+    assert np.array_equal(wrun, run.cpu().numpy())
+    out = np.empty(c.n, np.int64)
+    goff = np.empty(c.ngroups + 1, np.uint64)
+    _lib.check(L.syzgpu_minimize_grouped_fetch(out.ctypes.data, goff.ctypes.data, c.n, c.ngroups))
+    assert np.array_equal(out[: int(goff[-1])], want_idx)
