@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsyzgpu.so")
+LIB_PATH = os.environ.get("SYZGPU_LIB") or os.path.join(_HERE, "libsyzgpu.so")
 
 OK, EINVAL, ENODEV, ENOMEM, EHIP, EINTERNAL, ECAPACITY = range(7)
 DIFFERENCE, SYMMETRIC_DIFFERENCE, UNION, INTERSECTION = range(4)

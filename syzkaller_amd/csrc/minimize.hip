@@ -108,10 +108,10 @@ __global__ void k_grp_starts(const uint64_t* cnt_scan, uint32_t G, uint32_t nchu
 }
 
 // ---- 2. ranks ------------------------------------------------------------------------------------
-__global__ void k_ranks(const uint64_t* el, size_t n, const uint32_t* members, uint32_t* rank_of_member,
-                        uint32_t* ent_of_rank) {
+__global__ void k_ranks(const uint64_t* el, const uint32_t* perm, size_t n, const uint32_t* members,
+                        uint32_t* rank_of_member, uint32_t* ent_of_rank) {
   for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t gidx = (uint32_t)el[r];
+    const uint32_t gidx = (uint32_t)el[perm[r]];
     rank_of_member[gidx] = (uint32_t)r;
     ent_of_rank[r] = members[gidx];
   }
@@ -331,6 +331,7 @@ void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   uint64_t* gstart = sc.get<uint64_t>("mz_gstart", G + 1);
   uint32_t* members = sc.get<uint32_t>("mz_members", n + 1);
   uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
+  uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
   uint32_t* rank_of_member = sc.get<uint32_t>("mz_rom", n + 1);
   uint32_t* ent_of_rank = sc.get<uint32_t>("mz_eor", n + 1);
   uint8_t* sel_rank = sc.get<uint8_t>("mz_sel", n + 1);
@@ -367,11 +368,11 @@ void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   if (*herr) fail(SYZGPU_EINVAL, "group id >= ngroups");
   std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
 
-  if (n) gosort_groups(el, n, gstart, G, s);
+  if (n) gosort_groups(el, perm, n, gstart, G, s);
   {
     ProfScope ps("ranks", s, (uint64_t)n * 16);
     if (n) {
-      k_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(el, n, members, rank_of_member, ent_of_rank);
+      k_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(el, perm, n, members, rank_of_member, ent_of_rank);
       SYZ_LAUNCHED();
     }
   }

@@ -10,10 +10,9 @@ struct Seg {
   uint32_t pad;
 };
 
-constexpr uint32_t FIN_MAX = 1024;  // segments up to this size are finished by one wave in LDS
-
-// gosort.hip
-void gosort_groups(uint64_t* el, size_t n, const uint64_t* gstart_dev, uint32_t ngroups, hipStream_t s);
+// gosort.hip: the element at sorted position r of the groups' ranges is el[perm[r]]
+void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const uint64_t* gstart_dev, uint32_t ngroups,
+                   hipStream_t s);
 
 // setops.hip
 uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64_t na, const uint32_t* b,
