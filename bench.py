@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="programs in the CPU baseline sample")
     ap.add_argument("--profile", type=int, default=1, help="per-kernel HIP event timing in the timed region")
+    ap.add_argument("--raw-steps", type=int, default=2, help="also time Minimize from the raw CSR (no store)")
     return ap.parse_args()
 
 
@@ -79,7 +80,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from syzkaller_amd import _lib, synth
+    from syzkaller_amd import _lib, cover, synth
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -115,10 +116,21 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
-    def step():
+    # ingest: the resident corpus store (per-call dense PC ids), built once like mgr.corpus is loaded
+    torch.cuda.synchronize()
+    t_ing = time.perf_counter()
+    store = cover.CoverStore.from_device(d_pcs, d_off, d_grp, d_len, corp.n, G, sptr)
+    torch.cuda.synchronize()
+    ingest_s = time.perf_counter() - t_ing
+    store_info = store.info()
+
+    def step_raw():
         _lib.check(L.syzgpu_minimize_grouped_dev(d_pcs.data_ptr(), d_off.data_ptr(), d_grp.data_ptr(),
                                                  d_len.data_ptr(), corp.n, G, C, d_sel.data_ptr(),
                                                  d_hist.data_ptr(), sptr))
+
+    def step():
+        _lib.check(L.syzgpu_corpus_minimize_dev(store.handle, C, d_sel.data_ptr(), d_hist.data_ptr(), sptr))
         if world > 1:
             dist.all_reduce(d_hist, op=dist.ReduceOp.SUM)  # the one exchange: (C+1) int64
         _lib.check(L.syzgpu_prio_choice_dev(d_static.data_ptr(), d_hist.data_ptr(), C, None, d_prios.data_ptr(),
@@ -154,6 +166,16 @@ def main():
             e["ms"] += float(ms[i])
             e["launches"] += 1
             e["bytes"] += int(by[i])
+    # the same Minimize from the raw CSR every time (no store): reported beside the headline
+    raw_ms = None
+    if args.raw_steps > 0:
+        step_raw()
+        torch.cuda.synchronize()
+        t0r = time.perf_counter()
+        for _ in range(args.raw_steps):
+            step_raw()
+        torch.cuda.synchronize()
+        raw_ms = (time.perf_counter() - t0r) / args.raw_steps * 1e3
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -180,8 +202,8 @@ def main():
             d = kern[dom]
             avg_ms = d["ms"] / d["launches"]
             n_local = corp.n
-            alg = 4 * sum_pcs + 10 * n_local if dom.startswith(("bucket", "group", "ranks", "select", "gosort"))\
-                else d["bytes"] / d["launches"]
+            alg = 4 * sum_pcs + 10 * n_local if dom.startswith(("bucket", "group", "ranks", "select", "gosort",
+                                                                "panel", "el_init")) else d["bytes"] / d["launches"]
             ach = alg / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
@@ -218,6 +240,12 @@ def main():
             "kernels_ms_per_step": {k: round(v["ms"] / args.steps, 4) for k, v in
                                     sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},
             "cpu_baseline": cpu,
+            "ingest": {"seconds": round(ingest_s, 4), "progs_per_s": round(corp.n / ingest_s, 1),
+                       "note": "one-time build of the resident store from device CSR (not in value)",
+                       **store_info},
+            "raw_path": None if raw_ms is None else
+            {"ms_per_step": round(raw_ms, 3), "progs_per_s": round(corp.n / (raw_ms * 1e-3), 1),
+             "note": "Minimize from raw CSR each step (bucket scatter + LDS hash), no store"},
             "gen_s": round(gen_s, 2),
         }
         print(json.dumps(out), flush=True)

@@ -128,6 +128,25 @@ int syzgpu_prio_choice_dev(const float* static_prios, const int64_t* len_hist, i
 int syzgpu_minimize_grouped_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n,
                                   uint32_t ngroups);
 
+/* ---- resident corpus store (device analog of syz-manager's mgr.corpus, manager.go:52-65) ------- */
+/* Ingest a corpus once: per call (group) every distinct PC gets a dense id, covers become sorted id
+ * lists split at 32768-id windows. Covers must be canonical (sorted, duplicate-free — what the
+ * executor produces, executor.cc:572-585). The store keeps its own copies; inputs may be freed. */
+typedef struct syzgpu_corpus syzgpu_corpus;
+int syzgpu_corpus_create(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                         const uint16_t* prog_len /* may be NULL */, size_t n, uint32_t ngroups,
+                         syzgpu_corpus** out);
+int syzgpu_corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                             const uint16_t* prog_len, size_t n, uint32_t ngroups, void* stream,
+                             syzgpu_corpus** out);
+int syzgpu_corpus_destroy(syzgpu_corpus* c);
+/* minimizeCorpus on the store (manager.go:507-527): same results as syzgpu_minimize_grouped(_dev). */
+int syzgpu_corpus_minimize(syzgpu_corpus* c, int64_t* out_idx, uint64_t* group_out_off);
+int syzgpu_corpus_minimize_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,
+                               void* stream);
+/* info[0..5] = entries, calls, PCs, distinct (call, PC) ids, panel work items, shared tables */
+int syzgpu_corpus_info(const syzgpu_corpus* c, uint64_t* info, size_t cap);
+
 /* Per-kernel timing of the last *_dev call (HIP events on the call's stream), for the benchmark's
  * roofline. names/ms arrays of capacity cap; returns the number of kernels recorded. */
 int syzgpu_profile_enable(int on);

@@ -40,6 +40,12 @@ SIGNATURES = {
     "syzgpu_minimize_grouped_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _c.c_int32, _vp, _vp, _vp]),
     "syzgpu_prio_choice_dev": (_c.c_int, [_vp, _vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_minimize_grouped_fetch": (_c.c_int, [_vp, _vp, _sz, _c.c_uint32]),
+    "syzgpu_corpus_create": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp]),
+    "syzgpu_corpus_create_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp, _vp]),
+    "syzgpu_corpus_destroy": (_c.c_int, [_vp]),
+    "syzgpu_corpus_minimize": (_c.c_int, [_vp, _vp, _vp]),
+    "syzgpu_corpus_minimize_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp]),
+    "syzgpu_corpus_info": (_c.c_int, [_vp, _vp, _sz]),
     "syzgpu_profile_enable": (_c.c_int, [_c.c_int]),
     "syzgpu_profile_read": (_sz, [_vp, _vp, _vp, _sz]),
 }

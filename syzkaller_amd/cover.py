@@ -138,3 +138,53 @@ def NoveltyBatch(pcs, off, group, ngroups, maxcover_pcs, maxcover_off, flakes):
     check(lib().syzgpu_novelty_batch(ptr(pcs), ptr(off), ptr(group), n, ngroups, ptr(mc), ptr(mco), ptr(fl),
                                      fl.size, ptr(is_new), ptr(out), cap, ptr(ooff)))
     return is_new[:n].copy(), out[: int(ooff[-1])].copy(), ooff
+
+
+class CoverStore:
+    """Device-resident corpus (the analog of syz-manager's mgr.corpus): ingest once, then Minimize
+    every call group as often as the manager needs (manager.go:507-527 on each Connect / hub sync).
+    Covers must be canonical (as the executor produces them)."""
+
+    def __init__(self, pcs, off, group, ngroups, prog_len=None):
+        pcs, off, group = _u32(pcs), np.ascontiguousarray(off, dtype=np.uint64), _u32(group)
+        pl = None if prog_len is None else np.ascontiguousarray(prog_len, dtype=np.uint16)
+        h = np.zeros(1, dtype=np.uint64)
+        check(lib().syzgpu_corpus_create(ptr(pcs), ptr(off), ptr(group), ptr(pl), off.size - 1, ngroups, ptr(h)))
+        self._h = int(h[0])
+        self.n = off.size - 1
+        self.ngroups = ngroups
+
+    @classmethod
+    def from_device(cls, d_pcs, d_off, d_group, d_prog_len, n, ngroups, stream=0):
+        self = cls.__new__(cls)
+        h = np.zeros(1, dtype=np.uint64)
+        check(lib().syzgpu_corpus_create_dev(ptr(d_pcs), ptr(d_off), ptr(d_group), ptr(d_prog_len), n, ngroups,
+                                             stream, ptr(h)))
+        self._h, self.n, self.ngroups = int(h[0]), n, ngroups
+        return self
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self):
+        v = np.zeros(6, dtype=np.uint64)
+        check(lib().syzgpu_corpus_info(self._h, ptr(v), 6))
+        return dict(zip(["entries", "calls", "pcs", "ids", "work_items", "shared_tables"], (int(x) for x in v)))
+
+    def Minimize(self):
+        out = np.empty(max(self.n, 1), dtype=np.int64)
+        goff = np.zeros(self.ngroups + 1, dtype=np.uint64)
+        check(lib().syzgpu_corpus_minimize(self._h, ptr(out), ptr(goff)))
+        return out[: int(goff[-1])].copy(), goff
+
+    def close(self):
+        if getattr(self, "_h", 0):
+            lib().syzgpu_corpus_destroy(self._h)
+            self._h = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

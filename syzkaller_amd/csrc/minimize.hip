@@ -14,6 +14,7 @@
 //   5. selected ranks in increasing order per group = Go's selection order.
 // Everything is integer work: bit-exact by construction.
 #include <algorithm>
+#include <memory>
 #include <numeric>
 
 #include "pipeline.hpp"
@@ -522,3 +523,582 @@ int syzgpu_minimize(const uint32_t* pcs, const uint64_t* off, size_t ncov, int64
 
 }  // extern "C"
 
+namespace syz {
+
+
+// =====================================================================================================
+// Resident corpus store (the device analog of syz-manager's mgr.corpus, manager.go:52-65).
+//
+// Ingest turns the raw CSR covers into per-call dense PC ids once: every distinct PC of call g gets
+// an id in [0, P_g) (hash buckets of the call, an LDS table per bucket), every cover becomes its
+// sorted id list, and each cover records where its list crosses every 32768-id window. Minimize on
+// the store is then one streaming pass: a workgroup per (call, id-window, cover chunk) keeps the
+// window's min Go-sort rank per id in a direct-mapped LDS table (no hashing, no scatter), and the
+// rank that wins an id marks its input as kept (cover.go:116-129 as first occurrence).
+// =====================================================================================================
+constexpr uint32_t WIN_BITS = 15;
+constexpr uint32_t WIN = 1u << WIN_BITS;  // ids per LDS window (u32 min-rank table = 128 KB)
+constexpr uint64_t PANEL_CHUNK_OCC = 1u << 20;
+
+__global__ __launch_bounds__(BK_BLOCK) void k_bucket_scatter_pos(const Chunk* chunks, const GBucket* gb,
+                                                                 const uint32_t* members, const uint64_t* off,
+                                                                 const uint32_t* pcs, const uint64_t* boff,
+                                                                 uint32_t* bcursor, uint2* items) {
+  __shared__ uint32_t hist[HIST_LDS];
+  const Chunk ch = chunks[blockIdx.x];
+  const GBucket b = gb[ch.g];
+  const uint32_t nb = 1u << b.bits;
+  const bool lds = nb <= HIST_LDS;
+  if (lds) {
+    for (uint32_t i = threadIdx.x; i < nb; i += BK_BLOCK) hist[i] = 0;
+    __syncthreads();
+    for (uint32_t m = ch.mbeg; m < ch.mend; m++) {
+      const uint32_t e = members[m];
+      for (uint64_t k = off[e] + threadIdx.x; k < off[e + 1]; k += BK_BLOCK)
+        atomicAdd(&hist[bucket_local(pcs[k], b.bits)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += BK_BLOCK)
+      if (hist[i]) hist[i] = atomicAdd(&bcursor[b.base + i], hist[i]);
+    __syncthreads();
+  }
+  for (uint32_t m = ch.mbeg; m < ch.mend; m++) {
+    const uint32_t e = members[m];
+    for (uint64_t k = off[e] + threadIdx.x; k < off[e + 1]; k += BK_BLOCK) {
+      const uint32_t pc = pcs[k];
+      const uint32_t lb = bucket_local(pc, b.bits);
+      const uint32_t slot = lds ? atomicAdd(&hist[lb], 1u) : atomicAdd(&bcursor[b.base + lb], 1u);
+      items[boff[b.base + lb] + slot] = make_uint2(pc, (uint32_t)k);
+    }
+  }
+}
+
+// LDS open-addressing set keyed by pc; the sentinel pc 0xFFFFFFFF lives in slot HT_SLOTS (extra).
+__device__ __forceinline__ int ht_insert(uint32_t* keys, uint32_t pc) {
+  if (pc == HT_EMPTY) {
+    keys[HT_SLOTS] = 1;
+    return (int)HT_SLOTS;
+  }
+  uint32_t h = hslot(pc);
+  for (uint32_t probes = 0; probes < HT_SLOTS; probes++) {
+    const uint32_t cur = keys[h];
+    if (cur == pc) return (int)h;
+    if (cur == HT_EMPTY) {
+      const uint32_t old = atomicCAS(&keys[h], HT_EMPTY, pc);
+      if (old == HT_EMPTY || old == pc) return (int)h;
+    }
+    h = (h + 1) & (HT_SLOTS - 1);
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int ht_find(const uint32_t* keys, uint32_t pc) {
+  if (pc == HT_EMPTY) return (int)HT_SLOTS;
+  uint32_t h = hslot(pc);
+  for (uint32_t probes = 0; probes < HT_SLOTS; probes++) {
+    const uint32_t cur = keys[h];
+    if (cur == pc) return (int)h;
+    if (cur == HT_EMPTY) return -1;
+    h = (h + 1) & (HT_SLOTS - 1);
+  }
+  return -1;
+}
+
+// mode 0: count distinct keys per bucket. mode 1: assign ids id_base[b] + rank(slot), write the
+// dictionary and ids[k] for every occurrence.
+__global__ __launch_bounds__(HT_BLOCK) void k_bucket_ids(int mode, const uint64_t* boff, uint32_t nbuckets,
+                                                         const uint2* items, uint32_t* dcount, const uint64_t* dscan,
+                                                         const uint32_t* bucket_group, const GBucket* gb,
+                                                         const uint64_t* gdict, uint32_t* dict, uint32_t* ids,
+                                                         int* err) {
+  __shared__ uint32_t keys[HT_SLOTS + 1];
+  __shared__ uint32_t rank[HT_SLOTS + 1];
+  __shared__ uint32_t red[HT_BLOCK / 64 + 1];
+  __shared__ int full;
+  for (uint32_t bk = blockIdx.x; bk < nbuckets; bk += gridDim.x) {
+    const uint64_t beg = boff[bk], end = boff[bk + 1];
+    for (uint32_t i = threadIdx.x; i <= HT_SLOTS; i += HT_BLOCK) keys[i] = i == HT_SLOTS ? 0 : HT_EMPTY;
+    if (threadIdx.x == 0) full = 0;
+    __syncthreads();
+    for (uint64_t k = beg + threadIdx.x; k < end; k += HT_BLOCK)
+      if (ht_insert(keys, items[k].x) < 0) full = 1;
+    __syncthreads();
+    if (full) {
+      if (threadIdx.x == 0) atomicOr(err, 4);
+      continue;
+    }
+    // rank occupied slots (slot order; the sentinel slot last)
+    uint32_t base = 0;
+    for (uint32_t s0 = 0; s0 <= HT_SLOTS; s0 += HT_BLOCK) {
+      const uint32_t s = s0 + threadIdx.x;
+      uint32_t occ = 0;
+      if (s < HT_SLOTS)
+        occ = keys[s] != HT_EMPTY;
+      else if (s == HT_SLOTS)
+        occ = keys[HT_SLOTS] != 0;
+      uint32_t tot;
+      const uint32_t r = block_excl_scan<HT_BLOCK>(occ, red, &tot);
+      if (s <= HT_SLOTS) rank[s] = occ ? base + r : 0xFFFFFFFFu;
+      base += tot;
+    }
+    if (mode == 0) {
+      if (threadIdx.x == 0) dcount[bk] = base;
+      __syncthreads();
+      continue;
+    }
+    const uint32_t g = bucket_group[bk];
+    const uint32_t idb = (uint32_t)(dscan[bk] - dscan[gb[g].base]);
+    for (uint32_t s = threadIdx.x; s <= HT_SLOTS; s += HT_BLOCK)
+      if (rank[s] != 0xFFFFFFFFu) dict[gdict[g] + idb + rank[s]] = s == HT_SLOTS ? HT_EMPTY : keys[s];
+    __syncthreads();
+    for (uint64_t k = beg + threadIdx.x; k < end; k += HT_BLOCK) {
+      const uint2 it = items[k];
+      ids[it.y] = idb + rank[ht_find(keys, it.x)];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_bucket_group(const GBucket* gb, uint32_t G, uint32_t* bucket_group) {
+  for (uint32_t g = blockIdx.x; g < G; g += gridDim.x)
+    for (uint32_t b = threadIdx.x; b < (1u << gb[g].bits); b += blockDim.x) bucket_group[gb[g].base + b] = g;
+}
+
+// splits[sbase[e] + j] = offset inside cover e of the first id >= j * WIN, j in [0, nwin(g)]
+__global__ void k_splits(const uint32_t* ids, const uint64_t* off, const uint32_t* group, size_t n,
+                         const uint32_t* nwin, const uint64_t* sbase, uint32_t* splits) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t nw = nwin[group[e]];
+    const uint64_t b = off[e], len = off[e + 1] - b;
+    uint32_t* sp = splits + sbase[e];
+    sp[0] = 0;
+    for (uint32_t j = 1; j < nw; j++)
+      sp[j] = (uint32_t)(lower_bound_dev<uint32_t>(ids, b, b + len, j << WIN_BITS) - b);
+    sp[nw] = (uint32_t)len;
+  }
+}
+
+__global__ void k_split_count(const uint32_t* group, size_t n, const uint32_t* nwin, uint64_t* cnt) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    cnt[e] = nwin[group[e]] + 1;
+}
+
+__global__ void k_el_init(const uint32_t* members, const uint64_t* off, size_t n, uint64_t* el) {
+  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t e = members[m];
+    el[m] = ((off[e + 1] - off[e]) << 32) | m;
+  }
+}
+
+struct PanelWork {
+  uint32_t g, win, mbeg, mend;  // call, id window, member range of the cover chunk
+  uint32_t nids;                // ids in this window (<= WIN)
+  uint32_t gtab;                // 0xFFFFFFFF: sole chunk, emit directly; else index of a global table
+  uint32_t pad0, pad1;
+};
+
+constexpr int PM_BLOCK = 1024;
+
+// min Go-sort rank per id of one window over one chunk of covers, LDS direct-mapped
+__global__ __launch_bounds__(PM_BLOCK) void k_panel_min(const PanelWork* work, const uint32_t* members,
+                                                        const uint64_t* off, const uint64_t* sbase,
+                                                        const uint32_t* splits, const uint32_t* ids,
+                                                        const uint32_t* rank_of_member, uint8_t* sel_rank,
+                                                        uint32_t* gtabs) {
+  __shared__ uint32_t tab[WIN];
+  const PanelWork w = work[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < w.nids; i += PM_BLOCK) tab[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  const uint32_t wbase = w.win << WIN_BITS;
+  const int wave = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  for (uint32_t m = w.mbeg + wave; m < w.mend; m += PM_BLOCK / 64) {
+    const uint32_t e = members[m];
+    const uint32_t R = rank_of_member[m];
+    const uint64_t sb = sbase[e];
+    const uint64_t b = off[e];
+    const uint32_t s0 = splits[sb + w.win], s1 = splits[sb + w.win + 1];
+    for (uint32_t k = s0 + lane; k < s1; k += 64) {
+      const uint32_t id = ids[b + k] - wbase;
+      if (tab[id] > R) atomicMin(&tab[id], R);
+    }
+  }
+  __syncthreads();
+  if (w.gtab == 0xFFFFFFFFu) {
+    for (uint32_t i = threadIdx.x; i < w.nids; i += PM_BLOCK) {
+      const uint32_t r = tab[i];
+      if (r != 0xFFFFFFFFu) sel_rank[r] = 1;
+    }
+  } else {
+    uint32_t* gt = gtabs + (size_t)w.gtab * WIN;
+    for (uint32_t i = threadIdx.x; i < w.nids; i += PM_BLOCK) {
+      const uint32_t r = tab[i];
+      if (r != 0xFFFFFFFFu) atomicMin(&gt[i], r);
+    }
+  }
+}
+
+__global__ void k_gtab_emit(const uint32_t* gtabs, size_t total, uint8_t* sel_rank) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t r = gtabs[i];
+    if (r != 0xFFFFFFFFu) sel_rank[r] = 1;
+  }
+}
+
+// ---- the store object ----------------------------------------------------------------------------------
+template <class T>
+struct DevArr {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    free();
+    n = count;
+    SYZ_HIP(hipMalloc(&p, (count ? count : 1) * sizeof(T)));
+  }
+  void free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct Corpus {
+  size_t n = 0;
+  uint32_t G = 0;
+  uint64_t total_pcs = 0, total_ids = 0;
+  DevArr<uint64_t> off, gstart, sbase, gdict;
+  DevArr<uint32_t> group, members, ids, splits, nwin, dict, gtabs;
+  DevArr<uint16_t> prog_len;
+  DevArr<PanelWork> work;
+  std::vector<PanelWork> hwork;
+  uint32_t ngtabs = 0;
+  bool have_sel = false;
+  ~Corpus() {
+    off.free(); gstart.free(); sbase.free(); gdict.free(); group.free(); members.free(); ids.free();
+    splits.free(); nwin.free(); dict.free(); gtabs.free(); prog_len.free(); work.free();
+  }
+};
+
+Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
+                          size_t n, uint32_t G, hipStream_t s) {
+  Context& c = ctx();
+  if (G == 0 || G > MAX_GROUPS) fail(SYZGPU_EINVAL, "ngroups out of range (1..4096)");
+  if (n >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
+  std::unique_ptr<Corpus> cp(new Corpus());
+  Corpus& K = *cp;
+  K.n = n;
+  K.G = G;
+  Scratch& sc = c.scratch;
+  // host copy of the offsets (for sizes and the per-cover sort launch)
+  std::vector<uint64_t> hoff(n + 1);
+  SYZ_HIP(hipMemcpyAsync(hoff.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (hoff[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
+  K.total_pcs = hoff[n];
+  if (K.total_pcs >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "more than 2^32 PCs in one store");
+  K.off.alloc(n + 1);
+  K.group.alloc(n);
+  K.prog_len.alloc(n);
+  K.members.alloc(n);
+  K.gstart.alloc(G + 1);
+  K.ids.alloc(K.total_pcs);
+  SYZ_HIP(hipMemcpyAsync(K.off.p, off, (n + 1) * 8, hipMemcpyDeviceToDevice, s));
+  if (n) SYZ_HIP(hipMemcpyAsync(K.group.p, group, n * 4, hipMemcpyDeviceToDevice, s));
+  if (n && prog_len) SYZ_HIP(hipMemcpyAsync(K.prog_len.p, prog_len, n * 2, hipMemcpyDeviceToDevice, s));
+  if (n && !prog_len) SYZ_HIP(hipMemsetAsync(K.prog_len.p, 0, n * 2, s));
+  // 1. group partition
+  const uint32_t nchunks = (uint32_t)((n + PW_ITEMS - 1) / PW_ITEMS);
+  int* err = sc.get<int>("cs_err", 2);
+  uint32_t* cnt = sc.get<uint32_t>("mz_cnt", (size_t)G * nchunks + 1);
+  uint64_t* cnt_scan = sc.get<uint64_t>("mz_cnt_scan", (size_t)G * nchunks + 1);
+  uint64_t* gpcs = sc.get<uint64_t>("mz_gpcs", G + 1);
+  uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
+  SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
+  SYZ_HIP(hipMemsetAsync(cnt, 0, ((size_t)G * nchunks + 1) * 4, s));
+  SYZ_HIP(hipMemsetAsync(gpcs, 0, (G + 1) * 8, s));
+  if (n) {
+    const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
+    k_grp_count<<<wg, 256, 4 * G * 4, s>>>(group, n, G, nchunks, cnt, err);
+    SYZ_LAUNCHED();
+    k_grp_sumlen<<<grid_for(n, 256, 2048), 256, G * 8, s>>>(group, off, n, G, gpcs);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(cnt, cnt_scan, (size_t)G * nchunks, s);
+  k_grp_starts<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(cnt_scan, G, nchunks, n, K.gstart.p);
+  SYZ_LAUNCHED();
+  if (n) {
+    const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
+    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, cnt_scan, K.members.p, el);
+    SYZ_LAUNCHED();
+  }
+  std::vector<uint64_t> hstart(G + 1), hpcs(G);
+  int herr[2];
+  SYZ_HIP(hipMemcpyAsync(hstart.data(), K.gstart.p, (G + 1) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hpcs.data(), gpcs, G * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (herr[0]) fail(SYZGPU_EINVAL, "group id >= ngroups");
+  // 2. hash buckets per call (<= HT_ROUND_ITEMS occurrences expected per bucket)
+  std::vector<GBucket> hgb(G);
+  std::vector<Chunk> hch;
+  uint32_t nbuckets = 0;
+  for (uint32_t g = 0; g < G; g++) {
+    const uint64_t np = hpcs[g];
+    uint32_t bits = 0;
+    while (bits < 24 && ((uint64_t)HT_ROUND_ITEMS << bits) < np) bits++;
+    hgb[g] = GBucket{nbuckets, bits};
+    nbuckets += 1u << bits;
+    const uint64_t ng = hstart[g + 1] - hstart[g];
+    if (ng == 0) continue;
+    const uint64_t avg = std::max<uint64_t>(1, np / ng);
+    const uint64_t target = std::max<uint64_t>(32768, 4ull << bits);
+    const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ng, target / avg));
+    for (uint64_t m = hstart[g]; m < hstart[g + 1]; m += per)
+      hch.push_back(Chunk{g, (uint32_t)m, (uint32_t)std::min<uint64_t>(hstart[g + 1], m + per), 0});
+  }
+  GBucket* dgb = sc.get<GBucket>("mz_gb", G);
+  Chunk* dch = sc.get<Chunk>("mz_chunks", hch.size() + 1);
+  uint32_t* bcount = sc.get<uint32_t>("mz_bcount", nbuckets + 1);
+  uint64_t* boff = sc.get<uint64_t>("mz_boff", nbuckets + 1);
+  uint32_t* bcursor = sc.get<uint32_t>("mz_bcursor", nbuckets + 1);
+  uint32_t* bgroup = sc.get<uint32_t>("cs_bgroup", nbuckets + 1);
+  uint32_t* dcount = sc.get<uint32_t>("cs_dcount", nbuckets + 1);
+  uint64_t* dscan = sc.get<uint64_t>("cs_dscan", nbuckets + 1);
+  uint2* items = sc.get<uint2>("mz_items", K.total_pcs + 1);
+  SYZ_HIP(hipMemcpyAsync(dgb, hgb.data(), G * sizeof(GBucket), hipMemcpyHostToDevice, s));
+  if (!hch.empty()) SYZ_HIP(hipMemcpyAsync(dch, hch.data(), hch.size() * sizeof(Chunk), hipMemcpyHostToDevice, s));
+  SYZ_HIP(hipMemsetAsync(bcount, 0, (nbuckets + 1) * 4, s));
+  SYZ_HIP(hipMemsetAsync(bcursor, 0, (nbuckets + 1) * 4, s));
+  k_bucket_group<<<std::min<uint32_t>(G, 1024), 256, 0, s>>>(dgb, G, bgroup);
+  SYZ_LAUNCHED();
+  if (!hch.empty()) {
+    k_bucket_count<<<(unsigned)hch.size(), BK_BLOCK, 0, s>>>(dch, dgb, K.members.p, off, pcs, bcount);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(bcount, boff, nbuckets, s);
+  if (!hch.empty()) {
+    k_bucket_scatter_pos<<<(unsigned)hch.size(), BK_BLOCK, 0, s>>>(dch, dgb, K.members.p, off, pcs, boff, bcursor,
+                                                                   items);
+    SYZ_LAUNCHED();
+  }
+  // 3. dense ids: count distinct per bucket, scan, assign
+  const unsigned hb = std::min<uint32_t>(std::max<uint32_t>(nbuckets, 1), 65536);
+  k_bucket_ids<<<hb, HT_BLOCK, 0, s>>>(0, boff, nbuckets, items, dcount, nullptr, bgroup, dgb, nullptr, nullptr,
+                                       nullptr, err);
+  SYZ_LAUNCHED();
+  exclusive_scan_u32(dcount, dscan, nbuckets, s);
+  std::vector<uint64_t> hds(nbuckets + 1);
+  SYZ_HIP(hipMemcpyAsync(hds.data(), dscan, (nbuckets + 1) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (herr[0] & 4) fail(SYZGPU_EINTERNAL, "coverstore: hash bucket overflow");
+  std::vector<uint64_t> hgdict(G + 1);
+  std::vector<uint32_t> hnwin(G);
+  for (uint32_t g = 0; g < G; g++) {
+    const uint64_t p_g = hds[hgb[g].base + (1u << hgb[g].bits)] - hds[hgb[g].base];
+    hgdict[g] = hds[hgb[g].base];
+    hnwin[g] = (uint32_t)std::max<uint64_t>(1, (p_g + WIN - 1) / WIN);
+  }
+  hgdict[G] = hds[nbuckets];
+  K.total_ids = hds[nbuckets];
+  K.dict.alloc(K.total_ids);
+  K.gdict.alloc(G + 1);
+  K.nwin.alloc(G);
+  SYZ_HIP(hipMemcpyAsync(K.gdict.p, hgdict.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
+  SYZ_HIP(hipMemcpyAsync(K.nwin.p, hnwin.data(), G * 4, hipMemcpyHostToDevice, s));
+  k_bucket_ids<<<hb, HT_BLOCK, 0, s>>>(1, boff, nbuckets, items, dcount, dscan, bgroup, dgb, K.gdict.p, K.dict.p,
+                                       K.ids.p, err);
+  SYZ_LAUNCHED();
+  // 4. every cover as a sorted id list (ids are unique within a cover iff its PCs are)
+  uint64_t* clen = sc.get<uint64_t>("cs_clen", n + 1);
+  canonicalize_batch_dev(K.ids.p, K.off.p, hoff.data(), n, clen, s);
+  std::vector<uint64_t> hclen(n);
+  if (n) SYZ_HIP(hipMemcpyAsync(hclen.data(), clen, n * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  for (size_t e = 0; e < n; e++)
+    if (hclen[e] != hoff[e + 1] - hoff[e])
+      fail(SYZGPU_EINVAL, "coverstore needs canonical covers (sorted, duplicate-free); Canonicalize first");
+  // 5. window splits
+  uint64_t* scount = sc.get<uint64_t>("cs_scount", n + 1);
+  K.sbase.alloc(n + 1);
+  if (n) {
+    k_split_count<<<grid_for(n, 256, 4096), 256, 0, s>>>(K.group.p, n, K.nwin.p, scount);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u64(scount, K.sbase.p, n, s);
+  uint64_t hsplits = 0;
+  SYZ_HIP(hipMemcpyAsync(&hsplits, K.sbase.p + n, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  K.splits.alloc(hsplits);
+  if (n) {
+    k_splits<<<grid_for(n, 256, 8192), 256, 0, s>>>(K.ids.p, K.off.p, K.group.p, n, K.nwin.p, K.sbase.p,
+                                                     K.splits.p);
+    SYZ_LAUNCHED();
+  }
+  // 6. panel work list: (call, window, cover chunk), ~PANEL_CHUNK_OCC occurrences per chunk
+  K.ngtabs = 0;
+  for (uint32_t g = 0; g < G; g++) {
+    const uint64_t ng = hstart[g + 1] - hstart[g];
+    if (ng == 0) continue;
+    const uint64_t p_g = hgdict[g + 1] - hgdict[g];
+    const uint64_t occ_per_win = std::max<uint64_t>(1, hpcs[g] / hnwin[g]);
+    const uint64_t nch = std::max<uint64_t>(1, (occ_per_win + PANEL_CHUNK_OCC - 1) / PANEL_CHUNK_OCC);
+    const uint64_t per = (ng + nch - 1) / nch;
+    for (uint32_t w = 0; w < hnwin[g]; w++) {
+      const uint32_t nids = (uint32_t)std::min<uint64_t>(WIN, p_g - (uint64_t)w * WIN);
+      const uint32_t gt = nch > 1 ? K.ngtabs++ : 0xFFFFFFFFu;
+      for (uint64_t m = hstart[g]; m < hstart[g + 1]; m += per)
+        K.hwork.push_back(PanelWork{g, w, (uint32_t)m, (uint32_t)std::min<uint64_t>(hstart[g + 1], m + per), nids,
+                                    gt, 0, 0});
+    }
+  }
+  K.work.alloc(K.hwork.size());
+  if (!K.hwork.empty())
+    SYZ_HIP(hipMemcpyAsync(K.work.p, K.hwork.data(), K.hwork.size() * sizeof(PanelWork), hipMemcpyHostToDevice, s));
+  K.gtabs.alloc((size_t)K.ngtabs * WIN);
+  SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (herr[0] & 4) fail(SYZGPU_EINTERNAL, "coverstore: hash bucket overflow");
+  return cp.release();
+}
+
+static Corpus* g_last_corpus = nullptr;
+
+void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s) {
+  Context& c = ctx();
+  Scratch& sc = c.scratch;
+  const size_t n = K.n;
+  const uint32_t G = K.G;
+  int* err = sc.get<int>("mz_err", 2);
+  uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
+  uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
+  uint32_t* rank_of_member = sc.get<uint32_t>("mz_rom", n + 1);
+  uint32_t* ent_of_rank = sc.get<uint32_t>("mz_eor", n + 1);
+  uint8_t* sel_rank = sc.get<uint8_t>("mz_sel", n + 1);
+  SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
+  SYZ_HIP(hipMemsetAsync(sel_rank, 0, n + 1, s));
+  if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
+  if (K.ngtabs) SYZ_HIP(hipMemsetAsync(K.gtabs.p, 0xFF, (size_t)K.ngtabs * WIN * 4, s));
+  {
+    ProfScope ps("el_init", s, (uint64_t)n * 20);
+    if (n) {
+      k_el_init<<<grid_for(n, 256, 8192), 256, 0, s>>>(K.members.p, K.off.p, n, el);
+      SYZ_LAUNCHED();
+    }
+  }
+  if (n) gosort_groups(el, perm, n, K.gstart.p, G, s);
+  {
+    ProfScope ps("ranks", s, (uint64_t)n * 16);
+    if (n) {
+      k_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(el, perm, n, K.members.p, rank_of_member, ent_of_rank);
+      SYZ_LAUNCHED();
+    }
+  }
+  {
+    ProfScope ps("panel_min", s, K.total_pcs * 4 + (uint64_t)n * 10);
+    if (!K.hwork.empty()) {
+      k_panel_min<<<(unsigned)K.hwork.size(), PM_BLOCK, 0, s>>>(K.work.p, K.members.p, K.off.p, K.sbase.p,
+                                                                K.splits.p, K.ids.p, rank_of_member, sel_rank,
+                                                                K.gtabs.p);
+      SYZ_LAUNCHED();
+    }
+    if (K.ngtabs) {
+      k_gtab_emit<<<grid_for((size_t)K.ngtabs * WIN, 256, 8192), 256, 0, s>>>(K.gtabs.p, (size_t)K.ngtabs * WIN,
+                                                                              sel_rank);
+      SYZ_LAUNCHED();
+    }
+  }
+  {
+    ProfScope ps("select_out", s, (uint64_t)n * 8);
+    if (n) {
+      k_select_out<<<grid_for(n, 256, 2048), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
+          sel_rank, ent_of_rank, n, len_hist ? K.prog_len.p : nullptr, C, selected, len_hist, err);
+      SYZ_LAUNCHED();
+    }
+  }
+  if (len_hist) {
+    int* h = c.pinned.get<int>(4);
+    SYZ_HIP(hipMemcpyAsync(h, err, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (h[0] & 2) fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
+  }
+  g_min.gstart = K.gstart.p;
+  g_min.sel_rank = sel_rank;
+  g_min.ent_of_rank = ent_of_rank;
+  c.last_n = n;
+  c.last_groups = G;
+  c.have_last = true;
+  g_last_corpus = &K;
+}
+
+}  // namespace syz
+
+extern "C" {
+
+int syzgpu_corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                             const uint16_t* prog_len, size_t n, uint32_t ngroups, void* stream,
+                             syzgpu_corpus** out) {
+  SYZ_API_BODY({
+    if (!out || !off) fail(SYZGPU_EINVAL, "null pointer");
+    *out = reinterpret_cast<syzgpu_corpus*>(
+        corpus_create_dev(pcs, off, group, prog_len, n, ngroups, (hipStream_t)stream));
+  })
+}
+
+int syzgpu_corpus_create(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
+                         size_t n, uint32_t ngroups, syzgpu_corpus** out) {
+  SYZ_API_BODY({
+    if (!out || !off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
+    hipStream_t s = C_.stream;
+    const uint64_t tot = off[n];
+    uint32_t* dp = C_.scratch.get<uint32_t>("cc_pcs", tot + 1);
+    uint64_t* doff = C_.scratch.get<uint64_t>("cc_off", n + 1);
+    uint32_t* dg = C_.scratch.get<uint32_t>("cc_grp", n + 1);
+    uint16_t* dl = prog_len ? C_.scratch.get<uint16_t>("cc_len", n + 1) : nullptr;
+    if (tot) SYZ_HIP(hipMemcpyAsync(dp, pcs, tot * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (n) SYZ_HIP(hipMemcpyAsync(dg, group, n * 4, hipMemcpyHostToDevice, s));
+    if (dl && n) SYZ_HIP(hipMemcpyAsync(dl, prog_len, n * 2, hipMemcpyHostToDevice, s));
+    *out = reinterpret_cast<syzgpu_corpus*>(corpus_create_dev(dp, doff, dg, dl, n, ngroups, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+  })
+}
+
+int syzgpu_corpus_destroy(syzgpu_corpus* cp) {
+  SYZ_API_BODY({
+    Corpus* K = reinterpret_cast<Corpus*>(cp);
+    if (K == g_last_corpus) {
+      g_last_corpus = nullptr;
+      C_.have_last = false;
+    }
+    delete K;
+  })
+}
+
+int syzgpu_corpus_minimize_dev(syzgpu_corpus* cp, int32_t C, uint8_t* selected, int64_t* len_hist, void* stream) {
+  SYZ_API_BODY({
+    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    if (len_hist && C <= 0) fail(SYZGPU_EINVAL, "len_hist needs C > 0");
+    corpus_minimize_dev(*reinterpret_cast<Corpus*>(cp), C, selected, len_hist, (hipStream_t)stream);
+  })
+}
+
+int syzgpu_corpus_minimize(syzgpu_corpus* cp, int64_t* out_idx, uint64_t* group_out_off) {
+  SYZ_API_BODY({
+    if (!cp || !group_out_off) fail(SYZGPU_EINVAL, "null pointer");
+    Corpus& K = *reinterpret_cast<Corpus*>(cp);
+    corpus_minimize_dev(K, 0, nullptr, nullptr, C_.stream);
+    minimize_fetch(out_idx, group_out_off, K.n, K.G, C_.stream);
+  })
+}
+
+int syzgpu_corpus_info(const syzgpu_corpus* cp, uint64_t* info, size_t cap) {
+  SYZ_API_BODY({
+    if (!cp || !info) fail(SYZGPU_EINVAL, "null pointer");
+    const Corpus& K = *reinterpret_cast<const Corpus*>(cp);
+    const uint64_t v[6] = {K.n, K.G, K.total_pcs, K.total_ids, K.hwork.size(), K.ngtabs};
+    for (size_t i = 0; i < cap && i < 6; i++) info[i] = v[i];
+  })
+}
+
+}  // extern "C"

@@ -160,6 +160,13 @@ def _grouped_parity(c):
     got, ggoff = cover.MinimizeCorpus(c.pcs, c.off, c.group, c.ngroups)
     assert np.array_equal(wgoff, ggoff)
     assert np.array_equal(want, got)
+    # the resident store path (ingest once, minimize twice) gives the same selection
+    st = cover.CoverStore(c.pcs, c.off, c.group, c.ngroups, c.prog_len)
+    for _ in range(2):
+        sgot, sgoff = st.Minimize()
+        assert np.array_equal(wgoff, sgoff)
+        assert np.array_equal(want, sgot)
+    st.close()
     return got
 
 
@@ -198,6 +205,23 @@ def test_minimize_corpus_property_full_size():
         k = kept[int(goff[g]):int(goff[g + 1])]
         assert np.all(np.diff(lens[k]) <= 0)
         assert np.all(c.group[k] == g)
+
+
+def test_store_many_windows_and_chunks():
+    # calls with more than 32768 distinct PCs (several id windows) and windows split over chunks
+    c = synth.corpus(0x5EED0005, 40_000, 2, 400_000, len_median=600.0)
+    st = cover.CoverStore(c.pcs, c.off, c.group, c.ngroups, c.prog_len)
+    info = st.info()
+    assert info["ids"] > 2 * 32768 and info["work_items"] > 2
+    want, wgoff = oracle.minimize_grouped(c.pcs, c.off, c.group, c.ngroups)
+    got, goff = st.Minimize()
+    assert np.array_equal(want, got) and np.array_equal(wgoff, goff)
+
+
+def test_store_rejects_non_canonical_covers():
+    with pytest.raises(_lib.SyzGpuError) as e:
+        cover.CoverStore(np.array([5, 5, 7], np.uint32), np.array([0, 3], np.uint64), np.array([0], np.uint32), 1)
+    assert e.value.code == _lib.EINVAL
 
 
 def test_minimize_rejects_bad_group():
