@@ -203,7 +203,7 @@ def main():
             avg_ms = d["ms"] / d["launches"]
             n_local = corp.n
             alg = 4 * sum_pcs + 10 * n_local if dom.startswith(("bucket", "group", "ranks", "select", "gosort",
-                                                                "panel", "el_init")) else d["bytes"] / d["launches"]
+                                                                "panel", "el_init", "vec_min")) else d["bytes"] / d["launches"]
             ach = alg / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,

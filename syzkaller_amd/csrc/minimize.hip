@@ -14,6 +14,7 @@
 //   5. selected ranks in increasing order per group = Go's selection order.
 // Everything is integer work: bit-exact by construction.
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <numeric>
 
@@ -270,9 +271,12 @@ __global__ __launch_bounds__(HT_BLOCK) void k_bucket_hash(const uint64_t* boff, 
 }
 
 // ---- 5. selection outputs --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_select_out(const uint8_t* sel_rank, const uint32_t* ent_of_rank, size_t n,
-                                                    const uint16_t* prog_len, int32_t C, uint8_t* selected,
-                                                    int64_t* hist, int* err) {
+// BITS: the winners arrive as a rank bitmap (store path) and sel_rank is written from it;
+// otherwise sel_rank (bytes) is the input.
+template <bool BITS>
+__global__ __launch_bounds__(256) void k_select_out(const uint32_t* sel_bits, uint8_t* sel_rank,
+                                                    const uint32_t* ent_of_rank, size_t n, const uint16_t* prog_len,
+                                                    int32_t C, uint8_t* selected, int64_t* hist, int* err) {
   extern __shared__ unsigned long long lh[];
   const bool do_hist = prog_len != nullptr;
   if (do_hist) {
@@ -281,7 +285,13 @@ __global__ __launch_bounds__(256) void k_select_out(const uint8_t* sel_rank, con
   }
   for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
     const uint32_t e = ent_of_rank[r];
-    const uint8_t s = sel_rank[r];
+    uint8_t s;
+    if (BITS) {
+      s = (uint8_t)((sel_bits[r >> 5] >> (r & 31)) & 1u);
+      sel_rank[r] = s;
+    } else {
+      s = sel_rank[r];
+    }
     if (selected) selected[e] = s;
     if (do_hist && s) {
       const uint32_t L = prog_len[e];
@@ -430,8 +440,8 @@ void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   {
     ProfScope ps("select_out", s, (uint64_t)n * 8);
     if (n) {
-      k_select_out<<<grid_for(n, 256, 2048), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
-          sel_rank, ent_of_rank, n, len_hist ? prog_len : nullptr, C, selected, len_hist, err);
+      k_select_out<false><<<grid_for(n, 256, 2048), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
+          nullptr, sel_rank, ent_of_rank, n, len_hist ? prog_len : nullptr, C, selected, len_hist, err);
       SYZ_LAUNCHED();
     }
   }
@@ -538,7 +548,6 @@ namespace syz {
 // =====================================================================================================
 constexpr uint32_t WIN_BITS = 15;
 constexpr uint32_t WIN = 1u << WIN_BITS;  // ids per LDS window (u32 min-rank table = 128 KB)
-constexpr uint64_t PANEL_CHUNK_OCC = 1u << 20;
 
 __global__ __launch_bounds__(BK_BLOCK) void k_bucket_scatter_pos(const Chunk* chunks, const GBucket* gb,
                                                                  const uint32_t* members, const uint64_t* off,
@@ -690,59 +699,165 @@ __global__ void k_el_init(const uint32_t* members, const uint64_t* off, size_t n
   }
 }
 
-struct PanelWork {
-  uint32_t g, win, mbeg, mend;  // call, id window, member range of the cover chunk
-  uint32_t nids;                // ids in this window (<= WIN)
-  uint32_t gtab;                // 0xFFFFFFFF: sole chunk, emit directly; else index of a global table
-  uint32_t pad0, pad1;
+// ---- vector stream ---------------------------------------------------------------------------------
+// Panel p = (call g, id window w). Its stream is the concatenation, in member (corpus) order, of every
+// cover's slice of ids in window w, as window-relative u16, each slice padded to a multiple of VEC
+// with copies of its last id (min is idempotent, so padding never changes a result). Every VEC-id
+// vector belongs to exactly one member: vmem[v] names it, so the kernel needs no segment search.
+constexpr uint32_t VEC = 8;                 // ids per 16-byte vector
+constexpr uint64_t CHUNK_VECS = 1u << 16;   // vectors per work item (1 MiB of ids)
+constexpr uint32_t BM_WORDS = 6144;         // LDS rank bitmap: 196608 ranks per pass
+constexpr uint32_t RANK_NONE = 0xFFFFFFFFu;
+
+struct VecWork {
+  uint32_t g;     // call group
+  uint32_t nids;  // ids in this window (<= WIN)
+  uint64_t vbeg, vend;
+  uint32_t gtab;  // RANK_NONE: sole chunk of its panel, emit directly; else index of a global table
+  uint32_t pad;
 };
 
-constexpr int PM_BLOCK = 1024;
+constexpr int VM_BLOCK = 1024;
 
-// min Go-sort rank per id of one window over one chunk of covers, LDS direct-mapped
-__global__ __launch_bounds__(PM_BLOCK) void k_panel_min(const PanelWork* work, const uint32_t* members,
-                                                        const uint64_t* off, const uint64_t* sbase,
-                                                        const uint32_t* splits, const uint32_t* ids,
-                                                        const uint32_t* rank_of_member, uint8_t* sel_rank,
-                                                        uint32_t* gtabs) {
-  __shared__ uint32_t tab[WIN];
-  const PanelWork w = work[blockIdx.x];
-  for (uint32_t i = threadIdx.x; i < w.nids; i += PM_BLOCK) tab[i] = 0xFFFFFFFFu;
-  __syncthreads();
-  const uint32_t wbase = w.win << WIN_BITS;
-  const int wave = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  for (uint32_t m = w.mbeg + wave; m < w.mend; m += PM_BLOCK / 64) {
-    const uint32_t e = members[m];
-    const uint32_t R = rank_of_member[m];
-    const uint64_t sb = sbase[e];
-    const uint64_t b = off[e];
-    const uint32_t s0 = splits[sb + w.win], s1 = splits[sb + w.win + 1];
-    for (uint32_t k = s0 + lane; k < s1; k += 64) {
-      const uint32_t id = ids[b + k] - wbase;
-      if (tab[id] > R) atomicMin(&tab[id], R);
-    }
-  }
-  __syncthreads();
-  if (w.gtab == 0xFFFFFFFFu) {
-    for (uint32_t i = threadIdx.x; i < w.nids; i += PM_BLOCK) {
+// Winning ranks of a window table (LDS or global) -> set bits of sel_bits (global rank bitmap).
+// Ranks of call g lie in [gstart[g], gstart[g+1]); they are deduplicated through an LDS bitmap so
+// that each kept input costs one bit-OR per table instead of one store per id.
+__device__ __forceinline__ void emit_winners(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
+                                             uint32_t* bm, uint32_t* sel_bits) {
+  for (uint64_t base = 0; base < ng; base += (uint64_t)BM_WORDS * 32) {
+    const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BM_WORDS * 32, ng - base);
+    const uint32_t words = (span + 31) / 32;
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
       const uint32_t r = tab[i];
-      if (r != 0xFFFFFFFFu) sel_rank[r] = 1;
+      if (r == RANK_NONE) continue;
+      const uint64_t lr = (uint64_t)r - gbase - base;
+      if (lr < span) atomicOr(&bm[lr >> 5], 1u << (lr & 31));
     }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
+      const uint32_t wv = bm[i];
+      if (!wv) continue;
+      const uint64_t gb = gbase + base + 32ull * i;
+      const uint32_t sh = (uint32_t)(gb & 31);
+      atomicOr(&sel_bits[gb >> 5], wv << sh);
+      if (sh) {
+        const uint32_t hi = wv >> (32 - sh);
+        if (hi) atomicOr(&sel_bits[(gb >> 5) + 1], hi);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void tab_min(uint32_t* tab, uint32_t id, uint32_t R) {
+  if (tab[id] > R) atomicMin(&tab[id], R);
+}
+
+__device__ __forceinline__ void vec_update(uint32_t* tab, const uint4 q, uint32_t R) {
+  tab_min(tab, q.x & 0xFFFF, R);
+  tab_min(tab, q.x >> 16, R);
+  tab_min(tab, q.y & 0xFFFF, R);
+  tab_min(tab, q.y >> 16, R);
+  tab_min(tab, q.z & 0xFFFF, R);
+  tab_min(tab, q.z >> 16, R);
+  tab_min(tab, q.w & 0xFFFF, R);
+  tab_min(tab, q.w >> 16, R);
+}
+
+// One workgroup per work item: min Go-sort rank per id of one window over a chunk of its stream.
+__global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict__ work, const uint4* __restrict__ ids16,
+                                                      const uint32_t* __restrict__ vmem,
+                                                      const uint32_t* __restrict__ rank_of_member,
+                                                      const uint64_t* __restrict__ gstart, uint32_t* sel_bits,
+                                                      uint32_t* gtabs) {
+  __shared__ uint32_t tab[WIN];
+  __shared__ uint32_t bm[BM_WORDS];
+  const VecWork w = work[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) tab[i] = RANK_NONE;
+  __syncthreads();
+  uint64_t v = w.vbeg + threadIdx.x;
+  // four vectors in flight per lane
+  for (; v + 3 * VM_BLOCK < w.vend; v += 4 * VM_BLOCK) {
+    const uint4 q0 = ids16[v], q1 = ids16[v + VM_BLOCK], q2 = ids16[v + 2 * VM_BLOCK], q3 = ids16[v + 3 * VM_BLOCK];
+    const uint32_t m0 = vmem[v], m1 = vmem[v + VM_BLOCK], m2 = vmem[v + 2 * VM_BLOCK], m3 = vmem[v + 3 * VM_BLOCK];
+    const uint32_t r0 = rank_of_member[m0], r1 = rank_of_member[m1], r2 = rank_of_member[m2],
+                   r3 = rank_of_member[m3];
+    vec_update(tab, q0, r0);
+    vec_update(tab, q1, r1);
+    vec_update(tab, q2, r2);
+    vec_update(tab, q3, r3);
+  }
+  for (; v < w.vend; v += VM_BLOCK) vec_update(tab, ids16[v], rank_of_member[vmem[v]]);
+  __syncthreads();
+  if (w.gtab == RANK_NONE) {
+    const uint64_t gb = gstart[w.g];
+    emit_winners(tab, w.nids, gb, gstart[w.g + 1] - gb, bm, sel_bits);
   } else {
     uint32_t* gt = gtabs + (size_t)w.gtab * WIN;
-    for (uint32_t i = threadIdx.x; i < w.nids; i += PM_BLOCK) {
+    for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) {
       const uint32_t r = tab[i];
-      if (r != 0xFFFFFFFFu) atomicMin(&gt[i], r);
+      if (r != RANK_NONE && gt[i] > r) atomicMin(&gt[i], r);
     }
   }
 }
 
-__global__ void k_gtab_emit(const uint32_t* gtabs, size_t total, uint8_t* sel_rank) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t r = gtabs[i];
-    if (r != 0xFFFFFFFFu) sel_rank[r] = 1;
+struct GtabInfo {
+  uint32_t g, nids;
+};
+
+__global__ __launch_bounds__(VM_BLOCK) void k_gtab_emit(const GtabInfo* info, const uint32_t* gtabs,
+                                                        const uint64_t* gstart, uint32_t* sel_bits) {
+  __shared__ uint32_t bm[BM_WORDS];
+  const GtabInfo t = info[blockIdx.x];
+  const uint64_t gb = gstart[t.g];
+  emit_winners(gtabs + (size_t)blockIdx.x * WIN, t.nids, gb, gstart[t.g + 1] - gb, bm, sel_bits);
+}
+
+// vcount[tbase[g] + w * N_g + mloc] = vectors of member m's slice in window w
+__global__ void k_vcount(const uint32_t* members, const uint32_t* group, const uint64_t* gstart, size_t n,
+                         const uint32_t* nwin, const uint64_t* tbase, const uint64_t* sbase, const uint32_t* splits,
+                         uint32_t* vcount) {
+  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t e = members[m];
+    const uint32_t g = group[e];
+    const uint64_t ng = gstart[g + 1] - gstart[g], mloc = m - gstart[g];
+    const uint32_t* sp = splits + sbase[e];
+    for (uint32_t w = 0; w < nwin[g]; w++)
+      vcount[tbase[g] + (uint64_t)w * ng + mloc] = (sp[w + 1] - sp[w] + VEC - 1) / VEC;
   }
+}
+
+// One wave per member: write its slices (window-relative u16, padded with the last id) and vmem.
+__global__ __launch_bounds__(256) void k_vfill(const uint32_t* members, const uint32_t* group, const uint64_t* gstart,
+                                               size_t n, const uint32_t* nwin, const uint64_t* tbase,
+                                               const uint64_t* sbase, const uint32_t* splits, const uint64_t* off,
+                                               const uint32_t* ids, const uint64_t* voff, uint16_t* ids16,
+                                               uint32_t* vmem) {
+  const size_t m = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (m >= n) return;
+  const unsigned lane = __lane_id();
+  const uint32_t e = members[m];
+  const uint32_t g = group[e];
+  const uint64_t ng = gstart[g + 1] - gstart[g], mloc = m - gstart[g];
+  const uint32_t* sp = splits + sbase[e];
+  const uint32_t* src = ids + off[e];
+  for (uint32_t w = 0; w < nwin[g]; w++) {
+    const uint32_t s0 = sp[w], s1 = sp[w + 1];
+    if (s1 == s0) continue;
+    const uint64_t vo = voff[tbase[g] + (uint64_t)w * ng + mloc];
+    const uint32_t len = s1 - s0, padded = (len + VEC - 1) / VEC * VEC;
+    const uint32_t wb = w << WIN_BITS;
+    for (uint32_t k = lane; k < padded; k += 64)
+      ids16[vo * VEC + k] = (uint16_t)(src[s0 + min(k, len - 1)] - wb);
+    for (uint32_t k = lane; k < padded / VEC; k += 64) vmem[vo + k] = (uint32_t)m;
+  }
+}
+
+__global__ void k_gather_u64(const uint64_t* src, const uint64_t* idx, size_t n, uint64_t* dst) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[idx[i]];
 }
 
 // ---- the store object ----------------------------------------------------------------------------------
@@ -765,17 +880,17 @@ struct DevArr {
 struct Corpus {
   size_t n = 0;
   uint32_t G = 0;
-  uint64_t total_pcs = 0, total_ids = 0;
-  DevArr<uint64_t> off, gstart, sbase, gdict;
-  DevArr<uint32_t> group, members, ids, splits, nwin, dict, gtabs;
-  DevArr<uint16_t> prog_len;
-  DevArr<PanelWork> work;
-  std::vector<PanelWork> hwork;
+  uint64_t total_pcs = 0, total_ids = 0, total_vecs = 0;
+  DevArr<uint64_t> off, gstart, gdict;
+  DevArr<uint32_t> group, members, nwin, dict, gtabs, vmem;
+  DevArr<uint16_t> prog_len, ids16;
+  DevArr<VecWork> work;
+  DevArr<GtabInfo> gtinfo;
+  std::vector<VecWork> hwork;
   uint32_t ngtabs = 0;
-  bool have_sel = false;
   ~Corpus() {
-    off.free(); gstart.free(); sbase.free(); gdict.free(); group.free(); members.free(); ids.free();
-    splits.free(); nwin.free(); dict.free(); gtabs.free(); prog_len.free(); work.free();
+    off.free(); gstart.free(); gdict.free(); group.free(); members.free(); nwin.free(); dict.free();
+    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free(); gtinfo.free();
   }
 };
 
@@ -801,7 +916,7 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   K.prog_len.alloc(n);
   K.members.alloc(n);
   K.gstart.alloc(G + 1);
-  K.ids.alloc(K.total_pcs);
+  uint32_t* ids = sc.get<uint32_t>("cs_ids", K.total_pcs + 1);
   SYZ_HIP(hipMemcpyAsync(K.off.p, off, (n + 1) * 8, hipMemcpyDeviceToDevice, s));
   if (n) SYZ_HIP(hipMemcpyAsync(K.group.p, group, n * 4, hipMemcpyDeviceToDevice, s));
   if (n && prog_len) SYZ_HIP(hipMemcpyAsync(K.prog_len.p, prog_len, n * 2, hipMemcpyDeviceToDevice, s));
@@ -907,55 +1022,100 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   SYZ_HIP(hipMemcpyAsync(K.gdict.p, hgdict.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
   SYZ_HIP(hipMemcpyAsync(K.nwin.p, hnwin.data(), G * 4, hipMemcpyHostToDevice, s));
   k_bucket_ids<<<hb, HT_BLOCK, 0, s>>>(1, boff, nbuckets, items, dcount, dscan, bgroup, dgb, K.gdict.p, K.dict.p,
-                                       K.ids.p, err);
+                                       ids, err);
   SYZ_LAUNCHED();
   // 4. every cover as a sorted id list (ids are unique within a cover iff its PCs are)
   uint64_t* clen = sc.get<uint64_t>("cs_clen", n + 1);
-  canonicalize_batch_dev(K.ids.p, K.off.p, hoff.data(), n, clen, s);
+  canonicalize_batch_dev(ids, K.off.p, hoff.data(), n, clen, s);
   std::vector<uint64_t> hclen(n);
   if (n) SYZ_HIP(hipMemcpyAsync(hclen.data(), clen, n * 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   for (size_t e = 0; e < n; e++)
     if (hclen[e] != hoff[e + 1] - hoff[e])
       fail(SYZGPU_EINVAL, "coverstore needs canonical covers (sorted, duplicate-free); Canonicalize first");
-  // 5. window splits
+  // 5. window splits (ingest intermediates)
   uint64_t* scount = sc.get<uint64_t>("cs_scount", n + 1);
-  K.sbase.alloc(n + 1);
+  uint64_t* sbase = sc.get<uint64_t>("cs_sbase", n + 1);
   if (n) {
     k_split_count<<<grid_for(n, 256, 4096), 256, 0, s>>>(K.group.p, n, K.nwin.p, scount);
     SYZ_LAUNCHED();
   }
-  exclusive_scan_u64(scount, K.sbase.p, n, s);
+  exclusive_scan_u64(scount, sbase, n, s);
   uint64_t hsplits = 0;
-  SYZ_HIP(hipMemcpyAsync(&hsplits, K.sbase.p + n, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(&hsplits, sbase + n, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
-  K.splits.alloc(hsplits);
+  uint32_t* splits = sc.get<uint32_t>("cs_splits", hsplits + 1);
   if (n) {
-    k_splits<<<grid_for(n, 256, 8192), 256, 0, s>>>(K.ids.p, K.off.p, K.group.p, n, K.nwin.p, K.sbase.p,
-                                                     K.splits.p);
+    k_splits<<<grid_for(n, 256, 8192), 256, 0, s>>>(ids, K.off.p, K.group.p, n, K.nwin.p, sbase, splits);
     SYZ_LAUNCHED();
   }
-  // 6. panel work list: (call, window, cover chunk), ~PANEL_CHUNK_OCC occurrences per chunk
+  // 6. vector stream: panel-major (call, window), member order inside a panel
+  std::vector<uint64_t> htbase(G + 1, 0);
+  for (uint32_t g = 0; g < G; g++) htbase[g + 1] = htbase[g] + (uint64_t)hnwin[g] * (hstart[g + 1] - hstart[g]);
+  const uint64_t T = htbase[G];
+  uint64_t* tbase = sc.get<uint64_t>("cs_tbase", G + 1);
+  uint32_t* vcount = sc.get<uint32_t>("cs_vcount", T + 1);
+  uint64_t* voff = sc.get<uint64_t>("cs_voff", T + 1);
+  SYZ_HIP(hipMemcpyAsync(tbase, htbase.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
+  if (n) {
+    k_vcount<<<grid_for(n, 256, 8192), 256, 0, s>>>(K.members.p, K.group.p, K.gstart.p, n, K.nwin.p, tbase, sbase,
+                                                     splits, vcount);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(vcount, voff, T, s);
+  // panel boundaries: voff at tbase[g] + w * N_g for every (g, w), plus the total
+  std::vector<uint64_t> hpidx;
+  for (uint32_t g = 0; g < G; g++)
+    for (uint32_t w = 0; w < hnwin[g]; w++) hpidx.push_back(htbase[g] + (uint64_t)w * (hstart[g + 1] - hstart[g]));
+  hpidx.push_back(T);
+  uint64_t* dpidx = sc.get<uint64_t>("cs_pidx", hpidx.size());
+  uint64_t* dpv = sc.get<uint64_t>("cs_pv", hpidx.size());
+  SYZ_HIP(hipMemcpyAsync(dpidx, hpidx.data(), hpidx.size() * 8, hipMemcpyHostToDevice, s));
+  k_gather_u64<<<grid_for(hpidx.size(), 256, 1024), 256, 0, s>>>(voff, dpidx, hpidx.size(), dpv);
+  SYZ_LAUNCHED();
+  std::vector<uint64_t> hpv(hpidx.size());
+  SYZ_HIP(hipMemcpyAsync(hpv.data(), dpv, hpidx.size() * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  K.total_vecs = hpv.back();
+  K.ids16.alloc(K.total_vecs * VEC);
+  K.vmem.alloc(K.total_vecs);
+  if (n) {
+    k_vfill<<<(unsigned)((n * 64 + 255) / 256), 256, 0, s>>>(K.members.p, K.group.p, K.gstart.p, n, K.nwin.p, tbase,
+                                                            sbase, splits, K.off.p, ids, voff, K.ids16.p, K.vmem.p);
+    SYZ_LAUNCHED();
+  }
+  // 7. work items: chunks of <= CHUNK_VECS vectors of one panel; a split panel merges through a
+  // global table. Largest first, so the tail of the grid is short.
   K.ngtabs = 0;
+  uint64_t chunk_vecs = CHUNK_VECS;
+  if (const char* cv = getenv("SYZGPU_CHUNK_VECS")) chunk_vecs = std::max<uint64_t>(1, strtoull(cv, nullptr, 10));
+  std::vector<GtabInfo> hgt;
+  size_t pi = 0;
   for (uint32_t g = 0; g < G; g++) {
-    const uint64_t ng = hstart[g + 1] - hstart[g];
-    if (ng == 0) continue;
     const uint64_t p_g = hgdict[g + 1] - hgdict[g];
-    const uint64_t occ_per_win = std::max<uint64_t>(1, hpcs[g] / hnwin[g]);
-    const uint64_t nch = std::max<uint64_t>(1, (occ_per_win + PANEL_CHUNK_OCC - 1) / PANEL_CHUNK_OCC);
-    const uint64_t per = (ng + nch - 1) / nch;
-    for (uint32_t w = 0; w < hnwin[g]; w++) {
+    for (uint32_t w = 0; w < hnwin[g]; w++, pi++) {
+      const uint64_t vb = hpv[pi], ve = hpv[pi + 1];
+      if (ve == vb) continue;
       const uint32_t nids = (uint32_t)std::min<uint64_t>(WIN, p_g - (uint64_t)w * WIN);
-      const uint32_t gt = nch > 1 ? K.ngtabs++ : 0xFFFFFFFFu;
-      for (uint64_t m = hstart[g]; m < hstart[g + 1]; m += per)
-        K.hwork.push_back(PanelWork{g, w, (uint32_t)m, (uint32_t)std::min<uint64_t>(hstart[g + 1], m + per), nids,
-                                    gt, 0, 0});
+      const uint64_t nch = (ve - vb + chunk_vecs - 1) / chunk_vecs;
+      uint32_t gt = RANK_NONE;
+      if (nch > 1) {
+        gt = K.ngtabs++;
+        hgt.push_back(GtabInfo{g, nids});
+      }
+      const uint64_t per = (ve - vb + nch - 1) / nch;
+      for (uint64_t v = vb; v < ve; v += per) K.hwork.push_back(VecWork{g, nids, v, std::min(ve, v + per), gt, 0});
     }
   }
+  std::stable_sort(K.hwork.begin(), K.hwork.end(),
+                   [](const VecWork& x, const VecWork& y) { return x.vend - x.vbeg > y.vend - y.vbeg; });
   K.work.alloc(K.hwork.size());
   if (!K.hwork.empty())
-    SYZ_HIP(hipMemcpyAsync(K.work.p, K.hwork.data(), K.hwork.size() * sizeof(PanelWork), hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(K.work.p, K.hwork.data(), K.hwork.size() * sizeof(VecWork), hipMemcpyHostToDevice, s));
   K.gtabs.alloc((size_t)K.ngtabs * WIN);
+  K.gtinfo.alloc(hgt.size());
+  if (!hgt.empty())
+    SYZ_HIP(hipMemcpyAsync(K.gtinfo.p, hgt.data(), hgt.size() * sizeof(GtabInfo), hipMemcpyHostToDevice, s));
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   if (herr[0] & 4) fail(SYZGPU_EINTERNAL, "coverstore: hash bucket overflow");
@@ -976,7 +1136,8 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   uint32_t* ent_of_rank = sc.get<uint32_t>("mz_eor", n + 1);
   uint8_t* sel_rank = sc.get<uint8_t>("mz_sel", n + 1);
   SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
-  SYZ_HIP(hipMemsetAsync(sel_rank, 0, n + 1, s));
+  uint32_t* sel_bits = sc.get<uint32_t>("mz_selbits", n / 32 + 2);
+  SYZ_HIP(hipMemsetAsync(sel_bits, 0, (n / 32 + 2) * 4, s));
   if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
   if (K.ngtabs) SYZ_HIP(hipMemsetAsync(K.gtabs.p, 0xFF, (size_t)K.ngtabs * WIN * 4, s));
   {
@@ -995,24 +1156,24 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
     }
   }
   {
-    ProfScope ps("panel_min", s, K.total_pcs * 4 + (uint64_t)n * 10);
+    ProfScope ps("vec_min", s, K.total_vecs * 20 + (uint64_t)n * 4);
     if (!K.hwork.empty()) {
-      k_panel_min<<<(unsigned)K.hwork.size(), PM_BLOCK, 0, s>>>(K.work.p, K.members.p, K.off.p, K.sbase.p,
-                                                                K.splits.p, K.ids.p, rank_of_member, sel_rank,
-                                                                K.gtabs.p);
+      k_vec_min<<<(unsigned)K.hwork.size(), VM_BLOCK, 0, s>>>(K.work.p, reinterpret_cast<const uint4*>(K.ids16.p),
+                                                              K.vmem.p, rank_of_member, K.gstart.p, sel_bits,
+                                                              K.gtabs.p);
       SYZ_LAUNCHED();
     }
-    if (K.ngtabs) {
-      k_gtab_emit<<<grid_for((size_t)K.ngtabs * WIN, 256, 8192), 256, 0, s>>>(K.gtabs.p, (size_t)K.ngtabs * WIN,
-                                                                              sel_rank);
-      SYZ_LAUNCHED();
-    }
+  }
+  if (K.ngtabs) {
+    ProfScope ps("gtab_emit", s, (uint64_t)K.ngtabs * WIN * 4);
+    k_gtab_emit<<<K.ngtabs, VM_BLOCK, 0, s>>>(K.gtinfo.p, K.gtabs.p, K.gstart.p, sel_bits);
+    SYZ_LAUNCHED();
   }
   {
     ProfScope ps("select_out", s, (uint64_t)n * 8);
     if (n) {
-      k_select_out<<<grid_for(n, 256, 2048), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
-          sel_rank, ent_of_rank, n, len_hist ? K.prog_len.p : nullptr, C, selected, len_hist, err);
+      k_select_out<true><<<grid_for(n, 256, 2048), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
+          sel_bits, sel_rank, ent_of_rank, n, len_hist ? K.prog_len.p : nullptr, C, selected, len_hist, err);
       SYZ_LAUNCHED();
     }
   }

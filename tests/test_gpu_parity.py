@@ -218,6 +218,69 @@ def test_store_many_windows_and_chunks():
     assert np.array_equal(want, got) and np.array_equal(wgoff, goff)
 
 
+def _store_parity(c):
+    st = cover.CoverStore(c.pcs, c.off, c.group, c.ngroups, c.prog_len)
+    want, wgoff = oracle.minimize_grouped(c.pcs, c.off, c.group, c.ngroups)
+    got, goff = st.Minimize()
+    assert np.array_equal(wgoff, goff)
+    assert np.array_equal(want, got)
+    got2, _ = st.Minimize()  # the store is reusable: same answer on every call
+    assert np.array_equal(got2, got)
+    return st
+
+
+@pytest.mark.parametrize("seed,n,G,P", [(0x5EED0001, 10_000, 289, 50_000), (0x5EED0002, 100_000, 289, 500_000),
+                                        (11, 30_000, 7, 200_000)])
+def test_store_matches_oracle(seed, n, G, P):
+    _store_parity(synth.corpus(seed, n, G, P))
+
+
+def test_store_split_panels(monkeypatch):
+    # every window's stream split over many work items -> per-window global tables + gtab_emit
+    monkeypatch.setenv("SYZGPU_CHUNK_VECS", "97")
+    st = _store_parity(synth.corpus(0x5EED0006, 20_000, 13, 120_000))
+    assert st.info()["shared_tables"] > 10
+
+
+def test_store_big_group_several_bitmap_passes():
+    # one call with > 196608 entries: the LDS rank bitmap of the winners' emit takes several passes
+    _store_parity(synth.corpus(0x5EED0007, 260_000, 1, 40_000, len_median=8.0, len_sigma=0.7))
+
+
+def test_store_sentinel_and_empty_covers():
+    c = synth.corpus(0x5EED0008, 5_000, 5, 20_000, len_median=20.0)
+    covers = [c.cover(i).copy() for i in range(c.n)]
+    for i in range(0, c.n, 53):
+        covers[i] = np.zeros(0, np.uint32)            # empty cover: never kept
+    for i in range(7, c.n, 31):
+        if covers[i].size:
+            covers[i][-1] = 0xFFFFFFFF                   # Minimize's map counts the sentinel (cover.go:115-127)
+    pcs, off = cover.to_csr(covers)
+    c2 = synth.Corpus(pcs, off, c.group, c.prog_len, c.ngroups)
+    _store_parity(c2)
+
+
+def test_store_resident_pipeline_matches_oracle():
+    import torch
+    C = 1159
+    c = synth.corpus(0x5EED0009, 50_000, 289, 300_000)
+    dev = torch.device("cuda:0")
+    st = cover.CoverStore(c.pcs, c.off, c.group, c.ngroups, c.prog_len)
+    sel = torch.zeros(c.n, dtype=torch.uint8, device=dev)
+    hist = torch.zeros(C + 1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    L = _lib.lib()
+    for _ in range(2):
+        _lib.check(L.syzgpu_corpus_minimize_dev(st.handle, C, sel.data_ptr(), hist.data_ptr(), stream))
+    torch.cuda.synchronize()
+    want_idx, _ = oracle.minimize_grouped(c.pcs, c.off, c.group, c.ngroups)
+    want_sel = np.zeros(c.n, np.uint8)
+    want_sel[want_idx] = 1
+    assert np.array_equal(sel.cpu().numpy(), want_sel)
+    want_hist = np.bincount(c.prog_len[want_sel == 1], minlength=C + 1)
+    assert np.array_equal(hist.cpu().numpy(), want_hist)
+
+
 def test_store_rejects_non_canonical_covers():
     with pytest.raises(_lib.SyzGpuError) as e:
         cover.CoverStore(np.array([5, 5, 7], np.uint32), np.array([0, 3], np.uint64), np.array([0], np.uint32), 1)
