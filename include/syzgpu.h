@@ -86,7 +86,9 @@ int syzgpu_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint
 /* syz-fuzzer/fuzzer.go:446-470 execute (and syz-manager/manager.go:609-616 NewInput) over a batch:
  * covers are processed in order; cover k of group g is new iff (cov \ maxCover[g]) \ flakes != {},
  * and then maxCover[g] = Union(maxCover[g], that difference). mc/mc_off is the CSR of the ngroups
- * maxCover tables on entry; the updated tables are written to out_mc/out_mc_off (capacity out_cap). */
+ * maxCover tables on entry; the updated tables are written to out_mc/out_mc_off (capacity out_cap,
+ * SYZGPU_ECAPACITY if too small). Covers, tables and flakes must be canonical (strictly increasing,
+ * as the executor and cover.Union produce them), else SYZGPU_EINVAL. */
 int syzgpu_novelty_batch(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
                          uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off,
                          const uint32_t* flakes, size_t nflakes, uint8_t* is_new, uint32_t* out_mc,

@@ -1,0 +1,150 @@
+"""Parity of the batch new-coverage check (syz-fuzzer/fuzzer.go:446-470 execute; manager.go:609-616
+NewInput) on the MI355X against the oracle's literal restatement (oracle.c oracle_novelty).
+
+Bit-exact: is_new flags and every updated maxCover table. BASELINE.json configs[2] ("1M fresh
+execution covers diffed against maxCover") is covered at a reduced size with the same shapes, plus
+the edge cases foreach gives the path: the 0xFFFFFFFF sentinel (dropped by Difference and by Union),
+flakes, empty covers, empty tables.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle  # noqa: E402
+
+from syzkaller_amd import _lib, cover, synth  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(pcs, off, grp, G, mcp, mco, flakes):
+    w_new, w_mc, w_off = oracle.novelty(pcs, off, grp, G, mcp, mco, flakes)
+    g_new, g_mc, g_off = cover.NoveltyBatch(pcs, off, grp, G, mcp, mco, flakes)
+    assert np.array_equal(w_off, g_off)
+    assert np.array_equal(w_mc, g_mc)
+    assert np.array_equal(w_new, g_new)
+    return g_new
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_novelty_random_small(seed):
+    rnd = np.random.default_rng(seed)
+    G = 4
+    for _ in range(20):
+        n = int(rnd.integers(0, 60))
+        covs = [np.unique(rnd.integers(0, 80, size=int(rnd.integers(0, 12)))).astype(np.uint32) for _ in range(n)]
+        grp = rnd.integers(0, G, size=n).astype(np.uint32)
+        mc = [np.unique(rnd.integers(0, 80, size=int(rnd.integers(0, 20)))).astype(np.uint32) for _ in range(G)]
+        flakes = np.unique(rnd.integers(0, 80, size=int(rnd.integers(0, 8)))).astype(np.uint32)
+        pcs, off = oracle.to_csr(covs)
+        mcp, mco = oracle.to_csr(mc)
+        _check(pcs, off, grp, G, mcp, mco, flakes)
+
+
+def test_novelty_sentinel_flakes_empty():
+    S = 0xFFFFFFFF
+    covs = [[1, 2, S], [S], [], [3, 4], [4, 5], [7], [1, S], [9, S]]
+    grp = [0, 1, 1, 2, 2, 3, 0, 3]
+    mc = [[1, 2], [S], [3, S], [S], []]  # group 1 never updated (keeps S); group 2/3 updated (lose S)
+    flakes = [5, 9]
+    covs = [np.array(c, np.uint32) for c in covs]
+    pcs, off = oracle.to_csr(covs)
+    mcp, mco = oracle.to_csr([np.array(m, np.uint32) for m in mc])
+    new = _check(pcs, off, np.array(grp, np.uint32), 5, mcp, mco, np.array(flakes, np.uint32))
+    assert list(new) == [0, 0, 0, 1, 0, 1, 0, 0]
+
+
+def _maxcover_of(c):
+    lens = np.diff(c.off).astype(np.int64)
+    ent = np.repeat(np.arange(c.n), lens)
+    keys = np.unique((c.group[ent].astype(np.uint64) << np.uint64(32)) | c.pcs.astype(np.uint64))
+    g = (keys >> np.uint64(32)).astype(np.int64)
+    mco = np.zeros(c.ngroups + 1, np.uint64)
+    np.cumsum(np.bincount(g, minlength=c.ngroups), out=mco[1:])
+    return (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32), mco
+
+
+def _config3(n_seed, n_fresh, P):
+    G = 289
+    seedc = synth.corpus(0x5EED0003, n_seed, G, P)
+    mcp, mco = _maxcover_of(seedc)
+    fresh = synth.corpus(0x5EED0103, n_fresh, G, P)
+    rnd = np.random.default_rng(3)
+    flakes = np.unique(rnd.choice(fresh.pcs, size=5000)).astype(np.uint32)
+    return fresh, mcp, mco, flakes
+
+
+def test_novelty_config3_shape_vs_oracle():
+    # configs[2] at a size the literal oracle (O(|maxCover|) merges per cover, like Go) finishes in
+    # seconds: maxCover0 from a seeded corpus, a fresh batch, 5k flakes
+    fresh, mcp, mco, flakes = _config3(1_000, 8_000, 100_000)
+    new = _check(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes)
+    assert 0 < new.sum() < fresh.n
+
+
+def test_novelty_config3_property_large():
+    # size-independent characterisation at a larger size (the oracle would take minutes):
+    #   cover k is new  <=>  some pc of cov_k \ flakes \ {0xFFFFFFFF} \ maxCover0[g] occurs first in cov_k
+    #   table_out[g]    == maxCover0[g] u (covers of g \ flakes \ {0xFFFFFFFF})   (no sentinel in this data)
+    fresh, mcp, mco, flakes = _config3(10_000, 200_000, 500_000)
+    G = 289
+    new, out, ooff = cover.NoveltyBatch(fresh.pcs, fresh.off, fresh.group, G, mcp, mco, flakes)
+    lens = np.diff(fresh.off).astype(np.int64)
+    ent = np.repeat(np.arange(fresh.n), lens)
+    key = (fresh.group[ent].astype(np.uint64) << np.uint64(32)) | fresh.pcs.astype(np.uint64)
+    mg = np.repeat(np.arange(G), np.diff(mco).astype(np.int64)).astype(np.uint64)
+    mkey = (mg << np.uint64(32)) | mcp.astype(np.uint64)
+    keep = ~np.isin(fresh.pcs, flakes) & ~np.isin(key, mkey)
+    uk, first = np.unique(key[keep], return_index=True)
+    want_new = np.zeros(fresh.n, np.uint8)
+    want_new[ent[keep][first]] = 1
+    assert np.array_equal(new, want_new)
+    want_keys = np.union1d(mkey, uk)
+    og = np.repeat(np.arange(G), np.diff(ooff).astype(np.int64)).astype(np.uint64)
+    assert np.array_equal((og << np.uint64(32)) | out.astype(np.uint64), want_keys)
+
+
+def test_novelty_empty_batch_and_tables():
+    _check(np.zeros(0, np.uint32), np.zeros(1, np.uint64), np.zeros(0, np.uint32), 3,
+           np.zeros(0, np.uint32), np.zeros(4, np.uint64), np.zeros(0, np.uint32))
+
+
+@pytest.mark.parametrize("what", ["cover", "table", "flakes", "group"])
+def test_novelty_rejects_bad_input(what):
+    pcs = np.array([1, 2, 3], np.uint32)
+    off = np.array([0, 3], np.uint64)
+    grp = np.array([0], np.uint32)
+    mcp = np.array([4, 5], np.uint32)
+    mco = np.array([0, 2, 2], np.uint64)
+    fl = np.array([7, 8], np.uint32)
+    if what == "cover":
+        pcs = np.array([2, 1, 3], np.uint32)
+    elif what == "table":
+        mcp = np.array([5, 5], np.uint32)
+    elif what == "flakes":
+        fl = np.array([8, 7], np.uint32)
+    else:
+        grp = np.array([2], np.uint32)
+    with pytest.raises(_lib.SyzGpuError) as e:
+        cover.NoveltyBatch(pcs, off, grp, 2, mcp, mco, fl)
+    assert e.value.code == _lib.EINVAL
+
+
+def test_novelty_capacity_error():
+    import ctypes
+    pcs = np.array([1, 2, 3], np.uint32)
+    off = np.array([0, 3], np.uint64)
+    grp = np.array([0], np.uint32)
+    mco = np.zeros(2, np.uint64)
+    is_new = np.zeros(1, np.uint8)
+    out = np.zeros(2, np.uint32)
+    ooff = np.zeros(2, np.uint64)
+    p = lambda a: a.ctypes.data
+    rc = _lib.lib().syzgpu_novelty_batch(p(pcs), p(off), p(grp), 1, 1, p(out), p(mco), None, 0, p(is_new), p(out),
+                                         2, p(ooff))
+    assert rc == _lib.ECAPACITY
+    del ctypes
