@@ -48,15 +48,45 @@ def parse():
     return ap.parse_args()
 
 
-def lpt_assign(weights, nranks):
-    """Longest-processing-time assignment of call groups to ranks (deterministic on every rank)."""
-    owner = np.zeros(weights.size, dtype=np.int64)
-    load = np.zeros(nranks, dtype=np.float64)
-    for g in np.argsort(-weights, kind="stable"):
-        r = int(np.argmin(load))
-        owner[g] = r
-        load[r] += weights[g]
-    return owner, load
+def kernel_model(name, corp, store_info, C):
+    """(bound, algorithmic bytes per launch) of a kernel, SURVEY.md §8(d) / DESIGN.md §3."""
+    n, sum_pcs = corp.n, int(corp.off[-1])
+    if name == "vec_min":  # Minimize over the whole local corpus: 4 B per PC + offsets + group id
+        return "hbm", 4 * sum_pcs + 10 * n
+    if name == "select_out":
+        return "hbm", 10 * n
+    if name == "prio_choice":
+        return "hbm", 16 * C * C
+    return "latency", None  # gosort_* (L2-resident dependent partitions), ranks, small helpers
+
+
+def roofline(kern, corp, store_info, C):
+    """Roofline of the dominant HBM-bound kernel (time from HIP events on the launch stream); the
+    latency-bound kernels are listed with their time so the step breakdown stays complete."""
+    rows = []
+    for name, d in kern.items():
+        bound, alg = kernel_model(name, corp, store_info, C)
+        rows.append((d["ms"], name, bound, alg, d))
+    rows.sort(reverse=True)
+    hbm = [r for r in rows if r[2] == "hbm"]
+    if not hbm:
+        return None
+    _, name, bound, alg, d = hbm[0]
+    avg_ms = d["ms"] / d["launches"]
+    ach = alg / (avg_ms * 1e-3) / 1e9
+    out = {"bound": bound, "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_ms": round(avg_ms, 4),
+           "algorithmic_bytes_per_launch": int(alg), "design_bytes_per_launch": int(d["bytes"] / d["launches"]),
+           "dominant_kernel_overall": rows[0][1]}
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            pm = json.load(open(tf))
+            if name in pm.get("kernels", {}) and pm.get("workload") == "config4-1M":
+                out["traffic"] = pm["kernels"][name]["hbm_bytes_per_launch"]
+        except Exception:
+            pass
+    return out
 
 
 def static_matrix(C, seed=7):
@@ -80,7 +110,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from syzkaller_amd import _lib, cover, synth
+    from syzkaller_amd import _lib, cover, sharding, synth
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -94,10 +124,8 @@ def main():
     C, G = args.calls, args.ngroups
     p = synth.params(args.seed, args.progs_per_gpu * world, G, args.npcs)
     group, off, plen = synth.layout(p)
-    lens = (off[1:] - off[:-1]).astype(np.float64)
-    gw = np.bincount(group, weights=lens, minlength=G)  # work per group ~ its PCs
-    owner, load = lpt_assign(gw, world)
-    ids = np.nonzero(owner[group] == rank)[0]
+    owner, load = sharding.lpt_assign(sharding.group_weights(group, off, G), world)
+    ids = sharding.local_entries(group, owner, rank)
     corp = synth.subcorpus(p, ids, group, off, plen)
     gen_s = time.time() - t0
 
@@ -131,8 +159,7 @@ def main():
 
     def step():
         _lib.check(L.syzgpu_corpus_minimize_dev(store.handle, C, d_sel.data_ptr(), d_hist.data_ptr(), sptr))
-        if world > 1:
-            dist.all_reduce(d_hist, op=dist.ReduceOp.SUM)  # the one exchange: (C+1) int64
+        sharding.allreduce_hist(d_hist, dist)  # the one exchange: (C+1) int64
         _lib.check(L.syzgpu_prio_choice_dev(d_static.data_ptr(), d_hist.data_ptr(), C, None, d_prios.data_ptr(),
                                             d_run.data_ptr(), d_pres.data_ptr(), sptr))
 
@@ -198,26 +225,7 @@ def main():
         # launch processes (Minimize: 4 B per PC + 10 B per program), over its measured average time
         roof = None
         if kern:
-            dom = max(kern, key=lambda n: kern[n]["ms"])
-            d = kern[dom]
-            avg_ms = d["ms"] / d["launches"]
-            n_local = corp.n
-            alg = 4 * sum_pcs + 10 * n_local if dom.startswith(("bucket", "group", "ranks", "select", "gosort",
-                                                                "panel", "el_init", "vec_min")) else d["bytes"] / d["launches"]
-            ach = alg / (avg_ms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                    "avg_launch_ms": round(avg_ms, 4),
-                    "design_bytes_per_launch": int(d["bytes"] / d["launches"]),
-                    "algorithmic_bytes_per_launch": int(alg)}
-            tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(tf):
-                try:
-                    pm = json.load(open(tf))
-                    if dom in pm.get("kernels", {}) and pm.get("workload") == "config4-1M":
-                        roof["traffic"] = pm["kernels"][dom]["hbm_bytes_per_launch"]
-                except Exception:
-                    pass
+            roof = roofline(kern, corp, store_info, C)
         path_bytes = 4 * sum_pcs_all + 10 * total_progs + 16 * C * C
         cpu = None
         if args.cpu_baseline and world == 1:

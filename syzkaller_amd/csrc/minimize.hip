@@ -1257,8 +1257,8 @@ int syzgpu_corpus_info(const syzgpu_corpus* cp, uint64_t* info, size_t cap) {
   SYZ_API_BODY({
     if (!cp || !info) fail(SYZGPU_EINVAL, "null pointer");
     const Corpus& K = *reinterpret_cast<const Corpus*>(cp);
-    const uint64_t v[6] = {K.n, K.G, K.total_pcs, K.total_ids, K.hwork.size(), K.ngtabs};
-    for (size_t i = 0; i < cap && i < 6; i++) info[i] = v[i];
+    const uint64_t v[7] = {K.n, K.G, K.total_pcs, K.total_ids, K.hwork.size(), K.ngtabs, K.total_vecs};
+    for (size_t i = 0; i < cap && i < 7; i++) info[i] = v[i];
   })
 }
 
