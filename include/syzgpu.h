@@ -66,6 +66,11 @@ int syzgpu_intersection(const uint32_t* a, size_t na, const uint32_t* b, size_t 
 int syzgpu_minimize(const uint32_t* pcs, const uint64_t* off, size_t ncov, int64_t* out_idx,
                     size_t* out_n);
 
+/* cover/cover.go:106-113: the permutation sort.Sort(minInputArray) gives Minimize's inputs (Go 1.6-1.18
+ * quickSort; Less = longer cover first, unstable). For each group g of lens[group_off[g] ..
+ * group_off[g+1]), perm[group_off[g] + r] = index inside the group of the input at sorted position r. */
+int syzgpu_minimize_order(const uint64_t* lens, const uint64_t* group_off, uint32_t ngroups, int64_t* perm);
+
 /* ---- batched forms (one launch for many covers / pairs) ------------------------------------- */
 /* Canonicalize every cover of a CSR in place; out_len[i] = new length of cover i. */
 int syzgpu_canonicalize_batch(uint32_t* pcs, const uint64_t* off, size_t ncov, uint64_t* out_len);

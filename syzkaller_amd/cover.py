@@ -100,6 +100,18 @@ def MinimizeCorpus(pcs, off, group, ngroups):
     return out[: int(goff[-1])].copy(), goff
 
 
+def MinimizeOrder(lens, group_off=None):
+    """cover.go:106-113: Go sort.Sort order of Minimize's inputs per group (index inside the group of
+    the input at each sorted position), for cover lengths `lens` split by `group_off`."""
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    if group_off is None:
+        group_off = np.array([0, lens.size], dtype=np.uint64)
+    group_off = np.ascontiguousarray(group_off, dtype=np.uint64)
+    perm = np.empty(max(lens.size, 1), dtype=np.int64)
+    check(lib().syzgpu_minimize_order(ptr(lens), ptr(group_off), group_off.size - 1, ptr(perm)))
+    return perm[: lens.size].copy()
+
+
 _OPS = {"difference": _lib.DIFFERENCE, "symmetric_difference": _lib.SYMMETRIC_DIFFERENCE,
         "union": _lib.UNION, "intersection": _lib.INTERSECTION}
 

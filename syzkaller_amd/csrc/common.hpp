@@ -79,6 +79,12 @@ struct Context {
   size_t last_n = 0;
   uint32_t last_groups = 0;
   bool have_last = false;
+  std::vector<hipEvent_t> gs_events;  // gosort level-count events (reused)
+  hipStream_t side = nullptr;         // second stream: independent work overlapped with the main one
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipStream_t cap = nullptr;           // capture stream for the gosort level graphs
+  hipGraphExec_t gl_exec[2] = {nullptr, nullptr};
+  std::vector<const void*> gl_key;
 };
 
 // Returns the initialised context of the current device (lazily init(0)); throws ENODEV.
@@ -96,19 +102,20 @@ struct Prof {
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   void reset();
-  void begin(const char* name, hipStream_t s, uint64_t bytes);
-  void end(hipStream_t s);
+  size_t begin(const char* name, hipStream_t s, uint64_t bytes);
+  void end(size_t rec, hipStream_t s);
 };
 Prof& prof();
 
 struct ProfScope {
   hipStream_t s;
   bool on;
+  size_t rec = 0;
   ProfScope(const char* name, hipStream_t st, uint64_t bytes) : s(st), on(prof().on) {
-    if (on) prof().begin(name, s, bytes);
+    if (on) rec = prof().begin(name, s, bytes);
   }
   ~ProfScope() {
-    if (on) prof().end(s);
+    if (on) prof().end(rec, s);
   }
 };
 

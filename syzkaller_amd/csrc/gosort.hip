@@ -1,47 +1,58 @@
-// The permutation Go's sort.Sort (Go 1.7 quickSort) produces for cover.Minimize's input array
-// (cover/cover.go:106-113, minInputArray.Less = len(a[i].cov) > len(a[j].cov), :140-143),
-// computed on the GPU for every call group at once, in ONE persistent launch.
+// The permutation Go's sort.Sort (Go 1.6 .. 1.18 quickSort) produces for cover.Minimize's input array
+// (cover/cover.go:106-113, minInputArray.Less = len(a[i].cov) > len(a[j].cov), :140-143), computed
+// on the GPU for every call group at once.
 //
 // sort.Sort is unstable: among equal lengths the order depends on the exact sequence of swaps, and
 // that order decides which inputs Minimize keeps. The simulation performs exactly the
-// swaps of the sequential algorithm, with each doPivot's O(n) loops run in parallel:
-//   * the Hoare loop pairs the k-th element > pivot from the left with the k-th element <= pivot
-//     from the right for every k below the number of misplaced elements: both lists are built by
-//     ordered compaction (prefix scans / ballots) and swapped pairwise;
-//   * the "protect" duplicate pass is the same pairing with (== pivot) vs (< pivot);
-//   * the O(1) parts (Tukey ninther + medianOfThree, the dups probe) gather their <= 9 elements in
-//     parallel and evaluate the sequential decision logic on registers in every lane;
-//   * leaves (<= 12 elements: gap-6 shell pass + insertionSort) are six disjoint compare-swaps plus
-//     a STABLE sort — insertionSort only moves an element past strictly greater ones — done as a
-//     lane-parallel rank computation.
-// Disjoint subranges are independent, so nodes are scheduled through a global work queue:
-//   segment > T_LDS   one 1024-thread workgroup partitions it in place in HBM, pushes the children;
-//   segment <= T_LDS  one workgroup sorts it to completion in LDS (1024-thread cooperative
-//                     partitions above WAVE_MAX, then one wave per sub-segment) and writes the
-//                     local permutation to perm[].
-// Elements are (len << 32) | member index in HBM and (len << 14) | local index in LDS; Less only
-// compares the length field.
+// swaps of the sequential algorithm (oracle/gosort.h restates it):
+//   * the O(1) decisions of doPivot (Tukey ninther + medianOfThree, the dups probe) and the leaves
+//     (gap-6 shell pass + insertionSort on <= 12 elements) and heapSort run as the SAME sequential
+//     code, one thread per segment;
+//   * the two O(n) loops of doPivot are replaced by their closed form: the Hoare loop swaps the k-th
+//     misplaced element from the left (len < pivot len, left of the final boundary) with the k-th
+//     misplaced element from the right, and the boundary is lo+1 + #(len >= pivot len); the
+//     "protect" duplicate loop is the same pairing with (len <= pivot) vs (len > pivot) on [lo+1, b).
+//     Counting and ordered compaction are data-parallel.
+// Quicksort nodes of one level are independent, so they are processed LEVEL-SYNCHRONOUSLY:
+//   segment > T_SEG   global levels: every segment of the level split into 4096-element tiles,
+//                     one kernel per step (pivot / count / tile counts / lists / swap / probe /
+//                     protect x4 / finish), children routed by size;
+//   segment <= T_SEG  one workgroup per pack of segments in LDS (call groups <= T_SEG are packed
+//                     up to T_SEG elements; global-level children get a workgroup each); inside, all
+//                     active segments advance one doPivot per level with workgroup-wide scans.
+// Elements are (len << 32) | position in HBM and (len << SH) | local index in LDS (u32 when every
+// length of the pack fits, otherwise a u64 instantiation); Less only compares the length field.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "pipeline.hpp"
 
 namespace syz {
 
-#ifdef SYZ_GS_DEBUG
-#define GSD(...) printf(__VA_ARGS__)
+#ifdef SYZ_GS_STATS
+// diagnostic build only: [0] packs [1] levels [2] cycles total [3] pivot [4] part0 [5] probe [6] part1
+// [7] children [8] heap sorts [9] heap elements [10] max active segments [11] leaves
+__device__ unsigned long long g_gs_stats[16];
+#define GS_STAT_ADD(i, v) atomicAdd(&g_gs_stats[i], (unsigned long long)(v))
+#define GS_STAT_MAX(i, v) atomicMax(&g_gs_stats[i], (unsigned long long)(v))
+#define GS_T() __builtin_amdgcn_s_memtime()
 #else
-#define GSD(...)
+#define GS_STAT_ADD(i, v)
+#define GS_STAT_MAX(i, v)
+#define GS_T() 0ull
 #endif
 
-constexpr int GS_BLOCK = 1024;
-constexpr int GS_WAVES = GS_BLOCK / 64;
-constexpr uint32_t T_LDS = 16384;     // segment sorted entirely in LDS (u32 packed elements)
-constexpr uint32_t WAVE_MAX = 1024;   // sub-segments handled by a single wave
-constexpr uint32_t LDS_SHIFT = 14;    // local index bits
-constexpr uint32_t LEN_LIMIT = 1u << 18;
-constexpr uint32_t STACK_A = 64;
-constexpr uint32_t LIST_B = 128;   // phase-A leaves: <= 2 per cooperative partition
-constexpr uint32_t STACK_W = 64;   // >= sort.Sort maxDepth budget + 1
+constexpr uint32_t T_SEG = 8192;   // largest segment sorted in LDS
+constexpr int LS_BLOCK = 512;      // LDS workgroup
+constexpr int LS_ITEMS = T_SEG / LS_BLOCK;
+constexpr int LS_SH = 13;  // local index bits of the packed u32 LDS element (T_SEG = 2^13)
+static_assert((1u << LS_SH) == T_SEG, "LS_SH");
+constexpr uint32_t LS_MAXS = T_SEG / 13 + 4;  // active segments (> 12 elements) per pack
+constexpr int GL_BLOCK = 256;      // global-level tile workgroup
+constexpr int GL_ITEMS = 16;
+constexpr uint32_t GL_TILE = GL_BLOCK * GL_ITEMS;
 
 template <int SH, class T>
 __device__ __forceinline__ bool LT(T x, T y) {  // Go's Less: longer cover first
@@ -59,7 +70,59 @@ __device__ __forceinline__ void swp(P d, uint32_t i, uint32_t j) {
   d[j] = t;
 }
 
-// medianOfThree(data, m1, m0, m2) on values: moves the median into a1 (= data[m1]).
+// ---- sequential pieces, exactly as oracle/gosort.h -------------------------------------------------
+template <int SH, class P>
+__device__ void seq_mo3(P d, uint32_t m1, uint32_t m0, uint32_t m2) {
+  if (LT<SH>(d[m1], d[m0])) swp(d, m1, m0);
+  if (LT<SH>(d[m2], d[m1])) {
+    swp(d, m2, m1);
+    if (LT<SH>(d[m1], d[m0])) swp(d, m1, m0);
+  }
+}
+
+// doPivot's pivot choice; leaves the pivot at d[lo], returns m.
+template <int SH, class P>
+__device__ uint32_t seq_pivot(P d, uint32_t lo, uint32_t hi) {
+  const uint32_t m = (uint32_t)(((uint64_t)lo + hi) >> 1);
+  if (hi - lo > 40) {
+    const uint32_t s = (hi - lo) / 8;
+    seq_mo3<SH>(d, lo, lo + s, lo + 2 * s);
+    seq_mo3<SH>(d, m, m - s, m + s);
+    seq_mo3<SH>(d, hi - 1, hi - 1 - s, hi - 1 - 2 * s);
+  }
+  seq_mo3<SH>(d, lo, m, hi - 1);
+  return m;
+}
+
+// doPivot after the Hoare loop (b == c == bnd): the dups probe. Returns protect.
+template <int SH, class P>
+__device__ bool seq_probe(P d, uint32_t lo, uint32_t hi, uint32_t m, uint32_t bnd, uint32_t* bout, uint32_t* cout) {
+  uint32_t b = bnd, c = bnd;
+  bool protect = hi - c < 5;
+  if (!protect && hi - c < (hi - lo) / 4) {
+    int dups = 0;
+    if (!LT<SH>(d[lo], d[hi - 1])) {
+      swp(d, c, hi - 1);
+      c++;
+      dups++;
+    }
+    if (!LT<SH>(d[b - 1], d[lo])) {
+      b--;
+      dups++;
+    }
+    if (!LT<SH>(d[m], d[lo])) {
+      swp(d, m, b - 1);
+      b--;
+      dups++;
+    }
+    protect = dups > 1;
+  }
+  *bout = b;
+  *cout = c;
+  return protect;
+}
+
+// medianOfThree(data, m1, m0, m2) on register values: moves the median into a1 (= data[m1]).
 template <int SH, class T>
 __device__ __forceinline__ void mo3v(T& a1, T& a0, T& a2) {
   if (LT<SH>(a1, a0)) {
@@ -79,8 +142,9 @@ __device__ __forceinline__ void mo3v(T& a1, T& a0, T& a2) {
   }
 }
 
-// doPivot's pivot selection, executed by a full wave (all lanes compute redundantly on registers).
-// Leaves the pivot at d[lo]; returns m.
+// seq_pivot by a whole wave: the (at most 9, distinct) positions are loaded by 9 lanes at once, the
+// medianOfThree network runs on registers in every lane, and the changed positions are stored back.
+// One memory round trip each way instead of a dependent chain (used on el[] in HBM / L2).
 template <int SH, class P>
 __device__ uint32_t wave_pivot(P d, uint32_t lo, uint32_t hi) {
   using T = typename std::remove_reference<decltype(d[0])>::type;
@@ -100,7 +164,7 @@ __device__ uint32_t wave_pivot(P d, uint32_t lo, uint32_t hi) {
       case 8: pos = hi - 1; break;
       default: break;
     }
-    T mine = lane < 9 ? d[pos] : T(0);
+    const T mine = lane < 9 ? d[pos] : T(0);
     T v0 = __shfl(mine, 0), v1 = __shfl(mine, 1), v2 = __shfl(mine, 2), v3 = __shfl(mine, 3),
       v4 = __shfl(mine, 4), v5 = __shfl(mine, 5), v6 = __shfl(mine, 6), v7 = __shfl(mine, 7),
       v8 = __shfl(mine, 8);
@@ -123,20 +187,19 @@ __device__ uint32_t wave_pivot(P d, uint32_t lo, uint32_t hi) {
     if (lane < 9 && out != mine) d[pos] = out;
   } else {
     const uint32_t pos = lane == 0 ? lo : (lane == 1 ? m : hi - 1);
-    T mine = lane < 3 ? d[pos] : T(0);
+    const T mine = lane < 3 ? d[pos] : T(0);
     T v0 = __shfl(mine, 0), v1 = __shfl(mine, 1), v2 = __shfl(mine, 2);
     mo3v<SH>(v0, v1, v2);  // medianOfThree(lo, m, hi-1)
-    T out = lane == 0 ? v0 : (lane == 1 ? v1 : v2);
+    const T out = lane == 0 ? v0 : (lane == 1 ? v1 : v2);
     if (lane < 3 && out != mine) d[pos] = out;
   }
   return m;
 }
 
-// doPivot's dups probe after the main partition (b == c == bnd on entry), one full wave.
-// The five positions it may touch are cached by position, so aliasing (m == b-1) is exact.
+// seq_probe by a whole wave. Its positions hi-1, bnd, bnd-1, bnd-2, m are distinct whenever the
+// probe runs (bnd > hi - (hi-lo)/4 and hi - bnd >= 5), and are cached by position.
 template <int SH, class P>
-__device__ bool wave_probe(P d, uint32_t lo, uint32_t hi, uint32_t m, uint32_t bnd, uint32_t* bout,
-                           uint32_t* cout) {
+__device__ bool wave_probe(P d, uint32_t lo, uint32_t hi, uint32_t m, uint32_t bnd, uint32_t* bout, uint32_t* cout) {
   using T = typename std::remove_reference<decltype(d[0])>::type;
   uint32_t b = bnd, c = bnd;
   bool protect = hi - c < 5;
@@ -144,12 +207,11 @@ __device__ bool wave_probe(P d, uint32_t lo, uint32_t hi, uint32_t m, uint32_t b
     const unsigned lane = __lane_id();
     const uint32_t p0 = hi - 1, p1 = bnd, p2 = bnd - 1, p3 = bnd - 2, p4 = m;
     const uint32_t pos = lane == 0 ? p0 : lane == 1 ? p1 : lane == 2 ? p2 : lane == 3 ? p3 : lane == 4 ? p4 : lo;
-    T mine = lane < 6 ? d[pos] : T(0);
+    const T mine = lane < 6 ? d[pos] : T(0);
     T v0 = __shfl(mine, 0), v1 = __shfl(mine, 1), v2 = __shfl(mine, 2), v3 = __shfl(mine, 3),
-      v4 = __shfl(mine, 4), pv = __shfl(mine, 5);
-    auto get = [&](uint32_t p) -> T {
-      return p == p0 ? v0 : p == p1 ? v1 : p == p2 ? v2 : p == p3 ? v3 : v4;
-    };
+      v4 = __shfl(mine, 4);
+    const T pv = __shfl(mine, 5);
+    auto get = [&](uint32_t p) -> T { return p == p0 ? v0 : p == p1 ? v1 : p == p2 ? v2 : p == p3 ? v3 : v4; };
     auto set = [&](uint32_t p, T x) {
       if (p == p0) v0 = x;
       if (p == p1) v1 = x;
@@ -159,7 +221,7 @@ __device__ bool wave_probe(P d, uint32_t lo, uint32_t hi, uint32_t m, uint32_t b
     };
     int dups = 0;
     if (!LT<SH>(pv, get(hi - 1))) {  // data[hi-1] = pivot: swap(c, hi-1); c++
-      T t = get(c);
+      const T t = get(c);
       set(c, get(hi - 1));
       set(hi - 1, t);
       c++;
@@ -170,14 +232,14 @@ __device__ bool wave_probe(P d, uint32_t lo, uint32_t hi, uint32_t m, uint32_t b
       dups++;
     }
     if (!LT<SH>(get(m), pv)) {  // data[m] = pivot: swap(m, b-1); b--
-      T t = get(m);
+      const T t = get(m);
       set(m, get(b - 1));
       set(b - 1, t);
       b--;
       dups++;
     }
     protect = dups > 1;
-    T out = lane == 0 ? v0 : lane == 1 ? v1 : lane == 2 ? v2 : lane == 3 ? v3 : v4;
+    const T out = lane == 0 ? v0 : lane == 1 ? v1 : lane == 2 ? v2 : lane == 3 ? v3 : v4;
     if (lane < 5 && out != mine) d[pos] = out;
   }
   *bout = b;
@@ -185,31 +247,13 @@ __device__ bool wave_probe(P d, uint32_t lo, uint32_t hi, uint32_t m, uint32_t b
   return protect;
 }
 
-// quickSort's tail for 2..12 elements: gap-6 shell pass (six disjoint compare-swaps) then
-// insertionSort (= a stable sort under Less), one full wave.
+// quickSort's tail for 2..12 elements: gap-6 shell pass, then insertionSort.
 template <int SH, class P>
-__device__ void wave_leaf(P d, uint32_t lo, uint32_t hi) {
-  using T = typename std::remove_reference<decltype(d[0])>::type;
-  const uint32_t n = hi - lo;
-  const unsigned lane = __lane_id();
-  T x = lane < n ? d[lo + lane] : T(0);
-  const unsigned partner = lane < 6 ? lane + 6 : lane - 6;
-  T y = __shfl(x, partner < 64 ? partner : 0);
-  if (lane < n && partner < n && lane < 12) {
-    if (lane >= 6) {
-      if (LT<SH>(x, y)) x = y;  // Less(i, i-6): lane i takes data[i-6]
-    } else {
-      if (LT<SH>(y, x)) x = y;  // Less(j+6, j): lane j takes data[j+6]
-    }
-  }
-  uint32_t rank = 0;
-  for (uint32_t j = 0; j < n; j++) {
-    const T xj = __shfl(x, j);
-    if (LT<SH>(xj, x) || (j < lane && KEY<SH>(xj) == KEY<SH>(x))) rank++;
-  }
-  wave_sync();
-  if (lane < n) d[lo + rank] = x;
-  wave_sync();
+__device__ void seq_leaf(P d, uint32_t a, uint32_t b) {
+  for (uint32_t i = a + 6; i < b; i++)
+    if (LT<SH>(d[i], d[i - 6])) swp(d, i, i - 6);
+  for (uint32_t i = a + 1; i < b; i++)
+    for (uint32_t j = i; j > a && LT<SH>(d[j], d[j - 1]); j--) swp(d, j, j - 1);
 }
 
 template <int SH, class P>
@@ -226,7 +270,7 @@ __device__ void sift_down(P d, uint32_t lo, uint32_t hi, uint32_t first) {
 }
 
 template <int SH, class P>
-__device__ void heap_sort(P d, uint32_t a, uint32_t b) {  // one thread
+__device__ void heap_sort(P d, uint32_t a, uint32_t b) {
   const uint32_t first = a, hi = b - a;
   for (int64_t i = ((int64_t)hi - 1) / 2; i >= 0; i--) sift_down<SH>(d, (uint32_t)i, hi, first);
   for (int64_t i = (int64_t)hi - 1; i >= 0; i--) {
@@ -235,440 +279,910 @@ __device__ void heap_sort(P d, uint32_t a, uint32_t b) {  // one thread
   }
 }
 
-// ---- ordered compaction helpers ----------------------------------------------------------------
-template <class Pred, class Q>
-__device__ uint32_t wave_collect(uint32_t beg, uint32_t end, Pred pred, Q out) {
-  uint32_t k = 0;
-  for (uint32_t base = beg; base < end; base += 64) {
-    const uint32_t p = base + __lane_id();
-    const bool f = p < end && pred(p);
-    const uint64_t mask = __ballot(f);
-    if (f) out[k + __popcll(mask & lanemask_lt())] = p;
-    k += __popcll(mask);
-  }
-  return k;
-}
-
-// Block-wide: every thread takes a contiguous run of the range; counts, scans, then writes in order.
-template <class Pred, class Q>
-__device__ uint32_t block_collect(uint32_t beg, uint32_t end, Pred pred, Q out, uint32_t* red) {
-  const uint32_t n = end > beg ? end - beg : 0;
-  const uint32_t per = (n + GS_BLOCK - 1) / GS_BLOCK;
-  const uint32_t s = beg + threadIdx.x * per;
-  const uint32_t e = min(end, s + per);
-  uint32_t cnt = 0;
-  for (uint32_t p = s; p < e; p++) cnt += pred(p) ? 1u : 0u;
-  uint32_t tot;
-  uint32_t k = block_excl_scan<GS_BLOCK>(cnt, red, &tot);
-  for (uint32_t p = s; p < e; p++)
-    if (pred(p)) out[k++] = p;
-  __syncthreads();
-  return tot;
-}
-
-template <class Pred>
-__device__ uint32_t block_count(uint32_t beg, uint32_t end, Pred pred, uint32_t* red) {
-  uint32_t c = 0;
-  for (uint32_t p = beg + threadIdx.x; p < end; p += GS_BLOCK) c += pred(p) ? 1u : 0u;
-  return block_sum<GS_BLOCK>(c, red);
-}
-
-// ---- one doPivot by the whole workgroup on an array in LDS (u32) or HBM (u64) ----------------------
-// A/B: position scratch (tA/tB + lo indexing). Returns false if depth was exhausted (caller sorts).
-template <int SH, class P, class Q>
-__device__ void block_dopivot(P d, Q A, Q B, uint32_t lo, uint32_t hi, uint32_t* red, uint32_t* sh,
-                              uint32_t* mlo, uint32_t* mhi) {
-  if (threadIdx.x < 64) {
-    const uint32_t m = wave_pivot<SH>(d, lo, hi);
-    if (threadIdx.x == 0) {
-      sh[0] = KEY<SH>(d[lo]);
-      sh[1] = m;
+// The same leaf in registers: the shell pass swaps the disjoint pairs (i-6, i), and insertionSort
+// only moves an element past strictly Less ones, so it is the STABLE sort by Less: the element at i
+// lands at #{j : Less(j, i)} + #{j < i : equal}. Loads and stores are independent (no LDS chains).
+template <int SH, class P>
+__device__ void reg_leaf(P d, uint32_t a, uint32_t n) {
+  using E = typename std::remove_reference<decltype(d[0])>::type;
+  E x[12];
+#pragma unroll
+  for (uint32_t i = 0; i < 12; i++) x[i] = i < n ? d[a + i] : (E)0;
+#pragma unroll
+  for (uint32_t i = 6; i < 12; i++)
+    if (i < n && LT<SH>(x[i], x[i - 6])) {
+      const E t = x[i];
+      x[i] = x[i - 6];
+      x[i - 6] = t;
     }
-  }
-  __syncthreads();
-  const uint32_t plen = sh[0], m = sh[1];
-  auto key = [&](uint32_t p) { return KEY<SH>(d[p]); };
-  const uint32_t bnd = lo + 1 + block_count(lo + 1, hi - 1, [&](uint32_t p) { return key(p) >= plen; }, red);
-  const uint32_t nG = block_collect(lo + 1, bnd, [&](uint32_t p) { return key(p) < plen; }, A + lo, red);
-  (void)block_collect(bnd, hi - 1, [&](uint32_t p) { return key(p) >= plen; }, B + lo, red);
-  for (uint32_t k = threadIdx.x; k < nG; k += GS_BLOCK) swp(d, A[lo + k], B[lo + nG - 1 - k]);
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    uint32_t b, c;
-    const bool protect = wave_probe<SH>(d, lo, hi, m, bnd, &b, &c);
-    if (threadIdx.x == 0) {
-      sh[2] = b;
-      sh[3] = c;
-      sh[4] = protect;
+#pragma unroll
+  for (uint32_t i = 0; i < 12; i++) {
+    if (i >= n) break;
+    const uint32_t ki = KEY<SH>(x[i]);
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 12; j++) {
+      const uint32_t kj = KEY<SH>(x[j]);
+      r += (j < n && (kj > ki || (j < i && kj == ki))) ? 1u : 0u;
     }
-  }
-  __syncthreads();
-  uint32_t b = sh[2];
-  const uint32_t c = sh[3];
-  if (sh[4]) {
-    // protect pass over [lo+1, b): len > plen stays left, len <= plen goes right
-    const uint32_t b2 = lo + 1 + block_count(lo + 1, b, [&](uint32_t p) { return key(p) > plen; }, red);
-    const uint32_t nE = block_collect(lo + 1, b2, [&](uint32_t p) { return key(p) <= plen; }, A + lo, red);
-    (void)block_collect(b2, b, [&](uint32_t p) { return key(p) > plen; }, B + lo, red);
-    for (uint32_t k = threadIdx.x; k < nE; k += GS_BLOCK) swp(d, A[lo + k], B[lo + nE - 1 - k]);
-    __syncthreads();
-    b = b2;
-  }
-  if (threadIdx.x == 0) swp(d, lo, b - 1);
-  __syncthreads();
-  *mlo = b - 1;
-  *mhi = c;
-}
-
-// One doPivot by a single wave on LDS.
-template <class P, class Q>
-__device__ void wave_dopivot(P d, Q A, Q B, uint32_t lo, uint32_t hi, uint32_t* mlo, uint32_t* mhi) {
-  constexpr int SH = LDS_SHIFT;
-  const uint32_t m = wave_pivot<SH>(d, lo, hi);
-  wave_sync();
-  const uint32_t plen = KEY<SH>(d[lo]);
-  auto key = [&](uint32_t p) { return KEY<SH>(d[p]); };
-  uint32_t lc = 0;
-  for (uint32_t p = lo + 1 + __lane_id(); p < hi - 1; p += 64) lc += key(p) >= plen;
-  const uint32_t bnd = lo + 1 + wave_sum(lc);
-  const uint32_t nG = wave_collect(lo + 1, bnd, [&](uint32_t p) { return key(p) < plen; }, A + lo);
-  (void)wave_collect(bnd, hi - 1, [&](uint32_t p) { return key(p) >= plen; }, B + lo);
-  wave_sync();
-  for (uint32_t k = __lane_id(); k < nG; k += 64) swp(d, A[lo + k], B[lo + nG - 1 - k]);
-  wave_sync();
-  uint32_t b, c;
-  const bool protect = wave_probe<SH>(d, lo, hi, m, bnd, &b, &c);
-  wave_sync();
-  if (protect) {
-    uint32_t xc = 0;
-    for (uint32_t p = lo + 1 + __lane_id(); p < b; p += 64) xc += key(p) > plen;
-    const uint32_t b2 = lo + 1 + wave_sum(xc);
-    const uint32_t nE = wave_collect(lo + 1, b2, [&](uint32_t p) { return key(p) <= plen; }, A + lo);
-    (void)wave_collect(b2, b, [&](uint32_t p) { return key(p) > plen; }, B + lo);
-    wave_sync();
-    for (uint32_t k = __lane_id(); k < nE; k += 64) swp(d, A[lo + k], B[lo + nE - 1 - k]);
-    wave_sync();
-    b = b2;
-  }
-  if (__lane_id() == 0) swp(d, lo, b - 1);
-  wave_sync();
-  *mlo = b - 1;
-  *mhi = c;
-}
-
-// quickSort(d, lo, hi, depth) entirely by one wave (sub-segment <= WAVE_MAX in LDS).
-__device__ void wave_quicksort(uint32_t* d, uint16_t* A, uint16_t* B, uint32_t* stk, uint32_t lo, uint32_t hi,
-                               int32_t depth) {
-  constexpr int SH = LDS_SHIFT;
-  int sp = 0;
-  if (__lane_id() == 0) {
-    stk[0] = lo;
-    stk[1] = hi;
-    stk[2] = (uint32_t)depth;
-  }
-  sp = 1;
-  wave_sync();
-  while (sp > 0) {
-    sp--;
-    const uint32_t a = stk[3 * sp], b = stk[3 * sp + 1];
-    const int32_t dep = (int32_t)stk[3 * sp + 2];
-    wave_sync();
-    if (__lane_id() == 0) GSD("wq pop [%u,%u) dep %d sp %d\n", a, b, dep, sp);
-    if (b - a <= 12) {
-      if (b - a > 1) wave_leaf<SH>(d, a, b);
-      if (__lane_id() == 0) GSD("leaf done\n");
-      continue;
-    }
-    if (dep == 0) {
-      if (__lane_id() == 0) heap_sort<SH>(d, a, b);
-      wave_sync();
-      continue;
-    }
-    uint32_t mlo, mhi;
-    wave_dopivot(d, A, B, a, b, &mlo, &mhi);
-    if (__lane_id() == 0) {
-      stk[3 * sp] = a;
-      stk[3 * sp + 1] = mlo;
-      stk[3 * sp + 2] = (uint32_t)(dep - 1);
-      stk[3 * sp + 3] = mhi;
-      stk[3 * sp + 4] = b;
-      stk[3 * sp + 5] = (uint32_t)(dep - 1);
-    }
-    sp += 2;
-    wave_sync();
+    d[a + r] = x[i];
   }
 }
 
-struct QCtl {
-  uint32_t head, tail, pending, err;
+// A node of quickSort(data, lo, hi, depth) that is not a doPivot: leaf or depth-exhausted heapSort.
+template <int SH, class P>
+__device__ void seq_terminal(P d, uint32_t lo, uint32_t hi, int32_t depth) {
+  if (hi - lo <= 12) {
+    if (hi - lo > 1) reg_leaf<SH>(d, lo, hi - lo);
+  } else if (depth == 0) {
+    GS_STAT_ADD(8, 1);
+    GS_STAT_ADD(9, hi - lo);
+    heap_sort<SH>(d, lo, hi);
+  }
+}
+
+__host__ __device__ inline int32_t go_max_depth(uint64_t n) {
+  int32_t depth = 0;
+  for (uint64_t i = n; i > 0; i >>= 1) depth++;
+  return depth * 2;
+}
+
+// =====================================================================================================
+// LDS level-synchronous sorter: one workgroup per pack.
+// =====================================================================================================
+struct Pack {
+  uint32_t plo, phi;    // element range in el[] (whole segments)
+  uint32_t sbeg, send;  // its segments in the segment array
 };
 
-struct GsLds {
-  uint32_t d[T_LDS];
-  uint16_t A[T_LDS];
-  uint16_t B[T_LDS];
-  uint32_t red[GS_BLOCK / 64 + 1];
-  uint32_t sh[8];
-  uint32_t stackA[STACK_A * 3];
-  uint32_t listB[LIST_B * 3];
-  uint32_t stackW[GS_WAVES][STACK_W * 3];
-  uint32_t nA, nB, flag;
+// LDS view of the pack's elements with one pad word per 16: a thread's contiguous 16-element chunk
+// then starts on its own bank, so chunk walks are conflict-free (a plain array is 16-way).
+template <class E>
+struct PadRef {
+  E* v;
+  __device__ __forceinline__ E& operator[](uint32_t i) const { return v[i + (i >> 4)]; }
 };
 
-// Sort el[lo, lo+n) (n <= T_LDS) completely in LDS; writes perm[lo + p] = lo + source offset.
-// Returns false (nothing written) if a length does not fit the packed LDS format.
-__device__ bool lds_sort(const uint64_t* __restrict__ el, uint32_t* __restrict__ perm, uint32_t lo, uint32_t n,
-                         int32_t depth, GsLds& L) {
-  constexpr int SH = LDS_SHIFT;
-  if (threadIdx.x == 0) {
-    L.flag = 0;
-    L.nA = 0;
-    L.nB = 0;
+template <class E>
+struct LsLds {
+  E dv[T_SEG + T_SEG / 16];
+  __device__ __forceinline__ PadRef<E> D() { return PadRef<E>{dv}; }
+  uint16_t ab[T_SEG];       // misplaced-left positions by rank in [0, T/2), misplaced-right in [T/2, T)
+  uint16_t abs[T_SEG / 2];  // segment of each misplaced-left entry
+  uint16_t lo[2][LS_MAXS], hi[2][LS_MAXS];
+  int8_t dep[2][LS_MAXS];
+  uint32_t pl[LS_MAXS], cnt[LS_MAXS];
+  uint16_t m[LS_MAXS], bnd[LS_MAXS], b[LS_MAXS], c[LS_MAXS], base[LS_MAXS];
+  uint8_t prot[LS_MAXS];
+  uint32_t red[LS_BLOCK / 64 + 1];
+  uint32_t na, tot, flag, anyprot;
+};
+
+// first active segment with hi > p (segments sorted, disjoint)
+template <class L>
+__device__ __forceinline__ uint32_t seg_at(const L& S, int cur, uint32_t na, uint32_t p) {
+  uint32_t a = 0, z = na;
+  while (a < z) {
+    const uint32_t mid = (a + z) >> 1;
+    if (S.hi[cur][mid] <= p)
+      a = mid + 1;
+    else
+      z = mid;
   }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += GS_BLOCK) {
-    const uint64_t len = el[lo + i] >> 32;
-    if (len >= LEN_LIMIT) L.flag = 1;
-    L.d[i] = ((uint32_t)len << SH) | i;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) GSD("lds loaded n %u flag %u\n", n, L.flag);
-  if (L.flag) return false;
-  // phase A: cooperative partitions of sub-segments larger than one wave's share
-  if (threadIdx.x == 0) {
-    if (n > WAVE_MAX && depth > 0) {
-      L.stackA[0] = 0;
-      L.stackA[1] = n;
-      L.stackA[2] = (uint32_t)depth;
-      L.nA = 1;
-    } else {
-      L.listB[0] = 0;
-      L.listB[1] = n;
-      L.listB[2] = (uint32_t)depth;
-      L.nB = 1;
+  return a;
+}
+
+// One compaction round of the level: mode 0 = Hoare pass (bnd, pairs len<pl | len>=pl on
+// [lo+1, hi-1)), mode 1 = protect pass (pairs len<=pl | len>pl on [lo+1, b)).
+// Thread t owns the chunk [16t, 16t+16) held in registers. Active segments have more than 12
+// elements, so a chunk meets at most 3 of them (sfirst .. sfirst+2): their fields are loaded once
+// into registers and every per-element step is branch-free.
+template <int SH, class E, class L>
+__device__ void ls_partition(L& S, int cur, uint32_t na, uint32_t n, int mode) {
+  unsigned long long tq0 = GS_T();
+  (void)tq0;
+  constexpr uint32_t H = T_SEG / 2;
+  const uint32_t i0 = threadIdx.x * LS_ITEMS;
+  const bool live = i0 < n;
+  E x[LS_ITEMS];
+  uint32_t sf = na, slo[3], shi[3], spl[3], sa[3], se[3], cnt[3] = {0, 0, 0};
+  uint32_t segoff = 0xFFFFFFFFu;  // 2 bits per element: segment sf + k, 3 = in no active segment
+  uint32_t inr = 0, left = 0;     // bit i: in the pass range / stays left
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < LS_ITEMS; i++) x[i] = S.D()[i0 + i];
+    sf = seg_at(S, cur, na, i0);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const uint32_t ss = sf + k;
+      if (ss < na) {
+        slo[k] = S.lo[cur][ss];
+        shi[k] = S.hi[cur][ss];
+        spl[k] = S.pl[ss];
+        const bool act = mode == 0 || S.prot[ss];
+        sa[k] = slo[k] + 1;
+        se[k] = act ? (mode == 0 ? shi[k] - 1 : S.b[ss]) : 0;
+      } else {
+        slo[k] = 0xFFFFFFFFu;
+        shi[k] = 0;
+        spl[k] = 0;
+        sa[k] = 1;
+        se[k] = 0;
+      }
     }
-  }
-  __syncthreads();
-  while (L.nA > 0) {
-    const uint32_t top = L.nA - 1;
-    const uint32_t a = L.stackA[3 * top], b = L.stackA[3 * top + 1];
-    const int32_t dep = (int32_t)L.stackA[3 * top + 2];
-    __syncthreads();
-    if (threadIdx.x == 0) L.nA = top;
-    uint32_t mlo, mhi;
-    block_dopivot<SH>(L.d, L.A, L.B, a, b, L.red, L.sh, &mlo, &mhi);
-    if (threadIdx.x == 0) {
-      const uint32_t ca[2] = {a, mhi}, cb[2] = {mlo, b};
-      for (int k = 0; k < 2; k++) {
-        const uint32_t s = cb[k] - ca[k];
-        if (s <= 1) continue;
-        if (s > WAVE_MAX && dep - 1 > 0) {
-          L.stackA[3 * L.nA] = ca[k];
-          L.stackA[3 * L.nA + 1] = cb[k];
-          L.stackA[3 * L.nA + 2] = (uint32_t)(dep - 1);
-          L.nA++;
-        } else {
-          L.listB[3 * L.nB] = ca[k];
-          L.listB[3 * L.nB + 1] = cb[k];
-          L.listB[3 * L.nB + 2] = (uint32_t)(dep - 1);
-          L.nB++;
+#pragma unroll
+    for (int i = 0; i < LS_ITEMS; i++) {
+      const uint32_t p = i0 + i;
+      const uint32_t k = p >= shi[0] ? (p >= shi[1] ? 2u : 1u) : 0u;
+      const uint32_t lo = k == 0 ? slo[0] : (k == 1 ? slo[1] : slo[2]);
+      const uint32_t hi = k == 0 ? shi[0] : (k == 1 ? shi[1] : shi[2]);
+      if (p >= lo && p < hi) {
+        segoff &= ~(3u << (2 * i));
+        segoff |= k << (2 * i);
+        const uint32_t a = k == 0 ? sa[0] : (k == 1 ? sa[1] : sa[2]);
+        const uint32_t e = k == 0 ? se[0] : (k == 1 ? se[1] : se[2]);
+        if (p >= a && p < e) {
+          const uint32_t pl = k == 0 ? spl[0] : (k == 1 ? spl[1] : spl[2]);
+          const uint32_t key = KEY<SH>(x[i]);
+          const bool st = mode == 0 ? key >= pl : key > pl;
+          inr |= 1u << i;
+          left |= (st ? 1u : 0u) << i;
+          if (st) {
+            if (k == 0) cnt[0]++;
+            else if (k == 1) cnt[1]++;
+            else cnt[2]++;
+          }
         }
       }
     }
-    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      if (cnt[k]) atomicAdd(&S.cnt[sf + k], cnt[k]);
   }
-  // phase B: one wave per remaining sub-segment
-  const int w = threadIdx.x >> 6;
-  if (threadIdx.x == 0) GSD("phase B nB %u\n", L.nB);
-  for (uint32_t i = w; i < L.nB; i += GS_WAVES) {
-    const uint32_t a = L.listB[3 * i], b = L.listB[3 * i + 1];
-    const int32_t dep = (int32_t)L.listB[3 * i + 2];
-    if (b - a > WAVE_MAX && dep == 0) {
-      if (__lane_id() == 0) heap_sort<SH>(L.d, a, b);  // depth-exhausted large sub-segment
-      wave_sync();
-    } else {
-      wave_quicksort(L.d, L.A, L.B, L.stackW[w], a, b, dep);
-    }
-  }
-  if (__lane_id() == 0) GSD("wave %d phase B done\n", w);
   __syncthreads();
-  if (threadIdx.x == 0) GSD("perm write\n");
-  for (uint32_t i = threadIdx.x; i < n; i += GS_BLOCK) perm[lo + i] = lo + (L.d[i] & ((1u << SH) - 1));
-  return true;
+  unsigned long long tq1 = GS_T();
+  for (uint32_t q = threadIdx.x; q < na; q += LS_BLOCK) S.bnd[q] = (uint16_t)(S.lo[cur][q] + 1 + S.cnt[q]);
+  __syncthreads();
+  unsigned long long tq2 = GS_T();
+  // classes: 1 = misplaced left, 2 = misplaced right (2 bits per element); packed rank counts
+  uint32_t cl = 0, packed = 0;
+  uint32_t sbd[3] = {0, 0, 0};
+  if (live) {
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      if (sf + k < na) sbd[k] = S.bnd[sf + k];
+#pragma unroll
+    for (int i = 0; i < LS_ITEMS; i++) {
+      if (!((inr >> i) & 1u)) continue;
+      const uint32_t k = (segoff >> (2 * i)) & 3u;
+      const uint32_t bd = k == 0 ? sbd[0] : (k == 1 ? sbd[1] : sbd[2]);
+      const bool st = (left >> i) & 1u;
+      const uint32_t f = (i0 + i) < bd ? (st ? 0u : 1u) : (st ? 2u : 0u);
+      cl |= f << (2 * i);
+      packed += f == 1 ? 1u : (f == 2 ? 0x10000u : 0u);
+    }
+  }
+  uint32_t tot;
+  const uint32_t pre = block_excl_scan<LS_BLOCK>(packed, S.red, &tot);
+  uint32_t rl = pre & 0xFFFF, rr = pre >> 16;
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < LS_ITEMS; i++) {
+      const uint32_t k = (segoff >> (2 * i)) & 3u;
+      if (k == 3) continue;
+      const uint32_t p = i0 + i;
+      const uint32_t lo = k == 0 ? slo[0] : (k == 1 ? slo[1] : slo[2]);
+      if (p == lo + 1) S.base[sf + k] = (uint16_t)rl;
+      const uint32_t f = (cl >> (2 * i)) & 3u;
+      if (f == 1) {
+        S.ab[rl] = (uint16_t)p;
+        S.abs[rl] = (uint16_t)(sf + k);
+        rl++;
+      } else if (f == 2) {
+        S.ab[H + rr++] = (uint16_t)p;
+      }
+    }
+  }
+  if (threadIdx.x == 0) S.tot = tot & 0xFFFF;
+  __syncthreads();
+  unsigned long long tq3 = GS_T();
+  // swap the k-th misplaced-left with the k-th misplaced-right from the right end
+  // every element takes part in at most one pair, so all loads of a thread's pairs can be issued
+  // before any store: the dependent LDS chain is paid once, not once per pair
+  const uint32_t nl = S.tot;
+  constexpr int SW = T_SEG / 2 / LS_BLOCK;  // pairs per thread at most
+  uint32_t pp[SW], qq[SW];
+  E vp[SW], vq[SW];
+#pragma unroll
+  for (int j = 0; j < SW; j++) {
+    const uint32_t g = threadIdx.x + j * LS_BLOCK;
+    pp[j] = g < nl ? S.ab[g] : 0;
+    qq[j] = g < nl ? S.abs[g] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < SW; j++) {
+    const uint32_t g = threadIdx.x + j * LS_BLOCK;
+    if (g < nl) {
+      const uint32_t sg = qq[j];
+      const uint32_t bs = S.base[sg];
+      const uint32_t be = sg + 1 < na ? S.base[sg + 1] : nl;
+      qq[j] = S.ab[H + be + bs - 1 - g];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < SW; j++) {
+    const uint32_t g = threadIdx.x + j * LS_BLOCK;
+    if (g < nl) {
+      vp[j] = S.D()[pp[j]];
+      vq[j] = S.D()[qq[j]];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < SW; j++) {
+    const uint32_t g = threadIdx.x + j * LS_BLOCK;
+    if (g < nl) {
+      S.D()[pp[j]] = vq[j];
+      S.D()[qq[j]] = vp[j];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && mode == 0) {
+    GS_STAT_ADD(12, tq1 - tq0);
+    GS_STAT_ADD(13, tq2 - tq1);
+    GS_STAT_ADD(14, tq3 - tq2);
+    GS_STAT_ADD(15, GS_T() - tq3);
+  }
+  (void)tq1; (void)tq2; (void)tq3;
 }
 
-// ---- kernels -------------------------------------------------------------------------------------
-// Level kernel: one workgroup per segment larger than T_LDS, partitioned in place in HBM; children
-// are routed to the next level (large) or to the LDS list.
-__device__ __forceinline__ void route(Seg s, uint32_t* cnt, Seg* big, Seg* lds, Seg* heap) {
-  const uint32_t n = s.hi - s.lo;
-  if (n <= 1) return;
-  if (n <= T_LDS) {
-    lds[atomicAdd(&cnt[1], 1u)] = s;
-  } else if (s.depth == 0) {
-    heap[atomicAdd(&cnt[2], 1u)] = s;
-  } else {
-    big[atomicAdd(&cnt[0], 1u)] = s;
+template <int SH, class E>
+__global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict__ el, uint32_t* __restrict__ perm,
+                                                      const Pack* __restrict__ packs, uint32_t npacks_host,
+                                                      const uint32_t* npacks_dev, const Seg* __restrict__ segs,
+                                                      uint32_t* bounce_cnt, Pack* bounce) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  LsLds<E>& S = *reinterpret_cast<LsLds<E>*>(smem);
+  constexpr uint64_t LEN_LIMIT = SH >= 32 ? ~0ull : (1ull << (sizeof(E) * 8 - SH));
+  const uint32_t npacks = npacks_dev ? *npacks_dev : npacks_host;
+  for (uint32_t pi = blockIdx.x; pi < npacks; pi += gridDim.x) {
+    const Pack pk = packs[pi];
+    const uint32_t n = pk.phi - pk.plo;
+    if (threadIdx.x == 0) {
+      S.flag = 0;
+      S.na = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += LS_BLOCK) {
+      const uint64_t len = el[pk.plo + i] >> 32;
+      if (len >= LEN_LIMIT) S.flag = 1;
+      S.D()[i] = (E)(((E)len << SH) | (E)i);
+    }
+    __syncthreads();
+    if (S.flag) {  // a length does not fit this element format: the wide instantiation takes it
+      if (threadIdx.x == 0) bounce[atomicAdd(bounce_cnt, 1u)] = pk;
+      __syncthreads();
+      continue;
+    }
+    // initial segments: terminal ones are finished right here, the others become active (in order)
+    {
+      const uint32_t ns = pk.send - pk.sbeg;
+      uint32_t tot;
+      // ordered placement: contiguous per-thread ranges of segments, counted then scanned
+      const uint32_t per = (ns + LS_BLOCK - 1) / LS_BLOCK;
+      const uint32_t k0 = threadIdx.x * per, k1 = min(ns, k0 + per);
+      uint32_t cntA = 0;
+      for (uint32_t k = k0; k < k1; k++) {
+        const Seg sg = segs[pk.sbeg + k];
+        if (sg.hi - sg.lo > 12 && sg.depth > 0) cntA++;
+      }
+      uint32_t o = block_excl_scan<LS_BLOCK>(cntA, S.red, &tot);
+      for (uint32_t k = k0; k < k1; k++) {
+        const Seg sg = segs[pk.sbeg + k];
+        const uint32_t lo = sg.lo - pk.plo, hi = sg.hi - pk.plo;
+        if (hi - lo > 12 && sg.depth > 0) {
+          S.lo[0][o] = (uint16_t)lo;
+          S.hi[0][o] = (uint16_t)hi;
+          S.dep[0][o] = (int8_t)sg.depth;
+          o++;
+        } else {
+          seq_terminal<SH>(S.D(), lo, hi, sg.depth);
+        }
+      }
+      if (threadIdx.x == 0) S.na = tot;
+      __syncthreads();
+    }
+    int cur = 0;
+    unsigned long long tA = GS_T(), tB, tC, tD, tE, tF, tS = tA;
+    (void)tB; (void)tC; (void)tD; (void)tE; (void)tF; (void)tS;
+    if (threadIdx.x == 0) GS_STAT_ADD(0, 1);
+    while (S.na > 0) {
+      const uint32_t na = S.na;
+      if (threadIdx.x == 0) {
+        GS_STAT_ADD(1, 1);
+        GS_STAT_MAX(10, na);
+      }
+      tA = GS_T();
+      // pivot choice, one thread per segment
+      for (uint32_t s = threadIdx.x; s < na; s += LS_BLOCK) {
+        const uint32_t lo = S.lo[cur][s], hi = S.hi[cur][s];
+        S.m[s] = (uint16_t)seq_pivot<SH>(S.D(), lo, hi);
+        S.pl[s] = KEY<SH>(S.D()[lo]);
+        S.cnt[s] = 0;
+      }
+      if (threadIdx.x == 0) S.anyprot = 0;
+      __syncthreads();
+      tB = GS_T();
+      ls_partition<SH, E>(S, cur, na, n, 0);
+      tC = GS_T();
+      // dups probe, one thread per segment
+      for (uint32_t s = threadIdx.x; s < na; s += LS_BLOCK) {
+        uint32_t b, c;
+        S.prot[s] = seq_probe<SH>(S.D(), S.lo[cur][s], S.hi[cur][s], S.m[s], S.bnd[s], &b, &c);
+        S.b[s] = (uint16_t)b;
+        S.c[s] = (uint16_t)c;
+        S.cnt[s] = 0;
+        if (S.prot[s]) S.anyprot = 1;
+      }
+      __syncthreads();
+      tD = GS_T();
+      if (S.anyprot) ls_partition<SH, E>(S, cur, na, n, 1);
+      tE = GS_T();
+      // pivot into the middle; children: terminal ones finish now, the others stay active in order
+      const uint32_t per = (na + LS_BLOCK - 1) / LS_BLOCK;
+      const uint32_t s0 = threadIdx.x * per, s1 = min(na, s0 + per);
+      uint32_t cntA = 0;
+      for (uint32_t s = s0; s < s1; s++) {
+        const uint32_t lo = S.lo[cur][s], hi = S.hi[cur][s];
+        const uint32_t b = S.prot[s] ? S.bnd[s] : S.b[s];
+        const uint32_t mlo = b - 1, mhi = S.c[s];
+        const int32_t dep = S.dep[cur][s] - 1;
+        swp(S.D(), lo, b - 1);
+        S.b[s] = (uint16_t)mlo;  // reuse: child boundaries
+        if (mlo - lo > 12 && dep > 0) cntA++;
+        else seq_terminal<SH>(S.D(), lo, mlo, dep);
+        if (hi - mhi > 12 && dep > 0) cntA++;
+        else seq_terminal<SH>(S.D(), mhi, hi, dep);
+      }
+      uint32_t tot;
+      uint32_t o = block_excl_scan<LS_BLOCK>(cntA, S.red, &tot);
+      const int nx = cur ^ 1;
+      for (uint32_t s = s0; s < s1; s++) {
+        const uint32_t lo = S.lo[cur][s], hi = S.hi[cur][s];
+        const uint32_t mlo = S.b[s], mhi = S.c[s];
+        const int32_t dep = S.dep[cur][s] - 1;
+        if (mlo - lo > 12 && dep > 0) {
+          S.lo[nx][o] = (uint16_t)lo;
+          S.hi[nx][o] = (uint16_t)mlo;
+          S.dep[nx][o] = (int8_t)dep;
+          o++;
+        }
+        if (hi - mhi > 12 && dep > 0) {
+          S.lo[nx][o] = (uint16_t)mhi;
+          S.hi[nx][o] = (uint16_t)hi;
+          S.dep[nx][o] = (int8_t)dep;
+          o++;
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) S.na = tot;
+      cur = nx;
+      __syncthreads();
+      tF = GS_T();
+      if (threadIdx.x == 0) {
+        GS_STAT_ADD(3, tB - tA);
+        GS_STAT_ADD(4, tC - tB);
+        GS_STAT_ADD(5, tD - tC);
+        GS_STAT_ADD(6, tE - tD);
+        GS_STAT_ADD(7, tF - tE);
+      }
+    }
+    if (threadIdx.x == 0) GS_STAT_ADD(2, GS_T() - tS);
+    constexpr E MASK = (E)((1ull << SH) - 1);
+    for (uint32_t i = threadIdx.x; i < n; i += LS_BLOCK) perm[pk.plo + i] = pk.plo + (uint32_t)(S.D()[i] & MASK);
+    __syncthreads();
   }
 }
 
-__global__ __launch_bounds__(GS_BLOCK) void k_gs_level(uint64_t* __restrict__ el, uint32_t* __restrict__ tmpA,
-                                                       uint32_t* __restrict__ tmpB, const Seg* segs,
-                                                       uint32_t nsegs, uint32_t* cnt, Seg* big, Seg* lds,
-                                                       Seg* heap) {
-  __shared__ uint32_t red[GS_BLOCK / 64 + 1];
-  __shared__ uint32_t sh[8];
-  for (uint32_t si = blockIdx.x; si < nsegs; si += gridDim.x) {
-    const Seg sg = segs[si];
-    uint32_t mlo, mhi;
-    block_dopivot<32>(el, tmpA, tmpB, sg.lo, sg.hi, red, sh, &mlo, &mhi);
+// =====================================================================================================
+// Global levels: segments larger than T_SEG, in place in el[] (HBM / L2).
+// =====================================================================================================
+struct GLvl {
+  uint32_t pl, m, cnt, bnd, b, c, prot, ng;
+};
+
+struct GCtl {
+  uint32_t nnext, nlds, nheap, pad;
+};
+
+// Per-level state, double-buffered: level L reads buffer L&1 and its finish kernel writes the
+// children (segments, their pivots, their tiles) into buffer (L+1)&1, so the host never waits
+// between levels. Tiles are reserved with atomics; a tile only needs its (segment, tile) pair.
+struct GPlan {
+  uint32_t nseg, ntiles;
+};
+
+struct GLevel {
+  Seg* segs;
+  GLvl* lv;
+  uint32_t* toff;
+  uint2* tseg;
+  GPlan* plan;
+};
+
+// one wave per segment: reserve tiles, write the tile list, choose the pivot
+__device__ __forceinline__ void gl_admit(uint64_t* el, const Seg& sg, uint32_t idx, GLevel nx) {
+  const uint32_t nt = (sg.hi - sg.lo + GL_TILE - 1) / GL_TILE;
+  uint32_t t0 = 0;
+  if (__lane_id() == 0) t0 = atomicAdd(&nx.plan->ntiles, nt);
+  t0 = __shfl(t0, 0);
+  for (uint32_t t = __lane_id(); t < nt; t += 64) nx.tseg[t0 + t] = make_uint2(idx, t);
+  const uint32_t m = wave_pivot<32>(el, sg.lo, sg.hi);
+  wave_sync();
+  if (__lane_id() == 0) {
+    nx.segs[idx] = sg;
+    nx.toff[idx] = t0;
+    GLvl L{};
+    L.m = m;
+    L.pl = KEY<32>(el[sg.lo]);
+    nx.lv[idx] = L;
+  }
+}
+
+// initial level: the big call groups
+__global__ __launch_bounds__(64) void k_gl_init(uint64_t* el, const Seg* big, uint32_t nbig, GLevel nx) {
+  for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
+    uint32_t idx = 0;
+    if (__lane_id() == 0) idx = atomicAdd(&nx.plan->nseg, 1u);
+    idx = __shfl(idx, 0);
+    gl_admit(el, big[i], idx, nx);
+  }
+}
+
+// the range and the "stays left" predicate of a pass
+__device__ __forceinline__ bool gl_range(const Seg& sg, const GLvl& L, int mode, uint32_t* a, uint32_t* e) {
+  if (mode == 1 && !L.prot) return false;
+  *a = sg.lo + 1;
+  *e = mode == 0 ? sg.hi - 1 : L.b;
+  return *a < *e;
+}
+__device__ __forceinline__ bool gl_left(uint32_t k, uint32_t pl, int mode) { return mode == 0 ? k >= pl : k > pl; }
+
+__global__ __launch_bounds__(GL_BLOCK) void k_gl_count(const uint64_t* el, const Seg* segs, const GPlan* plan,
+                                                       const uint2* tseg, GLvl* lv, int mode, GPlan* next_plan) {
+  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
+  if (next_plan && blockIdx.x == 0 && threadIdx.x == 0) *next_plan = GPlan{0, 0};  // free since level L-1
+  for (uint32_t tb = blockIdx.x; tb < plan->ntiles; tb += gridDim.x) {
+    const uint2 st = tseg[tb];
+    const Seg sg = segs[st.x];
+    const GLvl L = lv[st.x];
+    uint32_t a, e;
+    if (!gl_range(sg, L, mode, &a, &e)) continue;  // uniform per block
+    const uint32_t t0 = sg.lo + st.y * GL_TILE;
+    uint32_t c = 0;
+#pragma unroll 4
+    for (int i = 0; i < GL_ITEMS; i++) {
+      const uint32_t p = t0 + i * GL_BLOCK + threadIdx.x;
+      if (p >= a && p < e) c += gl_left(KEY<32>(el[p]), L.pl, mode) ? 1u : 0u;
+    }
+    c = block_sum<GL_BLOCK>(c, red);
+    if (threadIdx.x == 0 && c) atomicAdd(&lv[st.x].cnt, c);
+  }
+}
+
+// class of position p: 1 misplaced-left, 2 misplaced-right
+__device__ __forceinline__ uint32_t gl_cls(uint64_t v, uint32_t p, uint32_t a, uint32_t e, uint32_t bd, uint32_t pl,
+                                           int mode) {
+  if (p < a || p >= e) return 0;
+  const bool left = gl_left(KEY<32>(v), pl, mode);
+  if (p < bd) return left ? 0 : 1;
+  return left ? 2 : 0;
+}
+
+// Tile of 4096 elements staged in LDS with coalesced loads; thread t owns the run [16t, 16t+16).
+__device__ __forceinline__ void gl_stage(const uint64_t* el, uint32_t t0, uint32_t hi, uint64_t* tile) {
+  for (uint32_t i = threadIdx.x; i < GL_TILE; i += GL_BLOCK) {
+    const uint32_t p = t0 + i;
+    tile[i + (i >> 4)] = p < hi ? el[p] : 0;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(GL_BLOCK) void k_gl_tiles(const uint64_t* el, const Seg* segs, const GPlan* plan,
+                                                       const uint2* tseg, const uint32_t* toff, GLvl* lv,
+                                                       uint64_t* tcnt, int mode) {
+  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
+  __shared__ uint64_t tile[GL_TILE + GL_TILE / 16];
+  for (uint32_t tb = blockIdx.x; tb < plan->ntiles; tb += gridDim.x) {
+    const uint2 st = tseg[tb];
+    const Seg sg = segs[st.x];
+    const GLvl L = lv[st.x];
+    uint32_t a, e;
+    if (!gl_range(sg, L, mode, &a, &e)) continue;
+    const uint32_t bd = a + L.cnt;
+    const uint32_t t0 = sg.lo + st.y * GL_TILE;
+    gl_stage(el, t0, sg.hi, tile);
+    const uint32_t r0 = threadIdx.x * GL_ITEMS;
+    uint32_t packed = 0;
+    for (int i = 0; i < GL_ITEMS; i++) {
+      const uint32_t f = gl_cls(tile[r0 + i + (r0 >> 4)], t0 + r0 + i, a, e, bd, L.pl, mode);
+      packed += f == 1 ? 1u : (f == 2 ? 0x10000u : 0u);
+    }
+    packed = block_sum<GL_BLOCK>(packed, red);  // per tile < 2^16 per half
     if (threadIdx.x == 0) {
-      route(Seg{sg.lo, mlo, sg.depth - 1, 0}, cnt, big, lds, heap);
-      route(Seg{mhi, sg.hi, sg.depth - 1, 0}, cnt, big, lds, heap);
+      tcnt[tb] = (uint64_t)(packed & 0xFFFF) | ((uint64_t)(packed >> 16) << 32);
+      if (st.y == 0) lv[st.x].bnd = bd;
     }
     __syncthreads();
   }
 }
 
-// LDS kernel: one workgroup per segment of at most T_LDS elements, sorted to completion.
-__global__ __launch_bounds__(GS_BLOCK) void k_gs_lds(uint64_t* __restrict__ el, uint32_t* __restrict__ perm,
-                                                     const Seg* segs, uint32_t nsegs, uint32_t* cnt,
-                                                     Seg* heap) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  GsLds& L = *reinterpret_cast<GsLds*>(smem);
-  for (uint32_t si = blockIdx.x; si < nsegs; si += gridDim.x) {
-    const Seg sg = segs[si];
-    const bool ok = lds_sort(el, perm, sg.lo, sg.hi - sg.lo, sg.depth, L);
-    if (!ok && threadIdx.x == 0) heap[atomicAdd(&cnt[3], 1u)] = sg;  // lengths >= 2^18: HBM path
+__global__ __launch_bounds__(GL_BLOCK) void k_gl_lists(const uint64_t* el, const Seg* segs, const GPlan* plan,
+                                                       const uint2* tseg, const uint32_t* toff, GLvl* lv,
+                                                       const uint64_t* tcnt, uint32_t* A, uint32_t* B, int mode) {
+  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
+  __shared__ uint64_t tbase;
+  __shared__ uint64_t tile[GL_TILE + GL_TILE / 16];
+  for (uint32_t tb = blockIdx.x; tb < plan->ntiles; tb += gridDim.x) {
+    const uint2 st = tseg[tb];
+    const Seg sg = segs[st.x];
+    const GLvl L = lv[st.x];
+    uint32_t a, e;
+    if (!gl_range(sg, L, mode, &a, &e)) continue;
+    const uint32_t t0 = sg.lo + st.y * GL_TILE;
+    const uint32_t ntile = (sg.hi - sg.lo + GL_TILE - 1) / GL_TILE;
+    const uint32_t first = toff[st.x];
+    if (threadIdx.x < 64) {  // prefix of the earlier tiles of this segment (and the total, last tile)
+      uint64_t acc = 0;
+      for (uint32_t t = __lane_id(); t < st.y; t += 64) acc += tcnt[first + t];
+      acc = wave_sum(acc);
+      if (threadIdx.x == 0) {
+        tbase = acc;
+        if (st.y == ntile - 1) lv[st.x].ng = (uint32_t)(acc + tcnt[tb]);
+      }
+    }
+    gl_stage(el, t0, sg.hi, tile);
+    const uint32_t bd = L.bnd;
+    const uint32_t r0 = threadIdx.x * GL_ITEMS;
+    uint32_t cls[GL_ITEMS];
+    uint32_t packed = 0;
+    for (int i = 0; i < GL_ITEMS; i++) {
+      cls[i] = gl_cls(tile[r0 + i + (r0 >> 4)], t0 + r0 + i, a, e, bd, L.pl, mode);
+      packed += cls[i] == 1 ? 1u : (cls[i] == 2 ? 0x10000u : 0u);
+    }
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<GL_BLOCK>(packed, red, &tot);  // in-tile ranks < 2^16 per half
+    uint32_t rl = (pre & 0xFFFF) + (uint32_t)tbase, rr = (pre >> 16) + (uint32_t)(tbase >> 32);
+    for (int i = 0; i < GL_ITEMS; i++) {
+      if (cls[i] == 1) A[sg.lo + rl++] = t0 + r0 + i;
+      if (cls[i] == 2) B[sg.lo + rr++] = t0 + r0 + i;
+    }
     __syncthreads();
   }
 }
 
-// Fallbacks in HBM: depth-exhausted heapSort (one thread per segment), and segments whose lengths do
-// not fit the packed LDS format (quickSort by one workgroup, sequentially with cached pivots).
-__global__ void k_gs_heap(uint64_t* el, const Seg* segs, uint32_t nsegs) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nsegs; i += gridDim.x * blockDim.x)
+// tile t of a segment swaps pairs k in [t*TILE/2, (t+1)*TILE/2) (ng <= len/2 <= ntile*TILE/2)
+__global__ __launch_bounds__(GL_BLOCK) void k_gl_swap(uint64_t* el, const Seg* segs, const GPlan* plan,
+                                                      const uint2* tseg, const GLvl* lv, const uint32_t* A,
+                                                      const uint32_t* B, int mode) {
+  for (uint32_t tb = blockIdx.x; tb < plan->ntiles; tb += gridDim.x) {
+    const uint2 st = tseg[tb];
+    const Seg sg = segs[st.x];
+    const GLvl L = lv[st.x];
+    if (mode == 1 && !L.prot) continue;
+    const uint32_t ng = L.ng;
+    const uint32_t k0 = st.y * (GL_TILE / 2), k1 = min(ng, k0 + GL_TILE / 2);
+    for (uint32_t k = k0 + threadIdx.x; k < k1; k += GL_BLOCK) swp(el, A[sg.lo + k], B[sg.lo + ng - 1 - k]);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_gl_probe(uint64_t* el, const Seg* segs, const GPlan* plan, GLvl* lv) {
+  for (uint32_t s = blockIdx.x; s < plan->nseg; s += gridDim.x) {
+    const Seg sg = segs[s];
+    GLvl L = lv[s];
+    uint32_t b, c;
+    L.prot = wave_probe<32>(el, sg.lo, sg.hi, L.m, L.bnd, &b, &c);
+    if (__lane_id() == 0) {
+      L.b = b;
+      L.c = c;
+      L.cnt = 0;
+      L.ng = 0;
+      lv[s] = L;
+    }
+  }
+}
+
+// one wave per segment: pivot into the middle, route the children; children that stay in the
+// global levels are admitted to the next level right here (tiles + pivot choice).
+__global__ __launch_bounds__(64) void k_gl_finish(uint64_t* el, GLevel cur, GLevel nx, GCtl* ctl, Seg* lds,
+                                                  Seg* heap) {
+  for (uint32_t s = blockIdx.x; s < cur.plan->nseg; s += gridDim.x) {
+    const Seg sg = cur.segs[s];
+    const GLvl L = cur.lv[s];
+    const uint32_t b = L.prot ? L.bnd : L.b;
+    if (__lane_id() == 0) swp(el, sg.lo, b - 1);
+    wave_sync();
+    const int32_t dep = sg.depth - 1;
+    const Seg ch[2] = {Seg{sg.lo, b - 1, dep, 0}, Seg{L.c, sg.hi, dep, 0}};
+    for (int k = 0; k < 2; k++) {
+      const uint32_t len = ch[k].hi - ch[k].lo;
+      if (len <= 1) continue;
+      if (len <= T_SEG) {
+        if (__lane_id() == 0) lds[atomicAdd(&ctl->nlds, 1u)] = ch[k];
+      } else if (dep == 0) {
+        if (__lane_id() == 0) heap[atomicAdd(&ctl->nheap, 1u)] = ch[k];
+      } else {
+        uint32_t idx = 0;
+        if (__lane_id() == 0) idx = atomicAdd(&nx.plan->nseg, 1u);
+        idx = __shfl(idx, 0);
+        gl_admit(el, ch[k], idx, nx);
+      }
+    }
+  }
+}
+
+__global__ void k_gs_heap(uint64_t* el, const Seg* segs, const uint32_t* nsegs) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < *nsegs; i += gridDim.x * blockDim.x)
     heap_sort<32>(el, segs[i].lo, segs[i].hi);
 }
 
-__global__ __launch_bounds__(GS_BLOCK) void k_gs_wide(uint64_t* __restrict__ el, uint32_t* __restrict__ tmpA,
-                                                      uint32_t* __restrict__ tmpB, const Seg* segs,
-                                                      uint32_t nsegs) {
-  __shared__ uint32_t red[GS_BLOCK / 64 + 1];
-  __shared__ uint32_t sh[8];
-  __shared__ uint32_t stk[3 * 256];
-  __shared__ uint32_t sp;
-  for (uint32_t si = blockIdx.x; si < nsegs; si += gridDim.x) {
-    if (threadIdx.x == 0) {
-      stk[0] = segs[si].lo;
-      stk[1] = segs[si].hi;
-      stk[2] = (uint32_t)segs[si].depth;
-      sp = 1;
-    }
-    __syncthreads();
-    while (sp > 0) {
-      const uint32_t a = stk[3 * (sp - 1)], b = stk[3 * (sp - 1) + 1];
-      const int32_t dep = (int32_t)stk[3 * (sp - 1) + 2];
-      __syncthreads();
-      if (threadIdx.x == 0) sp--;
-      if (b - a <= 12) {
-        if (b - a > 1 && threadIdx.x < 64) wave_leaf<32>(el, a, b);
-      } else if (dep == 0) {
-        if (threadIdx.x == 0) heap_sort<32>(el, a, b);
-      } else {
-        uint32_t mlo, mhi;
-        block_dopivot<32>(el, tmpA, tmpB, a, b, red, sh, &mlo, &mhi);
-        if (threadIdx.x == 0) {
-          stk[3 * sp] = a;
-          stk[3 * sp + 1] = mlo;
-          stk[3 * sp + 2] = (uint32_t)(dep - 1);
-          stk[3 * sp + 3] = mhi;
-          stk[3 * sp + 4] = b;
-          stk[3 * sp + 5] = (uint32_t)(dep - 1);
-          sp += 2;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-__global__ void k_gs_init(const uint64_t* gstart, uint32_t ngroups, uint32_t* perm, size_t n, uint32_t* cnt,
-                          Seg* big, Seg* lds, Seg* heap) {
+__global__ void k_gs_init(uint32_t* perm, size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     perm[i] = (uint32_t)i;
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += gridDim.x * blockDim.x) {
-    const uint32_t lo = (uint32_t)gstart[g], hi = (uint32_t)gstart[g + 1];
-    uint32_t depth = 0;
-    for (uint32_t i = hi - lo; i > 0; i >>= 1) depth++;  // maxDepth = 2*ceil(lg(n+1))
-    route(Seg{lo, hi, (int32_t)(2 * depth), 0}, cnt, big, lds, heap);
-  }
 }
 
-// Sorts every group's [gstart[g], gstart[g+1]) range with Go's sort.Sort semantics.
-// Result: the element at sorted position r is el[perm[r]].
-void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const uint64_t* gstart_dev, uint32_t ngroups,
-                   hipStream_t s) {
-  Context& c = ctx();
-  const size_t maxseg = n / 2 + ngroups + 16;
-  Seg* bigA = c.scratch.get<Seg>("gs_bigA", maxseg);
-  Seg* bigB = c.scratch.get<Seg>("gs_bigB", maxseg);
-  Seg* lds = c.scratch.get<Seg>("gs_lds", maxseg);
-  Seg* heap = c.scratch.get<Seg>("gs_heap", maxseg);
-  Seg* wide = c.scratch.get<Seg>("gs_wide", maxseg);
-  uint32_t* tmpA = c.scratch.get<uint32_t>("gs_tmpA", n + 1);
-  uint32_t* tmpB = c.scratch.get<uint32_t>("gs_tmpB", n + 1);
-  uint32_t* cnt = c.scratch.get<uint32_t>("gs_cnt", 8);  // big, lds, heap, wide
-  uint32_t* hcnt = c.pinned.get<uint32_t>(8);
-  static bool attr_set = false;
-  if (!attr_set) {
-    SYZ_HIP(hipFuncSetAttribute((const void*)k_gs_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(GsLds)));
-    attr_set = true;
+// dynamic LDS segments (children of global levels): one pack per segment
+__global__ void k_dyn_packs(const Seg* segs, const uint32_t* n, Pack* packs) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < *n; i += gridDim.x * blockDim.x)
+    packs[i] = Pack{segs[i].lo, segs[i].hi, i, i + 1};
+}
+
+// ---- host driver -------------------------------------------------------------------------------------
+template <int SH, class E>
+static void launch_ls(const uint64_t* el, uint32_t* perm, const Pack* packs, uint32_t npacks_host,
+                      const uint32_t* npacks_dev, unsigned grid, const Seg* segs, uint32_t* bounce_cnt, Pack* bounce,
+                      hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    SYZ_HIP(hipFuncSetAttribute((const void*)k_ls_sort<SH, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(LsLds<E>)));
+    attr = true;
   }
-  SYZ_HIP(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), s));
+  if (grid == 0) return;
+  k_ls_sort<SH, E><<<grid, LS_BLOCK, sizeof(LsLds<E>), s>>>(el, perm, packs, npacks_host, npacks_dev, segs,
+                                                            bounce_cnt, bounce);
+  SYZ_LAUNCHED();
+}
+
+// The static part of a sort over fixed call-group boundaries: which groups start the global levels,
+// and how the small ones are packed for the LDS sorter. Built once per corpus layout.
+GosortPlan::~GosortPlan() {
+  if (small) (void)hipFree(small);
+  if (packs) (void)hipFree(packs);
+  if (big) (void)hipFree(big);
+}
+
+void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ngroups, hipStream_t s) {
+  std::vector<Seg> big, small;
+  std::vector<Pack> packs;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    const uint32_t lo = (uint32_t)hstart[g], hi = (uint32_t)hstart[g + 1];
+    if (hi - lo <= 1) continue;
+    const Seg sg{lo, hi, go_max_depth(hi - lo), 0};
+    if (hi - lo > T_SEG) {
+      big.push_back(sg);
+      continue;
+    }
+    if (packs.empty() || hi - packs.back().plo > T_SEG) {
+      packs.push_back(Pack{lo, hi, (uint32_t)small.size(), (uint32_t)small.size() + 1});
+    } else {
+      packs.back().phi = hi;
+      packs.back().send++;
+    }
+    small.push_back(sg);
+  }
+  P.n = hstart[ngroups];
+  P.nsmall = (uint32_t)small.size();
+  P.npacks = (uint32_t)packs.size();
+  P.nbig = (uint32_t)big.size();
+  P.big_total = 0;
+  for (const Seg& sg : big) P.big_total += sg.hi - sg.lo;
+  SYZ_HIP(hipMalloc(&P.small, (small.size() + 1) * sizeof(Seg)));
+  SYZ_HIP(hipMalloc(&P.packs, (packs.size() + 1) * sizeof(Pack)));
+  SYZ_HIP(hipMalloc(&P.big, (big.size() + 1) * sizeof(Seg)));
+  if (!small.empty()) SYZ_HIP(hipMemcpy(P.small, small.data(), small.size() * sizeof(Seg), hipMemcpyHostToDevice));
+  if (!packs.empty()) SYZ_HIP(hipMemcpy(P.packs, packs.data(), packs.size() * sizeof(Pack), hipMemcpyHostToDevice));
+  if (!big.empty()) SYZ_HIP(hipMemcpy(P.big, big.data(), big.size() * sizeof(Seg), hipMemcpyHostToDevice));
+  (void)s;
+}
+
+void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const std::vector<uint64_t>& hstart, uint32_t ngroups,
+                   hipStream_t s) {
+  GosortPlan P;
+  gosort_plan(P, hstart, ngroups, s);
+  gosort_run(el, perm, n, P, s);
+  SYZ_HIP(hipStreamSynchronize(s));  // P's device arrays are freed on return
+}
+
+// Sorts every call group's range (as planned in P) with Go's sort.Sort semantics. Result: the element
+// at sorted position r is el[perm[r]]. Enqueues everything on s; the host only waits for the
+// level-count events of the global levels.
+void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hipStream_t s) {
+  Context& c = ctx();
+  Scratch& sc = c.scratch;
+  if (n >= 0xFFFFFFF0ull || n != P.n) fail(SYZGPU_EINVAL, "gosort: plan does not match the elements");
+  const size_t maxseg = n / (T_SEG / 2) + (size_t)P.nbig * 2 + 16;
+  const size_t maxlds = n / 2 + 16;
+  const Seg* d_small = P.small;
+  const Pack* d_packs = P.packs;
+  Seg* dlds = sc.get<Seg>("gs_lds", maxlds);
+  Pack* dpacks = sc.get<Pack>("gs_dpacks", maxlds);
+  Seg* heap = sc.get<Seg>("gs_heap", maxseg);
+  Pack* bounceS = sc.get<Pack>("gs_bounceS", (size_t)P.npacks + 1);
+  Pack* bounceD = sc.get<Pack>("gs_bounceD", maxlds);
+  uint32_t* A = sc.get<uint32_t>("gs_A", n + 1);
+  uint32_t* B = sc.get<uint32_t>("gs_B", n + 1);
+  // ctl[0]: next-level count (reset by each plan) and the accumulated LDS / heap children;
+  // ctl[2]: bounce counters of the static (nnext) and dynamic (nlds) LDS launches; ctl[3]: scratch
+  GCtl* ctl = sc.get<GCtl>("gs_ctl", 4);
+  char* pin = c.pinned.get<char>(1024);
+  GCtl* hctl = reinterpret_cast<GCtl*>(pin);
+  uint32_t* hn = reinterpret_cast<uint32_t*>(pin + 256);
+  SYZ_HIP(hipMemsetAsync(ctl, 0, 4 * sizeof(GCtl), s));
   {
     ProfScope ps("gosort_init", s, (uint64_t)n * 4);
-    k_gs_init<<<grid_for(std::max<size_t>(n, ngroups), 256, 2048), 256, 0, s>>>(gstart_dev, ngroups, perm, n, cnt,
-                                                                                bigA, lds, heap);
+    k_gs_init<<<grid_for(n, 256, 4096), 256, 0, s>>>(perm, n);
     SYZ_LAUNCHED();
   }
-  SYZ_HIP(hipMemcpyAsync(hcnt, cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  // levels of segments larger than T_LDS (only the biggest call groups have any)
-  for (int level = 0; hcnt[0] > 0; level++) {
-    const uint32_t nbig = hcnt[0];
-    SYZ_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), s));
-    {
-      ProfScope ps("gosort_level", s, 0);
-      k_gs_level<<<std::min<uint32_t>(nbig, 2048), GS_BLOCK, 0, s>>>(el, tmpA, tmpB, bigA, nbig, cnt, bigB, lds,
-                                                                     heap);
-      SYZ_LAUNCHED();
+  // the small call groups (packed) are independent of the big ones: sort them on the side stream
+  // while the main stream runs the global levels
+  if (!c.side) {
+    SYZ_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
+  }
+  const bool fork = P.npacks && P.nbig;
+  hipStream_t ss = fork ? c.side : s;
+  if (P.npacks) {
+    if (fork) {
+      SYZ_HIP(hipEventRecord(c.ev_fork, s));
+      SYZ_HIP(hipStreamWaitEvent(ss, c.ev_fork, 0));
     }
-    std::swap(bigA, bigB);
-    SYZ_HIP(hipMemcpyAsync(hcnt, cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
-    if (level > 256) fail(SYZGPU_EINTERNAL, "gosort: level limit");
+    ProfScope ps("gosort_lds_small", ss, (uint64_t)n * 12);
+    launch_ls<LS_SH, uint32_t>(el, perm, d_packs, P.npacks, nullptr, std::min<uint32_t>(P.npacks, 65535), d_small,
+                            &ctl[2].nnext, bounceS, ss);
   }
-  const uint32_t nlds = hcnt[1], nheap = hcnt[2];
-  if (nheap) {
-    k_gs_heap<<<grid_for(nheap, 64, 4096), 64, 0, s>>>(el, heap, nheap);
-    SYZ_LAUNCHED();
-  }
-  if (nlds) {
-    ProfScope ps("gosort_lds", s, (uint64_t)n * 12);
-    SYZ_HIP(hipMemsetAsync(cnt + 3, 0, sizeof(uint32_t), s));
-    k_gs_lds<<<std::min<uint32_t>(nlds, 4096), GS_BLOCK, sizeof(GsLds), s>>>(el, perm, lds, nlds, cnt, wide);
-    SYZ_LAUNCHED();
-    SYZ_HIP(hipMemcpyAsync(hcnt + 3, cnt + 3, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
-    if (hcnt[3]) {  // lengths beyond the packed LDS format: sort those segments in HBM
-      k_gs_wide<<<std::min<uint32_t>(hcnt[3], 2048), GS_BLOCK, 0, s>>>(el, tmpA, tmpB, wide, hcnt[3]);
-      SYZ_LAUNCHED();
+  if (fork) SYZ_HIP(hipEventRecord(c.ev_join, ss));
+  // global levels: the host issues level after level without waiting; each level's segment count is
+  // copied back asynchronously and the host stops issuing once a finished level reports zero
+  // (levels issued after the last real one find nseg == 0 and return at once).
+  if (P.nbig) {
+    const uint32_t nbig = P.nbig;
+    const size_t max_tiles = n / GL_TILE + maxseg + 1;
+    uint64_t* tcnt = sc.get<uint64_t>("gs_tcnt", max_tiles);
+    GLevel lvl[2];
+    for (int p = 0; p < 2; p++) {
+      const std::string k = std::to_string(p);
+      lvl[p].segs = sc.get<Seg>("gs_seg" + k, maxseg);
+      lvl[p].lv = sc.get<GLvl>("gs_lv" + k, maxseg);
+      lvl[p].toff = sc.get<uint32_t>("gs_toff" + k, maxseg);
+      lvl[p].tseg = sc.get<uint2>("gs_tseg" + k, max_tiles);
+      lvl[p].plan = sc.get<GPlan>("gs_plan" + k, 1);
     }
+    constexpr int MAXLV = 64;
+    uint32_t* hhist = hn + 4;  // pinned, per-level counts
+    std::vector<hipEvent_t>& ev = c.gs_events;
+    while (ev.size() < (size_t)MAXLV) {
+      hipEvent_t e;
+      SYZ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev.push_back(e);
+    }
+    // grids sized to what the big groups can ever need (their elements only shrink level by level):
+    // idle workgroups of a grid-stride kernel still cost dispatch time on every one of the ~10
+    // dependent launches of a level
+    const size_t segs_max = P.big_total / T_SEG + P.nbig + 1;
+    const unsigned tgrid = (unsigned)std::min<size_t>(P.big_total / GL_TILE + segs_max, 2048);
+    const unsigned wgrid = (unsigned)std::min<size_t>(segs_max, 1024);  // one wave per segment
+    int issued = 0, checked = 0;
+    bool done = false;
+    ProfScope ps("gosort_level", s, 0);
+    SYZ_HIP(hipMemsetAsync(lvl[0].plan, 0, sizeof(GPlan), s));
+    k_gl_init<<<std::min<uint32_t>(nbig, 1024), 64, 0, s>>>(el, P.big, nbig, lvl[0]);
+    SYZ_LAUNCHED();
+    // one level = 10 dependent kernels with fixed arguments per buffer parity: both parities are
+    // captured once into HIP graphs and replayed, so a level costs one graph launch on the host
+    auto enqueue_level = [&](hipStream_t q, int parity) {
+      const GLevel cur = lvl[parity], nx = lvl[parity ^ 1];
+      for (int mode = 0; mode < 2; mode++) {
+        k_gl_count<<<tgrid, GL_BLOCK, 0, q>>>(el, cur.segs, cur.plan, cur.tseg, cur.lv, mode,
+                                              mode == 0 ? nx.plan : nullptr);
+        SYZ_LAUNCHED();
+        k_gl_tiles<<<tgrid, GL_BLOCK, 0, q>>>(el, cur.segs, cur.plan, cur.tseg, cur.toff, cur.lv, tcnt, mode);
+        SYZ_LAUNCHED();
+        k_gl_lists<<<tgrid, GL_BLOCK, 0, q>>>(el, cur.segs, cur.plan, cur.tseg, cur.toff, cur.lv, tcnt, A, B, mode);
+        SYZ_LAUNCHED();
+        k_gl_swap<<<tgrid, GL_BLOCK, 0, q>>>(el, cur.segs, cur.plan, cur.tseg, cur.lv, A, B, mode);
+        SYZ_LAUNCHED();
+        if (mode == 0) {
+          k_gl_probe<<<wgrid, 64, 0, q>>>(el, cur.segs, cur.plan, cur.lv);
+          SYZ_LAUNCHED();
+        }
+      }
+      k_gl_finish<<<wgrid, 64, 0, q>>>(el, cur, nx, &ctl[0], dlds, heap);
+      SYZ_LAUNCHED();
+    };
+    const std::vector<const void*> key = {el,        tcnt,          A,           B,           ctl,
+                                          dlds,      heap,          lvl[0].segs, lvl[0].lv,   lvl[0].toff,
+                                          lvl[0].tseg, lvl[0].plan, lvl[1].segs, lvl[1].lv,   lvl[1].toff,
+                                          lvl[1].tseg, lvl[1].plan, (const void*)(uintptr_t)tgrid,
+                                          (const void*)(uintptr_t)wgrid};
+    if (c.gl_key != key) {
+      for (int p = 0; p < 2; p++) {
+        if (c.gl_exec[p]) SYZ_HIP(hipGraphExecDestroy(c.gl_exec[p]));
+        c.gl_exec[p] = nullptr;
+      }
+      if (!c.cap) SYZ_HIP(hipStreamCreateWithFlags(&c.cap, hipStreamNonBlocking));
+      for (int p = 0; p < 2; p++) {
+        hipGraph_t g;
+        SYZ_HIP(hipStreamBeginCapture(c.cap, hipStreamCaptureModeThreadLocal));
+        enqueue_level(c.cap, p);
+        SYZ_HIP(hipStreamEndCapture(c.cap, &g));
+        SYZ_HIP(hipGraphInstantiate(&c.gl_exec[p], g, nullptr, nullptr, 0));
+        SYZ_HIP(hipGraphDestroy(g));
+      }
+      c.gl_key = key;
+    }
+    while (!done) {
+      if (issued >= MAXLV) fail(SYZGPU_EINTERNAL, "gosort: level limit");
+      const GLevel nx = lvl[(issued + 1) & 1];
+      SYZ_HIP(hipGraphLaunch(c.gl_exec[issued & 1], s));
+      SYZ_HIP(hipMemcpyAsync(hhist + issued, &nx.plan->nseg, 4, hipMemcpyDeviceToHost, s));
+      SYZ_HIP(hipEventRecord(ev[issued], s));
+      issued++;
+      // keep at most one level in flight ahead of the one whose count we wait for (a level issued
+      // past the last real one still costs ~10 near-empty launches)
+      while (checked < issued) {
+        const bool must = issued - checked > 1;
+        if (!must && hipEventQuery(ev[checked]) != hipSuccess) break;
+        SYZ_HIP(hipEventSynchronize(ev[checked]));
+        if (hhist[checked] == 0) {
+          done = true;
+          break;
+        }
+        checked++;
+      }
+    }
+    if (getenv("SYZGPU_GS_DEBUG")) {
+      SYZ_HIP(hipStreamSynchronize(s));
+      fprintf(stderr, "gosort: %d levels issued, segments per level:", issued);
+      for (int l = 0; l < issued; l++) fprintf(stderr, " %u", hhist[l]);
+      fprintf(stderr, "\n");
+    }
+    // children that reached the LDS size and depth-exhausted big ones: counts stay on the device
+    k_gs_heap<<<64, 64, 0, s>>>(el, heap, &ctl[0].nheap);
+    SYZ_LAUNCHED();
+    k_dyn_packs<<<256, 256, 0, s>>>(dlds, &ctl[0].nlds, dpacks);
+    SYZ_LAUNCHED();
+    ProfScope ps2("gosort_lds", s, (uint64_t)n * 12);
+    launch_ls<LS_SH, uint32_t>(el, perm, dpacks, 0, &ctl[0].nlds, 2048, dlds, &ctl[2].nlds, bounceD, s);
   }
+  if (fork) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
+  // packs with a length that does not fit the u32 element (>= 2^20 PCs) were bounced: the u64
+  // instantiation sorts them (a launch over an empty bounce list returns at once)
+  if (P.npacks)
+    launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, s);
+  if (P.nbig) launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nnext, bounceD, s);
 }
 
-}  // namespace syz
+#ifdef SYZ_GS_STATS
+extern "C" int syzgpu_debug_gosort_stats(unsigned long long* out, int reset) {
+  hipDeviceSynchronize();
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gs_stats), sizeof(unsigned long long) * 16);
+  if (reset) {
+    unsigned long long z[16] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_gs_stats), z, sizeof(z));
+  }
+  return 0;
+}
+#endif
 
-static_assert(sizeof(syz::GsLds) <= 160 * 1024, "gosort LDS budget");
+}  // namespace syz

@@ -321,6 +321,20 @@ __global__ void k_group_out_off(const uint64_t* pos, const uint64_t* gstart, uin
 
 // ---- host orchestration ------------------------------------------------------------------------------
 
+// syzgpu_minimize_order helpers: elements (len << 32) | index, output index within the group
+__global__ void k_order_el(const uint64_t* lens, size_t n, uint64_t* el) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    el[i] = (lens[i] << 32) | (uint64_t)i;
+}
+
+__global__ void k_order_out(const uint64_t* el, const uint32_t* perm, const uint64_t* goff, uint32_t G, size_t n,
+                            int64_t* out) {
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t g = (uint32_t)upper_bound_dev<uint64_t>(goff, 0, G + 1, r) - 1;
+    out[r] = (int64_t)(uint32_t)el[perm[r]] - (int64_t)goff[g];
+  }
+}
+
 struct MinState {
   uint64_t* gstart = nullptr;
   uint8_t* sel_rank = nullptr;
@@ -379,7 +393,7 @@ void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   if (*herr) fail(SYZGPU_EINVAL, "group id >= ngroups");
   std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
 
-  if (n) gosort_groups(el, perm, n, gstart, G, s);
+  if (n) gosort_groups(el, perm, n, hstart, G, s);
   {
     ProfScope ps("ranks", s, (uint64_t)n * 16);
     if (n) {
@@ -513,6 +527,39 @@ int syzgpu_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint
     if (n) SYZ_HIP(hipMemcpyAsync(dg, group, n * 4, hipMemcpyHostToDevice, s));
     minimize_grouped_dev(dp, doff, dg, nullptr, n, ngroups, 0, nullptr, nullptr, s);
     minimize_fetch(out_idx, group_out_off, n, ngroups, s);
+  })
+}
+
+int syzgpu_minimize_order(const uint64_t* lens, const uint64_t* group_off, uint32_t ngroups, int64_t* perm) {
+  SYZ_API_BODY({
+    if (!group_off || ngroups == 0) fail(SYZGPU_EINVAL, "null pointer / no groups");
+    if (group_off[0] != 0) fail(SYZGPU_EINVAL, "group offsets must start at 0");
+    const size_t n = group_off[ngroups];
+    if (n && (!lens || !perm)) fail(SYZGPU_EINVAL, "null pointer");
+    if (n >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many inputs");
+    for (uint32_t g = 0; g < ngroups; g++)
+      if (group_off[g + 1] < group_off[g]) fail(SYZGPU_EINVAL, "group offsets must be non-decreasing");
+    for (size_t i = 0; i < n; i++)
+      if (lens[i] >> 32) fail(SYZGPU_EINVAL, "cover length >= 2^32");
+    hipStream_t s = C_.stream;
+    Scratch& sc = C_.scratch;
+    uint64_t* dl = sc.get<uint64_t>("mo_lens", n + 1);
+    uint64_t* dgo = sc.get<uint64_t>("mo_goff", ngroups + 1);
+    uint64_t* el = sc.get<uint64_t>("mo_el", n + 1);
+    uint32_t* p = sc.get<uint32_t>("mo_perm", n + 1);
+    int64_t* out = sc.get<int64_t>("mo_out", n + 1);
+    if (n) SYZ_HIP(hipMemcpyAsync(dl, lens, n * 8, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(dgo, group_off, (ngroups + 1) * 8, hipMemcpyHostToDevice, s));
+    if (n) {
+      k_order_el<<<grid_for(n, 256, 4096), 256, 0, s>>>(dl, n, el);
+      SYZ_LAUNCHED();
+      std::vector<uint64_t> hs(group_off, group_off + ngroups + 1);
+      gosort_groups(el, p, n, hs, ngroups, s);
+      k_order_out<<<grid_for(n, 256, 4096), 256, 0, s>>>(el, p, dgo, ngroups, n, out);
+      SYZ_LAUNCHED();
+      SYZ_HIP(hipMemcpyAsync(perm, out, n * 8, hipMemcpyDeviceToHost, s));
+    }
+    SYZ_HIP(hipStreamSynchronize(s));
   })
 }
 
@@ -887,6 +934,9 @@ struct Corpus {
   DevArr<VecWork> work;
   DevArr<GtabInfo> gtinfo;
   std::vector<VecWork> hwork;
+  std::vector<uint64_t> hstart;
+  GosortPlan gsplan;
+  uint32_t max_prog_len = 0;
   uint32_t ngtabs = 0;
   ~Corpus() {
     off.free(); gstart.free(); gdict.free(); group.free(); members.free(); nwin.free(); dict.free();
@@ -1119,6 +1169,13 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   if (herr[0] & 4) fail(SYZGPU_EINTERNAL, "coverstore: hash bucket overflow");
+  K.hstart = hstart;
+  gosort_plan(K.gsplan, hstart, G, s);
+  if (n && prog_len) {  // len(p.Calls) > C is rejected per call without a device round trip
+    std::vector<uint16_t> hl(n);
+    SYZ_HIP(hipMemcpy(hl.data(), prog_len, n * 2, hipMemcpyDeviceToHost));
+    K.max_prog_len = *std::max_element(hl.begin(), hl.end());
+  }
   return cp.release();
 }
 
@@ -1126,6 +1183,8 @@ static Corpus* g_last_corpus = nullptr;
 
 void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s) {
   Context& c = ctx();
+  if (len_hist && (int64_t)K.max_prog_len > (int64_t)C)
+    fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
   Scratch& sc = c.scratch;
   const size_t n = K.n;
   const uint32_t G = K.G;
@@ -1147,7 +1206,7 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
       SYZ_LAUNCHED();
     }
   }
-  if (n) gosort_groups(el, perm, n, K.gstart.p, G, s);
+  if (n) gosort_run(el, perm, n, K.gsplan, s);
   {
     ProfScope ps("ranks", s, (uint64_t)n * 16);
     if (n) {
@@ -1176,12 +1235,6 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
           sel_bits, sel_rank, ent_of_rank, n, len_hist ? K.prog_len.p : nullptr, C, selected, len_hist, err);
       SYZ_LAUNCHED();
     }
-  }
-  if (len_hist) {
-    int* h = c.pinned.get<int>(4);
-    SYZ_HIP(hipMemcpyAsync(h, err, 8, hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
-    if (h[0] & 2) fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
   }
   g_min.gstart = K.gstart.p;
   g_min.sel_rank = sel_rank;

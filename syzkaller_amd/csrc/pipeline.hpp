@@ -11,7 +11,22 @@ struct Seg {
 };
 
 // gosort.hip: the element at sorted position r of the groups' ranges is el[perm[r]]
-void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const uint64_t* gstart_dev, uint32_t ngroups,
+struct Pack;
+struct GosortPlan {
+  size_t n = 0;
+  uint32_t nsmall = 0, npacks = 0, nbig = 0;
+  uint64_t big_total = 0;  // elements in the groups that start the global levels
+  Seg* small = nullptr;
+  Pack* packs = nullptr;
+  Seg* big = nullptr;
+  GosortPlan() = default;
+  GosortPlan(const GosortPlan&) = delete;
+  GosortPlan& operator=(const GosortPlan&) = delete;
+  ~GosortPlan();
+};
+void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ngroups, hipStream_t s);
+void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hipStream_t s);
+void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const std::vector<uint64_t>& hstart, uint32_t ngroups,
                    hipStream_t s);
 
 // setops.hip

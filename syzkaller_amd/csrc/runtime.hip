@@ -79,7 +79,7 @@ void Prof::reset() {
   used = 0;
 }
 
-void Prof::begin(const char* name, hipStream_t s, uint64_t bytes) {
+size_t Prof::begin(const char* name, hipStream_t s, uint64_t bytes) {
   if (used + 2 > pool.size()) {
     for (int i = 0; i < 64; i++) {
       hipEvent_t e;
@@ -91,9 +91,10 @@ void Prof::begin(const char* name, hipStream_t s, uint64_t bytes) {
   used += 2;
   SYZ_HIP(hipEventRecord(r.a, s));
   recs.push_back(r);
+  return recs.size() - 1;
 }
 
-void Prof::end(hipStream_t s) { SYZ_HIP(hipEventRecord(recs.back().b, s)); }
+void Prof::end(size_t rec, hipStream_t s) { SYZ_HIP(hipEventRecord(recs[rec].b, s)); }
 
 // ---- device-wide exclusive scan: reduce tiles, scan tile sums (recursively), add back ----------
 constexpr int SCAN_BLOCK = 256;
