@@ -4,7 +4,7 @@
 //
 // sort.Sort is unstable: among equal lengths the order depends on the exact sequence of swaps, and
 // that order decides which inputs Minimize keeps. The simulation performs exactly the
-// swaps of the sequential algorithm (oracle/gosort.h restates it):
+// swaps of the sequential algorithm (Go 1.6-1.18 sort/sort.go quickSort, doPivot, insertionSort):
 //   * the O(1) decisions of doPivot (Tukey ninther + medianOfThree, the dups probe) and the leaves
 //     (gap-6 shell pass + insertionSort on <= 12 elements) and heapSort run as the SAME sequential
 //     code, one thread per segment;
@@ -70,7 +70,7 @@ __device__ __forceinline__ void swp(P d, uint32_t i, uint32_t j) {
   d[j] = t;
 }
 
-// ---- sequential pieces, exactly as oracle/gosort.h -------------------------------------------------
+// ---- sequential pieces, exactly as Go sort/sort.go -------------------------------------------------
 template <int SH, class P>
 __device__ void seq_mo3(P d, uint32_t m1, uint32_t m0, uint32_t m2) {
   if (LT<SH>(d[m1], d[m0])) swp(d, m1, m0);
