@@ -79,7 +79,7 @@ struct Context {
   size_t last_n = 0;
   uint32_t last_groups = 0;
   bool have_last = false;
-  std::vector<hipEvent_t> gs_events;  // gosort level-count events (reused)
+  std::vector<hipEvent_t> gs_events;  // gosort per-level events (reused)
   hipStream_t side = nullptr;         // second stream: independent work overlapped with the main one
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipStream_t cap = nullptr;           // capture stream for the gosort level graphs

@@ -543,9 +543,18 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
   extern __shared__ __attribute__((aligned(16))) char smem[];
   LsLds<E>& S = *reinterpret_cast<LsLds<E>*>(smem);
   constexpr uint64_t LEN_LIMIT = SH >= 32 ? ~0ull : (1ull << (sizeof(E) * 8 - SH));
-  const uint32_t npacks = npacks_dev ? *npacks_dev : npacks_host;
+  // packs == nullptr: the items are single segments segs[range[0] .. range[1]) (children of the global
+  // levels, npacks_dev points at that range)
+  const uint32_t base = packs ? 0 : npacks_dev[0];
+  const uint32_t npacks = packs ? (npacks_dev ? *npacks_dev : npacks_host) : npacks_dev[1] - npacks_dev[0];
   for (uint32_t pi = blockIdx.x; pi < npacks; pi += gridDim.x) {
-    const Pack pk = packs[pi];
+    Pack pk;
+    if (packs) {
+      pk = packs[pi];
+    } else {
+      const Seg sg = segs[base + pi];
+      pk = Pack{sg.lo, sg.hi, base + pi, base + pi + 1};
+    }
     const uint32_t n = pk.phi - pk.plo;
     if (threadIdx.x == 0) {
       S.flag = 0;
@@ -1040,7 +1049,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
   }
-  const bool fork = P.npacks && P.nbig;
+  const bool fork = P.npacks && P.nbig && !getenv("SYZGPU_GS_NOFORK");
   hipStream_t ss = fork ? c.side : s;
   if (P.npacks) {
     if (fork) {
@@ -1110,7 +1119,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
       k_gl_finish<<<wgrid, 64, 0, q>>>(el, cur, nx, &ctl[0], dlds, heap);
       SYZ_LAUNCHED();
     };
-    const std::vector<const void*> key = {el,        tcnt,          A,           B,           ctl,
+    const std::vector<const void*> key = {el,   tcnt,          A,           B,           ctl,
                                           dlds,      heap,          lvl[0].segs, lvl[0].lv,   lvl[0].toff,
                                           lvl[0].tseg, lvl[0].plan, lvl[1].segs, lvl[1].lv,   lvl[1].toff,
                                           lvl[1].tseg, lvl[1].plan, (const void*)(uintptr_t)tgrid,
@@ -1160,10 +1169,11 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     // children that reached the LDS size and depth-exhausted big ones: counts stay on the device
     k_gs_heap<<<64, 64, 0, s>>>(el, heap, &ctl[0].nheap);
     SYZ_LAUNCHED();
-    k_dyn_packs<<<256, 256, 0, s>>>(dlds, &ctl[0].nlds, dpacks);
-    SYZ_LAUNCHED();
+    // the LDS-sized children of all levels, one workgroup each ([0, nlds) via &ctl[0].nnext == 0);
+    // running them per level beside the levels was measured slower: they take the CUs the
+    // latency-bound level kernels need
     ProfScope ps2("gosort_lds", s, (uint64_t)n * 12);
-    launch_ls<LS_SH, uint32_t>(el, perm, dpacks, 0, &ctl[0].nlds, 2048, dlds, &ctl[2].nlds, bounceD, s);
+    launch_ls<LS_SH, uint32_t>(el, perm, nullptr, 0, &ctl[0].nnext, 1024, dlds, &ctl[2].nlds, bounceD, s);
   }
   if (fork) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
   // packs with a length that does not fit the u32 element (>= 2^20 PCs) were bounced: the u64
@@ -1171,6 +1181,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   if (P.npacks)
     launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, s);
   if (P.nbig) launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nnext, bounceD, s);
+  (void)dpacks;
 }
 
 #ifdef SYZ_GS_STATS
