@@ -112,12 +112,19 @@ def main():
 
     from syzkaller_amd import _lib, cover, sharding, synth
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # SYZ_BENCH_BACKEND=gloo + SYZ_BENCH_SAME_DEVICE=1 rehearse the N>1 path with every rank on GPU 0
+    # (the real run is one rank per GPU over RCCL, backend "nccl")
+    backend = os.environ.get("SYZ_BENCH_BACKEND", "nccl")
+    dev_index = 0 if os.environ.get("SYZ_BENCH_SAME_DEVICE") == "1" else local
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     L = _lib.lib()
-    _lib.check(L.syzgpu_init(local))
+    _lib.check(L.syzgpu_init(dev_index))
 
     # ---- corpus (synthetic, deterministic; generated on the host, then made resident) ----
     t0 = time.time()
@@ -205,14 +212,14 @@ def main():
         raw_ms = (time.perf_counter() - t0r) / args.raw_steps * 1e3
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        sharding.allreduce(t, dist, dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     total_progs = args.progs_per_gpu * world
     sum_pcs = int(corp.off[-1])
     if world > 1:
         tt = torch.tensor([sum_pcs], dtype=torch.int64, device=dev)
-        dist.all_reduce(tt)
+        sharding.allreduce(tt, dist)
         sum_pcs_all = int(tt.item())
     else:
         sum_pcs_all = sum_pcs

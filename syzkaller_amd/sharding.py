@@ -38,11 +38,24 @@ def local_entries(group, owner, rank):
     return np.nonzero(owner[np.asarray(group, np.int64)] == rank)[0]
 
 
+def allreduce(t, dist=None, op=None):
+    """In-place all-reduce of a torch tensor on any backend: RCCL takes device tensors directly, gloo
+    (CPU rehearsals of the N>1 path) goes through a host copy."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return t
+    op = dist.ReduceOp.SUM if op is None else op
+    if t.is_cuda and dist.get_backend() == "gloo":
+        tmp = t.cpu()
+        dist.all_reduce(tmp, op=op)
+        t.copy_(tmp)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
+
+
 def allreduce_hist(hist, dist=None):
     """Sum the kept-program length histograms of all ranks in place (torch tensor, any backend)."""
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
-    return hist
+    return allreduce(hist, dist)
 
 
 def assemble_selection(kept_global, group, ngroups, dist=None):
