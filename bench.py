@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "corpus progs/sec: cover.Minimize + calcDynamicPrio, 1M progs, 1/2/4/8 GPUs"
+ROOF_KERNEL = "vec_min"  # the HBM-bound Minimize stream
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured copy)
 
 
@@ -45,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="programs in the CPU baseline sample")
     ap.add_argument("--profile", type=int, default=1, help="per-kernel HIP event timing in the timed region")
     ap.add_argument("--raw-steps", type=int, default=2, help="also time Minimize from the raw CSR (no store)")
+    ap.add_argument("--emulate", default="", help="W:r — rehearsal: run rank r's shard of a W-rank job on this "
+                    "one process (no collectives; the printed line is that rank's time, not a job value)")
     return ap.parse_args()
 
 
@@ -102,6 +105,7 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    emu_world, emu_rank = (int(x) for x in args.emulate.split(":")) if args.emulate else (world, rank)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
@@ -129,10 +133,10 @@ def main():
     # ---- corpus (synthetic, deterministic; generated on the host, then made resident) ----
     t0 = time.time()
     C, G = args.calls, args.ngroups
-    p = synth.params(args.seed, args.progs_per_gpu * world, G, args.npcs)
+    p = synth.params(args.seed, args.progs_per_gpu * emu_world, G, args.npcs)
     group, off, plen = synth.layout(p)
-    owner, load = sharding.lpt_assign(sharding.group_weights(group, off, G), world)
-    ids = sharding.local_entries(group, owner, rank)
+    owner, load = sharding.lpt_assign(sharding.group_weights(group, off, G), emu_world)
+    ids = sharding.local_entries(group, owner, emu_rank)
     corp = synth.subcorpus(p, ids, group, off, plen)
     gen_s = time.time() - t0
 
@@ -173,7 +177,25 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+
+    def read_prof():
+        cap = 4096
+        names = ctypes.create_string_buffer(48 * cap)
+        ms = np.zeros(cap, np.float32)
+        by = np.zeros(cap, np.uint64)
+        k = L.syzgpu_profile_read(names, ms.ctypes.data, by.ctypes.data, cap)
+        out, raw = {}, names.raw
+        for i in range(k):
+            nm = raw[48 * i:48 * (i + 1)].split(b"\0")[0].decode()
+            e = out.setdefault(nm, {"ms": 0.0, "launches": 0, "bytes": 0})
+            e["ms"] += float(ms[i])
+            e["launches"] += 1
+            e["bytes"] += int(by[i])
+        return out
+
+    # timed region: HIP events (on the launch stream) around the roofline kernel only
     if args.profile:
+        L.syzgpu_profile_only(ROOF_KERNEL.encode())
         L.syzgpu_profile_enable(1)
     if world > 1:
         dist.barrier()
@@ -185,21 +207,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    roof_ev = read_prof() if args.profile else {}
+    L.syzgpu_profile_enable(0)
+    # per-kernel breakdown: a separate, untimed pass with events around every kernel
     kern = {}
     if args.profile:
-        cap = 4096
-        names = ctypes.create_string_buffer(48 * cap)
-        ms = np.zeros(cap, np.float32)
-        by = np.zeros(cap, np.uint64)
-        k = L.syzgpu_profile_read(names, ms.ctypes.data, by.ctypes.data, cap)
+        L.syzgpu_profile_only(None)
+        L.syzgpu_profile_enable(1)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        kern = read_prof()
         L.syzgpu_profile_enable(0)
-        raw = names.raw
-        for i in range(k):
-            nm = raw[48 * i:48 * (i + 1)].split(b"\0")[0].decode()
-            e = kern.setdefault(nm, {"ms": 0.0, "launches": 0, "bytes": 0})
-            e["ms"] += float(ms[i])
-            e["launches"] += 1
-            e["bytes"] += int(by[i])
     # the same Minimize from the raw CSR every time (no store): reported beside the headline
     raw_ms = None
     if args.raw_steps > 0:
@@ -231,8 +250,10 @@ def main():
         # roofline of the dominant kernel: algorithmic bytes per SURVEY.md §8(d) for the units one
         # launch processes (Minimize: 4 B per PC + 10 B per program), over its measured average time
         roof = None
-        if kern:
-            roof = roofline(kern, corp, store_info, C)
+        if roof_ev:
+            roof = roofline(roof_ev, corp, store_info, C)
+            if roof and kern:
+                roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
         path_bytes = 4 * sum_pcs_all + 10 * total_progs + 16 * C * C
         cpu = None
         if args.cpu_baseline and world == 1:
@@ -252,7 +273,7 @@ def main():
                               "achieved": round(path_bytes / (ms_step * 1e-3) / 1e9, 1),
                               "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                               "frac": round(path_bytes / (ms_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)},
-            "kernels_ms_per_step": {k: round(v["ms"] / args.steps, 4) for k, v in
+            "kernels_ms_per_step_untimed_pass": {k: round(v["ms"] / args.steps, 4) for k, v in
                                     sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},
             "cpu_baseline": cpu,
             "ingest": {"seconds": round(ingest_s, 4), "progs_per_s": round(corp.n / ingest_s, 1),

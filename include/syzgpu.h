@@ -158,6 +158,9 @@ int syzgpu_corpus_info(const syzgpu_corpus* c, uint64_t* info, size_t cap);
 /* Per-kernel timing of the last *_dev call (HIP events on the call's stream), for the benchmark's
  * roofline. names/ms arrays of capacity cap; returns the number of kernels recorded. */
 int syzgpu_profile_enable(int on);
+/* Restrict the recording to the scopes named `name` (NULL: all), so that the timed region of the
+ * benchmark carries one event pair per step for its roofline kernel only. */
+int syzgpu_profile_only(const char* name);
 size_t syzgpu_profile_read(char (*names)[48], float* ms, uint64_t* bytes, size_t cap);
 
 #ifdef __cplusplus

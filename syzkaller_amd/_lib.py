@@ -48,6 +48,7 @@ SIGNATURES = {
     "syzgpu_corpus_minimize_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp]),
     "syzgpu_corpus_info": (_c.c_int, [_vp, _vp, _sz]),
     "syzgpu_profile_enable": (_c.c_int, [_c.c_int]),
+    "syzgpu_profile_only": (_c.c_int, [_c.c_char_p]),
     "syzgpu_profile_read": (_sz, [_vp, _vp, _vp, _sz]),
 }
 

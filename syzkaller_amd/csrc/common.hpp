@@ -79,12 +79,14 @@ struct Context {
   size_t last_n = 0;
   uint32_t last_groups = 0;
   bool have_last = false;
-  std::vector<hipEvent_t> gs_events;  // gosort per-level events (reused)
   hipStream_t side = nullptr;         // second stream: independent work overlapped with the main one
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipStream_t cap = nullptr;           // capture stream for the gosort level graphs
-  hipGraphExec_t gl_exec[2] = {nullptr, nullptr};
+  hipStream_t cap = nullptr;           // capture stream for the gosort round graph
+  hipGraphExec_t gl_exec[2][4] = {};  // [start parity][rounds - 1]: global-round graphs
   std::vector<const void*> gl_key;
+  unsigned long long* gr_host = nullptr;  // host-mapped progress word of the global rounds
+  unsigned long long* gr_dev = nullptr;   // its device address
+  uint32_t gr_epoch = 0;
 };
 
 // Returns the initialised context of the current device (lazily init(0)); throws ENODEV.
@@ -93,6 +95,8 @@ Context& ctx();
 // Kernel timing (bench roofline). Records named events around launches when enabled.
 struct Prof {
   bool on = false;
+  std::string only;  // when non-empty, only scopes of this name are recorded
+  bool match(const char* name) const { return only.empty() || only == name; }
   struct Rec {
     std::string name;
     hipEvent_t a, b;
@@ -111,7 +115,7 @@ struct ProfScope {
   hipStream_t s;
   bool on;
   size_t rec = 0;
-  ProfScope(const char* name, hipStream_t st, uint64_t bytes) : s(st), on(prof().on) {
+  ProfScope(const char* name, hipStream_t st, uint64_t bytes) : s(st), on(prof().on && prof().match(name)) {
     if (on) rec = prof().begin(name, s, bytes);
   }
   ~ProfScope() {

@@ -695,17 +695,28 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
 // =====================================================================================================
 // Global levels: segments larger than T_SEG, in place in el[] (HBM / L2).
 // =====================================================================================================
+// One ROUND advances every big segment by one pass of doPivot's O(n) loops, in three kernels:
+//   k_gr_count  per 4096-element tile: #(stays left) in the pass range
+//   k_gr_lists  per tile: the rank of every misplaced element straight from the prefix of "stays
+//               left" counts (no second scan): with L(p) = #left in [a, p) and T = #left in [a, e),
+//               the boundary is a + T, a misplaced-left element (not left, p < bnd) has rank
+//               k = (p - a) - L(p) from the left, a misplaced-right one (left, p >= bnd) has rank
+//               T - 1 - L(p) from the right, and the Hoare loop swaps equal ranks
+//   k_gr_swap   the swaps; the last tile of a segment to finish (agent-scope release / acquire
+//               through a per-segment arrival counter) runs the segment's O(1) tail: the dups probe,
+//               then either re-admits the segment for its protect pass next round or swaps the
+//               pivot into place and routes the children (next round / LDS sorter / heapSort).
+// A round is three dependent launches; the protect pass costs its segment one extra round.
+typedef __attribute__((address_space(1))) unsigned long long gu64;  // global (not flat) 8-byte word
+
 struct GLvl {
-  uint32_t pl, m, cnt, bnd, b, c, prot, ng;
+  uint32_t pl, m, bnd, b, c, mode, ng, pad;  // mode 0: Hoare pass, 1: protect pass
 };
 
 struct GCtl {
-  uint32_t nnext, nlds, nheap, pad;
+  uint32_t nnext, nlds, nheap, round;  // nnext stays 0: [nnext, nlds) is the LDS children range
 };
 
-// Per-level state, double-buffered: level L reads buffer L&1 and its finish kernel writes the
-// children (segments, their pivots, their tiles) into buffer (L+1)&1, so the host never waits
-// between levels. Tiles are reserved with atomics; a tile only needs its (segment, tile) pair.
 struct GPlan {
   uint32_t nseg, ntiles;
 };
@@ -714,77 +725,83 @@ struct GLevel {
   Seg* segs;
   GLvl* lv;
   uint32_t* toff;
+  uint32_t* done;  // tiles of the segment whose swaps have been published
   uint2* tseg;
   GPlan* plan;
 };
 
-// one wave per segment: reserve tiles, write the tile list, choose the pivot
-__device__ __forceinline__ void gl_admit(uint64_t* el, const Seg& sg, uint32_t idx, GLevel nx) {
-  const uint32_t nt = (sg.hi - sg.lo + GL_TILE - 1) / GL_TILE;
+__device__ __forceinline__ uint32_t gl_ntiles(const Seg& sg) { return (sg.hi - sg.lo + GL_TILE - 1) / GL_TILE; }
+
+// one wave: reserve the segment's tiles in nx and publish its pass state
+__device__ __forceinline__ void gl_enter(const Seg& sg, const GLvl& L, uint32_t idx, GLevel nx) {
+  const uint32_t nt = gl_ntiles(sg);
   uint32_t t0 = 0;
   if (__lane_id() == 0) t0 = atomicAdd(&nx.plan->ntiles, nt);
   t0 = __shfl(t0, 0);
   for (uint32_t t = __lane_id(); t < nt; t += 64) nx.tseg[t0 + t] = make_uint2(idx, t);
-  const uint32_t m = wave_pivot<32>(el, sg.lo, sg.hi);
-  wave_sync();
   if (__lane_id() == 0) {
     nx.segs[idx] = sg;
     nx.toff[idx] = t0;
-    GLvl L{};
-    L.m = m;
-    L.pl = KEY<32>(el[sg.lo]);
+    nx.done[idx] = 0;
     nx.lv[idx] = L;
   }
 }
 
-// initial level: the big call groups
-__global__ __launch_bounds__(64) void k_gl_init(uint64_t* el, const Seg* big, uint32_t nbig, GLevel nx) {
-  for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
-    uint32_t idx = 0;
-    if (__lane_id() == 0) idx = atomicAdd(&nx.plan->nseg, 1u);
-    idx = __shfl(idx, 0);
-    gl_admit(el, big[i], idx, nx);
-  }
+// one wave: a new doPivot node enters the next round (pivot choice, Hoare pass)
+__device__ __forceinline__ void gl_admit(uint64_t* el, const Seg& sg, GLevel nx) {
+  uint32_t idx = 0;
+  if (__lane_id() == 0) idx = atomicAdd(&nx.plan->nseg, 1u);
+  idx = __shfl(idx, 0);
+  const uint32_t m = wave_pivot<32>(el, sg.lo, sg.hi);
+  wave_sync();
+  GLvl L{};
+  L.m = m;
+  if (__lane_id() == 0) L.pl = KEY<32>(el[sg.lo]);
+  gl_enter(sg, L, idx, nx);
+}
+
+// initial round: the big call groups; the call's epoch tags the host progress words
+__global__ __launch_bounds__(64) void k_gl_init(uint64_t* el, const Seg* big, uint32_t nbig, GLevel nx, GCtl* ctl,
+                                                uint32_t epoch) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl->round = epoch << 16;
+  for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) gl_admit(el, big[i], nx);
 }
 
 // the range and the "stays left" predicate of a pass
-__device__ __forceinline__ bool gl_range(const Seg& sg, const GLvl& L, int mode, uint32_t* a, uint32_t* e) {
-  if (mode == 1 && !L.prot) return false;
+__device__ __forceinline__ bool gl_range(const Seg& sg, const GLvl& L, uint32_t* a, uint32_t* e) {
   *a = sg.lo + 1;
-  *e = mode == 0 ? sg.hi - 1 : L.b;
+  *e = L.mode == 0 ? sg.hi - 1 : L.b;
   return *a < *e;
 }
-__device__ __forceinline__ bool gl_left(uint32_t k, uint32_t pl, int mode) { return mode == 0 ? k >= pl : k > pl; }
+__device__ __forceinline__ bool gl_left(uint32_t k, const GLvl& L) { return L.mode == 0 ? k >= L.pl : k > L.pl; }
 
-__global__ __launch_bounds__(GL_BLOCK) void k_gl_count(const uint64_t* el, const Seg* segs, const GPlan* plan,
-                                                       const uint2* tseg, GLvl* lv, int mode, GPlan* next_plan) {
+__global__ __launch_bounds__(GL_BLOCK) void k_gr_count(const uint64_t* el, GLevel cur, GPlan* next_plan,
+                                                       uint32_t* tcnt, GCtl* ctl, unsigned long long* host_word) {
   __shared__ uint32_t red[GL_BLOCK / 64 + 1];
-  if (next_plan && blockIdx.x == 0 && threadIdx.x == 0) *next_plan = GPlan{0, 0};  // free since level L-1
-  for (uint32_t tb = blockIdx.x; tb < plan->ntiles; tb += gridDim.x) {
-    const uint2 st = tseg[tb];
-    const Seg sg = segs[st.x];
-    const GLvl L = lv[st.x];
-    uint32_t a, e;
-    if (!gl_range(sg, L, mode, &a, &e)) continue;  // uniform per block
-    const uint32_t t0 = sg.lo + st.y * GL_TILE;
-    uint32_t c = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *next_plan = GPlan{0, 0};  // read by the previous round only
+    // progress word for the host: (epoch << 48 | round << 32) | segments in this round
+    const uint32_t r = ++ctl->round;
+    __hip_atomic_store(host_word, ((unsigned long long)r << 32) | cur.plan->nseg, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const uint32_t ntiles = cur.plan->ntiles;
+  for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
+    const uint2 st = cur.tseg[tb];
+    const Seg sg = cur.segs[st.x];
+    const GLvl L = cur.lv[st.x];
+    uint32_t a, e, c = 0;
+    if (gl_range(sg, L, &a, &e)) {
+      const uint32_t t0 = sg.lo + st.y * GL_TILE;
 #pragma unroll 4
-    for (int i = 0; i < GL_ITEMS; i++) {
-      const uint32_t p = t0 + i * GL_BLOCK + threadIdx.x;
-      if (p >= a && p < e) c += gl_left(KEY<32>(el[p]), L.pl, mode) ? 1u : 0u;
+      for (int i = 0; i < GL_ITEMS; i++) {
+        const uint32_t p = t0 + i * GL_BLOCK + threadIdx.x;
+        if (p >= a && p < e) c += gl_left(KEY<32>(el[p]), L) ? 1u : 0u;
+      }
     }
     c = block_sum<GL_BLOCK>(c, red);
-    if (threadIdx.x == 0 && c) atomicAdd(&lv[st.x].cnt, c);
+    if (threadIdx.x == 0) tcnt[tb] = c;
   }
-}
-
-// class of position p: 1 misplaced-left, 2 misplaced-right
-__device__ __forceinline__ uint32_t gl_cls(uint64_t v, uint32_t p, uint32_t a, uint32_t e, uint32_t bd, uint32_t pl,
-                                           int mode) {
-  if (p < a || p >= e) return 0;
-  const bool left = gl_left(KEY<32>(v), pl, mode);
-  if (p < bd) return left ? 0 : 1;
-  return left ? 2 : 0;
 }
 
 // Tile of 4096 elements staged in LDS with coalesced loads; thread t owns the run [16t, 16t+16).
@@ -796,136 +813,287 @@ __device__ __forceinline__ void gl_stage(const uint64_t* el, uint32_t t0, uint32
   __syncthreads();
 }
 
-__global__ __launch_bounds__(GL_BLOCK) void k_gl_tiles(const uint64_t* el, const Seg* segs, const GPlan* plan,
-                                                       const uint2* tseg, const uint32_t* toff, GLvl* lv,
-                                                       uint64_t* tcnt, int mode) {
+__global__ __launch_bounds__(GL_BLOCK) void k_gr_lists(const uint64_t* el, GLevel cur, const uint32_t* tcnt,
+                                                       uint32_t* A, uint32_t* B) {
   __shared__ uint32_t red[GL_BLOCK / 64 + 1];
+  __shared__ uint32_t tpre[2];
   __shared__ uint64_t tile[GL_TILE + GL_TILE / 16];
-  for (uint32_t tb = blockIdx.x; tb < plan->ntiles; tb += gridDim.x) {
-    const uint2 st = tseg[tb];
-    const Seg sg = segs[st.x];
-    const GLvl L = lv[st.x];
+  const uint32_t ntiles = cur.plan->ntiles;
+  for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
+    const uint2 st = cur.tseg[tb];
+    const Seg sg = cur.segs[st.x];
+    const GLvl L = cur.lv[st.x];
     uint32_t a, e;
-    if (!gl_range(sg, L, mode, &a, &e)) continue;
-    const uint32_t bd = a + L.cnt;
+    if (!gl_range(sg, L, &a, &e)) continue;  // uniform per block
     const uint32_t t0 = sg.lo + st.y * GL_TILE;
-    gl_stage(el, t0, sg.hi, tile);
-    const uint32_t r0 = threadIdx.x * GL_ITEMS;
-    uint32_t packed = 0;
-    for (int i = 0; i < GL_ITEMS; i++) {
-      const uint32_t f = gl_cls(tile[r0 + i + (r0 >> 4)], t0 + r0 + i, a, e, bd, L.pl, mode);
-      packed += f == 1 ? 1u : (f == 2 ? 0x10000u : 0u);
-    }
-    packed = block_sum<GL_BLOCK>(packed, red);  // per tile < 2^16 per half
-    if (threadIdx.x == 0) {
-      tcnt[tb] = (uint64_t)(packed & 0xFFFF) | ((uint64_t)(packed >> 16) << 32);
-      if (st.y == 0) lv[st.x].bnd = bd;
-    }
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(GL_BLOCK) void k_gl_lists(const uint64_t* el, const Seg* segs, const GPlan* plan,
-                                                       const uint2* tseg, const uint32_t* toff, GLvl* lv,
-                                                       const uint64_t* tcnt, uint32_t* A, uint32_t* B, int mode) {
-  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
-  __shared__ uint64_t tbase;
-  __shared__ uint64_t tile[GL_TILE + GL_TILE / 16];
-  for (uint32_t tb = blockIdx.x; tb < plan->ntiles; tb += gridDim.x) {
-    const uint2 st = tseg[tb];
-    const Seg sg = segs[st.x];
-    const GLvl L = lv[st.x];
-    uint32_t a, e;
-    if (!gl_range(sg, L, mode, &a, &e)) continue;
-    const uint32_t t0 = sg.lo + st.y * GL_TILE;
-    const uint32_t ntile = (sg.hi - sg.lo + GL_TILE - 1) / GL_TILE;
-    const uint32_t first = toff[st.x];
-    if (threadIdx.x < 64) {  // prefix of the earlier tiles of this segment (and the total, last tile)
-      uint64_t acc = 0;
-      for (uint32_t t = __lane_id(); t < st.y; t += 64) acc += tcnt[first + t];
-      acc = wave_sum(acc);
+    if (t0 + GL_TILE <= a || t0 >= e) continue;  // tile outside the pass range (protect pass)
+    if (threadIdx.x < 64) {  // #left in the earlier tiles of this segment, and in all of them
+      const uint32_t first = cur.toff[st.x], nt = gl_ntiles(sg);
+      uint32_t pre = 0, all = 0;
+      for (uint32_t t = __lane_id(); t < nt; t += 64) {
+        const uint32_t v = tcnt[first + t];
+        all += v;
+        pre += t < st.y ? v : 0u;
+      }
+      pre = wave_sum(pre);
+      all = wave_sum(all);
       if (threadIdx.x == 0) {
-        tbase = acc;
-        if (st.y == ntile - 1) lv[st.x].ng = (uint32_t)(acc + tcnt[tb]);
+        tpre[0] = pre;
+        tpre[1] = all;
       }
     }
     gl_stage(el, t0, sg.hi, tile);
-    const uint32_t bd = L.bnd;
+    const uint32_t T = tpre[1], bnd = a + T;
     const uint32_t r0 = threadIdx.x * GL_ITEMS;
-    uint32_t cls[GL_ITEMS];
-    uint32_t packed = 0;
+    uint32_t lbits = 0, rbits = 0;  // bit i: in range / stays left
+#pragma unroll
     for (int i = 0; i < GL_ITEMS; i++) {
-      cls[i] = gl_cls(tile[r0 + i + (r0 >> 4)], t0 + r0 + i, a, e, bd, L.pl, mode);
-      packed += cls[i] == 1 ? 1u : (cls[i] == 2 ? 0x10000u : 0u);
+      const uint32_t p = t0 + r0 + i;
+      const bool in = p >= a && p < e;
+      rbits |= (in ? 1u : 0u) << i;
+      lbits |= ((in && gl_left(KEY<32>(tile[r0 + i + (r0 >> 4)]), L)) ? 1u : 0u) << i;
     }
     uint32_t tot;
-    const uint32_t pre = block_excl_scan<GL_BLOCK>(packed, red, &tot);  // in-tile ranks < 2^16 per half
-    uint32_t rl = (pre & 0xFFFF) + (uint32_t)tbase, rr = (pre >> 16) + (uint32_t)(tbase >> 32);
+    uint32_t lp = tpre[0] + block_excl_scan<GL_BLOCK>((uint32_t)__popc(lbits), red, &tot);  // L(first position)
+    uint32_t nml = 0;
+#pragma unroll
     for (int i = 0; i < GL_ITEMS; i++) {
-      if (cls[i] == 1) A[sg.lo + rl++] = t0 + r0 + i;
-      if (cls[i] == 2) B[sg.lo + rr++] = t0 + r0 + i;
+      const uint32_t p = t0 + r0 + i;
+      if (!((rbits >> i) & 1u)) continue;
+      const bool left = (lbits >> i) & 1u;
+      if (!left && p < bnd) {
+        A[sg.lo + (p - a) - lp] = p;
+        nml++;
+      } else if (left && p >= bnd) {
+        B[sg.lo + T - 1 - lp] = p;
+      }
+      lp += left ? 1u : 0u;
+    }
+    nml = block_sum<GL_BLOCK>(nml, red);
+    if (threadIdx.x == 0) {
+      if (nml) atomicAdd(&cur.lv[st.x].ng, nml);
+      if (t0 <= a && a < t0 + GL_TILE) cur.lv[st.x].bnd = bnd;
+    }
+  }
+}
+
+// ---- the O(1) tail of a segment, by one wave after all its swaps are visible ----------------------
+// Every element the tail touches is loaded once into a lane-distributed cache (lane i holds the
+// value at position pos_i; the lowest lane holding a position owns it), updated in registers and
+// stored once: two dependent memory round trips (probe + pivot positions, then the children's
+// pivot-of-nine positions) instead of one per step.
+struct WCache {
+  uint32_t pos;
+  uint64_t val;
+  bool dirty;
+  __device__ __forceinline__ int owner(uint32_t p) const {
+    const unsigned long long bal = __ballot(pos == p);
+    return bal ? __ffsll((long long)bal) - 1 : 0;
+  }
+  __device__ __forceinline__ uint64_t get(uint32_t p) const { return __shfl(val, owner(p)); }
+  __device__ __forceinline__ void set(uint32_t p, uint64_t v) {
+    if ((int)__lane_id() == owner(p)) {
+      val = v;
+      dirty = true;
+    }
+  }
+  __device__ __forceinline__ void swap(uint32_t i, uint32_t j) {
+    const uint64_t a = get(i), b = get(j);
+    set(i, b);
+    set(j, a);
+  }
+};
+
+// medianOfThree(data, m1, m0, m2) through the cache
+__device__ __forceinline__ void wc_mo3(WCache& W, uint32_t m1, uint32_t m0, uint32_t m2) {
+  if (LT<32>(W.get(m1), W.get(m0))) W.swap(m1, m0);
+  if (LT<32>(W.get(m2), W.get(m1))) {
+    W.swap(m2, m1);
+    if (LT<32>(W.get(m1), W.get(m0))) W.swap(m1, m0);
+  }
+}
+
+// doPivot's pivot-of-nine / medianOfThree positions of [lo, hi) (slot j < 9, 0xFFFFFFFF if unused)
+__device__ __forceinline__ uint32_t pivot_pos(uint32_t lo, uint32_t hi, uint32_t j) {
+  const uint32_t m = (uint32_t)(((uint64_t)lo + hi) >> 1);
+  if (hi - lo > 40) {
+    const uint32_t s = (hi - lo) / 8;
+    const uint32_t P[9] = {lo, lo + s, lo + 2 * s, m - s, m, m + s, hi - 1 - 2 * s, hi - 1 - s, hi - 1};
+    return P[j];
+  }
+  return j == 0 ? lo : (j == 1 ? m : (j == 2 ? hi - 1 : 0xFFFFFFFFu));
+}
+
+__device__ __forceinline__ void wc_pivot(WCache& W, uint32_t lo, uint32_t hi) {
+  const uint32_t m = (uint32_t)(((uint64_t)lo + hi) >> 1);
+  if (hi - lo > 40) {
+    const uint32_t s = (hi - lo) / 8;
+    wc_mo3(W, lo, lo + s, lo + 2 * s);
+    wc_mo3(W, m, m - s, m + s);
+    wc_mo3(W, hi - 1, hi - 1 - s, hi - 1 - 2 * s);
+  }
+  wc_mo3(W, lo, m, hi - 1);
+}
+
+__device__ void gl_tail(uint64_t* el, const Seg& sg, const GLvl& L, GLevel nx, GCtl* ctl, Seg* lds, Seg* heap) {
+  const uint32_t lane = __lane_id(), lo = sg.lo, hi = sg.hi;
+  // round trip 1: lo, the probe positions (hi-1, bnd, bnd-1, bnd-2, m), the final place of the
+  // pivot (b-1 for b in bnd, bnd-1, bnd-2), or the protect pass's b-1
+  WCache W{0xFFFFFFFFu, 0, false};
+  {
+    uint32_t p = 0xFFFFFFFFu;
+    if (L.mode == 0) {
+      const uint32_t P[7] = {lo, hi - 1, L.bnd, L.bnd - 1, L.bnd - 2, L.bnd - 3, L.m};
+      if (lane < 7) p = P[lane];
+    } else {
+      if (lane == 0) p = lo;
+      if (lane == 1) p = L.bnd - 1;
+    }
+    if (p != 0xFFFFFFFFu && p >= lo && p < hi) {
+      W.pos = p;
+      W.val = el[p];
+    }
+  }
+  uint32_t b, c;
+  bool protect = false;
+  if (L.mode == 0) {  // doPivot's dups probe (sort.go), on the cache
+    b = L.bnd;
+    c = L.bnd;
+    protect = hi - c < 5;
+    if (!protect && hi - c < (hi - lo) / 4) {
+      const uint64_t pv = W.get(lo);
+      int dups = 0;
+      if (!LT<32>(pv, W.get(hi - 1))) {  // data[hi-1] = pivot
+        W.swap(c, hi - 1);
+        c++;
+        dups++;
+      }
+      if (!LT<32>(W.get(b - 1), pv)) {  // data[b-1] = pivot
+        b--;
+        dups++;
+      }
+      if (!LT<32>(W.get(L.m), pv)) {  // data[m] = pivot
+        W.swap(L.m, b - 1);
+        b--;
+        dups++;
+      }
+      protect = dups > 1;
+    }
+  } else {
+    b = L.bnd;
+    c = L.c;
+  }
+  Seg ch[2];
+  uint32_t nadm = 0, ntl = 0;
+  bool adm[2] = {false, false};
+  if (protect) {  // the protect pass over [lo+1, b) next round
+    uint32_t idx = 0;
+    if (lane == 0) idx = atomicAdd(&nx.plan->nseg, 1u);
+    idx = __shfl(idx, 0);
+    GLvl P = L;
+    P.mode = 1;
+    P.b = b;
+    P.c = c;
+    P.bnd = lo + 1;  // the boundary if the range [lo+1, b) is empty
+    P.ng = 0;
+    if (W.dirty) el[W.pos] = W.val;
+    gl_enter(sg, P, idx, nx);
+    return;
+  }
+  W.swap(lo, b - 1);  // pivot into its final place
+  const int32_t dep = sg.depth - 1;
+  ch[0] = Seg{lo, b - 1, dep, 0};
+  ch[1] = Seg{c, hi, dep, 0};
+  for (int k = 0; k < 2; k++) {
+    const uint32_t len = ch[k].hi - ch[k].lo;
+    if (len <= 1) continue;
+    if (len <= T_SEG) {
+      if (lane == 0) lds[atomicAdd(&ctl->nlds, 1u)] = ch[k];
+    } else if (dep == 0) {
+      if (lane == 0) heap[atomicAdd(&ctl->nheap, 1u)] = ch[k];
+    } else {
+      adm[k] = true;
+      nadm++;
+      ntl += gl_ntiles(ch[k]);
+    }
+  }
+  if (nadm) {
+    // round trip 2: the admitted children's pivot positions (lanes 8.. and 24..), beside the slot
+    // reservations; positions already cached take the cached value
+    uint32_t p = 0xFFFFFFFFu;
+    if (lane >= 8 && lane < 17 && adm[0]) p = pivot_pos(ch[0].lo, ch[0].hi, lane - 8);
+    if (lane >= 24 && lane < 33 && adm[1]) p = pivot_pos(ch[1].lo, ch[1].hi, lane - 24);
+    const unsigned long long have = __ballot(W.pos != 0xFFFFFFFFu);
+    int src = -1;
+    for (unsigned long long h = have; h; h &= h - 1) {  // cached lanes, lowest first
+      const int l = __ffsll((long long)h) - 1;
+      if (src < 0 && p != 0xFFFFFFFFu && __shfl(W.pos, l) == p) src = l;
+      else (void)__shfl(W.pos, l);
+    }
+    uint32_t r = 0;
+    if (lane == 0) r = atomicAdd(&nx.plan->nseg, nadm);
+    if (lane == 1) r = atomicAdd(&nx.plan->ntiles, ntl);
+    const uint64_t cached = __shfl(W.val, src < 0 ? (int)lane : src);
+    if (p != 0xFFFFFFFFu) {
+      W.pos = p;
+      W.val = src >= 0 ? cached : el[p];
+    }
+    const uint32_t idx0 = __shfl(r, 0), t00 = __shfl(r, 1);
+    uint32_t idx = idx0, t0 = t00;
+    for (int k = 0; k < 2; k++) {
+      if (!adm[k]) continue;
+      wc_pivot(W, ch[k].lo, ch[k].hi);
+      const uint32_t nt = gl_ntiles(ch[k]);
+      for (uint32_t t = lane; t < nt; t += 64) nx.tseg[t0 + t] = make_uint2(idx, t);
+      const uint64_t piv = W.get(ch[k].lo);
+      if (lane == 0) {
+        GLvl C{};
+        C.m = (uint32_t)(((uint64_t)ch[k].lo + ch[k].hi) >> 1);
+        C.pl = KEY<32>(piv);
+        nx.segs[idx] = ch[k];
+        nx.toff[idx] = t0;
+        nx.done[idx] = 0;
+        nx.lv[idx] = C;
+      }
+      idx++;
+      t0 += nt;
+    }
+  }
+  if (W.dirty) el[W.pos] = W.val;
+}
+
+// tile t of a segment swaps the pairs k in [t*TILE/2, (t+1)*TILE/2) (ng <= len/2 <= ntile*TILE/2);
+// the last tile of the segment to arrive runs its tail. The swapped elements are stored
+// write-through (agent scope, sc1), so publishing them needs no L2 write-back.
+__global__ __launch_bounds__(GL_BLOCK) void k_gr_swap(uint64_t* el, GLevel cur, GLevel nx, const uint32_t* A,
+                                                      const uint32_t* B, GCtl* ctl, Seg* lds, Seg* heap) {
+  __shared__ uint32_t last;
+  const uint32_t ntiles = cur.plan->ntiles;
+  for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
+    const uint2 st = cur.tseg[tb];
+    const Seg sg = cur.segs[st.x];
+    const uint32_t ng = cur.lv[st.x].ng;
+    const uint32_t k0 = st.y * (GL_TILE / 2), k1 = min(ng, k0 + GL_TILE / 2);
+    for (uint32_t k = k0 + threadIdx.x; k < k1; k += GL_BLOCK) {
+      const uint32_t i = A[sg.lo + k], j = B[sg.lo + k];
+      const uint64_t x = el[i], y = el[j];
+      __hip_atomic_store((gu64*)&el[i], y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu64*)&el[j], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(&cur.done[st.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old + 1 == gl_ntiles(sg);
     }
     __syncthreads();
-  }
-}
-
-// tile t of a segment swaps pairs k in [t*TILE/2, (t+1)*TILE/2) (ng <= len/2 <= ntile*TILE/2)
-__global__ __launch_bounds__(GL_BLOCK) void k_gl_swap(uint64_t* el, const Seg* segs, const GPlan* plan,
-                                                      const uint2* tseg, const GLvl* lv, const uint32_t* A,
-                                                      const uint32_t* B, int mode) {
-  for (uint32_t tb = blockIdx.x; tb < plan->ntiles; tb += gridDim.x) {
-    const uint2 st = tseg[tb];
-    const Seg sg = segs[st.x];
-    const GLvl L = lv[st.x];
-    if (mode == 1 && !L.prot) continue;
-    const uint32_t ng = L.ng;
-    const uint32_t k0 = st.y * (GL_TILE / 2), k1 = min(ng, k0 + GL_TILE / 2);
-    for (uint32_t k = k0 + threadIdx.x; k < k1; k += GL_BLOCK) swp(el, A[sg.lo + k], B[sg.lo + ng - 1 - k]);
-  }
-}
-
-__global__ __launch_bounds__(64) void k_gl_probe(uint64_t* el, const Seg* segs, const GPlan* plan, GLvl* lv) {
-  for (uint32_t s = blockIdx.x; s < plan->nseg; s += gridDim.x) {
-    const Seg sg = segs[s];
-    GLvl L = lv[s];
-    uint32_t b, c;
-    L.prot = wave_probe<32>(el, sg.lo, sg.hi, L.m, L.bnd, &b, &c);
-    if (__lane_id() == 0) {
-      L.b = b;
-      L.c = c;
-      L.cnt = 0;
-      L.ng = 0;
-      lv[s] = L;
+    if (last && threadIdx.x < 64) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const GLvl L = cur.lv[st.x];
+      gl_tail(el, sg, L, nx, ctl, lds, heap);
     }
-  }
-}
-
-// one wave per segment: pivot into the middle, route the children; children that stay in the
-// global levels are admitted to the next level right here (tiles + pivot choice).
-__global__ __launch_bounds__(64) void k_gl_finish(uint64_t* el, GLevel cur, GLevel nx, GCtl* ctl, Seg* lds,
-                                                  Seg* heap) {
-  for (uint32_t s = blockIdx.x; s < cur.plan->nseg; s += gridDim.x) {
-    const Seg sg = cur.segs[s];
-    const GLvl L = cur.lv[s];
-    const uint32_t b = L.prot ? L.bnd : L.b;
-    if (__lane_id() == 0) swp(el, sg.lo, b - 1);
-    wave_sync();
-    const int32_t dep = sg.depth - 1;
-    const Seg ch[2] = {Seg{sg.lo, b - 1, dep, 0}, Seg{L.c, sg.hi, dep, 0}};
-    for (int k = 0; k < 2; k++) {
-      const uint32_t len = ch[k].hi - ch[k].lo;
-      if (len <= 1) continue;
-      if (len <= T_SEG) {
-        if (__lane_id() == 0) lds[atomicAdd(&ctl->nlds, 1u)] = ch[k];
-      } else if (dep == 0) {
-        if (__lane_id() == 0) heap[atomicAdd(&ctl->nheap, 1u)] = ch[k];
-      } else {
-        uint32_t idx = 0;
-        if (__lane_id() == 0) idx = atomicAdd(&nx.plan->nseg, 1u);
-        idx = __shfl(idx, 0);
-        gl_admit(el, ch[k], idx, nx);
-      }
-    }
+    __syncthreads();
   }
 }
 
@@ -1033,9 +1201,6 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   // ctl[0]: next-level count (reset by each plan) and the accumulated LDS / heap children;
   // ctl[2]: bounce counters of the static (nnext) and dynamic (nlds) LDS launches; ctl[3]: scratch
   GCtl* ctl = sc.get<GCtl>("gs_ctl", 4);
-  char* pin = c.pinned.get<char>(1024);
-  GCtl* hctl = reinterpret_cast<GCtl*>(pin);
-  uint32_t* hn = reinterpret_cast<uint32_t*>(pin + 256);
   SYZ_HIP(hipMemsetAsync(ctl, 0, 4 * sizeof(GCtl), s));
   {
     ProfScope ps("gosort_init", s, (uint64_t)n * 4);
@@ -1067,104 +1232,118 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   if (P.nbig) {
     const uint32_t nbig = P.nbig;
     const size_t max_tiles = n / GL_TILE + maxseg + 1;
-    uint64_t* tcnt = sc.get<uint64_t>("gs_tcnt", max_tiles);
+    uint32_t* tcnt = sc.get<uint32_t>("gs_tcnt", max_tiles);
     GLevel lvl[2];
     for (int p = 0; p < 2; p++) {
       const std::string k = std::to_string(p);
       lvl[p].segs = sc.get<Seg>("gs_seg" + k, maxseg);
       lvl[p].lv = sc.get<GLvl>("gs_lv" + k, maxseg);
       lvl[p].toff = sc.get<uint32_t>("gs_toff" + k, maxseg);
+      lvl[p].done = sc.get<uint32_t>("gs_done" + k, maxseg);
       lvl[p].tseg = sc.get<uint2>("gs_tseg" + k, max_tiles);
       lvl[p].plan = sc.get<GPlan>("gs_plan" + k, 1);
     }
-    constexpr int MAXLV = 64;
-    uint32_t* hhist = hn + 4;  // pinned, per-level counts
-    std::vector<hipEvent_t>& ev = c.gs_events;
-    while (ev.size() < (size_t)MAXLV) {
-      hipEvent_t e;
-      SYZ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      ev.push_back(e);
+    if (!c.gr_host) {
+      SYZ_HIP(hipHostMalloc((void**)&c.gr_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+      SYZ_HIP(hipHostGetDevicePointer((void**)&c.gr_dev, c.gr_host, 0));
+      *c.gr_host = 0;
     }
-    // grids sized to what the big groups can ever need (their elements only shrink level by level):
-    // idle workgroups of a grid-stride kernel still cost dispatch time on every one of the ~10
-    // dependent launches of a level
+    // grids sized to what the big groups can ever need (their elements only shrink round by round):
+    // idle workgroups of a grid-stride kernel still cost dispatch time on every launch
     const size_t segs_max = P.big_total / T_SEG + P.nbig + 1;
     const unsigned tgrid = (unsigned)std::min<size_t>(P.big_total / GL_TILE + segs_max, 2048);
-    const unsigned wgrid = (unsigned)std::min<size_t>(segs_max, 1024);  // one wave per segment
-    int issued = 0, checked = 0;
-    bool done = false;
     ProfScope ps("gosort_level", s, 0);
+    const uint32_t epoch = (++c.gr_epoch & 0x7FFFu) | 0x8000u;
     SYZ_HIP(hipMemsetAsync(lvl[0].plan, 0, sizeof(GPlan), s));
-    k_gl_init<<<std::min<uint32_t>(nbig, 1024), 64, 0, s>>>(el, P.big, nbig, lvl[0]);
+    k_gl_init<<<std::min<uint32_t>(nbig, 1024), 64, 0, s>>>(el, P.big, nbig, lvl[0], ctl, epoch);
     SYZ_LAUNCHED();
-    // one level = 10 dependent kernels with fixed arguments per buffer parity: both parities are
-    // captured once into HIP graphs and replayed, so a level costs one graph launch on the host
-    auto enqueue_level = [&](hipStream_t q, int parity) {
+    // one round = 3 dependent kernels with fixed arguments per buffer parity; RPG rounds (parity 0,
+    // 1, 0, 1) are captured once into a HIP graph and replayed
+    constexpr uint32_t RPG = 4;
+    auto enqueue_round = [&](hipStream_t q, int parity) {
       const GLevel cur = lvl[parity], nx = lvl[parity ^ 1];
-      for (int mode = 0; mode < 2; mode++) {
-        k_gl_count<<<tgrid, GL_BLOCK, 0, q>>>(el, cur.segs, cur.plan, cur.tseg, cur.lv, mode,
-                                              mode == 0 ? nx.plan : nullptr);
-        SYZ_LAUNCHED();
-        k_gl_tiles<<<tgrid, GL_BLOCK, 0, q>>>(el, cur.segs, cur.plan, cur.tseg, cur.toff, cur.lv, tcnt, mode);
-        SYZ_LAUNCHED();
-        k_gl_lists<<<tgrid, GL_BLOCK, 0, q>>>(el, cur.segs, cur.plan, cur.tseg, cur.toff, cur.lv, tcnt, A, B, mode);
-        SYZ_LAUNCHED();
-        k_gl_swap<<<tgrid, GL_BLOCK, 0, q>>>(el, cur.segs, cur.plan, cur.tseg, cur.lv, A, B, mode);
-        SYZ_LAUNCHED();
-        if (mode == 0) {
-          k_gl_probe<<<wgrid, 64, 0, q>>>(el, cur.segs, cur.plan, cur.lv);
-          SYZ_LAUNCHED();
-        }
-      }
-      k_gl_finish<<<wgrid, 64, 0, q>>>(el, cur, nx, &ctl[0], dlds, heap);
+      k_gr_count<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx.plan, tcnt, ctl, c.gr_dev);
+      SYZ_LAUNCHED();
+      k_gr_lists<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, tcnt, A, B);
+      SYZ_LAUNCHED();
+      k_gr_swap<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx, A, B, ctl, dlds, heap);
       SYZ_LAUNCHED();
     };
-    const std::vector<const void*> key = {el,   tcnt,          A,           B,           ctl,
-                                          dlds,      heap,          lvl[0].segs, lvl[0].lv,   lvl[0].toff,
-                                          lvl[0].tseg, lvl[0].plan, lvl[1].segs, lvl[1].lv,   lvl[1].toff,
-                                          lvl[1].tseg, lvl[1].plan, (const void*)(uintptr_t)tgrid,
-                                          (const void*)(uintptr_t)wgrid};
+    const std::vector<const void*> key = {el,          tcnt,        A,           B,           ctl,         dlds,
+                                          heap,        lvl[0].segs, lvl[0].lv,   lvl[0].toff, lvl[0].done, lvl[0].tseg,
+                                          lvl[0].plan, lvl[1].segs, lvl[1].lv,   lvl[1].toff, lvl[1].done, lvl[1].tseg,
+                                          lvl[1].plan, c.gr_dev,    (const void*)(uintptr_t)tgrid};
     if (c.gl_key != key) {
-      for (int p = 0; p < 2; p++) {
-        if (c.gl_exec[p]) SYZ_HIP(hipGraphExecDestroy(c.gl_exec[p]));
-        c.gl_exec[p] = nullptr;
-      }
-      if (!c.cap) SYZ_HIP(hipStreamCreateWithFlags(&c.cap, hipStreamNonBlocking));
-      for (int p = 0; p < 2; p++) {
-        hipGraph_t g;
-        SYZ_HIP(hipStreamBeginCapture(c.cap, hipStreamCaptureModeThreadLocal));
-        enqueue_level(c.cap, p);
-        SYZ_HIP(hipStreamEndCapture(c.cap, &g));
-        SYZ_HIP(hipGraphInstantiate(&c.gl_exec[p], g, nullptr, nullptr, 0));
-        SYZ_HIP(hipGraphDestroy(g));
-      }
+      for (auto& row : c.gl_exec)
+        for (auto& g : row) {
+          if (g) SYZ_HIP(hipGraphExecDestroy(g));
+          g = nullptr;
+        }
       c.gl_key = key;
     }
-    while (!done) {
-      if (issued >= MAXLV) fail(SYZGPU_EINTERNAL, "gosort: level limit");
-      const GLevel nx = lvl[(issued + 1) & 1];
-      SYZ_HIP(hipGraphLaunch(c.gl_exec[issued & 1], s));
-      SYZ_HIP(hipMemcpyAsync(hhist + issued, &nx.plan->nseg, 4, hipMemcpyDeviceToHost, s));
-      SYZ_HIP(hipEventRecord(ev[issued], s));
-      issued++;
-      // keep at most one level in flight ahead of the one whose count we wait for (a level issued
-      // past the last real one still costs ~10 near-empty launches)
-      while (checked < issued) {
-        const bool must = issued - checked > 1;
-        if (!must && hipEventQuery(ev[checked]) != hipSuccess) break;
-        SYZ_HIP(hipEventSynchronize(ev[checked]));
-        if (hhist[checked] == 0) {
-          done = true;
-          break;
-        }
-        checked++;
+    // graph of k rounds starting at buffer parity p, captured on first use
+    auto graph = [&](int p, uint32_t k) -> hipGraphExec_t {
+      hipGraphExec_t& ex = c.gl_exec[p][k - 1];
+      if (!ex) {
+        if (!c.cap) SYZ_HIP(hipStreamCreateWithFlags(&c.cap, hipStreamNonBlocking));
+        hipGraph_t g;
+        SYZ_HIP(hipStreamBeginCapture(c.cap, hipStreamCaptureModeThreadLocal));
+        for (uint32_t r = 0; r < k; r++) enqueue_round(c.cap, (int)((p + r) & 1));
+        SYZ_HIP(hipStreamEndCapture(c.cap, &g));
+        SYZ_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+        SYZ_HIP(hipGraphDestroy(g));
       }
+      return ex;
+    };
+    // The host issues rounds without waiting for them. The first count kernel of every round writes
+    // (epoch, round, segments) into host-mapped memory; the host stops once a round of this call
+    // reports zero segments (rounds issued past it find nothing and return at once). With a hint
+    // (the rounds the previous run of this plan needed), exactly hint + 1 rounds are issued up front
+    // and the last one reports zero; otherwise rounds go out RPG at a time, at most AHEAD beyond the
+    // last one seen running.
+    constexpr uint32_t MAXR = 512, AHEAD = RPG + 2;
+    volatile unsigned long long* hw = c.gr_host;
+    uint32_t issued = 0, seen = 0;
+    auto launch = [&](uint32_t k) {
+      if (issued + k > MAXR) fail(SYZGPU_EINTERNAL, "gosort: round limit");
+      SYZ_HIP(hipGraphLaunch(graph((int)(issued & 1), k), s));
+      issued += k;
+    };
+    bool done = false;
+    uint32_t last_rounds = 0;
+    auto poll = [&]() -> bool {  // true: a round of this call reported zero segments
+      const unsigned long long w = *hw;
+      if ((uint32_t)(w >> 48) != epoch) return false;
+      const uint32_t r = (uint32_t)(w >> 32) & 0xFFFFu, ns = (uint32_t)w;
+      if (r > seen) seen = r;
+      if (ns == 0) {
+        last_rounds = r - 1;
+        return true;
+      }
+      return false;
+    };
+    const bool hinted = P.rounds_hint > 0;
+    if (hinted)
+      while (issued < P.rounds_hint + 1) launch(std::min<uint32_t>(RPG, P.rounds_hint + 1 - issued));
+    else
+      launch(RPG);
+    while (!(done = poll())) {
+      if (!hinted && issued - seen < AHEAD) {
+        launch(RPG);
+        continue;
+      }
+      if (hipStreamQuery(s) == hipSuccess) {  // everything issued has run
+        if ((done = poll())) break;
+        if (seen < issued) fail(SYZGPU_EINTERNAL, "gosort: no progress word from the rounds");
+        launch(RPG);
+        continue;
+      }
+      __builtin_ia32_pause();
     }
+    P.rounds_hint = last_rounds;
     if (getenv("SYZGPU_GS_DEBUG")) {
       SYZ_HIP(hipStreamSynchronize(s));
-      fprintf(stderr, "gosort: %d levels issued, segments per level:", issued);
-      for (int l = 0; l < issued; l++) fprintf(stderr, " %u", hhist[l]);
-      fprintf(stderr, "\n");
+      fprintf(stderr, "gosort: %u rounds issued, %u with segments\n", issued, last_rounds);
     }
     // children that reached the LDS size and depth-exhausted big ones: counts stay on the device
     k_gs_heap<<<64, 64, 0, s>>>(el, heap, &ctl[0].nheap);

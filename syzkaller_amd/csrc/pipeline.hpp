@@ -16,6 +16,7 @@ struct GosortPlan {
   size_t n = 0;
   uint32_t nsmall = 0, npacks = 0, nbig = 0;
   uint64_t big_total = 0;  // elements in the groups that start the global levels
+  mutable uint32_t rounds_hint = 0;  // global rounds the last run of this plan needed (issued up front)
   Seg* small = nullptr;
   Pack* packs = nullptr;
   Seg* big = nullptr;

@@ -230,6 +230,11 @@ int syzgpu_profile_enable(int on) {
   return SYZGPU_OK;
 }
 
+int syzgpu_profile_only(const char* name) {
+  prof().only = name ? name : "";
+  return SYZGPU_OK;
+}
+
 size_t syzgpu_profile_read(char (*names)[48], float* ms, uint64_t* bytes, size_t cap) {
   Prof& p = prof();
   size_t k = 0;
