@@ -161,6 +161,24 @@ __device__ __forceinline__ T wave_incl_scan(T x) {
   return x;
 }
 
+// 32-bit inclusive wave64 scan on DPP (row_shr within 16-lane rows, then row_bcast:15 / :31):
+// seven VALU steps instead of six LDS-latency shuffles.
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t x) {
+  return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW, BANK, false);
+}
+template <>
+__device__ __forceinline__ uint32_t wave_incl_scan<uint32_t>(uint32_t v) {
+  uint32_t x = v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);             // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xF, 0xF, false);             // row_shr:3
+  x = dpp_add<0x114, 0xF, 0xE>(x);  // row_shr:4, lanes 4..15 of each row
+  x = dpp_add<0x118, 0xF, 0xC>(x);  // row_shr:8, lanes 8..15
+  x = dpp_add<0x142, 0xA, 0xF>(x);  // row_bcast:15 into rows 1 and 3
+  x = dpp_add<0x143, 0xC, 0xF>(x);  // row_bcast:31 into rows 2 and 3
+  return x;
+}
+
 template <class T>
 __device__ __forceinline__ T wave_sum(T x) {
 #pragma unroll
@@ -178,29 +196,25 @@ __device__ __forceinline__ T wave_min(T x) {
   return x;
 }
 
-// Exclusive scan across a workgroup of BLOCK threads. lds needs BLOCK/64 + 1 slots.
+// Exclusive scan across a workgroup of BLOCK threads. lds needs BLOCK/64 + 1 slots. Every thread
+// reads the (at most 16) wave totals itself: two barriers, no serial pass.
 template <int BLOCK, class T>
 __device__ __forceinline__ T block_excl_scan(T v, T* lds, T* total) {
+  constexpr int W = BLOCK / 64;
   const int w = threadIdx.x >> 6;
-  const unsigned l = __lane_id();
-  T x = wave_incl_scan(v);
-  if (l == 63) lds[w] = x;
+  const T x = wave_incl_scan(v);
+  if (__lane_id() == 63) lds[w] = x;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    T s = 0;
+  T pre = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < BLOCK / 64; i++) {
-      T t = lds[i];
-      lds[i] = s;
-      s += t;
-    }
-    lds[BLOCK / 64] = s;
+  for (int i = 0; i < W; i++) {
+    const T t = lds[i];
+    pre += i < w ? t : T(0);
+    tot += t;
   }
-  __syncthreads();
-  T r = x - v + lds[w];
-  *total = lds[BLOCK / 64];
-  __syncthreads();
-  return r;
+  *total = tot;
+  __syncthreads();  // lds reusable
+  return x - v + pre;
 }
 
 template <int BLOCK, class T>

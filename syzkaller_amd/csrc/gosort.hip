@@ -34,7 +34,7 @@ namespace syz {
 #ifdef SYZ_GS_STATS
 // diagnostic build only: [0] packs [1] levels [2] cycles total [3] pivot [4] part0 [5] probe [6] part1
 // [7] children [8] heap sorts [9] heap elements [10] max active segments [11] leaves
-__device__ unsigned long long g_gs_stats[16];
+__device__ unsigned long long g_gs_stats[24];
 #define GS_STAT_ADD(i, v) atomicAdd(&g_gs_stats[i], (unsigned long long)(v))
 #define GS_STAT_MAX(i, v) atomicMax(&g_gs_stats[i], (unsigned long long)(v))
 #define GS_T() __builtin_amdgcn_s_memtime()
@@ -347,15 +347,18 @@ template <class E>
 struct LsLds {
   E dv[T_SEG + T_SEG / 16];
   __device__ __forceinline__ PadRef<E> D() { return PadRef<E>{dv}; }
-  uint16_t ab[T_SEG];       // misplaced-left positions by rank in [0, T/2), misplaced-right in [T/2, T)
-  uint16_t abs[T_SEG / 2];  // segment of each misplaced-left entry
+  uint16_t bl[T_SEG];               // misplaced-right positions, at lo + rank from the right
+  uint32_t cpre[LS_BLOCK + 1];      // #left before each chunk (pass scan), [LS_BLOCK] = total
+  uint32_t cmask[LS_BLOCK];         // left bits of each chunk
   uint16_t lo[2][LS_MAXS], hi[2][LS_MAXS];
   int8_t dep[2][LS_MAXS];
-  uint32_t pl[LS_MAXS], cnt[LS_MAXS];
-  uint16_t m[LS_MAXS], bnd[LS_MAXS], b[LS_MAXS], c[LS_MAXS], base[LS_MAXS];
+  uint32_t pl[LS_MAXS], cnt[LS_MAXS];  // cnt: T | (#left before the range << 16) of the pass
+  uint16_t m[LS_MAXS], bnd[LS_MAXS], b[LS_MAXS], c[LS_MAXS];
   uint8_t prot[LS_MAXS];
+  uint32_t wl[LS_MAXS];  // segments of 13..WQ elements for the wave sorter: lo | hi << 16
+  int8_t wd[LS_MAXS];    // and their depth budget
   uint32_t red[LS_BLOCK / 64 + 1];
-  uint32_t na, tot, flag, anyprot;
+  uint32_t na, tot, flag, anyprot, nw;
 };
 
 // first active segment with hi > p (segments sorted, disjoint)
@@ -372,158 +375,148 @@ __device__ __forceinline__ uint32_t seg_at(const L& S, int cur, uint32_t na, uin
   return a;
 }
 
-// One compaction round of the level: mode 0 = Hoare pass (bnd, pairs len<pl | len>=pl on
-// [lo+1, hi-1)), mode 1 = protect pass (pairs len<=pl | len>pl on [lo+1, b)).
-// Thread t owns the chunk [16t, 16t+16) held in registers. Active segments have more than 12
-// elements, so a chunk meets at most 3 of them (sfirst .. sfirst+2): their fields are loaded once
-// into registers and every per-element step is branch-free.
+// One pass of doPivot's O(n) loop over every active segment of the pack: mode 0 = Hoare pass
+// (stays left: len >= pivot len, on [lo+1, hi-1)), mode 1 = protect pass (stays left: len > pivot
+// len, on [lo+1, b)).
+// Closed form (as in the global rounds): with L(p) = #left in [a, p) and T = #left in [a, e), the
+// boundary is a + T; a misplaced-left element (not left, p < bnd) has rank (p - a) - L(p) from the
+// left, a misplaced-right one (left, p >= bnd) has rank T - 1 - L(p) from the right, and the loop
+// swaps equal ranks. L comes from ONE workgroup scan of per-chunk left counts (no atomics); the
+// misplaced-right positions go to a list indexed inside the segment's own range, and each
+// misplaced-left element fetches its partner from it and performs the swap.
+// Thread t owns the chunk [16t, 16t+16). Active segments have more than 12 elements, so a chunk
+// meets at most 3 of them (sf .. sf+2).
+// bits j of a 16-element chunk starting at i0 whose position lies in [a, e)
+__device__ __forceinline__ uint32_t chunk_range(uint32_t i0, uint32_t a, uint32_t e) {
+  const int32_t lo = max(0, min((int32_t)LS_ITEMS, (int32_t)a - (int32_t)i0));
+  const int32_t hi = max(0, min((int32_t)LS_ITEMS, (int32_t)e - (int32_t)i0));
+  return (uint32_t)((1ull << hi) - 1ull) & ~(uint32_t)((1ull << lo) - 1ull);  // 0 when hi <= lo
+}
+
+// #left in [0, p) of the pack (p <= T_SEG), from the chunk prefixes and masks
+template <class L>
+__device__ __forceinline__ uint32_t ls_lpre(const L& S, uint32_t p) {
+  const uint32_t t = p >> 4, j = p & 15u;
+  return j ? S.cpre[t] + __popc(S.cmask[t] & ((1u << j) - 1u)) : S.cpre[t];
+}
+
 template <int SH, class E, class L>
 __device__ void ls_partition(L& S, int cur, uint32_t na, uint32_t n, int mode) {
   unsigned long long tq0 = GS_T();
   (void)tq0;
-  constexpr uint32_t H = T_SEG / 2;
   const uint32_t i0 = threadIdx.x * LS_ITEMS;
-  const bool live = i0 < n;
-  E x[LS_ITEMS];
-  uint32_t sf = na, slo[3], shi[3], spl[3], sa[3], se[3], cnt[3] = {0, 0, 0};
-  uint32_t segoff = 0xFFFFFFFFu;  // 2 bits per element: segment sf + k, 3 = in no active segment
-  uint32_t inr = 0, left = 0;     // bit i: in the pass range / stays left
+  uint32_t sf = 0, mseg[3] = {0, 0, 0}, slo[3] = {0, 0, 0}, inr = 0, left = 0;
+  bool live = i0 < n && na > 0;
   if (live) {
-#pragma unroll
-    for (int i = 0; i < LS_ITEMS; i++) x[i] = S.D()[i0 + i];
     sf = seg_at(S, cur, na, i0);
+    live = sf < na && S.lo[cur][sf] < i0 + LS_ITEMS;
+  }
+  if (live) {
+    uint32_t key[LS_ITEMS];
+#pragma unroll
+    for (int i = 0; i < LS_ITEMS; i++) key[i] = KEY<SH>(S.D()[i0 + i]);
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       const uint32_t ss = sf + k;
-      if (ss < na) {
-        slo[k] = S.lo[cur][ss];
-        shi[k] = S.hi[cur][ss];
-        spl[k] = S.pl[ss];
-        const bool act = mode == 0 || S.prot[ss];
-        sa[k] = slo[k] + 1;
-        se[k] = act ? (mode == 0 ? shi[k] - 1 : S.b[ss]) : 0;
-      } else {
-        slo[k] = 0xFFFFFFFFu;
-        shi[k] = 0;
-        spl[k] = 0;
-        sa[k] = 1;
-        se[k] = 0;
-      }
-    }
+      if (ss >= na) break;
+      const uint32_t lo = S.lo[cur][ss];
+      if (lo >= i0 + LS_ITEMS) break;
+      slo[k] = lo;
+      mseg[k] = chunk_range(i0, lo, S.hi[cur][ss]);
+      if (mode == 1 && !S.prot[ss]) continue;
+      const uint32_t r = chunk_range(i0, lo + 1, mode == 0 ? S.hi[cur][ss] - 1u : (uint32_t)S.b[ss]);
+      if (!r) continue;
+      const uint32_t pl = S.pl[ss];
+      uint32_t ge = 0;
 #pragma unroll
-    for (int i = 0; i < LS_ITEMS; i++) {
-      const uint32_t p = i0 + i;
-      const uint32_t k = p >= shi[0] ? (p >= shi[1] ? 2u : 1u) : 0u;
-      const uint32_t lo = k == 0 ? slo[0] : (k == 1 ? slo[1] : slo[2]);
-      const uint32_t hi = k == 0 ? shi[0] : (k == 1 ? shi[1] : shi[2]);
-      if (p >= lo && p < hi) {
-        segoff &= ~(3u << (2 * i));
-        segoff |= k << (2 * i);
-        const uint32_t a = k == 0 ? sa[0] : (k == 1 ? sa[1] : sa[2]);
-        const uint32_t e = k == 0 ? se[0] : (k == 1 ? se[1] : se[2]);
-        if (p >= a && p < e) {
-          const uint32_t pl = k == 0 ? spl[0] : (k == 1 ? spl[1] : spl[2]);
-          const uint32_t key = KEY<SH>(x[i]);
-          const bool st = mode == 0 ? key >= pl : key > pl;
-          inr |= 1u << i;
-          left |= (st ? 1u : 0u) << i;
-          if (st) {
-            if (k == 0) cnt[0]++;
-            else if (k == 1) cnt[1]++;
-            else cnt[2]++;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; k++)
-      if (cnt[k]) atomicAdd(&S.cnt[sf + k], cnt[k]);
-  }
-  __syncthreads();
-  unsigned long long tq1 = GS_T();
-  for (uint32_t q = threadIdx.x; q < na; q += LS_BLOCK) S.bnd[q] = (uint16_t)(S.lo[cur][q] + 1 + S.cnt[q]);
-  __syncthreads();
-  unsigned long long tq2 = GS_T();
-  // classes: 1 = misplaced left, 2 = misplaced right (2 bits per element); packed rank counts
-  uint32_t cl = 0, packed = 0;
-  uint32_t sbd[3] = {0, 0, 0};
-  if (live) {
-#pragma unroll
-    for (int k = 0; k < 3; k++)
-      if (sf + k < na) sbd[k] = S.bnd[sf + k];
-#pragma unroll
-    for (int i = 0; i < LS_ITEMS; i++) {
-      if (!((inr >> i) & 1u)) continue;
-      const uint32_t k = (segoff >> (2 * i)) & 3u;
-      const uint32_t bd = k == 0 ? sbd[0] : (k == 1 ? sbd[1] : sbd[2]);
-      const bool st = (left >> i) & 1u;
-      const uint32_t f = (i0 + i) < bd ? (st ? 0u : 1u) : (st ? 2u : 0u);
-      cl |= f << (2 * i);
-      packed += f == 1 ? 1u : (f == 2 ? 0x10000u : 0u);
+      for (int i = 0; i < LS_ITEMS; i++) ge |= ((mode == 0 ? key[i] >= pl : key[i] > pl) ? 1u : 0u) << i;
+      inr |= r;
+      left |= r & ge;
     }
   }
   uint32_t tot;
-  const uint32_t pre = block_excl_scan<LS_BLOCK>(packed, S.red, &tot);
-  uint32_t rl = pre & 0xFFFF, rr = pre >> 16;
-  if (live) {
+  const uint32_t pre = block_excl_scan<LS_BLOCK>((uint32_t)__popc(left), S.red, &tot);
+  S.cpre[threadIdx.x] = pre;
+  S.cmask[threadIdx.x] = left;
+  if (threadIdx.x == 0) S.cpre[LS_BLOCK] = tot;
+  __syncthreads();
+  unsigned long long tq1 = GS_T();
+  // per segment: the boundary and the left count before the range
+  for (uint32_t q = threadIdx.x; q < na; q += LS_BLOCK) {
+    if (mode == 1 && !S.prot[q]) continue;
+    const uint32_t a = S.lo[cur][q] + 1u, e = mode == 0 ? S.hi[cur][q] - 1u : (uint32_t)S.b[q];
+    if (a >= e) {
+      S.bnd[q] = (uint16_t)a;
+      S.cnt[q] = 0;
+      continue;
+    }
+    const uint32_t la = ls_lpre(S, a), T = ls_lpre(S, e) - la;
+    S.bnd[q] = (uint16_t)(a + T);
+    S.cnt[q] = T | (la << 16);
+  }
+  __syncthreads();
+  unsigned long long tq2 = GS_T();
+  // misplaced-right: B[lo + rank from the right] = p; misplaced-left: remembered in ml
+  uint32_t ml = 0;
+  uint32_t sbd[3] = {0, 0, 0}, sT[3] = {0, 0, 0}, sla[3] = {0, 0, 0};
+  if (inr) {
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      if (mseg[k] & inr) {
+        const uint32_t cv = S.cnt[sf + k];
+        sbd[k] = S.bnd[sf + k];
+        sT[k] = cv & 0xFFFFu;
+        sla[k] = cv >> 16;
+      }
+    uint32_t lp = pre;
 #pragma unroll
     for (int i = 0; i < LS_ITEMS; i++) {
-      const uint32_t k = (segoff >> (2 * i)) & 3u;
-      if (k == 3) continue;
-      const uint32_t p = i0 + i;
-      const uint32_t lo = k == 0 ? slo[0] : (k == 1 ? slo[1] : slo[2]);
-      if (p == lo + 1) S.base[sf + k] = (uint16_t)rl;
-      const uint32_t f = (cl >> (2 * i)) & 3u;
-      if (f == 1) {
-        S.ab[rl] = (uint16_t)p;
-        S.abs[rl] = (uint16_t)(sf + k);
-        rl++;
-      } else if (f == 2) {
-        S.ab[H + rr++] = (uint16_t)p;
+      if ((inr >> i) & 1u) {
+        const uint32_t p = i0 + i;
+        const uint32_t k = ((mseg[0] >> i) & 1u) ? 0u : (((mseg[1] >> i) & 1u) ? 1u : 2u);
+        const uint32_t bd = k == 0 ? sbd[0] : (k == 1 ? sbd[1] : sbd[2]);
+        const bool lf = (left >> i) & 1u;
+        if (!lf && p < bd) ml |= 1u << i;
+        if (lf && p >= bd) {
+          const uint32_t T = k == 0 ? sT[0] : (k == 1 ? sT[1] : sT[2]);
+          const uint32_t la = k == 0 ? sla[0] : (k == 1 ? sla[1] : sla[2]);
+          const uint32_t lo = k == 0 ? slo[0] : (k == 1 ? slo[1] : slo[2]);
+          S.bl[lo + T - 1u - (lp - la)] = (uint16_t)p;
+        }
+        lp += lf ? 1u : 0u;
       }
     }
   }
-  if (threadIdx.x == 0) S.tot = tot & 0xFFFF;
   __syncthreads();
   unsigned long long tq3 = GS_T();
-  // swap the k-th misplaced-left with the k-th misplaced-right from the right end
-  // every element takes part in at most one pair, so all loads of a thread's pairs can be issued
-  // before any store: the dependent LDS chain is paid once, not once per pair
-  const uint32_t nl = S.tot;
-  constexpr int SW = T_SEG / 2 / LS_BLOCK;  // pairs per thread at most
-  uint32_t pp[SW], qq[SW];
-  E vp[SW], vq[SW];
+  if (ml) {  // the swaps, by the misplaced-left side (pairs are disjoint); loads before stores
+    uint32_t lp = pre;
+    uint32_t qq[LS_ITEMS];
 #pragma unroll
-  for (int j = 0; j < SW; j++) {
-    const uint32_t g = threadIdx.x + j * LS_BLOCK;
-    pp[j] = g < nl ? S.ab[g] : 0;
-    qq[j] = g < nl ? S.abs[g] : 0;
-  }
-#pragma unroll
-  for (int j = 0; j < SW; j++) {
-    const uint32_t g = threadIdx.x + j * LS_BLOCK;
-    if (g < nl) {
-      const uint32_t sg = qq[j];
-      const uint32_t bs = S.base[sg];
-      const uint32_t be = sg + 1 < na ? S.base[sg + 1] : nl;
-      qq[j] = S.ab[H + be + bs - 1 - g];
+    for (int i = 0; i < LS_ITEMS; i++) {
+      qq[i] = 0;
+      if ((ml >> i) & 1u) {
+        const uint32_t p = i0 + i;
+        const uint32_t k = ((mseg[0] >> i) & 1u) ? 0u : (((mseg[1] >> i) & 1u) ? 1u : 2u);
+        const uint32_t la = k == 0 ? sla[0] : (k == 1 ? sla[1] : sla[2]);
+        const uint32_t lo = k == 0 ? slo[0] : (k == 1 ? slo[1] : slo[2]);
+        qq[i] = S.bl[lo + (p - lo - 1u) - (lp - la)];  // partner: same rank from the right
+      }
+      lp += (left >> i) & 1u;
     }
-  }
+    E vp[LS_ITEMS], vq[LS_ITEMS];
 #pragma unroll
-  for (int j = 0; j < SW; j++) {
-    const uint32_t g = threadIdx.x + j * LS_BLOCK;
-    if (g < nl) {
-      vp[j] = S.D()[pp[j]];
-      vq[j] = S.D()[qq[j]];
-    }
-  }
+    for (int i = 0; i < LS_ITEMS; i++)
+      if ((ml >> i) & 1u) {
+        vp[i] = S.D()[i0 + i];
+        vq[i] = S.D()[qq[i]];
+      }
 #pragma unroll
-  for (int j = 0; j < SW; j++) {
-    const uint32_t g = threadIdx.x + j * LS_BLOCK;
-    if (g < nl) {
-      S.D()[pp[j]] = vq[j];
-      S.D()[qq[j]] = vp[j];
-    }
+    for (int i = 0; i < LS_ITEMS; i++)
+      if ((ml >> i) & 1u) {
+        S.D()[i0 + i] = vq[i];
+        S.D()[qq[i]] = vp[i];
+      }
   }
   __syncthreads();
   if (threadIdx.x == 0 && mode == 0) {
@@ -533,6 +526,193 @@ __device__ void ls_partition(L& S, int cur, uint32_t na, uint32_t n, int mode) {
     GS_STAT_ADD(15, GS_T() - tq3);
   }
   (void)tq1; (void)tq2; (void)tq3;
+}
+
+// ---- wave sorter: a segment of 13..WQ elements finished by one wave, one element per lane ----------
+// Level-synchronous inside the wave: every lane knows its segment [s, e) (lane-relative) and depth,
+// all segments of the subtree advance one quickSort node per iteration, and doPivot's steps are
+// ballots (counts, ranks), shuffles (pivot-of-nine, probe, partner exchange) and two per-wave LDS
+// slot lists (the k-th misplaced element of a segment). No workgroup barriers.
+constexpr uint32_t WQ = 64;
+
+__device__ __forceinline__ uint64_t lmask(uint32_t a, uint32_t b) {  // lanes [a, b), 0 <= a, b <= 64
+  const uint64_t h = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
+  const uint64_t l = a >= 64 ? ~0ull : ((1ull << a) - 1ull);
+  return h & ~l;
+}
+
+// one O(n) loop of doPivot for every active lane segment: range [s+1, z), mode 0 stays left on
+// key >= pl, mode 1 on key > pl; returns the boundary s+1 + #left
+template <int SH, class E>
+__device__ __forceinline__ uint32_t wv_pass(E& v, uint32_t lane, bool act, uint32_t s, uint32_t e, uint32_t z,
+                                            uint32_t pl, int mode, uint8_t* slL, uint8_t* slR) {
+  const uint32_t a = s + 1;
+  const bool inr = act && lane >= a && lane < z;
+  const uint32_t key = KEY<SH>(v);
+  const bool lf = inr && (mode == 0 ? key >= pl : key > pl);
+  const uint64_t BL = __ballot(lf);
+  const uint32_t bnd = a + ((act && z > a) ? (uint32_t)__popcll(BL & lmask(a, z)) : 0u);
+  const bool ml = inr && !lf && lane < bnd, mr = inr && lf && lane >= bnd;
+  const uint64_t BML = __ballot(ml), BMR = __ballot(mr);
+  if (BML) {
+    const uint32_t rl = (uint32_t)__popcll(BML & lmask(s, lane));
+    const uint32_t rr = (uint32_t)__popcll(BMR & lmask(lane + 1, e));
+    if (ml) slL[s + rl] = (uint8_t)lane;
+    if (mr) slR[s + rr] = (uint8_t)lane;
+    wave_sync();
+    uint32_t partner = lane;
+    if (ml) partner = slR[s + rl];
+    if (mr) partner = slL[s + rr];
+    const E pv = __shfl(v, (int)partner);
+    if (ml || mr) v = pv;
+    wave_sync();
+  }
+  return bnd;
+}
+
+template <int SH, class E, class L>
+__device__ void wave_qs(L& S, uint32_t lo, uint32_t hi, int32_t dep0, uint8_t* slL, uint8_t* slR, E* slV) {
+  const uint32_t lane = __lane_id(), n = hi - lo;
+  E v = lane < n ? S.D()[lo + lane] : (E)0;
+  uint32_t s = 0, e = lane < n ? n : 0;  // this lane's segment; e <= s: finished
+  int32_t d = dep0;
+  for (;;) {
+    const uint32_t len = e > s ? e - s : 0u;
+    const bool leaf = len >= 2 && len <= 12;
+    const bool hp = len > 12 && d <= 0;
+    const bool act = len > 12 && d > 0;
+    if (__ballot(leaf)) {  // quickSort's tail: gap-6 shell pass (disjoint pairs), then insertionSort,
+                           // which is the stable sort by Less
+      const E up = __shfl(v, (int)(lane >= 6 ? lane - 6 : lane));
+      const E dn = __shfl(v, (int)(lane + 6 < 64 ? lane + 6 : lane));
+      if (leaf) {
+        if (lane >= s + 6) {
+          if (LT<SH>(v, up)) v = up;
+        } else if (lane + 6 < e) {
+          if (LT<SH>(dn, v)) v = dn;
+        }
+      }
+      const uint32_t k = KEY<SH>(v);
+      uint32_t r = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < 12; j++) {
+        const uint32_t kx = KEY<SH>(__shfl(v, (int)min(s + j, 63u)));
+        r += (s + j < e && (kx > k || (kx == k && s + j < lane))) ? 1u : 0u;
+      }
+      if (leaf) slV[s + r] = v;
+      wave_sync();
+      if (leaf) v = slV[lane];
+      wave_sync();
+    }
+    if (__ballot(hp)) {  // depth budget exhausted: heapSort by the segment's first lane, in LDS
+      if (lane < n) S.D()[lo + lane] = v;
+      wave_sync();
+      if (hp && lane == s) heap_sort<SH>(S.D(), lo + s, lo + e);
+      wave_sync();
+      if (lane < n) v = S.D()[lo + lane];
+    }
+    if (leaf || hp) s = e = lane;
+    if (!__ballot(act)) break;
+    // pivot choice (pivot-of-nine above 40 elements, then medianOfThree), moved into place
+    const uint32_t m = (s + e) >> 1, t = len / 8;
+    const bool nine = act && len > 40;
+    uint32_t P[9];
+    if (nine) {
+      P[0] = s; P[1] = s + t; P[2] = s + 2 * t; P[3] = m - t; P[4] = m; P[5] = m + t;
+      P[6] = e - 1 - 2 * t; P[7] = e - 1 - t; P[8] = e - 1;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 9; j++) P[j] = lane;
+      if (act) {
+        P[0] = s; P[1] = m; P[2] = e - 1;
+      }
+    }
+    E x[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) x[j] = __shfl(v, (int)P[j]);
+    if (nine) {
+      mo3v<SH>(x[0], x[1], x[2]);
+      mo3v<SH>(x[4], x[3], x[5]);
+      mo3v<SH>(x[8], x[7], x[6]);
+      mo3v<SH>(x[0], x[4], x[8]);
+    } else if (act) {
+      mo3v<SH>(x[0], x[1], x[2]);
+    }
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < 9; j++)
+        if (lane == P[j] && (nine || j < 3)) v = x[j];
+    }
+    const uint32_t pl = KEY<SH>(x[0]);
+    // Hoare pass
+    const uint32_t bnd = wv_pass<SH, E>(v, lane, act, s, e, e - 1, pl, 0, slL, slR);
+    // dups probe on positions e-1, bnd, bnd-1, bnd-2, m (distinct whenever it runs) and pivot s
+    uint32_t b = bnd, c = bnd;
+    bool prot = act && e - c < 5;
+    const bool probe = act && !prot && e - c < len / 4;
+    const uint32_t q0 = probe ? e - 1 : lane, q1 = probe ? bnd : lane, q2 = probe ? bnd - 1 : lane,
+                   q3 = probe ? bnd - 2 : lane, q4 = probe ? m : lane, qs = probe ? s : lane;
+    E y0 = __shfl(v, (int)q0), y1 = __shfl(v, (int)q1), y2 = __shfl(v, (int)q2), y3 = __shfl(v, (int)q3),
+      y4 = __shfl(v, (int)q4);
+    const E pv = __shfl(v, (int)qs);
+    if (probe) {
+      auto get = [&](uint32_t p) -> E { return p == q0 ? y0 : p == q1 ? y1 : p == q2 ? y2 : p == q3 ? y3 : y4; };
+      auto set = [&](uint32_t p, E w) {
+        if (p == q0) y0 = w;
+        if (p == q1) y1 = w;
+        if (p == q2) y2 = w;
+        if (p == q3) y3 = w;
+        if (p == q4) y4 = w;
+      };
+      int dups = 0;
+      if (!LT<SH>(pv, get(e - 1))) {  // data[hi-1] = pivot: swap(c, hi-1), c++
+        const E w = get(c);
+        set(c, get(e - 1));
+        set(e - 1, w);
+        c++;
+        dups++;
+      }
+      if (!LT<SH>(get(b - 1), pv)) {  // data[b-1] = pivot
+        b--;
+        dups++;
+      }
+      if (!LT<SH>(get(m), pv)) {  // data[m] = pivot: swap(m, b-1), b--
+        const E w = get(m);
+        set(m, get(b - 1));
+        set(b - 1, w);
+        b--;
+        dups++;
+      }
+      prot = dups > 1;
+      if (lane == q0) v = y0;
+      else if (lane == q1) v = y1;
+      else if (lane == q2) v = y2;
+      else if (lane == q3) v = y3;
+      else if (lane == q4) v = y4;
+    }
+    if (__ballot(prot)) {  // the protect pass over [s+1, b)
+      const uint32_t b2 = wv_pass<SH, E>(v, lane, prot, s, e, b, pl, 1, slL, slR);
+      if (prot) b = b2;
+    }
+    // pivot into its final place b-1; children [s, b-1) and [c, e)
+    const E xs = __shfl(v, (int)(act ? s : lane)), xb = __shfl(v, (int)(act ? b - 1 : lane));
+    if (act) {
+      if (lane == s) v = xb;
+      if (lane == b - 1) v = xs;
+      if (lane < b - 1) e = b - 1;
+      else if (lane >= c) s = c;
+      else s = e = lane;
+      d--;
+    }
+  }
+  if (lane < n) S.D()[lo + lane] = v;
+}
+
+template <class L>
+__device__ __forceinline__ void ls_wave_push(L& S, uint32_t lo, uint32_t hi, int32_t dep) {
+  const uint32_t i = atomicAdd(&S.nw, 1u);
+  S.wl[i] = lo | (hi << 16);
+  S.wd[i] = (int8_t)dep;
 }
 
 template <int SH, class E>
@@ -559,6 +739,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
     if (threadIdx.x == 0) {
       S.flag = 0;
       S.na = 0;
+      S.nw = 0;
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += LS_BLOCK) {
@@ -582,17 +763,19 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
       uint32_t cntA = 0;
       for (uint32_t k = k0; k < k1; k++) {
         const Seg sg = segs[pk.sbeg + k];
-        if (sg.hi - sg.lo > 12 && sg.depth > 0) cntA++;
+        if (sg.hi - sg.lo > WQ && sg.depth > 0) cntA++;
       }
       uint32_t o = block_excl_scan<LS_BLOCK>(cntA, S.red, &tot);
       for (uint32_t k = k0; k < k1; k++) {
         const Seg sg = segs[pk.sbeg + k];
         const uint32_t lo = sg.lo - pk.plo, hi = sg.hi - pk.plo;
-        if (hi - lo > 12 && sg.depth > 0) {
+        if (hi - lo > WQ && sg.depth > 0) {
           S.lo[0][o] = (uint16_t)lo;
           S.hi[0][o] = (uint16_t)hi;
           S.dep[0][o] = (int8_t)sg.depth;
           o++;
+        } else if (hi - lo > 12 && sg.depth > 0) {
+          ls_wave_push(S, lo, hi, sg.depth);
         } else {
           seq_terminal<SH>(S.D(), lo, hi, sg.depth);
         }
@@ -601,6 +784,8 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
       __syncthreads();
     }
     int cur = 0;
+    unsigned long long nlev = 0;
+    (void)nlev;
     unsigned long long tA = GS_T(), tB, tC, tD, tE, tF, tS = tA;
     (void)tB; (void)tC; (void)tD; (void)tE; (void)tF; (void)tS;
     if (threadIdx.x == 0) GS_STAT_ADD(0, 1);
@@ -609,6 +794,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
       if (threadIdx.x == 0) {
         GS_STAT_ADD(1, 1);
         GS_STAT_MAX(10, na);
+        nlev++;
       }
       tA = GS_T();
       // pivot choice, one thread per segment
@@ -647,9 +833,11 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
         const int32_t dep = S.dep[cur][s] - 1;
         swp(S.D(), lo, b - 1);
         S.b[s] = (uint16_t)mlo;  // reuse: child boundaries
-        if (mlo - lo > 12 && dep > 0) cntA++;
+        if (mlo - lo > WQ && dep > 0) cntA++;
+        else if (mlo - lo > 12 && dep > 0) ls_wave_push(S, lo, mlo, dep);
         else seq_terminal<SH>(S.D(), lo, mlo, dep);
-        if (hi - mhi > 12 && dep > 0) cntA++;
+        if (hi - mhi > WQ && dep > 0) cntA++;
+        else if (hi - mhi > 12 && dep > 0) ls_wave_push(S, mhi, hi, dep);
         else seq_terminal<SH>(S.D(), mhi, hi, dep);
       }
       uint32_t tot;
@@ -659,13 +847,13 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
         const uint32_t lo = S.lo[cur][s], hi = S.hi[cur][s];
         const uint32_t mlo = S.b[s], mhi = S.c[s];
         const int32_t dep = S.dep[cur][s] - 1;
-        if (mlo - lo > 12 && dep > 0) {
+        if (mlo - lo > WQ && dep > 0) {
           S.lo[nx][o] = (uint16_t)lo;
           S.hi[nx][o] = (uint16_t)mlo;
           S.dep[nx][o] = (int8_t)dep;
           o++;
         }
-        if (hi - mhi > 12 && dep > 0) {
+        if (hi - mhi > WQ && dep > 0) {
           S.lo[nx][o] = (uint16_t)mhi;
           S.hi[nx][o] = (uint16_t)hi;
           S.dep[nx][o] = (int8_t)dep;
@@ -685,7 +873,22 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
         GS_STAT_ADD(7, tF - tE);
       }
     }
-    if (threadIdx.x == 0) GS_STAT_ADD(2, GS_T() - tS);
+    {  // the wave sorter's segments, one per wave at a time
+      __syncthreads();
+      const uint32_t nw = S.nw, w = threadIdx.x >> 6;
+      uint8_t* scr = reinterpret_cast<uint8_t*>(S.bl) + w * (128 + 64 * sizeof(E));
+      for (uint32_t it = w; it < nw; it += LS_BLOCK / 64) {
+        const uint32_t x = S.wl[it];
+        wave_qs<SH, E>(S, x & 0xFFFFu, x >> 16, S.wd[it], scr, scr + 64, reinterpret_cast<E*>(scr + 128));
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) GS_STAT_ADD(11, nw);
+    }
+    if (threadIdx.x == 0) {
+      GS_STAT_ADD(2, GS_T() - tS);
+      GS_STAT_MAX(16, GS_T() - tS);  // slowest pack: cycles, its levels, its size
+      GS_STAT_MAX(17, ((GS_T() - tS) << 24) | ((unsigned long long)nlev << 14) | n);
+    }
     constexpr E MASK = (E)((1ull << SH) - 1);
     for (uint32_t i = threadIdx.x; i < n; i += LS_BLOCK) perm[pk.plo + i] = pk.plo + (uint32_t)(S.D()[i] & MASK);
     __syncthreads();
@@ -1366,9 +1569,9 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
 #ifdef SYZ_GS_STATS
 extern "C" int syzgpu_debug_gosort_stats(unsigned long long* out, int reset) {
   hipDeviceSynchronize();
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gs_stats), sizeof(unsigned long long) * 16);
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gs_stats), sizeof(unsigned long long) * 24);
   if (reset) {
-    unsigned long long z[16] = {0};
+    unsigned long long z[24] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(g_gs_stats), z, sizeof(z));
   }
   return 0;

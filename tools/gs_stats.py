@@ -22,7 +22,7 @@ np.cumsum(np.bincount(group, minlength=289), out=goff[1:])
 print("largest groups", sorted(np.diff(goff).tolist())[-5:], flush=True)
 L = _lib.lib()
 L.syzgpu_debug_gosort_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
-st = np.zeros(16, np.uint64)
+st = np.zeros(24, np.uint64)
 for it in range(3):
     L.syzgpu_debug_gosort_stats(st.ctypes.data, 1)
     t = time.perf_counter()
@@ -36,5 +36,7 @@ for it in range(3):
     print("  per pack: levels %.1f cycles %.0f | per level: pivot %.0f part0 %.0f probe %.0f part1 %.0f children %.0f"
           % (st[1] / pk, st[2] / pk, st[3] / max(1, st[1]), st[4] / max(1, st[1]), st[5] / max(1, st[1]),
              st[6] / max(1, st[1]), st[7] / max(1, st[1])), flush=True)
-    print("  part0 per level: walkA+atomics %.0f bnd %.0f classify+scan+write %.0f swap %.0f" %
+    print("  part0 per level: walk+scan %.0f bnd %.0f classify+list %.0f swap %.0f" %
           tuple(st[12 + i] / max(1, st[1]) for i in range(4)), flush=True)
+    x = int(st[17])
+    print("  slowest pack: %d cycles, %d levels, %d elements" % (x >> 24, (x >> 14) & 1023, x & 16383), flush=True)
