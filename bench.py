@@ -54,8 +54,10 @@ def parse():
 def kernel_model(name, corp, store_info, C):
     """(bound, algorithmic bytes per launch) of a kernel, SURVEY.md §8(d) / DESIGN.md §3."""
     n, sum_pcs = corp.n, int(corp.off[-1])
-    if name == "vec_min":  # Minimize over the whole local corpus: 4 B per PC + offsets + group id
-        return "hbm", 4 * sum_pcs + 10 * n
+    if name == "vec_min":  # Minimize over the big call groups: 4 B per PC + offsets + group id
+        return "hbm", 4 * store_info["big_pcs"] + 10 * store_info["big_entries"]
+    if name == "vec_min_small":  # the small call groups' Minimize (side stream, overlapped)
+        return "hbm", 4 * (sum_pcs - store_info["big_pcs"]) + 10 * (n - store_info["big_entries"])
     if name == "select_out":
         return "hbm", 10 * n
     if name == "prio_choice":

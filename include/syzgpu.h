@@ -151,8 +151,9 @@ int syzgpu_corpus_destroy(syzgpu_corpus* c);
 int syzgpu_corpus_minimize(syzgpu_corpus* c, int64_t* out_idx, uint64_t* group_out_off);
 int syzgpu_corpus_minimize_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,
                                void* stream);
-/* info[0..6] = entries, calls, PCs, distinct (call, PC) ids, work items, shared window tables,
- * 16-byte id vectors of the stream */
+/* info[0..8] = entries, calls, PCs, distinct (call, PC) ids, work items, shared window tables,
+ * 16-byte id vectors of the stream, entries and PCs of the call groups sorted by the global rounds
+ * (more than 8192 entries) */
 int syzgpu_corpus_info(const syzgpu_corpus* c, uint64_t* info, size_t cap);
 
 /* Per-kernel timing of the last *_dev call (HIP events on the call's stream), for the benchmark's

@@ -180,10 +180,10 @@ class CoverStore:
         return self._h
 
     def info(self):
-        v = np.zeros(7, dtype=np.uint64)
-        check(lib().syzgpu_corpus_info(self._h, ptr(v), 7))
-        return dict(zip(["entries", "calls", "pcs", "ids", "work_items", "shared_tables", "vectors"],
-                        (int(x) for x in v)))
+        v = np.zeros(9, dtype=np.uint64)
+        check(lib().syzgpu_corpus_info(self._h, ptr(v), 9))
+        return dict(zip(["entries", "calls", "pcs", "ids", "work_items", "shared_tables", "vectors",
+                         "big_entries", "big_pcs"], (int(x) for x in v)))
 
     def Minimize(self):
         out = np.empty(max(self.n, 1), dtype=np.int64)

@@ -44,7 +44,7 @@ __device__ unsigned long long g_gs_stats[24];
 #define GS_T() 0ull
 #endif
 
-constexpr uint32_t T_SEG = 8192;   // largest segment sorted in LDS
+constexpr uint32_t T_SEG = GS_T_SEG;  // largest segment sorted in LDS
 constexpr int LS_BLOCK = 512;      // LDS workgroup
 constexpr int LS_ITEMS = T_SEG / LS_BLOCK;
 constexpr int LS_SH = 13;  // local index bits of the packed u32 LDS element (T_SEG = 2^13)
@@ -1365,7 +1365,10 @@ void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ng
   P.npacks = (uint32_t)packs.size();
   P.nbig = (uint32_t)big.size();
   P.big_total = 0;
-  for (const Seg& sg : big) P.big_total += sg.hi - sg.lo;
+  for (const Seg& sg : big) {
+    P.big_total += sg.hi - sg.lo;
+    P.big_max = std::max<uint64_t>(P.big_max, sg.hi - sg.lo);
+  }
   SYZ_HIP(hipMalloc(&P.small, (small.size() + 1) * sizeof(Seg)));
   SYZ_HIP(hipMalloc(&P.packs, (packs.size() + 1) * sizeof(Pack)));
   SYZ_HIP(hipMalloc(&P.big, (big.size() + 1) * sizeof(Seg)));
@@ -1386,7 +1389,8 @@ void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const std::vector<uin
 // Sorts every call group's range (as planned in P) with Go's sort.Sort semantics. Result: the element
 // at sorted position r is el[perm[r]]. Enqueues everything on s; the host only waits for the
 // level-count events of the global levels.
-void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hipStream_t s) {
+void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hipStream_t s,
+                const std::function<void(hipStream_t)>& small_done, const std::function<void(hipStream_t)>& big_done) {
   Context& c = ctx();
   Scratch& sc = c.scratch;
   if (n >= 0xFFFFFFF0ull || n != P.n) fail(SYZGPU_EINVAL, "gosort: plan does not match the elements");
@@ -1424,10 +1428,16 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
       SYZ_HIP(hipEventRecord(c.ev_fork, s));
       SYZ_HIP(hipStreamWaitEvent(ss, c.ev_fork, 0));
     }
-    ProfScope ps("gosort_lds_small", ss, (uint64_t)n * 12);
-    launch_ls<LS_SH, uint32_t>(el, perm, d_packs, P.npacks, nullptr, std::min<uint32_t>(P.npacks, 65535), d_small,
-                            &ctl[2].nnext, bounceS, ss);
+    {
+      ProfScope ps("gosort_lds_small", ss, (uint64_t)n * 12);
+      launch_ls<LS_SH, uint32_t>(el, perm, d_packs, P.npacks, nullptr, std::min<uint32_t>(P.npacks, 65535), d_small,
+                              &ctl[2].nnext, bounceS, ss);
+    }
+    // packs with a length that does not fit the u32 element (>= 2^19 PCs) were bounced: the u64
+    // instantiation sorts them (a launch over an empty bounce list returns at once)
+    launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, ss);
   }
+  if (small_done) small_done(ss);
   if (fork) SYZ_HIP(hipEventRecord(c.ev_join, ss));
   // global levels: the host issues level after level without waiting; each level's segment count is
   // copied back asynchronously and the host stops issuing once a finished level reports zero
@@ -1554,15 +1564,14 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     // the LDS-sized children of all levels, one workgroup each ([0, nlds) via &ctl[0].nnext == 0);
     // running them per level beside the levels was measured slower: they take the CUs the
     // latency-bound level kernels need
-    ProfScope ps2("gosort_lds", s, (uint64_t)n * 12);
-    launch_ls<LS_SH, uint32_t>(el, perm, nullptr, 0, &ctl[0].nnext, 1024, dlds, &ctl[2].nlds, bounceD, s);
+    {
+      ProfScope ps2("gosort_lds", s, (uint64_t)n * 12);
+      launch_ls<LS_SH, uint32_t>(el, perm, nullptr, 0, &ctl[0].nnext, 1024, dlds, &ctl[2].nlds, bounceD, s);
+    }
+    launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nlds, bounceD, s);
   }
+  if (big_done) big_done(s);
   if (fork) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
-  // packs with a length that does not fit the u32 element (>= 2^20 PCs) were bounced: the u64
-  // instantiation sorts them (a launch over an empty bounce list returns at once)
-  if (P.npacks)
-    launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, s);
-  if (P.nbig) launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nnext, bounceD, s);
   (void)dpacks;
 }
 

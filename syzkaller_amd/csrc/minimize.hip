@@ -119,6 +119,18 @@ __global__ void k_ranks(const uint64_t* el, const uint32_t* perm, size_t n, cons
   }
 }
 
+// the same over element ranges given as {lo, hi, ...} records (gosort packs or big call groups):
+// blockIdx.y picks the range, the x blocks stride over it
+__global__ void k_ranks_ranges(const uint64_t* el, const uint32_t* perm, const uint4* ranges, const uint32_t* members,
+                               uint32_t* rank_of_member, uint32_t* ent_of_rank) {
+  const uint4 rg = ranges[blockIdx.y];
+  for (uint32_t r = rg.x + blockIdx.x * blockDim.x + threadIdx.x; r < rg.y; r += gridDim.x * blockDim.x) {
+    const uint32_t gidx = (uint32_t)el[perm[r]];
+    rank_of_member[gidx] = r;
+    ent_of_rank[r] = members[gidx];
+  }
+}
+
 // ---- 3. bucket passes ------------------------------------------------------------------------------
 struct Chunk {
   uint32_t g, mbeg, mend, pad;
@@ -931,9 +943,11 @@ struct Corpus {
   DevArr<uint64_t> off, gstart, gdict;
   DevArr<uint32_t> group, members, nwin, dict, gtabs, vmem;
   DevArr<uint16_t> prog_len, ids16;
-  DevArr<VecWork> work;
+  DevArr<VecWork> work;  // work items of the big call groups first, then those of the small ones
   DevArr<GtabInfo> gtinfo;
   std::vector<VecWork> hwork;
+  size_t nbig_work = 0;                        // work items of the big call groups
+  uint64_t big_entries = 0, big_pcs = 0;       // entries / PCs in call groups above GS_T_SEG
   std::vector<uint64_t> hstart;
   GosortPlan gsplan;
   uint32_t max_prog_len = 0;
@@ -1157,8 +1171,21 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
       for (uint64_t v = vb; v < ve; v += per) K.hwork.push_back(VecWork{g, nids, v, std::min(ve, v + per), gt, 0});
     }
   }
-  std::stable_sort(K.hwork.begin(), K.hwork.end(),
-                   [](const VecWork& x, const VecWork& y) { return x.vend - x.vbeg > y.vend - y.vbeg; });
+  // big call groups (sorted by the global rounds) first, small ones (LDS packs, sorted on the side
+  // stream) after: each class's Minimize runs as soon as its own sort is done
+  auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
+  std::stable_sort(K.hwork.begin(), K.hwork.end(), [&](const VecWork& x, const VecWork& y) {
+    const bool bx = is_big(x.g), by = is_big(y.g);
+    if (bx != by) return bx;
+    return x.vend - x.vbeg > y.vend - y.vbeg;
+  });
+  K.nbig_work = 0;
+  while (K.nbig_work < K.hwork.size() && is_big(K.hwork[K.nbig_work].g)) K.nbig_work++;
+  for (uint32_t g = 0; g < G; g++)
+    if (is_big(g)) {
+      K.big_entries += hstart[g + 1] - hstart[g];
+      K.big_pcs += hpcs[g];
+    }
   K.work.alloc(K.hwork.size());
   if (!K.hwork.empty())
     SYZ_HIP(hipMemcpyAsync(K.work.p, K.hwork.data(), K.hwork.size() * sizeof(VecWork), hipMemcpyHostToDevice, s));
@@ -1206,23 +1233,35 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
       SYZ_LAUNCHED();
     }
   }
-  if (n) gosort_run(el, perm, n, K.gsplan, s);
-  {
-    ProfScope ps("ranks", s, (uint64_t)n * 16);
-    if (n) {
-      k_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(el, perm, n, K.members.p, rank_of_member, ent_of_rank);
+  // ranks + Minimize per class, each right after its own sort: the small call groups' on the side
+  // stream while the big ones still run their global rounds
+  const GosortPlan& P = K.gsplan;
+  auto vec_min = [&](hipStream_t q, size_t first, size_t count) {
+    if (count)
+      k_vec_min<<<(unsigned)count, VM_BLOCK, 0, q>>>(K.work.p + first, reinterpret_cast<const uint4*>(K.ids16.p),
+                                                     K.vmem.p, rank_of_member, K.gstart.p, sel_bits, K.gtabs.p);
+    SYZ_LAUNCHED();
+  };
+  auto small_done = [&](hipStream_t q) {
+    if (P.npacks) {  // a pack holds at most GS_T_SEG elements
+      k_ranks_ranges<<<dim3(GS_T_SEG / 1024, P.npacks), 256, 0, q>>>(
+          el, perm, reinterpret_cast<const uint4*>(P.packs), K.members.p, rank_of_member, ent_of_rank);
       SYZ_LAUNCHED();
     }
-  }
-  {
-    ProfScope ps("vec_min", s, K.total_vecs * 20 + (uint64_t)n * 4);
-    if (!K.hwork.empty()) {
-      k_vec_min<<<(unsigned)K.hwork.size(), VM_BLOCK, 0, s>>>(K.work.p, reinterpret_cast<const uint4*>(K.ids16.p),
-                                                              K.vmem.p, rank_of_member, K.gstart.p, sel_bits,
-                                                              K.gtabs.p);
+    ProfScope ps("vec_min_small", q, (K.total_pcs - K.big_pcs) * 4 + (n - K.big_entries) * 10);
+    vec_min(q, K.nbig_work, K.hwork.size() - K.nbig_work);
+  };
+  auto big_done = [&](hipStream_t q) {
+    if (P.nbig) {
+      const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>(1, P.big_max / 2048), 256);
+      k_ranks_ranges<<<dim3(gx, P.nbig), 256, 0, q>>>(el, perm, reinterpret_cast<const uint4*>(P.big), K.members.p,
+                                                     rank_of_member, ent_of_rank);
       SYZ_LAUNCHED();
     }
-  }
+    ProfScope ps("vec_min", q, K.big_pcs * 4 + K.big_entries * 10);
+    vec_min(q, 0, K.nbig_work);
+  };
+  if (n) gosort_run(el, perm, n, P, s, small_done, big_done);
   if (K.ngtabs) {
     ProfScope ps("gtab_emit", s, (uint64_t)K.ngtabs * WIN * 4);
     k_gtab_emit<<<K.ngtabs, VM_BLOCK, 0, s>>>(K.gtinfo.p, K.gtabs.p, K.gstart.p, sel_bits);
@@ -1310,8 +1349,9 @@ int syzgpu_corpus_info(const syzgpu_corpus* cp, uint64_t* info, size_t cap) {
   SYZ_API_BODY({
     if (!cp || !info) fail(SYZGPU_EINVAL, "null pointer");
     const Corpus& K = *reinterpret_cast<const Corpus*>(cp);
-    const uint64_t v[7] = {K.n, K.G, K.total_pcs, K.total_ids, K.hwork.size(), K.ngtabs, K.total_vecs};
-    for (size_t i = 0; i < cap && i < 7; i++) info[i] = v[i];
+    const uint64_t v[9] = {K.n,      K.G,          K.total_pcs,   K.total_ids,  K.hwork.size(),
+                           K.ngtabs, K.total_vecs, K.big_entries, K.big_pcs};
+    for (size_t i = 0; i < cap && i < 9; i++) info[i] = v[i];
   })
 }
 

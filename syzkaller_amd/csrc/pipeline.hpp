@@ -1,5 +1,7 @@
 // Internal interfaces between the kernels of libsyzgpu.so.
 #pragma once
+#include <functional>
+
 #include "common.hpp"
 
 namespace syz {
@@ -11,11 +13,13 @@ struct Seg {
 };
 
 // gosort.hip: the element at sorted position r of the groups' ranges is el[perm[r]]
+constexpr uint32_t GS_T_SEG = 8192;  // call groups above this many entries start the global rounds
 struct Pack;
 struct GosortPlan {
   size_t n = 0;
   uint32_t nsmall = 0, npacks = 0, nbig = 0;
   uint64_t big_total = 0;  // elements in the groups that start the global levels
+  uint64_t big_max = 0;    // elements in the largest of them
   mutable uint32_t rounds_hint = 0;  // global rounds the last run of this plan needed (issued up front)
   Seg* small = nullptr;
   Pack* packs = nullptr;
@@ -26,7 +30,12 @@ struct GosortPlan {
   ~GosortPlan();
 };
 void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ngroups, hipStream_t s);
-void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hipStream_t s);
+// small_done(q) is enqueued on stream q once the packed (small) call groups are sorted, big_done(q)
+// once the big ones are; both run before gosort_run's streams join, so per-class consumers overlap
+// with the other class's sort.
+void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hipStream_t s,
+                const std::function<void(hipStream_t)>& small_done = {},
+                const std::function<void(hipStream_t)>& big_done = {});
 void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const std::vector<uint64_t>& hstart, uint32_t ngroups,
                    hipStream_t s);
 
