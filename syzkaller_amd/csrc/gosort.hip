@@ -45,8 +45,10 @@ __device__ unsigned long long g_gs_stats[24];
 #endif
 
 constexpr uint32_t T_SEG = GS_T_SEG;  // largest segment sorted in LDS
-constexpr int LS_BLOCK = 512;      // LDS workgroup
-constexpr int LS_ITEMS = T_SEG / LS_BLOCK;
+constexpr int LS_BLOCK = 1024;     // LDS workgroup (16 waves: the wave sorter runs 16 segments at once)
+constexpr int LS_ITEMS = T_SEG / LS_BLOCK;  // elements per thread chunk
+constexpr int LS_ISH = 3;                   // log2(LS_ITEMS)
+static_assert((1 << LS_ISH) == LS_ITEMS, "LS_ISH");
 constexpr int LS_SH = 13;  // local index bits of the packed u32 LDS element (T_SEG = 2^13)
 static_assert((1u << LS_SH) == T_SEG, "LS_SH");
 constexpr uint32_t LS_MAXS = T_SEG / 13 + 4;  // active segments (> 12 elements) per pack
@@ -335,17 +337,17 @@ struct Pack {
   uint32_t sbeg, send;  // its segments in the segment array
 };
 
-// LDS view of the pack's elements with one pad word per 16: a thread's contiguous 16-element chunk
-// then starts on its own bank, so chunk walks are conflict-free (a plain array is 16-way).
+// LDS view of the pack's elements with one pad word per chunk: a thread's contiguous LS_ITEMS-element
+// chunk then starts on its own bank, so chunk walks are conflict-free (a plain array is 8-way).
 template <class E>
 struct PadRef {
   E* v;
-  __device__ __forceinline__ E& operator[](uint32_t i) const { return v[i + (i >> 4)]; }
+  __device__ __forceinline__ E& operator[](uint32_t i) const { return v[i + (i >> LS_ISH)]; }
 };
 
 template <class E>
 struct LsLds {
-  E dv[T_SEG + T_SEG / 16];
+  E dv[T_SEG + T_SEG / LS_ITEMS];
   __device__ __forceinline__ PadRef<E> D() { return PadRef<E>{dv}; }
   uint16_t bl[T_SEG];               // misplaced-right positions, at lo + rank from the right
   uint32_t cpre[LS_BLOCK + 1];      // #left before each chunk (pass scan), [LS_BLOCK] = total
@@ -384,9 +386,9 @@ __device__ __forceinline__ uint32_t seg_at(const L& S, int cur, uint32_t na, uin
 // swaps equal ranks. L comes from ONE workgroup scan of per-chunk left counts (no atomics); the
 // misplaced-right positions go to a list indexed inside the segment's own range, and each
 // misplaced-left element fetches its partner from it and performs the swap.
-// Thread t owns the chunk [16t, 16t+16). Active segments have more than 12 elements, so a chunk
-// meets at most 3 of them (sf .. sf+2).
-// bits j of a 16-element chunk starting at i0 whose position lies in [a, e)
+// Thread t owns the chunk [8t, 8t+8). Active segments have more than WQ elements, so a chunk meets at
+// most 2 of them (the code allows 3: sf .. sf+2).
+// bits j of a chunk starting at i0 whose position lies in [a, e)
 __device__ __forceinline__ uint32_t chunk_range(uint32_t i0, uint32_t a, uint32_t e) {
   const int32_t lo = max(0, min((int32_t)LS_ITEMS, (int32_t)a - (int32_t)i0));
   const int32_t hi = max(0, min((int32_t)LS_ITEMS, (int32_t)e - (int32_t)i0));
@@ -396,7 +398,7 @@ __device__ __forceinline__ uint32_t chunk_range(uint32_t i0, uint32_t a, uint32_
 // #left in [0, p) of the pack (p <= T_SEG), from the chunk prefixes and masks
 template <class L>
 __device__ __forceinline__ uint32_t ls_lpre(const L& S, uint32_t p) {
-  const uint32_t t = p >> 4, j = p & 15u;
+  const uint32_t t = p >> LS_ISH, j = p & (LS_ITEMS - 1u);
   return j ? S.cpre[t] + __popc(S.cmask[t] & ((1u << j) - 1u)) : S.cpre[t];
 }
 
@@ -1017,7 +1019,7 @@ __device__ __forceinline__ void gl_stage(const uint64_t* el, uint32_t t0, uint32
 }
 
 __global__ __launch_bounds__(GL_BLOCK) void k_gr_lists(const uint64_t* el, GLevel cur, const uint32_t* tcnt,
-                                                       uint32_t* A, uint32_t* B) {
+                                                       uint32_t* A, uint32_t* B, uint64_t* VA, uint64_t* VB) {
   __shared__ uint32_t red[GL_BLOCK / 64 + 1];
   __shared__ uint32_t tpre[2];
   __shared__ uint64_t tile[GL_TILE + GL_TILE / 16];
@@ -1064,11 +1066,13 @@ __global__ __launch_bounds__(GL_BLOCK) void k_gr_lists(const uint64_t* el, GLeve
       const uint32_t p = t0 + r0 + i;
       if (!((rbits >> i) & 1u)) continue;
       const bool left = (lbits >> i) & 1u;
-      if (!left && p < bnd) {
+      if (!left && p < bnd) {  // position and value, so the swap kernel only scatters
         A[sg.lo + (p - a) - lp] = p;
+        VA[sg.lo + (p - a) - lp] = tile[r0 + i + (r0 >> 4)];
         nml++;
       } else if (left && p >= bnd) {
         B[sg.lo + T - 1 - lp] = p;
+        VB[sg.lo + T - 1 - lp] = tile[r0 + i + (r0 >> 4)];
       }
       lp += left ? 1u : 0u;
     }
@@ -1266,10 +1270,13 @@ __device__ void gl_tail(uint64_t* el, const Seg& sg, const GLvl& L, GLevel nx, G
 }
 
 // tile t of a segment swaps the pairs k in [t*TILE/2, (t+1)*TILE/2) (ng <= len/2 <= ntile*TILE/2);
-// the last tile of the segment to arrive runs its tail. The swapped elements are stored
-// write-through (agent scope, sc1), so publishing them needs no L2 write-back.
+// the last tile of the segment to arrive runs its tail. The lists carry the values, so a swap is two
+// scattered stores. WT: write-through stores (agent scope, sc1) need no L2 write-back before the
+// arrival; otherwise plain stores and one release fence per workgroup.
+template <bool WT>
 __global__ __launch_bounds__(GL_BLOCK) void k_gr_swap(uint64_t* el, GLevel cur, GLevel nx, const uint32_t* A,
-                                                      const uint32_t* B, GCtl* ctl, Seg* lds, Seg* heap) {
+                                                      const uint32_t* B, const uint64_t* VA, const uint64_t* VB,
+                                                      GCtl* ctl, Seg* lds, Seg* heap) {
   __shared__ uint32_t last;
   const uint32_t ntiles = cur.plan->ntiles;
   for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
@@ -1279,13 +1286,22 @@ __global__ __launch_bounds__(GL_BLOCK) void k_gr_swap(uint64_t* el, GLevel cur, 
     const uint32_t k0 = st.y * (GL_TILE / 2), k1 = min(ng, k0 + GL_TILE / 2);
     for (uint32_t k = k0 + threadIdx.x; k < k1; k += GL_BLOCK) {
       const uint32_t i = A[sg.lo + k], j = B[sg.lo + k];
-      const uint64_t x = el[i], y = el[j];
-      __hip_atomic_store((gu64*)&el[i], y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu64*)&el[j], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t x = VA[sg.lo + k], y = VB[sg.lo + k];
+      if (WT) {
+        __hip_atomic_store((gu64*)&el[i], y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu64*)&el[j], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        el[i] = y;
+        el[j] = x;
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
     __syncthreads();
     if (threadIdx.x == 0) {
+      if (!WT) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       const uint32_t old = __hip_atomic_fetch_add(&cur.done[st.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last = old + 1 == gl_ntiles(sg);
     }
@@ -1405,6 +1421,8 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   Pack* bounceD = sc.get<Pack>("gs_bounceD", maxlds);
   uint32_t* A = sc.get<uint32_t>("gs_A", n + 1);
   uint32_t* B = sc.get<uint32_t>("gs_B", n + 1);
+  uint64_t* VA = sc.get<uint64_t>("gs_VA", n + 1);
+  uint64_t* VB = sc.get<uint64_t>("gs_VB", n + 1);
   // ctl[0]: next-level count (reset by each plan) and the accumulated LDS / heap children;
   // ctl[2]: bounce counters of the static (nnext) and dynamic (nlds) LDS launches; ctl[3]: scratch
   GCtl* ctl = sc.get<GCtl>("gs_ctl", 4);
@@ -1473,19 +1491,24 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     // one round = 3 dependent kernels with fixed arguments per buffer parity; RPG rounds (parity 0,
     // 1, 0, 1) are captured once into a HIP graph and replayed
     constexpr uint32_t RPG = 4;
+    const bool wt = !getenv("SYZGPU_GR_FENCE");  // A/B switch: write-through swaps vs release fence
     auto enqueue_round = [&](hipStream_t q, int parity) {
       const GLevel cur = lvl[parity], nx = lvl[parity ^ 1];
       k_gr_count<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx.plan, tcnt, ctl, c.gr_dev);
       SYZ_LAUNCHED();
-      k_gr_lists<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, tcnt, A, B);
+      k_gr_lists<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, tcnt, A, B, VA, VB);
       SYZ_LAUNCHED();
-      k_gr_swap<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx, A, B, ctl, dlds, heap);
+      if (wt)
+        k_gr_swap<true><<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx, A, B, VA, VB, ctl, dlds, heap);
+      else
+        k_gr_swap<false><<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx, A, B, VA, VB, ctl, dlds, heap);
       SYZ_LAUNCHED();
     };
     const std::vector<const void*> key = {el,          tcnt,        A,           B,           ctl,         dlds,
                                           heap,        lvl[0].segs, lvl[0].lv,   lvl[0].toff, lvl[0].done, lvl[0].tseg,
                                           lvl[0].plan, lvl[1].segs, lvl[1].lv,   lvl[1].toff, lvl[1].done, lvl[1].tseg,
-                                          lvl[1].plan, c.gr_dev,    (const void*)(uintptr_t)tgrid};
+                                          lvl[1].plan, c.gr_dev,    (const void*)(uintptr_t)tgrid,
+                                          VA,          VB,          (const void*)(uintptr_t)wt};
     if (c.gl_key != key) {
       for (auto& row : c.gl_exec)
         for (auto& g : row) {

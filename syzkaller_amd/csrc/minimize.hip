@@ -825,40 +825,45 @@ __device__ __forceinline__ void vec_update(uint32_t* tab, const uint4 q, uint32_
   tab_min(tab, q.w >> 16, R);
 }
 
-// One workgroup per work item: min Go-sort rank per id of one window over a chunk of its stream.
-__global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict__ work, const uint4* __restrict__ ids16,
+// One workgroup per work item (grid-stride over the items, so a launch can be held to part of the
+// chip): min Go-sort rank per id of one window over a chunk of its stream.
+__global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict__ work, uint32_t nitems,
+                                                      const uint4* __restrict__ ids16,
                                                       const uint32_t* __restrict__ vmem,
                                                       const uint32_t* __restrict__ rank_of_member,
                                                       const uint64_t* __restrict__ gstart, uint32_t* sel_bits,
                                                       uint32_t* gtabs) {
   __shared__ uint32_t tab[WIN];
   __shared__ uint32_t bm[BM_WORDS];
-  const VecWork w = work[blockIdx.x];
-  for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) tab[i] = RANK_NONE;
-  __syncthreads();
-  uint64_t v = w.vbeg + threadIdx.x;
-  // four vectors in flight per lane
-  for (; v + 3 * VM_BLOCK < w.vend; v += 4 * VM_BLOCK) {
-    const uint4 q0 = ids16[v], q1 = ids16[v + VM_BLOCK], q2 = ids16[v + 2 * VM_BLOCK], q3 = ids16[v + 3 * VM_BLOCK];
-    const uint32_t m0 = vmem[v], m1 = vmem[v + VM_BLOCK], m2 = vmem[v + 2 * VM_BLOCK], m3 = vmem[v + 3 * VM_BLOCK];
-    const uint32_t r0 = rank_of_member[m0], r1 = rank_of_member[m1], r2 = rank_of_member[m2],
-                   r3 = rank_of_member[m3];
-    vec_update(tab, q0, r0);
-    vec_update(tab, q1, r1);
-    vec_update(tab, q2, r2);
-    vec_update(tab, q3, r3);
-  }
-  for (; v < w.vend; v += VM_BLOCK) vec_update(tab, ids16[v], rank_of_member[vmem[v]]);
-  __syncthreads();
-  if (w.gtab == RANK_NONE) {
-    const uint64_t gb = gstart[w.g];
-    emit_winners(tab, w.nids, gb, gstart[w.g + 1] - gb, bm, sel_bits);
-  } else {
-    uint32_t* gt = gtabs + (size_t)w.gtab * WIN;
-    for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) {
-      const uint32_t r = tab[i];
-      if (r != RANK_NONE && gt[i] > r) atomicMin(&gt[i], r);
+  for (uint32_t wi = blockIdx.x; wi < nitems; wi += gridDim.x) {
+    const VecWork w = work[wi];
+    for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) tab[i] = RANK_NONE;
+    __syncthreads();
+    uint64_t v = w.vbeg + threadIdx.x;
+    // four vectors in flight per lane
+    for (; v + 3 * VM_BLOCK < w.vend; v += 4 * VM_BLOCK) {
+      const uint4 q0 = ids16[v], q1 = ids16[v + VM_BLOCK], q2 = ids16[v + 2 * VM_BLOCK], q3 = ids16[v + 3 * VM_BLOCK];
+      const uint32_t m0 = vmem[v], m1 = vmem[v + VM_BLOCK], m2 = vmem[v + 2 * VM_BLOCK], m3 = vmem[v + 3 * VM_BLOCK];
+      const uint32_t r0 = rank_of_member[m0], r1 = rank_of_member[m1], r2 = rank_of_member[m2],
+                     r3 = rank_of_member[m3];
+      vec_update(tab, q0, r0);
+      vec_update(tab, q1, r1);
+      vec_update(tab, q2, r2);
+      vec_update(tab, q3, r3);
     }
+    for (; v < w.vend; v += VM_BLOCK) vec_update(tab, ids16[v], rank_of_member[vmem[v]]);
+    __syncthreads();
+    if (w.gtab == RANK_NONE) {
+      const uint64_t gb = gstart[w.g];
+      emit_winners(tab, w.nids, gb, gstart[w.g + 1] - gb, bm, sel_bits);
+    } else {
+      uint32_t* gt = gtabs + (size_t)w.gtab * WIN;
+      for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) {
+        const uint32_t r = tab[i];
+        if (r != RANK_NONE && gt[i] > r) atomicMin(&gt[i], r);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1236,10 +1241,14 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   // ranks + Minimize per class, each right after its own sort: the small call groups' on the side
   // stream while the big ones still run their global rounds
   const GosortPlan& P = K.gsplan;
-  auto vec_min = [&](hipStream_t q, size_t first, size_t count) {
+  // the small class runs beside the big class's latency-bound global rounds: it is held to part of
+  // the chip (its workgroups fill a CU's LDS), so the rounds keep CUs to run on
+  static const unsigned side_cus = getenv("SYZGPU_SIDE_CUS") ? (unsigned)atoi(getenv("SYZGPU_SIDE_CUS")) : 128u;
+  auto vec_min = [&](hipStream_t q, size_t first, size_t count, unsigned max_grid) {
     if (count)
-      k_vec_min<<<(unsigned)count, VM_BLOCK, 0, q>>>(K.work.p + first, reinterpret_cast<const uint4*>(K.ids16.p),
-                                                     K.vmem.p, rank_of_member, K.gstart.p, sel_bits, K.gtabs.p);
+      k_vec_min<<<(unsigned)std::min<size_t>(count, max_grid), VM_BLOCK, 0, q>>>(
+          K.work.p + first, (uint32_t)count, reinterpret_cast<const uint4*>(K.ids16.p), K.vmem.p, rank_of_member,
+          K.gstart.p, sel_bits, K.gtabs.p);
     SYZ_LAUNCHED();
   };
   auto small_done = [&](hipStream_t q) {
@@ -1249,7 +1258,7 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
       SYZ_LAUNCHED();
     }
     ProfScope ps("vec_min_small", q, (K.total_pcs - K.big_pcs) * 4 + (n - K.big_entries) * 10);
-    vec_min(q, K.nbig_work, K.hwork.size() - K.nbig_work);
+    vec_min(q, K.nbig_work, K.hwork.size() - K.nbig_work, side_cus);
   };
   auto big_done = [&](hipStream_t q) {
     if (P.nbig) {
@@ -1259,7 +1268,7 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
       SYZ_LAUNCHED();
     }
     ProfScope ps("vec_min", q, K.big_pcs * 4 + K.big_entries * 10);
-    vec_min(q, 0, K.nbig_work);
+    vec_min(q, 0, K.nbig_work, 1u << 20);
   };
   if (n) gosort_run(el, perm, n, P, s, small_done, big_done);
   if (K.ngtabs) {
