@@ -320,6 +320,48 @@ __global__ __launch_bounds__(256) void k_select_out(const uint32_t* sel_bits, ui
   }
 }
 
+// Store path: kept flags in ENTRY order (coalesced stores; the rank-ordered form walks a permutation)
+// and the len(p.Calls) histogram of kept programs of the groups this rank counts (count_hist[g]).
+__global__ __launch_bounds__(256) void k_select_store(const uint32_t* sel_bits, const uint32_t* member_of,
+                                                      const uint32_t* rank_of_member, size_t n,
+                                                      const uint16_t* prog_len, const uint32_t* group,
+                                                      const uint8_t* count_hist, int32_t C, uint8_t* selected,
+                                                      int64_t* hist, int* err) {
+  extern __shared__ unsigned long long lh[];
+  const bool do_hist = hist != nullptr;
+  if (do_hist) {
+    for (int32_t i = threadIdx.x; i <= C; i += blockDim.x) lh[i] = 0;
+    __syncthreads();
+  }
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t r = rank_of_member[member_of[e]];
+    const uint32_t s = (sel_bits[r >> 5] >> (r & 31)) & 1u;
+    if (selected) selected[e] = (uint8_t)s;
+    if (do_hist && s && (!count_hist || count_hist[group[e]])) {
+      const uint32_t L = prog_len[e];
+      if ((int32_t)L > C)
+        atomicOr(err, 2);
+      else
+        atomicAdd(&lh[L], 1ull);
+    }
+  }
+  if (do_hist) {
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i <= C; i += blockDim.x)
+      if (lh[i]) atomicAdd((unsigned long long*)&hist[i], lh[i]);
+  }
+}
+
+__global__ void k_bits_to_bytes(const uint32_t* bits, size_t n, uint8_t* out) {
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
+    out[r] = (uint8_t)((bits[r >> 5] >> (r & 31)) & 1u);
+}
+
+__global__ void k_invert(const uint32_t* members, size_t n, uint32_t* member_of) {
+  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x)
+    member_of[members[m]] = (uint32_t)m;
+}
+
 __global__ void k_compact_ranks(const uint8_t* sel_rank, const uint64_t* pos, const uint32_t* ent_of_rank, size_t n,
                                 int64_t* out) {
   for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
@@ -351,6 +393,7 @@ struct MinState {
   uint64_t* gstart = nullptr;
   uint8_t* sel_rank = nullptr;
   uint32_t* ent_of_rank = nullptr;
+  const uint32_t* sel_bits = nullptr;  // store path: sel_rank is expanded from these on fetch
 };
 static MinState g_min;
 
@@ -480,6 +523,7 @@ void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   g_min.gstart = gstart;
   g_min.sel_rank = sel_rank;
   g_min.ent_of_rank = ent_of_rank;
+  g_min.sel_bits = nullptr;
   c.last_n = n;
   c.last_groups = G;
   c.have_last = true;
@@ -491,6 +535,10 @@ void minimize_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n, uint32_
   uint64_t* pos = c.scratch.get<uint64_t>("mz_pos", n + 1);
   int64_t* dout = c.scratch.get<int64_t>("mz_out", n + 1);
   uint64_t* dgoff = c.scratch.get<uint64_t>("mz_goff", G + 1);
+  if (g_min.sel_bits && n) {
+    k_bits_to_bytes<<<grid_for(n, 256, 4096), 256, 0, s>>>(g_min.sel_bits, n, g_min.sel_rank);
+    SYZ_LAUNCHED();
+  }
   exclusive_scan_u8(g_min.sel_rank, pos, n, s);
   if (n) {
     k_compact_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(g_min.sel_rank, pos, g_min.ent_of_rank, n, dout);
@@ -781,6 +829,7 @@ constexpr int VM_BLOCK = 1024;
 // Winning ranks of a window table (LDS or global) -> set bits of sel_bits (global rank bitmap).
 // Ranks of call g lie in [gstart[g], gstart[g+1]); they are deduplicated through an LDS bitmap so
 // that each kept input costs one bit-OR per table instead of one store per id.
+template <bool ATOMIC_READ = false>
 __device__ __forceinline__ void emit_winners(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
                                              uint32_t* bm, uint32_t* sel_bits) {
   for (uint64_t base = 0; base < ng; base += (uint64_t)BM_WORDS * 32) {
@@ -789,7 +838,7 @@ __device__ __forceinline__ void emit_winners(const uint32_t* tab, uint32_t nids,
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
-      const uint32_t r = tab[i];
+      const uint32_t r = ATOMIC_READ ? __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tab[i];
       if (r == RANK_NONE) continue;
       const uint64_t lr = (uint64_t)r - gbase - base;
       if (lr < span) atomicOr(&bm[lr >> 5], 1u << (lr & 31));
@@ -832,9 +881,10 @@ __global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict_
                                                       const uint32_t* __restrict__ vmem,
                                                       const uint32_t* __restrict__ rank_of_member,
                                                       const uint64_t* __restrict__ gstart, uint32_t* sel_bits,
-                                                      uint32_t* gtabs) {
+                                                      uint32_t* gtabs, const uint32_t* gtchunks, uint32_t* gtdone) {
   __shared__ uint32_t tab[WIN];
   __shared__ uint32_t bm[BM_WORDS];
+  __shared__ uint32_t last;
   for (uint32_t wi = blockIdx.x; wi < nitems; wi += gridDim.x) {
     const VecWork w = work[wi];
     for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) tab[i] = RANK_NONE;
@@ -860,24 +910,29 @@ __global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict_
       uint32_t* gt = gtabs + (size_t)w.gtab * WIN;
       for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) {
         const uint32_t r = tab[i];
-        if (r != RANK_NONE && gt[i] > r) atomicMin(&gt[i], r);
+        if (r != RANK_NONE && __hip_atomic_load(&gt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > r)
+          __hip_atomic_fetch_min(&gt[i], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // the last chunk of a split panel to arrive emits the shared table's winners. The table is
+      // written and read only by agent-scope atomics, so the hand-off needs no cache fences: every
+      // wave's atomics are complete (vmcnt) before the arrival is counted.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(&gtdone[w.gtab], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old + 1 == gtchunks[w.gtab];
+      }
+      __syncthreads();
+      if (last) {
+        const uint64_t gb = gstart[w.g];
+        emit_winners<true>(gt, w.nids, gb, gstart[w.g + 1] - gb, bm, sel_bits);
       }
     }
     __syncthreads();
   }
 }
 
-struct GtabInfo {
-  uint32_t g, nids;
-};
 
-__global__ __launch_bounds__(VM_BLOCK) void k_gtab_emit(const GtabInfo* info, const uint32_t* gtabs,
-                                                        const uint64_t* gstart, uint32_t* sel_bits) {
-  __shared__ uint32_t bm[BM_WORDS];
-  const GtabInfo t = info[blockIdx.x];
-  const uint64_t gb = gstart[t.g];
-  emit_winners(gtabs + (size_t)blockIdx.x * WIN, t.nids, gb, gstart[t.g + 1] - gb, bm, sel_bits);
-}
 
 // vcount[tbase[g] + w * N_g + mloc] = vectors of member m's slice in window w
 __global__ void k_vcount(const uint32_t* members, const uint32_t* group, const uint64_t* gstart, size_t n,
@@ -946,10 +1001,10 @@ struct Corpus {
   uint32_t G = 0;
   uint64_t total_pcs = 0, total_ids = 0, total_vecs = 0;
   DevArr<uint64_t> off, gstart, gdict;
-  DevArr<uint32_t> group, members, nwin, dict, gtabs, vmem;
+  DevArr<uint32_t> group, members, member_of, nwin, dict, gtabs, vmem;
+  DevArr<uint32_t> gtchunks, gtdone;  // work items per shared window table, and their arrivals
   DevArr<uint16_t> prog_len, ids16;
   DevArr<VecWork> work;  // work items of the big call groups first, then those of the small ones
-  DevArr<GtabInfo> gtinfo;
   std::vector<VecWork> hwork;
   size_t nbig_work = 0;                        // work items of the big call groups
   uint64_t big_entries = 0, big_pcs = 0;       // entries / PCs in call groups above GS_T_SEG
@@ -958,8 +1013,9 @@ struct Corpus {
   uint32_t max_prog_len = 0;
   uint32_t ngtabs = 0;
   ~Corpus() {
-    off.free(); gstart.free(); gdict.free(); group.free(); members.free(); nwin.free(); dict.free();
-    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free(); gtinfo.free();
+    off.free(); gstart.free(); gdict.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
+    gtchunks.free(); gtdone.free();
+    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free();
   }
 };
 
@@ -1013,6 +1069,11 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   if (n) {
     const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
     k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, cnt_scan, K.members.p, el);
+    SYZ_LAUNCHED();
+  }
+  K.member_of.alloc(n);
+  if (n) {
+    k_invert<<<grid_for(n, 256, 4096), 256, 0, s>>>(K.members.p, n, K.member_of.p);
     SYZ_LAUNCHED();
   }
   std::vector<uint64_t> hstart(G + 1), hpcs(G);
@@ -1158,7 +1219,6 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   K.ngtabs = 0;
   uint64_t chunk_vecs = CHUNK_VECS;
   if (const char* cv = getenv("SYZGPU_CHUNK_VECS")) chunk_vecs = std::max<uint64_t>(1, strtoull(cv, nullptr, 10));
-  std::vector<GtabInfo> hgt;
   size_t pi = 0;
   for (uint32_t g = 0; g < G; g++) {
     const uint64_t p_g = hgdict[g + 1] - hgdict[g];
@@ -1170,7 +1230,6 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
       uint32_t gt = RANK_NONE;
       if (nch > 1) {
         gt = K.ngtabs++;
-        hgt.push_back(GtabInfo{g, nids});
       }
       const uint64_t per = (ve - vb + nch - 1) / nch;
       for (uint64_t v = vb; v < ve; v += per) K.hwork.push_back(VecWork{g, nids, v, std::min(ve, v + per), gt, 0});
@@ -1195,9 +1254,14 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   if (!K.hwork.empty())
     SYZ_HIP(hipMemcpyAsync(K.work.p, K.hwork.data(), K.hwork.size() * sizeof(VecWork), hipMemcpyHostToDevice, s));
   K.gtabs.alloc((size_t)K.ngtabs * WIN);
-  K.gtinfo.alloc(hgt.size());
-  if (!hgt.empty())
-    SYZ_HIP(hipMemcpyAsync(K.gtinfo.p, hgt.data(), hgt.size() * sizeof(GtabInfo), hipMemcpyHostToDevice, s));
+  {  // work items per shared table: the vec_min chunk that brings the count to it emits the table
+    std::vector<uint32_t> hch(K.ngtabs, 0);
+    for (const VecWork& w : K.hwork)
+      if (w.gtab != RANK_NONE) hch[w.gtab]++;
+    K.gtchunks.alloc(K.ngtabs);
+    K.gtdone.alloc(K.ngtabs);
+    if (K.ngtabs) SYZ_HIP(hipMemcpy(K.gtchunks.p, hch.data(), K.ngtabs * 4, hipMemcpyHostToDevice));
+  }
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   if (herr[0] & 4) fail(SYZGPU_EINTERNAL, "coverstore: hash bucket overflow");
@@ -1230,7 +1294,10 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   uint32_t* sel_bits = sc.get<uint32_t>("mz_selbits", n / 32 + 2);
   SYZ_HIP(hipMemsetAsync(sel_bits, 0, (n / 32 + 2) * 4, s));
   if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
-  if (K.ngtabs) SYZ_HIP(hipMemsetAsync(K.gtabs.p, 0xFF, (size_t)K.ngtabs * WIN * 4, s));
+  if (K.ngtabs) {
+    SYZ_HIP(hipMemsetAsync(K.gtabs.p, 0xFF, (size_t)K.ngtabs * WIN * 4, s));
+    SYZ_HIP(hipMemsetAsync(K.gtdone.p, 0, (size_t)K.ngtabs * 4, s));
+  }
   {
     ProfScope ps("el_init", s, (uint64_t)n * 20);
     if (n) {
@@ -1248,7 +1315,7 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
     if (count)
       k_vec_min<<<(unsigned)std::min<size_t>(count, max_grid), VM_BLOCK, 0, q>>>(
           K.work.p + first, (uint32_t)count, reinterpret_cast<const uint4*>(K.ids16.p), K.vmem.p, rank_of_member,
-          K.gstart.p, sel_bits, K.gtabs.p);
+          K.gstart.p, sel_bits, K.gtabs.p, K.gtchunks.p, K.gtdone.p);
     SYZ_LAUNCHED();
   };
   auto small_done = [&](hipStream_t q) {
@@ -1271,22 +1338,19 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
     vec_min(q, 0, K.nbig_work, 1u << 20);
   };
   if (n) gosort_run(el, perm, n, P, s, small_done, big_done);
-  if (K.ngtabs) {
-    ProfScope ps("gtab_emit", s, (uint64_t)K.ngtabs * WIN * 4);
-    k_gtab_emit<<<K.ngtabs, VM_BLOCK, 0, s>>>(K.gtinfo.p, K.gtabs.p, K.gstart.p, sel_bits);
-    SYZ_LAUNCHED();
-  }
   {
     ProfScope ps("select_out", s, (uint64_t)n * 8);
     if (n) {
-      k_select_out<true><<<grid_for(n, 256, 2048), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
-          sel_bits, sel_rank, ent_of_rank, n, len_hist ? K.prog_len.p : nullptr, C, selected, len_hist, err);
+      k_select_store<<<grid_for(n, 256, 512), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
+          sel_bits, K.member_of.p, rank_of_member, n, len_hist ? K.prog_len.p : nullptr, K.group.p, nullptr, C,
+          selected, len_hist, err);
       SYZ_LAUNCHED();
     }
   }
   g_min.gstart = K.gstart.p;
   g_min.sel_rank = sel_rank;
   g_min.ent_of_rank = ent_of_rank;
+  g_min.sel_bits = sel_bits;
   c.last_n = n;
   c.last_groups = G;
   c.have_last = true;
