@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="programs in the CPU baseline sample")
     ap.add_argument("--profile", type=int, default=1, help="per-kernel HIP event timing in the timed region")
     ap.add_argument("--raw-steps", type=int, default=2, help="also time Minimize from the raw CSR (no store)")
+    ap.add_argument("--split-largest", type=int, default=0,
+                    help="rehearsal: force the largest call group into this many PC-key parts")
     ap.add_argument("--emulate", default="", help="W:r — rehearsal: run rank r's shard of a W-rank job on this "
                     "one process (no collectives; the printed line is that rank's time, not a job value)")
     return ap.parse_args()
@@ -54,8 +56,10 @@ def parse():
 def kernel_model(name, corp, store_info, C):
     """(bound, algorithmic bytes per launch) of a kernel, SURVEY.md §8(d) / DESIGN.md §3."""
     n, sum_pcs = corp.n, int(corp.off[-1])
-    if name == "vec_min":  # Minimize over the big call groups: 4 B per PC + offsets + group id
-        return "hbm", 4 * store_info["big_pcs"] + 10 * store_info["big_entries"]
+    if name == "vec_min":  # Minimize over the big call groups (this rank's PC-key parts of them): 4 B per
+        # PC + offsets + group id
+        share = store_info["big_vecs"] / max(1, store_info["big_vecs_all"])
+        return "hbm", int(4 * store_info["big_pcs"] * share) + 10 * store_info["big_entries"]
     if name == "vec_min_small":  # the small call groups' Minimize (side stream, overlapped)
         return "hbm", 4 * (sum_pcs - store_info["big_pcs"]) + 10 * (n - store_info["big_entries"])
     if name == "select_out":
@@ -137,8 +141,14 @@ def main():
     C, G = args.calls, args.ngroups
     p = synth.params(args.seed, args.progs_per_gpu * emu_world, G, args.npcs)
     group, off, plen = synth.layout(p)
-    owner, load = sharding.lpt_assign(sharding.group_weights(group, off, G), emu_world)
-    ids = sharding.local_entries(group, owner, emu_rank)
+    # key-space sharding plan: call groups whole or split by dense-PC windows over ranks
+    ent_g, pcs_g = sharding.layout_stats(group, off, G)
+    plan = sharding.plan_parts(ent_g, pcs_g, emu_world)
+    if args.split_largest > 1:
+        k = np.ones(G, np.int64)
+        k[int(np.argmax(ent_g))] = min(args.split_largest, emu_world)
+        plan = sharding.KeyPlan(*sharding._assign(ent_g, pcs_g, k, emu_world), ent_g)
+    ids = plan.local_entries(group, emu_rank)
     corp = synth.subcorpus(p, ids, group, off, plen)
     gen_s = time.time() - t0
 
@@ -163,6 +173,13 @@ def main():
     store = cover.CoverStore.from_device(d_pcs, d_off, d_grp, d_len, corp.n, G, sptr)
     torch.cuda.synchronize()
     ingest_s = time.perf_counter() - t_ing
+    part, nparts, count_hist = plan.store_parts(emu_rank)
+    split_g, split_off, split_bytes = plan.split_groups()
+    held = plan.held(emu_rank)
+    xg, xo = split_g[held[split_g]], split_off[held[split_g]]
+    if split_g.size:
+        store.set_parts(part, nparts, count_hist)
+    d_x = torch.zeros(max(split_bytes, 1), dtype=torch.uint8, device=dev)
     store_info = store.info()
 
     def step_raw():
@@ -171,8 +188,18 @@ def main():
                                                  d_hist.data_ptr(), sptr))
 
     def step():
-        _lib.check(L.syzgpu_corpus_minimize_dev(store.handle, C, d_sel.data_ptr(), d_hist.data_ptr(), sptr))
-        sharding.allreduce_hist(d_hist, dist)  # the one exchange: (C+1) int64
+        if split_g.size:  # split groups: OR the partial selections across their ranks
+            store.minimize_begin(sptr)
+            d_x.zero_()
+            if xg.size:
+                store.export_sel(xg, xo, d_x, sptr)
+            sharding.allreduce_max_u8(d_x, dist)
+            if xg.size:
+                store.import_sel(xg, xo, d_x, sptr)
+            store.minimize_end(C, d_sel, d_hist, sptr)
+        else:
+            _lib.check(L.syzgpu_corpus_minimize_dev(store.handle, C, d_sel.data_ptr(), d_hist.data_ptr(), sptr))
+        sharding.allreduce_hist(d_hist, dist)  # kept-length histogram: (C+1) int64
         _lib.check(L.syzgpu_prio_choice_dev(d_static.data_ptr(), d_hist.data_ptr(), C, None, d_prios.data_ptr(),
                                             d_run.data_ptr(), d_pres.data_ptr(), sptr))
 
@@ -237,13 +264,7 @@ def main():
         elapsed = float(t.item())
 
     total_progs = args.progs_per_gpu * world
-    sum_pcs = int(corp.off[-1])
-    if world > 1:
-        tt = torch.tensor([sum_pcs], dtype=torch.int64, device=dev)
-        sharding.allreduce(tt, dist)
-        sum_pcs_all = int(tt.item())
-    else:
-        sum_pcs_all = sum_pcs
+    sum_pcs_all = int(off[-1])  # the whole job's corpus (a split group is held by several ranks)
     ms_step = elapsed / args.steps * 1e3
     value = total_progs * args.steps / elapsed
 
@@ -256,7 +277,7 @@ def main():
             roof = roofline(roof_ev, corp, store_info, C)
             if roof and kern:
                 roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
-        path_bytes = 4 * sum_pcs_all + 10 * total_progs + 16 * C * C
+        path_bytes = 4 * int(off[-1]) + 10 * total_progs + 16 * C * C  # the whole job's corpus
         cpu = None
         if args.cpu_baseline and world == 1:
             cpu = cpu_baseline(corp, st, min(args.cpu_sample, corp.n))
@@ -268,8 +289,11 @@ def main():
             "config": {"workload": "config4-1M: 1M programs/GPU, 2M-PC space, 289 calls, C=1159",
                        "progs_per_gpu": args.progs_per_gpu, "total_progs": total_progs,
                        "sum_pcs": sum_pcs_all, "ngroups": G, "npcs": args.npcs, "calls": C,
-                       "parallelism": "call-group sharded x%d + RCCL all-reduce of the length histogram" % world,
-                       "max_rank_load_share": round(float(load.max() / load.sum()), 4)},
+                       "parallelism": "call groups sharded x%d, %d split by PC-key windows (RCCL MAX all-reduce "
+                                      "of %d selection bytes) + RCCL all-reduce of the length histogram"
+                                      % (world, int(split_g.size), split_bytes),
+                       "modelled_rank_us": [round(float(x), 1) for x in plan.cost],
+                       "split_groups": {int(g): list(plan.ranks[g]) for g in split_g}},
             "roofline": roof,
             "path_roofline": {"bytes_per_step": path_bytes,
                               "achieved": round(path_bytes / (ms_step * 1e-3) / 1e9, 1),

@@ -151,10 +151,30 @@ int syzgpu_corpus_destroy(syzgpu_corpus* c);
 int syzgpu_corpus_minimize(syzgpu_corpus* c, int64_t* out_idx, uint64_t* group_out_off);
 int syzgpu_corpus_minimize_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,
                                void* stream);
-/* info[0..8] = entries, calls, PCs, distinct (call, PC) ids, work items, shared window tables,
+/* info[0..10] = entries, calls, PCs, distinct (call, PC) ids, work items, shared window tables,
  * 16-byte id vectors of the stream, entries and PCs of the call groups sorted by the global rounds
- * (more than 8192 entries) */
+ * (more than 8192 entries), id vectors of those groups in this store's key parts / in all */
 int syzgpu_corpus_info(const syzgpu_corpus* c, uint64_t* info, size_t cap);
+
+/* Key-space sharding of minimizeCorpus over ranks (the multi-GPU form of manager.go:523-527; no
+ * reference counterpart). part/nparts per call group (NULL or nparts[g] <= 1: the
+ * whole group): this store runs Minimize over part[g] of the group's dense-PC windows only. An input
+ * is kept iff SOME of its PCs first occurs at it, so the partial selections of a group OR together
+ * (syzgpu_corpus_export_sel_dev -> a MAX all-reduce -> syzgpu_corpus_import_sel_dev) to the full one.
+ * count_hist[g] (NULL: all) says which groups this rank adds to len_hist (one rank per split group). */
+int syzgpu_corpus_set_parts(syzgpu_corpus* c, const uint16_t* part, const uint16_t* nparts,
+                            const uint8_t* count_hist);
+/* syzgpu_corpus_minimize_dev in two halves around that exchange: _begin sorts and runs the
+ * first-occurrence pass; _end writes the kept flags and the length histogram. */
+int syzgpu_corpus_minimize_begin_dev(syzgpu_corpus* c, void* stream);
+int syzgpu_corpus_minimize_end_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,
+                                   void* stream);
+/* The selection of groups[0..ngroups) (host array) as one byte per group-relative rank, at device
+ * buffer offsets offsets[j] (host array); import ORs the bytes back into the selection. */
+int syzgpu_corpus_export_sel_dev(syzgpu_corpus* c, const uint32_t* groups, const uint64_t* offsets,
+                                 uint32_t ngroups, uint8_t* buf, void* stream);
+int syzgpu_corpus_import_sel_dev(syzgpu_corpus* c, const uint32_t* groups, const uint64_t* offsets,
+                                 uint32_t ngroups, const uint8_t* buf, void* stream);
 
 /* Per-kernel timing of the last *_dev call (HIP events on the call's stream), for the benchmark's
  * roofline. names/ms arrays of capacity cap; returns the number of kernels recorded. */

@@ -180,10 +180,34 @@ class CoverStore:
         return self._h
 
     def info(self):
-        v = np.zeros(9, dtype=np.uint64)
-        check(lib().syzgpu_corpus_info(self._h, ptr(v), 9))
+        v = np.zeros(11, dtype=np.uint64)
+        check(lib().syzgpu_corpus_info(self._h, ptr(v), 11))
         return dict(zip(["entries", "calls", "pcs", "ids", "work_items", "shared_tables", "vectors",
-                         "big_entries", "big_pcs"], (int(x) for x in v)))
+                         "big_entries", "big_pcs", "big_vecs", "big_vecs_all"], (int(x) for x in v)))
+
+    # ---- key-space sharding (the multi-GPU form of minimizeCorpus, syzkaller_amd/sharding.py) ----
+    def set_parts(self, part, nparts, count_hist=None):
+        """Keep part[g] of nparts[g] of every call group's dense-PC windows (see syzgpu.h)."""
+        part = np.ascontiguousarray(part, dtype=np.uint16)
+        nparts = np.ascontiguousarray(nparts, dtype=np.uint16)
+        ch = None if count_hist is None else np.ascontiguousarray(count_hist, dtype=np.uint8)
+        check(lib().syzgpu_corpus_set_parts(self._h, ptr(part), ptr(nparts), ptr(ch)))
+
+    def minimize_begin(self, stream=0):
+        check(lib().syzgpu_corpus_minimize_begin_dev(self._h, stream))
+
+    def export_sel(self, groups, offsets, buf, stream=0):
+        g = np.ascontiguousarray(groups, dtype=np.uint32)
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        check(lib().syzgpu_corpus_export_sel_dev(self._h, ptr(g), ptr(o), g.size, ptr(buf), stream))
+
+    def import_sel(self, groups, offsets, buf, stream=0):
+        g = np.ascontiguousarray(groups, dtype=np.uint32)
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        check(lib().syzgpu_corpus_import_sel_dev(self._h, ptr(g), ptr(o), g.size, ptr(buf), stream))
+
+    def minimize_end(self, C, selected=None, len_hist=None, stream=0):
+        check(lib().syzgpu_corpus_minimize_end_dev(self._h, C, ptr(selected), ptr(len_hist), stream))
 
     def Minimize(self):
         out = np.empty(max(self.n, 1), dtype=np.int64)

@@ -821,7 +821,7 @@ struct VecWork {
   uint32_t nids;  // ids in this window (<= WIN)
   uint64_t vbeg, vend;
   uint32_t gtab;  // RANK_NONE: sole chunk of its panel, emit directly; else index of a global table
-  uint32_t pad;
+  uint32_t win;   // id window of the panel (the unit of key-space sharding)
 };
 
 constexpr int VM_BLOCK = 1024;
@@ -875,7 +875,9 @@ __device__ __forceinline__ void vec_update(uint32_t* tab, const uint4 q, uint32_
 }
 
 // One workgroup per work item (grid-stride over the items, so a launch can be held to part of the
-// chip): min Go-sort rank per id of one window over a chunk of its stream.
+// chip): min Go-sort rank per id of one window over a chunk of its stream. SIDE only names the
+// small-class launch apart in profiles.
+template <bool SIDE>
 __global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict__ work, uint32_t nitems,
                                                       const uint4* __restrict__ ids16,
                                                       const uint32_t* __restrict__ vmem,
@@ -1008,16 +1010,95 @@ struct Corpus {
   std::vector<VecWork> hwork;
   size_t nbig_work = 0;                        // work items of the big call groups
   uint64_t big_entries = 0, big_pcs = 0;       // entries / PCs in call groups above GS_T_SEG
+  std::vector<VecWork> hwork_all;              // every work item (hwork: those of this rank's key parts)
+  uint64_t big_vecs_all = 0, big_vecs = 0;     // id vectors of the big groups: all / in hwork
+  DevArr<uint8_t> count_hist;                  // groups counted in len_hist (set_parts); unset: all
+  bool has_count_hist = false;
+  DevArr<uint32_t> xg;                         // selection-exchange list (groups, byte offsets)
+  DevArr<uint64_t> xo;
+  std::vector<uint64_t> xkey;
   std::vector<uint64_t> hstart;
   GosortPlan gsplan;
   uint32_t max_prog_len = 0;
   uint32_t ngtabs = 0;
   ~Corpus() {
     off.free(); gstart.free(); gdict.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
-    gtchunks.free(); gtdone.free();
+    gtchunks.free(); gtdone.free(); count_hist.free(); xg.free(); xo.free();
     gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free();
   }
 };
+
+// Orders this rank's work items and uploads them: big call groups (sorted by the global rounds)
+// first, small ones (LDS packs, sorted on the side stream) after, so each class's Minimize runs as
+// soon as its own sort is done; largest first inside a class, so the tail of the grid is short.
+static void corpus_upload_work(Corpus& K, hipStream_t s) {
+  const std::vector<uint64_t>& hstart = K.hstart;
+  auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
+  std::stable_sort(K.hwork.begin(), K.hwork.end(), [&](const VecWork& x, const VecWork& y) {
+    const bool bx = is_big(x.g), by = is_big(y.g);
+    if (bx != by) return bx;
+    return x.vend - x.vbeg > y.vend - y.vbeg;
+  });
+  K.nbig_work = 0;
+  K.big_vecs = 0;
+  while (K.nbig_work < K.hwork.size() && is_big(K.hwork[K.nbig_work].g))
+    K.big_vecs += K.hwork[K.nbig_work].vend - K.hwork[K.nbig_work].vbeg, K.nbig_work++;
+  K.work.alloc(K.hwork.size());
+  if (!K.hwork.empty())
+    SYZ_HIP(hipMemcpyAsync(K.work.p, K.hwork.data(), K.hwork.size() * sizeof(VecWork), hipMemcpyHostToDevice, s));
+  // work items per shared table: the vec_min chunk that brings the count to it emits the table
+  std::vector<uint32_t> hch(K.ngtabs, 0);
+  for (const VecWork& w : K.hwork)
+    if (w.gtab != RANK_NONE) hch[w.gtab]++;
+  if (K.ngtabs) SYZ_HIP(hipMemcpyAsync(K.gtchunks.p, hch.data(), K.ngtabs * 4, hipMemcpyHostToDevice, s));
+  SYZ_HIP(hipStreamSynchronize(s));  // hch / hwork are host temporaries
+}
+
+// Key-space sharding: call group g's id windows are dealt into nparts[g] parts by
+// vector count (longest-processing-time, identical on every rank) and this store keeps part[g].
+// The partial selections of one group on its ranks OR together to the full selection, because an
+// input is kept iff SOME of its PCs first occurs at it.
+static void corpus_set_parts(Corpus& K, const uint16_t* part, const uint16_t* nparts, const uint8_t* count_hist,
+                             hipStream_t s) {
+  const uint32_t G = K.G;
+  std::vector<int> keep_part(G, -1);  // -1: whole group
+  for (uint32_t g = 0; g < G; g++) {
+    const uint32_t k = nparts ? nparts[g] : 1;
+    if (k > 1) {
+      if (!part || part[g] >= k) fail(SYZGPU_EINVAL, "part[g] must be < nparts[g]");
+      keep_part[g] = part[g];
+    }
+  }
+  // vectors per (group, window), then windows -> parts per split group
+  std::map<std::pair<uint32_t, uint32_t>, uint64_t> wvec;
+  for (const VecWork& w : K.hwork_all)
+    if (keep_part[w.g] >= 0) wvec[{w.g, w.win}] += w.vend - w.vbeg;
+  std::map<std::pair<uint32_t, uint32_t>, int> wpart;
+  for (uint32_t g = 0; g < G; g++) {
+    if (keep_part[g] < 0) continue;
+    std::vector<std::pair<uint64_t, uint32_t>> ws;  // (vectors, window)
+    for (auto it = wvec.lower_bound({g, 0}); it != wvec.end() && it->first.first == g; ++it)
+      ws.push_back({it->second, it->first.second});
+    std::stable_sort(ws.begin(), ws.end(), [](const auto& a, const auto& b) {
+      return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    std::vector<uint64_t> load(nparts[g], 0);
+    for (const auto& x : ws) {
+      const int p = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      load[p] += x.first;
+      wpart[{g, x.second}] = p;
+    }
+  }
+  K.hwork.clear();
+  for (const VecWork& w : K.hwork_all)
+    if (keep_part[w.g] < 0 || wpart[{w.g, w.win}] == keep_part[w.g]) K.hwork.push_back(w);
+  K.has_count_hist = count_hist != nullptr;
+  if (count_hist) {
+    K.count_hist.alloc(G);
+    SYZ_HIP(hipMemcpyAsync(K.count_hist.p, count_hist, G, hipMemcpyHostToDevice, s));
+  }
+  corpus_upload_work(K, s);
+}
 
 Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
                           size_t n, uint32_t G, hipStream_t s) {
@@ -1232,36 +1313,22 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
         gt = K.ngtabs++;
       }
       const uint64_t per = (ve - vb + nch - 1) / nch;
-      for (uint64_t v = vb; v < ve; v += per) K.hwork.push_back(VecWork{g, nids, v, std::min(ve, v + per), gt, 0});
+      for (uint64_t v = vb; v < ve; v += per) K.hwork.push_back(VecWork{g, nids, v, std::min(ve, v + per), gt, w});
     }
   }
-  // big call groups (sorted by the global rounds) first, small ones (LDS packs, sorted on the side
-  // stream) after: each class's Minimize runs as soon as its own sort is done
-  auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
-  std::stable_sort(K.hwork.begin(), K.hwork.end(), [&](const VecWork& x, const VecWork& y) {
-    const bool bx = is_big(x.g), by = is_big(y.g);
-    if (bx != by) return bx;
-    return x.vend - x.vbeg > y.vend - y.vbeg;
-  });
-  K.nbig_work = 0;
-  while (K.nbig_work < K.hwork.size() && is_big(K.hwork[K.nbig_work].g)) K.nbig_work++;
+  K.hstart = hstart;
   for (uint32_t g = 0; g < G; g++)
-    if (is_big(g)) {
+    if (hstart[g + 1] - hstart[g] > GS_T_SEG) {
       K.big_entries += hstart[g + 1] - hstart[g];
       K.big_pcs += hpcs[g];
     }
-  K.work.alloc(K.hwork.size());
-  if (!K.hwork.empty())
-    SYZ_HIP(hipMemcpyAsync(K.work.p, K.hwork.data(), K.hwork.size() * sizeof(VecWork), hipMemcpyHostToDevice, s));
+  K.hwork_all = K.hwork;
+  for (const VecWork& w : K.hwork_all)
+    if (hstart[w.g + 1] - hstart[w.g] > GS_T_SEG) K.big_vecs_all += w.vend - w.vbeg;
   K.gtabs.alloc((size_t)K.ngtabs * WIN);
-  {  // work items per shared table: the vec_min chunk that brings the count to it emits the table
-    std::vector<uint32_t> hch(K.ngtabs, 0);
-    for (const VecWork& w : K.hwork)
-      if (w.gtab != RANK_NONE) hch[w.gtab]++;
-    K.gtchunks.alloc(K.ngtabs);
-    K.gtdone.alloc(K.ngtabs);
-    if (K.ngtabs) SYZ_HIP(hipMemcpy(K.gtchunks.p, hch.data(), K.ngtabs * 4, hipMemcpyHostToDevice));
-  }
+  K.gtchunks.alloc(K.ngtabs);
+  K.gtdone.alloc(K.ngtabs);
+  corpus_upload_work(K, s);
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   if (herr[0] & 4) fail(SYZGPU_EINTERNAL, "coverstore: hash bucket overflow");
@@ -1277,23 +1344,20 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
 
 static Corpus* g_last_corpus = nullptr;
 
-void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s) {
+// minimizeCorpus, first half: the Go-sort ranks and the first-occurrence pass into the rank bitmap
+// (this rank's key parts only, see corpus_set_parts).
+void corpus_minimize_begin(Corpus& K, hipStream_t s) {
   Context& c = ctx();
-  if (len_hist && (int64_t)K.max_prog_len > (int64_t)C)
-    fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
   Scratch& sc = c.scratch;
   const size_t n = K.n;
-  const uint32_t G = K.G;
   int* err = sc.get<int>("mz_err", 2);
   uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
   uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
   uint32_t* rank_of_member = sc.get<uint32_t>("mz_rom", n + 1);
   uint32_t* ent_of_rank = sc.get<uint32_t>("mz_eor", n + 1);
-  uint8_t* sel_rank = sc.get<uint8_t>("mz_sel", n + 1);
   SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
   uint32_t* sel_bits = sc.get<uint32_t>("mz_selbits", n / 32 + 2);
   SYZ_HIP(hipMemsetAsync(sel_bits, 0, (n / 32 + 2) * 4, s));
-  if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
   if (K.ngtabs) {
     SYZ_HIP(hipMemsetAsync(K.gtabs.p, 0xFF, (size_t)K.ngtabs * WIN * 4, s));
     SYZ_HIP(hipMemsetAsync(K.gtdone.p, 0, (size_t)K.ngtabs * 4, s));
@@ -1311,11 +1375,13 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   // the small class runs beside the big class's latency-bound global rounds: it is held to part of
   // the chip (its workgroups fill a CU's LDS), so the rounds keep CUs to run on
   static const unsigned side_cus = getenv("SYZGPU_SIDE_CUS") ? (unsigned)atoi(getenv("SYZGPU_SIDE_CUS")) : 128u;
-  auto vec_min = [&](hipStream_t q, size_t first, size_t count, unsigned max_grid) {
-    if (count)
-      k_vec_min<<<(unsigned)std::min<size_t>(count, max_grid), VM_BLOCK, 0, q>>>(
-          K.work.p + first, (uint32_t)count, reinterpret_cast<const uint4*>(K.ids16.p), K.vmem.p, rank_of_member,
-          K.gstart.p, sel_bits, K.gtabs.p, K.gtchunks.p, K.gtdone.p);
+  auto vec_min = [&](hipStream_t q, size_t first, size_t count, bool side) {
+    if (!count) return;
+    const unsigned grid = (unsigned)std::min<size_t>(count, side ? side_cus : (1u << 20));
+    auto* k = side ? k_vec_min<true> : k_vec_min<false>;
+    k<<<grid, VM_BLOCK, 0, q>>>(K.work.p + first, (uint32_t)count, reinterpret_cast<const uint4*>(K.ids16.p),
+                                K.vmem.p, rank_of_member, K.gstart.p, sel_bits, K.gtabs.p, K.gtchunks.p,
+                                K.gtdone.p);
     SYZ_LAUNCHED();
   };
   auto small_done = [&](hipStream_t q) {
@@ -1325,7 +1391,7 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
       SYZ_LAUNCHED();
     }
     ProfScope ps("vec_min_small", q, (K.total_pcs - K.big_pcs) * 4 + (n - K.big_entries) * 10);
-    vec_min(q, K.nbig_work, K.hwork.size() - K.nbig_work, side_cus);
+    vec_min(q, K.nbig_work, K.hwork.size() - K.nbig_work, true);
   };
   auto big_done = [&](hipStream_t q) {
     if (P.nbig) {
@@ -1334,27 +1400,93 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
                                                      rank_of_member, ent_of_rank);
       SYZ_LAUNCHED();
     }
-    ProfScope ps("vec_min", q, K.big_pcs * 4 + K.big_entries * 10);
-    vec_min(q, 0, K.nbig_work, 1u << 20);
+    // algorithmic bytes of this rank's share: the PCs of its key parts (in proportion to their id
+    // vectors) plus offsets and group id of every big-group entry
+    const double share = K.big_vecs_all ? (double)K.big_vecs / (double)K.big_vecs_all : 0.0;
+    ProfScope ps("vec_min", q, (uint64_t)(K.big_pcs * 4 * share) + K.big_entries * 10);
+    vec_min(q, 0, K.nbig_work, false);
   };
   if (n) gosort_run(el, perm, n, P, s, small_done, big_done);
-  {
-    ProfScope ps("select_out", s, (uint64_t)n * 8);
-    if (n) {
-      k_select_store<<<grid_for(n, 256, 512), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
-          sel_bits, K.member_of.p, rank_of_member, n, len_hist ? K.prog_len.p : nullptr, K.group.p, nullptr, C,
-          selected, len_hist, err);
-      SYZ_LAUNCHED();
-    }
-  }
   g_min.gstart = K.gstart.p;
-  g_min.sel_rank = sel_rank;
+  g_min.sel_rank = sc.get<uint8_t>("mz_sel", n + 1);
   g_min.ent_of_rank = ent_of_rank;
   g_min.sel_bits = sel_bits;
   c.last_n = n;
-  c.last_groups = G;
+  c.last_groups = K.G;
   c.have_last = true;
   g_last_corpus = &K;
+}
+
+// Selection of the listed call groups as one byte per group-relative rank, at byte offsets boff[j]
+// of buf (export), or OR-ed back into the rank bitmap (import): the cross-rank exchange of split
+// groups. blockIdx.y = list index.
+__global__ void k_sel_xchg(uint32_t* sel_bits, const uint64_t* gstart, const uint32_t* groups, const uint64_t* boff,
+                           uint8_t* buf, int import) {
+  const uint32_t g = groups[blockIdx.y];
+  const uint64_t gb = gstart[g], ng = gstart[g + 1] - gb, o = boff[blockIdx.y];
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < ng; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t R = gb + r;
+    if (import) {
+      if (buf[o + r]) atomicOr(&sel_bits[R >> 5], 1u << (R & 31));
+    } else {
+      buf[o + r] = (uint8_t)((sel_bits[R >> 5] >> (R & 31)) & 1u);
+    }
+  }
+}
+
+void corpus_sel_xchg(Corpus& K, const uint32_t* groups, const uint64_t* offsets, uint32_t ng, uint8_t* buf,
+                     int import, hipStream_t s) {
+  if (!ng) return;
+  if (!groups || !offsets || !buf) fail(SYZGPU_EINVAL, "null pointer");
+  uint64_t maxn = 0;
+  for (uint32_t j = 0; j < ng; j++) {
+    if (groups[j] >= K.G) fail(SYZGPU_EINVAL, "group id >= ngroups");
+    maxn = std::max<uint64_t>(maxn, K.hstart[groups[j] + 1] - K.hstart[groups[j]]);
+  }
+  Scratch& sc = ctx().scratch;
+  uint32_t* sel_bits = sc.get<uint32_t>("mz_selbits", K.n / 32 + 2);
+  // the exchange list is the same on every step: uploaded once per distinct list, so the step itself
+  // never waits on the host
+  std::vector<uint64_t> key(groups, groups + ng);
+  key.insert(key.end(), offsets, offsets + ng);
+  if (key != K.xkey) {
+    K.xg.alloc(ng);
+    K.xo.alloc(ng);
+    SYZ_HIP(hipMemcpyAsync(K.xg.p, groups, ng * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(K.xo.p, offsets, ng * 8, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipStreamSynchronize(s));  // caller-owned host memory
+    K.xkey = key;
+  }
+  const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>(1, (maxn + 1023) / 1024), 1024);
+  k_sel_xchg<<<dim3(gx, ng), 256, 0, s>>>(sel_bits, K.gstart.p, K.xg.p, K.xo.p, buf, import);
+  SYZ_LAUNCHED();
+}
+
+// minimizeCorpus, second half: kept flags per entry and the length histogram of the kept programs
+// of the groups this rank counts.
+void corpus_minimize_end(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s) {
+  if (len_hist && (int64_t)K.max_prog_len > (int64_t)C)
+    fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
+  Scratch& sc = ctx().scratch;
+  const size_t n = K.n;
+  int* err = sc.get<int>("mz_err", 2);
+  uint32_t* rank_of_member = sc.get<uint32_t>("mz_rom", n + 1);
+  uint32_t* sel_bits = sc.get<uint32_t>("mz_selbits", n / 32 + 2);
+  if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
+  ProfScope ps("select_out", s, (uint64_t)n * 8);
+  if (n) {
+    k_select_store<<<grid_for(n, 256, 512), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
+        sel_bits, K.member_of.p, rank_of_member, n, len_hist ? K.prog_len.p : nullptr, K.group.p,
+        K.has_count_hist ? K.count_hist.p : nullptr, C, selected, len_hist, err);
+    SYZ_LAUNCHED();
+  }
+}
+
+void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s) {
+  if (len_hist && (int64_t)K.max_prog_len > (int64_t)C)
+    fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
+  corpus_minimize_begin(K, s);
+  corpus_minimize_end(K, C, selected, len_hist, s);
 }
 
 }  // namespace syz
@@ -1422,9 +1554,50 @@ int syzgpu_corpus_info(const syzgpu_corpus* cp, uint64_t* info, size_t cap) {
   SYZ_API_BODY({
     if (!cp || !info) fail(SYZGPU_EINVAL, "null pointer");
     const Corpus& K = *reinterpret_cast<const Corpus*>(cp);
-    const uint64_t v[9] = {K.n,      K.G,          K.total_pcs,   K.total_ids,  K.hwork.size(),
-                           K.ngtabs, K.total_vecs, K.big_entries, K.big_pcs};
-    for (size_t i = 0; i < cap && i < 9; i++) info[i] = v[i];
+    const uint64_t v[11] = {K.n,      K.G,          K.total_pcs,   K.total_ids, K.hwork.size(), K.ngtabs,
+                            K.total_vecs, K.big_entries, K.big_pcs, K.big_vecs,  K.big_vecs_all};
+    for (size_t i = 0; i < cap && i < 11; i++) info[i] = v[i];
+  })
+}
+
+int syzgpu_corpus_set_parts(syzgpu_corpus* cp, const uint16_t* part, const uint16_t* nparts,
+                            const uint8_t* count_hist) {
+  SYZ_API_BODY({
+    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    corpus_set_parts(*reinterpret_cast<Corpus*>(cp), part, nparts, count_hist, C_.stream);
+  })
+}
+
+int syzgpu_corpus_minimize_begin_dev(syzgpu_corpus* cp, void* stream) {
+  SYZ_API_BODY({
+    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    corpus_minimize_begin(*reinterpret_cast<Corpus*>(cp), (hipStream_t)stream);
+  })
+}
+
+int syzgpu_corpus_export_sel_dev(syzgpu_corpus* cp, const uint32_t* groups, const uint64_t* offsets,
+                                 uint32_t ngroups, uint8_t* buf, void* stream) {
+  SYZ_API_BODY({
+    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    corpus_sel_xchg(*reinterpret_cast<Corpus*>(cp), groups, offsets, ngroups, buf, 0, (hipStream_t)stream);
+  })
+}
+
+int syzgpu_corpus_import_sel_dev(syzgpu_corpus* cp, const uint32_t* groups, const uint64_t* offsets,
+                                 uint32_t ngroups, const uint8_t* buf, void* stream) {
+  SYZ_API_BODY({
+    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    corpus_sel_xchg(*reinterpret_cast<Corpus*>(cp), groups, offsets, ngroups, const_cast<uint8_t*>(buf), 1,
+                    (hipStream_t)stream);
+  })
+}
+
+int syzgpu_corpus_minimize_end_dev(syzgpu_corpus* cp, int32_t C, uint8_t* selected, int64_t* len_hist,
+                                   void* stream) {
+  SYZ_API_BODY({
+    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    if (len_hist && C <= 0) fail(SYZGPU_EINVAL, "len_hist needs C > 0");
+    corpus_minimize_end(*reinterpret_cast<Corpus*>(cp), C, selected, len_hist, (hipStream_t)stream);
   })
 }
 

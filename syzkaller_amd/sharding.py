@@ -33,6 +33,118 @@ def lpt_assign(weights, nranks):
     return owner, load
 
 
+# ---- key-space sharding: call groups split over ranks by dense-PC windows ----------
+# Cost model of one rank's step, calibrated on MI355X with the bench workload: the
+# Go-sort latency of its largest big call group (global rounds + LDS sort, grows by a level per
+# doubling), plus the first-occurrence stream over its big groups' PCs, plus the per-entry passes
+# (sort rounds over every held entry, ranks, selection output). Small groups (<= 8192 entries) sort
+# in LDS packs and stream on the side stream, overlapped; their PCs are charged a fraction. A split
+# group costs every holder its full sort (latency and entries) but only its share of the PCs.
+SMALL_GROUP = 8192
+LAT_REF_N, LAT_REF_US, LAT_PER_DOUBLING_US = 203_000, 520.0, 73.0
+US_PER_PC = 0.92e-6
+US_PER_ENTRY = 8.0e-5
+SMALL_PC_FRACTION = 0.3
+
+
+def sort_latency_us(n):
+    if n <= SMALL_GROUP:
+        return 0.0
+    return max(0.0, LAT_REF_US + LAT_PER_DOUBLING_US * float(np.log2(n / LAT_REF_N)))
+
+
+class KeyPlan:
+    """ranks[g] = tuple of the ranks holding the parts of call group g (part j on ranks[g][j]; the
+    first is the group's primary: it counts the group in the length histogram and reports its
+    selection). Identical on every rank (a pure function of the corpus layout)."""
+
+    def __init__(self, ranks, cost, entries):
+        self.ranks, self.cost, self.entries = ranks, np.asarray(cost), np.asarray(entries, np.int64)
+        self.ngroups = len(ranks)
+
+    def owner(self):
+        """Primary rank per group (-1: empty group)."""
+        return np.array([r[0] if r else -1 for r in self.ranks], np.int64)
+
+    def held(self, rank):
+        return np.array([rank in r for r in self.ranks], bool)
+
+    def local_entries(self, group, rank):
+        """Global corpus entry ids (ascending) of every group this rank holds a part of."""
+        return np.nonzero(self.held(rank)[np.asarray(group, np.int64)])[0]
+
+    def store_parts(self, rank):
+        """(part u16[G], nparts u16[G], count_hist u8[G]) for CoverStore.set_parts on this rank."""
+        part = np.zeros(self.ngroups, np.uint16)
+        nparts = np.ones(self.ngroups, np.uint16)
+        count = np.zeros(self.ngroups, np.uint8)
+        for g, r in enumerate(self.ranks):
+            if rank in r:
+                nparts[g] = len(r)
+                part[g] = r.index(rank)
+                count[g] = 1 if r[0] == rank else 0
+        return part, nparts, count
+
+    def split_groups(self):
+        """(groups, byte offsets, total bytes) of the selection exchange: every split group, one byte
+        per entry, in group order — the same buffer layout on every rank."""
+        gs = np.array([g for g, r in enumerate(self.ranks) if len(r) > 1], np.uint32)
+        off = np.zeros(gs.size + 1, np.uint64)
+        if gs.size:
+            np.cumsum(self.entries[gs], out=off[1:])
+        return gs, off[:-1], int(off[-1])
+
+
+def _assign(entries, pcs, k, nranks):
+    lat = np.array([sort_latency_us(int(n)) for n in entries])
+    big = entries > SMALL_GROUP
+    w = US_PER_PC * pcs * np.where(big, 1.0, SMALL_PC_FRACTION) / np.maximum(k, 1) + US_PER_ENTRY * entries
+    items = [(lat[g] + w[g], g, j) for g in range(entries.size) if entries[g] > 0 for j in range(k[g])]
+    items.sort(key=lambda t: (-t[0], t[1], t[2]))
+    cur_lat, cur_w = np.zeros(nranks), np.zeros(nranks)
+    ranks = [[] for _ in range(entries.size)]
+    for _, g, j in items:
+        best, best_cost = -1, None
+        for r in range(nranks):
+            if r in ranks[g]:
+                continue
+            c = max(cur_lat[r], lat[g]) + cur_w[r] + w[g]
+            if best_cost is None or c < best_cost - 1e-9:
+                best, best_cost = r, c
+        ranks[g].append(best)
+        cur_lat[best] = max(cur_lat[best], lat[g])
+        cur_w[best] += w[g]
+    return [tuple(r) for r in ranks], cur_lat + cur_w
+
+
+def plan_parts(entries, pcs, nranks, max_rounds=24):
+    """Key-space sharding plan: start with whole groups, then keep doubling the part count of the
+    heaviest group on the bottleneck rank while the modelled step (max over ranks) improves."""
+    entries = np.asarray(entries, np.int64)
+    pcs = np.asarray(pcs, np.float64)
+    k = np.ones(entries.size, np.int64)
+    ranks, cost = _assign(entries, pcs, k, nranks)
+    for _ in range(max_rounds):
+        r = int(np.argmax(cost))
+        cand = [g for g in range(entries.size) if r in ranks[g] and k[g] < nranks and entries[g] > SMALL_GROUP]
+        if not cand:
+            break
+        g = max(cand, key=lambda x: (sort_latency_us(int(entries[x])) + US_PER_PC * pcs[x] / k[x], -x))
+        k2 = k.copy()
+        k2[g] = min(nranks, k[g] * 2)
+        ranks2, cost2 = _assign(entries, pcs, k2, nranks)
+        if cost2.max() >= cost.max() - 1e-6:
+            break
+        k, ranks, cost = k2, ranks2, cost2
+    return KeyPlan(ranks, cost, entries)
+
+
+def layout_stats(group, off, ngroups):
+    """(entries per group, PCs per group) of a CSR corpus layout."""
+    g = np.asarray(group, np.int64)
+    return np.bincount(g, minlength=ngroups), group_weights(group, off, ngroups)
+
+
 def local_entries(group, owner, rank):
     """Global corpus entry ids (ascending, i.e. corpus order) whose call group this rank owns."""
     return np.nonzero(owner[np.asarray(group, np.int64)] == rank)[0]
@@ -58,10 +170,16 @@ def allreduce_hist(hist, dist=None):
     return allreduce(hist, dist)
 
 
+def allreduce_max_u8(buf, dist=None):
+    """The selection exchange of split groups: bytes OR-ed across ranks (MAX over 0/1 bytes)."""
+    return allreduce(buf, dist, None if dist is None else dist.ReduceOp.MAX)
+
+
 def assemble_selection(kept_global, group, ngroups, dist=None):
     """Group-major kept entry ids over all ranks, groups ascending (the order syzgpu_minimize_grouped
     returns; the reference concatenates groups in Go map order). Each rank passes its
-    kept GLOBAL ids group-major; returns (ids, group_off) on every rank."""
+    kept GLOBAL ids group-major, each group from exactly one rank (its primary); returns
+    (ids, group_off) on every rank."""
     kept_global = np.asarray(kept_global, np.int64)
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
         parts = [None] * dist.get_world_size()

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Parse the FETCH_SIZE / WRITE_SIZE passes of tools/gpu_pmc.sh into profiles/pmc_traffic.json.
 
-FETCH_SIZE and WRITE_SIZE are KiB per dispatch. On gfx950 FETCH_SIZE reports half the bytes of a wide
+FETCH_SIZE and WRITE_SIZE are KiB per dispatch. The two vec_min launches of a step (big call groups on
+the main stream, small ones on the side stream) are told apart by their template argument. On gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced streaming read (MI355X_MICROARCH.md §HBM), so it is doubled; WRITE_SIZE is exact for 16-B
 stores and taken as is. Per kernel: the mean over its dispatches of the bench command (3 timed + 1
 warmup steps), as HBM bytes per launch.
@@ -12,11 +13,14 @@ import json
 import os
 import sys
 
-SHORT = {"k_vec_min": "vec_min", "k_gtab_emit": "gtab_emit", "k_select_out": "select_out", "k_gs_level": "gosort_level",
-         "k_gs_lds": "gosort_lds", "k_prio_row": "prio_choice", "k_ranks": "ranks", "k_el_init": "el_init"}
+SHORT = {"k_vec_min": "vec_min", "k_select_store": "select_out", "k_gr_count": "gosort_round",
+         "k_gr_lists": "gosort_round", "k_gr_swap": "gosort_round", "k_ls_sort": "gosort_lds",
+         "k_prio_row": "prio_choice", "k_ranks": "ranks", "k_el_init": "el_init"}
 
 
-def short(name):
+def short(name, grid):
+    if "k_vec_min<true>" in name:
+        return "vec_min_small"
     for k, v in SHORT.items():
         if k in name:
             return v
@@ -29,7 +33,7 @@ def read(d, counter):
         for row in csv.DictReader(open(f)):
             if row.get("Counter_Name") != counter:
                 continue
-            s = short(row.get("Kernel_Name", ""))
+            s = short(row.get("Kernel_Name", ""), int(float(row.get("Grid_Size", 0) or 0)))
             if s:
                 vals.setdefault(s, []).append(float(row["Counter_Value"]))
     return vals
