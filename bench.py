@@ -9,8 +9,9 @@ HBM before the timed region; the output selection, priorities and ChoiceTable st
 
 Workload (BASELINE.json configs[3], per GPU): 1M programs, 2M-PC space, 289 calls, C = 1159,
 synthetic corpus from the seeded generator (SURVEY.md §8d shapes). Weak scaling: at N GPUs the
-corpus has N x 1M programs; call groups are partitioned over ranks (a group's Minimize is
-independent of every other group) and the only exchange is an RCCL all-reduce of the (C+1)-entry
+corpus has N x 1M programs; call groups go to ranks whole or, when one is heavier than a rank's share,
+split by dense-PC windows over several ranks (syzkaller_amd/sharding.py plan_parts). The exchanges are
+an RCCL MAX all-reduce of the split groups' selection bytes and an RCCL all-reduce of the (C+1)-entry
 program-length histogram that feeds CalculatePriorities.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--progs-per-gpu 1000000]
