@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="programs in the CPU baseline sample")
     ap.add_argument("--profile", type=int, default=1, help="per-kernel HIP event timing in the timed region")
     ap.add_argument("--raw-steps", type=int, default=2, help="also time Minimize from the raw CSR (no store)")
+    ap.add_argument("--novelty", type=int, default=1, help="also time config 3 (triage batch) at N=1")
+    ap.add_argument("--novelty-covers", type=int, default=1_000_000)
+    ap.add_argument("--novelty-cpu-sample", type=int, default=20_000)
     ap.add_argument("--split-largest", type=int, default=0,
                     help="rehearsal: force the largest call group into this many PC-key parts")
     ap.add_argument("--emulate", default="", help="W:r — rehearsal: run rank r's shard of a W-rank job on this "
@@ -282,6 +285,9 @@ def main():
         cpu = None
         if args.cpu_baseline and world == 1:
             cpu = cpu_baseline(corp, st, min(args.cpu_sample, corp.n))
+        nov = None
+        if args.novelty and world == 1 and not args.emulate:
+            nov = novelty_leg(args, dev, L, read_prof)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "progs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
@@ -310,10 +316,84 @@ def main():
             {"ms_per_step": round(raw_ms, 3), "progs_per_s": round(corp.n / (raw_ms * 1e-3), 1),
              "note": "Minimize from raw CSR each step (bucket scatter + LDS hash), no store"},
             "gen_s": round(gen_s, 2),
+            "novelty_config3": nov,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def novelty_leg(args, dev, L, read_prof):
+    """BASELINE.json configs[2]: a syz-fuzzer triage batch of 1M fresh execution covers against
+    maxCover (fuzzer.go:446-470 per cover, in order), maxCover0 = the union of a 100k-program corpus
+    per call, 5k flakes. Device-resident inputs; one step = syzgpu_novelty_batch_dev (is_new flags and
+    the updated tables). The oracle's literal per-cover merge is timed on a sample beside it."""
+    import torch
+    from syzkaller_amd import cover, synth
+    G = args.ngroups
+    base = synth.corpus(args.seed + 0x30, 100_000, G, args.npcs)
+    _, mcp, mco = cover.NoveltyBatch(base.pcs, base.off, base.group, G, np.zeros(0, np.uint32),
+                                     np.zeros(G + 1, np.uint64), np.zeros(0, np.uint32))
+    rnd = np.random.default_rng(3)
+    flakes = np.unique(rnd.choice(base.pcs, 5000, replace=False))
+    b = synth.corpus(args.seed + 0x31, args.novelty_covers, G, args.npcs)
+
+    def t(a):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+        return torch.from_numpy(np.ascontiguousarray(a).view(view.get(a.dtype, a.dtype))).to(dev)
+    d = [t(b.pcs), t(b.off), t(b.group), t(mcp), t(mco), t(flakes)]
+    cap = int(mcp.size + b.pcs.size + 1)
+    is_new = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    out = torch.empty(cap, dtype=torch.int32, device=dev)
+    ooff = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        cover.NoveltyBatchDev(d[0], d[1], d[2], b.n, G, d[3], d[4], int(mco[-1]), d[5], flakes.size,
+                              int(b.off[-1]), is_new, out, cap, ooff, sptr)
+    step()
+    torch.cuda.synchronize()
+    steps = max(1, args.steps // 2)
+    L.syzgpu_profile_only(None)  # every novelty scope: events on the launch stream, inside the timed loop
+    L.syzgpu_profile_enable(1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ev = read_prof()
+    L.syzgpu_profile_enable(0)
+    nl = int(b.off[-1])
+    # SURVEY.md §8(d) bytes of one batch: cover PCs + CSR offsets + group ids read once, is_new written,
+    # maxCover0 read, the updated tables written
+    alg_batch = 4 * nl + 8 * (b.n + 1) + 4 * b.n + b.n + 4 * int(mco[-1]) + 4 * int(ooff[-1].item())
+    res = {"workload": "config3: 1M fresh covers (%d PCs) vs maxCover0 of a 100k corpus (%d PCs), %d flakes"
+                       % (nl, int(mco[-1]), flakes.size),
+           "metric": "triage covers/sec", "value": round(b.n * steps / el, 1), "ms_per_batch": round(el / steps * 1e3, 3),
+           "new_covers": int(is_new.sum().item()), "maxcover_out_pcs": int(ooff[-1].item()),
+           "kernels_ms_per_batch": {k: round(e["ms"] / steps, 4) for k, e in sorted(ev.items(), key=lambda x: -x[1]["ms"])},
+           "path_roofline": {"bytes_per_batch": alg_batch, "achieved": round(alg_batch / (el / steps) / 1e9, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(alg_batch / (el / steps) / 1e9 / HBM_PEAK_GBS, 4)}}
+    if ev:
+        dom, e = max(ev.items(), key=lambda x: x[1]["ms"])
+        ms = e["ms"] / e["launches"]
+        alg = e["bytes"] / e["launches"]
+        res["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "avg_launch_ms": round(ms, 3), "algorithmic_bytes_per_launch": int(alg)}
+    if args.cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        k = min(args.novelty_cpu_sample, b.n)
+        off = np.ascontiguousarray(b.off[: k + 1])
+        t1 = time.perf_counter()
+        oracle.novelty(b.pcs[: int(off[-1])], off, b.group[:k], G, mcp, mco, flakes)
+        dt = time.perf_counter() - t1
+        res["cpu_baseline"] = {"value": round(k / dt, 1), "unit": "covers/s", "cores": 1, "kind": "port",
+                               "sample": "first %d covers of the batch; oracle/liboracle.so literal per-cover "
+                                         "Difference/Union (fuzzer.go:446-470), %.2f s" % (k, dt)}
+    return res
 
 
 def cpu_baseline(corp, static, n_sample):

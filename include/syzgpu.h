@@ -98,6 +98,13 @@ int syzgpu_novelty_batch(const uint32_t* pcs, const uint64_t* off, const uint32_
                          uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off,
                          const uint32_t* flakes, size_t nflakes, uint8_t* is_new, uint32_t* out_mc,
                          size_t out_cap, uint64_t* out_mc_off);
+/* The same on device-resident inputs and outputs (every pointer in device memory; mc_total =
+ * mc_off[ngroups], total_pcs = off[n], out_mc_off written on the device). Returns after the stream has
+ * drained, with the same errors. */
+int syzgpu_novelty_batch_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                             uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off, size_t mc_total,
+                             const uint32_t* flakes, size_t nflakes, size_t total_pcs, uint8_t* is_new,
+                             uint32_t* out_mc, size_t out_cap, uint64_t* out_mc_off, void* stream);
 
 /* ---- prog/prio.go --------------------------------------------------------------------------- */
 /* prog/prio.go:137-154 calcDynamicPrio + normalizePrio (:158-192). prog_len[i] = len(p.Calls) of

@@ -152,6 +152,15 @@ def NoveltyBatch(pcs, off, group, ngroups, maxcover_pcs, maxcover_off, flakes):
     return is_new[:n].copy(), out[: int(ooff[-1])].copy(), ooff
 
 
+def NoveltyBatchDev(pcs, off, group, n, ngroups, mc, mc_off, mc_total, flakes, nflakes, total_pcs, is_new, out_mc,
+                    out_cap, out_mc_off, stream=0):
+    """NoveltyBatch on device-resident arrays (torch tensors or device pointers); outputs stay on the
+    device (out_mc_off[ngroups] = the updated tables' total)."""
+    check(lib().syzgpu_novelty_batch_dev(ptr(pcs), ptr(off), ptr(group), n, ngroups, ptr(mc), ptr(mc_off), mc_total,
+                                         ptr(flakes), nflakes, total_pcs, ptr(is_new), ptr(out_mc), out_cap,
+                                         ptr(out_mc_off), stream))
+
+
 class CoverStore:
     """Device-resident corpus (the analog of syz-manager's mgr.corpus): ingest once, then Minimize
     every call group as often as the manager needs (manager.go:507-527 on each Connect / hub sync).

@@ -43,6 +43,15 @@ class Scratch {
   T* get(const std::string& name, size_t count) {
     return static_cast<T*>(get(name, count * sizeof(T) + 16));
   }
+  // A buffer whose users return it to all-`fill` bytes before they finish (sparse clean-up instead
+  // of a full memset per call). It is filled on (re)allocation, and again when the previous user
+  // did not hand it back with put_clean (an error path left it dirty).
+  void* get_clean(const std::string& name, size_t bytes, int fill, hipStream_t s);
+  template <class T>
+  T* get_clean(const std::string& name, size_t count, int fill, hipStream_t s) {
+    return static_cast<T*>(get_clean(name, count * sizeof(T) + 16, fill, s));
+  }
+  void put_clean(const std::string& name) { bufs_[name].clean = true; }
   void release();
   ~Scratch() { release(); }
 
@@ -50,6 +59,7 @@ class Scratch {
   struct Buf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool clean = false;
   };
   std::map<std::string, Buf> bufs_;
 };

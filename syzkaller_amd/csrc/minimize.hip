@@ -825,6 +825,10 @@ struct VecWork {
 };
 
 constexpr int VM_BLOCK = 1024;
+#ifndef SYZ_VM_DEPTH
+#define SYZ_VM_DEPTH 4
+#endif
+constexpr int VM_DEPTH = SYZ_VM_DEPTH;  // vectors per lane per pipelined batch (k_vec_min)
 
 // Winning ranks of a window table (LDS or global) -> set bits of sel_bits (global rank bitmap).
 // Ranks of call g lie in [gstart[g], gstart[g+1]); they are deduplicated through an LDS bitmap so
@@ -891,17 +895,44 @@ __global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict_
     const VecWork w = work[wi];
     for (uint32_t i = threadIdx.x; i < w.nids; i += VM_BLOCK) tab[i] = RANK_NONE;
     __syncthreads();
+    // The loop is bound by bytes in flight per CU (a dependent vmem -> rank gather per vector), so
+    // it is software-pipelined: VM_DEPTH vectors per lane per batch, and the next batch's ids and
+    // members are loaded while the current batch's ranks are gathered and applied.
     uint64_t v = w.vbeg + threadIdx.x;
-    // four vectors in flight per lane
-    for (; v + 3 * VM_BLOCK < w.vend; v += 4 * VM_BLOCK) {
-      const uint4 q0 = ids16[v], q1 = ids16[v + VM_BLOCK], q2 = ids16[v + 2 * VM_BLOCK], q3 = ids16[v + 3 * VM_BLOCK];
-      const uint32_t m0 = vmem[v], m1 = vmem[v + VM_BLOCK], m2 = vmem[v + 2 * VM_BLOCK], m3 = vmem[v + 3 * VM_BLOCK];
-      const uint32_t r0 = rank_of_member[m0], r1 = rank_of_member[m1], r2 = rank_of_member[m2],
-                     r3 = rank_of_member[m3];
-      vec_update(tab, q0, r0);
-      vec_update(tab, q1, r1);
-      vec_update(tab, q2, r2);
-      vec_update(tab, q3, r3);
+    constexpr uint64_t STEP = (uint64_t)VM_DEPTH * VM_BLOCK;
+    if (v + (VM_DEPTH - 1) * VM_BLOCK < w.vend) {
+      uint4 q[VM_DEPTH];
+      uint32_t m[VM_DEPTH];
+#pragma unroll
+      for (int j = 0; j < VM_DEPTH; j++) {
+        q[j] = ids16[v + j * VM_BLOCK];
+        m[j] = vmem[v + j * VM_BLOCK];
+      }
+      for (;;) {
+        uint32_t r[VM_DEPTH];
+#pragma unroll
+        for (int j = 0; j < VM_DEPTH; j++) r[j] = rank_of_member[m[j]];
+        const uint64_t vn = v + STEP;
+        const bool more = vn + (VM_DEPTH - 1) * VM_BLOCK < w.vend;
+        uint4 qn[VM_DEPTH];
+        uint32_t mn[VM_DEPTH];
+        if (more) {
+#pragma unroll
+          for (int j = 0; j < VM_DEPTH; j++) {
+            qn[j] = ids16[vn + j * VM_BLOCK];
+            mn[j] = vmem[vn + j * VM_BLOCK];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < VM_DEPTH; j++) vec_update(tab, q[j], r[j]);
+        v = vn;
+        if (!more) break;
+#pragma unroll
+        for (int j = 0; j < VM_DEPTH; j++) {
+          q[j] = qn[j];
+          m[j] = mn[j];
+        }
+      }
     }
     for (; v < w.vend; v += VM_BLOCK) vec_update(tab, ids16[v], rank_of_member[vmem[v]]);
     __syncthreads();

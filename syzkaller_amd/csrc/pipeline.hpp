@@ -39,6 +39,11 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
 void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const std::vector<uint64_t>& hstart, uint32_t ngroups,
                    hipStream_t s);
 
+// radix.hip: stable LSD sort of (u64 key, u32 value) pairs by key bits [0, end_bit), RADIX_BITS per pass
+constexpr int RADIX_BITS = 8;
+void radix_sort_pairs(uint64_t*& keys, uint32_t*& vals, uint64_t*& ktmp, uint32_t*& vtmp, size_t n, int end_bit,
+                      hipStream_t s);
+
 // setops.hip
 uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64_t na, const uint32_t* b,
                          const uint64_t* boff, uint64_t nb, uint32_t npairs, uint32_t* out, uint64_t out_cap,

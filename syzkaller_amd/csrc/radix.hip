@@ -9,7 +9,7 @@ namespace syz {
 constexpr int RS_BLOCK = 512;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_BLOCK * RS_ITEMS;
-constexpr int RS_RADIX = 256;
+constexpr int RS_RADIX = 1 << RADIX_BITS;
 constexpr int RS_WAVES = RS_BLOCK / 64;
 
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint64_t* __restrict__ keys, size_t n, int shift,
@@ -108,7 +108,7 @@ void radix_sort_pairs(uint64_t*& keys, uint32_t*& vals, uint64_t*& ktmp, uint32_
   Scratch& sc = ctx().scratch;
   uint32_t* counts = sc.get<uint32_t>("rs_counts", ntiles * RS_RADIX + 1);
   uint64_t* offs = sc.get<uint64_t>("rs_offs", ntiles * RS_RADIX + 1);
-  for (int shift = 0; shift < end_bit; shift += 8) {
+  for (int shift = 0; shift < end_bit; shift += RADIX_BITS) {
     k_rs_hist<<<(unsigned)ntiles, RS_BLOCK, 0, s>>>(keys, n, shift, (uint32_t)ntiles, counts);
     SYZ_LAUNCHED();
     exclusive_scan_u32(counts, offs, ntiles * RS_RADIX, s);

@@ -24,6 +24,15 @@ void* Scratch::get(const std::string& name, size_t bytes) {
   return b.p;
 }
 
+void* Scratch::get_clean(const std::string& name, size_t bytes, int fill, hipStream_t s) {
+  void* old = bufs_[name].p;
+  void* p = get(name, bytes);
+  Buf& b = bufs_[name];
+  if (p != old || !b.clean) SYZ_HIP(hipMemsetAsync(p, fill, b.bytes, s));
+  b.clean = false;
+  return p;
+}
+
 void Scratch::release() {
   for (auto& kv : bufs_)
     if (kv.second.p) (void)hipFree(kv.second.p);

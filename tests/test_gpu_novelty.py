@@ -21,6 +21,14 @@ from syzkaller_amd import _lib, cover, synth  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["table", "sort"])
+def strategy(request, monkeypatch):
+    """Both device strategies: the keyed first-occurrence table (default) and the stable radix sort
+    (used when the table would not fit). SYZGPU_NOVELTY is read by the library on every call."""
+    monkeypatch.setenv("SYZGPU_NOVELTY", request.param)
+    return request.param
+
+
 def _check(pcs, off, grp, G, mcp, mco, flakes):
     w_new, w_mc, w_off = oracle.novelty(pcs, off, grp, G, mcp, mco, flakes)
     g_new, g_mc, g_off = cover.NoveltyBatch(pcs, off, grp, G, mcp, mco, flakes)
@@ -108,6 +116,39 @@ def test_novelty_config3_property_large():
     assert np.array_equal((og << np.uint64(32)) | out.astype(np.uint64), want_keys)
 
 
+def test_novelty_full_pc_space():
+    # PCs across the whole u32 space (first/last bitmap page, 0, 0xFFFFFFFE, the sentinel), several
+    # batches in a row (the table strategy's bitmap and table are left clean by each call)
+    rnd = np.random.default_rng(11)
+    edge = np.array([0, 1, 63, 64, 32767, 32768, 0x7FFFFFFF, 0x80000000, 0xFFFF8000, 0xFFFFFFFD, 0xFFFFFFFE],
+                    np.uint32)
+    G = 7
+    for _ in range(4):
+        pool = np.unique(np.concatenate([edge, rnd.integers(0, 2**32 - 1, size=300, dtype=np.uint64)
+                                         .astype(np.uint32)]))
+        n = 200
+        covs = [np.unique(rnd.choice(pool, size=int(rnd.integers(0, 40)))) for _ in range(n)]
+        covs[3] = np.append(covs[3], np.uint32(0xFFFFFFFF))  # the pool never holds the sentinel
+        grp = rnd.integers(0, G, size=n).astype(np.uint32)
+        mc = [np.unique(rnd.choice(pool, size=int(rnd.integers(0, 50)))) for _ in range(G)]
+        mc[2] = np.unique(np.append(mc[2], np.uint32(0xFFFFFFFF)))
+        mc[5] = np.array([0xFFFFFFFF], np.uint32)
+        flakes = np.unique(rnd.choice(pool, size=30))
+        pcs, off = oracle.to_csr(covs)
+        mcp, mco = oracle.to_csr(mc)
+        _check(pcs, off, grp, G, mcp, mco, flakes)
+
+
+def test_novelty_good_batch_after_rejected_one():
+    pcs = np.array([2, 1, 3], np.uint32)  # not canonical
+    off = np.array([0, 3], np.uint64)
+    with pytest.raises(_lib.SyzGpuError):
+        cover.NoveltyBatch(pcs, off, np.zeros(1, np.uint32), 2, np.array([4, 5], np.uint32),
+                           np.array([0, 2, 2], np.uint64), np.zeros(0, np.uint32))
+    fresh, mcp, mco, flakes = _config3(300, 2_000, 50_000)
+    _check(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes)
+
+
 def test_novelty_empty_batch_and_tables():
     _check(np.zeros(0, np.uint32), np.zeros(1, np.uint64), np.zeros(0, np.uint32), 3,
            np.zeros(0, np.uint32), np.zeros(4, np.uint64), np.zeros(0, np.uint32))
@@ -148,3 +189,39 @@ def test_novelty_capacity_error():
                                          2, p(ooff))
     assert rc == _lib.ECAPACITY
     del ctypes
+
+
+def test_novelty_device_entry_matches_host_entry():
+    import torch
+    dev = torch.device("cuda:0")
+    base = synth.corpus(0x5EED0041, 3_000, 31, 40_000)
+    mc_new, mcp, mco = cover.NoveltyBatch(base.pcs, base.off, base.group, 31, np.zeros(0, np.uint32),
+                                           np.zeros(32, np.uint64), np.zeros(0, np.uint32))
+    b = synth.corpus(0x5EED0042, 20_000, 31, 40_000)
+    flakes = np.unique(b.pcs[::997])
+    w_new, w_mc, w_off = cover.NoveltyBatch(b.pcs, b.off, b.group, 31, mcp, mco, flakes)
+
+    def t(a):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+        return torch.from_numpy(np.ascontiguousarray(a).view(view.get(a.dtype, a.dtype))).to(dev)
+    cap = int(mcp.size + b.pcs.size + 1)
+    is_new = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    out = torch.zeros(cap, dtype=torch.int32, device=dev)
+    ooff = torch.zeros(32, dtype=torch.int64, device=dev)
+    cover.NoveltyBatchDev(t(b.pcs), t(b.off), t(b.group), b.n, 31, t(mcp), t(mco), int(mco[-1]), t(flakes),
+                          flakes.size, int(b.off[-1]), is_new, out, cap, ooff)
+    torch.cuda.synchronize()
+    g_off = ooff.cpu().numpy().view(np.uint64)
+    assert np.array_equal(g_off, w_off)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32)[: int(g_off[-1])], w_mc)
+    assert np.array_equal(is_new.cpu().numpy(), w_new)
+    # capacity and canonical-flakes errors come back as status codes
+    with pytest.raises(_lib.SyzGpuError) as e:
+        cover.NoveltyBatchDev(t(b.pcs), t(b.off), t(b.group), b.n, 31, t(mcp), t(mco), int(mco[-1]), t(flakes),
+                              flakes.size, int(b.off[-1]), is_new, out, 10, ooff)
+    assert e.value.code == _lib.ECAPACITY
+    bad = t(flakes[::-1].copy())
+    with pytest.raises(_lib.SyzGpuError) as e:
+        cover.NoveltyBatchDev(t(b.pcs), t(b.off), t(b.group), b.n, 31, t(mcp), t(mco), int(mco[-1]), bad,
+                              flakes.size, int(b.off[-1]), is_new, out, cap, ooff)
+    assert e.value.code == _lib.EINVAL
