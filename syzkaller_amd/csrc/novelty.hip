@@ -178,7 +178,7 @@ constexpr uint32_t KT_TOFF = 1024;  // cover offsets staged per tile
 __global__ void k_kt_tiles(const uint64_t* __restrict__ off, const uint32_t* __restrict__ group, size_t n, uint32_t G,
                            uint64_t* tile_k0, int* err) {
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
-    if (err && group[k] >= G) atomicOr(err, 2);
+    if (group[k] >= G) atomicOr(err, 2);
     const uint64_t b = off[k], e = off[k + 1];
     for (uint64_t t = (b + KT_TILE - 1) / KT_TILE; t * KT_TILE < e; t++) tile_k0[t] = k;
   }
@@ -227,8 +227,8 @@ __device__ __forceinline__ int kt_tile_load(const uint32_t* __restrict__ pcs, ui
 }
 
 __device__ __forceinline__ void kt_tile_stage(const uint64_t* off, size_t n, const uint64_t* tile_k0, uint64_t* soff,
-                                              KtTile& T) {
-  T.k0 = tile_k0[blockIdx.x];
+                                              KtTile& T, uint64_t tile) {
+  T.k0 = tile_k0[tile];
   T.off = off;
   T.soff = soff;
   const uint64_t avail = n + 1 - T.k0;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(KT_TB) void k_kt_mark_cov(const uint32_t* __restric
                                                        u64a* bm, u64a* sum, int* err) {
   __shared__ uint64_t soff[KT_TOFF + 1];
   KtTile T;
-  kt_tile_stage(off, n, tile_k0, soff, T);
+  kt_tile_stage(off, n, tile_k0, soff, T, blockIdx.x);
   const uint64_t j0 = blockIdx.x * KT_TILE + (uint64_t)threadIdx.x * KT_TPC;
   uint32_t pc[KT_TPC], kk[KT_TPC];
   const int cnt = kt_tile_load(pcs, L, n, T, j0, pc, kk);
@@ -353,61 +353,38 @@ __global__ void k_kt_init_mc(const uint32_t* mc, const uint64_t* mc_off, uint32_
   }
 }
 
-// pass 2: T[g][d] = min(T[g][d], k+1) over the keys that are neither flakes nor 0xFFFFFFFF. The PCs
-// are walked in group order (covers stably sorted by group: perm, with voff their offsets in that
-// order), so the waves resident at any time share a few table rows and the row gathers and atomics
-// mostly hit L2 instead of spreading over the whole G x (P+1) table.
+// pass 2: T[g][d] = min(T[g][d], KT_COVER + k) over the keys that are not 0xFFFFFFFF (flakes hold
+// FLAKE, which the min never moves). Cover order, not group order: measured faster (10.5 vs 11.3 ms
+// at config 3), as resident waves then spread their atomics over many rows instead of racing on the
+// hot keys of one row.
 __global__ __launch_bounds__(KT_TB) void k_kt_first(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
-                                                    const uint32_t* __restrict__ group, const uint32_t* __restrict__ perm,
-                                                    const uint64_t* __restrict__ voff, size_t n, uint64_t L, uint32_t G,
+                                                    const uint32_t* __restrict__ group, size_t n, uint64_t L, uint32_t G,
                                                     const uint64_t* __restrict__ tile_k0, const uint2* __restrict__ dw,
                                                     uint64_t P, uint32_t* tab) {
   __shared__ uint64_t soff[KT_TOFF + 1];
   KtTile T;
-  kt_tile_stage(voff, n, tile_k0, soff, T);
+  kt_tile_stage(off, n, tile_k0, soff, T, blockIdx.x);
   const uint64_t j0 = blockIdx.x * KT_TILE + (uint64_t)threadIdx.x * KT_TPC;
-  if (j0 >= L) return;
-  const int cnt = (int)(L - j0 < (uint64_t)KT_TPC ? L - j0 : KT_TPC);
-  uint64_t c;
-  if (T.ns > 1 && T.soff[T.ns - 1] > j0)
-    c = T.k0 + upper_bound_dev<uint64_t>(T.soff, 0, T.ns, j0) - 1;
-  else
-    c = upper_bound_dev<uint64_t>(voff, T.k0 + T.ns - 1, n + 1, j0) - 1;
-  uint64_t hi = T.at(c + 1);
-  uint32_t k = perm[c];
-  uint64_t base = off[k] - T.at(c);
-  uint32_t g = group[k];
-  uint32_t pc[KT_TPC], kk[KT_TPC], gg[KT_TPC];
-#pragma unroll
-  for (int q = 0; q < KT_TPC; q++) {
-    if (q < cnt) {
-      while (j0 + q >= hi) {  // next non-empty cover in group order
-        c++;
-        const uint64_t lo = hi;
-        hi = T.at(c + 1);
-        if (hi > lo) {
-          k = perm[c];
-          base = off[k] - lo;
-          g = group[k];
-        }
-      }
-      pc[q] = pcs[base + j0 + q];
-    } else {
-      pc[q] = SENT;
-    }
-    kk[q] = k;
-    gg[q] = g;
-  }
+  uint32_t pc[KT_TPC], kk[KT_TPC];
+  const int cnt = kt_tile_load(pcs, L, n, T, j0, pc, kk);
+  if (!cnt) return;
   uint2 q2[KT_TPC];
 #pragma unroll
   for (int q = 0; q < KT_TPC; q++) q2[q] = dw[pc[q] >> 5];
+  uint32_t gg[KT_TPC];
+  uint32_t last_k = ~0u, last_g = 0;
+#pragma unroll
+  for (int q = 0; q < KT_TPC; q++) {
+    if (kk[q] != last_k) last_k = kk[q], last_g = group[kk[q]];
+    gg[q] = last_g;
+  }
   uint64_t idx[KT_TPC];
   uint32_t cur[KT_TPC];
   bool ok[KT_TPC];
 #pragma unroll
   for (int q = 0; q < KT_TPC; q++) {
     const uint32_t d = q2[q].y + (uint32_t)__popc(q2[q].x & ((1u << (pc[q] & 31)) - 1));
-    ok[q] = pc[q] != SENT && gg[q] < G;
+    ok[q] = q < cnt && pc[q] != SENT && gg[q] < G;
     idx[q] = ok[q] ? (uint64_t)gg[q] * (P + 1) + d : 0;
     cur[q] = ok[q] ? tab[idx[q]] : 0;
   }
@@ -415,22 +392,6 @@ __global__ __launch_bounds__(KT_TB) void k_kt_first(const uint32_t* __restrict__
   for (int q = 0; q < KT_TPC; q++) {
     const uint32_t me = kk[q] + KT_COVER;
     if (ok[q] && cur[q] > me) atomicMin(&tab[idx[q]], me);  // a stale larger value only costs an atomic
-  }
-}
-
-// covers by group, stably: keys = group (G for an out-of-range one), vals = cover index
-__global__ void k_kt_gkeys(const uint32_t* group, size_t n, uint32_t G, uint64_t* keys, uint32_t* vals) {
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t g = group[k];
-    keys[k] = g < G ? g : G;
-    vals[k] = (uint32_t)k;
-  }
-}
-
-__global__ void k_kt_vlen(const uint64_t* off, const uint32_t* perm, size_t n, uint64_t* vlen) {
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t k = perm[c];
-    vlen[c] = off[k + 1] - off[k];
   }
 }
 
@@ -557,28 +518,6 @@ static bool novelty_table(const uint32_t* d_pcs, const uint64_t* d_off, const ui
     k_kt_pages<<<1, 1024, 0, s>>>(sum, plist, d_ctl);
     SYZ_LAUNCHED();
   }
-  // the group order of pass 2
-  uint32_t* perm = nullptr;
-  uint64_t* voff = sc.get<uint64_t>("kt_voff", n + 1);
-  uint64_t* vtile_k0 = sc.get<uint64_t>("kt_vtile_k0", ntiles + 1);
-  if (n) {
-    uint64_t* gk = sc.get<uint64_t>("kt_gk", n);
-    uint64_t* gkt = sc.get<uint64_t>("kt_gkt", n);
-    uint32_t* gv = sc.get<uint32_t>("kt_gv", n);
-    uint32_t* gvt = sc.get<uint32_t>("kt_gvt", n);
-    uint64_t* vlen = sc.get<uint64_t>("kt_vlen", n);
-    k_kt_gkeys<<<grid_for(n, 256, 16384), 256, 0, s>>>(d_grp, n, G, gk, gv);
-    SYZ_LAUNCHED();
-    int gb = 1;
-    while ((1ull << gb) <= G) gb++;
-    radix_sort_pairs(gk, gv, gkt, gvt, n, gb, s);
-    perm = gv;
-    k_kt_vlen<<<grid_for(n, 256, 16384), 256, 0, s>>>(d_off, perm, n, vlen);
-    SYZ_LAUNCHED();
-    exclusive_scan_u64(vlen, voff, n, s);
-    k_kt_tiles<<<grid_for(n, 256, 16384), 256, 0, s>>>(voff, d_grp, n, G, vtile_k0, nullptr);
-    SYZ_LAUNCHED();
-  }
   SYZ_HIP(hipMemcpyAsync(ctl, d_ctl, 4, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   const uint32_t npages = ctl[0];
@@ -631,7 +570,7 @@ static bool novelty_table(const uint32_t* d_pcs, const uint64_t* d_off, const ui
   {
     ProfScope ps("novelty_first", s, L * 4 + n * 12 + 8);
     if (ntiles) {
-      k_kt_first<<<(unsigned)ntiles, KT_TB, 0, s>>>(d_pcs, d_off, d_grp, perm, voff, n, L, G, vtile_k0, dw, P, tab);
+      k_kt_first<<<(unsigned)ntiles, KT_TB, 0, s>>>(d_pcs, d_off, d_grp, n, L, G, tile_k0, dw, P, tab);
       SYZ_LAUNCHED();
     }
   }
