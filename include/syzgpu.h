@@ -106,6 +106,27 @@ int syzgpu_novelty_batch_dev(const uint32_t* pcs, const uint64_t* off, const uin
                              const uint32_t* flakes, size_t nflakes, size_t total_pcs, uint8_t* is_new,
                              uint32_t* out_mc, size_t out_cap, uint64_t* out_mc_off, void* stream);
 
+/* ---- program text: prog/encoding.go, hash/hash.go --------------------------------------------- */
+/* One pass over each serialized program (CSR: program i is data[off[i], off[i+1])):
+ *   ncalls[i] = len(p.Calls) as prog.Deserialize builds it (encoding.go:120-127): bufio.Scanner lines
+ *               (one trailing '\r' dropped) that are non-empty and do not start with '#';
+ *               the input minimizeCorpus deserializes every kept program for (manager.go:531-538);
+ *   status[i] = prog.CallSet's checks (encoding.go:522-551), 0 = ok, else an OR of
+ *               SYZGPU_PROG_NO_BRACKET (a call line without '('), SYZGPU_PROG_EMPTY_NAME,
+ *               SYZGPU_PROG_LINE_TOO_LONG (bufio.ErrTooLong: a line of >= 64 KiB),
+ *               SYZGPU_PROG_NO_CALLS;
+ *   sigs[20*i]= hash.Hash(prog) = sha1.Sum (hash/hash.go:13-15), the key of the persistent corpus
+ *               prune (manager.go:541-553) and of the hub's corpus (syz-hub/state/state.go:159-250).
+ * Any output may be NULL. Host-pointer form: */
+enum { SYZGPU_PROG_NO_BRACKET = 1, SYZGPU_PROG_EMPTY_NAME = 2, SYZGPU_PROG_LINE_TOO_LONG = 4,
+       SYZGPU_PROG_NO_CALLS = 8 };
+int syzgpu_prog_scan(const uint8_t* data, const uint64_t* off, size_t n, uint32_t* ncalls, uint8_t* status,
+                     uint8_t* sigs);
+/* Device form: only programs with sel[i] != 0 are scanned (sel NULL = all), outputs of the others are
+ * left untouched; sigs must be 4-byte aligned. Enqueued on `stream`; returns once the work is queued. */
+int syzgpu_prog_scan_dev(const uint8_t* data, const uint64_t* off, size_t n, const uint8_t* sel,
+                         uint32_t* ncalls, uint8_t* status, uint8_t* sigs, void* stream);
+
 /* ---- prog/prio.go --------------------------------------------------------------------------- */
 /* prog/prio.go:137-154 calcDynamicPrio + normalizePrio (:158-192). prog_len[i] = len(p.Calls) of
  * corpus program i (the only property the reference reads). out: C*C float32. */

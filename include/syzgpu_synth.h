@@ -40,6 +40,12 @@ int syzgpu_synth_fill(const syzgpu_synth_params* p, const uint32_t* group, const
 int syzgpu_synth_fill_ids(const syzgpu_synth_params* p, const uint64_t* ids, const uint32_t* group,
                           const uint64_t* off, uint64_t n, uint32_t* pcs, int nthreads);
 
+/* Serialized programs (prog.Serialize's text shape: one call per line, "rN = " results, comments,
+ * the odd empty line / CRLF / unterminated last line): program i has exactly prog_len[i] calls.
+ * data == NULL: write off[0..n] (CSR offsets) only; otherwise fill data[off[n]]. */
+int syzgpu_synth_prog_text(uint64_t seed, const uint16_t* prog_len, uint64_t n, uint64_t* off, uint8_t* data,
+                           int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -391,3 +391,115 @@ int oracle_novelty(const uint32_t* pcs, const uint64_t* off, const uint32_t* gro
   free(tlen);
   return rc;
 }
+
+/* ---- prog/encoding.go: Deserialize's call count and CallSet's checks ------------------------- */
+
+/* bufio.ScanLines (Go stdlib bufio/scan.go): a token is the bytes up to '\n' with one trailing '\r'
+ * dropped; a final unterminated line is returned at EOF; a token that needs 64 KiB or more of buffer
+ * stops the scanner with ErrTooLong (MaxScanTokenSize = 64*1024). Third-party dependency: Go stdlib
+ * bufio, version not pinned (README.md:67 requires Go >= 1.7); restated from its published source. */
+#define SCAN_MAX_TOKEN (64 * 1024)
+
+void oracle_prog_scan(const uint8_t* data, size_t len, uint32_t* ncalls, uint8_t* status) {
+  uint32_t calls = 0;
+  uint8_t st = 0;
+  size_t i = 0;
+  while (i < len) { /* for s.Scan() */
+    size_t e = i;
+    while (e < len && data[e] != '\n') e++;
+    size_t line_len = e - i;
+    if (line_len >= SCAN_MAX_TOKEN) {
+      st |= 4; /* Scan() returns false: both Deserialize and CallSet stop here */
+      break;
+    }
+    size_t tok = line_len;
+    if (tok > 0 && data[i + tok - 1] == '\r') tok--; /* dropCR */
+    const uint8_t* ln = data + i;
+    /* encoding.go:124 `if p.EOF() || p.Char() == '#' { continue }`;
+     * encoding.go:527 `if len(ln) == 0 || ln[0] == '#' { continue }` */
+    if (tok > 0 && ln[0] != '#') {
+      calls++;
+      size_t bracket = 0;
+      while (bracket < tok && ln[bracket] != '(') bracket++; /* bytes.IndexByte(ln, '(') */
+      if (bracket == tok) {
+        st |= 1; /* "line does not contain opening bracket" */
+      } else {
+        size_t b = 0; /* call := ln[:bracket] */
+        size_t eq = 0;
+        while (eq < bracket && ln[eq] != '=') eq++;
+        if (eq < bracket) { /* if eq := bytes.IndexByte(call, '='); eq != -1 */
+          eq++;
+          while (eq < bracket && ln[eq] == ' ') eq++;
+          b = eq;
+        }
+        if (bracket - b == 0) st |= 2; /* "call name is empty" */
+      }
+    }
+    i = e + 1; /* past '\n' (or past the end for the final unterminated line) */
+  }
+  if (calls == 0) st |= 8; /* "program does not contain any calls" */
+  *ncalls = calls;
+  *status = st;
+}
+
+/* ---- hash/hash.go: sha1.Sum ------------------------------------------------------------------ */
+
+static uint32_t rol32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+
+static void sha1_compress(uint32_t h[5], const uint8_t blk[64]) {
+  uint32_t w[80];
+  for (int t = 0; t < 16; t++)
+    w[t] = (uint32_t)blk[4 * t] << 24 | (uint32_t)blk[4 * t + 1] << 16 | (uint32_t)blk[4 * t + 2] << 8 |
+           (uint32_t)blk[4 * t + 3];
+  for (int t = 16; t < 80; t++) w[t] = rol32(w[t - 3] ^ w[t - 8] ^ w[t - 14] ^ w[t - 16], 1);
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+  for (int t = 0; t < 80; t++) {
+    uint32_t f, k;
+    if (t < 20) {
+      f = (b & c) | (~b & d);
+      k = 0x5A827999u;
+    } else if (t < 40) {
+      f = b ^ c ^ d;
+      k = 0x6ED9EBA1u;
+    } else if (t < 60) {
+      f = (b & c) | (b & d) | (c & d);
+      k = 0x8F1BBCDCu;
+    } else {
+      f = b ^ c ^ d;
+      k = 0xCA62C1D6u;
+    }
+    uint32_t tmp = rol32(a, 5) + f + e + k + w[t];
+    e = d;
+    d = c;
+    c = rol32(b, 30);
+    b = a;
+    a = tmp;
+  }
+  h[0] += a;
+  h[1] += b;
+  h[2] += c;
+  h[3] += d;
+  h[4] += e;
+}
+
+void oracle_sha1(const uint8_t* data, size_t len, uint8_t* sig) {
+  uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+  size_t i = 0;
+  for (; i + 64 <= len; i += 64) sha1_compress(h, data + i);
+  uint8_t tail[128];
+  memset(tail, 0, sizeof(tail));
+  size_t r = len - i;
+  memcpy(tail, data + i, r);
+  tail[r] = 0x80;
+  size_t tl = r + 1 + 8 <= 64 ? 64 : 128;
+  uint64_t bits = (uint64_t)len * 8;
+  for (int k = 0; k < 8; k++) tail[tl - 1 - k] = (uint8_t)(bits >> (8 * k));
+  sha1_compress(h, tail);
+  if (tl == 128) sha1_compress(h, tail + 64);
+  for (int k = 0; k < 5; k++) {
+    sig[4 * k] = (uint8_t)(h[k] >> 24);
+    sig[4 * k + 1] = (uint8_t)(h[k] >> 16);
+    sig[4 * k + 2] = (uint8_t)(h[k] >> 8);
+    sig[4 * k + 3] = (uint8_t)h[k];
+  }
+}

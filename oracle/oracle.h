@@ -67,6 +67,16 @@ int oracle_novelty(const uint32_t* pcs, const uint64_t* off, const uint32_t* gro
                    const uint32_t* flakes, size_t nflakes, uint8_t* is_new, uint32_t* out_mc,
                    uint64_t* out_mc_off, size_t out_cap);
 
+/* Program text, one program (data, len):
+ *   *ncalls = len(p.Calls) of prog.Deserialize (prog/encoding.go:120-127, parser.Scan :437-449 over
+ *             bufio.Scanner/ScanLines): lines that are non-empty and do not start with '#';
+ *   *status = prog.CallSet's errors (encoding.go:522-551) as bits: 1 a call line without '(',
+ *             2 an empty call name, 4 bufio.ErrTooLong (a line of >= 64 KiB), 8 no calls. */
+void oracle_prog_scan(const uint8_t* data, size_t len, uint32_t* ncalls, uint8_t* status);
+
+/* hash/hash.go:13-15  Hash = sha1.Sum (FIPS 180-4 SHA-1), digest into sig[20]. */
+void oracle_sha1(const uint8_t* data, size_t len, uint8_t* sig);
+
 #ifdef __cplusplus
 }
 #endif

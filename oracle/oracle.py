@@ -45,6 +45,10 @@ def lib():
         L.oracle_build_choice_table.argtypes = [_f32p, _u8p, ctypes.c_int32, _i64p, _u8p]
         L.oracle_novelty.argtypes = [_u32p, _u64p, _u32p, ctypes.c_size_t, ctypes.c_uint32, _u32p, _u64p,
                                      _u32p, ctypes.c_size_t, _u8p, _u32p, _u64p, ctypes.c_size_t]
+        L.oracle_prog_scan.argtypes = [_u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), _u8p]
+        L.oracle_prog_scan.restype = None
+        L.oracle_sha1.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+        L.oracle_sha1.restype = None
         _LIB = L
     return _LIB
 
@@ -158,3 +162,32 @@ def novelty(pcs, off, group, ngroups, mc, mc_off, flakes):
                                 _p(mc_off, _u64p), _p(flakes, _u32p), flakes.size, _p(is_new, _u8p),
                                 _p(out_mc, _u32p), _p(out_off, _u64p), cap), "novelty")
     return is_new[:n].copy(), out_mc[: int(out_off[-1])].copy(), out_off
+
+
+def prog_scan(data, off):
+    """(ncalls u32[n], status u8[n]) per program of a CSR byte blob (oracle_prog_scan)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    n = off.size - 1
+    nc = np.zeros(max(n, 1), np.uint32)
+    st = np.zeros(max(n, 1), np.uint8)
+    L = lib()
+    base = data.ctypes.data
+    for i in range(n):
+        b = int(off[i])
+        L.oracle_prog_scan(ctypes.cast(base + b, _u8p), int(off[i + 1]) - b,
+                           ctypes.cast(nc.ctypes.data + 4 * i, ctypes.POINTER(ctypes.c_uint32)),
+                           ctypes.cast(st.ctypes.data + i, _u8p))
+    return nc[:n].copy(), st[:n].copy()
+
+
+def sha1(data, off):
+    """sigs u8[n, 20] (oracle_sha1 per program)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    n = off.size - 1
+    sig = np.zeros((max(n, 1), 20), np.uint8)
+    L = lib()
+    base = data.ctypes.data
+    for i in range(n):
+        b = int(off[i])
+        L.oracle_sha1(ctypes.cast(base + b, _u8p), int(off[i + 1]) - b, ctypes.cast(sig.ctypes.data + 20 * i, _u8p))
+    return sig[:n].copy()

@@ -37,6 +37,8 @@ SIGNATURES = {
                                         _vp]),
     "syzgpu_novelty_batch_dev": (_c.c_int, [_vp, _vp, _vp, _sz, _c.c_uint32, _vp, _vp, _sz, _vp, _sz, _sz, _vp,
                                             _vp, _sz, _vp, _vp]),
+    "syzgpu_prog_scan": (_c.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
+    "syzgpu_prog_scan_dev": (_c.c_int, [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_dynamic_prio": (_c.c_int, [_vp, _sz, _c.c_int32, _vp]),
     "syzgpu_calculate_priorities": (_c.c_int, [_vp, _vp, _sz, _c.c_int32, _vp]),
     "syzgpu_build_choice_table": (_c.c_int, [_vp, _vp, _c.c_int32, _vp, _vp]),

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -203,4 +204,66 @@ extern "C" int syzgpu_synth_fill_ids(const syzgpu_synth_params* p, const uint64_
 extern "C" int syzgpu_synth_fill(const syzgpu_synth_params* p, const uint32_t* group,
                                  const uint64_t* off, uint32_t* pcs, int nthreads) {
   return syzgpu_synth_fill_ids(p, nullptr, group, off, p->n, pcs, nthreads);
+}
+
+// ---- serialized programs (prog.Serialize's text shape, prog/encoding.go:19-117) -------------------
+namespace {
+const char* const kCallNames[] = {
+    "mmap", "openat$dir", "open", "close", "read", "write", "ioctl$sock_SIOCGIFINDEX", "socket$inet6_tcp",
+    "bind$inet6", "connect$inet6", "sendmsg$netlink", "recvmsg", "setsockopt$inet_tcp_int", "getsockopt",
+    "epoll_create1", "epoll_ctl$EPOLL_CTL_ADD", "pipe2", "dup3", "fcntl$setflags", "getpid", "clone",
+    "ptrace$peek", "keyctl$join", "add_key$user", "bpf$PROG_LOAD", "perf_event_open", "io_setup",
+    "io_submit", "memfd_create", "fallocate", "write$binfmt_elf64", "syz_open_dev$tty1"};
+const char* const kArgs[] = {"0x0", "0x1", "0xffffffffffffffff", "&(0x7f0000000000)='./file0\\x00'",
+                             "&(0x7f0000001000/0x1000)=nil", "0x3", "&(0x7f0000002000)={0x2, 0x4e20}",
+                             "&(0x7f0000003000)=\"a5ff\"", "0x40", "0x8912"};
+
+void prog_text(uint64_t seed, uint64_t i, uint32_t ncalls, std::string& s) {
+  Rng r(splitmix(seed * 0x100000001B3ull + i));
+  s.clear();
+  if (r.uniform() < 0.1) s += "# https://syzkaller.appspot.com/bug?id=" + std::to_string(r.next() % 100000) + "\n";
+  for (uint32_t c = 0; c < ncalls; c++) {
+    if (r.uniform() < 0.03) s += r.uniform() < 0.5 ? "\n" : "#\n";
+    if (r.uniform() < 0.5) s += "r" + std::to_string(c) + " = ";
+    s += kCallNames[r.next() % (sizeof(kCallNames) / sizeof(kCallNames[0]))];
+    s += "(";
+    const int nargs = (int)(r.next() % 7);
+    for (int a = 0; a < nargs; a++) {
+      if (a) s += ", ";
+      if (c > 0 && r.uniform() < 0.15)
+        s += "r" + std::to_string(r.next() % c);
+      else
+        s += kArgs[r.next() % (sizeof(kArgs) / sizeof(kArgs[0]))];
+    }
+    s += ")";
+    if (r.uniform() < 0.02) s += "\r";
+    if (c + 1 < ncalls || r.uniform() < 0.9) s += "\n";
+  }
+}
+}  // namespace
+
+extern "C" int syzgpu_synth_prog_text(uint64_t seed, const uint16_t* prog_len, uint64_t n, uint64_t* off,
+                                      uint8_t* data, int nthreads) {
+  if (!prog_len || !off) return 1;
+  if (!data) {  // sizes pass: off[0..n]
+    std::vector<uint64_t> len(n);
+    parallel_for(n, nthreads, [&](uint64_t b, uint64_t e) {
+      std::string s;
+      for (uint64_t i = b; i < e; i++) {
+        prog_text(seed, i, prog_len[i], s);
+        len[i] = s.size();
+      }
+    });
+    off[0] = 0;
+    for (uint64_t i = 0; i < n; i++) off[i + 1] = off[i] + len[i];
+    return 0;
+  }
+  parallel_for(n, nthreads, [&](uint64_t b, uint64_t e) {
+    std::string s;
+    for (uint64_t i = b; i < e; i++) {
+      prog_text(seed, i, prog_len[i], s);
+      std::memcpy(data + off[i], s.data(), s.size());
+    }
+  });
+  return 0;
 }

@@ -4,6 +4,8 @@
     calcDynamicPrio(prog_lens, C)            prio.go:137  (+ normalizePrio, prio.go:158)
     BuildChoiceTable(prios, enabled=None)    prio.go:202  -> ChoiceTable
     ChoiceTable.Choose(rng, call)            prio.go:230  (consumer; host-side, not part of the GPU path)
+    CallCounts(data, off)                    encoding.go:120-127  len(p.Calls) of Deserialize, batched
+    CallSetStatus(data, off)                 encoding.go:522-551  CallSet's checks, batched
 
 The reference reads only len(p.Calls) of each corpus program, so programs are
 passed as an array of call counts. calcStaticPriorities needs the generated sys.Calls type graph,
@@ -64,3 +66,44 @@ def BuildChoiceTable(prios, enabled=None):
     present = np.empty(C, dtype=np.uint8)
     check(lib().syzgpu_build_choice_table(ptr(prios), ptr(en), C, ptr(run), ptr(present)))
     return ChoiceTable(run, present, en)
+
+
+# prog.CallSet errors (encoding.go:529-549) as status bits of ProgScan
+NO_BRACKET, EMPTY_NAME, LINE_TOO_LONG, NO_CALLS = 1, 2, 4, 8
+
+
+def _blob(data, off):
+    if isinstance(data, (list, tuple)):  # [][]byte
+        off = np.zeros(len(data) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(d) for d in data])
+        data = np.frombuffer(b"".join(data), dtype=np.uint8) if data else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(data, dtype=np.uint8), np.ascontiguousarray(off, dtype=np.uint64)
+
+
+def ProgScan(data, off=None, ncalls=True, status=True, sigs=True):
+    """One pass over serialized programs (a list of bytes, or a CSR blob + offsets): returns
+    (ncalls u32[n], status u8[n], sigs u8[n, 20]); the ones not asked for are None."""
+    data, off = _blob(data, off)
+    n = off.size - 1
+    nc = np.zeros(max(n, 1), np.uint32) if ncalls else None
+    st = np.zeros(max(n, 1), np.uint8) if status else None
+    sg = np.zeros((max(n, 1), 20), np.uint8) if sigs else None
+    check(lib().syzgpu_prog_scan(ptr(data), ptr(off), n, ptr(nc), ptr(st), ptr(sg)))
+    return tuple(None if a is None else a[:n].copy() for a in (nc, st, sg))
+
+
+def CallCounts(data, off=None):
+    """len(p.Calls) of prog.Deserialize for every program (what CalculatePriorities reads)."""
+    return ProgScan(data, off, status=False, sigs=False)[0]
+
+
+def CallSetStatus(data, off=None):
+    """0 where prog.CallSet would succeed, else an OR of NO_BRACKET / EMPTY_NAME / LINE_TOO_LONG /
+    NO_CALLS."""
+    return ProgScan(data, off, ncalls=False, sigs=False)[1]
+
+
+def ProgScanDev(data, off, n, sel, ncalls, status, sigs, stream=0):
+    """ProgScan on device-resident arrays (torch tensors or device pointers); sel (u8[n] or None)
+    restricts the scan to selected programs; enqueued on `stream`."""
+    check(lib().syzgpu_prog_scan_dev(ptr(data), ptr(off), n, ptr(sel), ptr(ncalls), ptr(status), ptr(sigs), stream))

@@ -43,6 +43,8 @@ def _lib():
                                         ctypes.c_void_p, ctypes.c_int]
         L.syzgpu_synth_fill_ids.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+        L.syzgpu_synth_prog_text.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_int]
         _LIB = L
     return _LIB
 
@@ -114,3 +116,18 @@ def subcorpus(p, ids, group, off, plen, nthreads=None):
                                     ids.size, pcs.ctypes.data, nthreads):
         raise ValueError("bad synth params")
     return Corpus(pcs, soff, sgroup, np.ascontiguousarray(plen[ids]), int(p.ngroups))
+
+
+def prog_text(seed, prog_len, nthreads=None):
+    """Serialized programs with exactly prog_len[i] calls each: (data uint8[], off uint64[n+1])."""
+    prog_len = np.ascontiguousarray(prog_len, dtype=np.uint16)
+    n = prog_len.size
+    nt = nthreads or min(16, os.cpu_count() or 1)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    L = _lib()
+    if L.syzgpu_synth_prog_text(seed, prog_len.ctypes.data, n, off.ctypes.data, None, nt):
+        raise RuntimeError("synth prog_text failed")
+    data = np.empty(int(off[-1]) + 4, dtype=np.uint8)
+    if L.syzgpu_synth_prog_text(seed, prog_len.ctypes.data, n, off.ctypes.data, data.ctypes.data, nt):
+        raise RuntimeError("synth prog_text failed")
+    return data[: int(off[-1])], off
