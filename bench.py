@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="programs in the CPU baseline sample")
     ap.add_argument("--profile", type=int, default=1, help="per-kernel HIP event timing in the timed region")
     ap.add_argument("--raw-steps", type=int, default=2, help="also time Minimize from the raw CSR (no store)")
+    ap.add_argument("--text", type=int, default=1, help="also time the text pass over the kept programs at N=1")
     ap.add_argument("--novelty", type=int, default=1, help="also time config 3 (triage batch) at N=1")
     ap.add_argument("--novelty-covers", type=int, default=1_000_000)
     ap.add_argument("--novelty-cpu-sample", type=int, default=20_000)
@@ -285,6 +286,9 @@ def main():
         cpu = None
         if args.cpu_baseline and world == 1:
             cpu = cpu_baseline(corp, st, min(args.cpu_sample, corp.n))
+        tail = None
+        if args.text and world == 1 and not args.emulate:
+            tail = text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step)
         nov = None
         if args.novelty and world == 1 and not args.emulate:
             nov = novelty_leg(args, dev, L, read_prof)
@@ -316,11 +320,84 @@ def main():
             {"ms_per_step": round(raw_ms, 3), "progs_per_s": round(corp.n / (raw_ms * 1e-3), 1),
              "note": "Minimize from raw CSR each step (bucket scatter + LDS hash), no store"},
             "gen_s": round(gen_s, 2),
+            "minimize_corpus_tail": tail,
             "novelty_config3": nov,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step):
+    """The rest of minimizeCorpus (manager.go:531-553) after Minimize: every kept program is
+    deserialized (prog.Deserialize -> len(p.Calls), encoding.go:120-127) and hashed (hash.Hash ->
+    the persistent-corpus prune, :541-550). One syzgpu_prog_scan_dev over the resident program text
+    of the corpus with the step's selection bytes as the mask; synthetic text with exactly prog_len
+    calls per program (synth.prog_text)."""
+    import torch
+    from syzkaller_amd import prog, synth
+    t0 = time.perf_counter()
+    data, off = synth.prog_text(args.seed + 0x40, corp.prog_len)
+    gen = time.perf_counter() - t0
+    n = corp.n
+    td = torch.from_numpy(data).to(dev)
+    to = torch.from_numpy(off.view(np.int64)).to(dev)
+    nc = torch.zeros(n, dtype=torch.int32, device=dev)
+    stt = torch.zeros(n, dtype=torch.uint8, device=dev)
+    sg = torch.zeros((n, 20), dtype=torch.uint8, device=dev)
+
+    def run():  # the manager needs len(p.Calls) and the signature; CallSet's checks are the hub's
+        prog.ProgScanDev(td, to, n, d_sel, nc, None, sg, sptr)
+    prog.ProgScanDev(td, to, n, d_sel, nc, stt, sg, sptr)  # once with the checks: a valid corpus
+    torch.cuda.synchronize()
+    sel = d_sel.cpu().numpy().astype(bool)
+    ok = bool((nc.cpu().numpy()[sel] == corp.prog_len[sel]).all() and not stt.cpu().numpy()[sel].any())
+    nc.zero_()
+    run()
+    torch.cuda.synchronize()
+    ok = ok and bool((nc.cpu().numpy()[sel] == corp.prog_len[sel]).all())
+    steps = max(1, args.steps)
+    L.syzgpu_profile_only(None)
+    L.syzgpu_profile_enable(1)
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t1) / steps
+    ev = read_prof()
+    L.syzgpu_profile_enable(0)
+    kept = int(sel.sum())
+    lens = np.diff(off).astype(np.int64)
+    kbytes = int(lens[sel].sum())
+    blocks = int(((lens[sel] + 8) // 64 + 1).sum())
+    res = {"what": "prog.Deserialize len(p.Calls) + hash.Hash over the kept programs",
+           "kept_programs": kept, "text_bytes": kbytes, "sha1_blocks": blocks, "ms": round(el * 1e3, 4),
+           "kept_progs_per_s": round(kept / el, 1), "ncalls_match_prog_len": ok, "gen_s": round(gen, 2),
+           "minimize_corpus_ms": round(ms_step + el * 1e3, 4),
+           "kernels_ms": {k: round(e["ms"] / steps, 4) for k, e in ev.items()}}
+    if "prog_lane" in ev:
+        e = ev["prog_lane"]
+        ms = e["ms"] / e["launches"]
+        alg = kbytes + 16 * kept + 24 * kept  # text + offsets read; ncalls and digest written
+        res["roofline"] = {"bound": "valu", "kernel": "prog_lane", "avg_launch_ms": round(ms, 4),
+                           "hbm_achieved": round(alg / (ms * 1e-3) / 1e9, 1), "hbm_peak": HBM_PEAK_GBS,
+                           "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "sha1_blocks_per_s": round(blocks / (ms * 1e-3), 1)}
+    if args.cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        idx = np.flatnonzero(sel)[:200_000]
+        sub_off = np.zeros(idx.size + 1, np.uint64)
+        sub_off[1:] = np.cumsum(lens[idx])
+        sub = np.frombuffer(b"".join(data[int(off[i]):int(off[i + 1])].tobytes() for i in idx), np.uint8)
+        t2 = time.perf_counter()
+        oracle.prog_scan(sub, sub_off)
+        oracle.sha1(sub, sub_off)
+        dt = time.perf_counter() - t2
+        res["cpu_baseline"] = {"value": round(idx.size / dt, 1), "unit": "kept progs/s", "cores": 1, "kind": "port",
+                               "sample": "first %d kept programs; oracle_prog_scan + oracle_sha1 per program, %.2f s"
+                                         % (idx.size, dt)}
+    return res
 
 
 def novelty_leg(args, dev, L, read_prof):

@@ -189,6 +189,28 @@ __device__ __forceinline__ uint32_t wave_incl_scan<uint32_t>(uint32_t v) {
   return x;
 }
 
+// Inclusive wave64 max-scan of int32 on the same DPP sequence (disabled / out-of-row lanes read
+// INT_MIN, the identity).
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ int32_t dpp_max(int32_t x) {
+  const int32_t y = __builtin_amdgcn_update_dpp((int)0x80000000, x, CTRL, ROW, BANK, false);
+  return x > y ? x : y;
+}
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v) {
+  int32_t x = v;
+  const int32_t a = __builtin_amdgcn_update_dpp((int)0x80000000, v, 0x111, 0xF, 0xF, false);
+  const int32_t b = __builtin_amdgcn_update_dpp((int)0x80000000, v, 0x112, 0xF, 0xF, false);
+  const int32_t c = __builtin_amdgcn_update_dpp((int)0x80000000, v, 0x113, 0xF, 0xF, false);
+  x = x > a ? x : a;
+  x = x > b ? x : b;
+  x = x > c ? x : c;
+  x = dpp_max<0x114, 0xF, 0xE>(x);
+  x = dpp_max<0x118, 0xF, 0xC>(x);
+  x = dpp_max<0x142, 0xA, 0xF>(x);
+  x = dpp_max<0x143, 0xC, 0xF>(x);
+  return x;
+}
+
 template <class T>
 __device__ __forceinline__ T wave_sum(T x) {
 #pragma unroll

@@ -29,16 +29,20 @@ def _check(progs=None, data=None, off=None):
     assert np.array_equal(nc, wnc)
     assert np.array_equal(st, wst)
     assert np.array_equal(sg, oracle.sha1(data, off))
-    return nc, st, sg
+    # the lane-per-program count (taken when no CallSet checks are asked for), alone and with SHA-1
+    assert np.array_equal(sprog.CallCounts(data, off), wnc)
+    nc2, st2, sg2 = sprog.ProgScan(data, off, status=False)
+    assert st2 is None and np.array_equal(nc2, wnc) and np.array_equal(sg2, sg)
+    return nc, st, sg, data, off
 
 
 def test_callset_table_and_sha1_known_answers():
     with open(os.path.join(ROOT, "tests", "golden", "progtext_vectors.json")) as f:
         v = json.load(f)
-    nc, st, _ = _check([c["prog"] for c in v["callset"]])
+    nc, st = _check([c["prog"] for c in v["callset"]])[:2]
     assert [s == 0 for s in st] == [c["ok"] for c in v["callset"]]
     msgs = [bytes.fromhex(x["hex"]) if x["hex"] is not None else b"a" * x["repeat_a"] for x in v["sha1"]]
-    _, _, sg = _check(msgs)
+    sg = _check(msgs)[2]
     assert [bytes(s).hex() for s in sg] == [x["digest"] for x in v["sha1"]]
     assert shash.Hash(b"abc").String() == "a9993e364706816aba3e25717850c26c9cd0d89d"
     assert shash.FromString(shash.Hash(b"abc").String()) == shash.Hash(b"abc")
@@ -55,14 +59,23 @@ def test_every_length_and_alignment():
     alphabet = np.frombuffer(b"abc()=# \r\n\n\n$,0x", np.uint8)
     progs = [rnd.choice(alphabet, size=k).tobytes() for k in range(0, 400)]
     progs += [rnd.choice(alphabet, size=int(rnd.integers(0, 3000))).tobytes() for _ in range(300)]
+    progs += [rnd.choice(np.frombuffer(b"a\r\n#", np.uint8), size=int(rnd.integers(60, 200))).tobytes() for _ in range(300)]
     rnd.shuffle(progs)
     _check(progs)
+
+
+def test_count_only_mode_matches():
+    # ncalls without status runs the count-only kernel (no CallSet scans); long lines go serial
+    S = "x" * 65535
+    progs = ["a()\n" + S + "x\nb()\n", "a()\r\n\r\n#x\nb(", "", "\n\n", "r0 = f()\n" * 300] * 3
+    data, off = sprog._blob([p.encode() for p in progs], None)
+    assert np.array_equal(sprog.CallCounts(data, off), oracle.prog_scan(data, off)[0])
 
 
 def test_synthetic_corpus():
     c = synth.corpus(0x5EED0021, 20_000, 97, 40_000)
     d, o = synth.prog_text(0x77, c.prog_len)
-    nc, st, _ = _check(data=d, off=o)
+    nc, st = _check(data=d, off=o)[:2]
     assert np.array_equal(nc, c.prog_len.astype(np.uint32)) and not st.any()
 
 
