@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--text", type=int, default=1, help="also time the text pass over the kept programs at N=1")
     ap.add_argument("--novelty", type=int, default=1, help="also time config 3 (triage batch) at N=1")
     ap.add_argument("--novelty-covers", type=int, default=1_000_000)
+    ap.add_argument("--analytics", type=int, default=1, help="also time the manager's cover analytics at N=1")
+    ap.add_argument("--analytics-cpu-sample", type=int, default=10_000)
     ap.add_argument("--novelty-cpu-sample", type=int, default=20_000)
     ap.add_argument("--split-largest", type=int, default=0,
                     help="rehearsal: force the largest call group into this many PC-key parts")
@@ -292,6 +294,9 @@ def main():
         nov = None
         if args.novelty and world == 1 and not args.emulate:
             nov = novelty_leg(args, dev, L, read_prof)
+        ana = None
+        if args.analytics and world == 1 and not args.emulate:
+            ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "progs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
@@ -322,6 +327,7 @@ def main():
             "gen_s": round(gen_s, 2),
             "minimize_corpus_tail": tail,
             "novelty_config3": nov,
+            "cover_analytics": ana,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -398,6 +404,68 @@ def text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step):
                                "sample": "first %d kept programs; oracle_prog_scan + oracle_sha1 per program, %.2f s"
                                          % (idx.size, dt)}
     return res
+
+
+def analytics_leg(args, dev, L, read_prof, store, corp, sptr):
+    """syz-manager's cover analytics (html.go:67-97 httpSummary per-call table and "cover" stat,
+    html.go:213-237 uniqueCover both ways, html.go:158-170 httpCorpus's per-input UniqueCover) on the
+    bench's resident 1M-program store: one syzgpu_corpus_cover_stats_dev per step, outputs in HBM.
+    The oracle's literal restatement (Union grown input by input, Go-map counts) is timed on a sample."""
+    import torch
+    G, n = corp.ngroups, corp.n
+    d64 = torch.zeros(3 * G + 3, dtype=torch.int64, device=dev)
+    d_iu = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+    p = d64.data_ptr()
+
+    def run():
+        _lib_check(L.syzgpu_corpus_cover_stats_dev(store.handle, p, p + 8 * G, p + 16 * G, p + 24 * G,
+                                                   d_iu.data_ptr(), sptr))
+    run()
+    torch.cuda.synchronize()
+    h = d64.cpu().numpy().view(np.uint64)
+    tot = [int(x) for x in h[3 * G:3 * G + 3]]
+    # size-independent identities: every input counted once, every one-call PC in one call, the
+    # per-input unique counts add up to uniqueCover(false) (no 0xFFFFFFFF in synthetic covers)
+    ok = bool(int(h[:G].sum()) == n and int(h[2 * G:3 * G].sum()) == tot[1]
+              and int(d_iu.sum().item()) == tot[2] and tot[0] >= int(h[G:2 * G].max()))
+    steps = max(1, args.steps)
+    L.syzgpu_profile_only(None)
+    L.syzgpu_profile_enable(1)
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t1) / steps
+    ev = read_prof()
+    L.syzgpu_profile_enable(0)
+    res = {"what": "per-call Inputs/Cover/UniqueCover, total cover, uniqueCover(true/false), per-input UniqueCover",
+           "ms": round(el * 1e3, 4), "progs_per_s": round(n / el, 1), "cover": tot[0],
+           "unique_per_call": tot[1], "unique_per_input": tot[2], "identities_hold": ok,
+           "kernels_ms": {k: round(e["ms"] / steps, 4) for k, e in sorted(ev.items(), key=lambda kv: -kv[1]["ms"])}}
+    if "cs_uniq" in ev:
+        e = ev["cs_uniq"]
+        ms = e["ms"] / e["launches"]
+        alg = 4 * int(corp.off[-1]) + 10 * n  # the covers once (4 B per PC) + offsets and call id
+        res["roofline"] = {"bound": "hbm", "kernel": "cs_uniq", "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms, 4),
+                           "algorithmic_bytes_per_launch": alg}
+    if args.cpu_baseline and args.analytics_cpu_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        k = min(args.analytics_cpu_sample, n)
+        t2 = time.perf_counter()
+        oracle.cover_stats(corp.pcs[:int(corp.off[k])], corp.off[:k + 1], corp.group[:k], G)
+        dt = time.perf_counter() - t2
+        res["cpu_baseline"] = {"value": round(k / dt, 1), "unit": "progs/s", "cores": 1, "kind": "port",
+                               "sample": "first %d programs of the corpus; oracle_cover_stats (literal html.go), "
+                                         "%.2f s" % (k, dt)}
+    return res
+
+
+def _lib_check(rc):
+    from syzkaller_amd import _lib
+    _lib.check(rc)
 
 
 def novelty_leg(args, dev, L, read_prof):

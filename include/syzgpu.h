@@ -204,6 +204,30 @@ int syzgpu_corpus_export_sel_dev(syzgpu_corpus* c, const uint32_t* groups, const
 int syzgpu_corpus_import_sel_dev(syzgpu_corpus* c, const uint32_t* groups, const uint64_t* offsets,
                                  uint32_t ngroups, const uint8_t* buf, void* stream);
 
+/* ---- the manager's cover analytics on the store (syz-manager/html.go) ------------------------- */
+/* Per call group g (arrays of ngroups, any may be NULL):
+ *   call_inputs[g] = CallCov.count, call_cover[g] = len(CallCov.cov) (the Union of the call's covers),
+ *   call_unique[g] = len(Intersection(CallCov.cov, uniqueCover(true)))       html.go:67-92
+ * totals[0] = len(cov), the Union over calls ("cover" stat, html.go:88-97);
+ * totals[1] = len(uniqueCover(true)), totals[2] = len(uniqueCover(false))  html.go:213-237
+ * input_unique[e] = len(Intersection(corpus[e].Cover, uniqueCover(false))), corpus order
+ *                                                                          html.go:158-170 (httpCorpus)
+ * Union/Intersection never emit 0xFFFFFFFF (foreach, cover.go:81-102); uniqueCover keeps it unless
+ * it is its only PC (Canonicalize, cover.go:28-40). Host form, and a device form (all outputs device
+ * pointers, enqueued on stream): */
+int syzgpu_corpus_cover_stats(syzgpu_corpus* c, uint64_t* call_inputs, uint64_t* call_cover,
+                              uint64_t* call_unique, uint64_t* totals, uint32_t* input_unique);
+int syzgpu_corpus_cover_stats_dev(syzgpu_corpus* c, uint64_t* call_inputs, uint64_t* call_cover,
+                                  uint64_t* call_unique, uint64_t* totals, uint32_t* input_unique,
+                                  void* stream);
+/* httpCover's PC lists (html.go:186-211), sorted ascending:
+ *   call >= 0: the call's Union, intersected with uniqueCover(true) (unique = 1) or
+ *              uniqueCover(false) (unique = 2) when unique != 0;
+ *   call <  0: the Union of every call (unique = 0), or uniqueCover(unique == 1) itself.
+ * *out_n = the list length; SYZGPU_ECAPACITY (and nothing written) when it exceeds cap. */
+int syzgpu_corpus_cover(syzgpu_corpus* c, int64_t call, int unique, uint32_t* out, size_t cap,
+                        size_t* out_n);
+
 /* Per-kernel timing of the last *_dev call (HIP events on the call's stream), for the benchmark's
  * roofline. names/ms arrays of capacity cap; returns the number of kernels recorded. */
 int syzgpu_profile_enable(int on);

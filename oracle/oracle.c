@@ -503,3 +503,187 @@ void oracle_sha1(const uint8_t* data, size_t len, uint8_t* sig) {
     sig[4 * k + 3] = (uint8_t)h[k];
   }
 }
+
+/* ---- syz-manager/html.go: cover analytics over mgr.corpus ----------------------------------- */
+
+/* Open-addressing uint32 -> count map standing in for Go's map[uint32]int (html.go:214). */
+typedef struct {
+  uint64_t* slot; /* key + 1, 0 = free */
+  int64_t* cnt;
+  size_t mask, count;
+} u32map;
+
+static void u32map_init(u32map* m, size_t hint) {
+  size_t cap = 64;
+  while (cap < hint * 2) cap <<= 1;
+  m->slot = (uint64_t*)calloc(cap, sizeof(uint64_t));
+  m->cnt = (int64_t*)calloc(cap, sizeof(int64_t));
+  m->mask = cap - 1;
+  m->count = 0;
+}
+static void u32map_free(u32map* m) {
+  free(m->slot);
+  free(m->cnt);
+}
+static void u32map_inc(u32map* m, uint32_t k);
+static void u32map_grow(u32map* m) {
+  u32map n;
+  u32map_init(&n, m->mask + 1);
+  for (size_t i = 0; i <= m->mask; i++)
+    if (m->slot[i]) {
+      size_t j = u32hash((uint32_t)(m->slot[i] - 1)) & n.mask;
+      while (n.slot[j]) j = (j + 1) & n.mask;
+      n.slot[j] = m->slot[i];
+      n.cnt[j] = m->cnt[i];
+      n.count++;
+    }
+  u32map_free(m);
+  *m = n;
+}
+static void u32map_inc(u32map* m, uint32_t k) {
+  if ((m->count + 1) * 2 > m->mask + 1) u32map_grow(m);
+  for (size_t i = u32hash(k) & m->mask;; i = (i + 1) & m->mask) {
+    if (m->slot[i] == 0) {
+      m->slot[i] = (uint64_t)k + 1;
+      m->cnt[i] = 1;
+      m->count++;
+      return;
+    }
+    if (m->slot[i] == (uint64_t)k + 1) {
+      m->cnt[i]++;
+      return;
+    }
+  }
+}
+
+/* html.go:213-237 uniqueCover(perCall). Returns a malloc'ed, Canonicalized list in *out. */
+static size_t unique_cover(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                           uint32_t ngroups, int per_call, uint32_t** out) {
+  u32map total;
+  u32map_init(&total, 1024);
+  u32set* call_cover = NULL;
+  if (per_call) {
+    call_cover = (u32set*)calloc(ngroups ? ngroups : 1, sizeof(u32set));
+    for (uint32_t g = 0; g < ngroups; g++) u32set_init(&call_cover[g], 16);
+  }
+  for (size_t e = 0; e < n; e++) {
+    for (uint64_t j = off[e]; j < off[e + 1]; j++) {
+      const uint32_t pc = pcs[j];
+      if (per_call) {
+        if (u32set_has(&call_cover[group[e]], pc)) continue;
+        u32set_add(&call_cover[group[e]], pc);
+      }
+      u32map_inc(&total, pc);
+    }
+  }
+  size_t k = 0;
+  uint32_t* cov = (uint32_t*)malloc((total.count ? total.count : 1) * sizeof(uint32_t));
+  for (size_t i = 0; i <= total.mask; i++) /* map order: arbitrary, as in Go */
+    if (total.slot[i] && total.cnt[i] == 1) cov[k++] = (uint32_t)(total.slot[i] - 1);
+  size_t nk = 0;
+  oracle_canonicalize(cov, k, &nk);
+  u32map_free(&total);
+  if (per_call) {
+    for (uint32_t g = 0; g < ngroups; g++) free(call_cover[g].slot);
+    free(call_cover);
+  }
+  *out = cov;
+  return nk;
+}
+
+/* cc.cov = cover.Union(cc.cov, inp.Cover) for the inputs of group g (all inputs when g < 0). */
+static size_t union_of(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n, int64_t g,
+                       uint32_t** out) {
+  uint32_t* acc = (uint32_t*)malloc(sizeof(uint32_t));
+  size_t na = 0;
+  for (size_t e = 0; e < n; e++) {
+    if (g >= 0 && group[e] != (uint32_t)g) continue;
+    const size_t L = (size_t)(off[e + 1] - off[e]);
+    uint32_t* u = (uint32_t*)malloc((na + L + 1) * sizeof(uint32_t));
+    size_t nu = 0;
+    oracle_setop(2, acc, na, pcs + off[e], L, u, na + L + 1, &nu);
+    free(acc);
+    acc = u;
+    na = nu;
+  }
+  *out = acc;
+  return na;
+}
+
+static size_t intersection_len(const uint32_t* a, size_t na, const uint32_t* b, size_t nb) {
+  uint32_t* tmp = (uint32_t*)malloc((na < nb ? na : nb) * sizeof(uint32_t) + 4);
+  size_t k = 0;
+  oracle_setop(3, a, na, b, nb, tmp, (na < nb ? na : nb) + 1, &k);
+  free(tmp);
+  return k;
+}
+
+int oracle_cover_stats(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                       uint32_t ngroups, uint64_t* call_inputs, uint64_t* call_cover, uint64_t* call_unique,
+                       uint64_t* totals, uint32_t* input_unique) {
+  for (size_t e = 0; e < n; e++)
+    if (group[e] >= ngroups) return 1;
+  uint32_t *uc_call = NULL, *uc_input = NULL;
+  const size_t nuc_call = unique_cover(pcs, off, group, n, ngroups, 1, &uc_call);
+  const size_t nuc_input = unique_cover(pcs, off, group, n, ngroups, 0, &uc_input);
+  /* html.go:67-97: calls[inp.Call].count / .cov, cov = Union over calls (map order; Union commutes) */
+  uint32_t* cov = (uint32_t*)malloc(sizeof(uint32_t));
+  size_t ncov = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    uint64_t cnt = 0;
+    for (size_t e = 0; e < n; e++) cnt += group[e] == g;
+    uint32_t* cc = NULL;
+    const size_t ncc = union_of(pcs, off, group, n, g, &cc);
+    call_inputs[g] = cnt;
+    call_cover[g] = ncc;
+    call_unique[g] = intersection_len(cc, ncc, uc_call, nuc_call);
+    uint32_t* u = (uint32_t*)malloc((ncov + ncc + 1) * sizeof(uint32_t));
+    size_t nu = 0;
+    oracle_setop(2, cov, ncov, cc, ncc, u, ncov + ncc + 1, &nu);
+    free(cov);
+    cov = u;
+    ncov = nu;
+    free(cc);
+  }
+  totals[0] = ncov;
+  totals[1] = nuc_call;
+  totals[2] = nuc_input;
+  /* html.go:158-170 httpCorpus: len(cover.Intersection(inp.Cover, totalUnique)) */
+  for (size_t e = 0; e < n; e++)
+    input_unique[e] = (uint32_t)intersection_len(pcs + off[e], (size_t)(off[e + 1] - off[e]), uc_input, nuc_input);
+  free(cov);
+  free(uc_call);
+  free(uc_input);
+  return 0;
+}
+
+int oracle_corpus_cover(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                        uint32_t ngroups, int64_t call, int unique, uint32_t* out, size_t cap, size_t* out_n) {
+  if (call >= (int64_t)ngroups || unique < 0 || unique > 2) return 1;
+  uint32_t* res = NULL;
+  size_t nres = 0;
+  if (call < 0 && unique) {
+    nres = unique_cover(pcs, off, group, n, ngroups, unique == 1, &res);
+  } else {
+    nres = union_of(pcs, off, group, n, call, &res);
+    if (unique) {
+      uint32_t* uc = NULL;
+      const size_t nuc = unique_cover(pcs, off, group, n, ngroups, unique == 1, &uc);
+      uint32_t* x = (uint32_t*)malloc((nres + 1) * sizeof(uint32_t));
+      size_t nx = 0;
+      oracle_setop(3, res, nres, uc, nuc, x, nres + 1, &nx);
+      free(res);
+      free(uc);
+      res = x;
+      nres = nx;
+    }
+  }
+  *out_n = nres;
+  int rc = 0;
+  if (nres > cap)
+    rc = 6;
+  else
+    memcpy(out, res, nres * sizeof(uint32_t));
+  free(res);
+  return rc;
+}

@@ -77,6 +77,18 @@ void oracle_prog_scan(const uint8_t* data, size_t len, uint32_t* ncalls, uint8_t
 /* hash/hash.go:13-15  Hash = sha1.Sum (FIPS 180-4 SHA-1), digest into sig[20]. */
 void oracle_sha1(const uint8_t* data, size_t len, uint8_t* sig);
 
+/* syz-manager/html.go:67-97 (per call: CallCov.count, len(CallCov.cov), len(Intersection(cov,
+ * uniqueCover(true))); totals[0] = len of the Union over calls), html.go:213-237 uniqueCover
+ * (totals[1] = perCall, totals[2] = per input) and html.go:158-170 (input_unique[e] =
+ * len(Intersection(corpus[e].Cover, uniqueCover(false)))). Literal: Union grown input by input. */
+int oracle_cover_stats(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                       uint32_t ngroups, uint64_t* call_inputs, uint64_t* call_cover, uint64_t* call_unique,
+                       uint64_t* totals, uint32_t* input_unique);
+
+/* httpCover's lists (html.go:186-211) in the form of syzgpu_corpus_cover (include/syzgpu.h). */
+int oracle_corpus_cover(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                        uint32_t ngroups, int64_t call, int unique, uint32_t* out, size_t cap, size_t* out_n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -49,6 +49,10 @@ def lib():
         L.oracle_prog_scan.restype = None
         L.oracle_sha1.argtypes = [_u8p, ctypes.c_size_t, _u8p]
         L.oracle_sha1.restype = None
+        L.oracle_cover_stats.argtypes = [_u32p, _u64p, _u32p, ctypes.c_size_t, ctypes.c_uint32, _u64p, _u64p,
+                                         _u64p, _u64p, _u32p]
+        L.oracle_corpus_cover.argtypes = [_u32p, _u64p, _u32p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int64,
+                                          ctypes.c_int, _u32p, ctypes.c_size_t, _szp]
         _LIB = L
     return _LIB
 
@@ -191,3 +195,29 @@ def sha1(data, off):
         b = int(off[i])
         L.oracle_sha1(ctypes.cast(base + b, _u8p), int(off[i + 1]) - b, ctypes.cast(sig.ctypes.data + 20 * i, _u8p))
     return sig[:n].copy()
+
+
+def cover_stats(pcs, off, group, ngroups):
+    """syz-manager/html.go analytics (see oracle_cover_stats): dict of numpy arrays."""
+    pcs = np.ascontiguousarray(pcs, dtype=np.uint32)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    group = np.ascontiguousarray(group, dtype=np.uint32)
+    n = off.size - 1
+    ci, cc, cu = (np.zeros(max(ngroups, 1), dtype=np.uint64) for _ in range(3))
+    tot = np.zeros(3, dtype=np.uint64)
+    iu = np.zeros(max(n, 1), dtype=np.uint32)
+    _check(lib().oracle_cover_stats(_p(pcs, _u32p), _p(off, _u64p), _p(group, _u32p), n, ngroups, _p(ci, _u64p),
+                                    _p(cc, _u64p), _p(cu, _u64p), _p(tot, _u64p), _p(iu, _u32p)), "cover_stats")
+    return dict(call_inputs=ci[:ngroups], call_cover=cc[:ngroups], call_unique=cu[:ngroups], totals=tot,
+                input_unique=iu[:n])
+
+
+def corpus_cover(pcs, off, group, ngroups, call, unique):
+    pcs = np.ascontiguousarray(pcs, dtype=np.uint32)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    group = np.ascontiguousarray(group, dtype=np.uint32)
+    out = np.empty(pcs.size + 1, dtype=np.uint32)
+    m = ctypes.c_size_t()
+    _check(lib().oracle_corpus_cover(_p(pcs, _u32p), _p(off, _u64p), _p(group, _u32p), off.size - 1, ngroups, call,
+                                     unique, _p(out, _u32p), out.size, ctypes.byref(m)), "corpus_cover")
+    return out[: m.value].copy()

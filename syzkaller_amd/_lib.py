@@ -56,6 +56,9 @@ SIGNATURES = {
     "syzgpu_corpus_minimize_end_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp]),
     "syzgpu_corpus_export_sel_dev": (_c.c_int, [_vp, _vp, _vp, _c.c_uint32, _vp, _vp]),
     "syzgpu_corpus_import_sel_dev": (_c.c_int, [_vp, _vp, _vp, _c.c_uint32, _vp, _vp]),
+    "syzgpu_corpus_cover_stats": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "syzgpu_corpus_cover_stats_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "syzgpu_corpus_cover": (_c.c_int, [_vp, _c.c_int64, _c.c_int, _vp, _sz, _vp]),
     "syzgpu_profile_enable": (_c.c_int, [_c.c_int]),
     "syzgpu_profile_only": (_c.c_int, [_c.c_char_p]),
     "syzgpu_profile_read": (_sz, [_vp, _vp, _vp, _sz]),

@@ -15,12 +15,14 @@ Batched forms serve the manager/fuzzer loops that call these per input:
     SetOpBatch(op, a_list, b_list)             one launch for many pairs
     CanonicalizeBatch(pcs, off)
     NoveltyBatch(...)                          syz-fuzzer/fuzzer.go:446-470
+    CoverStore(...)                            the resident mgr.corpus: Minimize, and the manager's cover
+                                               analytics CoverStats / Cover / UniqueCover (html.go)
 Covers are numpy uint32 arrays. Go's nil result is returned as an empty array.
 """
 import numpy as np
 
 from . import _lib
-from ._lib import check, lib, ptr
+from ._lib import ECAPACITY, check, lib, ptr
 
 SENT = 0xFFFFFFFF  # cover.go:17
 
@@ -223,6 +225,37 @@ class CoverStore:
         goff = np.zeros(self.ngroups + 1, dtype=np.uint64)
         check(lib().syzgpu_corpus_minimize(self._h, ptr(out), ptr(goff)))
         return out[: int(goff[-1])].copy(), goff
+
+    # ---- the manager's cover analytics (syz-manager/html.go) ----
+    def CoverStats(self):
+        """html.go:67-97 per call (Inputs, Cover, UniqueCover), the "cover" stat, len(uniqueCover(perCall))
+        (html.go:213-237) and httpCorpus's per-input UniqueCover (html.go:158-170), in one GPU pass."""
+        G, n = self.ngroups, self.n
+        ci, cc, cu = (np.zeros(max(G, 1), dtype=np.uint64) for _ in range(3))
+        tot = np.zeros(3, dtype=np.uint64)
+        iu = np.zeros(max(n, 1), dtype=np.uint32)
+        check(lib().syzgpu_corpus_cover_stats(self._h, ptr(ci), ptr(cc), ptr(cu), ptr(tot), ptr(iu)))
+        return dict(call_inputs=ci[:G], call_cover=cc[:G], call_unique=cu[:G], cover=int(tot[0]),
+                    unique_per_call=int(tot[1]), unique_per_input=int(tot[2]), input_unique=iu[:n])
+
+    def Cover(self, call=-1, unique=0):
+        """httpCover's PC list (html.go:186-211): call >= 0 -> that call's Union [∩ uniqueCover(unique == 1)];
+        call < 0 -> the Union of all calls (unique = 0) or uniqueCover(unique == 1) itself."""
+        L = lib()
+        m = np.zeros(1, dtype=np.uint64)
+        cap = 1 << 16
+        while True:
+            out = np.empty(cap, dtype=np.uint32)
+            rc = L.syzgpu_corpus_cover(self._h, call, unique, ptr(out), cap, ptr(m))
+            if rc == ECAPACITY and int(m[0]) > cap:
+                cap = int(m[0])
+                continue
+            check(rc)
+            return out[: int(m[0])].copy()
+
+    def UniqueCover(self, perCall):
+        """html.go:213-237 uniqueCover(perCall)."""
+        return self.Cover(-1, 1 if perCall else 2)
 
     def close(self):
         if getattr(self, "_h", 0):

@@ -18,7 +18,7 @@
 #include <memory>
 #include <numeric>
 
-#include "pipeline.hpp"
+#include "store.hpp"
 
 namespace syz {
 
@@ -653,8 +653,6 @@ namespace syz {
 // window's min Go-sort rank per id in a direct-mapped LDS table (no hashing, no scatter), and the
 // rank that wins an id marks its input as kept (cover.go:116-129 as first occurrence).
 // =====================================================================================================
-constexpr uint32_t WIN_BITS = 15;
-constexpr uint32_t WIN = 1u << WIN_BITS;  // ids per LDS window (u32 min-rank table = 128 KB)
 
 __global__ __launch_bounds__(BK_BLOCK) void k_bucket_scatter_pos(const Chunk* chunks, const GBucket* gb,
                                                                  const uint32_t* members, const uint64_t* off,
@@ -811,18 +809,6 @@ __global__ void k_el_init(const uint32_t* members, const uint64_t* off, size_t n
 // cover's slice of ids in window w, as window-relative u16, each slice padded to a multiple of VEC
 // with copies of its last id (min is idempotent, so padding never changes a result). Every VEC-id
 // vector belongs to exactly one member: vmem[v] names it, so the kernel needs no segment search.
-constexpr uint32_t VEC = 8;                 // ids per 16-byte vector
-constexpr uint64_t CHUNK_VECS = 1u << 16;   // vectors per work item (1 MiB of ids)
-constexpr uint32_t BM_WORDS = 6144;         // LDS rank bitmap: 196608 ranks per pass
-constexpr uint32_t RANK_NONE = 0xFFFFFFFFu;
-
-struct VecWork {
-  uint32_t g;     // call group
-  uint32_t nids;  // ids in this window (<= WIN)
-  uint64_t vbeg, vend;
-  uint32_t gtab;  // RANK_NONE: sole chunk of its panel, emit directly; else index of a global table
-  uint32_t win;   // id window of the panel (the unit of key-space sharding)
-};
 
 constexpr int VM_BLOCK = 1024;
 #ifndef SYZ_VM_DEPTH
@@ -1013,51 +999,6 @@ __global__ void k_gather_u64(const uint64_t* src, const uint64_t* idx, size_t n,
 }
 
 // ---- the store object ----------------------------------------------------------------------------------
-template <class T>
-struct DevArr {
-  T* p = nullptr;
-  size_t n = 0;
-  void alloc(size_t count) {
-    free();
-    n = count;
-    SYZ_HIP(hipMalloc(&p, (count ? count : 1) * sizeof(T)));
-  }
-  void free() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
-};
-
-struct Corpus {
-  size_t n = 0;
-  uint32_t G = 0;
-  uint64_t total_pcs = 0, total_ids = 0, total_vecs = 0;
-  DevArr<uint64_t> off, gstart, gdict;
-  DevArr<uint32_t> group, members, member_of, nwin, dict, gtabs, vmem;
-  DevArr<uint32_t> gtchunks, gtdone;  // work items per shared window table, and their arrivals
-  DevArr<uint16_t> prog_len, ids16;
-  DevArr<VecWork> work;  // work items of the big call groups first, then those of the small ones
-  std::vector<VecWork> hwork;
-  size_t nbig_work = 0;                        // work items of the big call groups
-  uint64_t big_entries = 0, big_pcs = 0;       // entries / PCs in call groups above GS_T_SEG
-  std::vector<VecWork> hwork_all;              // every work item (hwork: those of this rank's key parts)
-  uint64_t big_vecs_all = 0, big_vecs = 0;     // id vectors of the big groups: all / in hwork
-  DevArr<uint8_t> count_hist;                  // groups counted in len_hist (set_parts); unset: all
-  bool has_count_hist = false;
-  DevArr<uint32_t> xg;                         // selection-exchange list (groups, byte offsets)
-  DevArr<uint64_t> xo;
-  std::vector<uint64_t> xkey;
-  std::vector<uint64_t> hstart;
-  GosortPlan gsplan;
-  uint32_t max_prog_len = 0;
-  uint32_t ngtabs = 0;
-  ~Corpus() {
-    off.free(); gstart.free(); gdict.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
-    gtchunks.free(); gtdone.free(); count_hist.free(); xg.free(); xo.free();
-    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free();
-  }
-};
 
 // Orders this rank's work items and uploads them: big call groups (sorted by the global rounds)
 // first, small ones (LDS packs, sorted on the side stream) after, so each class's Minimize runs as

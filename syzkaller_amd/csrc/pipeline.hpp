@@ -43,6 +43,8 @@ void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const std::vector<uin
 constexpr int RADIX_BITS = 8;
 void radix_sort_pairs(uint64_t*& keys, uint32_t*& vals, uint64_t*& ktmp, uint32_t*& vtmp, size_t n, int end_bit,
                       hipStream_t s);
+void radix_sort_pairs(uint32_t*& keys, uint32_t*& vals, uint32_t*& ktmp, uint32_t*& vtmp, size_t n, int end_bit,
+                      hipStream_t s);
 
 // setops.hip
 uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64_t na, const uint32_t* b,

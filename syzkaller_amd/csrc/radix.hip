@@ -12,14 +12,15 @@ constexpr int RS_TILE = RS_BLOCK * RS_ITEMS;
 constexpr int RS_RADIX = 1 << RADIX_BITS;
 constexpr int RS_WAVES = RS_BLOCK / 64;
 
-__global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint64_t* __restrict__ keys, size_t n, int shift,
+template <class KT>
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const KT* __restrict__ keys, size_t n, int shift,
                                                       uint32_t ntiles, uint32_t* __restrict__ counts) {
   __shared__ uint32_t h[RS_WAVES][RS_RADIX];
   for (int i = threadIdx.x; i < RS_WAVES * RS_RADIX; i += RS_BLOCK) (&h[0][0])[i] = 0;
   __syncthreads();
   const int w = threadIdx.x >> 6;
   const size_t base = (size_t)blockIdx.x * RS_TILE + threadIdx.x;
-  uint64_t k[RS_ITEMS];
+  KT k[RS_ITEMS];
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; i++) {
     const size_t p = base + (size_t)i * RS_BLOCK;
@@ -37,10 +38,11 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const uint64_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint64_t* __restrict__ kin,
+template <class KT>
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const KT* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin, size_t n, int shift,
                                                          uint32_t ntiles, const uint64_t* __restrict__ offs,
-                                                         uint64_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+                                                         KT* __restrict__ kout, uint32_t* __restrict__ vout) {
   __shared__ uint32_t run[RS_RADIX];
   __shared__ uint32_t wc[RS_WAVES][RS_RADIX];
   __shared__ uint64_t goff[RS_RADIX];
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint64_t* __restr
   for (int i = threadIdx.x; i < RS_WAVES * RS_RADIX; i += RS_BLOCK) (&wc[0][0])[i] = 0;
   const int w = threadIdx.x >> 6;
   const size_t base = (size_t)blockIdx.x * RS_TILE + threadIdx.x;
-  uint64_t k[RS_ITEMS];
+  KT k[RS_ITEMS];
   uint32_t v[RS_ITEMS];
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; i++) {
@@ -99,8 +101,9 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const uint64_t* __restr
 
 // Sorts n pairs by key bits [0, end_bit), stably. Ping-pongs between (keys, vals) and (ktmp, vtmp);
 // on return keys/vals point at the sorted arrays (the pointers may be swapped with the tmp ones).
-void radix_sort_pairs(uint64_t*& keys, uint32_t*& vals, uint64_t*& ktmp, uint32_t*& vtmp, size_t n, int end_bit,
-                      hipStream_t s) {
+template <class KT>
+static void radix_sort_pairs_t(KT*& keys, uint32_t*& vals, KT*& ktmp, uint32_t*& vtmp, size_t n, int end_bit,
+                               hipStream_t s) {
   if (n <= 1) return;
   if (n >= (1ull << 40)) fail(SYZGPU_EINVAL, "radix sort: too many items");
   const size_t ntiles = (n + RS_TILE - 1) / RS_TILE;
@@ -109,14 +112,24 @@ void radix_sort_pairs(uint64_t*& keys, uint32_t*& vals, uint64_t*& ktmp, uint32_
   uint32_t* counts = sc.get<uint32_t>("rs_counts", ntiles * RS_RADIX + 1);
   uint64_t* offs = sc.get<uint64_t>("rs_offs", ntiles * RS_RADIX + 1);
   for (int shift = 0; shift < end_bit; shift += RADIX_BITS) {
-    k_rs_hist<<<(unsigned)ntiles, RS_BLOCK, 0, s>>>(keys, n, shift, (uint32_t)ntiles, counts);
+    k_rs_hist<KT><<<(unsigned)ntiles, RS_BLOCK, 0, s>>>(keys, n, shift, (uint32_t)ntiles, counts);
     SYZ_LAUNCHED();
     exclusive_scan_u32(counts, offs, ntiles * RS_RADIX, s);
-    k_rs_scatter<<<(unsigned)ntiles, RS_BLOCK, 0, s>>>(keys, vals, n, shift, (uint32_t)ntiles, offs, ktmp, vtmp);
+    k_rs_scatter<KT><<<(unsigned)ntiles, RS_BLOCK, 0, s>>>(keys, vals, n, shift, (uint32_t)ntiles, offs, ktmp, vtmp);
     SYZ_LAUNCHED();
     std::swap(keys, ktmp);
     std::swap(vals, vtmp);
   }
+}
+
+void radix_sort_pairs(uint64_t*& keys, uint32_t*& vals, uint64_t*& ktmp, uint32_t*& vtmp, size_t n, int end_bit,
+                      hipStream_t s) {
+  radix_sort_pairs_t(keys, vals, ktmp, vtmp, n, end_bit, s);
+}
+
+void radix_sort_pairs(uint32_t*& keys, uint32_t*& vals, uint32_t*& ktmp, uint32_t*& vtmp, size_t n, int end_bit,
+                      hipStream_t s) {
+  radix_sort_pairs_t(keys, vals, ktmp, vtmp, n, end_bit, s);
 }
 
 }  // namespace syz

@@ -1,0 +1,78 @@
+// The resident corpus store (the device analog of syz-manager's mgr.corpus, manager.go:52-65),
+// shared by Minimize (minimize.hip) and the manager's cover analytics (analytics.hip).
+#pragma once
+#include <vector>
+
+#include "pipeline.hpp"
+
+namespace syz {
+
+constexpr uint32_t WIN_BITS = 15;
+constexpr uint32_t WIN = 1u << WIN_BITS;  // ids per LDS window (u32 min-rank table = 128 KB)
+
+constexpr uint32_t VEC = 8;                 // ids per 16-byte vector
+constexpr uint64_t CHUNK_VECS = 1u << 16;   // vectors per work item (1 MiB of ids)
+constexpr uint32_t BM_WORDS = 6144;         // LDS rank bitmap: 196608 ranks per pass
+constexpr uint32_t RANK_NONE = 0xFFFFFFFFu;
+
+struct VecWork {
+  uint32_t g;     // call group
+  uint32_t nids;  // ids in this window (<= WIN)
+  uint64_t vbeg, vend;
+  uint32_t gtab;  // RANK_NONE: sole chunk of its panel, emit directly; else index of a global table
+  uint32_t win;   // id window of the panel (the unit of key-space sharding)
+};
+
+// the cover analytics of a store (analytics.hip), computed on first use and kept with it
+struct CoverStats;
+void corpus_stats_free(CoverStats*);
+
+template <class T>
+struct DevArr {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    free();
+    n = count;
+    SYZ_HIP(hipMalloc(&p, (count ? count : 1) * sizeof(T)));
+  }
+  void free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct Corpus {
+  size_t n = 0;
+  uint32_t G = 0;
+  uint64_t total_pcs = 0, total_ids = 0, total_vecs = 0;
+  DevArr<uint64_t> off, gstart, gdict;
+  DevArr<uint32_t> group, members, member_of, nwin, dict, gtabs, vmem;
+  DevArr<uint32_t> gtchunks, gtdone;  // work items per shared window table, and their arrivals
+  DevArr<uint16_t> prog_len, ids16;
+  DevArr<VecWork> work;  // work items of the big call groups first, then those of the small ones
+  std::vector<VecWork> hwork;
+  size_t nbig_work = 0;                        // work items of the big call groups
+  uint64_t big_entries = 0, big_pcs = 0;       // entries / PCs in call groups above GS_T_SEG
+  std::vector<VecWork> hwork_all;              // every work item (hwork: those of this rank's key parts)
+  uint64_t big_vecs_all = 0, big_vecs = 0;     // id vectors of the big groups: all / in hwork
+  DevArr<uint8_t> count_hist;                  // groups counted in len_hist (set_parts); unset: all
+  bool has_count_hist = false;
+  DevArr<uint32_t> xg;                         // selection-exchange list (groups, byte offsets)
+  DevArr<uint64_t> xo;
+  std::vector<uint64_t> xkey;
+  std::vector<uint64_t> hstart;
+  GosortPlan gsplan;
+  uint32_t max_prog_len = 0;
+  uint32_t ngtabs = 0;
+  CoverStats* stats = nullptr;
+  ~Corpus() {
+    corpus_stats_free(stats);
+    off.free(); gstart.free(); gdict.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
+    gtchunks.free(); gtdone.free(); count_hist.free(); xg.free(); xo.free();
+    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free();
+  }
+};
+
+}  // namespace syz

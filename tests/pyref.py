@@ -278,3 +278,42 @@ def novelty(covers, groups, maxcover, flakes):
         else:
             is_new.append(0)
     return is_new, mc
+
+
+# ---- syz-manager/html.go:67-97, 158-170, 186-237 ----------------------------------------------
+def unique_cover(covers, calls, per_call):
+    """html.go:213-237 literally: dict counts, Canonicalize of the count==1 keys."""
+    total = {}
+    call_cover = {}
+    for cov, c in zip(covers, calls):
+        if per_call and c not in call_cover:
+            call_cover[c] = {}
+        for pc in cov:
+            pc = int(pc)
+            if per_call:
+                if call_cover[c].get(pc):
+                    continue
+                call_cover[c][pc] = True
+            total[pc] = total.get(pc, 0) + 1
+    return canonicalize([pc for pc, n in total.items() if n == 1])
+
+
+def cover_stats(covers, calls, ngroups):
+    """httpSummary's per-call table and "cover" stat, and httpCorpus's per-input UniqueCover."""
+    cc = {}
+    for cov, c in zip(covers, calls):
+        if c not in cc:
+            cc[c] = [0, []]
+        cc[c][0] += 1
+        cc[c][1] = setop("union", cc[c][1], list(cov))
+    total_unique = unique_cover(covers, calls, True)
+    cov_all = []
+    ci, ccov, cu = [0] * ngroups, [0] * ngroups, [0] * ngroups
+    for c, (count, cov) in cc.items():
+        cov_all = setop("union", cov_all, cov)
+        ci[c], ccov[c] = count, len(cov)
+        cu[c] = len(setop("intersection", cov, total_unique))
+    uc_input = unique_cover(covers, calls, False)
+    iu = [len(setop("intersection", list(cov), uc_input)) for cov in covers]
+    return dict(call_inputs=ci, call_cover=ccov, call_unique=cu, cover=len(cov_all),
+                unique_per_call=len(total_unique), unique_per_input=len(uc_input), input_unique=iu)
