@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--text", type=int, default=1, help="also time the text pass over the kept programs at N=1")
     ap.add_argument("--novelty", type=int, default=1, help="also time config 3 (triage batch) at N=1")
     ap.add_argument("--novelty-covers", type=int, default=1_000_000)
+    ap.add_argument("--hub", type=int, default=1, help="also time config 5's hub ingest (scan + SHA-1 + dedup) at N=1")
     ap.add_argument("--analytics", type=int, default=1, help="also time the manager's cover analytics at N=1")
     ap.add_argument("--analytics-cpu-sample", type=int, default=10_000)
     ap.add_argument("--novelty-cpu-sample", type=int, default=20_000)
@@ -294,6 +295,9 @@ def main():
         nov = None
         if args.novelty and world == 1 and not args.emulate:
             nov = novelty_leg(args, dev, L, read_prof)
+        hubr = None
+        if args.hub and world == 1 and not args.emulate:
+            hubr = hub_leg(args, dev, L, read_prof, corp, sptr)
         ana = None
         if args.analytics and world == 1 and not args.emulate:
             ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr)
@@ -328,6 +332,7 @@ def main():
             "minimize_corpus_tail": tail,
             "novelty_config3": nov,
             "cover_analytics": ana,
+            "hub_ingest_config5": hubr,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -460,6 +465,100 @@ def analytics_leg(args, dev, L, read_prof, store, corp, sptr):
         res["cpu_baseline"] = {"value": round(k / dt, 1), "unit": "progs/s", "cores": 1, "kind": "port",
                                "sample": "first %d programs of the corpus; oracle_cover_stats (literal html.go), "
                                          "%.2f s" % (k, dt)}
+    return res
+
+
+def hub_leg(args, dev, L, read_prof, corp, sptr):
+    """BASELINE.json configs[4]'s ingest: syz-hub receives the corpora of 8 managers (here 8 x 125k
+    programs per GPU, 10% of them copies of another manager's programs) and adds them to its corpus
+    (state.go:209-223 addInput: prog.CallSet checks, hash.Hash, map insert on first occurrence). One step
+    = empty the hub's signature set, syzgpu_prog_scan_dev (checks + SHA-1 of every program) and
+    syzgpu_sigset_insert_dev of the whole batch in order; program text resident in HBM."""
+    import torch
+    from syzkaller_amd import prog, synth
+    n = corp.n
+    t0 = time.perf_counter()
+    data, off = synth.prog_text(args.seed + 0x50, corp.prog_len)
+    rnd = np.random.default_rng(9)
+    idx = np.arange(n)
+    dup = rnd.random(n) < 0.10
+    mgr = idx // max(1, n // 8)
+    src = rnd.integers(0, n, int(dup.sum()))
+    idx[dup] = src  # a copy of another program (mostly another manager's)
+    lens = (off[1:] - off[:-1]).astype(np.int64)[idx]
+    noff = np.zeros(n + 1, np.int64)
+    noff[1:] = np.cumsum(lens)
+    d_data = torch.from_numpy(data).to(dev)
+    byte_prog = torch.repeat_interleave(torch.arange(n, device=dev), torch.from_numpy(lens).to(dev))
+    starts = torch.from_numpy(off[:-1].astype(np.int64)[idx]).to(dev)
+    d_noff = torch.from_numpy(noff).to(dev)
+    pos = torch.arange(int(noff[-1]), device=dev, dtype=torch.int64)
+    blob = d_data[starts[byte_prog] + pos - d_noff[:-1][byte_prog]].contiguous()
+    del byte_prog, pos, d_data
+    gen = time.perf_counter() - t0
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    sigs = torch.zeros((n, 20), dtype=torch.uint8, device=dev)
+    added = torch.zeros(n, dtype=torch.uint8, device=dev)
+    h = np.zeros(1, np.uint64)
+    _lib_check(L.syzgpu_sigset_create(n, h.ctypes.data))
+    hs = int(h[0])
+    na = np.zeros(1, np.uint64)
+
+    def run():
+        _lib_check(L.syzgpu_sigset_clear(hs, sptr))
+        prog.ProgScanDev(blob, d_noff, n, None, None, status, sigs, sptr)
+        _lib_check(L.syzgpu_sigset_insert_dev(hs, sigs.data_ptr(), None, n, 1, added.data_ptr(), na.ctypes.data,
+                                              sptr))
+    run()
+    torch.cuda.synchronize()
+    sg = sigs.cpu().numpy()
+    distinct = np.unique(sg.view(np.dtype((np.void, 20))).ravel(), return_index=True)[1]
+    want = np.zeros(n, np.uint8)
+    want[distinct] = 1
+    ok = bool(not status.cpu().numpy().any() and np.array_equal(added.cpu().numpy(), want))
+    steps = max(1, args.steps)
+    L.syzgpu_profile_only(None)
+    L.syzgpu_profile_enable(1)
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t1) / steps
+    ev = read_prof()
+    L.syzgpu_profile_enable(0)
+    L.syzgpu_sigset_destroy(hs)
+    res = {"workload": "config5 ingest: 8 managers x %d programs, %.1f%% copies; %d distinct added" %
+                       (n // 8, 100.0 * dup.mean(), int(na[0])),
+           "metric": "hub ingest progs/sec", "ms": round(el * 1e3, 4), "progs_per_s": round(n / el, 1),
+           "text_bytes": int(noff[-1]), "added_first_occurrences_match": ok, "gen_s": round(gen, 2),
+           "kernels_ms": {k: round(e["ms"] / steps, 4) for k, e in sorted(ev.items(), key=lambda kv: -kv[1]["ms"])}}
+    if "prog_lane" in ev:
+        e = ev["prog_lane"]
+        ms = e["ms"] / e["launches"]
+        blocks = int(((lens + 8) // 64 + 1).sum())
+        res["roofline"] = {"bound": "valu", "kernel": "prog_lane", "avg_launch_ms": round(ms, 4),
+                           "sha1_blocks_per_s": round(blocks / (ms * 1e-3), 1),
+                           "hbm_achieved": round((int(noff[-1]) + 44 * n) / (ms * 1e-3) / 1e9, 1),
+                           "hbm_peak": HBM_PEAK_GBS}
+    if args.cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        k = min(200_000, n)
+        hb = blob[:int(noff[k])].cpu().numpy()
+        ho = noff[:k + 1].astype(np.uint64)
+        t2 = time.perf_counter()
+        _, st = oracle.prog_scan(hb, ho)
+        sg2 = oracle.sha1(hb, ho)
+        seen = set()
+        for i in range(k):  # the hub's map insert (st.Corpus[sig] == nil)
+            if not st[i] & ~4:
+                b = sg2[i].tobytes()
+                if b not in seen:
+                    seen.add(b)
+        dt = time.perf_counter() - t2
+        res["cpu_baseline"] = {"value": round(k / dt, 1), "unit": "progs/s", "cores": 1, "kind": "port",
+                               "sample": "first %d programs of the batch; oracle_prog_scan + oracle_sha1 + a "
+                                         "Python set insert, %.2f s" % (k, dt)}
     return res
 
 

@@ -228,6 +228,37 @@ int syzgpu_corpus_cover_stats_dev(syzgpu_corpus* c, uint64_t* call_inputs, uint6
 int syzgpu_corpus_cover(syzgpu_corpus* c, int64_t call, int unique, uint32_t* out, size_t cap,
                         size_t* out_n);
 
+/* ---- signature sets: hash.Sig-keyed corpus maps (syz-hub/state/state.go, syz-manager/persistent.go) -- */
+/* A device-resident set of 20-byte program signatures (hash.Hash = sha1.Sum, hash/hash.go:13-15, as
+ * syzgpu_prog_scan writes them), each with a uint64 seq: the hub's Corpus map[hash.Sig]*Input
+ * (state.go:23-26, Input.seq), a manager's Corpus map[hash.Sig]bool (state.go:30-40) and the manager's
+ * PersistentSet (persistent.go:91-102). Signature arrays are n*20 bytes, 4-byte aligned.
+ *   insert: addInput (state.go:200-223) over a batch in order: items with mask[i] == 0 (prog.CallSet
+ *           failed) are skipped; added[i] = 1 iff item i is the first of its signature in the batch and
+ *           the signature was not in the set (it is inserted with `seq`); *nadded = the number added.
+ *   lookup: found[i] = the signature is in the set (seq[i] its seq, 0 if absent).
+ *   erase:  delete(map, sig) (state.go:164-171, 238-250; persistent.go:95-101): erased[i] = item i
+ *           removed it (one item per signature); *nerased = the number removed.
+ *   export: every signature in the set (map iteration order: unspecified) with its seq. */
+typedef struct syzgpu_sigset syzgpu_sigset;
+int syzgpu_sigset_create(size_t capacity_hint, syzgpu_sigset** out);
+int syzgpu_sigset_destroy(syzgpu_sigset* set);
+int syzgpu_sigset_size(const syzgpu_sigset* set, uint64_t* n);
+int syzgpu_sigset_clear(syzgpu_sigset* set, void* stream); /* empty it, keeping its capacity */
+int syzgpu_sigset_insert(syzgpu_sigset* set, const uint8_t* sigs, const uint8_t* mask, size_t n, uint64_t seq,
+                         uint8_t* added, uint64_t* nadded);
+int syzgpu_sigset_lookup(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8_t* found, uint64_t* seq);
+int syzgpu_sigset_erase(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8_t* erased, uint64_t* nerased);
+int syzgpu_sigset_export(syzgpu_sigset* set, uint8_t* sigs, uint64_t* seq, size_t cap, size_t* out_n);
+/* device forms (sigs/mask/added/found/seq/erased device pointers; enqueued on stream, the counts are
+ * returned after the batch completes) */
+int syzgpu_sigset_insert_dev(syzgpu_sigset* set, const uint8_t* sigs, const uint8_t* mask, size_t n,
+                             uint64_t seq, uint8_t* added, uint64_t* nadded, void* stream);
+int syzgpu_sigset_lookup_dev(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8_t* found,
+                             uint64_t* seq, void* stream);
+int syzgpu_sigset_erase_dev(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8_t* erased,
+                            uint64_t* nerased, void* stream);
+
 /* Per-kernel timing of the last *_dev call (HIP events on the call's stream), for the benchmark's
  * roofline. names/ms arrays of capacity cap; returns the number of kernels recorded. */
 int syzgpu_profile_enable(int on);

@@ -59,6 +59,17 @@ SIGNATURES = {
     "syzgpu_corpus_cover_stats": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_corpus_cover_stats_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_corpus_cover": (_c.c_int, [_vp, _c.c_int64, _c.c_int, _vp, _sz, _vp]),
+    "syzgpu_sigset_create": (_c.c_int, [_sz, _vp]),
+    "syzgpu_sigset_destroy": (_c.c_int, [_vp]),
+    "syzgpu_sigset_size": (_c.c_int, [_vp, _vp]),
+    "syzgpu_sigset_clear": (_c.c_int, [_vp, _vp]),
+    "syzgpu_sigset_insert": (_c.c_int, [_vp, _vp, _vp, _sz, _c.c_uint64, _vp, _vp]),
+    "syzgpu_sigset_lookup": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
+    "syzgpu_sigset_erase": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
+    "syzgpu_sigset_export": (_c.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    "syzgpu_sigset_insert_dev": (_c.c_int, [_vp, _vp, _vp, _sz, _c.c_uint64, _vp, _vp, _vp]),
+    "syzgpu_sigset_lookup_dev": (_c.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
+    "syzgpu_sigset_erase_dev": (_c.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
     "syzgpu_profile_enable": (_c.c_int, [_c.c_int]),
     "syzgpu_profile_only": (_c.c_int, [_c.c_char_p]),
     "syzgpu_profile_read": (_sz, [_vp, _vp, _vp, _sz]),

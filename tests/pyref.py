@@ -317,3 +317,103 @@ def cover_stats(covers, calls, ngroups):
     iu = [len(setop("intersection", list(cov), uc_input)) for cov in covers]
     return dict(call_inputs=ci, call_cover=ccov, call_unique=cu, cover=len(cov_all),
                 unique_per_call=len(total_unique), unique_per_input=len(uc_input), input_unique=iu)
+
+
+# ---- syz-hub/state/state.go (in memory), prog.CallSet (encoding.go:522-551) ------------------
+def call_set(data):
+    """prog.CallSet: the call names, or None on its errors (bufio.Scanner lines, 64 KiB limit)."""
+    calls = set()
+    lines = bytes(data).split(b"\n")
+    if lines and lines[-1] == b"":
+        lines = lines[:-1]
+    for ln in lines:
+        if len(ln) >= 64 * 1024:
+            break  # bufio.ErrTooLong stops the Scan loop; CallSet does not look at s.Err()
+        if ln.endswith(b"\r"):
+            ln = ln[:-1]
+        if not ln or ln[:1] == b"#":
+            continue
+        b = ln.find(b"(")
+        if b == -1:
+            return None
+        call = ln[:b]
+        eq = call.find(b"=")
+        if eq != -1:
+            eq += 1
+            while eq < len(call) and call[eq:eq + 1] == b" ":
+                eq += 1
+            call = call[eq:]
+        if not call:
+            return None
+        calls.add(call)
+    if not calls:
+        return None
+    return calls
+
+
+class HubState:
+    """state.go's Connect / Sync / addInput / pendingInputs / purgeCorpus with Go maps as dicts."""
+
+    def __init__(self):
+        import hashlib
+        self._sha1 = lambda b: hashlib.sha1(bytes(b)).digest()
+        self.seq = 0
+        self.corpus = {}  # sig -> (seq, prog)
+        self.managers = {}
+
+    def connect(self, name, fresh, calls, corpus):
+        self.seq += 1
+        mgr = self.managers.setdefault(name, {"seq": 0, "calls": set(), "corpus": {}})
+        if fresh:
+            mgr["seq"] = 0
+        mgr["calls"] = set(c.encode() if isinstance(c, str) else c for c in calls)
+        mgr["corpus"] = {}
+        for p in corpus:
+            self._add(mgr, p)
+        self._purge()
+
+    def sync(self, name, add, dels):
+        mgr = self.managers[name]
+        if dels:
+            for h in dels:
+                try:
+                    sig = bytes.fromhex(h)
+                except ValueError:
+                    continue
+                if len(sig) != 20:
+                    continue
+                mgr["corpus"].pop(sig, None)
+            self._purge()
+        if add:
+            self.seq += 1
+            for p in add:
+                self._add(mgr, p)
+        return self._pending(mgr)
+
+    def _add(self, mgr, p):
+        if call_set(p) is None:
+            return
+        sig = self._sha1(p)
+        mgr["corpus"][sig] = True
+        if sig not in self.corpus:
+            self.corpus[sig] = (self.seq, bytes(p))
+
+    def _pending(self, mgr):
+        if mgr["seq"] == self.seq:
+            return []
+        out = []
+        for sig, (seq, p) in self.corpus.items():
+            if mgr["seq"] > seq or mgr["corpus"].get(sig):
+                continue
+            if not call_set(p) <= mgr["calls"]:
+                continue
+            out.append(p)
+        mgr["seq"] = self.seq
+        return out
+
+    def _purge(self):
+        used = set()
+        for m in self.managers.values():
+            used |= set(m["corpus"])
+        for sig in [s for s in self.corpus if s not in used]:
+            del self.corpus[sig]
