@@ -471,7 +471,7 @@ def analytics_leg(args, dev, L, read_prof, store, corp, sptr):
 def hub_leg(args, dev, L, read_prof, corp, sptr):
     """BASELINE.json configs[4]'s ingest: syz-hub receives the corpora of 8 managers (here 8 x 125k
     programs per GPU, 10% of them copies of another manager's programs) and adds them to its corpus
-    (state.go:209-223 addInput: prog.CallSet checks, hash.Hash, map insert on first occurrence). One step
+    (state.go:211-228 addInput: prog.CallSet checks, hash.Hash, map insert on first occurrence). One step
     = empty the hub's signature set, syzgpu_prog_scan_dev (checks + SHA-1 of every program) and
     syzgpu_sigset_insert_dev of the whole batch in order; program text resident in HBM."""
     import torch
@@ -551,7 +551,7 @@ def hub_leg(args, dev, L, read_prof, corp, sptr):
         sg2 = oracle.sha1(hb, ho)
         seen = set()
         for i in range(k):  # the hub's map insert (st.Corpus[sig] == nil)
-            if not st[i] & ~4:
+            if not (int(st[i]) & ~4):
                 b = sg2[i].tobytes()
                 if b not in seen:
                     seen.add(b)

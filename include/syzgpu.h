@@ -233,7 +233,7 @@ int syzgpu_corpus_cover(syzgpu_corpus* c, int64_t call, int unique, uint32_t* ou
  * syzgpu_prog_scan writes them), each with a uint64 seq: the hub's Corpus map[hash.Sig]*Input
  * (state.go:23-26, Input.seq), a manager's Corpus map[hash.Sig]bool (state.go:30-40) and the manager's
  * PersistentSet (persistent.go:91-102). Signature arrays are n*20 bytes, 4-byte aligned.
- *   insert: addInput (state.go:200-223) over a batch in order: items with mask[i] == 0 (prog.CallSet
+ *   insert: addInput (state.go:211-228) over a batch in order: items with mask[i] == 0 (prog.CallSet
  *           failed) are skipped; added[i] = 1 iff item i is the first of its signature in the batch and
  *           the signature was not in the set (it is inserted with `seq`); *nadded = the number added.
  *   lookup: found[i] = the signature is in the set (seq[i] its seq, 0 if absent).

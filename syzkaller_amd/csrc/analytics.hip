@@ -3,7 +3,7 @@
 //                                uniqueCover(true))); the total cover len(Union over calls)
 //   uniqueCover  html.go:213-237 PCs counted once over calls (perCall) or over inputs, Canonicalized
 //   httpCorpus   html.go:158-170 per input: len(Intersection(inp.Cover, uniqueCover(false)))
-//   httpCover    html.go:186-211 the PC lists themselves
+//   httpCover    html.go:184-211 the PC lists themselves
 // The store already holds every call's distinct PCs as dense ids (dict) and every cover as a
 // panel-major id stream, so:
 //   1. k_vec_uniq streams the panels once (like k_vec_min) and keeps, per (call, id), the only input

@@ -1,6 +1,6 @@
 // Device-resident sets of program signatures (hash.Sig = sha1.Sum, hash/hash.go:13-15): the hub's
-// corpus map[hash.Sig]*Input with each input's seq (syz-hub/state/state.go:23-26, 209-222), a manager's
-// map[hash.Sig]bool (state.go:30-40, 206-208) and the manager's PersistentSet (syz-manager/
+// corpus map[hash.Sig]*Input with each input's seq (syz-hub/state/state.go:23-26, 211-228), a manager's
+// map[hash.Sig]bool (state.go:30-40, 211-218) and the manager's PersistentSet (syz-manager/
 // persistent.go:91-102, pruned by minimizeCorpus, manager.go:541-553).
 //
 // Open addressing with linear probing over 2^k slots, kept at most half full. A slot is claimed with one
@@ -9,7 +9,7 @@
 // for a slot claimed in the current batch, against the claiming item's own input signature, which
 // is always visible - so one launch resolves a whole batch with no waits on another lane's store and
 // exact 160-bit comparisons. In a batch, the FIRST item (batch order, atomicMin) of a new signature
-// is the one reported as added: the Go loop (state.go:209-223) inserts on the first occurrence and
+// is the one reported as added: the Go loop (state.go:211-228) inserts on the first occurrence and
 // finds the entry for the later ones. Erase keeps the slot (a tombstone keeps probe chains intact);
 // inserting the signature again revives it.
 #include <algorithm>
@@ -140,8 +140,12 @@ __global__ void k_sig_added(SigView T, const uint64_t* slot_of, const uint8_t* s
       a = T.claim[s] == round && T.owner[s] == (uint32_t)i;
     }
     if (added) added[i] = a;
-    if (a) atomicAdd(&nnew[0], 1ull);
-    if (state[i] == SG_NEW) atomicAdd(&nnew[1], 1ull);  // slots claimed (not revived)
+    // per-wave counts, one atomic per wave: the added items and the slots claimed (not revived)
+    const uint64_t ba = __ballot(a), bn = __ballot(state[i] == SG_NEW);
+    if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+      if (ba) atomicAdd(&nnew[0], (unsigned long long)__popcll(ba));
+      if (bn) atomicAdd(&nnew[1], (unsigned long long)__popcll(bn));
+    }
   }
 }
 
@@ -154,22 +158,25 @@ __global__ __launch_bounds__(SG_BLOCK) void k_sig_find(SigView T, const uint32_t
     sig_load(sigs, i, w);
     uint64_t s = sig_home(w, T.mask);
     uint8_t f = 0;
+    uint64_t q = 0;
     for (uint64_t probes = 0; probes <= T.mask; probes++, s = (s + 1) & T.mask) {
       if (T.tag[s] == 0) break;
       if (!sig_eq(T.key + 5 * s, w)) continue;
       if (mode == 0) {
         f = !T.dead[s];
-        if (seq_out) seq_out[i] = f ? T.seq[s] : 0;
+        if (f) q = T.seq[s];
       } else if (!T.dead[s]) {
         f = atomicExch(&T.dead[s], 1u) == 0;  // duplicates in one erase batch: one of them erases
-        if (f) {
-          T.owner[s] = 0xFFFFFFFFu;  // a later batch that revives it takes its first item as owner
-          atomicAdd(nerased, 1ull);
-        }
+        if (f) T.owner[s] = 0xFFFFFFFFu;      // a later batch that revives it takes its first item as owner
       }
       break;
     }
     if (found) found[i] = f;
+    if (seq_out) seq_out[i] = q;
+    if (mode == 1) {  // one atomic per wave
+      const uint64_t b = __ballot(f);
+      if (b && __lane_id() == __ffsll((long long)__ballot(1)) - 1) atomicAdd(nerased, (unsigned long long)__popcll(b));
+    }
   }
 }
 

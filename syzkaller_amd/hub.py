@@ -8,11 +8,11 @@ reference keeps in Go structures: the program bytes by signature, the managers' 
 counters. Files and RPC (state.go's directories, syz-hub/hub.go) are out of scope.
 
     SigSet                 map[hash.Sig]bool / map[hash.Sig]*Input (the seq of each entry)
-    State.Connect          state.go:130-157
+    State.Connect          state.go:128-157
     State.Sync             state.go:159-185
-    State.pendingInputs    state.go:187-207 (map order: the result is a set, as in the reference)
-    State.addInputs        state.go:209-225 (a batch of addInput calls, in order)
-    State.purgeCorpus      state.go:234-250
+    State.pendingInputs    state.go:188-209 (map order: the result is a set, as in the reference)
+    State.addInputs        state.go:211-228 (a batch of addInput calls, in order)
+    State.purgeCorpus      state.go:236-250
     PersistentSet.minimize persistent.go:91-102
 """
 import numpy as np
