@@ -817,36 +817,39 @@ constexpr int VM_BLOCK = 1024;
 constexpr int VM_DEPTH = SYZ_VM_DEPTH;  // vectors per lane per pipelined batch (k_vec_min)
 
 // Winning ranks of a window table (LDS or global) -> set bits of sel_bits (global rank bitmap).
-// Ranks of call g lie in [gstart[g], gstart[g+1]); they are deduplicated through an LDS bitmap so
-// that each kept input costs one bit-OR per table instead of one store per id.
+// Ranks of call g lie in [gstart[g], gstart[g+1]). Winners are mostly early ranks (the longest covers
+// come first in Go-sort order), so the first BM_WORDS*32 ranks of the call are deduplicated through
+// an LDS bitmap (one bit-OR per kept input instead of one per id) and the rarer later ones go straight
+// to sel_bits: one pass over the table whatever the call's size.
 template <bool ATOMIC_READ = false>
 __device__ __forceinline__ void emit_winners(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
                                              uint32_t* bm, uint32_t* sel_bits) {
-  for (uint64_t base = 0; base < ng; base += (uint64_t)BM_WORDS * 32) {
-    const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BM_WORDS * 32, ng - base);
-    const uint32_t words = (span + 31) / 32;
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
-      const uint32_t r = ATOMIC_READ ? __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tab[i];
-      if (r == RANK_NONE) continue;
-      const uint64_t lr = (uint64_t)r - gbase - base;
-      if (lr < span) atomicOr(&bm[lr >> 5], 1u << (lr & 31));
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
-      const uint32_t wv = bm[i];
-      if (!wv) continue;
-      const uint64_t gb = gbase + base + 32ull * i;
-      const uint32_t sh = (uint32_t)(gb & 31);
-      atomicOr(&sel_bits[gb >> 5], wv << sh);
-      if (sh) {
-        const uint32_t hi = wv >> (32 - sh);
-        if (hi) atomicOr(&sel_bits[(gb >> 5) + 1], hi);
-      }
-    }
-    __syncthreads();
+  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BM_WORDS * 32, ng);
+  const uint32_t words = (span + 31) / 32;
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
+    const uint32_t r = ATOMIC_READ ? __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tab[i];
+    if (r == RANK_NONE) continue;
+    const uint64_t lr = (uint64_t)r - gbase;
+    if (lr < span)
+      atomicOr(&bm[lr >> 5], 1u << (lr & 31));
+    else
+      atomicOr(&sel_bits[r >> 5], 1u << (r & 31));
   }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
+    const uint32_t wv = bm[i];
+    if (!wv) continue;
+    const uint64_t gb = gbase + 32ull * i;
+    const uint32_t sh = (uint32_t)(gb & 31);
+    atomicOr(&sel_bits[gb >> 5], wv << sh);
+    if (sh) {
+      const uint32_t hi = wv >> (32 - sh);
+      if (hi) atomicOr(&sel_bits[(gb >> 5) + 1], hi);
+    }
+  }
+  __syncthreads();
 }
 
 __device__ __forceinline__ void tab_min(uint32_t* tab, uint32_t id, uint32_t R) {
