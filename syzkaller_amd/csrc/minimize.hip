@@ -1273,7 +1273,11 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   // 7. work items: chunks of <= CHUNK_VECS vectors of one panel; a split panel merges through a
   // global table. Largest first, so the tail of the grid is short.
   K.ngtabs = 0;
-  uint64_t chunk_vecs = CHUNK_VECS;
+  // Work-item size: about one item per CU for each class (a workgroup fills its CU's LDS, so every
+  // item pays a pipeline fill, a table init and an emit with HBM idle; measured at config 4: 64K-vector
+  // items 0.235 ms, 196K 0.180 ms, 256K 0.214 ms as the tail grows). total/300, in [16K, 256K].
+  uint64_t chunk_vecs = std::min<uint64_t>(
+      CHUNK_VECS_MAX, std::max<uint64_t>(CHUNK_VECS_MIN, (K.total_vecs / 300 + 4095) / 4096 * 4096));
   if (const char* cv = getenv("SYZGPU_CHUNK_VECS")) chunk_vecs = std::max<uint64_t>(1, strtoull(cv, nullptr, 10));
   size_t pi = 0;
   for (uint32_t g = 0; g < G; g++) {

@@ -11,7 +11,8 @@ constexpr uint32_t WIN_BITS = 15;
 constexpr uint32_t WIN = 1u << WIN_BITS;  // ids per LDS window (u32 min-rank table = 128 KB)
 
 constexpr uint32_t VEC = 8;                 // ids per 16-byte vector
-constexpr uint64_t CHUNK_VECS = 1u << 16;   // vectors per work item (1 MiB of ids)
+constexpr uint64_t CHUNK_VECS_MIN = 1u << 14;  // vectors per work item: bounds of the per-store size
+constexpr uint64_t CHUNK_VECS_MAX = 1u << 18;
 constexpr uint32_t BM_WORDS = 6144;         // LDS rank bitmap: 196608 ranks per pass
 constexpr uint32_t RANK_NONE = 0xFFFFFFFFu;
 
