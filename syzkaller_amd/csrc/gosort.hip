@@ -45,6 +45,9 @@ __device__ unsigned long long g_gs_stats[24];
 #endif
 
 constexpr uint32_t T_SEG = GS_T_SEG;  // largest segment sorted in LDS
+#ifndef GS_T_CHILD_DEFAULT
+#define GS_T_CHILD_DEFAULT T_SEG
+#endif
 constexpr int LS_BLOCK = 1024;     // LDS workgroup (16 waves: the wave sorter runs 16 segments at once)
 constexpr int LS_ITEMS = T_SEG / LS_BLOCK;  // elements per thread chunk
 constexpr int LS_ISH = 3;                   // log2(LS_ITEMS)
@@ -52,6 +55,22 @@ static_assert((1 << LS_ISH) == LS_ITEMS, "LS_ISH");
 constexpr int LS_SH = 13;  // local index bits of the packed u32 LDS element (T_SEG = 2^13)
 static_assert((1u << LS_SH) == T_SEG, "LS_SH");
 constexpr uint32_t LS_MAXS = T_SEG / 13 + 4;  // active segments (> 12 elements) per pack
+// Children of the global rounds at most this long go to the LDS sorter; longer ones take another
+// global round. Below T_SEG this trades one more (latency-bound) round for a shorter post-round LDS
+// launch. Measured at config 4 (step ms): 8192 0.850, 4096 0.892, 2048 0.931 - the LDS launch barely
+// shrinks (its per-level costs are mostly fixed), so T_SEG stays. SYZGPU_GS_T_CHILD overrides.
+__constant__ uint32_t g_t_child = T_SEG;
+static uint32_t t_child_host() {
+  static const uint32_t v = [] {
+    uint32_t x = GS_T_CHILD_DEFAULT;
+    if (const char* e = getenv("SYZGPU_GS_T_CHILD")) x = (uint32_t)atoi(e);
+    if (x < 64) x = 64;
+    if (x > T_SEG) x = T_SEG;
+    SYZ_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_t_child), &x, sizeof(x)));
+    return x;
+  }();
+  return v;
+}
 constexpr int GL_BLOCK = 256;      // global-level tile workgroup
 constexpr int GL_ITEMS = 16;
 constexpr uint32_t GL_TILE = GL_BLOCK * GL_ITEMS;
@@ -1214,7 +1233,7 @@ __device__ void gl_tail(uint64_t* el, const Seg& sg, const GLvl& L, GLevel nx, G
   for (int k = 0; k < 2; k++) {
     const uint32_t len = ch[k].hi - ch[k].lo;
     if (len <= 1) continue;
-    if (len <= T_SEG) {
+    if (len <= g_t_child) {
       if (lane == 0) lds[atomicAdd(&ctl->nlds, 1u)] = ch[k];
     } else if (dep == 0) {
       if (lane == 0) heap[atomicAdd(&ctl->nheap, 1u)] = ch[k];
@@ -1410,7 +1429,8 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   Context& c = ctx();
   Scratch& sc = c.scratch;
   if (n >= 0xFFFFFFF0ull || n != P.n) fail(SYZGPU_EINVAL, "gosort: plan does not match the elements");
-  const size_t maxseg = n / (T_SEG / 2) + (size_t)P.nbig * 2 + 16;
+  const uint32_t tch = t_child_host();
+  const size_t maxseg = n / (tch / 2) + (size_t)P.nbig * 2 + 16;
   const size_t maxlds = n / 2 + 16;
   const Seg* d_small = P.small;
   const Pack* d_packs = P.packs;
@@ -1481,7 +1501,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     }
     // grids sized to what the big groups can ever need (their elements only shrink round by round):
     // idle workgroups of a grid-stride kernel still cost dispatch time on every launch
-    const size_t segs_max = P.big_total / T_SEG + P.nbig + 1;
+    const size_t segs_max = P.big_total / tch + P.nbig + 1;
     const unsigned tgrid = (unsigned)std::min<size_t>(P.big_total / GL_TILE + segs_max, 2048);
     ProfScope ps("gosort_level", s, 0);
     const uint32_t epoch = (++c.gr_epoch & 0x7FFFu) | 0x8000u;

@@ -333,16 +333,31 @@ __global__ __launch_bounds__(256) void k_select_store(const uint32_t* sel_bits, 
     for (int32_t i = threadIdx.x; i <= C; i += blockDim.x) lh[i] = 0;
     __syncthreads();
   }
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t r = rank_of_member[member_of[e]];
-    const uint32_t s = (sel_bits[r >> 5] >> (r & 31)) & 1u;
-    if (selected) selected[e] = (uint8_t)s;
-    if (do_hist && s && (!count_hist || count_hist[group[e]])) {
-      const uint32_t L = prog_len[e];
-      if ((int32_t)L > C)
-        atomicOr(err, 2);
-      else
-        atomicAdd(&lh[L], 1ull);
+  // SS_U entries per thread at once: the dependent gathers (member -> rank -> winner bit) of all of
+  // them are in flight together instead of one chain per grid-stride step
+  constexpr int SS_U = 8;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t e0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e0 < n; e0 += stride * SS_U) {
+    uint32_t r[SS_U], b[SS_U];
+#pragma unroll
+    for (int k = 0; k < SS_U; k++) r[k] = e0 + k * stride < n ? member_of[e0 + k * stride] : 0;
+#pragma unroll
+    for (int k = 0; k < SS_U; k++) r[k] = e0 + k * stride < n ? rank_of_member[r[k]] : 0;
+#pragma unroll
+    for (int k = 0; k < SS_U; k++) b[k] = e0 + k * stride < n ? sel_bits[r[k] >> 5] : 0;
+#pragma unroll
+    for (int k = 0; k < SS_U; k++) {
+      const size_t e = e0 + k * stride;
+      const bool in = e < n;
+      const uint32_t s = (b[k] >> (r[k] & 31)) & 1u;
+      if (in && selected) selected[e] = (uint8_t)s;
+      if (in && do_hist && s && (!count_hist || count_hist[group[e]])) {
+        const uint32_t L = prog_len[e];
+        if ((int32_t)L > C)
+          atomicOr(err, 2);
+        else
+          atomicAdd(&lh[L], 1ull);
+      }
     }
   }
   if (do_hist) {
@@ -1313,6 +1328,11 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   if (herr[0] & 4) fail(SYZGPU_EINTERNAL, "coverstore: hash bucket overflow");
   K.hstart = hstart;
   gosort_plan(K.gsplan, hstart, G, s);
+  K.el0.alloc(n);
+  if (n) {
+    k_el_init<<<grid_for(n, 256, 8192), 256, 0, s>>>(K.members.p, K.off.p, n, K.el0.p);
+    SYZ_LAUNCHED();
+  }
   if (n && prog_len) {  // len(p.Calls) > C is rejected per call without a device round trip
     std::vector<uint16_t> hl(n);
     SYZ_HIP(hipMemcpy(hl.data(), prog_len, n * 2, hipMemcpyDeviceToHost));
@@ -1344,8 +1364,9 @@ void corpus_minimize_begin(Corpus& K, hipStream_t s) {
   {
     ProfScope ps("el_init", s, (uint64_t)n * 20);
     if (n) {
-      k_el_init<<<grid_for(n, 256, 8192), 256, 0, s>>>(K.members.p, K.off.p, n, el);
-      SYZ_LAUNCHED();
+      // the sort keys (len(cov) << 32 | member) are part of the stored corpus (built at ingest),
+      // copied into the sort buffer, which the sort permutes in place
+      SYZ_HIP(hipMemcpyAsync(el, K.el0.p, n * 8, hipMemcpyDeviceToDevice, s));
     }
   }
   // ranks + Minimize per class, each right after its own sort: the small call groups' on the side

@@ -48,7 +48,7 @@ struct Corpus {
   size_t n = 0;
   uint32_t G = 0;
   uint64_t total_pcs = 0, total_ids = 0, total_vecs = 0;
-  DevArr<uint64_t> off, gstart, gdict;
+  DevArr<uint64_t> off, gstart, gdict, el0;  // el0: the Go-sort keys, len(cov) << 32 | member
   DevArr<uint32_t> group, members, member_of, nwin, dict, gtabs, vmem;
   DevArr<uint32_t> gtchunks, gtdone;  // work items per shared window table, and their arrivals
   DevArr<uint16_t> prog_len, ids16;
@@ -70,7 +70,7 @@ struct Corpus {
   CoverStats* stats = nullptr;
   ~Corpus() {
     corpus_stats_free(stats);
-    off.free(); gstart.free(); gdict.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
+    off.free(); gstart.free(); gdict.free(); el0.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
     gtchunks.free(); gtdone.free(); count_hist.free(); xg.free(); xo.free();
     gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free();
   }
