@@ -278,7 +278,8 @@ static CoverStats& corpus_analyze(Corpus& K, hipStream_t s) {
     {
       ProfScope ps("cs_runs", s, T * 9);
       const size_t lds = K.G <= CS_LDS_G ? (size_t)K.G * 4 : 0;
-      k_cs_runs<<<grid_for(T, CS_BLOCK, 2048), CS_BLOCK, lds, s>>>(S.skeys, S.svals, T, S.uq.p, K.members.p,
+      // few blocks: each flushes G call counts and 3 totals with atomics (same-address atomics serialize)
+      k_cs_runs<<<grid_for(T, CS_BLOCK, 512), CS_BLOCK, lds, s>>>(S.skeys, S.svals, T, S.uq.p, K.members.p,
                                                                   K.gdict.p, K.G, S.sflag.p, S.tot.p, S.sentg.p,
                                                                   S.call_unique.p, S.input_unique.p);
       SYZ_LAUNCHED();
