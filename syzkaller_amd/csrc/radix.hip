@@ -1,7 +1,7 @@
 // Stable LSD radix sort of (u64 key, u32 value) pairs: the sorting primitive behind the batch
-// novelty check (novelty.hip). 8-bit digits; per pass one histogram kernel, one device-wide scan of
-// the digit-major tile counts, and one scatter kernel that ranks every item stably inside its tile
-// (wave ballots give the rank among same-digit lanes, per-wave LDS counters order the waves).
+// novelty check (novelty.hip) and of the cover analytics (analytics.hip). 8-bit digits; per pass one
+// histogram kernel, one device-wide scan of the digit-major tile counts, and one scatter kernel that
+// ranks every item stably inside its tile and writes each digit's run out of LDS contiguously.
 #include "pipeline.hpp"
 
 namespace syz {
@@ -38,64 +38,94 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const KT* __restrict__ key
   }
 }
 
+// Scatter of one tile, stable. The tile is split into RS_WAVES contiguous wave slices (wave w holds
+// tile positions [w*WAVE_ITEMS, (w+1)*WAVE_ITEMS), lane-interleaved per round, so loads coalesce).
+// A wave ranks its own items with ballots against per-wave LDS digit counters - no workgroup barrier
+// per round - then one pass turns the counters into slice bases (tile digit offset + earlier waves),
+// the items land digit-sorted in LDS, and each digit's run leaves as consecutive stores.
 template <class KT>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const KT* __restrict__ kin,
                                                          const uint32_t* __restrict__ vin, size_t n, int shift,
                                                          uint32_t ntiles, const uint64_t* __restrict__ offs,
                                                          KT* __restrict__ kout, uint32_t* __restrict__ vout) {
-  __shared__ uint32_t run[RS_RADIX];
+  constexpr int WAVE_ITEMS = RS_ITEMS * 64;
+  __shared__ KT sk[RS_TILE];
+  __shared__ uint32_t sv[RS_TILE];
   __shared__ uint32_t wc[RS_WAVES][RS_RADIX];
-  __shared__ uint64_t goff[RS_RADIX];
-  for (int d = threadIdx.x; d < RS_RADIX; d += RS_BLOCK) {
-    run[d] = 0;
-    goff[d] = offs[(size_t)d * ntiles + blockIdx.x];
-  }
+  __shared__ uint64_t gshift[RS_RADIX];
+  __shared__ uint32_t lds[RS_BLOCK / 64 + 1];
   for (int i = threadIdx.x; i < RS_WAVES * RS_RADIX; i += RS_BLOCK) (&wc[0][0])[i] = 0;
   const int w = threadIdx.x >> 6;
-  const size_t base = (size_t)blockIdx.x * RS_TILE + threadIdx.x;
+  const uint32_t lane = __lane_id();
+  const size_t tile0 = (size_t)blockIdx.x * RS_TILE;
+  const uint32_t tn = (uint32_t)(n - tile0 < (size_t)RS_TILE ? n - tile0 : RS_TILE);
+  const uint32_t wbase = (uint32_t)w * WAVE_ITEMS + lane;
   KT k[RS_ITEMS];
   uint32_t v[RS_ITEMS];
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; i++) {
-    const size_t p = base + (size_t)i * RS_BLOCK;
-    k[i] = p < n ? kin[p] : 0;
-    v[i] = p < n ? vin[p] : 0;
+    const uint32_t p = wbase + i * 64;
+    k[i] = p < tn ? kin[tile0 + p] : 0;
+    v[i] = p < tn ? vin[tile0 + p] : 0;
   }
   __syncthreads();
   const uint64_t lt = lanemask_lt();
+  uint32_t r[RS_ITEMS];
 #pragma unroll
   for (int i = 0; i < RS_ITEMS; i++) {
-    // round i holds tile positions [i*BLOCK, (i+1)*BLOCK) in thread order: ranks stay stable
-    const bool valid = base + (size_t)i * RS_BLOCK < n;
-    const uint32_t d = valid ? (uint32_t)(k[i] >> shift) & (RS_RADIX - 1) : 0;
+    const bool valid = wbase + i * 64 < tn;
+    const uint32_t d = (uint32_t)(k[i] >> shift) & (RS_RADIX - 1);
     uint64_t peers = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
+    for (int b = 0; b < RADIX_BITS; b++) {
       const bool bit = (d >> b) & 1;
       const uint64_t bb = __ballot(bit);
       peers &= bit ? bb : ~bb;
     }
     const uint32_t wrank = __popcll(peers & lt);
-    if (valid && wrank == 0) wc[w][d] = __popcll(peers);
-    __syncthreads();
-    if (valid) {
-      uint32_t pre = run[d];
-      for (int x = 0; x < w; x++) pre += wc[x][d];
-      const uint64_t dst = goff[d] + pre + wrank;
-      kout[dst] = k[i];
-      vout[dst] = v[i];
-    }
-    __syncthreads();
-    for (int dd = threadIdx.x; dd < RS_RADIX; dd += RS_BLOCK) {
-      uint32_t s = 0;
+    const uint32_t before = wc[w][d];  // every peer reads before the leader's add (wave program order)
+    r[i] = before + wrank;
+    if (valid && wrank == 0) wc[w][d] = before + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // per digit: tile offset (scan over digits), then each wave's base inside it
+  uint32_t tot_d = 0;
+  if (threadIdx.x < RS_RADIX) {
 #pragma unroll
-      for (int x = 0; x < RS_WAVES; x++) {
-        s += wc[x][dd];
-        wc[x][dd] = 0;
-      }
-      run[dd] += s;
+    for (int x = 0; x < RS_WAVES; x++) tot_d += wc[x][threadIdx.x];
+  }
+  uint32_t total;
+  const uint32_t loff = block_excl_scan<RS_BLOCK>(tot_d, lds, &total);
+  if (threadIdx.x < RS_RADIX) {
+    uint32_t run = loff;
+#pragma unroll
+    for (int x = 0; x < RS_WAVES; x++) {
+      const uint32_t c = wc[x][threadIdx.x];
+      wc[x][threadIdx.x] = run;
+      run += c;
     }
-    __syncthreads();
+    gshift[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + blockIdx.x] - (uint64_t)loff;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < RS_ITEMS; i++) {
+    if (wbase + i * 64 < tn) {
+      const uint32_t d = (uint32_t)(k[i] >> shift) & (RS_RADIX - 1);
+      const uint32_t p = wc[w][d] + r[i];
+      sk[p] = k[i];
+      sv[p] = v[i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < RS_ITEMS; i++) {
+    const uint32_t p = threadIdx.x + i * RS_BLOCK;
+    if (p < tn) {
+      const KT key = sk[p];
+      const uint64_t dst = gshift[(uint32_t)(key >> shift) & (RS_RADIX - 1)] + p;
+      kout[dst] = key;
+      vout[dst] = sv[p];
+    }
   }
 }
 
