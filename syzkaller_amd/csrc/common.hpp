@@ -97,6 +97,7 @@ struct Context {
   unsigned long long* gr_host = nullptr;  // host-mapped progress word of the global rounds
   unsigned long long* gr_dev = nullptr;   // its device address
   uint32_t gr_epoch = 0;
+  uint32_t gr_resident = 0;  // workgroups of k_gr_persist resident at once (occupancy x CUs)
 };
 
 // Returns the initialised context of the current device (lazily init(0)); throws ENODEV.

@@ -1007,17 +1007,8 @@ __device__ __forceinline__ bool gl_range(const Seg& sg, const GLvl& L, uint32_t*
 }
 __device__ __forceinline__ bool gl_left(uint32_t k, const GLvl& L) { return L.mode == 0 ? k >= L.pl : k > L.pl; }
 
-__global__ __launch_bounds__(GL_BLOCK) void k_gr_count(const uint64_t* el, GLevel cur, GPlan* next_plan,
-                                                       uint32_t* tcnt, GCtl* ctl, unsigned long long* host_word) {
-  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *next_plan = GPlan{0, 0};  // read by the previous round only
-    // progress word for the host: (epoch << 48 | round << 32) | segments in this round
-    const uint32_t r = ++ctl->round;
-    __hip_atomic_store(host_word, ((unsigned long long)r << 32) | cur.plan->nseg, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  const uint32_t ntiles = cur.plan->ntiles;
+__device__ __forceinline__ void gr_count(const uint64_t* el, const GLevel& cur, uint32_t ntiles, uint32_t* tcnt,
+                                         uint32_t* red) {
   for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
     const uint2 st = cur.tseg[tb];
     const Seg sg = cur.segs[st.x];
@@ -1036,6 +1027,20 @@ __global__ __launch_bounds__(GL_BLOCK) void k_gr_count(const uint64_t* el, GLeve
   }
 }
 
+
+__global__ __launch_bounds__(GL_BLOCK) void k_gr_count(const uint64_t* el, GLevel cur, GPlan* next_plan,
+                                                       uint32_t* tcnt, GCtl* ctl, unsigned long long* host_word) {
+  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *next_plan = GPlan{0, 0};  // read by the previous round only
+    // progress word for the host: (epoch << 48 | round << 32) | segments in this round
+    const uint32_t r = ++ctl->round;
+    __hip_atomic_store(host_word, ((unsigned long long)r << 32) | cur.plan->nseg, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  gr_count(el, cur, cur.plan->ntiles, tcnt, red);
+}
+
 // Tile of 4096 elements staged in LDS with coalesced loads; thread t owns the run [16t, 16t+16).
 __device__ __forceinline__ void gl_stage(const uint64_t* el, uint32_t t0, uint32_t hi, uint64_t* tile) {
   for (uint32_t i = threadIdx.x; i < GL_TILE; i += GL_BLOCK) {
@@ -1045,12 +1050,9 @@ __device__ __forceinline__ void gl_stage(const uint64_t* el, uint32_t t0, uint32
   __syncthreads();
 }
 
-__global__ __launch_bounds__(GL_BLOCK) void k_gr_lists(const uint64_t* el, GLevel cur, const uint32_t* tcnt,
-                                                       uint32_t* A, uint32_t* B, uint64_t* VA, uint64_t* VB) {
-  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
-  __shared__ uint32_t tpre[2];
-  __shared__ uint64_t tile[GL_TILE + GL_TILE / 16];
-  const uint32_t ntiles = cur.plan->ntiles;
+__device__ __forceinline__ void gr_lists(const uint64_t* el, const GLevel& cur, uint32_t ntiles, const uint32_t* tcnt,
+                                         uint32_t* A, uint32_t* B, uint64_t* VA, uint64_t* VB, uint32_t* red,
+                                         uint32_t* tpre, uint64_t* tile) {
   for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
     const uint2 st = cur.tseg[tb];
     const Seg sg = cur.segs[st.x];
@@ -1109,6 +1111,15 @@ __global__ __launch_bounds__(GL_BLOCK) void k_gr_lists(const uint64_t* el, GLeve
       if (t0 <= a && a < t0 + GL_TILE) cur.lv[st.x].bnd = bnd;
     }
   }
+}
+
+
+__global__ __launch_bounds__(GL_BLOCK) void k_gr_lists(const uint64_t* el, GLevel cur, const uint32_t* tcnt,
+                                                       uint32_t* A, uint32_t* B, uint64_t* VA, uint64_t* VB) {
+  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
+  __shared__ uint32_t tpre[2];
+  __shared__ uint64_t tile[GL_TILE + GL_TILE / 16];
+  gr_lists(el, cur, cur.plan->ntiles, tcnt, A, B, VA, VB, red, tpre, tile);
 }
 
 // ---- the O(1) tail of a segment, by one wave after all its swaps are visible ----------------------
@@ -1301,11 +1312,9 @@ __device__ void gl_tail(uint64_t* el, const Seg& sg, const GLvl& L, GLevel nx, G
 // scattered stores. WT: write-through stores (agent scope, sc1) need no L2 write-back before the
 // arrival; otherwise plain stores and one release fence per workgroup.
 template <bool WT>
-__global__ __launch_bounds__(GL_BLOCK) void k_gr_swap(uint64_t* el, GLevel cur, GLevel nx, const uint32_t* A,
-                                                      const uint32_t* B, const uint64_t* VA, const uint64_t* VB,
-                                                      GCtl* ctl, Seg* lds, Seg* heap) {
-  __shared__ uint32_t last;
-  const uint32_t ntiles = cur.plan->ntiles;
+__device__ __forceinline__ void gr_swap(uint64_t* el, const GLevel& cur, uint32_t ntiles, const GLevel& nx,
+                                        const uint32_t* A, const uint32_t* B, const uint64_t* VA, const uint64_t* VB,
+                                        GCtl* ctl, Seg* lds, Seg* heap, uint32_t* last) {
   for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
     const uint2 st = cur.tseg[tb];
     const Seg sg = cur.segs[st.x];
@@ -1330,10 +1339,10 @@ __global__ __launch_bounds__(GL_BLOCK) void k_gr_swap(uint64_t* el, GLevel cur, 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       const uint32_t old = __hip_atomic_fetch_add(&cur.done[st.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = old + 1 == gl_ntiles(sg);
+      *last = old + 1 == gl_ntiles(sg);
     }
     __syncthreads();
-    if (last && threadIdx.x < 64) {
+    if (*last && threadIdx.x < 64) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const GLvl L = cur.lv[st.x];
@@ -1341,6 +1350,70 @@ __global__ __launch_bounds__(GL_BLOCK) void k_gr_swap(uint64_t* el, GLevel cur, 
     }
     __syncthreads();
   }
+}
+
+
+template <bool WT>
+__global__ __launch_bounds__(GL_BLOCK) void k_gr_swap(uint64_t* el, GLevel cur, GLevel nx, const uint32_t* A,
+                                                      const uint32_t* B, const uint64_t* VA, const uint64_t* VB,
+                                                      GCtl* ctl, Seg* lds, Seg* heap) {
+  __shared__ uint32_t last;
+  gr_swap<WT>(el, cur, cur.plan->ntiles, nx, A, B, VA, VB, ctl, lds, heap, &last);
+}
+
+// ---- persistent form: every round in ONE launch ------------------------------------------------
+// The three phases of a round are separated by grid barriers instead of kernel boundaries. The grid
+// never exceeds what the device holds at once (host: occupancy x CUs), so every workgroup is resident
+// and the barrier cannot wait on an unscheduled one. A barrier is the swap kernel's own publication
+// pattern: each wave drains its stores, one agent-scope release per workgroup, an arrival on one
+// agent-scope counter, then an agent-scope acquire. Every workgroup leaves the loop in the same round:
+// the next round's segment count is final before the barrier that ends a round, or at maxr.
+__device__ __forceinline__ void gr_grid_barrier(uint32_t* bar, uint32_t target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <bool WT>
+__global__ __launch_bounds__(GL_BLOCK) void k_gr_persist(uint64_t* el, GLevel l0, GLevel l1, uint32_t* tcnt,
+                                                         uint32_t* A, uint32_t* B, uint64_t* VA, uint64_t* VB,
+                                                         GCtl* ctl, Seg* lds, Seg* heap, uint32_t* bar,
+                                                         uint32_t maxr) {
+  __shared__ uint32_t red[GL_BLOCK / 64 + 1];
+  __shared__ uint32_t tpre[2];
+  __shared__ uint64_t tile[GL_TILE + GL_TILE / 16];
+  __shared__ uint32_t last;
+  __shared__ uint32_t plan[2];
+  uint32_t target = 0;
+  for (uint32_t r = 0; r < maxr; r++) {
+    const GLevel cur = (r & 1) ? l1 : l0, nx = (r & 1) ? l0 : l1;
+    if (threadIdx.x == 0) {
+      plan[0] = __hip_atomic_fetch_add(&cur.plan->nseg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      plan[1] = __hip_atomic_fetch_add(&cur.plan->ntiles, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const uint32_t nseg = plan[0], ntiles = plan[1];
+    if (nseg == 0) break;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // nx is read by nobody before the swap phase's tails
+      __hip_atomic_store(&nx.plan->nseg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&nx.plan->ntiles, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    gr_count(el, cur, ntiles, tcnt, red);
+    gr_grid_barrier(bar, target += gridDim.x);
+    gr_lists(el, cur, ntiles, tcnt, A, B, VA, VB, red, tpre, tile);
+    gr_grid_barrier(bar, target += gridDim.x);
+    gr_swap<WT>(el, cur, ntiles, nx, A, B, VA, VB, ctl, lds, heap, &last);
+    gr_grid_barrier(bar, target += gridDim.x);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl->round = 0x10000u | (target / gridDim.x / 3);  // rounds run
 }
 
 __global__ void k_gs_heap(uint64_t* el, const Seg* segs, const uint32_t* nsegs) {
@@ -1516,98 +1589,132 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     SYZ_HIP(hipMemsetAsync(lvl[0].plan, 0, sizeof(GPlan), s));
     k_gl_init<<<std::min<uint32_t>(nbig, 1024), 64, 0, s>>>(el, P.big, nbig, lvl[0], ctl, epoch);
     SYZ_LAUNCHED();
-    // one round = 3 dependent kernels with fixed arguments per buffer parity; RPG rounds (parity 0,
-    // 1, 0, 1) are captured once into a HIP graph and replayed
-    constexpr uint32_t RPG = 4;
+    // Default: the rounds as captured graphs of 3 launches each. SYZGPU_GR_PERSIST=1: all rounds in one
+    // persistent launch with grid barriers (k_gr_persist). Measured slower at config 4 (global rounds
+    // 0.74 ms at 64-256 workgroups vs 0.45 ms as graphs): a barrier's per-workgroup L2 write-back and
+    // invalidate costs more than the launch gap it replaces.
+    const char* pe = getenv("SYZGPU_GR_PERSIST");
     const bool wt = !getenv("SYZGPU_GR_FENCE");  // A/B switch: write-through swaps vs release fence
-    auto enqueue_round = [&](hipStream_t q, int parity) {
-      const GLevel cur = lvl[parity], nx = lvl[parity ^ 1];
-      k_gr_count<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx.plan, tcnt, ctl, c.gr_dev);
-      SYZ_LAUNCHED();
-      k_gr_lists<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, tcnt, A, B, VA, VB);
-      SYZ_LAUNCHED();
+    if (pe && !strcmp(pe, "1")) {
+      if (!c.gr_resident) {  // workgroups the device holds at once: the persistent grid never exceeds it
+        int per_cu = 0, cus = 0;
+        SYZ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_gr_persist<true>, GL_BLOCK, 0));
+        int per_cu2 = 0;
+        SYZ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_gr_persist<false>, GL_BLOCK, 0));
+        SYZ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
+        c.gr_resident = (uint32_t)std::max(1, std::min(per_cu, per_cu2) * cus);
+      }
+      // few workgroups: every barrier costs each of them an L2 write-back and invalidate
+      const char* pg = getenv("SYZGPU_GR_PGRID");
+      const unsigned want = pg ? (unsigned)std::max(1, atoi(pg)) : 256u;
+      const unsigned pgrid = std::min<unsigned>(std::min<unsigned>(tgrid, want), c.gr_resident);
+      uint32_t* bar = sc.get<uint32_t>("gs_bar", 1);
+      SYZ_HIP(hipMemsetAsync(bar, 0, 4, s));
+      constexpr uint32_t MAXR = 512;
       if (wt)
-        k_gr_swap<true><<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx, A, B, VA, VB, ctl, dlds, heap);
+        k_gr_persist<true><<<pgrid, GL_BLOCK, 0, s>>>(el, lvl[0], lvl[1], tcnt, A, B, VA, VB, ctl, dlds, heap, bar, MAXR);
       else
-        k_gr_swap<false><<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx, A, B, VA, VB, ctl, dlds, heap);
+        k_gr_persist<false><<<pgrid, GL_BLOCK, 0, s>>>(el, lvl[0], lvl[1], tcnt, A, B, VA, VB, ctl, dlds, heap, bar, MAXR);
       SYZ_LAUNCHED();
-    };
-    const std::vector<const void*> key = {el,          tcnt,        A,           B,           ctl,         dlds,
-                                          heap,        lvl[0].segs, lvl[0].lv,   lvl[0].toff, lvl[0].done, lvl[0].tseg,
-                                          lvl[0].plan, lvl[1].segs, lvl[1].lv,   lvl[1].toff, lvl[1].done, lvl[1].tseg,
-                                          lvl[1].plan, c.gr_dev,    (const void*)(uintptr_t)tgrid,
-                                          VA,          VB,          (const void*)(uintptr_t)wt};
-    if (c.gl_key != key) {
-      for (auto& row : c.gl_exec)
-        for (auto& g : row) {
-          if (g) SYZ_HIP(hipGraphExecDestroy(g));
-          g = nullptr;
+      if (getenv("SYZGPU_GS_DEBUG")) {
+        GCtl h;
+        SYZ_HIP(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipStreamSynchronize(s));
+        fprintf(stderr, "gosort: persistent grid %u, %u rounds\n", pgrid, h.round & 0xFFFFu);
+      }
+    } else {
+      // one round = 3 dependent kernels with fixed arguments per buffer parity; RPG rounds (parity 0,
+      // 1, 0, 1) are captured once into a HIP graph and replayed
+      constexpr uint32_t RPG = 4;
+      auto enqueue_round = [&](hipStream_t q, int parity) {
+        const GLevel cur = lvl[parity], nx = lvl[parity ^ 1];
+        k_gr_count<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx.plan, tcnt, ctl, c.gr_dev);
+        SYZ_LAUNCHED();
+        k_gr_lists<<<tgrid, GL_BLOCK, 0, q>>>(el, cur, tcnt, A, B, VA, VB);
+        SYZ_LAUNCHED();
+        if (wt)
+          k_gr_swap<true><<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx, A, B, VA, VB, ctl, dlds, heap);
+        else
+          k_gr_swap<false><<<tgrid, GL_BLOCK, 0, q>>>(el, cur, nx, A, B, VA, VB, ctl, dlds, heap);
+        SYZ_LAUNCHED();
+      };
+      const std::vector<const void*> key = {el,          tcnt,        A,           B,           ctl,         dlds,
+                                            heap,        lvl[0].segs, lvl[0].lv,   lvl[0].toff, lvl[0].done, lvl[0].tseg,
+                                            lvl[0].plan, lvl[1].segs, lvl[1].lv,   lvl[1].toff, lvl[1].done, lvl[1].tseg,
+                                            lvl[1].plan, c.gr_dev,    (const void*)(uintptr_t)tgrid,
+                                            VA,          VB,          (const void*)(uintptr_t)wt};
+      if (c.gl_key != key) {
+        for (auto& row : c.gl_exec)
+          for (auto& g : row) {
+            if (g) SYZ_HIP(hipGraphExecDestroy(g));
+            g = nullptr;
+          }
+        c.gl_key = key;
+      }
+      // graph of k rounds starting at buffer parity p, captured on first use
+      auto graph = [&](int p, uint32_t k) -> hipGraphExec_t {
+        hipGraphExec_t& ex = c.gl_exec[p][k - 1];
+        if (!ex) {
+          if (!c.cap) SYZ_HIP(hipStreamCreateWithFlags(&c.cap, hipStreamNonBlocking));
+          hipGraph_t g;
+          SYZ_HIP(hipStreamBeginCapture(c.cap, hipStreamCaptureModeThreadLocal));
+          for (uint32_t r = 0; r < k; r++) enqueue_round(c.cap, (int)((p + r) & 1));
+          SYZ_HIP(hipStreamEndCapture(c.cap, &g));
+          SYZ_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+          SYZ_HIP(hipGraphDestroy(g));
         }
-      c.gl_key = key;
-    }
-    // graph of k rounds starting at buffer parity p, captured on first use
-    auto graph = [&](int p, uint32_t k) -> hipGraphExec_t {
-      hipGraphExec_t& ex = c.gl_exec[p][k - 1];
-      if (!ex) {
-        if (!c.cap) SYZ_HIP(hipStreamCreateWithFlags(&c.cap, hipStreamNonBlocking));
-        hipGraph_t g;
-        SYZ_HIP(hipStreamBeginCapture(c.cap, hipStreamCaptureModeThreadLocal));
-        for (uint32_t r = 0; r < k; r++) enqueue_round(c.cap, (int)((p + r) & 1));
-        SYZ_HIP(hipStreamEndCapture(c.cap, &g));
-        SYZ_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-        SYZ_HIP(hipGraphDestroy(g));
-      }
-      return ex;
-    };
-    // The host issues rounds without waiting for them. The first count kernel of every round writes
-    // (epoch, round, segments) into host-mapped memory; the host stops once a round of this call
-    // reports zero segments (rounds issued past it find nothing and return at once). With a hint
-    // (the rounds the previous run of this plan needed), exactly hint + 1 rounds are issued up front
-    // and the last one reports zero; otherwise rounds go out RPG at a time, at most AHEAD beyond the
-    // last one seen running.
-    constexpr uint32_t MAXR = 512, AHEAD = RPG + 2;
-    volatile unsigned long long* hw = c.gr_host;
-    uint32_t issued = 0, seen = 0;
-    auto launch = [&](uint32_t k) {
-      if (issued + k > MAXR) fail(SYZGPU_EINTERNAL, "gosort: round limit");
-      SYZ_HIP(hipGraphLaunch(graph((int)(issued & 1), k), s));
-      issued += k;
-    };
-    bool done = false;
-    uint32_t last_rounds = 0;
-    auto poll = [&]() -> bool {  // true: a round of this call reported zero segments
-      const unsigned long long w = *hw;
-      if ((uint32_t)(w >> 48) != epoch) return false;
-      const uint32_t r = (uint32_t)(w >> 32) & 0xFFFFu, ns = (uint32_t)w;
-      if (r > seen) seen = r;
-      if (ns == 0) {
-        last_rounds = r - 1;
-        return true;
-      }
-      return false;
-    };
-    const bool hinted = P.rounds_hint > 0;
-    if (hinted)
-      while (issued < P.rounds_hint + 1) launch(std::min<uint32_t>(RPG, P.rounds_hint + 1 - issued));
-    else
-      launch(RPG);
-    while (!(done = poll())) {
-      if (!hinted && issued - seen < AHEAD) {
+        return ex;
+      };
+      // The host issues rounds without waiting for them. The first count kernel of every round writes
+      // (epoch, round, segments) into host-mapped memory; the host stops once a round of this call
+      // reports zero segments (rounds issued past it find nothing and return at once). With a hint
+      // (the rounds the previous run of this plan needed), exactly hint + 1 rounds are issued up front
+      // and the last one reports zero; otherwise rounds go out RPG at a time, at most AHEAD beyond the
+      // last one seen running.
+      constexpr uint32_t MAXR = 512, AHEAD = RPG + 2;
+      volatile unsigned long long* hw = c.gr_host;
+      uint32_t issued = 0, seen = 0;
+      auto launch = [&](uint32_t k) {
+        if (issued + k > MAXR) fail(SYZGPU_EINTERNAL, "gosort: round limit");
+        SYZ_HIP(hipGraphLaunch(graph((int)(issued & 1), k), s));
+        issued += k;
+      };
+      bool done = false;
+      uint32_t last_rounds = 0;
+      auto poll = [&]() -> bool {  // true: a round of this call reported zero segments
+        const unsigned long long w = *hw;
+        if ((uint32_t)(w >> 48) != epoch) return false;
+        const uint32_t r = (uint32_t)(w >> 32) & 0xFFFFu, ns = (uint32_t)w;
+        if (r > seen) seen = r;
+        if (ns == 0) {
+          last_rounds = r - 1;
+          return true;
+        }
+        return false;
+      };
+      const bool hinted = P.rounds_hint > 0;
+      if (hinted)
+        while (issued < P.rounds_hint + 1) launch(std::min<uint32_t>(RPG, P.rounds_hint + 1 - issued));
+      else
         launch(RPG);
-        continue;
+      while (!(done = poll())) {
+        if (!hinted && issued - seen < AHEAD) {
+          launch(RPG);
+          continue;
+        }
+        if (hipStreamQuery(s) == hipSuccess) {  // everything issued has run
+          if ((done = poll())) break;
+          if (seen < issued) fail(SYZGPU_EINTERNAL, "gosort: no progress word from the rounds");
+          launch(RPG);
+          continue;
+        }
+        __builtin_ia32_pause();
       }
-      if (hipStreamQuery(s) == hipSuccess) {  // everything issued has run
-        if ((done = poll())) break;
-        if (seen < issued) fail(SYZGPU_EINTERNAL, "gosort: no progress word from the rounds");
-        launch(RPG);
-        continue;
+      P.rounds_hint = last_rounds;
+      if (getenv("SYZGPU_GS_DEBUG")) {
+        SYZ_HIP(hipStreamSynchronize(s));
+        fprintf(stderr, "gosort: %u rounds issued, %u with segments\n", issued, last_rounds);
       }
-      __builtin_ia32_pause();
-    }
-    P.rounds_hint = last_rounds;
-    if (getenv("SYZGPU_GS_DEBUG")) {
-      SYZ_HIP(hipStreamSynchronize(s));
-      fprintf(stderr, "gosort: %u rounds issued, %u with segments\n", issued, last_rounds);
     }
     // children that reached the LDS size and depth-exhausted big ones: counts stay on the device
     k_gs_heap<<<64, 64, 0, s>>>(el, heap, &ctl[0].nheap);

@@ -100,3 +100,13 @@ def test_order_rejects_lengths_beyond_u32():
     with pytest.raises(_lib.SyzGpuError) as e:
         cover.MinimizeOrder(np.array([1, 1 << 33], np.uint64))
     assert e.value.code == _lib.EINVAL
+
+
+@pytest.mark.parametrize("kind", ["few5", "lognormal", "organ"])
+def test_order_persistent_rounds(kind, monkeypatch):
+    # the opt-in single-launch form of the global rounds (grid barriers instead of launches) must give
+    # the same permutation as the graph form
+    monkeypatch.setenv("SYZGPU_GR_PERSIST", "1")
+    monkeypatch.setenv("SYZGPU_GR_PGRID", "64")
+    rnd = np.random.default_rng(13)
+    _check_groups([_pattern(kind, 250_000, rnd), _pattern("saw", 40_000, rnd), _pattern(kind, 9000, rnd)])
