@@ -1,7 +1,8 @@
 // Stable LSD radix sort of (u64 key, u32 value) pairs: the sorting primitive behind the batch
 // novelty check (novelty.hip) and of the cover analytics (analytics.hip). 8-bit digits; per pass one
 // histogram kernel, one device-wide scan of the digit-major tile counts, and one scatter kernel that
-// ranks every item stably inside its tile and writes each digit's run out of LDS contiguously.
+// ranks every item stably inside its tile and writes each digit's run out of LDS contiguously. Passes
+// over digits on which all keys agree are skipped (kernel PCs share their top byte).
 #include "pipeline.hpp"
 
 namespace syz {
@@ -129,6 +130,25 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const KT* __restrict__ 
   }
 }
 
+// OR and AND of every key (bits[0] |=, bits[1] &=): a digit whose bits agree across all keys puts
+// every item in one bucket, so its pass would be an identity copy and is skipped.
+template <class KT>
+__global__ void k_rs_bits(const KT* __restrict__ keys, size_t n, unsigned long long* bits) {
+  unsigned long long o = 0, a = ~0ull;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    o |= keys[i];
+    a &= keys[i];
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    o |= __shfl_xor(o, d, 64);
+    a &= __shfl_xor(a, d, 64);
+  }
+  if (__lane_id() == 0) {
+    atomicOr(&bits[0], o);
+    atomicAnd(&bits[1], a);
+  }
+}
+
 // Sorts n pairs by key bits [0, end_bit), stably. Ping-pongs between (keys, vals) and (ktmp, vtmp);
 // on return keys/vals point at the sorted arrays (the pointers may be swapped with the tmp ones).
 template <class KT>
@@ -141,7 +161,18 @@ static void radix_sort_pairs_t(KT*& keys, uint32_t*& vals, KT*& ktmp, uint32_t*&
   Scratch& sc = ctx().scratch;
   uint32_t* counts = sc.get<uint32_t>("rs_counts", ntiles * RS_RADIX + 1);
   uint64_t* offs = sc.get<uint64_t>("rs_offs", ntiles * RS_RADIX + 1);
+  // one readback: the bits that differ between keys (RS_ALL_PASSES=1 runs every pass, for A/B)
+  unsigned long long* d_bits = sc.get<unsigned long long>("rs_bits", 2);
+  SYZ_HIP(hipMemsetAsync(d_bits, 0, 8, s));
+  SYZ_HIP(hipMemsetAsync(d_bits + 1, 0xFF, 8, s));
+  k_rs_bits<KT><<<grid_for(n, 256, 2048), 256, 0, s>>>(keys, n, d_bits);
+  SYZ_LAUNCHED();
+  unsigned long long* h_bits = ctx().pinned.get<unsigned long long>(2);
+  SYZ_HIP(hipMemcpyAsync(h_bits, d_bits, 16, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  const unsigned long long differ = getenv("SYZGPU_RS_ALL_PASSES") ? ~0ull : (h_bits[0] ^ h_bits[1]);
   for (int shift = 0; shift < end_bit; shift += RADIX_BITS) {
+    if (!((differ >> shift) & (RS_RADIX - 1))) continue;
     k_rs_hist<KT><<<(unsigned)ntiles, RS_BLOCK, 0, s>>>(keys, n, shift, (uint32_t)ntiles, counts);
     SYZ_LAUNCHED();
     exclusive_scan_u32(counts, offs, ntiles * RS_RADIX, s);
