@@ -225,3 +225,16 @@ def test_novelty_device_entry_matches_host_entry():
         cover.NoveltyBatchDev(t(b.pcs), t(b.off), t(b.group), b.n, 31, t(mcp), t(mco), int(mco[-1]), bad,
                               flakes.size, int(b.off[-1]), is_new, out, cap, ooff)
     assert e.value.code == _lib.EINVAL
+
+
+def test_novelty_identical_keys():
+    # one group, every cover the same PC: every radix digit agrees, so the sort strategy runs no pass
+    # and the first-occurrence rule must still pick cover 0 (and the tables' entry when present)
+    pc = np.uint32(0x81234567)
+    covs = [np.array([pc], np.uint32) for _ in range(3000)]
+    pcs, off = oracle.to_csr(covs)
+    grp = np.zeros(len(covs), np.uint32)
+    for mc in ([np.zeros(0, np.uint32)], [np.array([pc], np.uint32)]):
+        mcp, mco = oracle.to_csr(mc)
+        new = _check(pcs, off, grp, 1, mcp, mco, np.zeros(0, np.uint32))
+        assert int(new.sum()) == (0 if mcp.size else 1)
