@@ -175,6 +175,15 @@ int syzgpu_corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uin
                              const uint16_t* prog_len, size_t n, uint32_t ngroups, void* stream,
                              syzgpu_corpus** out);
 int syzgpu_corpus_destroy(syzgpu_corpus* c);
+/* mgr.corpus = append(mgr.corpus, inputs...) (NewInput, syz-manager/manager.go:609-616): appends n
+ * covers (CSR, offsets from 0; group ids < the store's ngroups) and returns the grown store in *out.
+ * Like Go's append the result is a new store: on success the old handle is released and must not be
+ * used; on error it stays valid and *out is untouched. The store is rebuilt on the device from its own
+ * copy of the covers, so only the new inputs cross PCIe. */
+int syzgpu_corpus_append(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                         const uint16_t* prog_len /* may be NULL */, size_t n, syzgpu_corpus** out);
+int syzgpu_corpus_append_dev(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                             const uint16_t* prog_len, size_t n, void* stream, syzgpu_corpus** out);
 /* minimizeCorpus on the store (manager.go:507-527): same results as syzgpu_minimize_grouped(_dev). */
 int syzgpu_corpus_minimize(syzgpu_corpus* c, int64_t* out_idx, uint64_t* group_out_off);
 int syzgpu_corpus_minimize_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,

@@ -186,6 +186,25 @@ class CoverStore:
         self._h, self.n, self.ngroups = int(h[0]), n, ngroups
         return self
 
+    def append(self, pcs, off, group, prog_len=None):
+        """mgr.corpus = append(mgr.corpus, inputs...) (NewInput, manager.go:609-616): the store grows in
+        place from the caller's view; underneath the library returns a new store and releases the old."""
+        pcs, off, group = _u32(pcs), np.ascontiguousarray(off, dtype=np.uint64), _u32(group)
+        pl = None if prog_len is None else np.ascontiguousarray(prog_len, dtype=np.uint16)
+        h = np.zeros(1, dtype=np.uint64)
+        check(lib().syzgpu_corpus_append(self._h, ptr(pcs), ptr(off), ptr(group), ptr(pl), off.size - 1, ptr(h)))
+        self._h = int(h[0])
+        self.n += off.size - 1
+        return self
+
+    def append_device(self, d_pcs, d_off, d_group, d_prog_len, n, stream=0):
+        h = np.zeros(1, dtype=np.uint64)
+        check(lib().syzgpu_corpus_append_dev(self._h, ptr(d_pcs), ptr(d_off), ptr(d_group), ptr(d_prog_len), n,
+                                             stream, ptr(h)))
+        self._h = int(h[0])
+        self.n += n
+        return self
+
     @property
     def handle(self):
         return self._h

@@ -1114,6 +1114,8 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   K.gstart.alloc(G + 1);
   uint32_t* ids = sc.get<uint32_t>("cs_ids", K.total_pcs + 1);
   SYZ_HIP(hipMemcpyAsync(K.off.p, off, (n + 1) * 8, hipMemcpyDeviceToDevice, s));
+  K.pcs.alloc(K.total_pcs);
+  if (K.total_pcs) SYZ_HIP(hipMemcpyAsync(K.pcs.p, pcs, K.total_pcs * 4, hipMemcpyDeviceToDevice, s));
   if (n) SYZ_HIP(hipMemcpyAsync(K.group.p, group, n * 4, hipMemcpyDeviceToDevice, s));
   if (n && prog_len) SYZ_HIP(hipMemcpyAsync(K.prog_len.p, prog_len, n * 2, hipMemcpyDeviceToDevice, s));
   if (n && !prog_len) SYZ_HIP(hipMemsetAsync(K.prog_len.p, 0, n * 2, s));
@@ -1489,9 +1491,88 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   corpus_minimize_end(K, C, selected, len_hist, s);
 }
 
+__global__ void k_shift_off(const uint64_t* off, size_t m, uint64_t base, uint64_t* out) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i <= m; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = off[i] + base;
+}
+
+// mgr.corpus = append(mgr.corpus, inputs...) (NewInput, manager.go:609-616) on a resident store: the
+// store is rebuilt on the device from its kept covers followed by the new ones (no re-upload of the
+// corpus); like Go's append the result is a new store, and the old one is released by the caller.
+Corpus* corpus_append_dev(Corpus& K, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                          const uint16_t* prog_len, size_t m, hipStream_t s) {
+  Scratch& sc = ctx().scratch;
+  uint64_t h[2] = {0, 0};
+  SYZ_HIP(hipMemcpyAsync(&h[0], off, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(&h[1], off + m, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (h[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
+  const size_t n = K.n, nt = n + m;
+  const uint64_t L = K.total_pcs, Lt = L + h[1];
+  if (nt >= 0xFFFFFFF0ull || Lt >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "appended store too large");
+  uint32_t* cp = sc.get<uint32_t>("ap_pcs", Lt + 1);
+  uint64_t* co = sc.get<uint64_t>("ap_off", nt + 1);
+  uint32_t* cg = sc.get<uint32_t>("ap_grp", nt + 1);
+  uint16_t* cl = sc.get<uint16_t>("ap_len", nt + 1);
+  if (L) SYZ_HIP(hipMemcpyAsync(cp, K.pcs.p, L * 4, hipMemcpyDeviceToDevice, s));
+  if (h[1]) SYZ_HIP(hipMemcpyAsync(cp + L, pcs, h[1] * 4, hipMemcpyDeviceToDevice, s));
+  SYZ_HIP(hipMemcpyAsync(co, K.off.p, n * 8, hipMemcpyDeviceToDevice, s));
+  k_shift_off<<<grid_for(m + 1, 256, 4096), 256, 0, s>>>(off, m, L, co + n);
+  SYZ_LAUNCHED();
+  if (n) SYZ_HIP(hipMemcpyAsync(cg, K.group.p, n * 4, hipMemcpyDeviceToDevice, s));
+  if (m) SYZ_HIP(hipMemcpyAsync(cg + n, group, m * 4, hipMemcpyDeviceToDevice, s));
+  if (n) SYZ_HIP(hipMemcpyAsync(cl, K.prog_len.p, n * 2, hipMemcpyDeviceToDevice, s));
+  if (m && prog_len) SYZ_HIP(hipMemcpyAsync(cl + n, prog_len, m * 2, hipMemcpyDeviceToDevice, s));
+  if (m && !prog_len) SYZ_HIP(hipMemsetAsync(cl + n, 0, m * 2, s));
+  Corpus* out = corpus_create_dev(cp, co, cg, cl, nt, K.G, s);
+  SYZ_HIP(hipStreamSynchronize(s));  // the scratch copies are reused by the next call
+  return out;
+}
+
+static void corpus_release(Corpus* K) {
+  if (K == g_last_corpus) {
+    g_last_corpus = nullptr;
+    ctx().have_last = false;
+  }
+  delete K;
+}
+
 }  // namespace syz
 
 extern "C" {
+
+int syzgpu_corpus_append_dev(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                             const uint16_t* prog_len, size_t n, void* stream, syzgpu_corpus** out) {
+  SYZ_API_BODY({
+    if (!cp || !out || !off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
+    Corpus* K = reinterpret_cast<Corpus*>(cp);
+    Corpus* N = corpus_append_dev(*K, pcs, off, group, prog_len, n, (hipStream_t)stream);
+    corpus_release(K);
+    *out = reinterpret_cast<syzgpu_corpus*>(N);
+  })
+}
+
+int syzgpu_corpus_append(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                         const uint16_t* prog_len, size_t n, syzgpu_corpus** out) {
+  SYZ_API_BODY({
+    if (!cp || !out || !off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
+    if (off[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
+    hipStream_t s = C_.stream;
+    const uint64_t tot = off[n];
+    uint32_t* dp = C_.scratch.get<uint32_t>("cc_pcs", tot + 1);
+    uint64_t* doff = C_.scratch.get<uint64_t>("cc_off", n + 1);
+    uint32_t* dg = C_.scratch.get<uint32_t>("cc_grp", n + 1);
+    uint16_t* dl = prog_len ? C_.scratch.get<uint16_t>("cc_len", n + 1) : nullptr;
+    if (tot) SYZ_HIP(hipMemcpyAsync(dp, pcs, tot * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (n) SYZ_HIP(hipMemcpyAsync(dg, group, n * 4, hipMemcpyHostToDevice, s));
+    if (dl && n) SYZ_HIP(hipMemcpyAsync(dl, prog_len, n * 2, hipMemcpyHostToDevice, s));
+    Corpus* K = reinterpret_cast<Corpus*>(cp);
+    Corpus* N = corpus_append_dev(*K, dp, doff, dg, dl, n, s);
+    corpus_release(K);
+    *out = reinterpret_cast<syzgpu_corpus*>(N);
+  })
+}
 
 int syzgpu_corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                              const uint16_t* prog_len, size_t n, uint32_t ngroups, void* stream,
@@ -1524,12 +1605,7 @@ int syzgpu_corpus_create(const uint32_t* pcs, const uint64_t* off, const uint32_
 
 int syzgpu_corpus_destroy(syzgpu_corpus* cp) {
   SYZ_API_BODY({
-    Corpus* K = reinterpret_cast<Corpus*>(cp);
-    if (K == g_last_corpus) {
-      g_last_corpus = nullptr;
-      C_.have_last = false;
-    }
-    delete K;
+    corpus_release(reinterpret_cast<Corpus*>(cp));
   })
 }
 

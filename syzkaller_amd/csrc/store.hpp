@@ -52,6 +52,7 @@ struct Corpus {
   DevArr<uint32_t> group, members, member_of, nwin, dict, gtabs, vmem;
   DevArr<uint32_t> gtchunks, gtdone;  // work items per shared window table, and their arrivals
   DevArr<uint16_t> prog_len, ids16;
+  DevArr<uint32_t> pcs;  // the raw covers (CSR with off), kept so an append can rebuild the store
   DevArr<VecWork> work;  // work items of the big call groups first, then those of the small ones
   std::vector<VecWork> hwork;
   size_t nbig_work = 0;                        // work items of the big call groups
@@ -72,7 +73,7 @@ struct Corpus {
     corpus_stats_free(stats);
     off.free(); gstart.free(); gdict.free(); el0.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
     gtchunks.free(); gtdone.free(); count_hist.free(); xg.free(); xo.free();
-    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free();
+    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free(); pcs.free();
   }
 };
 
