@@ -652,10 +652,21 @@ def cpu_baseline(corp, static, n_sample):
     pr = oracle.calculate_priorities(static, corp.prog_len[kept])
     oracle.build_choice_table(pr, None)
     dt = time.perf_counter() - t
+    # SURVEY.md §8d's stronger baseline: the call groups over the host threads this job may use
+    nth = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1))
+    t = time.perf_counter()
+    kept_mt, _ = oracle.minimize_grouped_mt(pcs, off, grp, corp.ngroups, nth)
+    pr = oracle.calculate_priorities(static, corp.prog_len[kept_mt])
+    oracle.build_choice_table(pr, None)
+    dt_mt = time.perf_counter() - t
     return {"value": round(n_sample / dt, 1), "unit": "progs/s", "cores": 1, "kind": "port",
             "sample": "first %d programs of the same corpus (%d PCs); oracle/liboracle.so: Minimize + "
                       "CalculatePriorities + BuildChoiceTable, %.2f s" % (n_sample, int(off[-1]), dt),
-            "cpu": _cpu_model()}
+            "cpu": _cpu_model(),
+            "multi_thread": {"value": round(n_sample / dt_mt, 1), "unit": "progs/s", "cores": nth,
+                             "same_selection": bool(np.array_equal(kept, kept_mt)),
+                             "sample": "the same sample; call groups over %d threads, largest first "
+                                       "(oracle_minimize_grouped_mt), %.2f s" % (nth, dt_mt)}}
 
 
 def _cpu_model():

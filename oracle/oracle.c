@@ -10,6 +10,7 @@
 #include "oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -227,6 +228,102 @@ int oracle_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint
   free(members);
   free(inputs);
   free(sel);
+  return 0;
+}
+
+/* The same minimizeCorpus with the call groups spread over nthreads host threads (SURVEY.md §8d's
+ * "stronger" CPU baseline: the groups are independent, manager.go:522-527). Groups are taken largest
+ * first from a shared counter; each writes its kept inputs into its own slice, then the slices are
+ * concatenated in group order, so the output equals oracle_minimize_grouped's. */
+typedef struct {
+  const uint32_t* pcs;
+  const uint64_t* off;
+  const uint64_t* cnt;
+  const int64_t* members;
+  const uint32_t* order;
+  uint32_t ngroups;
+  int64_t* sel;      /* group g's kept members at [cnt[g], cnt[g] + kept[g]) */
+  uint64_t* kept;
+  uint32_t next;     /* next index into order (atomic) */
+} mt_job;
+
+static void* mt_worker(void* arg) {
+  mt_job* J = (mt_job*)arg;
+  size_t cap = 0;
+  min_input* inputs = NULL;
+  int64_t* loc = NULL;
+  for (;;) {
+    const uint32_t t = __atomic_fetch_add(&J->next, 1u, __ATOMIC_RELAXED);
+    if (t >= J->ngroups) break;
+    const uint32_t g = J->order[t];
+    const size_t ng = (size_t)(J->cnt[g + 1] - J->cnt[g]);
+    if (ng > cap) {
+      cap = ng;
+      inputs = (min_input*)realloc(inputs, cap * sizeof(min_input));
+      loc = (int64_t*)realloc(loc, cap * sizeof(int64_t));
+    }
+    for (size_t i = 0; i < ng; i++) {
+      const int64_t e = J->members[J->cnt[g] + i];
+      inputs[i].idx = (int64_t)i;
+      inputs[i].len = J->off[e + 1] - J->off[e];
+      inputs[i].cov = J->pcs + J->off[e];
+    }
+    size_t m = 0;
+    if (ng) minimize_core(inputs, ng, loc, &m);
+    for (size_t k = 0; k < m; k++) J->sel[J->cnt[g] + k] = J->members[J->cnt[g] + loc[k]];
+    J->kept[g] = m;
+  }
+  free(inputs);
+  free(loc);
+  return NULL;
+}
+
+static const uint64_t* g_sort_cnt;
+static int cmp_group_size(const void* a, const void* b) {
+  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  const uint64_t sx = g_sort_cnt[x + 1] - g_sort_cnt[x], sy = g_sort_cnt[y + 1] - g_sort_cnt[y];
+  return sx < sy ? 1 : sx > sy ? -1 : (x > y) - (x < y);
+}
+
+int oracle_minimize_grouped_mt(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                               uint32_t ngroups, int nthreads, int64_t* out_idx, uint64_t* group_out_off) {
+  uint64_t* cnt = (uint64_t*)calloc((size_t)ngroups + 1, sizeof(uint64_t));
+  for (size_t i = 0; i < n; i++) {
+    if (group[i] >= ngroups) {
+      free(cnt);
+      return 1;
+    }
+    cnt[group[i] + 1]++;
+  }
+  for (uint32_t g = 0; g < ngroups; g++) cnt[g + 1] += cnt[g];
+  uint64_t* fill = (uint64_t*)malloc(((size_t)ngroups + 1) * sizeof(uint64_t));
+  memcpy(fill, cnt, ((size_t)ngroups + 1) * sizeof(uint64_t));
+  int64_t* members = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+  for (size_t i = 0; i < n; i++) members[fill[group[i]]++] = (int64_t)i;
+  uint32_t* order = (uint32_t*)malloc(((size_t)ngroups + 1) * sizeof(uint32_t));
+  for (uint32_t g = 0; g < ngroups; g++) order[g] = g;
+  g_sort_cnt = cnt;
+  qsort(order, ngroups, sizeof(uint32_t), cmp_group_size);
+  mt_job J = {pcs, off, cnt, members, order, ngroups, (int64_t*)malloc((n ? n : 1) * sizeof(int64_t)),
+              (uint64_t*)calloc((size_t)ngroups + 1, sizeof(uint64_t)), 0};
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc((size_t)nthreads * sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, mt_worker, &J);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  size_t outp = 0;
+  group_out_off[0] = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    memcpy(out_idx + outp, J.sel + cnt[g], J.kept[g] * sizeof(int64_t));
+    outp += J.kept[g];
+    group_out_off[g + 1] = outp;
+  }
+  free(th);
+  free(J.sel);
+  free(J.kept);
+  free(order);
+  free(cnt);
+  free(fill);
+  free(members);
   return 0;
 }
 

@@ -36,6 +36,9 @@ int oracle_minimize(const uint32_t* pcs, const uint64_t* off, size_t ncov, int64
  * out_idx receives corpus entry ids, group-major; group_out_off (ngroups+1) the group offsets. */
 int oracle_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                             size_t n, uint32_t ngroups, int64_t* out_idx, uint64_t* group_out_off);
+/* the same result with the call groups spread over nthreads host threads (the multi-core baseline) */
+int oracle_minimize_grouped_mt(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                               uint32_t ngroups, int nthreads, int64_t* out_idx, uint64_t* group_out_off);
 
 /* The Go-sort permutation Minimize uses: perm[p] = index (within the group) of the input at sorted
  * position p, for a list of cover lengths (cover/cover.go:106-113, 140-143). */

@@ -111,6 +111,18 @@ def minimize_grouped(pcs, off, group, ngroups):
     return out[: int(goff[-1])].copy(), goff
 
 
+def minimize_grouped_mt(pcs, off, group, ngroups, nthreads):
+    n = off.size - 1
+    group = np.ascontiguousarray(group, dtype=np.uint32)
+    out = np.empty(max(n, 1), dtype=np.int64)
+    goff = np.zeros(ngroups + 1, dtype=np.uint64)
+    f = lib().oracle_minimize_grouped_mt
+    f.argtypes = [_u32p, _u64p, _u32p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int, _i64p, _u64p]
+    _check(f(_p(pcs, _u32p), _p(off, _u64p), _p(group, _u32p), n, ngroups, int(nthreads), _p(out, _i64p),
+             _p(goff, _u64p)), "minimize_grouped_mt")
+    return out[: int(goff[-1])].copy(), goff
+
+
 def minimize_order(lens):
     lens = np.ascontiguousarray(lens, dtype=np.uint64)
     perm = np.empty(max(lens.size, 1), dtype=np.int64)

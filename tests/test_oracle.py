@@ -148,3 +148,13 @@ def test_novelty_matches_python_transliteration():
         assert list(is_new) == w_new
         for g in range(G):
             assert list(out_mc[int(out_off[g]):int(out_off[g + 1])]) == w_mc[g]
+
+
+def test_minimize_grouped_multithread_equals_serial():
+    # the multi-core CPU baseline (bench.py cpu_baseline.multi_thread) computes the same selection
+    from syzkaller_amd import synth
+    c = synth.corpus(0x5EED0001, 10_000, 289, 50_000)
+    want, wgoff = oracle.minimize_grouped(c.pcs, c.off, c.group, c.ngroups)
+    for nth in (1, 3, 8):
+        got, goff = oracle.minimize_grouped_mt(c.pcs, c.off, c.group, c.ngroups, nth)
+        assert np.array_equal(want, got) and np.array_equal(wgoff, goff)
