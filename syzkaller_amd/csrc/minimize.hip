@@ -83,7 +83,9 @@ __global__ __launch_bounds__(256) void k_grp_scatter(const uint32_t* group, cons
   for (size_t base = beg; base < end; base += 64) {
     const size_t i = base + __lane_id();
     const bool valid = i < end;
-    const uint32_t g = valid ? std::min(group[i], G - 1) : 0;
+    // an invalid id goes to group 0, exactly as k_grp_count counted it, so every slot stays inside
+    // [0, n) until the host reports the error
+    const uint32_t g = valid && group[i] < G ? group[i] : 0;
     uint64_t todo = __ballot(valid);
     while (todo) {
       const int leader = __ffsll((unsigned long long)todo) - 1;

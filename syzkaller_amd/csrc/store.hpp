@@ -7,13 +7,19 @@
 
 namespace syz {
 
-constexpr uint32_t WIN_BITS = 15;
+#ifndef SYZ_WIN_BITS
+#define SYZ_WIN_BITS 15
+#endif
+#ifndef SYZ_BM_WORDS
+#define SYZ_BM_WORDS 6144
+#endif
+constexpr uint32_t WIN_BITS = SYZ_WIN_BITS;  // compile-time A/B knob (tools/gpu_libvariants.sh)
 constexpr uint32_t WIN = 1u << WIN_BITS;  // ids per LDS window (u32 min-rank table = 128 KB)
 
 constexpr uint32_t VEC = 8;                 // ids per 16-byte vector
 constexpr uint64_t CHUNK_VECS_MIN = 1u << 14;  // vectors per work item: bounds of the per-store size
 constexpr uint64_t CHUNK_VECS_MAX = 1u << 18;
-constexpr uint32_t BM_WORDS = 6144;         // LDS rank bitmap: 196608 ranks per pass
+constexpr uint32_t BM_WORDS = SYZ_BM_WORDS;  // LDS rank bitmap: 196608 ranks per pass at 6144
 constexpr uint32_t RANK_NONE = 0xFFFFFFFFu;
 
 struct VecWork {
