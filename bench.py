@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--hub", type=int, default=1, help="also time config 5's hub ingest (scan + SHA-1 + dedup) at N=1")
     ap.add_argument("--analytics", type=int, default=1, help="also time the manager's cover analytics at N=1")
     ap.add_argument("--analytics-cpu-sample", type=int, default=10_000)
+    ap.add_argument("--append", type=int, default=10_000,
+                    help="also time a NewInput append of this many programs to the store at N=1 (0: off)")
     ap.add_argument("--novelty-cpu-sample", type=int, default=20_000)
     ap.add_argument("--split-largest", type=int, default=0,
                     help="rehearsal: force the largest call group into this many PC-key parts")
@@ -301,6 +303,9 @@ def main():
         ana = None
         if args.analytics and world == 1 and not args.emulate:
             ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr)
+        app = None
+        if args.append and world == 1 and not args.emulate:  # last: the append replaces the store
+            app = append_leg(args, dev, store, sptr, C, d_hist)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "progs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
@@ -333,10 +338,45 @@ def main():
             "novelty_config3": nov,
             "cover_analytics": ana,
             "hub_ingest_config5": hubr,
+            "store_append": app,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def append_leg(args, dev, store, sptr, C, d_hist):
+    """NewInput (manager.go:609-616) on the resident store: mgr.corpus = append(mgr.corpus, inputs) for
+    a batch of fresh programs (device-resident), then one minimizeCorpus over the grown store. The
+    append rebuilds the store on the device from its kept covers (syzgpu_corpus_append_dev)."""
+    import torch
+    from syzkaller_amd import _lib, synth
+    b = synth.corpus(args.seed + 0x40, args.append, args.ngroups, args.npcs)
+
+    def t(a):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64, np.dtype(np.uint16): np.int16}
+        return torch.from_numpy(np.ascontiguousarray(a).view(view.get(a.dtype, a.dtype))).to(dev)
+    d = [t(b.pcs), t(b.off), t(b.group), t(b.prog_len)]
+    n0 = store.n
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    store.append_device(d[0], d[1], d[2], d[3], b.n, sptr)
+    torch.cuda.synchronize()
+    app_s = time.perf_counter() - t0
+    sel = torch.zeros(store.n, dtype=torch.uint8, device=dev)
+    t0 = time.perf_counter()
+    _lib.check(_lib.lib().syzgpu_corpus_minimize_dev(store.handle, C, sel.data_ptr(), d_hist.data_ptr(), sptr))
+    torch.cuda.synchronize()
+    first_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    _lib.check(_lib.lib().syzgpu_corpus_minimize_dev(store.handle, C, sel.data_ptr(), d_hist.data_ptr(), sptr))
+    torch.cuda.synchronize()
+    again_ms = (time.perf_counter() - t0) * 1e3
+    return {"what": "syzgpu_corpus_append_dev of %d fresh programs onto the %d-program store, then "
+                    "minimizeCorpus over the grown store" % (b.n, n0),
+            "append_s": round(app_s, 4), "entries_after": int(store.n),
+            "kept_after": int(sel.sum().item()),
+            "minimize_ms_first": round(first_ms, 3), "minimize_ms": round(again_ms, 3)}
 
 
 def text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step):
