@@ -38,8 +38,7 @@ __global__ __launch_bounds__(256) void k_len_hist(const uint16_t* prog_len, cons
 }
 
 // H(k) = sum_{L > k} hist[L], clamped to 2^24 (the float32 accumulator's fixed point), as float.
-__global__ __launch_bounds__(PR_BLOCK) void k_suffix(const int64_t* hist, int32_t C, float* Hf) {
-  __shared__ int64_t red[PR_BLOCK / 64 + 1];
+__device__ __forceinline__ void block_suffix(const int64_t* hist, int32_t C, float* Hf, int64_t* red) {
   // process from the top: H(k) = total - sum_{L <= k} hist[L]
   int64_t carry = 0;
   int64_t total = 0;
@@ -62,6 +61,11 @@ __global__ __launch_bounds__(PR_BLOCK) void k_suffix(const int64_t* hist, int32_
   }
 }
 
+__global__ __launch_bounds__(PR_BLOCK) void k_suffix(const int64_t* hist, int32_t C, float* Hf) {
+  __shared__ int64_t red[PR_BLOCK / 64 + 1];
+  block_suffix(hist, C, Hf, red);
+}
+
 __device__ __forceinline__ int64_t go_f32_to_int(float x) {
   if (x != x) return INT64_MIN;
   if (x >= 9223372036854775808.0f || x < -9223372036854775808.0f) return INT64_MIN;
@@ -69,9 +73,19 @@ __device__ __forceinline__ int64_t go_f32_to_int(float x) {
 }
 
 // mode 0: dynamic from Hf (+ optional static multiply); mode 1: prios given (ChoiceTable only).
+// mode 0 with hist: every row block builds H in LDS itself (no separate suffix launch on the step's
+// critical path; the same integer sums, so the same floats)
 __global__ __launch_bounds__(PR_BLOCK) void k_prio_row(int mode, const float* Hf, const float* static_prios,
                                                        const float* prios_in, int32_t C, const uint8_t* enabled,
-                                                       float* prios_out, int64_t* run, uint8_t* present) {
+                                                       float* prios_out, int64_t* run, uint8_t* present,
+                                                       const int64_t* hist) {
+  extern __shared__ float Hs[];
+  __shared__ int64_t sred[PR_BLOCK / 64 + 1];
+  if (mode == 0 && hist) {
+    block_suffix(hist, C, Hs, sred);
+    __syncthreads();
+    Hf = Hs;
+  }
   __shared__ float rmax[PR_BLOCK / 64 + 1];
   __shared__ float rmin[PR_BLOCK / 64 + 1];
   __shared__ int32_t rnz[PR_BLOCK / 64 + 1];
@@ -172,18 +186,22 @@ void prio_choice_dev(const float* static_prios, const int64_t* len_hist, const f
   if (C <= 0 || C > MAX_C) fail(SYZGPU_EINVAL, "C out of range");
   if (prios_in) {
     ProfScope ps("choice_table", s, (uint64_t)C * C * 12);
-    k_prio_row<<<C, PR_BLOCK, 0, s>>>(1, nullptr, nullptr, prios_in, C, enabled, nullptr, run, present);
+    k_prio_row<<<C, PR_BLOCK, 0, s>>>(1, nullptr, nullptr, prios_in, C, enabled, nullptr, run, present, nullptr);
     SYZ_LAUNCHED();
     return;
   }
-  float* Hf = ctx().scratch.get<float>("pr_H", C + 1);
-  {
+  // SYZGPU_PRIO_SUFFIX=1: the suffix sums as their own launch (A/B reference)
+  static const bool sep = getenv("SYZGPU_PRIO_SUFFIX") != nullptr;
+  float* Hf = nullptr;
+  if (sep) {
+    Hf = ctx().scratch.get<float>("pr_H", C + 1);
     ProfScope ps("prio_suffix", s, (uint64_t)(C + 1) * 12);
     k_suffix<<<1, PR_BLOCK, 0, s>>>(len_hist, C, Hf);
     SYZ_LAUNCHED();
   }
   ProfScope ps("prio_choice", s, (uint64_t)C * C * ((static_prios ? 4 : 0) + (prios_out ? 4 : 0) + (run ? 8 : 0)));
-  k_prio_row<<<C, PR_BLOCK, 0, s>>>(0, Hf, static_prios, nullptr, C, enabled, prios_out, run, present);
+  k_prio_row<<<C, PR_BLOCK, sep ? 0 : (size_t)C * 4, s>>>(0, Hf, static_prios, nullptr, C, enabled, prios_out, run,
+                                                          present, sep ? nullptr : len_hist);
   SYZ_LAUNCHED();
 }
 
