@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "corpus progs/sec: cover.Minimize + calcDynamicPrio, 1M progs, 1/2/4/8 GPUs"
-ROOF_KERNEL = "vec_min"  # the HBM-bound Minimize stream
+ROOF_KERNEL = "part"  # the window transpose of the raw covers
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured copy)
 
 
@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="programs in the CPU baseline sample")
     ap.add_argument("--profile", type=int, default=1, help="per-kernel HIP event timing in the timed region")
-    ap.add_argument("--raw-steps", type=int, default=2, help="also time Minimize from the raw CSR (no store)")
+    ap.add_argument("--store", type=int, default=1, help="also time the resident-store side leg at N=1")
     ap.add_argument("--text", type=int, default=1, help="also time the text pass over the kept programs at N=1")
     ap.add_argument("--novelty", type=int, default=1, help="also time config 3 (triage batch) at N=1")
     ap.add_argument("--novelty-covers", type=int, default=1_000_000)
@@ -63,28 +63,29 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_model(name, corp, store_info, C):
-    """(bound, algorithmic bytes per launch) of a kernel, SURVEY.md §8(d) / DESIGN.md §3."""
-    n, sum_pcs = corp.n, int(corp.off[-1])
-    if name == "vec_min":  # Minimize over the big call groups (this rank's PC-key parts of them): 4 B per
-        # PC + offsets + group id
-        share = store_info["big_vecs"] / max(1, store_info["big_vecs_all"])
-        return "hbm", int(4 * store_info["big_pcs"] * share) + 10 * store_info["big_entries"]
-    if name == "vec_min_small":  # the small call groups' Minimize (side stream, overlapped)
-        return "hbm", 4 * (sum_pcs - store_info["big_pcs"]) + 10 * (n - store_info["big_entries"])
+def kernel_model(name, corp, info, C):
+    """(bound, algorithmic bytes per launch) of a kernel of the step, DESIGN.md §3.
+    part: the window transpose reads every PC once and writes it once as a 4-byte element, plus the
+          per-member offsets it reads (members, mpos, off, slice: 24 B per entry);
+    pmin / pmin_small: the first-occurrence tables read every element once (4 B per PC), the groups
+          sorted by the global rounds / the small ones (their PCs are not split out: the byte model
+          uses the step's PCs in proportion to the launch time of the two).
+    prio_choice: static in + prios out + run out (16 B per matrix cell)."""
+    n, pcs = corp.n, info["pcs"]
+    if name == "part":
+        return "hbm", 8 * pcs + 24 * n
     if name == "select_out":
         return "hbm", 10 * n
     if name == "prio_choice":
         return "hbm", 16 * C * C
-    return "latency", None  # gosort_* (L2-resident dependent partitions), ranks, small helpers
+    return "latency", None  # gosort_* (dependent partitions), pmin (split by class below), helpers
 
 
-def roofline(kern, corp, store_info, C):
-    """Roofline of the dominant HBM-bound kernel (time from HIP events on the launch stream); the
-    latency-bound kernels are listed with their time so the step breakdown stays complete."""
+def roofline(kern, corp, info, C):
+    """Roofline of the dominant HBM-bound kernel (time from HIP events on the launch stream)."""
     rows = []
     for name, d in kern.items():
-        bound, alg = kernel_model(name, corp, store_info, C)
+        bound, alg = kernel_model(name, corp, info, C)
         rows.append((d["ms"], name, bound, alg, d))
     rows.sort(reverse=True)
     hbm = [r for r in rows if r[2] == "hbm"]
@@ -95,8 +96,7 @@ def roofline(kern, corp, store_info, C):
     ach = alg / (avg_ms * 1e-3) / 1e9
     out = {"bound": bound, "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_ms": round(avg_ms, 4),
-           "algorithmic_bytes_per_launch": int(alg), "design_bytes_per_launch": int(d["bytes"] / d["launches"]),
-           "dominant_kernel_overall": rows[0][1]}
+           "algorithmic_bytes_per_launch": int(alg), "dominant_kernel_overall": rows[0][1]}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
@@ -151,7 +151,7 @@ def main():
     C, G = args.calls, args.ngroups
     p = synth.params(args.seed, args.progs_per_gpu * emu_world, G, args.npcs)
     group, off, plen = synth.layout(p)
-    # key-space sharding plan: call groups whole or split by dense-PC windows over ranks
+    # key-space sharding plan: call groups whole or split by PC-value ranges over ranks
     ent_g, pcs_g = sharding.layout_stats(group, off, G)
     plan = sharding.plan_parts(ent_g, pcs_g, emu_world)
     if args.split_largest > 1:
@@ -171,44 +171,36 @@ def main():
     d_static = torch.from_numpy(st).to(dev)
     d_sel = torch.zeros(corp.n, dtype=torch.uint8, device=dev)
     d_hist = torch.zeros(C + 1, dtype=torch.int64, device=dev)
+    d_out = torch.zeros(max(corp.n, 1), dtype=torch.int64, device=dev)
+    d_goff = torch.zeros(G + 1, dtype=torch.int64, device=dev)
     d_prios = torch.empty((C, C), dtype=torch.float32, device=dev)
     d_run = torch.empty((C, C), dtype=torch.int64, device=dev)
     d_pres = torch.empty(C, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
-    # ingest: the resident corpus store (per-call dense PC ids), built once like mgr.corpus is loaded
-    torch.cuda.synchronize()
-    t_ing = time.perf_counter()
-    store = cover.CoverStore.from_device(d_pcs, d_off, d_grp, d_len, corp.n, G, sptr)
-    torch.cuda.synchronize()
-    ingest_s = time.perf_counter() - t_ing
-    part, nparts, count_hist = plan.store_parts(emu_rank)
+    # key parts of split groups (PC ranges, identical on every rank) and the selection exchange
+    key_lo, key_hi = plan.key_ranges(emu_rank, sharding.split_bounds(plan, corp, emu_rank))
+    _, _, count_hist = plan.store_parts(emu_rank)
     split_g, split_off, split_bytes = plan.split_groups()
     held = plan.held(emu_rank)
     xg, xo = split_g[held[split_g]], split_off[held[split_g]]
-    if split_g.size:
-        store.set_parts(part, nparts, count_hist)
     d_x = torch.zeros(max(split_bytes, 1), dtype=torch.uint8, device=dev)
-    store_info = store.info()
-
-    def step_raw():
-        _lib.check(L.syzgpu_minimize_grouped_dev(d_pcs.data_ptr(), d_off.data_ptr(), d_grp.data_ptr(),
-                                                 d_len.data_ptr(), corp.n, G, C, d_sel.data_ptr(),
-                                                 d_hist.data_ptr(), sptr))
+    job = cover.MinimizeJob()
+    parts = split_g.size > 0
 
     def step():
-        if split_g.size:  # split groups: OR the partial selections across their ranks
-            store.minimize_begin(sptr)
+        # minimizeCorpus from the raw covers in HBM: group partition, Go-sort ranks, window transpose,
+        # first-occurrence tables, kept flags + length histogram + the group-major kept list
+        job.begin(d_pcs, d_off, d_grp, corp.n, G, d_len, key_lo if parts else None, key_hi if parts else None, sptr)
+        if parts:  # split groups: OR the partial selections across their ranks
             d_x.zero_()
             if xg.size:
-                store.export_sel(xg, xo, d_x, sptr)
+                job.export_sel(xg, xo, d_x, sptr)
             sharding.allreduce_max_u8(d_x, dist)
             if xg.size:
-                store.import_sel(xg, xo, d_x, sptr)
-            store.minimize_end(C, d_sel, d_hist, sptr)
-        else:
-            _lib.check(L.syzgpu_corpus_minimize_dev(store.handle, C, d_sel.data_ptr(), d_hist.data_ptr(), sptr))
+                job.import_sel(xg, xo, d_x, sptr)
+        job.end(C, count_hist if parts else None, d_sel, d_hist, d_out, d_goff, sptr)
         sharding.allreduce_hist(d_hist, dist)  # kept-length histogram: (C+1) int64
         _lib.check(L.syzgpu_prio_choice_dev(d_static.data_ptr(), d_hist.data_ptr(), C, None, d_prios.data_ptr(),
                                             d_run.data_ptr(), d_pres.data_ptr(), sptr))
@@ -248,6 +240,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     roof_ev = read_prof() if args.profile else {}
     L.syzgpu_profile_enable(0)
+    job_info = job.info()
     # per-kernel breakdown: a separate, untimed pass with events around every kernel
     kern = {}
     if args.profile:
@@ -258,16 +251,6 @@ def main():
         torch.cuda.synchronize()
         kern = read_prof()
         L.syzgpu_profile_enable(0)
-    # the same Minimize from the raw CSR every time (no store): reported beside the headline
-    raw_ms = None
-    if args.raw_steps > 0:
-        step_raw()
-        torch.cuda.synchronize()
-        t0r = time.perf_counter()
-        for _ in range(args.raw_steps):
-            step_raw()
-        torch.cuda.synchronize()
-        raw_ms = (time.perf_counter() - t0r) / args.raw_steps * 1e3
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         sharding.allreduce(t, dist, dist.ReduceOp.MAX)
@@ -280,41 +263,37 @@ def main():
 
     out = None
     if rank == 0:
-        # roofline of the dominant kernel: algorithmic bytes per SURVEY.md §8(d) for the units one
-        # launch processes (Minimize: 4 B per PC + 10 B per program), over its measured average time
+        # roofline of the dominant kernel: algorithmic bytes over its measured time
         roof = None
         if roof_ev:
-            roof = roofline(roof_ev, corp, store_info, C)
+            roof = roofline(roof_ev, corp, job_info, C)
             if roof and kern:
                 roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
-        path_bytes = 4 * int(off[-1]) + 10 * total_progs + 16 * C * C  # the whole job's corpus
+        path_bytes = 4 * int(off[-1]) + 10 * total_progs + 16 * C * C  # SURVEY.md §8(d), whole job
         cpu = None
         if args.cpu_baseline and world == 1:
             cpu = cpu_baseline(corp, st, min(args.cpu_sample, corp.n))
-        tail = None
-        if args.text and world == 1 and not args.emulate:
-            tail = text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step)
-        nov = None
-        if args.novelty and world == 1 and not args.emulate:
-            nov = novelty_leg(args, dev, L, read_prof)
-        hubr = None
-        if args.hub and world == 1 and not args.emulate:
-            hubr = hub_leg(args, dev, L, read_prof, corp, sptr)
-        ana = None
-        if args.analytics and world == 1 and not args.emulate:
-            ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr)
-        app = None
-        if args.append and world == 1 and not args.emulate:  # last: the append replaces the store
-            app = append_leg(args, dev, store, sptr, C, d_hist)
+        solo = world == 1 and not args.emulate
+        store_leg_res, store = (None, None)
+        if solo and (args.store or args.analytics or args.append):
+            store_leg_res, store = store_leg(args, L, corp, d_pcs, d_off, d_grp, d_len, d_sel, d_hist, C, G, sptr)
+        tail = text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step) if args.text and solo else None
+        nov = novelty_leg(args, dev, L, read_prof) if args.novelty and solo else None
+        hubr = hub_leg(args, dev, L, read_prof, corp, sptr) if args.hub and solo else None
+        ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr) if args.analytics and solo else None
+        app = append_leg(args, dev, store, sptr, C, d_hist) if args.append and solo else None  # last: replaces
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "progs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: seeded generator (SURVEY.md §8d shapes), device-resident before timing",
+            "data": "synthetic: seeded generator (SURVEY.md §8d shapes); raw covers resident in HBM, every step "
+                    "from the covers (no store or dictionary built ahead)",
             "config": {"workload": "config4-1M: 1M programs/GPU, 2M-PC space, 289 calls, C=1159",
                        "progs_per_gpu": args.progs_per_gpu, "total_progs": total_progs,
                        "sum_pcs": sum_pcs_all, "ngroups": G, "npcs": args.npcs, "calls": C,
-                       "parallelism": "call groups sharded x%d, %d split by PC-key windows (RCCL MAX all-reduce "
+                       "step": "minimizeCorpus from raw covers (partition + Go-sort ranks + window transpose + "
+                               "first-occurrence tables + kept flags/list) + CalculatePriorities + BuildChoiceTable",
+                       "parallelism": "call groups sharded x%d, %d split by PC-key ranges (RCCL MAX all-reduce "
                                       "of %d selection bytes) + RCCL all-reduce of the length histogram"
                                       % (world, int(split_g.size), split_bytes),
                        "modelled_rank_us": [round(float(x), 1) for x in plan.cost],
@@ -325,15 +304,11 @@ def main():
                               "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                               "frac": round(path_bytes / (ms_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)},
             "kernels_ms_per_step_untimed_pass": {k: round(v["ms"] / args.steps, 4) for k, v in
-                                    sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},
+                                                 sorted(kern.items(), key=lambda kv: -kv[1]["ms"])},
+            "job": job_info,
             "cpu_baseline": cpu,
-            "ingest": {"seconds": round(ingest_s, 4), "progs_per_s": round(corp.n / ingest_s, 1),
-                       "note": "one-time build of the resident store from device CSR (not in value)",
-                       **store_info},
-            "raw_path": None if raw_ms is None else
-            {"ms_per_step": round(raw_ms, 3), "progs_per_s": round(corp.n / (raw_ms * 1e-3), 1),
-             "note": "Minimize from raw CSR each step (bucket scatter + LDS hash), no store"},
             "gen_s": round(gen_s, 2),
+            "store_reuse": store_leg_res,
             "minimize_corpus_tail": tail,
             "novelty_config3": nov,
             "cover_analytics": ana,
@@ -343,6 +318,31 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def store_leg(args, L, corp, d_pcs, d_off, d_grp, d_len, d_sel, d_hist, C, G, sptr):
+    """Side leg (never the headline): the resident store (syzgpu_corpus_create_dev: per-call dense PC
+    ids built once, like mgr.corpus is loaded) and minimizeCorpus re-run on it with the same covers.
+    The store is what the manager's cover analytics and NewInput append work on."""
+    import torch
+    from syzkaller_amd import _lib, cover
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    store = cover.CoverStore.from_device(d_pcs, d_off, d_grp, d_len, corp.n, G, sptr)
+    torch.cuda.synchronize()
+    ingest_s = time.perf_counter() - t0
+    for _ in range(2):
+        _lib.check(L.syzgpu_corpus_minimize_dev(store.handle, C, d_sel.data_ptr(), d_hist.data_ptr(), sptr))
+    torch.cuda.synchronize()
+    steps = max(1, args.steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _lib.check(L.syzgpu_corpus_minimize_dev(store.handle, C, d_sel.data_ptr(), d_hist.data_ptr(), sptr))
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"what": "store ingest once + minimizeCorpus re-run on the unchanged store (NOT the headline: the "
+                    "store build is outside this loop)",
+            "ingest_s": round(ingest_s, 4), "minimize_ms": round(ms, 4), **store.info()}, store
 
 
 def append_leg(args, dev, store, sptr, C, d_hist):

@@ -11,8 +11,13 @@
  * returning (cgo pointer rules). The *_dev functions take device pointers (e.g. torch tensors) and a
  * hipStream_t passed as void*; they enqueue work and may return before it completes.
  *
- * Thread safety: every function may be called from several threads (Go goroutines); calls are
- * serialised internally per device context.
+ * Thread safety: every function may be called from several threads (Go goroutines) at once. A call
+ * holds a lane (streams, scratch memory, captured graphs) for its duration; concurrent calls get
+ * different lanes (up to SYZGPU_LANES, default 8; more callers wait) and run concurrently on the
+ * device. Handles (stores, jobs, signature sets) serialise the calls made on the same handle.
+ * syzgpu_minimize_grouped_fetch reads the calling thread's last syzgpu_minimize_grouped_dev; a
+ * Go caller that cannot pin its goroutine to a thread (runtime.LockOSThread) uses a job handle or
+ * syzgpu_minimize_grouped_ordered_dev, which return everything per call.
  */
 #ifndef SYZGPU_H
 #define SYZGPU_H
@@ -151,6 +156,44 @@ int syzgpu_minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const 
                                 const uint16_t* prog_len, size_t n, uint32_t ngroups, int32_t C,
                                 uint8_t* selected, int64_t* len_hist, void* stream);
 
+/* The same, and the kept list itself on the device: out_idx (capacity n) receives the kept entry ids
+ * group-major in Go's selection order and group_out_off (ngroups+1) the group boundaries — exactly
+ * syzgpu_minimize_grouped's outputs (any output may be NULL). Every step runs from the raw covers:
+ * group partition, Go-sort ranks and the window transpose + first-occurrence passes (panels.hip). */
+int syzgpu_minimize_grouped_ordered_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                        const uint16_t* prog_len, size_t n, uint32_t ngroups, int32_t C,
+                                        uint8_t* selected, int64_t* len_hist, int64_t* out_idx,
+                                        uint64_t* group_out_off, void* stream);
+
+/* minimizeCorpus as a job handle: the selection lives in the job between begin and end, so a
+ * multi-GPU step can exchange the selection of call groups split over ranks, and concurrent callers
+ * with their own jobs never share state. Device pointers; the inputs must stay valid until end.
+ *   begin:  group partition, Go-sort ranks, window transpose and first-occurrence passes; returns
+ *           once the selection is in the job (SYZGPU_EINVAL for bad group ids). key_lo/key_hi (host,
+ *           per group, or both NULL): this rank keeps only PCs in [key_lo[g], key_hi[g]] of group g
+ *           (a key part; covers must then be sorted); an input is kept iff SOME of its
+ *           PCs first occurs at it, so the parts' selections OR together to the full one.
+ *   export/import: the selection of groups[0..ngroups) (host array) as one byte per group-relative
+ *           rank at device offsets offsets[j] (host array) of buf; import ORs them back.
+ *   end:    the outputs of syzgpu_minimize_grouped_ordered_dev; count_hist (host, per group, NULL =
+ *           all) says which groups are added to len_hist (one rank per split group).
+ *   fetch:  host copies of the group-major kept list.
+ * info[0..4] = entries, groups, PCs, direct windows, open-addressing windows of the last begin. */
+typedef struct syzgpu_mz syzgpu_mz;
+int syzgpu_mz_create(syzgpu_mz** out);
+int syzgpu_mz_destroy(syzgpu_mz* job);
+int syzgpu_mz_begin_dev(syzgpu_mz* job, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                        const uint16_t* prog_len, size_t n, uint32_t ngroups, const uint32_t* key_lo,
+                        const uint32_t* key_hi, void* stream);
+int syzgpu_mz_export_sel_dev(syzgpu_mz* job, const uint32_t* groups, const uint64_t* offsets, uint32_t ngroups,
+                             uint8_t* buf, void* stream);
+int syzgpu_mz_import_sel_dev(syzgpu_mz* job, const uint32_t* groups, const uint64_t* offsets, uint32_t ngroups,
+                             const uint8_t* buf, void* stream);
+int syzgpu_mz_end_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist, uint8_t* selected, int64_t* len_hist,
+                      int64_t* out_idx, uint64_t* group_out_off, void* stream);
+int syzgpu_mz_fetch(syzgpu_mz* job, int64_t* out_idx, uint64_t* group_out_off);
+int syzgpu_mz_info(syzgpu_mz* job, uint64_t* info, size_t cap);
+
 /* Dynamic prio from a length histogram, normalize, multiply by static, and the ChoiceTable:
  * prog/prio.go:29-38, 137-192, 202-228 fused. enabled may be NULL. */
 int syzgpu_prio_choice_dev(const float* static_prios, const int64_t* len_hist, int32_t C,
@@ -158,8 +201,8 @@ int syzgpu_prio_choice_dev(const float* static_prios, const int64_t* len_hist, i
                            uint8_t* row_present, void* stream);
 
 /* Compact device selection flags into group-major kept entry ids in Go's selection order (the
- * order syzgpu_minimize_grouped returns). Valid after syzgpu_minimize_grouped_dev on the same
- * corpus and before the next call into the library on this thread's context. */
+ * order syzgpu_minimize_grouped returns). Valid after syzgpu_minimize_grouped_dev (or _ordered_dev)
+ * on the same thread and corpus size, until that thread's next minimize; SYZGPU_EINVAL otherwise. */
 int syzgpu_minimize_grouped_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n,
                                   uint32_t ngroups);
 

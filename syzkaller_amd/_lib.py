@@ -43,6 +43,16 @@ SIGNATURES = {
     "syzgpu_calculate_priorities": (_c.c_int, [_vp, _vp, _sz, _c.c_int32, _vp]),
     "syzgpu_build_choice_table": (_c.c_int, [_vp, _vp, _c.c_int32, _vp, _vp]),
     "syzgpu_minimize_grouped_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _c.c_int32, _vp, _vp, _vp]),
+    "syzgpu_minimize_grouped_ordered_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _c.c_int32, _vp, _vp,
+                                                       _vp, _vp, _vp]),
+    "syzgpu_mz_create": (_c.c_int, [_vp]),
+    "syzgpu_mz_destroy": (_c.c_int, [_vp]),
+    "syzgpu_mz_begin_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp, _vp, _vp]),
+    "syzgpu_mz_export_sel_dev": (_c.c_int, [_vp, _vp, _vp, _c.c_uint32, _vp, _vp]),
+    "syzgpu_mz_import_sel_dev": (_c.c_int, [_vp, _vp, _vp, _c.c_uint32, _vp, _vp]),
+    "syzgpu_mz_end_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "syzgpu_mz_fetch": (_c.c_int, [_vp, _vp, _vp]),
+    "syzgpu_mz_info": (_c.c_int, [_vp, _vp, _sz]),
     "syzgpu_prio_choice_dev": (_c.c_int, [_vp, _vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_minimize_grouped_fetch": (_c.c_int, [_vp, _vp, _sz, _c.c_uint32]),
     "syzgpu_corpus_create": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp]),

@@ -102,6 +102,73 @@ def MinimizeCorpus(pcs, off, group, ngroups):
     return out[: int(goff[-1])].copy(), goff
 
 
+def MinimizeCorpusDev(d_pcs, d_off, d_group, n, ngroups, d_prog_len=None, C=0, d_selected=None, d_len_hist=None,
+                      d_out_idx=None, d_group_out_off=None, stream=0):
+    """minimizeCorpus on device-resident covers (torch tensors / device pointers), every output on the
+    device: kept flags, the len(p.Calls) histogram of kept programs, and the group-major kept list in
+    Go's selection order with its group offsets (syzgpu_minimize_grouped_ordered_dev)."""
+    check(lib().syzgpu_minimize_grouped_ordered_dev(ptr(d_pcs), ptr(d_off), ptr(d_group), ptr(d_prog_len), n,
+                                                    ngroups, C, ptr(d_selected), ptr(d_len_hist), ptr(d_out_idx),
+                                                    ptr(d_group_out_off), stream))
+
+
+class MinimizeJob:
+    """minimizeCorpus as a job on device-resident covers (syzgpu_mz_*): begin, an optional exchange of
+    split groups' selections, end. key_lo/key_hi (per group, numpy u32) restrict this rank to a PC
+    range of each group (a key part); both None = whole groups."""
+
+    def __init__(self):
+        h = np.zeros(1, np.uint64)
+        check(lib().syzgpu_mz_create(ptr(h)))
+        self._h = int(h[0])
+
+    @property
+    def handle(self):
+        return self._h
+
+    def begin(self, d_pcs, d_off, d_group, n, ngroups, d_prog_len=None, key_lo=None, key_hi=None, stream=0):
+        self._keys = (None if key_lo is None else np.ascontiguousarray(key_lo, np.uint32),
+                      None if key_hi is None else np.ascontiguousarray(key_hi, np.uint32))
+        check(lib().syzgpu_mz_begin_dev(self._h, ptr(d_pcs), ptr(d_off), ptr(d_group), ptr(d_prog_len), n, ngroups,
+                                        ptr(self._keys[0]), ptr(self._keys[1]), stream))
+
+    def export_sel(self, groups, offsets, buf, stream=0):
+        g, o = np.ascontiguousarray(groups, np.uint32), np.ascontiguousarray(offsets, np.uint64)
+        check(lib().syzgpu_mz_export_sel_dev(self._h, ptr(g), ptr(o), g.size, ptr(buf), stream))
+
+    def import_sel(self, groups, offsets, buf, stream=0):
+        g, o = np.ascontiguousarray(groups, np.uint32), np.ascontiguousarray(offsets, np.uint64)
+        check(lib().syzgpu_mz_import_sel_dev(self._h, ptr(g), ptr(o), g.size, ptr(buf), stream))
+
+    def end(self, C=0, count_hist=None, d_selected=None, d_len_hist=None, d_out_idx=None, d_group_out_off=None,
+            stream=0):
+        ch = None if count_hist is None else np.ascontiguousarray(count_hist, np.uint8)
+        check(lib().syzgpu_mz_end_dev(self._h, C, ptr(ch), ptr(d_selected), ptr(d_len_hist), ptr(d_out_idx),
+                                      ptr(d_group_out_off), stream))
+
+    def fetch(self, n, ngroups):
+        out = np.empty(max(n, 1), np.int64)
+        goff = np.zeros(ngroups + 1, np.uint64)
+        check(lib().syzgpu_mz_fetch(self._h, ptr(out), ptr(goff)))
+        return out[: int(goff[-1])].copy(), goff
+
+    def info(self):
+        v = np.zeros(5, np.uint64)
+        check(lib().syzgpu_mz_info(self._h, ptr(v), 5))
+        return dict(zip(["entries", "groups", "pcs", "direct_windows", "hash_windows"], (int(x) for x in v)))
+
+    def close(self):
+        if self._h:
+            lib().syzgpu_mz_destroy(self._h)
+            self._h = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def MinimizeOrder(lens, group_off=None):
     """cover.go:106-113: Go sort.Sort order of Minimize's inputs per group (index inside the group of
     the input at each sorted position), for cover lengths `lens` split by `group_off`."""

@@ -361,6 +361,7 @@ int syzgpu_corpus_cover_stats_dev(syzgpu_corpus* cp, uint64_t* call_inputs, uint
                                   uint64_t* call_unique, uint64_t* totals, uint32_t* input_unique, void* stream) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     corpus_cover_stats_dev(*reinterpret_cast<Corpus*>(cp), call_inputs, call_cover, call_unique, totals,
                            input_unique, (hipStream_t)stream);
   })
@@ -371,6 +372,7 @@ int syzgpu_corpus_cover_stats(syzgpu_corpus* cp, uint64_t* call_inputs, uint64_t
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
     Corpus& K = *reinterpret_cast<Corpus*>(cp);
+    std::lock_guard<std::recursive_mutex> hl_(K.mu);
     hipStream_t s = C_.stream;
     const uint32_t G = K.G;
     const size_t n = K.n;
@@ -392,6 +394,7 @@ int syzgpu_corpus_cover(syzgpu_corpus* cp, int64_t call, int unique, uint32_t* o
   SYZ_API_BODY({
     if (!cp || !out_n) fail(SYZGPU_EINVAL, "null pointer");
     Corpus& K = *reinterpret_cast<Corpus*>(cp);
+    std::lock_guard<std::recursive_mutex> hl_(K.mu);
     hipStream_t s = C_.stream;
     uint32_t* d = C_.scratch.get<uint32_t>("cs_list", K.total_ids + 1);
     const uint64_t len = corpus_cover(K, call, unique, d, K.total_ids + 1, s);

@@ -6,7 +6,9 @@
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -79,16 +81,23 @@ class Pinned {
   size_t bytes_ = 0;
 };
 
+// A lane: everything one API call works with (streams, scratch, pinned staging, captured graphs).
+// Calls hold a lane for their duration; concurrent callers (goroutines, fuzzer procs under coverMu's
+// read lock, fuzzer.go:448-456) get different lanes and run concurrently on the device. A thread gets
+// the lane it used last when that one is free, so per-thread state (syzgpu_minimize_grouped_fetch)
+// survives between its calls; state shared across calls on different threads lives in handles.
+struct MinJob;
 struct Context {
   int device = -1;
+  uint64_t gen = 0;
   hipStream_t stream = nullptr;  // library-owned stream for host-pointer entry points
   Scratch scratch;
   Pinned pinned;
-  std::recursive_mutex mu;
-  // last minimize_grouped_dev state (for syzgpu_minimize_grouped_fetch)
-  size_t last_n = 0;
-  uint32_t last_groups = 0;
-  bool have_last = false;
+  // the last minimize of this lane (for syzgpu_minimize_grouped_fetch): which thread ran it, on
+  // which job; fetch on another thread or after the lane served someone else reports EINVAL
+  std::thread::id last_thread;
+  const MinJob* last_job = nullptr;
+  std::shared_ptr<MinJob> own_job;  // the lane's job for the one-call entry points
   hipStream_t side = nullptr;         // second stream: independent work overlapped with the main one
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipStream_t cap = nullptr;           // capture stream for the gosort round graph
@@ -98,10 +107,21 @@ struct Context {
   unsigned long long* gr_dev = nullptr;   // its device address
   uint32_t gr_epoch = 0;
   uint32_t gr_resident = 0;  // workgroups of k_gr_persist resident at once (occupancy x CUs)
+  hipStream_t part = nullptr;  // the raw Minimize's transpose pass, beside the Go sort
+  hipEvent_t ev_part0 = nullptr, ev_part1 = nullptr;
+  std::shared_ptr<struct GosortPlan> raw_plan;  // Go-sort plan of the last raw corpus layout
+  std::vector<uint64_t> raw_plan_key;
 };
 
-// Returns the initialised context of the current device (lazily init(0)); throws ENODEV.
+// The lane held by the calling thread (inside SYZ_API_BODY); lazily init(0); throws ENODEV.
 Context& ctx();
+// RAII: hold a lane for the calling thread (nested API calls reuse it).
+struct LaneGuard {
+  LaneGuard();
+  ~LaneGuard();
+  LaneGuard(const LaneGuard&) = delete;
+  LaneGuard& operator=(const LaneGuard&) = delete;
+};
 
 // Kernel timing (bench roofline). Records named events around launches when enabled.
 struct Prof {
@@ -312,8 +332,9 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 // Entry-point wrapper: runs body under the context lock, converts exceptions to status codes.
 #define SYZ_API_BODY(...)                                                                        \
   try {                                                                                          \
+    ::syz::LaneGuard lane_;                                                                      \
     ::syz::Context& C_ = ::syz::ctx();                                                           \
-    std::lock_guard<std::recursive_mutex> lk_(C_.mu);                                            \
+    (void)C_;                                                                                    \
     __VA_ARGS__;                                                                                 \
     return SYZGPU_OK;                                                                            \
   } catch (const ::syz::Error& e) {                                                              \

@@ -18,7 +18,7 @@
 #include <memory>
 #include <numeric>
 
-#include "store.hpp"
+#include "panels.hpp"
 
 namespace syz {
 
@@ -178,41 +178,6 @@ __global__ __launch_bounds__(BK_BLOCK) void k_bucket_count(const Chunk* chunks, 
   }
 }
 
-__global__ __launch_bounds__(BK_BLOCK) void k_bucket_scatter(const Chunk* chunks, const GBucket* gb,
-                                                             const uint32_t* members, const uint64_t* off,
-                                                             const uint32_t* pcs, const uint32_t* rank_of_member,
-                                                             const uint64_t* boff, uint32_t* bcursor, uint2* items) {
-  __shared__ uint32_t hist[HIST_LDS];
-  const Chunk ch = chunks[blockIdx.x];
-  const GBucket b = gb[ch.g];
-  const uint32_t nb = 1u << b.bits;
-  const bool lds = nb <= HIST_LDS;
-  if (lds) {
-    for (uint32_t i = threadIdx.x; i < nb; i += BK_BLOCK) hist[i] = 0;
-    __syncthreads();
-    for (uint32_t m = ch.mbeg; m < ch.mend; m++) {
-      const uint32_t e = members[m];
-      for (uint64_t k = off[e] + threadIdx.x; k < off[e + 1]; k += BK_BLOCK)
-        atomicAdd(&hist[bucket_local(pcs[k], b.bits)], 1u);
-    }
-    __syncthreads();
-    // reserve this chunk's slice of every touched bucket; hist becomes the running cursor
-    for (uint32_t i = threadIdx.x; i < nb; i += BK_BLOCK)
-      if (hist[i]) hist[i] = atomicAdd(&bcursor[b.base + i], hist[i]);
-    __syncthreads();
-  }
-  for (uint32_t m = ch.mbeg; m < ch.mend; m++) {
-    const uint32_t e = members[m];
-    const uint32_t R = rank_of_member[m];
-    for (uint64_t k = off[e] + threadIdx.x; k < off[e + 1]; k += BK_BLOCK) {
-      const uint32_t pc = pcs[k];
-      const uint32_t lb = bucket_local(pc, b.bits);
-      const uint32_t slot = lds ? atomicAdd(&hist[lb], 1u) : atomicAdd(&bcursor[b.base + lb], 1u);
-      items[boff[b.base + lb] + slot] = make_uint2(pc, R);
-    }
-  }
-}
-
 // ---- 4. hash pass: min rank per pc inside one bucket -------------------------------------------
 constexpr int HT_BLOCK = 512;
 constexpr uint32_t HT_SLOTS = 16384;
@@ -221,107 +186,7 @@ constexpr uint32_t HT_ROUND_ITEMS = 12288;
 
 __device__ __forceinline__ uint32_t hslot(uint32_t pc) { return (pc * 0x9E3779B1u) >> 18; }  // 14 bits
 
-__global__ __launch_bounds__(HT_BLOCK) void k_bucket_hash(const uint64_t* boff, uint32_t nbuckets, const uint2* items,
-                                                          uint8_t* sel_rank) {
-  __shared__ uint32_t keys[HT_SLOTS];
-  __shared__ uint32_t vals[HT_SLOTS];
-  __shared__ uint32_t sent_min;
-  __shared__ int full;
-  for (uint32_t bk = blockIdx.x; bk < nbuckets; bk += gridDim.x) {
-    const uint64_t beg = boff[bk], end = boff[bk + 1];
-    const uint64_t cnt = end - beg;
-    if (cnt == 0) continue;
-    uint32_t rounds = (uint32_t)((cnt + HT_ROUND_ITEMS - 1) / HT_ROUND_ITEMS);
-    for (;;) {
-      bool restart = false;
-      for (uint32_t r = 0; r < rounds && !restart; r++) {
-        for (uint32_t i = threadIdx.x; i < HT_SLOTS; i += HT_BLOCK) {
-          keys[i] = HT_EMPTY;
-          vals[i] = 0xFFFFFFFFu;
-        }
-        if (threadIdx.x == 0) {
-          sent_min = 0xFFFFFFFFu;
-          full = 0;
-        }
-        __syncthreads();
-        for (uint64_t k = beg + threadIdx.x; k < end; k += HT_BLOCK) {
-          const uint2 it = items[k];
-          const uint32_t pc = it.x, R = it.y;
-          if (rounds > 1 && (hash32(pc ^ 0x5bd1e995u) % rounds) != r) continue;
-          if (pc == HT_EMPTY) {
-            atomicMin(&sent_min, R);
-            continue;
-          }
-          uint32_t h = hslot(pc);
-          uint32_t probes = 0;
-          for (;;) {
-            const uint32_t cur = keys[h];
-            if (cur == pc || (cur == HT_EMPTY && atomicCAS(&keys[h], HT_EMPTY, pc) == HT_EMPTY) ||
-                keys[h] == pc) {
-              if (vals[h] > R) atomicMin(&vals[h], R);
-              break;
-            }
-            h = (h + 1) & (HT_SLOTS - 1);
-            if (++probes >= HT_SLOTS) {
-              full = 1;
-              break;
-            }
-          }
-        }
-        __syncthreads();
-        if (full) {
-          restart = true;
-        } else {
-          for (uint32_t i = threadIdx.x; i < HT_SLOTS; i += HT_BLOCK)
-            if (keys[i] != HT_EMPTY) sel_rank[vals[i]] = 1;
-          if (threadIdx.x == 0 && sent_min != 0xFFFFFFFFu) sel_rank[sent_min] = 1;
-        }
-        __syncthreads();
-      }
-      if (!restart) break;
-      rounds *= 2;  // completed rounds' marks are exact, re-marking is idempotent
-    }
-  }
-}
-
-// ---- 5. selection outputs --------------------------------------------------------------------------
-// BITS: the winners arrive as a rank bitmap (store path) and sel_rank is written from it;
-// otherwise sel_rank (bytes) is the input.
-template <bool BITS>
-__global__ __launch_bounds__(256) void k_select_out(const uint32_t* sel_bits, uint8_t* sel_rank,
-                                                    const uint32_t* ent_of_rank, size_t n, const uint16_t* prog_len,
-                                                    int32_t C, uint8_t* selected, int64_t* hist, int* err) {
-  extern __shared__ unsigned long long lh[];
-  const bool do_hist = prog_len != nullptr;
-  if (do_hist) {
-    for (int32_t i = threadIdx.x; i <= C; i += blockDim.x) lh[i] = 0;
-    __syncthreads();
-  }
-  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t e = ent_of_rank[r];
-    uint8_t s;
-    if (BITS) {
-      s = (uint8_t)((sel_bits[r >> 5] >> (r & 31)) & 1u);
-      sel_rank[r] = s;
-    } else {
-      s = sel_rank[r];
-    }
-    if (selected) selected[e] = s;
-    if (do_hist && s) {
-      const uint32_t L = prog_len[e];
-      if ((int32_t)L > C)
-        atomicOr(err, 2);
-      else
-        atomicAdd(&lh[L], 1ull);
-    }
-  }
-  if (do_hist) {
-    __syncthreads();
-    for (int32_t i = threadIdx.x; i <= C; i += blockDim.x)
-      if (lh[i]) atomicAdd((unsigned long long*)&hist[i], lh[i]);
-  }
-}
-
+// ---- 5. selection outputs ------------------------------------------------------------------------
 // Store path: kept flags in ENTRY order (coalesced stores; the rank-ordered form walks a permutation)
 // and the len(p.Calls) histogram of kept programs of the groups this rank counts (count_hist[g]).
 __global__ __launch_bounds__(256) void k_select_store(const uint32_t* sel_bits, const uint32_t* member_of,
@@ -369,25 +234,9 @@ __global__ __launch_bounds__(256) void k_select_store(const uint32_t* sel_bits, 
   }
 }
 
-__global__ void k_bits_to_bytes(const uint32_t* bits, size_t n, uint8_t* out) {
-  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
-    out[r] = (uint8_t)((bits[r >> 5] >> (r & 31)) & 1u);
-}
-
 __global__ void k_invert(const uint32_t* members, size_t n, uint32_t* member_of) {
   for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x)
     member_of[members[m]] = (uint32_t)m;
-}
-
-__global__ void k_compact_ranks(const uint8_t* sel_rank, const uint64_t* pos, const uint32_t* ent_of_rank, size_t n,
-                                int64_t* out) {
-  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
-    if (sel_rank[r]) out[pos[r]] = (int64_t)ent_of_rank[r];
-}
-
-__global__ void k_group_out_off(const uint64_t* pos, const uint64_t* gstart, uint32_t G, uint64_t* goff) {
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x)
-    goff[g] = pos[gstart[g]];
 }
 
 // ---- host orchestration ------------------------------------------------------------------------------
@@ -406,168 +255,92 @@ __global__ void k_order_out(const uint64_t* el, const uint32_t* perm, const uint
   }
 }
 
-struct MinState {
-  uint64_t* gstart = nullptr;
-  uint8_t* sel_rank = nullptr;
-  uint32_t* ent_of_rank = nullptr;
-  const uint32_t* sel_bits = nullptr;  // store path: sel_rank is expanded from these on fetch
-};
-static MinState g_min;
-
-void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
-                          size_t n, uint32_t G, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s) {
-  Context& c = ctx();
-  if (G == 0 || G > MAX_GROUPS) fail(SYZGPU_EINVAL, "ngroups out of range (1..4096)");
-  if (n >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
-  Scratch& sc = c.scratch;
+void group_partition_dev(const uint32_t* group, const uint64_t* off, size_t n, uint32_t G, uint64_t* gstart,
+                         uint32_t* members, uint64_t* el, int* err, hipStream_t s) {
+  Scratch& sc = ctx().scratch;
   const uint32_t nchunks = (uint32_t)((n + PW_ITEMS - 1) / PW_ITEMS);
-  int* err = sc.get<int>("mz_err", 2);
   uint32_t* cnt = sc.get<uint32_t>("mz_cnt", (size_t)G * nchunks + 1);
   uint64_t* cnt_scan = sc.get<uint64_t>("mz_cnt_scan", (size_t)G * nchunks + 1);
-  uint64_t* gpcs = sc.get<uint64_t>("mz_gpcs", G + 1);
-  uint64_t* gstart = sc.get<uint64_t>("mz_gstart", G + 1);
-  uint32_t* members = sc.get<uint32_t>("mz_members", n + 1);
-  uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
-  uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
-  uint32_t* rank_of_member = sc.get<uint32_t>("mz_rom", n + 1);
-  uint32_t* ent_of_rank = sc.get<uint32_t>("mz_eor", n + 1);
-  uint8_t* sel_rank = sc.get<uint8_t>("mz_sel", n + 1);
-  SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
   SYZ_HIP(hipMemsetAsync(cnt, 0, ((size_t)G * nchunks + 1) * 4, s));
-  SYZ_HIP(hipMemsetAsync(gpcs, 0, (G + 1) * 8, s));
-  SYZ_HIP(hipMemsetAsync(sel_rank, 0, n + 1, s));
-  if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
-  {
-    ProfScope ps("group_partition", s, (uint64_t)n * 28);
-    if (n) {
-      const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
-      k_grp_count<<<wg, 256, 4 * G * 4, s>>>(group, n, G, nchunks, cnt, err);
-      SYZ_LAUNCHED();
-      k_grp_sumlen<<<grid_for(n, 256, 2048), 256, G * 8, s>>>(group, off, n, G, gpcs);
-      SYZ_LAUNCHED();
-    }
-    exclusive_scan_u32(cnt, cnt_scan, (size_t)G * nchunks, s);
-    k_grp_starts<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(cnt_scan, G, nchunks, n, gstart);
+  const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
+  if (n) {
+    k_grp_count<<<wg, 256, 4 * G * 4, s>>>(group, n, G, nchunks, cnt, err);
     SYZ_LAUNCHED();
-    if (n) {
-      const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
-      k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, cnt_scan, members, el);
-      SYZ_LAUNCHED();
-    }
   }
-  // host needs the group layout to plan the sort roots and the bucket layout
-  uint64_t* hbuf = c.pinned.get<uint64_t>(2 * (size_t)G + 4);
-  int* herr = reinterpret_cast<int*>(hbuf + 2 * (size_t)G + 2);
-  SYZ_HIP(hipMemcpyAsync(hbuf, gstart, (G + 1) * 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(hbuf + G + 1, gpcs, G * 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(herr, err, 4, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  if (*herr) fail(SYZGPU_EINVAL, "group id >= ngroups");
-  std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
-
-  if (n) gosort_groups(el, perm, n, hstart, G, s);
-  {
-    ProfScope ps("ranks", s, (uint64_t)n * 16);
-    if (n) {
-      k_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(el, perm, n, members, rank_of_member, ent_of_rank);
-      SYZ_LAUNCHED();
-    }
+  exclusive_scan_u32(cnt, cnt_scan, (size_t)G * nchunks, s);
+  k_grp_starts<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(cnt_scan, G, nchunks, n, gstart);
+  SYZ_LAUNCHED();
+  if (n) {
+    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, cnt_scan, members, el);
+    SYZ_LAUNCHED();
   }
-
-  // bucket layout: ~HT_ROUND_ITEMS occurrences per bucket, power-of-two buckets per group
-  std::vector<GBucket> hgb(G);
-  std::vector<Chunk> hch;
-  uint32_t nbuckets = 0;
-  uint64_t total_pcs = 0;
-  for (uint32_t g = 0; g < G; g++) {
-    const uint64_t np = hpcs[g];
-    total_pcs += np;
-    uint32_t bits = 0;
-    while (bits < 24 && ((uint64_t)HT_ROUND_ITEMS << bits) < np) bits++;
-    hgb[g] = GBucket{nbuckets, bits};
-    nbuckets += 1u << bits;
-    const uint64_t ng = hstart[g + 1] - hstart[g];
-    if (ng == 0) continue;
-    const uint64_t avg = std::max<uint64_t>(1, np / ng);
-    const uint64_t target = std::max<uint64_t>(32768, 4ull << bits);
-    const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ng, target / avg));
-    for (uint64_t m = hstart[g]; m < hstart[g + 1]; m += per)
-      hch.push_back(Chunk{g, (uint32_t)m, (uint32_t)std::min<uint64_t>(hstart[g + 1], m + per), 0});
-  }
-  GBucket* dgb = sc.get<GBucket>("mz_gb", G);
-  Chunk* dch = sc.get<Chunk>("mz_chunks", hch.size() + 1);
-  uint32_t* bcount = sc.get<uint32_t>("mz_bcount", nbuckets + 1);
-  uint64_t* boff = sc.get<uint64_t>("mz_boff", nbuckets + 1);
-  uint32_t* bcursor = sc.get<uint32_t>("mz_bcursor", nbuckets + 1);
-  uint2* items = sc.get<uint2>("mz_items", total_pcs + 1);
-  SYZ_HIP(hipMemcpyAsync(dgb, hgb.data(), G * sizeof(GBucket), hipMemcpyHostToDevice, s));
-  if (!hch.empty()) SYZ_HIP(hipMemcpyAsync(dch, hch.data(), hch.size() * sizeof(Chunk), hipMemcpyHostToDevice, s));
-  SYZ_HIP(hipMemsetAsync(bcount, 0, (nbuckets + 1) * 4, s));
-  SYZ_HIP(hipMemsetAsync(bcursor, 0, (nbuckets + 1) * 4, s));
-  if (!hch.empty()) {
-    {
-      ProfScope ps("bucket_count", s, total_pcs * 4 + n * 16);
-      k_bucket_count<<<(unsigned)hch.size(), BK_BLOCK, 0, s>>>(dch, dgb, members, off, pcs, bcount);
-      SYZ_LAUNCHED();
-    }
-    exclusive_scan_u32(bcount, boff, nbuckets, s);
-    {
-      ProfScope ps("bucket_scatter", s, total_pcs * 12 + n * 20);
-      k_bucket_scatter<<<(unsigned)hch.size(), BK_BLOCK, 0, s>>>(dch, dgb, members, off, pcs, rank_of_member, boff,
-                                                                 bcursor, items);
-      SYZ_LAUNCHED();
-    }
-    {
-      ProfScope ps("bucket_hash", s, total_pcs * 8);
-      k_bucket_hash<<<std::min<uint32_t>(nbuckets, 65536), HT_BLOCK, 0, s>>>(boff, nbuckets, items, sel_rank);
-      SYZ_LAUNCHED();
-    }
-  }
-  {
-    ProfScope ps("select_out", s, (uint64_t)n * 8);
-    if (n) {
-      k_select_out<false><<<grid_for(n, 256, 2048), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
-          nullptr, sel_rank, ent_of_rank, n, len_hist ? prog_len : nullptr, C, selected, len_hist, err);
-      SYZ_LAUNCHED();
-    }
-  }
-  if (len_hist) {
-    int* h = c.pinned.get<int>(4);
-    SYZ_HIP(hipMemcpyAsync(h, err, 8, hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
-    if (h[0] & 2) fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
-  }
-  g_min.gstart = gstart;
-  g_min.sel_rank = sel_rank;
-  g_min.ent_of_rank = ent_of_rank;
-  g_min.sel_bits = nullptr;
-  c.last_n = n;
-  c.last_groups = G;
-  c.have_last = true;
 }
 
-void minimize_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n, uint32_t G, hipStream_t s) {
-  Context& c = ctx();
-  if (!c.have_last || c.last_n != n || c.last_groups != G) fail(SYZGPU_EINVAL, "no matching minimize result");
-  uint64_t* pos = c.scratch.get<uint64_t>("mz_pos", n + 1);
-  int64_t* dout = c.scratch.get<int64_t>("mz_out", n + 1);
-  uint64_t* dgoff = c.scratch.get<uint64_t>("mz_goff", G + 1);
-  if (g_min.sel_bits && n) {
-    k_bits_to_bytes<<<grid_for(n, 256, 4096), 256, 0, s>>>(g_min.sel_bits, n, g_min.sel_rank);
-    SYZ_LAUNCHED();
+// groups of one entry are not sorted (no pack or round touches them): their rank is their position
+__global__ void k_rank_init(const uint32_t* members, size_t n, uint32_t* rank_of_member, uint32_t* ent_of_rank) {
+  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x) {
+    rank_of_member[m] = (uint32_t)m;
+    ent_of_rank[m] = members[m];
   }
-  exclusive_scan_u8(g_min.sel_rank, pos, n, s);
-  if (n) {
-    k_compact_ranks<<<grid_for(n, 256, 65536), 256, 0, s>>>(g_min.sel_rank, pos, g_min.ent_of_rank, n, dout);
-    SYZ_LAUNCHED();
-  }
-  k_group_out_off<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(pos, g_min.gstart, G, dgoff);
+}
+
+void rank_init_dev(const uint32_t* members, size_t n, uint32_t* rank_of_member, uint32_t* ent_of_rank, hipStream_t s) {
+  if (!n) return;
+  k_rank_init<<<grid_for(n, 256, 4096), 256, 0, s>>>(members, n, rank_of_member, ent_of_rank);
   SYZ_LAUNCHED();
-  SYZ_HIP(hipMemcpyAsync(group_out_off, dgoff, (G + 1) * 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  const uint64_t m = group_out_off[G];
-  if (m) SYZ_HIP(hipMemcpyAsync(out_idx, dout, m * 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
+}
+
+void ranks_packs(const uint64_t* el, const uint32_t* perm, const GosortPlan& P, const uint32_t* members,
+                 uint32_t* rank_of_member, uint32_t* ent_of_rank, hipStream_t q) {
+  if (!P.npacks) return;  // a pack holds at most GS_T_SEG elements
+  k_ranks_ranges<<<dim3(GS_T_SEG / 1024, P.npacks), 256, 0, q>>>(el, perm, reinterpret_cast<const uint4*>(P.packs),
+                                                                 members, rank_of_member, ent_of_rank);
+  SYZ_LAUNCHED();
+}
+
+void ranks_big(const uint64_t* el, const uint32_t* perm, const GosortPlan& P, const uint32_t* members,
+               uint32_t* rank_of_member, uint32_t* ent_of_rank, hipStream_t q) {
+  if (!P.nbig) return;
+  const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>(1, P.big_max / 2048), 256);
+  k_ranks_ranges<<<dim3(gx, P.nbig), 256, 0, q>>>(el, perm, reinterpret_cast<const uint4*>(P.big), members,
+                                                 rank_of_member, ent_of_rank);
+  SYZ_LAUNCHED();
+}
+
+static MinJob& lane_job() {
+  Context& c = ctx();
+  if (!c.own_job) c.own_job = std::make_shared<MinJob>();
+  return *c.own_job;
+}
+
+// one call: begin + outputs on the lane's own job (remembered for syzgpu_minimize_grouped_fetch)
+void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
+                          size_t n, uint32_t G, int32_t C, uint8_t* selected, int64_t* len_hist, int64_t* out_idx,
+                          uint64_t* group_out_off, hipStream_t s) {
+  Context& c = ctx();
+  MinJob& J = lane_job();
+  c.last_job = nullptr;
+  RawMinArgs a{pcs, off, group, prog_len, n, G};
+  a.s = s;
+  minimize_raw_begin(J, a);
+  RawEndArgs e;
+  e.C = C;
+  e.selected = selected;
+  e.len_hist = len_hist;
+  e.out_idx = out_idx;
+  e.group_out_off = group_out_off;
+  e.s = s;
+  minimize_raw_end(J, e);
+  c.last_job = &J;
+  c.last_thread = std::this_thread::get_id();
+}
+
+void minimize_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n, uint32_t G) {
+  Context& c = ctx();
+  if (!c.own_job || c.last_job != c.own_job.get() || c.last_thread != std::this_thread::get_id() ||
+      c.own_job->n != n || c.own_job->G != G)
+    fail(SYZGPU_EINVAL, "no matching minimize result on this thread");
+  minimize_raw_fetch(*c.own_job, out_idx, group_out_off);
 }
 
 }  // namespace syz
@@ -581,12 +354,28 @@ int syzgpu_minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const 
                                 int64_t* len_hist, void* stream) {
   SYZ_API_BODY({
     if (len_hist && (C <= 0 || !prog_len)) fail(SYZGPU_EINVAL, "len_hist needs prog_len and C > 0");
-    minimize_grouped_dev(pcs, off, group, prog_len, n, ngroups, C, selected, len_hist, (hipStream_t)stream);
+    minimize_grouped_dev(pcs, off, group, prog_len, n, ngroups, C, selected, len_hist, nullptr, nullptr,
+                         (hipStream_t)stream);
+  })
+}
+
+int syzgpu_minimize_grouped_ordered_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                        const uint16_t* prog_len, size_t n, uint32_t ngroups, int32_t C,
+                                        uint8_t* selected, int64_t* len_hist, int64_t* out_idx,
+                                        uint64_t* group_out_off, void* stream) {
+  SYZ_API_BODY({
+    if (len_hist && (C <= 0 || !prog_len)) fail(SYZGPU_EINVAL, "len_hist needs prog_len and C > 0");
+    if (!off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
+    minimize_grouped_dev(pcs, off, group, prog_len, n, ngroups, C, selected, len_hist, out_idx, group_out_off,
+                         (hipStream_t)stream);
   })
 }
 
 int syzgpu_minimize_grouped_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n, uint32_t ngroups) {
-  SYZ_API_BODY({ minimize_fetch(out_idx, group_out_off, n, ngroups, C_.stream); })
+  SYZ_API_BODY({
+    if (!group_out_off) fail(SYZGPU_EINVAL, "null pointer");
+    minimize_fetch(out_idx, group_out_off, n, ngroups);
+  })
 }
 
 int syzgpu_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
@@ -602,8 +391,12 @@ int syzgpu_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint
     if (tot) SYZ_HIP(hipMemcpyAsync(dp, pcs, tot * 4, hipMemcpyHostToDevice, s));
     SYZ_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
     if (n) SYZ_HIP(hipMemcpyAsync(dg, group, n * 4, hipMemcpyHostToDevice, s));
-    minimize_grouped_dev(dp, doff, dg, nullptr, n, ngroups, 0, nullptr, nullptr, s);
-    minimize_fetch(out_idx, group_out_off, n, ngroups, s);
+    MinJob& J = lane_job();
+    C_.last_job = nullptr;
+    RawMinArgs a{dp, doff, dg, nullptr, n, ngroups};
+    a.s = s;
+    minimize_raw_begin(J, a);
+    minimize_raw_fetch(J, out_idx, group_out_off);
   })
 }
 
@@ -832,42 +625,6 @@ constexpr int VM_BLOCK = 1024;
 #define SYZ_VM_DEPTH 4
 #endif
 constexpr int VM_DEPTH = SYZ_VM_DEPTH;  // vectors per lane per pipelined batch (k_vec_min)
-
-// Winning ranks of a window table (LDS or global) -> set bits of sel_bits (global rank bitmap).
-// Ranks of call g lie in [gstart[g], gstart[g+1]). Winners are mostly early ranks (the longest covers
-// come first in Go-sort order), so the first BM_WORDS*32 ranks of the call are deduplicated through
-// an LDS bitmap (one bit-OR per kept input instead of one per id) and the rarer later ones go straight
-// to sel_bits: one pass over the table whatever the call's size.
-template <bool ATOMIC_READ = false>
-__device__ __forceinline__ void emit_winners(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
-                                             uint32_t* bm, uint32_t* sel_bits) {
-  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BM_WORDS * 32, ng);
-  const uint32_t words = (span + 31) / 32;
-  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
-    const uint32_t r = ATOMIC_READ ? __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tab[i];
-    if (r == RANK_NONE) continue;
-    const uint64_t lr = (uint64_t)r - gbase;
-    if (lr < span)
-      atomicOr(&bm[lr >> 5], 1u << (lr & 31));
-    else
-      atomicOr(&sel_bits[r >> 5], 1u << (r & 31));
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
-    const uint32_t wv = bm[i];
-    if (!wv) continue;
-    const uint64_t gb = gbase + 32ull * i;
-    const uint32_t sh = (uint32_t)(gb & 31);
-    atomicOr(&sel_bits[gb >> 5], wv << sh);
-    if (sh) {
-      const uint32_t hi = wv >> (32 - sh);
-      if (hi) atomicOr(&sel_bits[(gb >> 5) + 1], hi);
-    }
-  }
-  __syncthreads();
-}
 
 __device__ __forceinline__ void tab_min(uint32_t* tab, uint32_t id, uint32_t R) {
   if (tab[id] > R) atomicMin(&tab[id], R);
@@ -1345,7 +1102,6 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   return cp.release();
 }
 
-static Corpus* g_last_corpus = nullptr;
 
 // minimizeCorpus, first half: the Go-sort ranks and the first-occurrence pass into the rank bitmap
 // (this rank's key parts only, see corpus_set_parts).
@@ -1356,10 +1112,13 @@ void corpus_minimize_begin(Corpus& K, hipStream_t s) {
   int* err = sc.get<int>("mz_err", 2);
   uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
   uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
-  uint32_t* rank_of_member = sc.get<uint32_t>("mz_rom", n + 1);
-  uint32_t* ent_of_rank = sc.get<uint32_t>("mz_eor", n + 1);
+  K.rom.ensure(n + 1);
+  K.eor.ensure(n + 1);
+  K.sel_bits.ensure(n / 32 + 2);
+  uint32_t* rank_of_member = K.rom.p;
+  uint32_t* ent_of_rank = K.eor.p;
   SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
-  uint32_t* sel_bits = sc.get<uint32_t>("mz_selbits", n / 32 + 2);
+  uint32_t* sel_bits = K.sel_bits.p;
   SYZ_HIP(hipMemsetAsync(sel_bits, 0, (n / 32 + 2) * 4, s));
   if (K.ngtabs) {
     SYZ_HIP(hipMemsetAsync(K.gtabs.p, 0xFF, (size_t)K.ngtabs * WIN * 4, s));
@@ -1411,14 +1170,7 @@ void corpus_minimize_begin(Corpus& K, hipStream_t s) {
     vec_min(q, 0, K.nbig_work, false);
   };
   if (n) gosort_run(el, perm, n, P, s, small_done, big_done);
-  g_min.gstart = K.gstart.p;
-  g_min.sel_rank = sc.get<uint8_t>("mz_sel", n + 1);
-  g_min.ent_of_rank = ent_of_rank;
-  g_min.sel_bits = sel_bits;
-  c.last_n = n;
-  c.last_groups = K.G;
-  c.have_last = true;
-  g_last_corpus = &K;
+  K.begun = true;
 }
 
 // Selection of the listed call groups as one byte per group-relative rank, at byte offsets boff[j]
@@ -1447,8 +1199,8 @@ void corpus_sel_xchg(Corpus& K, const uint32_t* groups, const uint64_t* offsets,
     if (groups[j] >= K.G) fail(SYZGPU_EINVAL, "group id >= ngroups");
     maxn = std::max<uint64_t>(maxn, K.hstart[groups[j] + 1] - K.hstart[groups[j]]);
   }
-  Scratch& sc = ctx().scratch;
-  uint32_t* sel_bits = sc.get<uint32_t>("mz_selbits", K.n / 32 + 2);
+  if (!K.begun) fail(SYZGPU_EINVAL, "corpus: minimize_begin first");
+  uint32_t* sel_bits = K.sel_bits.p;
   // the exchange list is the same on every step: uploaded once per distinct list, so the step itself
   // never waits on the host
   std::vector<uint64_t> key(groups, groups + ng);
@@ -1474,8 +1226,9 @@ void corpus_minimize_end(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   Scratch& sc = ctx().scratch;
   const size_t n = K.n;
   int* err = sc.get<int>("mz_err", 2);
-  uint32_t* rank_of_member = sc.get<uint32_t>("mz_rom", n + 1);
-  uint32_t* sel_bits = sc.get<uint32_t>("mz_selbits", n / 32 + 2);
+  if (!K.begun) fail(SYZGPU_EINVAL, "corpus: minimize_begin first");
+  uint32_t* rank_of_member = K.rom.p;
+  uint32_t* sel_bits = K.sel_bits.p;
   if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
   ProfScope ps("select_out", s, (uint64_t)n * 8);
   if (n) {
@@ -1531,13 +1284,7 @@ Corpus* corpus_append_dev(Corpus& K, const uint32_t* pcs, const uint64_t* off, c
   return out;
 }
 
-static void corpus_release(Corpus* K) {
-  if (K == g_last_corpus) {
-    g_last_corpus = nullptr;
-    ctx().have_last = false;
-  }
-  delete K;
-}
+static void corpus_release(Corpus* K) { delete K; }
 
 }  // namespace syz
 
@@ -1548,7 +1295,9 @@ int syzgpu_corpus_append_dev(syzgpu_corpus* cp, const uint32_t* pcs, const uint6
   SYZ_API_BODY({
     if (!cp || !out || !off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
     Corpus* K = reinterpret_cast<Corpus*>(cp);
+    std::unique_lock<std::recursive_mutex> hl_(K->mu);
     Corpus* N = corpus_append_dev(*K, pcs, off, group, prog_len, n, (hipStream_t)stream);
+    hl_.unlock();
     corpus_release(K);
     *out = reinterpret_cast<syzgpu_corpus*>(N);
   })
@@ -1558,6 +1307,7 @@ int syzgpu_corpus_append(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t*
                          const uint16_t* prog_len, size_t n, syzgpu_corpus** out) {
   SYZ_API_BODY({
     if (!cp || !out || !off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
+    std::unique_lock<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     if (off[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
     hipStream_t s = C_.stream;
     const uint64_t tot = off[n];
@@ -1571,6 +1321,7 @@ int syzgpu_corpus_append(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t*
     if (dl && n) SYZ_HIP(hipMemcpyAsync(dl, prog_len, n * 2, hipMemcpyHostToDevice, s));
     Corpus* K = reinterpret_cast<Corpus*>(cp);
     Corpus* N = corpus_append_dev(*K, dp, doff, dg, dl, n, s);
+    hl_.unlock();
     corpus_release(K);
     *out = reinterpret_cast<syzgpu_corpus*>(N);
   })
@@ -1614,6 +1365,7 @@ int syzgpu_corpus_destroy(syzgpu_corpus* cp) {
 int syzgpu_corpus_minimize_dev(syzgpu_corpus* cp, int32_t C, uint8_t* selected, int64_t* len_hist, void* stream) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     if (len_hist && C <= 0) fail(SYZGPU_EINVAL, "len_hist needs C > 0");
     corpus_minimize_dev(*reinterpret_cast<Corpus*>(cp), C, selected, len_hist, (hipStream_t)stream);
   })
@@ -1622,15 +1374,24 @@ int syzgpu_corpus_minimize_dev(syzgpu_corpus* cp, int32_t C, uint8_t* selected, 
 int syzgpu_corpus_minimize(syzgpu_corpus* cp, int64_t* out_idx, uint64_t* group_out_off) {
   SYZ_API_BODY({
     if (!cp || !group_out_off) fail(SYZGPU_EINVAL, "null pointer");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     Corpus& K = *reinterpret_cast<Corpus*>(cp);
     corpus_minimize_dev(K, 0, nullptr, nullptr, C_.stream);
-    minimize_fetch(out_idx, group_out_off, K.n, K.G, C_.stream);
+    int64_t* dout = C_.scratch.get<int64_t>("mz_out", K.n + 1);
+    uint64_t* dgoff = C_.scratch.get<uint64_t>("mz_goff", K.G + 1);
+    sel_compact_dev(K.sel_bits.p, K.eor.p, K.gstart.p, K.n, K.G, dout, dgoff, C_.stream);
+    SYZ_HIP(hipMemcpyAsync(group_out_off, dgoff, (K.G + 1) * 8, hipMemcpyDeviceToHost, C_.stream));
+    SYZ_HIP(hipStreamSynchronize(C_.stream));
+    if (group_out_off[K.G] && out_idx)
+      SYZ_HIP(hipMemcpyAsync(out_idx, dout, group_out_off[K.G] * 8, hipMemcpyDeviceToHost, C_.stream));
+    SYZ_HIP(hipStreamSynchronize(C_.stream));
   })
 }
 
 int syzgpu_corpus_info(const syzgpu_corpus* cp, uint64_t* info, size_t cap) {
   SYZ_API_BODY({
     if (!cp || !info) fail(SYZGPU_EINVAL, "null pointer");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(const_cast<syzgpu_corpus*>(cp))->mu);
     const Corpus& K = *reinterpret_cast<const Corpus*>(cp);
     const uint64_t v[11] = {K.n,      K.G,          K.total_pcs,   K.total_ids, K.hwork.size(), K.ngtabs,
                             K.total_vecs, K.big_entries, K.big_pcs, K.big_vecs,  K.big_vecs_all};
@@ -1642,6 +1403,7 @@ int syzgpu_corpus_set_parts(syzgpu_corpus* cp, const uint16_t* part, const uint1
                             const uint8_t* count_hist) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     corpus_set_parts(*reinterpret_cast<Corpus*>(cp), part, nparts, count_hist, C_.stream);
   })
 }
@@ -1649,6 +1411,7 @@ int syzgpu_corpus_set_parts(syzgpu_corpus* cp, const uint16_t* part, const uint1
 int syzgpu_corpus_minimize_begin_dev(syzgpu_corpus* cp, void* stream) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     corpus_minimize_begin(*reinterpret_cast<Corpus*>(cp), (hipStream_t)stream);
   })
 }
@@ -1657,6 +1420,7 @@ int syzgpu_corpus_export_sel_dev(syzgpu_corpus* cp, const uint32_t* groups, cons
                                  uint32_t ngroups, uint8_t* buf, void* stream) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     corpus_sel_xchg(*reinterpret_cast<Corpus*>(cp), groups, offsets, ngroups, buf, 0, (hipStream_t)stream);
   })
 }
@@ -1665,6 +1429,7 @@ int syzgpu_corpus_import_sel_dev(syzgpu_corpus* cp, const uint32_t* groups, cons
                                  uint32_t ngroups, const uint8_t* buf, void* stream) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     corpus_sel_xchg(*reinterpret_cast<Corpus*>(cp), groups, offsets, ngroups, const_cast<uint8_t*>(buf), 1,
                     (hipStream_t)stream);
   })
@@ -1674,6 +1439,7 @@ int syzgpu_corpus_minimize_end_dev(syzgpu_corpus* cp, int32_t C, uint8_t* select
                                    void* stream) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
     if (len_hist && C <= 0) fail(SYZGPU_EINVAL, "len_hist needs C > 0");
     corpus_minimize_end(*reinterpret_cast<Corpus*>(cp), C, selected, len_hist, (hipStream_t)stream);
   })

@@ -1,0 +1,992 @@
+// minimizeCorpus from raw covers in HBM (syz-manager/manager.go:507-527 over cover/cover.go:105-131),
+// every step from the covers themselves: no dictionary or store built ahead of time.
+//
+// Minimize keeps input k (Go-sort position k of its call group) iff some PC of its cover first occurs
+// at k, so the work is a min-rank per (call, PC) key. Keys are split by PC value into
+// windows so that each key's min fits a workgroup's LDS, and the covers are transposed into those
+// windows by one streaming pass:
+//
+//   P  (k_part)  a workgroup per chunk (<= 16384 PCs of <= 64 consecutive members of one call group):
+//                window w = (pc - lo) >> S_g of every PC, histogram in LDS, the chunk's PCs rewritten
+//                window-major through an LDS staging buffer as u32 elements (pc offset in the window |
+//                member tag << S_g) and the window starts as a u16 row `desc` per chunk.
+//   M  (k_pmin)  a workgroup per (call, window): every chunk's run of that window, min Go-sort rank per
+//                offset in LDS — a direct-mapped 32K-entry table for dense calls (S = 15), an
+//                open-addressing table for sparse ones (wider windows) — and the rank that wins a key
+//                marks its input kept in a rank bitmap.
+//
+// P depends only on the covers, so it runs while gosort.hip computes the ranks; M waits for both.
+// Selection order, kept flags, the len(p.Calls) histogram and the group-major kept list
+// (syzgpu_minimize_grouped's output) are produced on the device in the same call.
+// Integer work throughout: bit-exact by construction (F2); tests/test_gpu_raw.py checks every output.
+#include <algorithm>
+#include <cstdlib>
+#include <memory>
+#include <numeric>
+
+#include "panels.hpp"
+
+namespace syz {
+
+constexpr uint32_t PCAP = 16384;  // PCs per chunk (the LDS staging buffer of k_part)
+constexpr uint32_t MEMB = 64;     // members per block: a 6-bit member tag in each element
+constexpr uint32_t WMAX = 1024;   // windows per call group
+constexpr uint32_t DS = 15;       // direct-mode window bits: a 32768-entry u32 min table
+constexpr uint32_t SMAX = 26;     // 32 - 6 tag bits
+constexpr int PP_BLOCK = 1024;
+constexpr int PP_WAVES = PP_BLOCK / 64;
+constexpr int PP_TPW = 20;  // 64-PC tiles per wave held in registers: PCAP/64 + MEMB tiles over 16 waves
+constexpr uint32_t HS = 8192;    // open-addressing slots of a sparse-window table
+constexpr int HM_BLOCK = 512;
+constexpr uint32_t HBM_WORDS = 2048;  // LDS winner bitmap of the sparse kernel (65536 ranks per pass)
+constexpr uint32_t DENSE = 8192;      // PCs per 32K-address window above which a call is direct-mode
+constexpr uint32_t HTARGET = 12288;   // PCs per window a sparse call's window size aims at
+
+static_assert(PP_TPW * PP_WAVES * 64 >= PCAP + 64 * MEMB, "k_part tiles per wave");
+
+// ---- per-entry statistics: PCs per call group and the PC span --------------------------------------
+__global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                                   size_t n, uint32_t G, uint64_t* gpcs, uint32_t* span) {
+  extern __shared__ unsigned long long lsum[];
+  __shared__ uint32_t slo, shi;
+  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) lsum[g] = 0;
+  if (threadIdx.x == 0) {
+    slo = 0xFFFFFFFFu;
+    shi = 0;
+  }
+  __syncthreads();
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint64_t a = off[i], b = off[i + 1];
+    const uint32_t g = group[i];
+    if (b > a) {
+      if (g < G) atomicAdd(&lsum[g], (unsigned long long)(b - a));
+      // covers are sorted (executor.cc:572-585): the first and last PC bound them; k_part checks
+      // every PC against the resulting windows and the call is redone on exact bounds otherwise
+      lo = min(lo, pcs[a]);
+      hi = max(hi, pcs[b - 1]);
+    }
+  }
+  lo = wave_min(lo);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t y = __shfl_xor(hi, d, 64);
+    hi = y > hi ? y : hi;
+  }
+  if (__lane_id() == 0) {
+    atomicMin(&slo, lo);
+    atomicMax(&shi, hi);
+  }
+  __syncthreads();
+  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+    if (lsum[g]) atomicAdd((unsigned long long*)&gpcs[g], lsum[g]);
+  if (threadIdx.x == 0) {
+    atomicMin(&span[0], slo);
+    atomicMax(&span[1], shi);
+  }
+}
+
+// exact bounds (the slow path when some cover is not sorted)
+__global__ __launch_bounds__(256) void k_minmax(const uint32_t* pcs, size_t L, uint32_t* span) {
+  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < L; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t v = pcs[i];
+    lo = min(lo, v);
+    hi = max(hi, v);
+  }
+  lo = wave_min(lo);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t y = __shfl_xor(hi, d, 64);
+    hi = y > hi ? y : hi;
+  }
+  if (__lane_id() == 0) {
+    atomicMin(&span[0], lo);
+    atomicMax(&span[1], hi);
+  }
+}
+
+__global__ void k_mlen(const uint64_t* el, size_t n, uint32_t* mlen) {
+  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x)
+    mlen[m] = (uint32_t)(el[m] >> 32);
+}
+
+// ---- blocks of 64 members and chunks of <= PCAP PCs -------------------------------------------------
+__global__ void k_blocks(const uint32_t* bgroup, uint32_t B, const uint32_t* gblock, const uint64_t* gstart,
+                         const uint64_t* mpos, uint32_t* nsub) {
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) {
+    const uint32_t g = bgroup[b];
+    const uint64_t mb = gstart[g] + (uint64_t)(b - gblock[g]) * MEMB;
+    const uint64_t me = min<uint64_t>(mb + MEMB, gstart[g + 1]);
+    const uint64_t sl = mpos[me] - mpos[mb];
+    nsub[b] = (uint32_t)((sl + PCAP - 1) / PCAP);
+  }
+}
+
+__global__ void k_chunks(const uint32_t* bgroup, uint32_t B, const uint32_t* gblock, const uint64_t* gstart,
+                         const uint64_t* mpos, const uint64_t* cstart, PChunk* chunks) {
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) {
+    const uint32_t g = bgroup[b];
+    const uint64_t mb = gstart[g] + (uint64_t)(b - gblock[g]) * MEMB;
+    const uint64_t me = min<uint64_t>(mb + MEMB, gstart[g + 1]);
+    const uint64_t base = mpos[mb], sl = mpos[me] - base;
+    uint64_t c = cstart[b];
+    for (uint64_t s = 0; s < sl; s += PCAP, c++)
+      chunks[c] = PChunk{base + s, (uint32_t)min<uint64_t>(PCAP, sl - s), (uint32_t)mb, (uint32_t)(me - mb),
+                         (uint32_t)s, g};
+  }
+}
+
+// gchunk[g] = first chunk of group g (chunks are group-major); gdesc[g] = its first desc row
+__global__ __launch_bounds__(1024) void k_gchunk(const uint32_t* gblock, uint32_t G, const uint64_t* cstart,
+                                                 const PGroup* pg, uint64_t* gchunk, uint64_t* gdesc) {
+  __shared__ uint64_t red[1024 / 64 + 1];
+  uint64_t run = 0;
+  for (uint32_t g0 = 0; g0 <= G; g0 += 1024) {
+    const uint32_t g = g0 + threadIdx.x;
+    uint64_t rows = 0;
+    if (g < G) rows = (cstart[gblock[g + 1]] - cstart[gblock[g]]) * (uint64_t)(pg[g].W + 1);
+    uint64_t tot;
+    const uint64_t pre = block_excl_scan<1024>(rows, red, &tot);
+    if (g <= G) {
+      gchunk[g] = cstart[gblock[g]];
+      gdesc[g] = run + pre;
+    }
+    run += tot;
+  }
+}
+
+// ---- P: transpose the covers into windows ---------------------------------------------------------
+__global__ __launch_bounds__(PP_BLOCK, 2) void k_part(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ members,
+                                                      const uint64_t* __restrict__ mpos,
+                                                      const uint32_t* __restrict__ sbeg, const PChunk* chunks,
+                                                      const uint64_t* nchunks_dev, const PGroup* pg,
+                                                      const uint64_t* gchunk, const uint64_t* gdesc, uint32_t lo,
+                                                      uint32_t* __restrict__ elems, uint16_t* __restrict__ desc,
+                                                      int* err) {
+  __shared__ uint32_t obuf[PCAP];
+  __shared__ uint32_t hist[WMAX + 1];
+  __shared__ uint32_t tpre[MEMB + 1];   // tiles before member m
+  __shared__ uint32_t mlo[MEMB], mhi[MEMB];  // the member's PCs inside this chunk, block coordinates
+  __shared__ uint64_t mraw[MEMB];            // off[entry] - block coordinate of the member's first PC
+  __shared__ uint32_t red[PP_WAVES + 1];
+  const uint64_t nch = *nchunks_dev;
+  const int wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const PChunk ch = chunks[c];
+    const PGroup gp = pg[ch.g];
+    const uint32_t S = gp.S, W = gp.W;
+    const uint32_t cb = ch.sub, ce = ch.sub + ch.len;
+    // member ranges and tiles
+    if (threadIdx.x < 64) {
+      const uint32_t m = threadIdx.x;
+      uint32_t nt = 0;
+      if (m < ch.nmem) {
+        const uint64_t p0 = mpos[ch.mb], a = mpos[ch.mb + m] - p0, b = mpos[ch.mb + m + 1] - p0;
+        const uint32_t x = (uint32_t)max<uint64_t>(a, cb), y = (uint32_t)min<uint64_t>(b, ce);
+        mlo[m] = x;
+        mhi[m] = y;
+        mraw[m] = off[members[ch.mb + m]] + (sbeg ? sbeg[ch.mb + m] : 0u) - a;
+        nt = y > x ? (y - x + 63) / 64 : 0;
+      }
+      const uint32_t inc = wave_incl_scan<uint32_t>(nt);
+      tpre[m] = inc - nt;
+      if (m == 63) tpre[64] = inc;
+    }
+    for (uint32_t i = threadIdx.x; i <= W; i += PP_BLOCK) hist[i] = 0;
+    __syncthreads();
+    const uint32_t ntiles = tpre[64];
+    const uint32_t nm = ch.nmem;
+    // pass 1: every PC of the chunk into registers, window histogram
+    uint32_t v[PP_TPW];
+#pragma unroll
+    for (int k = 0; k < PP_TPW; k++) {
+      const uint32_t t = wv + PP_WAVES * k;
+      v[k] = 0;
+      if (t < ntiles) {
+        const uint64_t bal = __ballot(lane < nm && tpre[lane] <= t);
+        const uint32_t m = __popcll(bal) - 1;
+        const uint32_t q = mlo[m] + (t - tpre[m]) * 64 + lane;
+        if (q < mhi[m]) v[k] = pcs[mraw[m] + q];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PP_TPW; k++) {
+      const uint32_t t = wv + PP_WAVES * k;
+      if (t < ntiles) {
+        const uint64_t bal = __ballot(lane < nm && tpre[lane] <= t);
+        const uint32_t m = __popcll(bal) - 1;
+        const uint32_t q = mlo[m] + (t - tpre[m]) * 64 + lane;
+        if (q < mhi[m]) {
+          const uint32_t w = (v[k] - lo) >> S;
+          if (w < W)
+            atomicAdd(&hist[w], 1u);
+          else
+            atomicOr(err, 1);  // outside [lo, hi]: an unsorted cover; redone on exact bounds
+        }
+      }
+    }
+    __syncthreads();
+    // window starts (exclusive scan) -> desc row and cursors
+    uint16_t* drow = desc + gdesc[ch.g] + (c - gchunk[ch.g]) * (uint64_t)(W + 1);
+    {
+      uint32_t run = 0;
+      for (uint32_t b0 = 0; b0 <= W; b0 += PP_BLOCK) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t x = i < W ? hist[i] : 0;
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan<PP_BLOCK>(x, red, &tot) + run;
+        if (i <= W) {
+          drow[i] = (uint16_t)pre;
+          hist[i] = pre;
+        }
+        run += tot;
+      }
+    }
+    __syncthreads();
+    // pass 2: element = offset in window | member tag, staged window-major in LDS
+    const uint32_t omask = (1u << S) - 1;
+#pragma unroll
+    for (int k = 0; k < PP_TPW; k++) {
+      const uint32_t t = wv + PP_WAVES * k;
+      if (t < ntiles) {
+        const uint64_t bal = __ballot(lane < nm && tpre[lane] <= t);
+        const uint32_t m = __popcll(bal) - 1;
+        const uint32_t q = mlo[m] + (t - tpre[m]) * 64 + lane;
+        if (q < mhi[m]) {
+          const uint32_t d = v[k] - lo, w = d >> S;
+          if (w < W) obuf[atomicAdd(&hist[w], 1u)] = (d & omask) | (m << S);
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t* dst = elems + ch.elem;
+    for (uint32_t i = threadIdx.x; i < ch.len; i += PP_BLOCK) dst[i] = obuf[i];
+    __syncthreads();
+  }
+}
+
+// ---- M: min rank per key of one (call, window) ------------------------------------------------------
+// The runs of the window in every chunk of the call, flattened across a wave: lane i of a batch of 64
+// runs finds its run by a binary search over the wave's inclusive run-length prefix.
+template <class F>
+__device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* __restrict__ chunks,
+                                                 const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
+                                                 const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems,
+                                                 const uint32_t* __restrict__ rank_of_member, int nwaves, F f) {
+  const uint32_t g = it.g, w = it.w;
+  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
+  const uint32_t W = pg[g].W, S = pg[g].S;
+  const uint16_t* d0 = desc + gdesc[g] + w;
+  const int wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  constexpr int U = 4;
+  for (uint64_t cb = c0 + (uint64_t)wv * 64; cb < c1; cb += (uint64_t)nwaves * 64) {
+    const uint64_t c = cb + lane;
+    uint32_t len = 0, mb = 0;
+    uint64_t st = 0;
+    if (c < c1) {
+      const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
+      const uint32_t s0 = d[0], s1 = d[1];
+      len = s1 - s0;
+      st = chunks[c].elem + s0;
+      mb = chunks[c].mb;
+    }
+    const uint32_t P = wave_incl_scan<uint32_t>(len);
+    const uint32_t E = P - len;
+    const uint32_t total = __shfl(P, 63, 64);
+    for (uint32_t t = 0; t < total; t += 64 * U) {
+      uint32_t x[U], mbs[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t i = t + 64 * u + lane;
+        ok[u] = i < total;
+        uint32_t j = 0;
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+          const uint32_t pj = __shfl(P, (int)(j + s - 1), 64);
+          if (pj <= i) j += s;
+        }
+        j = min(j, 63u);
+        const uint32_t lo32 = __shfl((uint32_t)st, (int)j, 64), hi32 = __shfl((uint32_t)(st >> 32), (int)j, 64);
+        const uint32_t ej = __shfl(E, (int)j, 64);
+        mbs[u] = __shfl(mb, (int)j, 64);
+        const uint64_t a = (((uint64_t)hi32 << 32) | lo32) + (i - ej);
+        x[u] = ok[u] ? elems[a] : 0;
+      }
+      uint32_t r[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) r[u] = ok[u] ? rank_of_member[mbs[u] + (x[u] >> S)] : 0;
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (ok[u]) f(x[u] & ((1u << S) - 1), r[u]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
+                                                      const uint64_t* gchunk, const uint64_t* gdesc,
+                                                      const PGroup* pg, const uint16_t* __restrict__ desc,
+                                                      const uint32_t* __restrict__ elems,
+                                                      const uint32_t* __restrict__ rank_of_member,
+                                                      const uint64_t* gstart, uint32_t* sel_bits) {
+  __shared__ uint32_t tab[1u << DS];
+  __shared__ uint32_t bm[BM_WORDS];
+  const PItem it = items[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < (1u << DS); i += 1024) tab[i] = RANK_NONE;
+  __syncthreads();
+  for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, 16, [&](uint32_t o, uint32_t R) {
+    if (tab[o] > R) atomicMin(&tab[o], R);
+  });
+  __syncthreads();
+  const uint64_t gb = gstart[it.g];
+  emit_winners(tab, 1u << DS, gb, gstart[it.g + 1] - gb, bm, sel_bits);
+}
+
+__device__ __forceinline__ uint32_t hslot13(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - 13); }
+static_assert(HS == 8192, "hslot13");
+
+// Sparse windows: open addressing keyed by the window offset. If the window holds more distinct keys
+// than fit, it is redone in R rounds (keys split by another hash), R doubling until every round fits;
+// a winner marked by a finished round stays valid (marks are ORs of exact winners).
+__global__ __launch_bounds__(HM_BLOCK) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
+                                                        const uint64_t* gchunk, const uint64_t* gdesc,
+                                                        const PGroup* pg, const uint16_t* __restrict__ desc,
+                                                        const uint32_t* __restrict__ elems,
+                                                        const uint32_t* __restrict__ rank_of_member,
+                                                        const uint64_t* gstart, uint32_t* sel_bits) {
+  __shared__ uint32_t keys[HS];
+  __shared__ uint32_t vals[HS];
+  __shared__ uint32_t bm[HBM_WORDS];
+  __shared__ uint32_t fill;
+  __shared__ int full;
+  const PItem it = items[blockIdx.x];
+  const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
+  uint32_t R = 1;
+  for (uint32_t round = 0; round < R;) {
+    for (uint32_t i = threadIdx.x; i < HS; i += HM_BLOCK) {
+      keys[i] = 0xFFFFFFFFu;
+      vals[i] = RANK_NONE;
+    }
+    if (threadIdx.x == 0) {
+      fill = 0;
+      full = 0;
+    }
+    __syncthreads();
+    const uint32_t rmask = R - 1;
+    for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, HM_BLOCK / 64,
+                     [&](uint32_t o, uint32_t Rk) {
+                       if (rmask && ((hash32(o) >> 7) & rmask) != round) return;
+                       uint32_t h = hslot13(o);
+                       for (uint32_t probes = 0; probes < HS; probes++) {
+                         uint32_t k = keys[h];
+                         if (k == 0xFFFFFFFFu) {
+                           k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
+                           if (k == 0xFFFFFFFFu) {
+                             if (atomicAdd(&fill, 1u) >= HS - HS / 8) full = 1;
+                             k = o;
+                           }
+                         }
+                         if (k == o) {
+                           if (vals[h] > Rk) atomicMin(&vals[h], Rk);
+                           return;
+                         }
+                         h = (h + 1) & (HS - 1);
+                       }
+                       full = 1;
+                     });
+    __syncthreads();
+    if (full) {  // redo every round with twice as many
+      R *= 2;
+      round = 0;
+      __syncthreads();
+      continue;
+    }
+    emit_winners<false, HBM_WORDS>(vals, HS, gb, ng, bm, sel_bits);
+    round++;
+  }
+}
+
+// ---- outputs: the group-major kept list in selection order ----------------------------------------
+__global__ void k_sel_wpop(const uint32_t* sel_bits, size_t nw, uint32_t* cnt) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x)
+    cnt[i] = __popc(sel_bits[i]);
+}
+
+__device__ __forceinline__ uint64_t sel_pos(const uint32_t* sel_bits, const uint64_t* wpos, size_t nw, uint64_t r) {
+  const uint64_t wi = r >> 5;
+  const uint32_t word = wi < nw ? sel_bits[wi] : 0u;
+  const uint32_t sh = (uint32_t)(r & 31);
+  return wpos[wi] + __popc(sh ? word & ((1u << sh) - 1) : 0u);
+}
+
+__global__ void k_sel_compact(const uint32_t* sel_bits, const uint64_t* wpos, const uint32_t* ent_of_rank, size_t n,
+                              int64_t* out) {
+  const size_t nw = (n + 31) / 32;
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
+    if ((sel_bits[r >> 5] >> (r & 31)) & 1u) out[sel_pos(sel_bits, wpos, nw, r)] = (int64_t)ent_of_rank[r];
+}
+
+__global__ void k_sel_goff(const uint32_t* sel_bits, const uint64_t* wpos, const uint64_t* gstart, uint32_t G,
+                           size_t n, uint64_t* goff) {
+  const size_t nw = (n + 31) / 32;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x)
+    goff[g] = sel_pos(sel_bits, wpos, nw, gstart[g]);
+}
+
+// ---- key parts: a call group restricted to a PC range (multi-GPU) --------------------
+// slice of member m's (sorted) cover inside [klo, khi]; members of whole groups keep their cover
+__global__ void k_slices(const uint32_t* pcs, const uint64_t* off, const uint32_t* members, const uint64_t* el,
+                         const uint32_t* group, size_t n, const uint32_t* krange, uint32_t* sbeg, uint32_t* slen) {
+  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t e = members[m];
+    const uint32_t L = (uint32_t)(el[m] >> 32);
+    const uint32_t klo = krange[2 * group[e]], khi = krange[2 * group[e] + 1];
+    if (klo == 0 && khi == 0xFFFFFFFFu) {
+      sbeg[m] = 0;
+      slen[m] = L;
+      continue;
+    }
+    const uint64_t b = off[e];
+    const uint64_t x = lower_bound_dev<uint32_t>(pcs, b, b + L, klo);
+    const uint64_t y = khi == 0xFFFFFFFFu ? b + L : lower_bound_dev<uint32_t>(pcs, x, b + L, khi + 1);
+    sbeg[m] = (uint32_t)(x - b);
+    slen[m] = (uint32_t)(y - x);
+  }
+}
+
+// ---- host orchestration ---------------------------------------------------------------------------------
+
+void plan_windows(uint64_t span, const uint64_t* gpcs, uint32_t G, std::vector<PGroup>& pg) {
+  pg.assign(G, PGroup{});
+  auto nwin = [&](uint32_t S) { return (span + (1ull << S) - 1) >> S; };
+  uint32_t smin = DS;
+  while (smin < 32 && nwin(smin) > WMAX) smin++;
+  const uint64_t w15 = nwin(DS);
+  for (uint32_t g = 0; g < G; g++) {
+    const uint64_t E = gpcs[g];
+    PGroup& p = pg[g];
+    if (smin == DS && E >= (uint64_t)DENSE * w15) {
+      p.S = DS;
+      p.W = (uint32_t)w15;
+      p.mode = PMODE_DIRECT;
+      continue;
+    }
+    // sparse: the widest window (<= 2^SMAX addresses) that still gives about HTARGET PCs per window
+    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(WMAX, (E + HTARGET - 1) / HTARGET));
+    uint32_t S = std::max(smin, DS);
+    while (S < SMAX && nwin(S + 1) >= want) S++;
+    if (S > SMAX) S = SMAX;
+    p.S = S;
+    p.W = (uint32_t)std::max<uint64_t>(1, nwin(S));
+    p.mode = PMODE_HASH;
+  }
+}
+
+static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span);
+
+void minimize_raw_begin(MinJob& J, const RawMinArgs& a) {
+  if (a.G == 0 || a.G > MAX_GROUPS_PM) fail(SYZGPU_EINVAL, "ngroups out of range (1..4096)");
+  if (a.n >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
+  if (!a.off || (a.n && !a.group)) fail(SYZGPU_EINVAL, "null pointer");
+  if (begin_once(J, a, nullptr)) return;
+  // some cover is not sorted: exact PC bounds, then once more (key parts need sorted covers)
+  if (a.key_lo) fail(SYZGPU_EINVAL, "key parts need canonical (sorted) covers");
+  Context& c = ctx();
+  uint32_t* span = c.scratch.get<uint32_t>("pm_xspan", 2);
+  uint32_t* h = c.pinned.get<uint32_t>(4);
+  h[0] = 0xFFFFFFFFu;
+  h[1] = 0;
+  SYZ_HIP(hipMemcpyAsync(span, h, 8, hipMemcpyHostToDevice, a.s));
+  uint64_t* L = c.pinned.get<uint64_t>(2) + 1;
+  SYZ_HIP(hipMemcpyAsync(L, a.off + a.n, 8, hipMemcpyDeviceToHost, a.s));
+  SYZ_HIP(hipStreamSynchronize(a.s));
+  if (*L) {
+    k_minmax<<<grid_for(*L, 256, 8192), 256, 0, a.s>>>(a.pcs, *L, span);
+    SYZ_LAUNCHED();
+  }
+  uint32_t x[2];
+  SYZ_HIP(hipMemcpyAsync(h, span, 8, hipMemcpyDeviceToHost, a.s));
+  SYZ_HIP(hipStreamSynchronize(a.s));
+  x[0] = h[0];
+  x[1] = h[1];
+  if (!begin_once(J, a, x)) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
+}
+
+// false: some PC lies outside the planned windows (an unsorted cover)
+static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span) {
+  Context& c = ctx();
+  Scratch& sc = c.scratch;
+  const size_t n = a.n;
+  const uint32_t G = a.G;
+  hipStream_t s = a.s;
+  J.begun = false;
+  J.n = n;
+  J.G = G;
+  J.group = a.group;
+  J.prog_len = a.prog_len;
+  J.gstart.ensure(G + 1);
+  J.sel_bits.ensure(n / 32 + 2);
+  J.ent_of_rank.ensure(n + 1);
+  J.rank_of_member.ensure(n + 1);
+  uint64_t* gstart = J.gstart.p;
+  uint32_t* rank_of_member = J.rank_of_member.p;
+  uint32_t* ent_of_rank = J.ent_of_rank.p;
+  uint32_t* sel_bits = J.sel_bits.p;
+  // ---- group partition (stable), sort keys, per-group PCs, span, member slices and offsets ----
+  uint32_t* members = sc.get<uint32_t>("mz_members", n + 1);
+  uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
+  uint64_t* gpcs = sc.get<uint64_t>("mz_gpcs", G + 1);
+  uint32_t* span = sc.get<uint32_t>("pm_span", 4);
+  int* err = sc.get<int>("mz_err", 2);
+  uint32_t* mlen = sc.get<uint32_t>("pm_mlen", n + 1);
+  uint32_t* sbeg = a.key_lo ? sc.get<uint32_t>("pm_sbeg", n + 1) : nullptr;
+  uint64_t* mpos = sc.get<uint64_t>("pm_mpos", n + 1);
+  SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
+  SYZ_HIP(hipMemsetAsync(gpcs, 0, (G + 1) * 8, s));
+  uint32_t* hinit = c.pinned.get<uint32_t>(16);
+  hinit[0] = 0xFFFFFFFFu;
+  hinit[1] = 0;
+  SYZ_HIP(hipMemcpyAsync(span, hinit, 8, hipMemcpyHostToDevice, s));
+  uint32_t* krange = nullptr;
+  if (a.key_lo) {
+    std::vector<uint32_t> kr(2 * (size_t)G);
+    for (uint32_t g = 0; g < G; g++) {
+      kr[2 * g] = a.key_lo[g];
+      kr[2 * g + 1] = a.key_hi[g];
+    }
+    krange = sc.get<uint32_t>("pm_krange", 2 * (size_t)G);
+    SYZ_HIP(hipMemcpyAsync(krange, kr.data(), kr.size() * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipStreamSynchronize(s));  // kr is a host temporary
+  }
+  {
+    ProfScope ps("group_partition", s, (uint64_t)n * 28);
+    group_partition_dev(a.group, a.off, n, G, gstart, members, el, err, s);
+    if (n) {
+      k_span_sums<<<grid_for(n, 256, 2048), 256, G * 8, s>>>(a.pcs, a.off, a.group, n, G, gpcs, span);
+      SYZ_LAUNCHED();
+      if (krange)
+        k_slices<<<grid_for(n, 256, 4096), 256, 0, s>>>(a.pcs, a.off, members, el, a.group, n, krange, sbeg, mlen);
+      else
+        k_mlen<<<grid_for(n, 256, 4096), 256, 0, s>>>(el, n, mlen);
+      SYZ_LAUNCHED();
+    }
+    exclusive_scan_u32(mlen, mpos, n, s);
+  }
+  uint64_t* hbuf = c.pinned.get<uint64_t>(2 * (size_t)G + 8);
+  SYZ_HIP(hipMemcpyAsync(hbuf, gstart, (G + 1) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hbuf + G + 1, gpcs, G * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hbuf + 2 * G + 1, span, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hbuf + 2 * G + 2, err, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (*reinterpret_cast<int*>(hbuf + 2 * G + 2)) fail(SYZGPU_EINVAL, "group id >= ngroups");
+  std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
+  uint32_t lo = reinterpret_cast<uint32_t*>(hbuf + 2 * G + 1)[0], hi = reinterpret_cast<uint32_t*>(hbuf + 2 * G + 1)[1];
+  if (exact_span) {
+    lo = exact_span[0];
+    hi = exact_span[1];
+  }
+  if (lo > hi) lo = hi = 0;  // no PCs at all
+  J.hstart = hstart;
+  const uint64_t spanw = (uint64_t)hi - lo + 1;
+  // ---- plan: window size per call group, blocks, chunk bound, work items ----
+  std::vector<PGroup> hpg;
+  plan_windows(spanw, hpcs.data(), G, hpg);
+  std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
+  uint64_t chunk_bound = 0, desc_bound = 0, total_pcs = 0;
+  for (uint32_t g = 0; g < G; g++) {
+    const uint64_t ng = hstart[g + 1] - hstart[g];
+    const uint32_t nb = (uint32_t)((ng + MEMB - 1) / MEMB);
+    hgblock[g + 1] = hgblock[g] + nb;
+    hbgroup.insert(hbgroup.end(), nb, g);
+    const uint64_t cb = nb + (hpcs[g] + PCAP - 1) / PCAP;  // a key part holds at most the whole group
+    chunk_bound += cb;
+    desc_bound += cb * (hpg[g].W + 1);
+    total_pcs += hpcs[g];
+  }
+  const uint32_t B = hgblock[G];
+  // work items: (call, window), the big groups (sorted by the global rounds) first, each class by
+  // mode, largest expected window first so the tail of the grid is short; a key part only its windows
+  const auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
+  std::vector<uint32_t> order(G);
+  std::iota(order.begin(), order.end(), 0u);
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+    return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W;
+  });
+  std::vector<PItem> items[2][2];  // [big][mode]
+  for (uint32_t g : order) {
+    if (!hpcs[g]) continue;
+    uint32_t w0 = 0, w1 = hpg[g].W;
+    if (a.key_lo) {
+      const uint32_t klo = std::max(a.key_lo[g], lo), khi = std::min(a.key_hi[g], hi);
+      if (klo > khi) continue;
+      w0 = (klo - lo) >> hpg[g].S;
+      w1 = std::min<uint32_t>(hpg[g].W, ((khi - lo) >> hpg[g].S) + 1);
+    }
+    auto& v = items[is_big(g) ? 1 : 0][hpg[g].mode];
+    for (uint32_t w = w0; w < w1; w++) v.push_back(PItem{g, w});
+  }
+  PGroup* dpg = sc.get<PGroup>("pm_pg", G + 1);
+  uint32_t* dgblock = sc.get<uint32_t>("pm_gblock", G + 1);
+  uint32_t* dbgroup = sc.get<uint32_t>("pm_bgroup", (size_t)B + 1);
+  size_t nitems = 0;
+  for (auto& r : items)
+    for (auto& v : r) nitems += v.size();
+  PItem* ditems = sc.get<PItem>("pm_items", nitems + 1);
+  // host staging in pinned memory: one synchronous point below covers the copies
+  const size_t stage_bytes =
+      (G + 1) * sizeof(PGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 + (nitems + 1) * sizeof(PItem);
+  uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
+  {
+    uint8_t* p = stage;
+    std::memcpy(p, hpg.data(), G * sizeof(PGroup));
+    SYZ_HIP(hipMemcpyAsync(dpg, p, G * sizeof(PGroup), hipMemcpyHostToDevice, s));
+    p += (G + 1) * sizeof(PGroup);
+    std::memcpy(p, hgblock.data(), (G + 1) * 4);
+    SYZ_HIP(hipMemcpyAsync(dgblock, p, (G + 1) * 4, hipMemcpyHostToDevice, s));
+    p += (G + 1) * 4;
+    if (B) {
+      std::memcpy(p, hbgroup.data(), (size_t)B * 4);
+      SYZ_HIP(hipMemcpyAsync(dbgroup, p, (size_t)B * 4, hipMemcpyHostToDevice, s));
+    }
+    p += ((size_t)B + 1) * 4;
+    size_t k = 0;
+    for (auto& r : items)
+      for (auto& v : r) {
+        if (!v.empty()) std::memcpy(p + k * sizeof(PItem), v.data(), v.size() * sizeof(PItem));
+        k += v.size();
+      }
+    if (nitems) SYZ_HIP(hipMemcpyAsync(ditems, p, nitems * sizeof(PItem), hipMemcpyHostToDevice, s));
+  }
+  // ---- blocks -> chunks ----
+  uint32_t* nsub = sc.get<uint32_t>("pm_nsub", (size_t)B + 1);
+  uint64_t* cstart = sc.get<uint64_t>("pm_cstart", (size_t)B + 1);
+  PChunk* chunks = sc.get<PChunk>("pm_chunks", chunk_bound + 1);
+  uint64_t* gchunk = sc.get<uint64_t>("pm_gchunk", G + 1);
+  uint64_t* gdesc = sc.get<uint64_t>("pm_gdesc", G + 1);
+  uint16_t* desc = sc.get<uint16_t>("pm_desc", desc_bound + 1);
+  uint32_t* elems = sc.get<uint32_t>("pm_elems", total_pcs + 1);
+  if (B) {
+    k_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, gstart, mpos, nsub);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(nsub, cstart, B, s);
+  if (B) {
+    k_chunks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, gstart, mpos, cstart, chunks);
+    SYZ_LAUNCHED();
+  }
+  k_gchunk<<<1, 1024, 0, s>>>(dgblock, G, cstart, dpg, gchunk, gdesc);
+  SYZ_LAUNCHED();
+  // ---- P on its own stream, beside the Go sort ----
+  if (!c.part) {
+    SYZ_HIP(hipStreamCreateWithFlags(&c.part, hipStreamNonBlocking));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
+  }
+  SYZ_HIP(hipEventRecord(c.ev_part0, s));
+  SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
+  if (chunk_bound) {
+    ProfScope ps("part", c.part, total_pcs * 8 + (uint64_t)n * 24);
+    const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, 512);
+    k_part<<<grid, PP_BLOCK, 0, c.part>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc,
+                                          lo, elems, desc, err);
+    SYZ_LAUNCHED();
+  }
+  SYZ_HIP(hipEventRecord(c.ev_part1, c.part));
+  // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
+  uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
+  SYZ_HIP(hipMemsetAsync(sel_bits, 0, (n / 32 + 2) * 4, s));
+  const size_t nd_small = items[0][PMODE_DIRECT].size(), nh_small = items[0][PMODE_HASH].size();
+  const size_t nd_big = items[1][PMODE_DIRECT].size(), nh_big = items[1][PMODE_HASH].size();
+  const size_t off_small_d = 0, off_small_h = nd_small, off_big_d = nd_small + nh_small,
+               off_big_h = off_big_d + nd_big;
+  auto run_m = [&](hipStream_t q, size_t first_d, size_t nd, size_t first_h, size_t nh, const char* tag) {
+    SYZ_HIP(hipStreamWaitEvent(q, c.ev_part1, 0));
+    ProfScope ps(tag, q, 0);
+    if (nd) {
+      k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + first_d, chunks, gchunk, gdesc, dpg, desc, elems,
+                                                  rank_of_member, gstart, sel_bits);
+      SYZ_LAUNCHED();
+    }
+    if (nh) {
+      k_pmin_hash<<<(unsigned)nh, HM_BLOCK, 0, q>>>(ditems + first_h, chunks, gchunk, gdesc, dpg, desc, elems,
+                                                    rank_of_member, gstart, sel_bits);
+      SYZ_LAUNCHED();
+    }
+  };
+  if (!J.plan || J.plan_key != hstart) {
+    J.plan = std::make_shared<GosortPlan>();
+    gosort_plan(*J.plan, hstart, G, s);
+    J.plan_key = hstart;
+  }
+  GosortPlan& P = *J.plan;
+  rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
+  auto small_done = [&](hipStream_t q) {
+    if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);
+    run_m(q, off_small_d, nd_small, off_small_h, nh_small, "pmin_small");
+  };
+  auto big_done = [&](hipStream_t q) {
+    if (P.nbig) ranks_big(el, perm, P, members, rank_of_member, ent_of_rank, q);
+    run_m(q, off_big_d, nd_big, off_big_h, nh_big, "pmin");
+  };
+  if (n) {
+    gosort_run(el, perm, n, P, s, small_done, big_done);
+  } else {
+    small_done(s);
+    big_done(s);
+  }
+  int* herr = c.pinned.get<int>(4);
+  SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  J.stats_total_pcs = total_pcs;
+  J.stats_items_direct = nd_small + nd_big;
+  J.stats_items_hash = nh_small + nh_big;
+  if (herr[0] & 1) {
+    if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
+    return false;
+  }
+  J.begun = true;
+  return true;
+}
+
+__global__ void k_job_xchg(uint32_t* sel_bits, const uint64_t* gstart, const uint32_t* groups, const uint64_t* boff,
+                           uint8_t* buf, int import) {
+  const uint32_t g = groups[blockIdx.y];
+  const uint64_t gb = gstart[g], ng = gstart[g + 1] - gb, o = boff[blockIdx.y];
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < ng; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t R = gb + r;
+    if (import) {
+      if (buf[o + r]) atomicOr(&sel_bits[R >> 5], 1u << (R & 31));
+    } else {
+      buf[o + r] = (uint8_t)((sel_bits[R >> 5] >> (R & 31)) & 1u);
+    }
+  }
+}
+
+void minimize_raw_xchg(MinJob& J, const uint32_t* groups, const uint64_t* offsets, uint32_t ng, uint8_t* buf,
+                       int import, hipStream_t s) {
+  if (!J.begun) fail(SYZGPU_EINVAL, "minimize job: begin first");
+  if (!ng) return;
+  if (!groups || !offsets || !buf) fail(SYZGPU_EINVAL, "null pointer");
+  uint64_t maxn = 0;
+  for (uint32_t j = 0; j < ng; j++) {
+    if (groups[j] >= J.G) fail(SYZGPU_EINVAL, "group id >= ngroups");
+    maxn = std::max<uint64_t>(maxn, J.hstart[groups[j] + 1] - J.hstart[groups[j]]);
+  }
+  std::vector<uint64_t> key(groups, groups + ng);
+  key.insert(key.end(), offsets, offsets + ng);
+  if (key != J.xkey) {  // the exchange list is the same every step: uploaded once
+    J.xg.ensure(ng);
+    J.xo.ensure(ng);
+    SYZ_HIP(hipMemcpyAsync(J.xg.p, groups, ng * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(J.xo.p, offsets, ng * 8, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    J.xkey = key;
+  }
+  const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>(1, (maxn + 1023) / 1024), 1024);
+  k_job_xchg<<<dim3(gx, ng), 256, 0, s>>>(J.sel_bits.p, J.gstart.p, J.xg.p, J.xo.p, buf, import);
+  SYZ_LAUNCHED();
+}
+
+__global__ __launch_bounds__(256) void k_sel_flags(const uint32_t* sel_bits, const uint32_t* ent_of_rank, size_t n,
+                                                   const uint16_t* prog_len, const uint32_t* group,
+                                                   const uint8_t* count_hist, int32_t C, uint8_t* selected,
+                                                   int64_t* hist, int* err) {
+  extern __shared__ unsigned long long lh[];
+  const bool do_hist = hist != nullptr;
+  if (do_hist) {
+    for (int32_t i = threadIdx.x; i <= C; i += blockDim.x) lh[i] = 0;
+    __syncthreads();
+  }
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t e = ent_of_rank[r];
+    const uint32_t s = (sel_bits[r >> 5] >> (r & 31)) & 1u;
+    if (selected) selected[e] = (uint8_t)s;
+    if (do_hist && s && (!count_hist || count_hist[group[e]])) {
+      const uint32_t L = prog_len[e];
+      if ((int32_t)L > C)
+        atomicOr(err, 2);
+      else
+        atomicAdd(&lh[L], 1ull);
+    }
+  }
+  if (do_hist) {
+    __syncthreads();
+    for (int32_t i = threadIdx.x; i <= C; i += blockDim.x)
+      if (lh[i]) atomicAdd((unsigned long long*)&hist[i], lh[i]);
+  }
+}
+
+void sel_compact_dev(const uint32_t* sel_bits, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
+                     int64_t* out_idx, uint64_t* group_out_off, hipStream_t s) {
+  Scratch& sc = ctx().scratch;
+  const size_t nw = (n + 31) / 32;
+  uint32_t* wcnt = sc.get<uint32_t>("pm_wcnt", nw + 1);
+  uint64_t* wpos = sc.get<uint64_t>("pm_wpos", nw + 2);
+  if (nw) {
+    k_sel_wpop<<<grid_for(nw, 256, 4096), 256, 0, s>>>(sel_bits, nw, wcnt);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(wcnt, wpos, nw, s);
+  if (out_idx && n) {
+    k_sel_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(sel_bits, wpos, ent_of_rank, n, out_idx);
+    SYZ_LAUNCHED();
+  }
+  if (group_out_off) {
+    k_sel_goff<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(sel_bits, wpos, gstart, G, n, group_out_off);
+    SYZ_LAUNCHED();
+  }
+}
+
+void minimize_raw_end(MinJob& J, const RawEndArgs& e) {
+  if (!J.begun) fail(SYZGPU_EINVAL, "minimize job: begin first");
+  if (e.len_hist && (e.C <= 0 || !J.prog_len)) fail(SYZGPU_EINVAL, "len_hist needs prog_len and C > 0");
+  Context& c = ctx();
+  Scratch& sc = c.scratch;
+  const size_t n = J.n;
+  const uint32_t G = J.G;
+  hipStream_t s = e.s;
+  int* err = sc.get<int>("mz_err", 2);
+  SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
+  const uint8_t* dcount = nullptr;
+  if (e.count_hist) {
+    J.count_hist.ensure(G);
+    SYZ_HIP(hipMemcpyAsync(J.count_hist.p, e.count_hist, G, hipMemcpyHostToDevice, s));
+    dcount = J.count_hist.p;
+  }
+  ProfScope ps("select_out", s, (uint64_t)n * 8);
+  if (e.len_hist) SYZ_HIP(hipMemsetAsync(e.len_hist, 0, (size_t)(e.C + 1) * 8, s));
+  if (n) {
+    k_sel_flags<<<grid_for(n, 256, 512), 256, e.len_hist ? (size_t)(e.C + 1) * 8 : 0, s>>>(
+        J.sel_bits.p, J.ent_of_rank.p, n, e.len_hist ? J.prog_len : nullptr, J.group, dcount, e.C, e.selected,
+        e.len_hist, err);
+    SYZ_LAUNCHED();
+  }
+  if (e.out_idx || e.group_out_off) sel_compact_dev(J.sel_bits.p, J.ent_of_rank.p, J.gstart.p, n, G, e.out_idx, e.group_out_off, s);
+  if (e.len_hist) {  // len(p.Calls) > C is Go's index-out-of-range panic (prio.go:148)
+    int* herr = c.pinned.get<int>(4);
+    SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (herr[0] & 2) fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
+  }
+}
+
+// host copies of the group-major kept list (the syzgpu_minimize_grouped outputs)
+void minimize_raw_fetch(MinJob& J, int64_t* out_idx, uint64_t* group_out_off) {
+  if (!J.begun) fail(SYZGPU_EINVAL, "no matching minimize result");
+  Context& c = ctx();
+  hipStream_t s = c.stream;
+  int64_t* dout = c.scratch.get<int64_t>("mz_out", J.n + 1);
+  uint64_t* dgoff = c.scratch.get<uint64_t>("mz_goff", J.G + 1);
+  RawEndArgs e{};
+  e.out_idx = dout;
+  e.group_out_off = dgoff;
+  e.s = s;
+  minimize_raw_end(J, e);
+  SYZ_HIP(hipMemcpyAsync(group_out_off, dgoff, (J.G + 1) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  const uint64_t m = group_out_off[J.G];
+  if (m && out_idx) SYZ_HIP(hipMemcpyAsync(out_idx, dout, m * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+}
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" {
+
+int syzgpu_mz_create(syzgpu_mz** out) {
+  SYZ_API_BODY({
+    if (!out) fail(SYZGPU_EINVAL, "null pointer");
+    *out = reinterpret_cast<syzgpu_mz*>(new MinJob());
+  })
+}
+
+int syzgpu_mz_destroy(syzgpu_mz* job) {
+  SYZ_API_BODY({
+    if (job) {
+      MinJob* J = reinterpret_cast<MinJob*>(job);
+      { std::lock_guard<std::recursive_mutex> hl_(J->mu); }
+      delete J;
+    }
+  })
+}
+
+int syzgpu_mz_begin_dev(syzgpu_mz* job, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                        const uint16_t* prog_len, size_t n, uint32_t ngroups, const uint32_t* key_lo,
+                        const uint32_t* key_hi, void* stream) {
+  SYZ_API_BODY({
+    if (!job) fail(SYZGPU_EINVAL, "null job");
+    if ((key_lo == nullptr) != (key_hi == nullptr)) fail(SYZGPU_EINVAL, "key_lo and key_hi go together");
+    MinJob& J = *reinterpret_cast<MinJob*>(job);
+    std::lock_guard<std::recursive_mutex> hl_(J.mu);
+    RawMinArgs a{pcs, off, group, prog_len, n, ngroups};
+    a.key_lo = key_lo;
+    a.key_hi = key_hi;
+    a.s = (hipStream_t)stream;
+    minimize_raw_begin(J, a);
+  })
+}
+
+int syzgpu_mz_export_sel_dev(syzgpu_mz* job, const uint32_t* groups, const uint64_t* offsets, uint32_t ngroups,
+                             uint8_t* buf, void* stream) {
+  SYZ_API_BODY({
+    if (!job) fail(SYZGPU_EINVAL, "null job");
+    MinJob& J = *reinterpret_cast<MinJob*>(job);
+    std::lock_guard<std::recursive_mutex> hl_(J.mu);
+    minimize_raw_xchg(J, groups, offsets, ngroups, buf, 0, (hipStream_t)stream);
+  })
+}
+
+int syzgpu_mz_import_sel_dev(syzgpu_mz* job, const uint32_t* groups, const uint64_t* offsets, uint32_t ngroups,
+                             const uint8_t* buf, void* stream) {
+  SYZ_API_BODY({
+    if (!job) fail(SYZGPU_EINVAL, "null job");
+    MinJob& J = *reinterpret_cast<MinJob*>(job);
+    std::lock_guard<std::recursive_mutex> hl_(J.mu);
+    minimize_raw_xchg(J, groups, offsets, ngroups, const_cast<uint8_t*>(buf), 1, (hipStream_t)stream);
+  })
+}
+
+int syzgpu_mz_end_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist, uint8_t* selected, int64_t* len_hist,
+                      int64_t* out_idx, uint64_t* group_out_off, void* stream) {
+  SYZ_API_BODY({
+    if (!job) fail(SYZGPU_EINVAL, "null job");
+    MinJob& J = *reinterpret_cast<MinJob*>(job);
+    std::lock_guard<std::recursive_mutex> hl_(J.mu);
+    RawEndArgs e;
+    e.C = C;
+    e.count_hist = count_hist;
+    e.selected = selected;
+    e.len_hist = len_hist;
+    e.out_idx = out_idx;
+    e.group_out_off = group_out_off;
+    e.s = (hipStream_t)stream;
+    minimize_raw_end(J, e);
+  })
+}
+
+int syzgpu_mz_fetch(syzgpu_mz* job, int64_t* out_idx, uint64_t* group_out_off) {
+  SYZ_API_BODY({
+    if (!job || !group_out_off) fail(SYZGPU_EINVAL, "null pointer");
+    MinJob& J = *reinterpret_cast<MinJob*>(job);
+    std::lock_guard<std::recursive_mutex> hl_(J.mu);
+    minimize_raw_fetch(J, out_idx, group_out_off);
+  })
+}
+
+int syzgpu_mz_info(syzgpu_mz* job, uint64_t* info, size_t cap) {
+  SYZ_API_BODY({
+    if (!job || !info) fail(SYZGPU_EINVAL, "null pointer");
+    MinJob& J = *reinterpret_cast<MinJob*>(job);
+    std::lock_guard<std::recursive_mutex> hl_(J.mu);
+    const uint64_t v[5] = {J.n, J.G, J.stats_total_pcs, J.stats_items_direct, J.stats_items_hash};
+    for (size_t i = 0; i < cap && i < 5; i++) info[i] = v[i];
+  })
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// The raw-cover Minimize pipeline (panels.hip) and the pieces of minimize.hip it shares.
+#pragma once
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "store.hpp"
+
+namespace syz {
+
+constexpr uint32_t MAX_GROUPS_PM = 4096;
+
+enum { PMODE_DIRECT = 0, PMODE_HASH = 1 };
+
+struct PGroup {          // per call group: window bits, windows, table kind
+  uint32_t S, W, mode, pad;
+};
+struct PItem {           // one (call group, window) min-rank table
+  uint32_t g, w;
+};
+struct PChunk {          // <= PCAP consecutive PCs of one 64-member block, in member order
+  uint64_t elem;         // first element (= position in the group-major concatenation of covers)
+  uint32_t len, mb;      // PCs; first member of the block
+  uint32_t nmem, sub;    // members in the block; offset of this chunk inside the block's PCs
+  uint32_t g, pad;
+};
+
+struct RawMinArgs {
+  const uint32_t* pcs;
+  const uint64_t* off;
+  const uint32_t* group;
+  const uint16_t* prog_len;  // may be null (no histogram then)
+  size_t n;
+  uint32_t G;
+  const uint32_t* key_lo = nullptr;  // host, per group: this rank's PC range [key_lo, key_hi] of it
+  const uint32_t* key_hi = nullptr;  // (null: whole groups)
+  hipStream_t s = nullptr;
+};
+struct RawEndArgs {
+  int32_t C = 0;
+  const uint8_t* count_hist = nullptr;  // host, per group: counted in len_hist (null: all)
+  uint8_t* selected = nullptr;          // device, n bytes in entry order
+  int64_t* len_hist = nullptr;          // device, C+1
+  int64_t* out_idx = nullptr;           // device, kept entries group-major in selection order
+  uint64_t* group_out_off = nullptr;    // device, G+1
+  hipStream_t s = nullptr;
+};
+
+// One minimizeCorpus job (the raw path): its selection lives here between begin and end, so a
+// multi-GPU step can exchange the selection of split call groups in between, and concurrent callers
+// with their own jobs never see each other's state.
+struct MinJob {
+  std::recursive_mutex mu;
+  size_t n = 0;
+  uint32_t G = 0;
+  bool begun = false;
+  const uint32_t* group = nullptr;     // caller's device buffers (valid from begin to end)
+  const uint16_t* prog_len = nullptr;
+  Grow<uint64_t> gstart;
+  Grow<uint32_t> sel_bits, ent_of_rank, rank_of_member, xg;
+  Grow<uint64_t> xo;
+  Grow<uint8_t> count_hist;
+  std::vector<uint64_t> hstart, xkey;
+  std::shared_ptr<GosortPlan> plan;  // Go-sort plan of the last layout (keeps its rounds hint)
+  std::vector<uint64_t> plan_key;
+  uint64_t stats_total_pcs = 0;
+  size_t stats_items_direct = 0, stats_items_hash = 0;
+};
+
+void minimize_raw_begin(MinJob& J, const RawMinArgs& a);
+void minimize_raw_xchg(MinJob& J, const uint32_t* groups, const uint64_t* offsets, uint32_t ng, uint8_t* buf,
+                       int import, hipStream_t s);
+void minimize_raw_end(MinJob& J, const RawEndArgs& e);
+void minimize_raw_fetch(MinJob& J, int64_t* out_idx, uint64_t* group_out_off);
+void plan_windows(uint64_t span, const uint64_t* gpcs, uint32_t G, std::vector<PGroup>& pg);
+// group-major kept list (device) from a rank bitmap
+void sel_compact_dev(const uint32_t* sel_bits, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
+                     int64_t* out_idx, uint64_t* group_out_off, hipStream_t s);
+
+// minimize.hip
+void group_partition_dev(const uint32_t* group, const uint64_t* off, size_t n, uint32_t G, uint64_t* gstart,
+                         uint32_t* members, uint64_t* el, int* err, hipStream_t s);
+void rank_init_dev(const uint32_t* members, size_t n, uint32_t* rank_of_member, uint32_t* ent_of_rank, hipStream_t s);
+void ranks_packs(const uint64_t* el, const uint32_t* perm, const GosortPlan& P, const uint32_t* members,
+                 uint32_t* rank_of_member, uint32_t* ent_of_rank, hipStream_t q);
+void ranks_big(const uint64_t* el, const uint32_t* perm, const GosortPlan& P, const uint32_t* members,
+               uint32_t* rank_of_member, uint32_t* ent_of_rank, hipStream_t q);
+
+}  // namespace syz

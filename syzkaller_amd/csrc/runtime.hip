@@ -1,5 +1,7 @@
 // Context, error state, scratch memory, profiling and the device-wide scans.
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -52,10 +54,28 @@ Pinned::~Pinned() {
   if (p_) (void)hipHostFree(p_);
 }
 
-static std::mutex g_ctx_mu;
-static Context* g_ctx = nullptr;
+// ---- lanes -------------------------------------------------------------------------------------------
+static std::mutex g_mu;                 // device choice and the lane pool
+static std::condition_variable g_cv;
+static int g_device = -1;
+static uint64_t g_gen = 1;              // bumped by syzgpu_shutdown: lanes of older generations are gone
+static std::vector<Context*> g_lanes;
+static std::vector<bool> g_busy;
+static thread_local Context* t_lane = nullptr;  // held for the current API call
+static thread_local int t_depth = 0;
+static thread_local Context* t_last = nullptr;   // affinity: the lane this thread used last
+static thread_local uint64_t t_last_gen = 0;
 
-static void init_device(int dev) {
+static size_t max_lanes() {
+  static const size_t v = [] {
+    const char* e = getenv("SYZGPU_LANES");
+    const long x = e ? atol(e) : 8;
+    return (size_t)(x < 1 ? 1 : x > 64 ? 64 : x);
+  }();
+  return v;
+}
+
+static void pick_device(int dev) {  // g_mu held
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n <= 0) fail(SYZGPU_ENODEV, "no HIP device available");
@@ -64,18 +84,85 @@ static void init_device(int dev) {
   SYZ_HIP(hipGetDeviceProperties(&prop, dev));
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     fail(SYZGPU_ENODEV, std::string("libsyzgpu is built for gfx950 only, found ") + prop.gcnArchName);
-  SYZ_HIP(hipSetDevice(dev));
-  Context* c = new Context();
-  c->device = dev;
+  g_device = dev;
+}
+
+static Context* new_lane() {  // g_mu held
+  SYZ_HIP(hipSetDevice(g_device));
+  std::unique_ptr<Context> c(new Context());
+  c->device = g_device;
+  c->gen = g_gen;
   SYZ_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  g_ctx = c;
+  g_lanes.push_back(c.get());
+  g_busy.push_back(false);
+  return c.release();
+}
+
+LaneGuard::LaneGuard() {
+  if (t_depth++ > 0) return;
+  std::unique_lock<std::mutex> lk(g_mu);
+  try {
+    if (g_device < 0) pick_device(0);
+    for (;;) {
+      size_t pick = g_lanes.size();
+      for (size_t i = 0; i < g_lanes.size(); i++)
+        if (!g_busy[i] && g_lanes[i] == t_last && t_last_gen == g_gen) pick = i;
+      if (pick == g_lanes.size())
+        for (size_t i = 0; i < g_lanes.size(); i++)
+          if (!g_busy[i]) {
+            pick = i;
+            break;
+          }
+      if (pick == g_lanes.size() && g_lanes.size() < max_lanes()) {
+        new_lane();
+        pick = g_lanes.size() - 1;
+      }
+      if (pick < g_lanes.size()) {
+        g_busy[pick] = true;
+        t_lane = g_lanes[pick];
+        t_last = t_lane;
+        t_last_gen = g_gen;
+        break;
+      }
+      g_cv.wait(lk);
+    }
+  } catch (...) {
+    t_depth--;
+    throw;
+  }
+  SYZ_HIP(hipSetDevice(t_lane->device));
+}
+
+LaneGuard::~LaneGuard() {
+  if (--t_depth > 0) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (size_t i = 0; i < g_lanes.size(); i++)
+    if (g_lanes[i] == t_lane) g_busy[i] = false;
+  t_lane = nullptr;
+  g_cv.notify_one();
 }
 
 Context& ctx() {
-  std::lock_guard<std::mutex> lk(g_ctx_mu);
-  if (!g_ctx) init_device(0);
-  SYZ_HIP(hipSetDevice(g_ctx->device));
-  return *g_ctx;
+  if (!t_lane) fail(SYZGPU_EINTERNAL, "no lane held (library entry point without SYZ_API_BODY)");
+  return *t_lane;
+}
+
+static void free_lane(Context* c) {
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  c->own_job.reset();
+  c->scratch.release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->part) (void)hipStreamDestroy(c->part);
+  if (c->cap) (void)hipStreamDestroy(c->cap);
+  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_part0, c->ev_part1})
+    if (e) (void)hipEventDestroy(e);
+  for (auto& row : c->gl_exec)
+    for (auto& g : row)
+      if (g) (void)hipGraphExecDestroy(g);
+  if (c->gr_host) (void)hipHostFree(c->gr_host);
+  delete c;
 }
 
 Prof& prof() {
@@ -83,12 +170,15 @@ Prof& prof() {
   return p;
 }
 
+static std::mutex g_prof_mu;
+
 void Prof::reset() {
   recs.clear();
   used = 0;
 }
 
 size_t Prof::begin(const char* name, hipStream_t s, uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
   if (used + 2 > pool.size()) {
     for (int i = 0; i < 64; i++) {
       hipEvent_t e;
@@ -103,7 +193,10 @@ size_t Prof::begin(const char* name, hipStream_t s, uint64_t bytes) {
   return recs.size() - 1;
 }
 
-void Prof::end(size_t rec, hipStream_t s) { SYZ_HIP(hipEventRecord(recs[rec].b, s)); }
+void Prof::end(size_t rec, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  SYZ_HIP(hipEventRecord(recs[rec].b, s));
+}
 
 // ---- device-wide exclusive scan: reduce tiles, scan tile sums (recursively), add back ----------
 constexpr int SCAN_BLOCK = 256;
@@ -190,12 +283,12 @@ extern "C" {
 
 int syzgpu_init(int device) {
   try {
-    std::lock_guard<std::mutex> lk(g_ctx_mu);
-    if (g_ctx) {
-      if (g_ctx->device == device) return SYZGPU_OK;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_device >= 0) {
+      if (g_device == device) return SYZGPU_OK;
       fail(SYZGPU_EINVAL, "already initialised on another device");
     }
-    init_device(device);
+    pick_device(device);
     return SYZGPU_OK;
   } catch (const Error& e) {
     set_last_error(e.msg);
@@ -203,14 +296,15 @@ int syzgpu_init(int device) {
   }
 }
 
+// Frees every lane; no call may be in flight (handles created before stay valid: they own their
+// device memory).
 int syzgpu_shutdown(void) {
-  std::lock_guard<std::mutex> lk(g_ctx_mu);
-  if (g_ctx) {
-    g_ctx->scratch.release();
-    if (g_ctx->stream) (void)hipStreamDestroy(g_ctx->stream);
-    delete g_ctx;
-    g_ctx = nullptr;
-  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (Context* c : g_lanes) free_lane(c);
+  g_lanes.clear();
+  g_busy.clear();
+  g_device = -1;
+  g_gen++;
   return SYZGPU_OK;
 }
 

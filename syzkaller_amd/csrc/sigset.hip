@@ -24,6 +24,7 @@ constexpr int SG_BLOCK = 256;
 constexpr uint32_t SG_PENDING = 0, SG_NEW = 1, SG_FOUND = 2;
 
 struct SigSet {
+  std::recursive_mutex mu;  // one call on a set at a time
   uint64_t cap = 0, mask = 0, live = 0, used = 0;  // used: slots ever claimed (live + tombstones)
   uint32_t round = 1;                               // the next insert batch
   uint64_t* tag = nullptr;   // 0 = empty, else (round << 32 | item + 1) of the claim
@@ -325,6 +326,8 @@ int syzgpu_sigset_destroy(syzgpu_sigset* set) {
 int syzgpu_sigset_clear(syzgpu_sigset* set, void* stream) {
   SYZ_API_BODY({
     if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
+    if (!set) fail(SYZGPU_EINVAL, "null set");
     SigSet& S = *reinterpret_cast<SigSet*>(set);
     hipStream_t s = (hipStream_t)stream;
     SYZ_HIP(hipMemsetAsync(S.tag, 0, S.cap * 8, s));
@@ -337,6 +340,8 @@ int syzgpu_sigset_clear(syzgpu_sigset* set, void* stream) {
 
 int syzgpu_sigset_size(const syzgpu_sigset* set, uint64_t* n) {
   SYZ_API_BODY({
+    if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
     if (!set || !n) fail(SYZGPU_EINVAL, "null pointer");
     *n = reinterpret_cast<const SigSet*>(set)->live;
   })
@@ -345,6 +350,8 @@ int syzgpu_sigset_size(const syzgpu_sigset* set, uint64_t* n) {
 int syzgpu_sigset_insert_dev(syzgpu_sigset* set, const uint8_t* sigs, const uint8_t* mask, size_t n, uint64_t seq,
                              uint8_t* added, uint64_t* nadded, void* stream) {
   SYZ_API_BODY({
+    if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
     if (!set || (n && !sigs)) fail(SYZGPU_EINVAL, "null pointer");
     sig_check_ptr(sigs);
     const uint64_t a = sigset_insert(*reinterpret_cast<SigSet*>(set), reinterpret_cast<const uint32_t*>(sigs), mask,
@@ -356,6 +363,8 @@ int syzgpu_sigset_insert_dev(syzgpu_sigset* set, const uint8_t* sigs, const uint
 int syzgpu_sigset_lookup_dev(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8_t* found, uint64_t* seq,
                              void* stream) {
   SYZ_API_BODY({
+    if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
     if (!set || (n && !sigs)) fail(SYZGPU_EINVAL, "null pointer");
     sig_check_ptr(sigs);
     sigset_find(*reinterpret_cast<SigSet*>(set), reinterpret_cast<const uint32_t*>(sigs), n, 0, found, seq,
@@ -366,6 +375,8 @@ int syzgpu_sigset_lookup_dev(syzgpu_sigset* set, const uint8_t* sigs, size_t n, 
 int syzgpu_sigset_erase_dev(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8_t* erased, uint64_t* nerased,
                             void* stream) {
   SYZ_API_BODY({
+    if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
     if (!set || (n && !sigs)) fail(SYZGPU_EINVAL, "null pointer");
     sig_check_ptr(sigs);
     const uint64_t e = sigset_find(*reinterpret_cast<SigSet*>(set), reinterpret_cast<const uint32_t*>(sigs), n, 1,
@@ -378,6 +389,8 @@ int syzgpu_sigset_erase_dev(syzgpu_sigset* set, const uint8_t* sigs, size_t n, u
 int syzgpu_sigset_insert(syzgpu_sigset* set, const uint8_t* sigs, const uint8_t* mask, size_t n, uint64_t seq,
                          uint8_t* added, uint64_t* nadded) {
   SYZ_API_BODY({
+    if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
     if (!set || (n && !sigs)) fail(SYZGPU_EINVAL, "null pointer");
     hipStream_t s = C_.stream;
     uint32_t* d = C_.scratch.get<uint32_t>("sgh_sigs", 5 * n + 5);
@@ -394,6 +407,8 @@ int syzgpu_sigset_insert(syzgpu_sigset* set, const uint8_t* sigs, const uint8_t*
 
 int syzgpu_sigset_lookup(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8_t* found, uint64_t* seq) {
   SYZ_API_BODY({
+    if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
     if (!set || (n && !sigs)) fail(SYZGPU_EINVAL, "null pointer");
     hipStream_t s = C_.stream;
     uint32_t* d = C_.scratch.get<uint32_t>("sgh_sigs", 5 * n + 5);
@@ -409,6 +424,8 @@ int syzgpu_sigset_lookup(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint
 
 int syzgpu_sigset_erase(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8_t* erased, uint64_t* nerased) {
   SYZ_API_BODY({
+    if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
     if (!set || (n && !sigs)) fail(SYZGPU_EINVAL, "null pointer");
     hipStream_t s = C_.stream;
     uint32_t* d = C_.scratch.get<uint32_t>("sgh_sigs", 5 * n + 5);
@@ -423,6 +440,8 @@ int syzgpu_sigset_erase(syzgpu_sigset* set, const uint8_t* sigs, size_t n, uint8
 
 int syzgpu_sigset_export(syzgpu_sigset* set, uint8_t* sigs, uint64_t* seq, size_t cap, size_t* out_n) {
   SYZ_API_BODY({
+    if (!set) fail(SYZGPU_EINVAL, "null set");
+    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<SigSet*>(const_cast<syzgpu_sigset*>(set))->mu);
     if (!set || !out_n) fail(SYZGPU_EINVAL, "null pointer");
     SigSet& S = *reinterpret_cast<SigSet*>(set);
     hipStream_t s = C_.stream;

@@ -34,6 +34,42 @@ struct VecWork {
 struct CoverStats;
 void corpus_stats_free(CoverStats*);
 
+// Winning ranks of a window table (LDS or global) -> set bits of sel_bits (global rank bitmap).
+// Ranks of call g lie in [gstart[g], gstart[g+1]). Winners are mostly early ranks (the longest covers
+// come first in Go-sort order), so the first BM_WORDS*32 ranks of the call are deduplicated through
+// an LDS bitmap (one bit-OR per kept input instead of one per id) and the rarer later ones go straight
+// to sel_bits: one pass over the table whatever the call's size.
+template <bool ATOMIC_READ = false, uint32_t BMW = BM_WORDS>
+__device__ __forceinline__ void emit_winners(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
+                                             uint32_t* bm, uint32_t* sel_bits) {
+  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BMW * 32, ng);
+  const uint32_t words = (span + 31) / 32;
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
+    const uint32_t r = ATOMIC_READ ? __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tab[i];
+    if (r == RANK_NONE) continue;
+    const uint64_t lr = (uint64_t)r - gbase;
+    if (lr < span)
+      atomicOr(&bm[lr >> 5], 1u << (lr & 31));
+    else
+      atomicOr(&sel_bits[r >> 5], 1u << (r & 31));
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
+    const uint32_t wv = bm[i];
+    if (!wv) continue;
+    const uint64_t gb = gbase + 32ull * i;
+    const uint32_t sh = (uint32_t)(gb & 31);
+    atomicOr(&sel_bits[gb >> 5], wv << sh);
+    if (sh) {
+      const uint32_t hi = wv >> (32 - sh);
+      if (hi) atomicOr(&sel_bits[(gb >> 5) + 1], hi);
+    }
+  }
+  __syncthreads();
+}
+
 template <class T>
 struct DevArr {
   T* p = nullptr;
@@ -50,7 +86,28 @@ struct DevArr {
   }
 };
 
+template <class T>
+struct Grow {  // grow-only device buffer owned by a handle
+  T* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t count) {
+    if (count <= cap && p) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = count + count / 8 + 16;
+    SYZ_HIP(hipMalloc(&p, want * sizeof(T)));
+    cap = want;
+  }
+  ~Grow() {
+    if (p) (void)hipFree(p);
+  }
+};
+
 struct Corpus {
+  std::recursive_mutex mu;  // one call on a store at a time (mgr.mu serialises them in the reference)
+  Grow<uint32_t> sel_bits, rom, eor;  // the selection between minimize_begin and _end
+  bool begun = false;
   size_t n = 0;
   uint32_t G = 0;
   uint64_t total_pcs = 0, total_ids = 0, total_vecs = 0;

@@ -1,5 +1,8 @@
 """Multi-GPU layout of minimizeCorpus (syz-manager/manager.go:507-553) — one process per GPU.
 
+Groups too heavy for one rank are split into key parts: PC-value ranges (split_bounds), each holder
+keeping the PCs of its range only (MinimizeJob.begin key_lo/key_hi).
+
 Every call group's Minimize is independent of every other group (manager.go:523-527 runs them one by
 one), so the corpus is sharded BY CALL GROUP: no data-path collective is needed for Minimize. The one
 real exchange is CalculatePriorities (prio.go:29-38) over ALL kept programs: it reads only
@@ -85,6 +88,19 @@ class KeyPlan:
                 count[g] = 1 if r[0] == rank else 0
         return part, nparts, count
 
+    def key_ranges(self, rank, bounds):
+        """(key_lo u32[G], key_hi u32[G]) of this rank for MinimizeJob.begin: [0, 2^32-1] for groups held
+        whole (or not held), part j of a split group g = [bounds[g][j], bounds[g][j+1] - 1]."""
+        lo = np.zeros(self.ngroups, np.uint32)
+        hi = np.full(self.ngroups, 0xFFFFFFFF, np.uint32)
+        for g, r in enumerate(self.ranks):
+            if len(r) > 1 and rank in r:
+                j = r.index(rank)
+                b = bounds[g]
+                lo[g] = np.uint32(b[j])
+                hi[g] = np.uint32(b[j + 1] - 1)
+        return lo, hi
+
     def split_groups(self):
         """(groups, byte offsets, total bytes) of the selection exchange: every split group, one byte
         per entry, in group order — the same buffer layout on every rank."""
@@ -137,6 +153,35 @@ def plan_parts(entries, pcs, nranks, max_rounds=24):
             break
         k, ranks, cost = k2, ranks2, cost2
     return KeyPlan(ranks, cost, entries)
+
+
+def split_bounds(plan, corp, rank, sample_every=16):
+    """PC-value boundaries of every split group this rank holds: bounds[g] = k+1 ascending values in
+    [0, 2^32] (b[0] = 0, b[k] = 2^32) at equal-count quantiles of the group's PCs, so the parts hold
+    about the same number of PCs. A pure function of the group's covers, which every holder has
+    whole, so all holders compute the same boundaries. corp: the rank's local corpus (global group ids)."""
+    bounds = {}
+    grp = np.asarray(corp.group, np.int64)
+    off = np.asarray(corp.off, np.int64)
+    for g, r in enumerate(plan.ranks):
+        if len(r) <= 1 or rank not in r:
+            continue
+        k = len(r)
+        ent = np.nonzero(grp == g)[0][::sample_every]
+        if ent.size:
+            sample = np.concatenate([corp.pcs[off[e]:off[e + 1]] for e in ent]).astype(np.uint64)
+        else:
+            sample = np.zeros(0, np.uint64)
+        b = [0]
+        if sample.size:
+            sample.sort()
+            for j in range(1, k):
+                b.append(max(b[-1] + 1, int(sample[min(sample.size - 1, (sample.size * j) // k)])))
+        else:
+            b += [(1 << 32) * j // k for j in range(1, k)]
+        b.append(1 << 32)
+        bounds[g] = np.array(b, np.uint64)
+    return bounds
 
 
 def layout_stats(group, off, ngroups):
