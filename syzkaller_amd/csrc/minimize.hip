@@ -276,6 +276,11 @@ void group_partition_dev(const uint32_t* group, const uint64_t* off, size_t n, u
   }
 }
 
+__global__ void k_bits_bytes(const uint32_t* bits, size_t n, uint8_t* out) {
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
+    out[r] = (uint8_t)((bits[r >> 5] >> (r & 31)) & 1u);
+}
+
 // groups of one entry are not sorted (no pack or round touches them): their rank is their position
 __global__ void k_rank_init(const uint32_t* members, size_t n, uint32_t* rank_of_member, uint32_t* ent_of_rank) {
   for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x) {
@@ -1379,7 +1384,15 @@ int syzgpu_corpus_minimize(syzgpu_corpus* cp, int64_t* out_idx, uint64_t* group_
     corpus_minimize_dev(K, 0, nullptr, nullptr, C_.stream);
     int64_t* dout = C_.scratch.get<int64_t>("mz_out", K.n + 1);
     uint64_t* dgoff = C_.scratch.get<uint64_t>("mz_goff", K.G + 1);
-    sel_compact_dev(K.sel_bits.p, K.eor.p, K.gstart.p, K.n, K.G, dout, dgoff, C_.stream);
+    {
+      uint8_t* s8 = C_.scratch.get<uint8_t>("mz_sel8", (K.n + 31) / 32 * 32 + 64);
+      SYZ_HIP(hipMemsetAsync(s8, 0, (K.n + 31) / 32 * 32 + 64, C_.stream));
+      if (K.n) {
+        k_bits_bytes<<<grid_for(K.n, 256, 4096), 256, 0, C_.stream>>>(K.sel_bits.p, K.n, s8);
+        SYZ_LAUNCHED();
+      }
+      sel_compact_dev(s8, K.eor.p, K.gstart.p, K.n, K.G, dout, dgoff, C_.stream);
+    }
     SYZ_HIP(hipMemcpyAsync(group_out_off, dgoff, (K.G + 1) * 8, hipMemcpyDeviceToHost, C_.stream));
     SYZ_HIP(hipStreamSynchronize(C_.stream));
     if (group_out_off[K.G] && out_idx)

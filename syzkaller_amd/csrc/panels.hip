@@ -35,14 +35,14 @@ constexpr uint32_t DS = 15;       // direct-mode window bits: a 32768-entry u32 
 constexpr uint32_t SMAX = 26;     // 32 - 6 tag bits
 constexpr int PP_BLOCK = 1024;
 constexpr int PP_WAVES = PP_BLOCK / 64;
-constexpr int PP_TPW = 20;  // 64-PC tiles per wave held in registers: PCAP/64 + MEMB tiles over 16 waves
-constexpr uint32_t HS = 8192;    // open-addressing slots of a sparse-window table
-constexpr int HM_BLOCK = 512;
+constexpr int PP_U = 4;     // 64-PC tiles per wave in flight in k_part's passes
+constexpr uint32_t HS = 16384;   // open-addressing slots of a sparse-window table (128 KB with the ranks)
+constexpr uint32_t HCAP = 8192;  // PCs per round of a sparse window: the table stays at most half full
+constexpr uint32_t HPROBE = 128; // a longer probe run means the table is full after all
 constexpr uint32_t HBM_WORDS = 2048;  // LDS winner bitmap of the sparse kernel (65536 ranks per pass)
 constexpr uint32_t DENSE = 8192;      // PCs per 32K-address window above which a call is direct-mode
-constexpr uint32_t HTARGET = 12288;   // PCs per window a sparse call's window size aims at
+constexpr uint32_t HTARGET = 8192;    // PCs per window a sparse call's window size aims at
 
-static_assert(PP_TPW * PP_WAVES * 64 >= PCAP + 64 * MEMB, "k_part tiles per wave");
 
 // ---- per-entry statistics: PCs per call group and the PC span --------------------------------------
 __global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(1024) void k_gchunk(const uint32_t* gblock, uint32_
 }
 
 // ---- P: transpose the covers into windows ---------------------------------------------------------
-__global__ __launch_bounds__(PP_BLOCK, 2) void k_part(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
+__global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_part(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
                                                       const uint32_t* __restrict__ members,
                                                       const uint64_t* __restrict__ mpos,
                                                       const uint32_t* __restrict__ sbeg, const PChunk* chunks,
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(PP_BLOCK, 2) void k_part(const uint32_t* __restrict
   const uint64_t nch = *nchunks_dev;
   const int wv = threadIdx.x >> 6;
   const unsigned lane = __lane_id();
-  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {  // one chunk per workgroup (grid = chunk bound)
     const PChunk ch = chunks[c];
     const PGroup gp = pg[ch.g];
     const uint32_t S = gp.S, W = gp.W;
@@ -199,33 +199,34 @@ __global__ __launch_bounds__(PP_BLOCK, 2) void k_part(const uint32_t* __restrict
     __syncthreads();
     const uint32_t ntiles = tpre[64];
     const uint32_t nm = ch.nmem;
-    // pass 1: every PC of the chunk into registers, window histogram
-    uint32_t v[PP_TPW];
+    // tile t of the chunk: member m (the last one whose tiles start at or before t) and PC q
+    auto tile = [&](uint32_t t, uint32_t& m, uint64_t& addr) -> bool {
+      const uint64_t bal = __ballot(lane < nm && tpre[lane] <= t);
+      m = __popcll(bal) - 1;
+      const uint32_t q = mlo[m] + (t - tpre[m]) * 64 + lane;
+      addr = mraw[m] + q;
+      return q < mhi[m];
+    };
+    // pass 1: window histogram (PP_U tiles per wave in flight)
+    for (uint32_t t0 = wv; t0 < ntiles; t0 += PP_WAVES * PP_U) {
+      uint32_t v[PP_U];
+      bool ok[PP_U];
 #pragma unroll
-    for (int k = 0; k < PP_TPW; k++) {
-      const uint32_t t = wv + PP_WAVES * k;
-      v[k] = 0;
-      if (t < ntiles) {
-        const uint64_t bal = __ballot(lane < nm && tpre[lane] <= t);
-        const uint32_t m = __popcll(bal) - 1;
-        const uint32_t q = mlo[m] + (t - tpre[m]) * 64 + lane;
-        if (q < mhi[m]) v[k] = pcs[mraw[m] + q];
+      for (int k = 0; k < PP_U; k++) {
+        const uint32_t t = t0 + PP_WAVES * k;
+        uint32_t m;
+        uint64_t ad;
+        ok[k] = t < ntiles && tile(t, m, ad);
+        v[k] = ok[k] ? pcs[ad] : 0u;
       }
-    }
 #pragma unroll
-    for (int k = 0; k < PP_TPW; k++) {
-      const uint32_t t = wv + PP_WAVES * k;
-      if (t < ntiles) {
-        const uint64_t bal = __ballot(lane < nm && tpre[lane] <= t);
-        const uint32_t m = __popcll(bal) - 1;
-        const uint32_t q = mlo[m] + (t - tpre[m]) * 64 + lane;
-        if (q < mhi[m]) {
-          const uint32_t w = (v[k] - lo) >> S;
-          if (w < W)
-            atomicAdd(&hist[w], 1u);
-          else
-            atomicOr(err, 1);  // outside [lo, hi]: an unsorted cover; redone on exact bounds
-        }
+      for (int k = 0; k < PP_U; k++) {
+        if (!ok[k]) continue;
+        const uint32_t w = (v[k] - lo) >> S;
+        if (w < W)
+          atomicAdd(&hist[w], 1u);
+        else
+          atomicOr(err, 1);  // outside [lo, hi]: an unsorted cover; redone on exact bounds
       }
     }
     __syncthreads();
@@ -246,19 +247,23 @@ __global__ __launch_bounds__(PP_BLOCK, 2) void k_part(const uint32_t* __restrict
       }
     }
     __syncthreads();
-    // pass 2: element = offset in window | member tag, staged window-major in LDS
+    // pass 2 (the chunk again, from L2): element = offset in window | member tag, window-major in LDS
     const uint32_t omask = (1u << S) - 1;
+    for (uint32_t t0 = wv; t0 < ntiles; t0 += PP_WAVES * PP_U) {
+      uint32_t v[PP_U], mm[PP_U];
+      bool ok[PP_U];
 #pragma unroll
-    for (int k = 0; k < PP_TPW; k++) {
-      const uint32_t t = wv + PP_WAVES * k;
-      if (t < ntiles) {
-        const uint64_t bal = __ballot(lane < nm && tpre[lane] <= t);
-        const uint32_t m = __popcll(bal) - 1;
-        const uint32_t q = mlo[m] + (t - tpre[m]) * 64 + lane;
-        if (q < mhi[m]) {
-          const uint32_t d = v[k] - lo, w = d >> S;
-          if (w < W) obuf[atomicAdd(&hist[w], 1u)] = (d & omask) | (m << S);
-        }
+      for (int k = 0; k < PP_U; k++) {
+        const uint32_t t = t0 + PP_WAVES * k;
+        uint64_t ad;
+        ok[k] = t < ntiles && tile(t, mm[k], ad);
+        v[k] = ok[k] ? pcs[ad] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < PP_U; k++) {
+        if (!ok[k]) continue;
+        const uint32_t d = v[k] - lo, w = d >> S;
+        if (w < W) obuf[atomicAdd(&hist[w], 1u)] = (d & omask) | (mm[k] << S);
       }
     }
     __syncthreads();
@@ -268,61 +273,122 @@ __global__ __launch_bounds__(PP_BLOCK, 2) void k_part(const uint32_t* __restrict
   }
 }
 
+// Winners of a window table -> sel8[rank] = 1 with plain byte stores (no atomics: a byte written by
+// several tables is written with the same value). Ranks of call g lie in [gbase, gbase + ng); the
+// first BMW*32 of them are deduplicated through an LDS bitmap first, so each kept input costs one
+// store per table, not one per key it wins.
+template <uint32_t BMW>
+__device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
+                                                  uint32_t* bm, uint8_t* sel8) {
+  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BMW * 32, ng);
+  const uint32_t words = (span + 31) / 32;
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
+    const uint32_t r = tab[i];
+    if (r == RANK_NONE) continue;
+    const uint64_t lr = (uint64_t)r - gbase;
+    if (lr < span) {
+      const uint32_t bit = 1u << (lr & 31);
+      if (!(bm[lr >> 5] & bit)) atomicOr(&bm[lr >> 5], bit);
+    } else {
+      sel8[r] = 1;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
+    uint32_t wv = bm[i];
+    while (wv) {
+      const uint32_t b = __ffs(wv) - 1;
+      sel8[gbase + 32ull * i + b] = 1;
+      wv &= wv - 1;
+    }
+  }
+  __syncthreads();
+}
+
 // ---- M: min rank per key of one (call, window) ------------------------------------------------------
-// The runs of the window in every chunk of the call, flattened across a wave: lane i of a batch of 64
-// runs finds its run by a binary search over the wave's inclusive run-length prefix.
+// A wave takes the window's runs of 64 chunks at a time (one chunk's run per lane of metadata) and
+// then walks them RB runs at a time: for each run one coalesced 256-byte load brings the Go-sort
+// ranks of the run's 64-member block into a register (lane m = member m), and the run's elements are
+// loaded one per lane; an element's rank is then a register shuffle by its member tag. RB runs'
+// loads are in flight together.
+constexpr int RB = 8;
+constexpr int TU = 4;  // slices in flight per long run
 template <class F>
 __device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* __restrict__ chunks,
                                                  const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
                                                  const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems,
-                                                 const uint32_t* __restrict__ rank_of_member, int nwaves, F f) {
+                                                 const uint32_t* __restrict__ rank_of_member, uint32_t nmem_total,
+                                                 int nwaves, F f) {
   const uint32_t g = it.g, w = it.w;
   const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
   const uint32_t W = pg[g].W, S = pg[g].S;
+  const uint32_t omask = (1u << S) - 1;
   const uint16_t* d0 = desc + gdesc[g] + w;
   const int wv = threadIdx.x >> 6;
   const unsigned lane = __lane_id();
-  constexpr int U = 4;
-  for (uint64_t cb = c0 + (uint64_t)wv * 64; cb < c1; cb += (uint64_t)nwaves * 64) {
-    const uint64_t c = cb + lane;
-    uint32_t len = 0, mb = 0;
-    uint64_t st = 0;
+  const uint32_t last_m = nmem_total ? nmem_total - 1 : 0;
+  // wave wv takes runs c0 + wv, c0 + wv + nwaves, ... (64 of them per batch), so a window with few
+  // chunks still spreads over every wave
+  const uint64_t nrun = c1 - c0;
+  for (uint64_t b0 = (uint64_t)wv; b0 < nrun; b0 += (uint64_t)nwaves * 64) {
+    const uint64_t c = c0 + b0 + (uint64_t)lane * nwaves;
+    uint32_t len = 0, mb = 0, stl = 0, sth = 0;
     if (c < c1) {
       const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
       const uint32_t s0 = d[0], s1 = d[1];
       len = s1 - s0;
-      st = chunks[c].elem + s0;
+      const uint64_t st = chunks[c].elem + s0;
+      stl = (uint32_t)st;
+      sth = (uint32_t)(st >> 32);
       mb = chunks[c].mb;
     }
-    const uint32_t P = wave_incl_scan<uint32_t>(len);
-    const uint32_t E = P - len;
-    const uint32_t total = __shfl(P, 63, 64);
-    for (uint32_t t = 0; t < total; t += 64 * U) {
-      uint32_t x[U], mbs[U];
-      bool ok[U];
+    const uint32_t nr = (uint32_t)min<uint64_t>(64, (nrun - b0 + nwaves - 1) / nwaves);
+    for (uint32_t r0 = 0; r0 < nr; r0 += RB) {
+      uint32_t rk[RB], e0[RB], e1[RB], ln[RB];
+      uint64_t sts[RB];
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t i = t + 64 * u + lane;
-        ok[u] = i < total;
-        uint32_t j = 0;
-#pragma unroll
-        for (int s = 32; s >= 1; s >>= 1) {
-          const uint32_t pj = __shfl(P, (int)(j + s - 1), 64);
-          if (pj <= i) j += s;
+      for (int r = 0; r < RB; r++) {
+        const uint32_t j = r0 + r;
+        ln[r] = j < nr ? (uint32_t)__builtin_amdgcn_readlane((int)len, (int)j) : 0u;
+        const uint32_t mbj = (uint32_t)__builtin_amdgcn_readlane((int)mb, (int)j);
+        sts[r] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sth, (int)j) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)stl, (int)j);
+        rk[r] = 0;
+        e0[r] = 0;
+        e1[r] = 0;
+        if (ln[r]) {
+          rk[r] = rank_of_member[min(mbj + lane, last_m)];
+          if (lane < ln[r]) e0[r] = elems[sts[r] + lane];
+          if (lane + 64 < ln[r]) e1[r] = elems[sts[r] + 64 + lane];
         }
-        j = min(j, 63u);
-        const uint32_t lo32 = __shfl((uint32_t)st, (int)j, 64), hi32 = __shfl((uint32_t)(st >> 32), (int)j, 64);
-        const uint32_t ej = __shfl(E, (int)j, 64);
-        mbs[u] = __shfl(mb, (int)j, 64);
-        const uint64_t a = (((uint64_t)hi32 << 32) | lo32) + (i - ej);
-        x[u] = ok[u] ? elems[a] : 0;
       }
-      uint32_t r[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) r[u] = ok[u] ? rank_of_member[mbs[u] + (x[u] >> S)] : 0;
+      for (int r = 0; r < RB; r++) {
+        if (!ln[r]) continue;
+        {
+          const uint32_t R = (uint32_t)__shfl((int)rk[r], (int)(e0[r] >> S), 64);
+          if (lane < ln[r]) f(e0[r] & omask, R);
+        }
+        if (ln[r] > 64) {
+          const uint32_t R = (uint32_t)__shfl((int)rk[r], (int)(e1[r] >> S), 64);
+          if (lane + 64 < ln[r]) f(e1[r] & omask, R);
+          for (uint32_t k = 128; k < ln[r]; k += 64 * TU) {  // long runs: TU 64-PC slices in flight
+            uint32_t x[TU];
 #pragma unroll
-      for (int u = 0; u < U; u++)
-        if (ok[u]) f(x[u] & ((1u << S) - 1), r[u]);
+            for (int u = 0; u < TU; u++) {
+              const uint32_t i = k + 64 * u + lane;
+              x[u] = i < ln[r] ? elems[sts[r] + i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < TU; u++) {
+              const uint32_t R2 = (uint32_t)__shfl((int)rk[r], (int)(x[u] >> S), 64);
+              if (k + 64 * u + lane < ln[r]) f(x[u] & omask, R2);
+            }
+          }
+        }
+      }
     }
   }
 }
@@ -332,63 +398,82 @@ __global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const 
                                                       const PGroup* pg, const uint16_t* __restrict__ desc,
                                                       const uint32_t* __restrict__ elems,
                                                       const uint32_t* __restrict__ rank_of_member,
-                                                      const uint64_t* gstart, uint32_t* sel_bits) {
+                                                      uint32_t nmem_total, const uint64_t* gstart,
+                                                      uint8_t* sel8, int dbg) {
   __shared__ uint32_t tab[1u << DS];
   __shared__ uint32_t bm[BM_WORDS];
   const PItem it = items[blockIdx.x];
   for (uint32_t i = threadIdx.x; i < (1u << DS); i += 1024) tab[i] = RANK_NONE;
   __syncthreads();
-  for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, 16, [&](uint32_t o, uint32_t R) {
-    if (tab[o] > R) atomicMin(&tab[o], R);
+  uint32_t acc = 0;
+  for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, [&](uint32_t o, uint32_t R) {
+    if (dbg & 1)
+      acc ^= o * 31 + R;
+    else if (tab[o] > R)
+      atomicMin(&tab[o], R);
   });
   __syncthreads();
+  if (acc == 0x9E3779B9u) sel8[0] = 1;
+  if (dbg & 2) return;
   const uint64_t gb = gstart[it.g];
-  emit_winners(tab, 1u << DS, gb, gstart[it.g + 1] - gb, bm, sel_bits);
+  emit_winner_bytes<BM_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, bm, sel8);
 }
 
-__device__ __forceinline__ uint32_t hslot13(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - 13); }
-static_assert(HS == 8192, "hslot13");
+// PCs of one (call, window) over all its chunks' runs (metadata only)
+__device__ uint32_t window_elem_count(const PItem it, const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
+                                      const uint16_t* __restrict__ desc, uint32_t* red) {
+  const uint32_t g = it.g, w = it.w, W = pg[g].W;
+  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
+  const uint16_t* d0 = desc + gdesc[g] + w;
+  uint32_t s = 0;
+  for (uint64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
+    const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
+    s += (uint32_t)d[1] - d[0];
+  }
+  return block_sum<1024>(s, red);
+}
 
-// Sparse windows: open addressing keyed by the window offset. If the window holds more distinct keys
-// than fit, it is redone in R rounds (keys split by another hash), R doubling until every round fits;
-// a winner marked by a finished round stays valid (marks are ORs of exact winners).
-__global__ __launch_bounds__(HM_BLOCK) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
-                                                        const uint64_t* gchunk, const uint64_t* gdesc,
-                                                        const PGroup* pg, const uint16_t* __restrict__ desc,
-                                                        const uint32_t* __restrict__ elems,
-                                                        const uint32_t* __restrict__ rank_of_member,
-                                                        const uint64_t* gstart, uint32_t* sel_bits) {
+__device__ __forceinline__ uint32_t hslot14(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - 14); }
+static_assert(HS == 16384, "hslot14");
+
+// Sparse windows: open addressing keyed by the window offset, kept at most half full: a window with
+// more than HCAP PCs is done in R = ceil(PCs / HCAP) rounds, each taking the keys of one residue of
+// another hash (so each round holds at most about HCAP distinct keys). A probe run longer than
+// HPROBE means the table is full after all: every round is redone with twice as many; a winner
+// marked by a finished round stays valid (marks are idempotent stores of exact winners).
+__global__ __launch_bounds__(1024) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
+                                                    const uint64_t* gchunk, const uint64_t* gdesc,
+                                                    const PGroup* pg, const uint16_t* __restrict__ desc,
+                                                    const uint32_t* __restrict__ elems,
+                                                    const uint32_t* __restrict__ rank_of_member,
+                                                    uint32_t nmem_total, const uint64_t* gstart, uint8_t* sel8) {
   __shared__ uint32_t keys[HS];
   __shared__ uint32_t vals[HS];
   __shared__ uint32_t bm[HBM_WORDS];
-  __shared__ uint32_t fill;
+  __shared__ uint32_t red[1024 / 64 + 1];
   __shared__ int full;
   const PItem it = items[blockIdx.x];
   const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
-  uint32_t R = 1;
+  const uint32_t E = window_elem_count(it, gchunk, gdesc, pg, desc, red);
+  if (E == 0) return;
+  uint32_t R = (E + HCAP - 1) / HCAP;
   for (uint32_t round = 0; round < R;) {
-    for (uint32_t i = threadIdx.x; i < HS; i += HM_BLOCK) {
+    for (uint32_t i = threadIdx.x; i < HS; i += 1024) {
       keys[i] = 0xFFFFFFFFu;
       vals[i] = RANK_NONE;
     }
-    if (threadIdx.x == 0) {
-      fill = 0;
-      full = 0;
-    }
+    if (threadIdx.x == 0) full = 0;
     __syncthreads();
-    const uint32_t rmask = R - 1;
-    for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, HM_BLOCK / 64,
+    const uint32_t RR = R, rr = round;
+    for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16,
                      [&](uint32_t o, uint32_t Rk) {
-                       if (rmask && ((hash32(o) >> 7) & rmask) != round) return;
-                       uint32_t h = hslot13(o);
-                       for (uint32_t probes = 0; probes < HS; probes++) {
+                       if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
+                       uint32_t h = hslot14(o);
+                       for (uint32_t probes = 0; probes < HPROBE; probes++) {
                          uint32_t k = keys[h];
                          if (k == 0xFFFFFFFFu) {
                            k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
-                           if (k == 0xFFFFFFFFu) {
-                             if (atomicAdd(&fill, 1u) >= HS - HS / 8) full = 1;
-                             k = o;
-                           }
+                           if (k == 0xFFFFFFFFu) k = o;
                          }
                          if (k == o) {
                            if (vals[h] > Rk) atomicMin(&vals[h], Rk);
@@ -399,42 +484,54 @@ __global__ __launch_bounds__(HM_BLOCK) void k_pmin_hash(const PItem* items, cons
                        full = 1;
                      });
     __syncthreads();
-    if (full) {  // redo every round with twice as many
+    if (full) {
       R *= 2;
       round = 0;
       __syncthreads();
       continue;
     }
-    emit_winners<false, HBM_WORDS>(vals, HS, gb, ng, bm, sel_bits);
+    emit_winner_bytes<HBM_WORDS>(vals, HS, gb, ng, bm, sel8);
     round++;
   }
 }
 
 // ---- outputs: the group-major kept list in selection order ----------------------------------------
-__global__ void k_sel_wpop(const uint32_t* sel_bits, size_t nw, uint32_t* cnt) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x)
-    cnt[i] = __popc(sel_bits[i]);
+// kept inputs per 32 ranks (bytes are 0/1)
+__global__ void k_sel_wpop(const uint8_t* sel8, size_t nw, uint32_t* cnt) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x) {
+    const uint4* q = reinterpret_cast<const uint4*>(sel8 + 32 * i);
+    const uint4 a = q[0], b = q[1];
+    cnt[i] = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(b.x) + __popc(b.y) + __popc(b.z) +
+             __popc(b.w);
+  }
 }
 
-__device__ __forceinline__ uint64_t sel_pos(const uint32_t* sel_bits, const uint64_t* wpos, size_t nw, uint64_t r) {
-  const uint64_t wi = r >> 5;
-  const uint32_t word = wi < nw ? sel_bits[wi] : 0u;
-  const uint32_t sh = (uint32_t)(r & 31);
-  return wpos[wi] + __popc(sh ? word & ((1u << sh) - 1) : 0u);
+__device__ __forceinline__ uint64_t sel_pos(const uint8_t* sel8, const uint64_t* wpos, uint64_t r) {
+  uint64_t p = wpos[r >> 5];
+  for (uint64_t k = r & ~31ull; k < r; k++) p += sel8[k];
+  return p;
 }
 
-__global__ void k_sel_compact(const uint32_t* sel_bits, const uint64_t* wpos, const uint32_t* ent_of_rank, size_t n,
+__global__ void k_sel_compact(const uint8_t* sel8, const uint64_t* wpos, const uint32_t* ent_of_rank, size_t n,
                               int64_t* out) {
-  const size_t nw = (n + 31) / 32;
-  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
-    if ((sel_bits[r >> 5] >> (r & 31)) & 1u) out[sel_pos(sel_bits, wpos, nw, r)] = (int64_t)ent_of_rank[r];
+  // one wave per 64 ranks: positions by a ballot prefix
+  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r - __lane_id() < n;
+       r += (size_t)gridDim.x * blockDim.x) {
+    const bool s = r < n && sel8[r];
+    const uint64_t bal = __ballot(s);
+    if (s) {
+      const uint64_t base = r - __lane_id();
+      const uint64_t lo32 = base >> 5;  // base is a multiple of 64
+      const uint64_t pos = wpos[lo32] + __popcll(bal & lanemask_lt());
+      out[pos] = (int64_t)ent_of_rank[r];
+    }
+  }
 }
 
-__global__ void k_sel_goff(const uint32_t* sel_bits, const uint64_t* wpos, const uint64_t* gstart, uint32_t G,
-                           size_t n, uint64_t* goff) {
-  const size_t nw = (n + 31) / 32;
+__global__ void k_sel_goff(const uint8_t* sel8, const uint64_t* wpos, const uint64_t* gstart, uint32_t G,
+                           uint64_t* goff) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x)
-    goff[g] = sel_pos(sel_bits, wpos, nw, gstart[g]);
+    goff[g] = sel_pos(sel8, wpos, gstart[g]);
 }
 
 // ---- key parts: a call group restricted to a PC range (multi-GPU) --------------------
@@ -488,6 +585,18 @@ void plan_windows(uint64_t span, const uint64_t* gpcs, uint32_t G, std::vector<P
 
 static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span);
 
+// diagnostic switches (SYZGPU_PM_DBG, timing experiments only; results are wrong when set):
+// 1 = direct tables not updated, 2 = no winner emit, 4 = no open-addressing windows
+static unsigned part_grid() {
+  static const unsigned v = getenv("SYZGPU_PART_GRID") ? (unsigned)atoi(getenv("SYZGPU_PART_GRID")) : (1u << 30);
+  return v ? v : 1u;
+}
+
+static int pm_dbg() {
+  static const int v = getenv("SYZGPU_PM_DBG") ? atoi(getenv("SYZGPU_PM_DBG")) : 0;
+  return v;
+}
+
 void minimize_raw_begin(MinJob& J, const RawMinArgs& a) {
   if (a.G == 0 || a.G > MAX_GROUPS_PM) fail(SYZGPU_EINVAL, "ngroups out of range (1..4096)");
   if (a.n >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
@@ -529,13 +638,13 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   J.group = a.group;
   J.prog_len = a.prog_len;
   J.gstart.ensure(G + 1);
-  J.sel_bits.ensure(n / 32 + 2);
+  J.sel8.ensure((n + 31) / 32 * 32 + 64);
   J.ent_of_rank.ensure(n + 1);
   J.rank_of_member.ensure(n + 1);
   uint64_t* gstart = J.gstart.p;
   uint32_t* rank_of_member = J.rank_of_member.p;
   uint32_t* ent_of_rank = J.ent_of_rank.p;
-  uint32_t* sel_bits = J.sel_bits.p;
+  uint8_t* sel8 = J.sel8.p;
   // ---- group partition (stable), sort keys, per-group PCs, span, member slices and offsets ----
   uint32_t* members = sc.get<uint32_t>("mz_members", n + 1);
   uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
@@ -682,7 +791,9 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_LAUNCHED();
   // ---- P on its own stream, beside the Go sort ----
   if (!c.part) {
-    SYZ_HIP(hipStreamCreateWithFlags(&c.part, hipStreamNonBlocking));
+    int least = 0, greatest = 0;
+    SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
   }
@@ -690,7 +801,9 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
   if (chunk_bound) {
     ProfScope ps("part", c.part, total_pcs * 8 + (uint64_t)n * 24);
-    const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, 512);
+    // one workgroup per chunk: workgroups retire all along, so the Go sort's kernels (on normal-priority
+    // streams, this one is the lowest) get CUs while P still runs
+    const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, part_grid());
     k_part<<<grid, PP_BLOCK, 0, c.part>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc,
                                           lo, elems, desc, err);
     SYZ_LAUNCHED();
@@ -698,7 +811,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_HIP(hipEventRecord(c.ev_part1, c.part));
   // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
   uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
-  SYZ_HIP(hipMemsetAsync(sel_bits, 0, (n / 32 + 2) * 4, s));
+  SYZ_HIP(hipMemsetAsync(sel8, 0, (n + 31) / 32 * 32 + 64, s));
   const size_t nd_small = items[0][PMODE_DIRECT].size(), nh_small = items[0][PMODE_HASH].size();
   const size_t nd_big = items[1][PMODE_DIRECT].size(), nh_big = items[1][PMODE_HASH].size();
   const size_t off_small_d = 0, off_small_h = nd_small, off_big_d = nd_small + nh_small,
@@ -708,12 +821,12 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     ProfScope ps(tag, q, 0);
     if (nd) {
       k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + first_d, chunks, gchunk, gdesc, dpg, desc, elems,
-                                                  rank_of_member, gstart, sel_bits);
+                                                  rank_of_member, (uint32_t)n, gstart, sel8, pm_dbg());
       SYZ_LAUNCHED();
     }
-    if (nh) {
-      k_pmin_hash<<<(unsigned)nh, HM_BLOCK, 0, q>>>(ditems + first_h, chunks, gchunk, gdesc, dpg, desc, elems,
-                                                    rank_of_member, gstart, sel_bits);
+    if (nh && !(pm_dbg() & 4)) {
+      k_pmin_hash<<<(unsigned)nh, 1024, 0, q>>>(ditems + first_h, chunks, gchunk, gdesc, dpg, desc, elems,
+                                                    rank_of_member, (uint32_t)n, gstart, sel8);
       SYZ_LAUNCHED();
     }
   };
@@ -752,16 +865,15 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   return true;
 }
 
-__global__ void k_job_xchg(uint32_t* sel_bits, const uint64_t* gstart, const uint32_t* groups, const uint64_t* boff,
+__global__ void k_job_xchg(uint8_t* sel8, const uint64_t* gstart, const uint32_t* groups, const uint64_t* boff,
                            uint8_t* buf, int import) {
   const uint32_t g = groups[blockIdx.y];
   const uint64_t gb = gstart[g], ng = gstart[g + 1] - gb, o = boff[blockIdx.y];
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < ng; r += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t R = gb + r;
     if (import) {
-      if (buf[o + r]) atomicOr(&sel_bits[R >> 5], 1u << (R & 31));
+      if (buf[o + r]) sel8[gb + r] = 1;
     } else {
-      buf[o + r] = (uint8_t)((sel_bits[R >> 5] >> (R & 31)) & 1u);
+      buf[o + r] = sel8[gb + r];
     }
   }
 }
@@ -787,11 +899,11 @@ void minimize_raw_xchg(MinJob& J, const uint32_t* groups, const uint64_t* offset
     J.xkey = key;
   }
   const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>(1, (maxn + 1023) / 1024), 1024);
-  k_job_xchg<<<dim3(gx, ng), 256, 0, s>>>(J.sel_bits.p, J.gstart.p, J.xg.p, J.xo.p, buf, import);
+  k_job_xchg<<<dim3(gx, ng), 256, 0, s>>>(J.sel8.p, J.gstart.p, J.xg.p, J.xo.p, buf, import);
   SYZ_LAUNCHED();
 }
 
-__global__ __launch_bounds__(256) void k_sel_flags(const uint32_t* sel_bits, const uint32_t* ent_of_rank, size_t n,
+__global__ __launch_bounds__(256) void k_sel_flags(const uint8_t* sel8, const uint32_t* ent_of_rank, size_t n,
                                                    const uint16_t* prog_len, const uint32_t* group,
                                                    const uint8_t* count_hist, int32_t C, uint8_t* selected,
                                                    int64_t* hist, int* err) {
@@ -803,7 +915,7 @@ __global__ __launch_bounds__(256) void k_sel_flags(const uint32_t* sel_bits, con
   }
   for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
     const uint32_t e = ent_of_rank[r];
-    const uint32_t s = (sel_bits[r >> 5] >> (r & 31)) & 1u;
+    const uint32_t s = sel8[r];
     if (selected) selected[e] = (uint8_t)s;
     if (do_hist && s && (!count_hist || count_hist[group[e]])) {
       const uint32_t L = prog_len[e];
@@ -820,23 +932,24 @@ __global__ __launch_bounds__(256) void k_sel_flags(const uint32_t* sel_bits, con
   }
 }
 
-void sel_compact_dev(const uint32_t* sel_bits, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
+// sel8 must hold 32 * ceil(n / 32) + 64 bytes, zero past n
+void sel_compact_dev(const uint8_t* sel8, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
                      int64_t* out_idx, uint64_t* group_out_off, hipStream_t s) {
   Scratch& sc = ctx().scratch;
   const size_t nw = (n + 31) / 32;
   uint32_t* wcnt = sc.get<uint32_t>("pm_wcnt", nw + 1);
   uint64_t* wpos = sc.get<uint64_t>("pm_wpos", nw + 2);
   if (nw) {
-    k_sel_wpop<<<grid_for(nw, 256, 4096), 256, 0, s>>>(sel_bits, nw, wcnt);
+    k_sel_wpop<<<grid_for(nw, 256, 4096), 256, 0, s>>>(sel8, nw, wcnt);
     SYZ_LAUNCHED();
   }
   exclusive_scan_u32(wcnt, wpos, nw, s);
   if (out_idx && n) {
-    k_sel_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(sel_bits, wpos, ent_of_rank, n, out_idx);
+    k_sel_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(sel8, wpos, ent_of_rank, n, out_idx);
     SYZ_LAUNCHED();
   }
   if (group_out_off) {
-    k_sel_goff<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(sel_bits, wpos, gstart, G, n, group_out_off);
+    k_sel_goff<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(sel8, wpos, gstart, G, group_out_off);
     SYZ_LAUNCHED();
   }
 }
@@ -861,11 +974,11 @@ void minimize_raw_end(MinJob& J, const RawEndArgs& e) {
   if (e.len_hist) SYZ_HIP(hipMemsetAsync(e.len_hist, 0, (size_t)(e.C + 1) * 8, s));
   if (n) {
     k_sel_flags<<<grid_for(n, 256, 512), 256, e.len_hist ? (size_t)(e.C + 1) * 8 : 0, s>>>(
-        J.sel_bits.p, J.ent_of_rank.p, n, e.len_hist ? J.prog_len : nullptr, J.group, dcount, e.C, e.selected,
+        J.sel8.p, J.ent_of_rank.p, n, e.len_hist ? J.prog_len : nullptr, J.group, dcount, e.C, e.selected,
         e.len_hist, err);
     SYZ_LAUNCHED();
   }
-  if (e.out_idx || e.group_out_off) sel_compact_dev(J.sel_bits.p, J.ent_of_rank.p, J.gstart.p, n, G, e.out_idx, e.group_out_off, s);
+  if (e.out_idx || e.group_out_off) sel_compact_dev(J.sel8.p, J.ent_of_rank.p, J.gstart.p, n, G, e.out_idx, e.group_out_off, s);
   if (e.len_hist) {  // len(p.Calls) > C is Go's index-out-of-range panic (prio.go:148)
     int* herr = c.pinned.get<int>(4);
     SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
