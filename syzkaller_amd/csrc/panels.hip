@@ -37,11 +37,12 @@ constexpr int PP_BLOCK = 1024;
 constexpr int PP_WAVES = PP_BLOCK / 64;
 constexpr int PP_U = 4;     // 64-PC tiles per wave in flight in k_part's passes
 constexpr uint32_t HS = 16384;   // open-addressing slots of a sparse-window table (128 KB with the ranks)
-constexpr uint32_t HCAP = 8192;  // PCs per round of a sparse window: the table stays at most half full
+constexpr uint32_t HCAP = 16384; // PCs per round of a sparse window (distinct keys <= PCs: at most full;
+                                 // calls repeat PCs, so tables are typically half full)
 constexpr uint32_t HPROBE = 128; // a longer probe run means the table is full after all
 constexpr uint32_t HBM_WORDS = 2048;  // LDS winner bitmap of the sparse kernel (65536 ranks per pass)
 constexpr uint32_t DENSE = 8192;      // PCs per 32K-address window above which a call is direct-mode
-constexpr uint32_t HTARGET = 8192;    // PCs per window a sparse call's window size aims at
+constexpr uint32_t HTARGET = 16384;   // PCs per window a sparse call's window size aims at
 
 
 // ---- per-entry statistics: PCs per call group and the PC span --------------------------------------
@@ -164,13 +165,14 @@ __global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))
                                                       const uint64_t* nchunks_dev, const PGroup* pg,
                                                       const uint64_t* gchunk, const uint64_t* gdesc, uint32_t lo,
                                                       uint32_t* __restrict__ elems, uint16_t* __restrict__ desc,
-                                                      int* err) {
+                                                      int* err, int dbg) {
   __shared__ uint32_t obuf[PCAP];
   __shared__ uint32_t hist[WMAX + 1];
   __shared__ uint32_t tpre[MEMB + 1];   // tiles before member m
   __shared__ uint32_t mlo[MEMB], mhi[MEMB];  // the member's PCs inside this chunk, block coordinates
   __shared__ uint64_t mraw[MEMB];            // off[entry] - block coordinate of the member's first PC
   __shared__ uint32_t red[PP_WAVES + 1];
+  __shared__ uint4 tinfo[PCAP / 64 + MEMB];
   const uint64_t nch = *nchunks_dev;
   const int wv = threadIdx.x >> 6;
   const unsigned lane = __lane_id();
@@ -199,13 +201,28 @@ __global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))
     __syncthreads();
     const uint32_t ntiles = tpre[64];
     const uint32_t nm = ch.nmem;
-    // tile t of the chunk: member m (the last one whose tiles start at or before t) and PC q
+    // tile table: per 64-PC tile its member, valid lanes and raw address (built once per chunk, so the
+    // passes read one 16-byte broadcast per tile)
+    for (uint32_t t = threadIdx.x; t < ntiles; t += PP_BLOCK) {
+      uint32_t lo_m = 0, hi_m = nm;  // largest m < nm with tpre[m] <= t
+      while (hi_m - lo_m > 1) {
+        const uint32_t mid = (lo_m + hi_m) >> 1;
+        if (tpre[mid] <= t)
+          lo_m = mid;
+        else
+          hi_m = mid;
+      }
+      const uint32_t m = lo_m;
+      const uint32_t q0 = mlo[m] + (t - tpre[m]) * 64;
+      const uint64_t base = mraw[m] + q0;
+      tinfo[t] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), min(64u, mhi[m] - q0) | (m << 8), 0u);
+    }
+    __syncthreads();
     auto tile = [&](uint32_t t, uint32_t& m, uint64_t& addr) -> bool {
-      const uint64_t bal = __ballot(lane < nm && tpre[lane] <= t);
-      m = __popcll(bal) - 1;
-      const uint32_t q = mlo[m] + (t - tpre[m]) * 64 + lane;
-      addr = mraw[m] + q;
-      return q < mhi[m];
+      const uint4 ti = tinfo[t];
+      m = ti.z >> 8;
+      addr = (((uint64_t)ti.y << 32) | ti.x) + lane;
+      return lane < (ti.z & 0xFFu);
     };
     // pass 1: window histogram (PP_U tiles per wave in flight)
     for (uint32_t t0 = wv; t0 < ntiles; t0 += PP_WAVES * PP_U) {
@@ -249,7 +266,7 @@ __global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))
     __syncthreads();
     // pass 2 (the chunk again, from L2): element = offset in window | member tag, window-major in LDS
     const uint32_t omask = (1u << S) - 1;
-    for (uint32_t t0 = wv; t0 < ntiles; t0 += PP_WAVES * PP_U) {
+    for (uint32_t t0 = wv; t0 < ntiles && !(dbg & 8); t0 += PP_WAVES * PP_U) {
       uint32_t v[PP_U], mm[PP_U];
       bool ok[PP_U];
 #pragma unroll
@@ -268,7 +285,8 @@ __global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
     __syncthreads();
     uint32_t* dst = elems + ch.elem;
-    for (uint32_t i = threadIdx.x; i < ch.len; i += PP_BLOCK) dst[i] = obuf[i];
+    if (!(dbg & 16))
+      for (uint32_t i = threadIdx.x; i < ch.len; i += PP_BLOCK) dst[i] = obuf[i];
     __syncthreads();
   }
 }
@@ -313,7 +331,7 @@ __device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t 
 // ranks of the run's 64-member block into a register (lane m = member m), and the run's elements are
 // loaded one per lane; an element's rank is then a register shuffle by its member tag. RB runs'
 // loads are in flight together.
-constexpr int RB = 8;
+constexpr int RB = 16;
 constexpr int TU = 4;  // slices in flight per long run
 template <class F>
 __device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* __restrict__ chunks,
@@ -586,10 +604,16 @@ void plan_windows(uint64_t span, const uint64_t* gpcs, uint32_t G, std::vector<P
 static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span);
 
 // diagnostic switches (SYZGPU_PM_DBG, timing experiments only; results are wrong when set):
-// 1 = direct tables not updated, 2 = no winner emit, 4 = no open-addressing windows
+// 1 = direct tables not updated, 2 = no winner emit, 4 = no open-addressing windows,
+// 8 = P without its second pass, 16 = P without the element stores
 static unsigned part_grid() {
   static const unsigned v = getenv("SYZGPU_PART_GRID") ? (unsigned)atoi(getenv("SYZGPU_PART_GRID")) : (1u << 30);
   return v ? v : 1u;
+}
+
+static bool pm_serial() {
+  static const bool v = getenv("SYZGPU_PM_SERIAL") && atoi(getenv("SYZGPU_PM_SERIAL")) != 0;
+  return v;
 }
 
 static int pm_dbg() {
@@ -797,18 +821,20 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
   }
+  // SYZGPU_PM_SERIAL=1 (timing experiments): P on the main stream, before the sort
+  hipStream_t pq = pm_serial() ? s : c.part;
   SYZ_HIP(hipEventRecord(c.ev_part0, s));
   SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
   if (chunk_bound) {
-    ProfScope ps("part", c.part, total_pcs * 8 + (uint64_t)n * 24);
+    ProfScope ps("part", pq, total_pcs * 8 + (uint64_t)n * 24);
     // one workgroup per chunk: workgroups retire all along, so the Go sort's kernels (on normal-priority
     // streams, this one is the lowest) get CUs while P still runs
     const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, part_grid());
-    k_part<<<grid, PP_BLOCK, 0, c.part>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc,
-                                          lo, elems, desc, err);
+    k_part<<<grid, PP_BLOCK, 0, pq>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc,
+                                      lo, elems, desc, err, pm_dbg());
     SYZ_LAUNCHED();
   }
-  SYZ_HIP(hipEventRecord(c.ev_part1, c.part));
+  SYZ_HIP(hipEventRecord(c.ev_part1, pq));
   // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
   uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
   SYZ_HIP(hipMemsetAsync(sel8, 0, (n + 31) / 32 * 32 + 64, s));
