@@ -36,6 +36,7 @@ constexpr uint32_t SMAX = 26;     // 32 - 6 tag bits
 constexpr int PP_BLOCK = 1024;
 constexpr int PP_WAVES = PP_BLOCK / 64;
 constexpr int PP_U = 4;     // 64-PC tiles per wave in flight in k_part's passes
+constexpr int PP_TPW2 = 20;  // 64-PC tiles per wave in k_part2 (all in flight)
 constexpr uint32_t HS = 16384;   // open-addressing slots of a sparse-window table (128 KB with the ranks)
 constexpr uint32_t HCAP = 16384; // PCs per round of a sparse window (distinct keys <= PCs: at most full;
                                  // calls repeat PCs, so tables are typically half full)
@@ -288,6 +289,184 @@ __global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))
     if (!(dbg & 16))
       for (uint32_t i = threadIdx.x; i < ch.len; i += PP_BLOCK) dst[i] = obuf[i];
     __syncthreads();
+  }
+}
+
+// ---- P, pipelined form (k_part2): tile tables precomputed, one persistent workgroup per CU ----------
+// k_tiles: a wave per chunk writes its tile table (raw address, valid lanes | member tag << 8, chunk
+// position of the tile's first PC) into a fixed TMAX-entry slot. k_part2 keeps three chunks in flight:
+// while chunk c is rewritten LDS-to-LDS and stored, the PCs of chunk c+G are loading into registers
+// and the tile table of chunk c+2G into LDS (G = grid), so each CU streams HBM while it works in LDS.
+constexpr uint32_t TMAX = PCAP / 64 + MEMB;  // tiles per chunk
+static_assert(TMAX <= PP_TPW2 * (PP_BLOCK / 64), "k_part2: tiles per wave");
+
+__global__ __launch_bounds__(256) void k_tiles(const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
+                                               const uint64_t* __restrict__ mpos, const uint32_t* __restrict__ sbeg,
+                                               const PChunk* chunks, const uint64_t* nchunks_dev, uint4* tiles,
+                                               uint32_t* ntiles) {
+  const uint64_t nch = *nchunks_dev;
+  const unsigned lane = __lane_id();
+  for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nch;
+       c += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const PChunk ch = chunks[c];
+    const uint32_t cb = ch.sub, ce = ch.sub + ch.len;
+    const uint32_t m = lane;
+    uint32_t nt = 0, x = 0, y = 0;
+    uint64_t raw = 0;
+    if (m < ch.nmem) {
+      const uint64_t p0 = mpos[ch.mb], a = mpos[ch.mb + m] - p0, b = mpos[ch.mb + m + 1] - p0;
+      x = (uint32_t)max<uint64_t>(a, cb);
+      y = (uint32_t)min<uint64_t>(b, ce);
+      raw = off[members[ch.mb + m]] + (sbeg ? sbeg[ch.mb + m] : 0u) - a;
+      nt = y > x ? (y - x + 63) / 64 : 0;
+    }
+    const uint32_t inc = wave_incl_scan<uint32_t>(nt);
+    const uint32_t pre = inc - nt;
+    const uint32_t total = __shfl(inc, 63, 64);
+    if (lane == 0) ntiles[c] = total;
+    uint4* tc = tiles + c * TMAX;
+    for (uint32_t t0 = 0; t0 < total; t0 += 64) {  // wave-uniform: the shuffles need every lane
+      const uint32_t t = t0 + lane;
+      uint32_t j = 0;  // the last member whose tiles start at or before t
+#pragma unroll
+      for (int s = 32; s >= 1; s >>= 1) {
+        const uint32_t pj = __shfl(pre, (int)(j + s) & 63, 64);
+        if (j + s < ch.nmem && pj <= t) j += s;
+      }
+      const uint32_t xj = __shfl(x, (int)j, 64), yj = __shfl(y, (int)j, 64), pj = __shfl(pre, (int)j, 64);
+      const uint64_t rj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(raw >> 32), (int)j, 64) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)raw, (int)j, 64);
+      const uint32_t q0 = xj + (t - pj) * 64;
+      const uint64_t base = rj + q0;
+      if (t < total) tc[t] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), min(64u, yj - q0) | (j << 8), q0 - cb);
+    }
+  }
+}
+
+struct PHead {  // the chunk a tile-table buffer holds
+  uint64_t elem, drow;
+  uint32_t S, W, len, nt, g, pad;
+};
+
+__global__ __launch_bounds__(PP_BLOCK) void k_part2(const uint32_t* __restrict__ pcs, const PChunk* chunks,
+                                                    const uint64_t* nchunks_dev, const uint4* __restrict__ tiles,
+                                                    const uint32_t* __restrict__ ntiles_c, const PGroup* pg,
+                                                    const uint64_t* gchunk, const uint64_t* gdesc, uint32_t lo,
+                                                    uint32_t* __restrict__ elems, uint16_t* __restrict__ desc,
+                                                    int* err) {
+  __shared__ uint32_t ibuf[PCAP];
+  __shared__ uint32_t obuf[PCAP];
+  __shared__ uint32_t hist[WMAX + 1];
+  __shared__ uint4 tt[3][TMAX];
+  __shared__ PHead hd[3];
+  __shared__ uint32_t red[PP_WAVES + 1];
+  const uint64_t nch = *nchunks_dev;
+  const int wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  const uint64_t G = gridDim.x;
+  // tile table + header of chunk cc into buffer b (every thread takes part; no barrier inside)
+  auto load_table = [&](uint64_t cc, int b) {
+    if (cc >= nch) return;
+    const uint32_t nt = ntiles_c[cc];
+    const uint4* src = tiles + cc * TMAX;
+    for (uint32_t t = threadIdx.x; t < nt; t += PP_BLOCK) tt[b][t] = src[t];
+    if (threadIdx.x == 0) {
+      const PChunk ch = chunks[cc];
+      const PGroup gp = pg[ch.g];
+      hd[b] = PHead{ch.elem, gdesc[ch.g] + (cc - gchunk[ch.g]) * (uint64_t)(gp.W + 1), gp.S, gp.W, ch.len, nt, ch.g, 0};
+    }
+  };
+  uint64_t c = blockIdx.x;
+  if (c >= nch) return;
+  for (uint32_t i = threadIdx.x; i <= WMAX; i += PP_BLOCK) hist[i] = 0;
+  load_table(c, 0);
+  load_table(c + G, 1);
+  __syncthreads();
+  uint32_t v[PP_TPW2];
+  {  // PCs of the first chunk: tile t = wv + PP_WAVES k of this wave
+    constexpr int B_ = 0;
+    const uint32_t nt_ = hd[B_].nt;
+#pragma unroll
+    for (int k = 0; k < PP_TPW2; k++) {
+      const uint32_t t = wv + PP_WAVES * k;
+      v[k] = 0;
+      if (t < nt_) {
+        const uint4 ti = tt[B_][t];
+        if (lane < (ti.z & 0xFFu)) v[k] = pcs[(((uint64_t)ti.y << 32) | ti.x) + lane];
+      }
+    }
+  }
+#pragma nounroll
+  for (uint32_t it = 0;; it++) {
+    const int b = (int)(it % 3), b1 = (int)((it + 1) % 3), b2 = (int)((it + 2) % 3);
+    const PHead h = hd[b];
+    const uint32_t S = h.S, W = h.W;
+    // pass 1: the chunk's PCs (registers) -> ibuf at their chunk positions, window histogram
+#pragma unroll
+    for (int k = 0; k < PP_TPW2; k++) {
+      const uint32_t t = wv + PP_WAVES * k;
+      if (t < h.nt) {
+        const uint4 ti = tt[b][t];
+        if (lane < (ti.z & 0xFFu)) {
+          ibuf[ti.w + lane] = v[k];
+          const uint32_t w = (v[k] - lo) >> S;
+          if (w < W)
+            atomicAdd(&hist[w], 1u);
+          else
+            atomicOr(err, 1);  // outside [lo, hi]: an unsorted cover; redone on exact bounds
+        }
+      }
+    }
+    load_table(c + 2 * G, b2);
+    __syncthreads();
+    // the next chunk's PCs start loading while this one is scanned, rewritten and stored
+    uint32_t vn[PP_TPW2];
+    {
+      const uint32_t nt_ = c + G < nch ? hd[b1].nt : 0u;
+#pragma unroll
+      for (int k = 0; k < PP_TPW2; k++) {
+        const uint32_t t = wv + PP_WAVES * k;
+        vn[k] = 0;
+        if (t < nt_) {
+          const uint4 ti = tt[b1][t];
+          if (lane < (ti.z & 0xFFu)) vn[k] = pcs[(((uint64_t)ti.y << 32) | ti.x) + lane];
+        }
+      }
+    }
+    {
+      uint16_t* drow = desc + h.drow;
+      uint32_t run = 0;
+      for (uint32_t b0 = 0; b0 <= W; b0 += PP_BLOCK) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t x = i < W ? hist[i] : 0;
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan<PP_BLOCK>(x, red, &tot) + run;
+        if (i <= W) {
+          drow[i] = (uint16_t)pre;
+          hist[i] = pre;
+        }
+        run += tot;
+      }
+    }
+    __syncthreads();
+    // pass 2: element = offset in window | member tag, window-major into obuf
+    const uint32_t omask = (1u << S) - 1;
+    for (uint32_t t = wv; t < h.nt; t += PP_WAVES) {
+      const uint4 ti = tt[b][t];
+      if (lane < (ti.z & 0xFFu)) {
+        const uint32_t d = ibuf[ti.w + lane] - lo, w = d >> S;
+        if (w < W) obuf[atomicAdd(&hist[w], 1u)] = (d & omask) | ((ti.z >> 8) << S);
+      }
+    }
+    __syncthreads();
+    uint32_t* dst = elems + h.elem;
+    for (uint32_t i = threadIdx.x; i < h.len; i += PP_BLOCK) dst[i] = obuf[i];
+    for (uint32_t i = threadIdx.x; i <= W; i += PP_BLOCK) hist[i] = 0;
+    __syncthreads();
+    c += G;
+    if (c >= nch) break;
+#pragma unroll
+    for (int k = 0; k < PP_TPW2; k++) v[k] = vn[k];
   }
 }
 
@@ -611,6 +790,11 @@ static unsigned part_grid() {
   return v ? v : 1u;
 }
 
+static int part_kind() {
+  static const int v = getenv("SYZGPU_PART") ? atoi(getenv("SYZGPU_PART")) : 1;
+  return v;
+}
+
 static bool pm_serial() {
   static const bool v = getenv("SYZGPU_PM_SERIAL") && atoi(getenv("SYZGPU_PM_SERIAL")) != 0;
   return v;
@@ -802,6 +986,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint64_t* gdesc = sc.get<uint64_t>("pm_gdesc", G + 1);
   uint16_t* desc = sc.get<uint16_t>("pm_desc", desc_bound + 1);
   uint32_t* elems = sc.get<uint32_t>("pm_elems", total_pcs + 1);
+  uint4* tiles = part_kind() == 2 ? sc.get<uint4>("pm_tiles", chunk_bound * TMAX + 1) : nullptr;
+  uint32_t* ntiles = part_kind() == 2 ? sc.get<uint32_t>("pm_ntiles", chunk_bound + 1) : nullptr;
   if (B) {
     k_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, gstart, mpos, nsub);
     SYZ_LAUNCHED();
@@ -829,9 +1015,19 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     ProfScope ps("part", pq, total_pcs * 8 + (uint64_t)n * 24);
     // one workgroup per chunk: workgroups retire all along, so the Go sort's kernels (on normal-priority
     // streams, this one is the lowest) get CUs while P still runs
-    const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, part_grid());
-    k_part<<<grid, PP_BLOCK, 0, pq>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc,
-                                      lo, elems, desc, err, pm_dbg());
+    if (part_kind() == 2) {
+      if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+      k_tiles<<<(unsigned)std::min<uint64_t>((chunk_bound + 3) / 4, 16384), 256, 0, pq>>>(
+          a.off, members, mpos, sbeg, chunks, cstart + B, tiles, ntiles);
+      SYZ_LAUNCHED();
+      const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, std::min<unsigned>(part_grid(), c.ncu));
+      k_part2<<<grid, PP_BLOCK, 0, pq>>>(a.pcs, chunks, cstart + B, tiles, ntiles, dpg, gchunk, gdesc, lo, elems,
+                                         desc, err);
+    } else {
+      const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, part_grid());
+      k_part<<<grid, PP_BLOCK, 0, pq>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc,
+                                        lo, elems, desc, err, pm_dbg());
+    }
     SYZ_LAUNCHED();
   }
   SYZ_HIP(hipEventRecord(c.ev_part1, pq));

@@ -6,7 +6,7 @@ TAG=${1:-pmc}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-export TMPDIR=/tmp SYZGPU_PM_SERIAL=1 SYZGPU_GS_NOFORK=1 PM_N=${PM_N:-1000000}
+export TMPDIR=/tmp SYZGPU_PM_SERIAL=1 SYZGPU_GS_NOFORK=1 PM_N=${PM_N:-1000000} SYZGPU_PART=${SYZGPU_PART:-1}
 cd /tmp
 i=0
 for CTR in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU" \
@@ -26,6 +26,6 @@ for f in glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), rec
         k = row["Kernel_Name"].split("(")[0][-30:]
         acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, c in sorted(acc.items()):
-    if "pmin" in k or "part" in k:
+    if "pmin" in k or "part" in k or "tiles" in k:
         print(k, {n: round(sum(v) / len(v)) for n, v in sorted(c.items())})
 PY
