@@ -278,11 +278,29 @@ static void* mt_worker(void* arg) {
   return NULL;
 }
 
-static const uint64_t* g_sort_cnt;
+/* (size, group) pairs: a stateless comparator, so concurrent callers share nothing (qsort has no
+ * context argument); largest first, ties by group id */
+typedef struct {
+  uint64_t size;
+  uint32_t g;
+} group_size;
 static int cmp_group_size(const void* a, const void* b) {
-  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
-  const uint64_t sx = g_sort_cnt[x + 1] - g_sort_cnt[x], sy = g_sort_cnt[y + 1] - g_sort_cnt[y];
-  return sx < sy ? 1 : sx > sy ? -1 : (x > y) - (x < y);
+  const group_size *x = (const group_size*)a, *y = (const group_size*)b;
+  return x->size < y->size ? 1 : x->size > y->size ? -1 : (x->g > y->g) - (x->g < y->g);
+}
+
+/* groups in decreasing size order (the LPT order both multi-thread oracles take them in) */
+static uint32_t* groups_by_size(const uint64_t* cnt, uint32_t ngroups) {
+  group_size* gs = (group_size*)malloc(((size_t)ngroups + 1) * sizeof(group_size));
+  for (uint32_t g = 0; g < ngroups; g++) {
+    gs[g].size = cnt[g + 1] - cnt[g];
+    gs[g].g = g;
+  }
+  qsort(gs, ngroups, sizeof(group_size), cmp_group_size);
+  uint32_t* order = (uint32_t*)malloc(((size_t)ngroups + 1) * sizeof(uint32_t));
+  for (uint32_t g = 0; g < ngroups; g++) order[g] = gs[g].g;
+  free(gs);
+  return order;
 }
 
 int oracle_minimize_grouped_mt(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
@@ -300,10 +318,7 @@ int oracle_minimize_grouped_mt(const uint32_t* pcs, const uint64_t* off, const u
   memcpy(fill, cnt, ((size_t)ngroups + 1) * sizeof(uint64_t));
   int64_t* members = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
   for (size_t i = 0; i < n; i++) members[fill[group[i]]++] = (int64_t)i;
-  uint32_t* order = (uint32_t*)malloc(((size_t)ngroups + 1) * sizeof(uint32_t));
-  for (uint32_t g = 0; g < ngroups; g++) order[g] = g;
-  g_sort_cnt = cnt;
-  qsort(order, ngroups, sizeof(uint32_t), cmp_group_size);
+  uint32_t* order = groups_by_size(cnt, ngroups);
   mt_job J = {pcs, off, cnt, members, order, ngroups, (int64_t*)malloc((n ? n : 1) * sizeof(int64_t)),
               (uint64_t*)calloc((size_t)ngroups + 1, sizeof(uint64_t)), 0};
   if (nthreads < 1) nthreads = 1;
@@ -486,6 +501,136 @@ int oracle_novelty(const uint32_t* pcs, const uint64_t* off, const uint32_t* gro
   }
   free(tab);
   free(tlen);
+  return rc;
+}
+
+/* The same batch as oracle_novelty, as a first-occurrence characterisation for canonical inputs
+ * (sorted covers, sorted duplicate-free tables, sorted flakes): per call, a cover is new iff one of
+ * its PCs other than the sentinel is in neither maxCover[call] nor flakes nor an earlier cover of the
+ * batch; a call's table becomes the sorted union of its old table and those PCs, without the
+ * sentinel (Union drops it, cover.go:63-70), and stays as it was when no cover of the call is new.
+ * A hash set per call instead of Go's per-cover merges makes it O(total PCs), and calls spread over
+ * nthreads host threads (largest first), so the full configs[2] batch (1M covers) checks in seconds.
+ * tests/test_oracle.py pins it to oracle_novelty on canonical random batches. */
+typedef struct {
+  const uint32_t *pcs, *mc, *flk;
+  const uint64_t *off, *mc_off, *cnt;
+  const int64_t* members;
+  const uint32_t* order;
+  size_t nflakes;
+  uint32_t ngroups, next;
+  uint8_t* is_new;
+  uint32_t** tab; /* per call: the new table (NULL: unchanged) */
+  size_t* tlen;
+} nov_job;
+
+static int cmp_u32(const void* a, const void* b) {
+  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  return (x > y) - (x < y);
+}
+
+static int in_sorted(const uint32_t* a, size_t n, uint32_t k) {
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    const size_t mid = (lo + hi) / 2;
+    if (a[mid] < k)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < n && a[lo] == k;
+}
+
+static void* nov_worker(void* arg) {
+  nov_job* J = (nov_job*)arg;
+  for (;;) {
+    const uint32_t t = __atomic_fetch_add(&J->next, 1u, __ATOMIC_RELAXED);
+    if (t >= J->ngroups) break;
+    const uint32_t g = J->order[t];
+    const uint32_t* old = J->mc + J->mc_off[g];
+    const size_t nold = (size_t)(J->mc_off[g + 1] - J->mc_off[g]);
+    const size_t ng = (size_t)(J->cnt[g + 1] - J->cnt[g]);
+    u32set seen;
+    u32set_init(&seen, nold + 1024);
+    for (size_t i = 0; i < nold; i++) u32set_add(&seen, old[i]);
+    size_t nnew = 0, cap = 0;
+    uint32_t* fresh = NULL;
+    for (size_t i = 0; i < ng; i++) {
+      const int64_t e = J->members[J->cnt[g] + i];
+      const uint32_t* cov = J->pcs + J->off[e];
+      const size_t L = (size_t)(J->off[e + 1] - J->off[e]);
+      for (size_t k = 0; k < L; k++) {
+        const uint32_t pc = cov[k];
+        if (pc == SENT || u32set_has(&seen, pc) || in_sorted(J->flk, J->nflakes, pc)) continue;
+        u32set_add(&seen, pc);
+        if (nnew == cap) {
+          cap = cap ? 2 * cap : 1024;
+          fresh = (uint32_t*)realloc(fresh, cap * sizeof(uint32_t));
+        }
+        fresh[nnew++] = pc;
+        J->is_new[e] = 1;
+      }
+    }
+    free(seen.slot);
+    if (nnew) {
+      qsort(fresh, nnew, sizeof(uint32_t), cmp_u32);
+      uint32_t* u = (uint32_t*)malloc((nold + nnew) * sizeof(uint32_t));
+      size_t nu = 0;
+      oracle_setop(2, old, nold, fresh, nnew, u, nold + nnew, &nu); /* drops the sentinel */
+      J->tab[g] = u;
+      J->tlen[g] = nu;
+    }
+    free(fresh);
+  }
+  return NULL;
+}
+
+int oracle_novelty_mt(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                      uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off, const uint32_t* flakes,
+                      size_t nflakes, int nthreads, uint8_t* is_new, uint32_t* out_mc, uint64_t* out_mc_off,
+                      size_t out_cap) {
+  uint64_t* cnt = (uint64_t*)calloc((size_t)ngroups + 1, sizeof(uint64_t));
+  for (size_t i = 0; i < n; i++) {
+    if (group[i] >= ngroups) {
+      free(cnt);
+      return 1;
+    }
+    cnt[group[i] + 1]++;
+  }
+  for (uint32_t g = 0; g < ngroups; g++) cnt[g + 1] += cnt[g];
+  uint64_t* fill = (uint64_t*)malloc(((size_t)ngroups + 1) * sizeof(uint64_t));
+  memcpy(fill, cnt, ((size_t)ngroups + 1) * sizeof(uint64_t));
+  int64_t* members = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+  for (size_t i = 0; i < n; i++) members[fill[group[i]]++] = (int64_t)i;
+  memset(is_new, 0, n);
+  nov_job J = {pcs, mc, flakes, off, mc_off, cnt, members, groups_by_size(cnt, ngroups), nflakes, ngroups, 0,
+               is_new, (uint32_t**)calloc((size_t)ngroups + 1, sizeof(uint32_t*)),
+               (size_t*)calloc((size_t)ngroups + 1, sizeof(size_t))};
+  if (nthreads < 1) nthreads = 1;
+  pthread_t* th = (pthread_t*)malloc((size_t)nthreads * sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, nov_worker, &J);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  int rc = 0;
+  size_t p = 0;
+  out_mc_off[0] = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    const uint32_t* src = J.tab[g] ? J.tab[g] : mc + mc_off[g];
+    const size_t len = J.tab[g] ? J.tlen[g] : (size_t)(mc_off[g + 1] - mc_off[g]);
+    if (!rc && p + len > out_cap) rc = 6;
+    if (!rc) {
+      memcpy(out_mc + p, src, len * sizeof(uint32_t));
+      p += len;
+    }
+    out_mc_off[g + 1] = p;
+    free(J.tab[g]);
+  }
+  free(th);
+  free(J.tab);
+  free(J.tlen);
+  free((void*)J.order);
+  free(cnt);
+  free(fill);
+  free(members);
   return rc;
 }
 

@@ -69,6 +69,12 @@ int oracle_novelty(const uint32_t* pcs, const uint64_t* off, const uint32_t* gro
                    uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off,
                    const uint32_t* flakes, size_t nflakes, uint8_t* is_new, uint32_t* out_mc,
                    uint64_t* out_mc_off, size_t out_cap);
+/* oracle_novelty for canonical inputs as a per-call first-occurrence characterisation (hash sets,
+ * calls over nthreads threads): the full-size configs[2] checker. */
+int oracle_novelty_mt(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
+                      uint32_t ngroups, const uint32_t* mc, const uint64_t* mc_off, const uint32_t* flakes,
+                      size_t nflakes, int nthreads, uint8_t* is_new, uint32_t* out_mc, uint64_t* out_mc_off,
+                      size_t out_cap);
 
 /* Program text, one program (data, len):
  *   *ncalls = len(p.Calls) of prog.Deserialize (prog/encoding.go:120-127, parser.Scan :437-449 over

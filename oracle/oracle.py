@@ -180,6 +180,26 @@ def novelty(pcs, off, group, ngroups, mc, mc_off, flakes):
     return is_new[:n].copy(), out_mc[: int(out_off[-1])].copy(), out_off
 
 
+def novelty_mt(pcs, off, group, ngroups, mc, mc_off, flakes, nthreads=16):
+    """oracle_novelty for canonical inputs, per-call first occurrence over nthreads host threads."""
+    n = off.size - 1
+    group = np.ascontiguousarray(group, dtype=np.uint32)
+    mc = np.ascontiguousarray(mc, dtype=np.uint32)
+    mc_off = np.ascontiguousarray(mc_off, dtype=np.uint64)
+    flakes = np.ascontiguousarray(flakes, dtype=np.uint32)
+    is_new = np.zeros(max(n, 1), dtype=np.uint8)
+    cap = int(mc.size + pcs.size + 1)
+    out_mc = np.empty(cap, dtype=np.uint32)
+    out_off = np.zeros(ngroups + 1, dtype=np.uint64)
+    f = lib().oracle_novelty_mt
+    f.argtypes = [_u32p, _u64p, _u32p, ctypes.c_size_t, ctypes.c_uint32, _u32p, _u64p, _u32p, ctypes.c_size_t,
+                  ctypes.c_int, _u8p, _u32p, _u64p, ctypes.c_size_t]
+    _check(f(_p(pcs, _u32p), _p(off, _u64p), _p(group, _u32p), n, ngroups, _p(mc, _u32p), _p(mc_off, _u64p),
+             _p(flakes, _u32p), flakes.size, int(nthreads), _p(is_new, _u8p), _p(out_mc, _u32p),
+             _p(out_off, _u64p), cap), "novelty_mt")
+    return is_new[:n].copy(), out_mc[: int(out_off[-1])].copy(), out_off
+
+
 def prog_scan(data, off):
     """(ncalls u32[n], status u8[n]) per program of a CSR byte blob (oracle_prog_scan)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)

@@ -2,7 +2,8 @@
 NewInput) on the MI355X against the oracle's literal restatement (oracle.c oracle_novelty).
 
 Bit-exact: is_new flags and every updated maxCover table. BASELINE.json configs[2] ("1M fresh
-execution covers diffed against maxCover") is covered at a reduced size with the same shapes, plus
+execution covers diffed against maxCover") is covered at full size (1M covers) against the
+per-call first-occurrence oracle and at reduced sizes against the literal one, plus
 the edge cases foreach gives the path: the 0xFFFFFFFF sentinel (dropped by Difference and by Union),
 flakes, empty covers, empty tables.
 """
@@ -114,6 +115,20 @@ def test_novelty_config3_property_large():
     want_keys = np.union1d(mkey, uk)
     og = np.repeat(np.arange(G), np.diff(ooff).astype(np.int64)).astype(np.uint64)
     assert np.array_equal((og << np.uint64(32)) | out.astype(np.uint64), want_keys)
+
+
+@pytest.mark.timeout(300)
+def test_novelty_config3_full_size():
+    # configs[2] at full size (the bench leg's shape): maxCover0 of a 100k-program corpus, 1M fresh
+    # covers (422M PCs) over a 2M-PC space, 5k flakes; checked against the per-call first-occurrence
+    # oracle (oracle_novelty_mt, pinned to the literal oracle_novelty in tests/test_oracle.py)
+    fresh, mcp, mco, flakes = _config3(100_000, 1_000_000, 2_000_000)
+    w_new, w_mc, w_off = oracle.novelty_mt(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes, 16)
+    g_new, g_mc, g_off = cover.NoveltyBatch(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes)
+    assert np.array_equal(w_off, g_off)
+    assert np.array_equal(w_mc, g_mc)
+    assert np.array_equal(w_new, g_new)
+    assert 0 < g_new.sum() < fresh.n
 
 
 def test_novelty_full_pc_space():

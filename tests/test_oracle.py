@@ -158,3 +158,49 @@ def test_minimize_grouped_multithread_equals_serial():
     for nth in (1, 3, 8):
         got, goff = oracle.minimize_grouped_mt(c.pcs, c.off, c.group, c.ngroups, nth)
         assert np.array_equal(want, got) and np.array_equal(wgoff, goff)
+
+
+@pytest.mark.parametrize("nth", [1, 4])
+def test_novelty_first_occurrence_equals_literal(nth):
+    # the full-size configs[2] checker (oracle_novelty_mt) against the literal per-cover merges, on
+    # canonical batches: sentinel in covers and tables, flakes, empty covers and tables, calls with no
+    # covers at all
+    rnd = np.random.default_rng(17)
+    S = 0xFFFFFFFF
+    for it in range(40):
+        G = int(rnd.integers(1, 7))
+        n = int(rnd.integers(0, 80))
+        covs = []
+        for _ in range(n):
+            c = np.unique(rnd.integers(0, 120, size=int(rnd.integers(0, 14)))).astype(np.uint32)
+            if rnd.random() < 0.1:
+                c = np.append(c, np.uint32(S))
+            covs.append(c)
+        grp = rnd.integers(0, G, size=n).astype(np.uint32)
+        mc = []
+        for _ in range(G):
+            m = np.unique(rnd.integers(0, 120, size=int(rnd.integers(0, 30)))).astype(np.uint32)
+            if rnd.random() < 0.2:
+                m = np.append(m, np.uint32(S))
+            mc.append(m)
+        flakes = np.unique(rnd.integers(0, 120, size=int(rnd.integers(0, 10)))).astype(np.uint32)
+        pcs, off = oracle.to_csr(covs)
+        mcp, mco = oracle.to_csr(mc)
+        w = oracle.novelty(pcs, off, grp, G, mcp, mco, flakes)
+        g = oracle.novelty_mt(pcs, off, grp, G, mcp, mco, flakes, nth)
+        assert np.array_equal(w[0], g[0]) and np.array_equal(w[1], g[1]) and np.array_equal(w[2], g[2]), it
+    # the bench shape at a size the literal oracle finishes quickly
+    from syzkaller_amd import synth
+    base = synth.corpus(0x5EED0003, 500, 289, 50_000)
+    lens = np.diff(base.off).astype(np.int64)
+    ent = np.repeat(np.arange(base.n), lens)
+    keys = np.unique((base.group[ent].astype(np.uint64) << np.uint64(32)) | base.pcs.astype(np.uint64))
+    mco = np.zeros(290, np.uint64)
+    np.cumsum(np.bincount((keys >> np.uint64(32)).astype(np.int64), minlength=289), out=mco[1:])
+    mcp = (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    fresh = synth.corpus(0x5EED0103, 3000, 289, 50_000)
+    flakes = np.unique(fresh.pcs[::97]).astype(np.uint32)
+    w = oracle.novelty(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes)
+    g = oracle.novelty_mt(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes, nth)
+    assert all(np.array_equal(a, b) for a, b in zip(w, g))
+    assert 0 < w[0].sum() < fresh.n
