@@ -3,9 +3,10 @@
 
 One step = cover.Minimize over every call group of a device-resident corpus
 (syz-manager/manager.go:507-527 -> cover/cover.go:105-131) + CalculatePriorities over the kept
-programs (prog/prio.go:29-38, 137-192) + BuildChoiceTable (prio.go:202-228), through the C ABI of
-libsyzgpu.so. Inputs (covers, call ids, program lengths, the static priority matrix) are resident in
-HBM before the timed region; the output selection, priorities and ChoiceTable stay in HBM.
+programs (prog/prio.go:29-38: calcStaticPriorities :40-135 on the int8 matrix cores from the usage
+matrix of sys/*.txt, calcDynamicPrio :137-192, their product) + BuildChoiceTable (prio.go:202-228),
+through the C ABI of libsyzgpu.so. Inputs (covers, call ids, program lengths, the usage matrix) are
+resident in HBM before the timed region; the output selection, priorities and ChoiceTable stay in HBM.
 
 Workload (BASELINE.json configs[3], per GPU): 1M programs, 2M-PC space, 289 calls, C = 1159,
 synthetic corpus from the seeded generator (SURVEY.md §8d shapes). Weak scaling: at N GPUs the
@@ -70,7 +71,8 @@ def kernel_model(name, corp, info, C):
     pmin / pmin_small: the first-occurrence tables read every element once (4 B per PC), the groups
           sorted by the global rounds / the small ones (their PCs are not split out: the byte model
           uses the step's PCs in proportion to the launch time of the two).
-    prio_choice: static in + prios out + run out (16 B per matrix cell)."""
+    prio_choice: static in + prios out + run out (16 B per matrix cell).
+    static_prio: latency-bound (a 1159 x 1159 x 395 int8 Gram per weight-class pair, ~10 MOP each)."""
     n, pcs = corp.n, info["pcs"]
     if name == "part":
         return "hbm", 8 * pcs + 24 * n
@@ -108,13 +110,19 @@ def roofline(kern, corp, info, C):
     return out
 
 
-def static_matrix(C, seed=7):
-    # calcStaticPriorities output stand-in (needs the generated sys.Calls type graph):
-    # values in [0.1, 1], self-priority = row max (prio.go:124-132)
-    rnd = np.random.default_rng(seed)
-    s = (rnd.random((C, C)) * 0.9 + 0.1).astype(np.float32)
-    np.fill_diagonal(s, s.max(axis=1))
-    return s
+def static_usage(C):
+    """calcStaticPriorities' input: the usage matrix of the reference's sys/*.txt (1159 calls, bundled
+    as package data by tools/gen_sys_usage.py); other call counts take a seeded matrix of the same
+    density and weights."""
+    from syzkaller_amd import sysdesc
+    u = sysdesc.bundled()
+    if u.C == C:
+        return u.weights
+    rnd = np.random.default_rng(7)
+    w = np.zeros((u.weights.shape[0], C), np.float32)
+    mask = rnd.random(w.shape) < np.count_nonzero(u.weights) / u.weights.size
+    w[mask] = rnd.choice(np.array([0.1, 0.2, 0.5, 1.0], np.float32), size=int(mask.sum()))
+    return w
 
 
 def main():
@@ -167,8 +175,9 @@ def main():
         return torch.from_numpy(a.view(view.get(a.dtype, a.dtype))).to(dev)
 
     d_pcs, d_off, d_grp, d_len = dt(corp.pcs), dt(corp.off), dt(corp.group), dt(corp.prog_len)
-    st = static_matrix(C)
-    d_static = torch.from_numpy(st).to(dev)
+    uses = static_usage(C)
+    d_uses = torch.from_numpy(uses).to(dev)
+    d_static = torch.empty((C, C), dtype=torch.float32, device=dev)
     d_sel = torch.zeros(corp.n, dtype=torch.uint8, device=dev)
     d_hist = torch.zeros(C + 1, dtype=torch.int64, device=dev)
     d_out = torch.zeros(max(corp.n, 1), dtype=torch.int64, device=dev)
@@ -202,6 +211,8 @@ def main():
                 job.import_sel(xg, xo, d_x, sptr)
         job.end(C, count_hist if parts else None, d_sel, d_hist, d_out, d_goff, sptr)
         sharding.allreduce_hist(d_hist, dist)  # kept-length histogram: (C+1) int64
+        # CalculatePriorities (prio.go:29-38): calcStaticPriorities (int8 MFMA) x normalized dynamic
+        _lib.check(L.syzgpu_static_priorities_dev(d_uses.data_ptr(), uses.shape[0], C, d_static.data_ptr(), sptr))
         _lib.check(L.syzgpu_prio_choice_dev(d_static.data_ptr(), d_hist.data_ptr(), C, None, d_prios.data_ptr(),
                                             d_run.data_ptr(), d_pres.data_ptr(), sptr))
 
@@ -272,7 +283,7 @@ def main():
         path_bytes = 4 * int(off[-1]) + 10 * total_progs + 16 * C * C  # SURVEY.md §8(d), whole job
         cpu = None
         if args.cpu_baseline and world == 1:
-            cpu = cpu_baseline(corp, st, min(args.cpu_sample, corp.n))
+            cpu = cpu_baseline(corp, uses, min(args.cpu_sample, corp.n))
         solo = world == 1 and not args.emulate
         store_leg_res, store = (None, None)
         if solo and (args.store or args.analytics or args.append):
@@ -680,8 +691,10 @@ def novelty_leg(args, dev, L, read_prof):
     return res
 
 
-def cpu_baseline(corp, static, n_sample):
-    """The oracle (single-threaded C restatement of the Go path) on the first n_sample programs."""
+def cpu_baseline(corp, uses, n_sample):
+    """The oracle (single-threaded C restatement of the Go path) on the first n_sample programs:
+    minimizeCorpus, then CalculatePriorities (calcStaticPriorities in Go's loop form, calcDynamicPrio,
+    the product) and BuildChoiceTable."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     off = np.ascontiguousarray(corp.off[: n_sample + 1])
@@ -689,14 +702,14 @@ def cpu_baseline(corp, static, n_sample):
     grp = np.ascontiguousarray(corp.group[:n_sample])
     t = time.perf_counter()
     kept, _ = oracle.minimize_grouped(pcs, off, grp, corp.ngroups)
-    pr = oracle.calculate_priorities(static, corp.prog_len[kept])
+    pr = oracle.calculate_priorities(oracle.static_priorities(uses), corp.prog_len[kept])
     oracle.build_choice_table(pr, None)
     dt = time.perf_counter() - t
     # SURVEY.md §8d's stronger baseline: the call groups over the host threads this job may use
     nth = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1))
     t = time.perf_counter()
     kept_mt, _ = oracle.minimize_grouped_mt(pcs, off, grp, corp.ngroups, nth)
-    pr = oracle.calculate_priorities(static, corp.prog_len[kept_mt])
+    pr = oracle.calculate_priorities(oracle.static_priorities(uses), corp.prog_len[kept_mt])
     oracle.build_choice_table(pr, None)
     dt_mt = time.perf_counter() - t
     return {"value": round(n_sample / dt, 1), "unit": "progs/s", "cores": 1, "kind": "port",

@@ -137,6 +137,17 @@ int syzgpu_prog_scan_dev(const uint8_t* data, const uint64_t* off, size_t n, con
  * corpus program i (the only property the reference reads). out: C*C float32. */
 int syzgpu_dynamic_prio(const uint16_t* prog_len, size_t nprogs, int32_t C, float* out);
 
+/* prog/prio.go:40-135 calcStaticPriorities. uses[k*C + c] = the weight call c uses usage key k with
+ * (the `uses` map of prio.go:41-104 as a dense nkeys x C float32 matrix, 0 = unused; at most 8
+ * distinct non-zero finite weights, SYZGPU_EINVAL otherwise; syzkaller_amd/sysdesc.py builds it from
+ * sys/ *.txt). prios (C*C float32) = for c0 != c1 the sum over keys of w0*w1 (:110-120), self-priority
+ * = the row maximum (:124-132), then normalizePrio (:133). The pair sums are exact (int8-MFMA counts
+ * per weight pair combined in float64) and rounded once: Go adds float32 products in its randomised
+ * map order, so its own runs differ in the last bits; every such order is within float32 rounding
+ * of this sum. */
+int syzgpu_static_priorities(const float* uses, size_t nkeys, int32_t C, float* prios);
+int syzgpu_static_priorities_dev(const float* uses, size_t nkeys, int32_t C, float* prios, void* stream);
+
 /* prog/prio.go:29-38 CalculatePriorities with calcStaticPriorities' C*C result as input. */
 int syzgpu_calculate_priorities(const float* static_prios, const uint16_t* prog_len, size_t nprogs,
                                 int32_t C, float* out);

@@ -409,6 +409,97 @@ int oracle_calculate_priorities(const float* static_prios, const uint16_t* prog_
   return 0;
 }
 
+/* prio.go:40-135 calcStaticPriorities from its `uses` map as a dense nkeys x C matrix (0 = unused).
+ * exact == 0: the Go loop (:110-120) with the keys taken in key_order (NULL: 0..nkeys-1) standing in
+ *   for Go's map iteration order, which Go randomises per run: float32 products added into float32
+ *   sums, so results differ in the last bits between orders, as Go's own runs do.
+ * exact == 1: the sum every such order approximates: per pair of weight classes (distinct non-zero
+ *   weights, ascending) the count of keys, times the float32 product of the two weights, added in
+ *   float64 in (class, class) order and rounded once (what syzgpu_static_priorities computes).
+ * Then self-priority = row max (:124-132) and normalizePrio (:133). */
+#define ST_KMAX 8
+int oracle_static_priorities(const float* uses, size_t nkeys, int32_t C, const int64_t* key_order, int exact,
+                             float* out) {
+  if (C <= 0) return 1;
+  const size_t CC = (size_t)C * C;
+  memset(out, 0, CC * sizeof(float));
+  if (!exact) {
+    for (size_t t = 0; t < nkeys; t++) {
+      const size_t k = key_order ? (size_t)key_order[t] : t;
+      if (k >= nkeys) return 1;
+      const float* w = uses + k * (size_t)C;
+      for (int32_t c0 = 0; c0 < C; c0++) {
+        if (w[c0] == 0) continue;
+        for (int32_t c1 = 0; c1 < C; c1++) {
+          if (w[c1] == 0 || c0 == c1) continue; /* :113-116 */
+          volatile float prod = w[c0] * w[c1];
+          volatile float sum = out[(size_t)c0 * C + c1] + prod;
+          out[(size_t)c0 * C + c1] = sum;
+        }
+      }
+    }
+  } else {
+    float cls[ST_KMAX];
+    int nk = 0;
+    for (size_t i = 0; i < nkeys * (size_t)C; i++) {
+      const float w = uses[i];
+      if (w == 0) continue;
+      if (!isfinite(w)) return 1;
+      int j = 0;
+      while (j < nk && cls[j] != w) j++;
+      if (j == nk) {
+        if (nk == ST_KMAX) return 1;
+        cls[nk++] = w;
+      }
+    }
+    for (int i = 1; i < nk; i++)
+      for (int j = i; j > 0 && cls[j - 1] > cls[j]; j--) {
+        const float t = cls[j];
+        cls[j] = cls[j - 1];
+        cls[j - 1] = t;
+      }
+    uint32_t* cnt = (uint32_t*)calloc((size_t)nk * nk * CC + 1, sizeof(uint32_t));
+    int32_t* kc = (int32_t*)malloc(((size_t)C + 1) * sizeof(int32_t));
+    int8_t* ka = (int8_t*)malloc(((size_t)C + 1) * sizeof(int8_t));
+    for (size_t k = 0; k < nkeys; k++) {
+      const float* w = uses + k * (size_t)C;
+      int m = 0;
+      for (int32_t c = 0; c < C; c++) {
+        if (w[c] == 0) continue;
+        int a = 0;
+        while (cls[a] != w[c]) a++;
+        kc[m] = c;
+        ka[m] = (int8_t)a;
+        m++;
+      }
+      for (int x = 0; x < m; x++)
+        for (int y = 0; y < m; y++)
+          if (x != y) cnt[((size_t)ka[x] * nk + ka[y]) * CC + (size_t)kc[x] * C + kc[y]]++;
+    }
+    for (size_t e = 0; e < CC; e++) {
+      double acc = 0.0;
+      for (int a = 0; a < nk; a++)
+        for (int b = 0; b < nk; b++) {
+          volatile float p = cls[a] * cls[b];
+          acc += (double)cnt[((size_t)a * nk + b) * CC + e] * (double)p;
+        }
+      out[e] = (float)acc;
+    }
+    free(cnt);
+    free(kc);
+    free(ka);
+  }
+  for (int32_t c0 = 0; c0 < C; c0++) { /* :124-132 */
+    float* pp = out + (size_t)c0 * C;
+    float max = 0;
+    for (int32_t j = 0; j < C; j++)
+      if (max < pp[j]) max = pp[j];
+    pp[c0] = max;
+  }
+  oracle_normalize_prio(out, C);
+  return 0;
+}
+
 /* Go on amd64 converts float32 -> int with CVTTSS2SQ: truncation toward zero; NaN and
  * out-of-range values give the "integer indefinite" 0x8000000000000000. */
 static inline int64_t go_f32_to_int(float x) {

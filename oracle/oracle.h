@@ -53,6 +53,10 @@ void oracle_normalize_prio(float* prios, int32_t C);
 
 /* prog/prio.go:29-38 CalculatePriorities with the static matrix given as input (prio.go:40-135 needs
  * the generated sys.Calls type graph, which the reference does not ship — SURVEY.md F8). */
+/* prio.go:40-135 calcStaticPriorities on its usage matrix: Go's loop in a given key order, or the
+ * exact per-weight-pair form the GPU computes (see oracle.c). */
+int oracle_static_priorities(const float* uses, size_t nkeys, int32_t C, const int64_t* key_order, int exact,
+                             float* out);
 int oracle_calculate_priorities(const float* static_prios, const uint16_t* prog_len, size_t nprogs,
                                 int32_t C, float* out);
 

@@ -153,6 +153,19 @@ def calculate_priorities(static, prog_len):
     return out
 
 
+def static_priorities(uses, key_order=None, exact=False):
+    """calcStaticPriorities (prio.go:40-135) of a nkeys x C usage matrix (oracle_static_priorities)."""
+    uses = np.ascontiguousarray(uses, dtype=np.float32)
+    nkeys, C = uses.shape
+    ko = None if key_order is None else np.ascontiguousarray(key_order, dtype=np.int64)
+    out = np.empty((C, C), dtype=np.float32)
+    f = lib().oracle_static_priorities
+    f.argtypes = [_f32p, ctypes.c_size_t, ctypes.c_int32, _i64p, ctypes.c_int, _f32p]
+    _check(f(_p(uses, _f32p), nkeys, C, None if ko is None else _p(ko, _i64p), int(bool(exact)), _p(out, _f32p)),
+           "static_priorities")
+    return out
+
+
 def build_choice_table(prios, enabled=None):
     prios = np.ascontiguousarray(prios, dtype=np.float32)
     C = prios.shape[0]

@@ -41,6 +41,8 @@ SIGNATURES = {
     "syzgpu_prog_scan_dev": (_c.c_int, [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_dynamic_prio": (_c.c_int, [_vp, _sz, _c.c_int32, _vp]),
     "syzgpu_calculate_priorities": (_c.c_int, [_vp, _vp, _sz, _c.c_int32, _vp]),
+    "syzgpu_static_priorities": (_c.c_int, [_vp, _sz, _c.c_int32, _vp]),
+    "syzgpu_static_priorities_dev": (_c.c_int, [_vp, _sz, _c.c_int32, _vp, _vp]),
     "syzgpu_build_choice_table": (_c.c_int, [_vp, _vp, _c.c_int32, _vp, _vp]),
     "syzgpu_minimize_grouped_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _c.c_int32, _vp, _vp, _vp]),
     "syzgpu_minimize_grouped_ordered_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _c.c_int32, _vp, _vp,

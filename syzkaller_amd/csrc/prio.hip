@@ -72,7 +72,9 @@ __device__ __forceinline__ int64_t go_f32_to_int(float x) {
   return (int64_t)x;
 }
 
-// mode 0: dynamic from Hf (+ optional static multiply); mode 1: prios given (ChoiceTable only).
+// mode 0: dynamic from Hf (+ optional static multiply); mode 1: prios given (ChoiceTable only);
+// mode 2: calcStaticPriorities' tail on the pair sums in prios_in (static_prio.hip): the diagonal
+// becomes the row's maximum (prio.go:124-132), then normalizePrio, written to prios_out (may alias).
 // mode 0 with hist: every row block builds H in LDS itself (no separate suffix launch on the step's
 // critical path; the same integer sums, so the same floats)
 __global__ __launch_bounds__(PR_BLOCK) void k_prio_row(int mode, const float* Hf, const float* static_prios,
@@ -94,11 +96,32 @@ __global__ __launch_bounds__(PR_BLOCK) void k_prio_row(int mode, const float* Hf
   const size_t row = (size_t)i * C;
   const int w = threadIdx.x >> 6;
   float mx = 0.0f, mn = 1e10f;
-  if (mode == 0) {
+  float dg = 0.0f;  // mode 2: the self-priority
+  if (mode == 2) {
+    float m = 0.0f;  // var max float32; if max < p { max = p } over the whole row (its diagonal is 0)
+    for (int32_t j = threadIdx.x; j < C; j += PR_BLOCK) {
+      const float p = prios_in[row + j];
+      if (m < p) m = p;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const float o = __shfl_xor(m, d, 64);
+      m = o > m ? o : m;
+    }
+    if (__lane_id() == 0) rmax[w] = m;
+    __syncthreads();
+    for (int k = 0; k < PR_BLOCK / 64; k++) dg = rmax[k] > dg ? rmax[k] : dg;
+    __syncthreads();
+  }
+  auto in_p = [&](int32_t j) -> float {
+    if (mode == 0) return (j == i) ? 0.0f : Hf[j > i ? j : i];
+    return (j == i) ? dg : prios_in[row + j];
+  };
+  if (mode != 1) {
     // row statistics of normalizePrio: max, min over non-zero, number of zeros (prio.go:160-173)
     int32_t nz = 0;
     for (int32_t j = threadIdx.x; j < C; j += PR_BLOCK) {
-      const float p = (j == i) ? 0.0f : Hf[j > i ? j : i];
+      const float p = in_p(j);
       if (mx < p) mx = p;
       if (p != 0 && mn > p) mn = p;
       if (p == 0) nz++;
@@ -142,8 +165,8 @@ __global__ __launch_bounds__(PR_BLOCK) void k_prio_row(int mode, const float* Hf
     const int32_t j = base + threadIdx.x;
     float p = 0.0f;
     if (j < C) {
-      if (mode == 0) {
-        p = (j == i) ? 0.0f : Hf[j > i ? j : i];
+      if (mode != 1) {
+        p = in_p(j);
         if (mx == 0) {
           p = 1.0f;
         } else {
@@ -170,6 +193,11 @@ __global__ __launch_bounds__(PR_BLOCK) void k_prio_row(int mode, const float* Hf
       carry += tot;
     }
   }
+}
+
+void static_prio_rows_dev(float* prios, int32_t C, hipStream_t s) {
+  k_prio_row<<<C, PR_BLOCK, 0, s>>>(2, nullptr, nullptr, prios, C, nullptr, prios, nullptr, nullptr, nullptr);
+  SYZ_LAUNCHED();
 }
 
 void len_hist_dev(const uint16_t* prog_len, const uint8_t* sel, size_t n, int32_t C, int64_t* hist, int* err,

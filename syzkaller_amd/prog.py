@@ -1,5 +1,6 @@
 """Host mirror of the reference's call-priority API (prog/prio.go) over libsyzgpu.so.
 
+    calcStaticPriorities(usage=None)         prio.go:40   (usage: sysdesc.Usage, default the bundled sys/*.txt)
     CalculatePriorities(static, prog_lens)   prio.go:29   (static = calcStaticPriorities() result)
     calcDynamicPrio(prog_lens, C)            prio.go:137  (+ normalizePrio, prio.go:158)
     BuildChoiceTable(prios, enabled=None)    prio.go:202  -> ChoiceTable
@@ -8,8 +9,9 @@
     CallSetStatus(data, off)                 encoding.go:522-551  CallSet's checks, batched
 
 The reference reads only len(p.Calls) of each corpus program, so programs are
-passed as an array of call counts. calcStaticPriorities needs the generated sys.Calls type graph,
-which the reference snapshot does not contain: its C*C result is an input.
+passed as an array of call counts. calcStaticPriorities walks the sys.Calls type graph that sysgen
+generates from sys/*.txt; sysdesc.py restates that walk on the host and hands the GPU the key-by-call
+weight matrix it produces (the contraction runs on the int8 matrix cores, static_prio.hip).
 """
 import numpy as np
 
@@ -24,6 +26,18 @@ def calcDynamicPrio(prog_lens, C):
     lens = _lens(prog_lens)
     out = np.empty((C, C), dtype=np.float32)
     check(lib().syzgpu_dynamic_prio(ptr(lens), lens.size, C, ptr(out)))
+    return out
+
+
+def calcStaticPriorities(usage=None):
+    """prio.go:40-135 for the calls of `usage` (sysdesc.Usage; default: the bundled sys/*.txt)."""
+    if usage is None:
+        from . import sysdesc
+        usage = sysdesc.bundled()
+    w = np.ascontiguousarray(usage.weights, dtype=np.float32)
+    C = w.shape[1]
+    out = np.empty((C, C), dtype=np.float32)
+    check(lib().syzgpu_static_priorities(ptr(w), w.shape[0], C, ptr(out)))
     return out
 
 
