@@ -217,10 +217,14 @@ int syzgpu_prio_choice_dev(const float* static_prios, const int64_t* len_hist, i
 int syzgpu_minimize_grouped_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n,
                                   uint32_t ngroups);
 
-/* ---- resident corpus store (device analog of syz-manager's mgr.corpus, manager.go:52-65) ------- */
-/* Ingest a corpus once: per call (group) every distinct PC gets a dense id, covers become sorted id
- * lists split at 32768-id windows. Covers must be canonical (sorted, duplicate-free — what the
- * executor produces, executor.cc:572-585). The store keeps its own copies; inputs may be freed. */
+/* ---- resident corpus (device analog of syz-manager's mgr.corpus, manager.go:52-65) ------------- */
+/* The corpus's covers live on the device as CSR (the store keeps its own copies; inputs may be
+ * freed). create also builds the dense-id index (per call every distinct PC gets an id, covers become
+ * id lists split at 32768-id windows), which minimizeCorpus, the cover analytics and key parts run on;
+ * create therefore needs canonical covers (sorted, duplicate-free: what the executor produces,
+ * executor.cc:572-585). Appends and keeps make the index stale: Minimize then runs on the raw
+ * pipeline over the covers (same results, no rebuild), the analytics and set_parts rebuild it, and
+ * syzgpu_corpus_reindex rebuilds it on request. */
 typedef struct syzgpu_corpus syzgpu_corpus;
 int syzgpu_corpus_create(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                          const uint16_t* prog_len /* may be NULL */, size_t n, uint32_t ngroups,
@@ -230,21 +234,36 @@ int syzgpu_corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uin
                              syzgpu_corpus** out);
 int syzgpu_corpus_destroy(syzgpu_corpus* c);
 /* mgr.corpus = append(mgr.corpus, inputs...) (NewInput, syz-manager/manager.go:609-616): appends n
- * covers (CSR, offsets from 0; group ids < the store's ngroups) and returns the grown store in *out.
- * Like Go's append the result is a new store: on success the old handle is released and must not be
- * used; on error it stays valid and *out is untouched. The store is rebuilt on the device from its own
- * copy of the covers, so only the new inputs cross PCIe. */
+ * covers (CSR, offsets from 0; group ids < the store's ngroups, checked by the next minimize) in
+ * place, O(new covers): one device copy plus a host read of two offsets. *out (may be NULL) receives
+ * the same handle. Batch the inputs of an RPC into one call: every call synchronises its stream. */
 int syzgpu_corpus_append(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                          const uint16_t* prog_len /* may be NULL */, size_t n, syzgpu_corpus** out);
 int syzgpu_corpus_append_dev(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                              const uint16_t* prog_len, size_t n, void* stream, syzgpu_corpus** out);
-/* minimizeCorpus on the store (manager.go:507-527): same results as syzgpu_minimize_grouped(_dev). */
+/* mgr.corpus = newCorpus (manager.go:529): the corpus becomes entries idx[0..m) of the current one,
+ * in that order (host / device int64 array); an index out of range is SYZGPU_EINVAL (corpus unchanged). */
+int syzgpu_corpus_keep(syzgpu_corpus* c, const int64_t* idx, size_t m);
+int syzgpu_corpus_keep_dev(syzgpu_corpus* c, const int64_t* idx, size_t m, void* stream);
+/* minimizeCorpus on the store (manager.go:507-527): same results as syzgpu_minimize_grouped(_dev).
+ * _ordered_dev also writes the group-major kept list and group offsets (device arrays, may be NULL). */
 int syzgpu_corpus_minimize(syzgpu_corpus* c, int64_t* out_idx, uint64_t* group_out_off);
 int syzgpu_corpus_minimize_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,
                                void* stream);
-/* info[0..10] = entries, calls, PCs, distinct (call, PC) ids, work items, shared window tables,
+int syzgpu_corpus_minimize_ordered_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,
+                                       int64_t* out_idx, uint64_t* group_out_off, void* stream);
+/* The manager's whole minimizeCorpus (manager.go:507-529): Minimize every call, then
+ * mgr.corpus = the kept entries in Go's order. selected / len_hist / out_idx / group_out_off are
+ * optional device outputs about the corpus BEFORE the keep (entry ids of the old corpus); *kept (host,
+ * may be NULL) = the new corpus's size. Returns after the keep. */
+int syzgpu_corpus_minimize_keep_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,
+                                    int64_t* out_idx, uint64_t* group_out_off, void* stream, uint64_t* kept);
+/* Rebuild the dense-id index now if appends or keeps made it stale. */
+int syzgpu_corpus_reindex(syzgpu_corpus* c, void* stream);
+/* info[0..11] = entries, calls, PCs, distinct (call, PC) ids, work items, shared window tables,
  * 16-byte id vectors of the stream, entries and PCs of the call groups sorted by the global rounds
- * (more than 8192 entries), id vectors of those groups in this store's key parts / in all */
+ * (more than 8192 entries), id vectors of those groups in this store's key parts / in all, and 1 if
+ * the index is current (fields 3..10 are 0 while it is stale) */
 int syzgpu_corpus_info(const syzgpu_corpus* c, uint64_t* info, size_t cap);
 
 /* Key-space sharding of minimizeCorpus over ranks (the multi-GPU form of manager.go:523-527; no
@@ -254,7 +273,7 @@ int syzgpu_corpus_info(const syzgpu_corpus* c, uint64_t* info, size_t cap);
  * (syzgpu_corpus_export_sel_dev -> a MAX all-reduce -> syzgpu_corpus_import_sel_dev) to the full one.
  * count_hist[g] (NULL: all) says which groups this rank adds to len_hist (one rank per split group). */
 int syzgpu_corpus_set_parts(syzgpu_corpus* c, const uint16_t* part, const uint16_t* nparts,
-                            const uint8_t* count_hist);
+                            const uint8_t* count_hist); /* kept across appends and keeps */
 /* syzgpu_corpus_minimize_dev in two halves around that exchange: _begin sorts and runs the
  * first-occurrence pass; _end writes the kept flags and the length histogram. */
 int syzgpu_corpus_minimize_begin_dev(syzgpu_corpus* c, void* stream);

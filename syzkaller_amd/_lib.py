@@ -59,6 +59,11 @@ SIGNATURES = {
     "syzgpu_minimize_grouped_fetch": (_c.c_int, [_vp, _vp, _sz, _c.c_uint32]),
     "syzgpu_corpus_create": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp]),
     "syzgpu_corpus_create_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp, _vp]),
+    "syzgpu_corpus_keep": (_c.c_int, [_vp, _vp, _sz]),
+    "syzgpu_corpus_keep_dev": (_c.c_int, [_vp, _vp, _sz, _vp]),
+    "syzgpu_corpus_minimize_ordered_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    "syzgpu_corpus_minimize_keep_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "syzgpu_corpus_reindex": (_c.c_int, [_vp, _vp]),
     "syzgpu_corpus_destroy": (_c.c_int, [_vp]),
     "syzgpu_corpus_append": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "syzgpu_corpus_append_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),

@@ -254,8 +254,8 @@ class CoverStore:
         return self
 
     def append(self, pcs, off, group, prog_len=None):
-        """mgr.corpus = append(mgr.corpus, inputs...) (NewInput, manager.go:609-616): the store grows in
-        place from the caller's view; underneath the library returns a new store and releases the old."""
+        """mgr.corpus = append(mgr.corpus, inputs...) (NewInput, manager.go:609-616): the covers are
+        appended in place on the device, O(new); Minimize then runs on the raw pipeline until a reindex."""
         pcs, off, group = _u32(pcs), np.ascontiguousarray(off, dtype=np.uint64), _u32(group)
         pl = None if prog_len is None else np.ascontiguousarray(prog_len, dtype=np.uint16)
         h = np.zeros(1, dtype=np.uint64)
@@ -272,15 +272,39 @@ class CoverStore:
         self.n += n
         return self
 
+    def keep(self, idx):
+        """mgr.corpus = newCorpus (manager.go:529): the corpus becomes entries idx, in that order."""
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        check(lib().syzgpu_corpus_keep(self._h, ptr(idx), idx.size))
+        self.n = idx.size
+        return self
+
+    def keep_device(self, d_idx, m, stream=0):
+        check(lib().syzgpu_corpus_keep_dev(self._h, ptr(d_idx), m, stream))
+        self.n = m
+        return self
+
+    def MinimizeKeep(self, C=0, d_selected=None, d_len_hist=None, d_out_idx=None, d_group_out_off=None, stream=0):
+        """The manager's minimizeCorpus (manager.go:507-529): Minimize every call, then keep the selected
+        entries in Go's order. The optional device outputs describe the corpus before the keep."""
+        kept = np.zeros(1, dtype=np.uint64)
+        check(lib().syzgpu_corpus_minimize_keep_dev(self._h, C, ptr(d_selected), ptr(d_len_hist), ptr(d_out_idx),
+                                                    ptr(d_group_out_off), stream, ptr(kept)))
+        self.n = int(kept[0])
+        return self.n
+
+    def reindex(self, stream=0):
+        check(lib().syzgpu_corpus_reindex(self._h, stream))
+
     @property
     def handle(self):
         return self._h
 
     def info(self):
-        v = np.zeros(11, dtype=np.uint64)
-        check(lib().syzgpu_corpus_info(self._h, ptr(v), 11))
+        v = np.zeros(12, dtype=np.uint64)
+        check(lib().syzgpu_corpus_info(self._h, ptr(v), 12))
         return dict(zip(["entries", "calls", "pcs", "ids", "work_items", "shared_tables", "vectors",
-                         "big_entries", "big_pcs", "big_vecs", "big_vecs_all"], (int(x) for x in v)))
+                         "big_entries", "big_pcs", "big_vecs", "big_vecs_all", "indexed"], (int(x) for x in v)))
 
     # ---- key-space sharding (the multi-GPU form of minimizeCorpus, syzkaller_amd/sharding.py) ----
     def set_parts(self, part, nparts, count_hist=None):

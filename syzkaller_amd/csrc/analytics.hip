@@ -19,7 +19,7 @@
 #include <algorithm>
 #include <cstring>
 
-#include "store.hpp"
+#include "corpus.hpp"
 
 namespace syz {
 
@@ -361,8 +361,9 @@ int syzgpu_corpus_cover_stats_dev(syzgpu_corpus* cp, uint64_t* call_inputs, uint
                                   uint64_t* call_unique, uint64_t* totals, uint32_t* input_unique, void* stream) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    corpus_cover_stats_dev(*reinterpret_cast<Corpus*>(cp), call_inputs, call_cover, call_unique, totals,
+    CorpusHandle& H = *reinterpret_cast<CorpusHandle*>(cp);
+    std::lock_guard<std::recursive_mutex> hl_(H.mu);
+    corpus_cover_stats_dev(corpus_index(H, (hipStream_t)stream), call_inputs, call_cover, call_unique, totals,
                            input_unique, (hipStream_t)stream);
   })
 }
@@ -371,9 +372,10 @@ int syzgpu_corpus_cover_stats(syzgpu_corpus* cp, uint64_t* call_inputs, uint64_t
                               uint64_t* totals, uint32_t* input_unique) {
   SYZ_API_BODY({
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
-    Corpus& K = *reinterpret_cast<Corpus*>(cp);
-    std::lock_guard<std::recursive_mutex> hl_(K.mu);
+    CorpusHandle& H = *reinterpret_cast<CorpusHandle*>(cp);
+    std::lock_guard<std::recursive_mutex> hl_(H.mu);
     hipStream_t s = C_.stream;
+    Corpus& K = corpus_index(H, s);
     const uint32_t G = K.G;
     const size_t n = K.n;
     uint64_t* d = C_.scratch.get<uint64_t>("cs_out", 3ull * G + 4);
@@ -393,9 +395,10 @@ int syzgpu_corpus_cover_stats(syzgpu_corpus* cp, uint64_t* call_inputs, uint64_t
 int syzgpu_corpus_cover(syzgpu_corpus* cp, int64_t call, int unique, uint32_t* out, size_t cap, size_t* out_n) {
   SYZ_API_BODY({
     if (!cp || !out_n) fail(SYZGPU_EINVAL, "null pointer");
-    Corpus& K = *reinterpret_cast<Corpus*>(cp);
-    std::lock_guard<std::recursive_mutex> hl_(K.mu);
+    CorpusHandle& H = *reinterpret_cast<CorpusHandle*>(cp);
+    std::lock_guard<std::recursive_mutex> hl_(H.mu);
     hipStream_t s = C_.stream;
+    Corpus& K = corpus_index(H, s);
     uint32_t* d = C_.scratch.get<uint32_t>("cs_list", K.total_ids + 1);
     const uint64_t len = corpus_cover(K, call, unique, d, K.total_ids + 1, s);
     *out_n = len;

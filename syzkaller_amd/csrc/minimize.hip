@@ -812,7 +812,7 @@ static void corpus_upload_work(Corpus& K, hipStream_t s) {
 // vector count (longest-processing-time, identical on every rank) and this store keeps part[g].
 // The partial selections of one group on its ranks OR together to the full selection, because an
 // input is kept iff SOME of its PCs first occurs at it.
-static void corpus_set_parts(Corpus& K, const uint16_t* part, const uint16_t* nparts, const uint8_t* count_hist,
+void corpus_set_parts(Corpus& K, const uint16_t* part, const uint16_t* nparts, const uint8_t* count_hist,
                              hipStream_t s) {
   const uint32_t G = K.G;
   std::vector<int> keep_part(G, -1);  // -1: whole group
@@ -878,8 +878,6 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   K.gstart.alloc(G + 1);
   uint32_t* ids = sc.get<uint32_t>("cs_ids", K.total_pcs + 1);
   SYZ_HIP(hipMemcpyAsync(K.off.p, off, (n + 1) * 8, hipMemcpyDeviceToDevice, s));
-  K.pcs.alloc(K.total_pcs);
-  if (K.total_pcs) SYZ_HIP(hipMemcpyAsync(K.pcs.p, pcs, K.total_pcs * 4, hipMemcpyDeviceToDevice, s));
   if (n) SYZ_HIP(hipMemcpyAsync(K.group.p, group, n * 4, hipMemcpyDeviceToDevice, s));
   if (n && prog_len) SYZ_HIP(hipMemcpyAsync(K.prog_len.p, prog_len, n * 2, hipMemcpyDeviceToDevice, s));
   if (n && !prog_len) SYZ_HIP(hipMemsetAsync(K.prog_len.p, 0, n * 2, s));
@@ -1244,6 +1242,15 @@ void corpus_minimize_end(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   }
 }
 
+// rank bitmap -> one byte per rank (sel_compact_dev's input)
+void sel_bits_bytes_dev(const uint32_t* bits, size_t n, uint8_t* out, hipStream_t s) {
+  SYZ_HIP(hipMemsetAsync(out, 0, (n + 31) / 32 * 32 + 64, s));
+  if (n) {
+    k_bits_bytes<<<grid_for(n, 256, 4096), 256, 0, s>>>(bits, n, out);
+    SYZ_LAUNCHED();
+  }
+}
+
 void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s) {
   if (len_hist && (int64_t)K.max_prog_len > (int64_t)C)
     fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
@@ -1251,211 +1258,5 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   corpus_minimize_end(K, C, selected, len_hist, s);
 }
 
-__global__ void k_shift_off(const uint64_t* off, size_t m, uint64_t base, uint64_t* out) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i <= m; i += (size_t)gridDim.x * blockDim.x)
-    out[i] = off[i] + base;
-}
-
-// mgr.corpus = append(mgr.corpus, inputs...) (NewInput, manager.go:609-616) on a resident store: the
-// store is rebuilt on the device from its kept covers followed by the new ones (no re-upload of the
-// corpus); like Go's append the result is a new store, and the old one is released by the caller.
-Corpus* corpus_append_dev(Corpus& K, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
-                          const uint16_t* prog_len, size_t m, hipStream_t s) {
-  Scratch& sc = ctx().scratch;
-  uint64_t h[2] = {0, 0};
-  SYZ_HIP(hipMemcpyAsync(&h[0], off, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(&h[1], off + m, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  if (h[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
-  const size_t n = K.n, nt = n + m;
-  const uint64_t L = K.total_pcs, Lt = L + h[1];
-  if (nt >= 0xFFFFFFF0ull || Lt >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "appended store too large");
-  uint32_t* cp = sc.get<uint32_t>("ap_pcs", Lt + 1);
-  uint64_t* co = sc.get<uint64_t>("ap_off", nt + 1);
-  uint32_t* cg = sc.get<uint32_t>("ap_grp", nt + 1);
-  uint16_t* cl = sc.get<uint16_t>("ap_len", nt + 1);
-  if (L) SYZ_HIP(hipMemcpyAsync(cp, K.pcs.p, L * 4, hipMemcpyDeviceToDevice, s));
-  if (h[1]) SYZ_HIP(hipMemcpyAsync(cp + L, pcs, h[1] * 4, hipMemcpyDeviceToDevice, s));
-  SYZ_HIP(hipMemcpyAsync(co, K.off.p, n * 8, hipMemcpyDeviceToDevice, s));
-  k_shift_off<<<grid_for(m + 1, 256, 4096), 256, 0, s>>>(off, m, L, co + n);
-  SYZ_LAUNCHED();
-  if (n) SYZ_HIP(hipMemcpyAsync(cg, K.group.p, n * 4, hipMemcpyDeviceToDevice, s));
-  if (m) SYZ_HIP(hipMemcpyAsync(cg + n, group, m * 4, hipMemcpyDeviceToDevice, s));
-  if (n) SYZ_HIP(hipMemcpyAsync(cl, K.prog_len.p, n * 2, hipMemcpyDeviceToDevice, s));
-  if (m && prog_len) SYZ_HIP(hipMemcpyAsync(cl + n, prog_len, m * 2, hipMemcpyDeviceToDevice, s));
-  if (m && !prog_len) SYZ_HIP(hipMemsetAsync(cl + n, 0, m * 2, s));
-  Corpus* out = corpus_create_dev(cp, co, cg, cl, nt, K.G, s);
-  SYZ_HIP(hipStreamSynchronize(s));  // the scratch copies are reused by the next call
-  return out;
-}
-
-static void corpus_release(Corpus* K) { delete K; }
-
 }  // namespace syz
 
-extern "C" {
-
-int syzgpu_corpus_append_dev(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
-                             const uint16_t* prog_len, size_t n, void* stream, syzgpu_corpus** out) {
-  SYZ_API_BODY({
-    if (!cp || !out || !off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
-    Corpus* K = reinterpret_cast<Corpus*>(cp);
-    std::unique_lock<std::recursive_mutex> hl_(K->mu);
-    Corpus* N = corpus_append_dev(*K, pcs, off, group, prog_len, n, (hipStream_t)stream);
-    hl_.unlock();
-    corpus_release(K);
-    *out = reinterpret_cast<syzgpu_corpus*>(N);
-  })
-}
-
-int syzgpu_corpus_append(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
-                         const uint16_t* prog_len, size_t n, syzgpu_corpus** out) {
-  SYZ_API_BODY({
-    if (!cp || !out || !off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
-    std::unique_lock<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    if (off[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
-    hipStream_t s = C_.stream;
-    const uint64_t tot = off[n];
-    uint32_t* dp = C_.scratch.get<uint32_t>("cc_pcs", tot + 1);
-    uint64_t* doff = C_.scratch.get<uint64_t>("cc_off", n + 1);
-    uint32_t* dg = C_.scratch.get<uint32_t>("cc_grp", n + 1);
-    uint16_t* dl = prog_len ? C_.scratch.get<uint16_t>("cc_len", n + 1) : nullptr;
-    if (tot) SYZ_HIP(hipMemcpyAsync(dp, pcs, tot * 4, hipMemcpyHostToDevice, s));
-    SYZ_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
-    if (n) SYZ_HIP(hipMemcpyAsync(dg, group, n * 4, hipMemcpyHostToDevice, s));
-    if (dl && n) SYZ_HIP(hipMemcpyAsync(dl, prog_len, n * 2, hipMemcpyHostToDevice, s));
-    Corpus* K = reinterpret_cast<Corpus*>(cp);
-    Corpus* N = corpus_append_dev(*K, dp, doff, dg, dl, n, s);
-    hl_.unlock();
-    corpus_release(K);
-    *out = reinterpret_cast<syzgpu_corpus*>(N);
-  })
-}
-
-int syzgpu_corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
-                             const uint16_t* prog_len, size_t n, uint32_t ngroups, void* stream,
-                             syzgpu_corpus** out) {
-  SYZ_API_BODY({
-    if (!out || !off) fail(SYZGPU_EINVAL, "null pointer");
-    *out = reinterpret_cast<syzgpu_corpus*>(
-        corpus_create_dev(pcs, off, group, prog_len, n, ngroups, (hipStream_t)stream));
-  })
-}
-
-int syzgpu_corpus_create(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
-                         size_t n, uint32_t ngroups, syzgpu_corpus** out) {
-  SYZ_API_BODY({
-    if (!out || !off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
-    hipStream_t s = C_.stream;
-    const uint64_t tot = off[n];
-    uint32_t* dp = C_.scratch.get<uint32_t>("cc_pcs", tot + 1);
-    uint64_t* doff = C_.scratch.get<uint64_t>("cc_off", n + 1);
-    uint32_t* dg = C_.scratch.get<uint32_t>("cc_grp", n + 1);
-    uint16_t* dl = prog_len ? C_.scratch.get<uint16_t>("cc_len", n + 1) : nullptr;
-    if (tot) SYZ_HIP(hipMemcpyAsync(dp, pcs, tot * 4, hipMemcpyHostToDevice, s));
-    SYZ_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
-    if (n) SYZ_HIP(hipMemcpyAsync(dg, group, n * 4, hipMemcpyHostToDevice, s));
-    if (dl && n) SYZ_HIP(hipMemcpyAsync(dl, prog_len, n * 2, hipMemcpyHostToDevice, s));
-    *out = reinterpret_cast<syzgpu_corpus*>(corpus_create_dev(dp, doff, dg, dl, n, ngroups, s));
-    SYZ_HIP(hipStreamSynchronize(s));
-  })
-}
-
-int syzgpu_corpus_destroy(syzgpu_corpus* cp) {
-  SYZ_API_BODY({
-    corpus_release(reinterpret_cast<Corpus*>(cp));
-  })
-}
-
-int syzgpu_corpus_minimize_dev(syzgpu_corpus* cp, int32_t C, uint8_t* selected, int64_t* len_hist, void* stream) {
-  SYZ_API_BODY({
-    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    if (len_hist && C <= 0) fail(SYZGPU_EINVAL, "len_hist needs C > 0");
-    corpus_minimize_dev(*reinterpret_cast<Corpus*>(cp), C, selected, len_hist, (hipStream_t)stream);
-  })
-}
-
-int syzgpu_corpus_minimize(syzgpu_corpus* cp, int64_t* out_idx, uint64_t* group_out_off) {
-  SYZ_API_BODY({
-    if (!cp || !group_out_off) fail(SYZGPU_EINVAL, "null pointer");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    Corpus& K = *reinterpret_cast<Corpus*>(cp);
-    corpus_minimize_dev(K, 0, nullptr, nullptr, C_.stream);
-    int64_t* dout = C_.scratch.get<int64_t>("mz_out", K.n + 1);
-    uint64_t* dgoff = C_.scratch.get<uint64_t>("mz_goff", K.G + 1);
-    {
-      uint8_t* s8 = C_.scratch.get<uint8_t>("mz_sel8", (K.n + 31) / 32 * 32 + 64);
-      SYZ_HIP(hipMemsetAsync(s8, 0, (K.n + 31) / 32 * 32 + 64, C_.stream));
-      if (K.n) {
-        k_bits_bytes<<<grid_for(K.n, 256, 4096), 256, 0, C_.stream>>>(K.sel_bits.p, K.n, s8);
-        SYZ_LAUNCHED();
-      }
-      sel_compact_dev(s8, K.eor.p, K.gstart.p, K.n, K.G, dout, dgoff, C_.stream);
-    }
-    SYZ_HIP(hipMemcpyAsync(group_out_off, dgoff, (K.G + 1) * 8, hipMemcpyDeviceToHost, C_.stream));
-    SYZ_HIP(hipStreamSynchronize(C_.stream));
-    if (group_out_off[K.G] && out_idx)
-      SYZ_HIP(hipMemcpyAsync(out_idx, dout, group_out_off[K.G] * 8, hipMemcpyDeviceToHost, C_.stream));
-    SYZ_HIP(hipStreamSynchronize(C_.stream));
-  })
-}
-
-int syzgpu_corpus_info(const syzgpu_corpus* cp, uint64_t* info, size_t cap) {
-  SYZ_API_BODY({
-    if (!cp || !info) fail(SYZGPU_EINVAL, "null pointer");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(const_cast<syzgpu_corpus*>(cp))->mu);
-    const Corpus& K = *reinterpret_cast<const Corpus*>(cp);
-    const uint64_t v[11] = {K.n,      K.G,          K.total_pcs,   K.total_ids, K.hwork.size(), K.ngtabs,
-                            K.total_vecs, K.big_entries, K.big_pcs, K.big_vecs,  K.big_vecs_all};
-    for (size_t i = 0; i < cap && i < 11; i++) info[i] = v[i];
-  })
-}
-
-int syzgpu_corpus_set_parts(syzgpu_corpus* cp, const uint16_t* part, const uint16_t* nparts,
-                            const uint8_t* count_hist) {
-  SYZ_API_BODY({
-    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    corpus_set_parts(*reinterpret_cast<Corpus*>(cp), part, nparts, count_hist, C_.stream);
-  })
-}
-
-int syzgpu_corpus_minimize_begin_dev(syzgpu_corpus* cp, void* stream) {
-  SYZ_API_BODY({
-    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    corpus_minimize_begin(*reinterpret_cast<Corpus*>(cp), (hipStream_t)stream);
-  })
-}
-
-int syzgpu_corpus_export_sel_dev(syzgpu_corpus* cp, const uint32_t* groups, const uint64_t* offsets,
-                                 uint32_t ngroups, uint8_t* buf, void* stream) {
-  SYZ_API_BODY({
-    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    corpus_sel_xchg(*reinterpret_cast<Corpus*>(cp), groups, offsets, ngroups, buf, 0, (hipStream_t)stream);
-  })
-}
-
-int syzgpu_corpus_import_sel_dev(syzgpu_corpus* cp, const uint32_t* groups, const uint64_t* offsets,
-                                 uint32_t ngroups, const uint8_t* buf, void* stream) {
-  SYZ_API_BODY({
-    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    corpus_sel_xchg(*reinterpret_cast<Corpus*>(cp), groups, offsets, ngroups, const_cast<uint8_t*>(buf), 1,
-                    (hipStream_t)stream);
-  })
-}
-
-int syzgpu_corpus_minimize_end_dev(syzgpu_corpus* cp, int32_t C, uint8_t* selected, int64_t* len_hist,
-                                   void* stream) {
-  SYZ_API_BODY({
-    if (!cp) fail(SYZGPU_EINVAL, "null corpus");
-    std::lock_guard<std::recursive_mutex> hl_(reinterpret_cast<Corpus*>(cp)->mu);
-    if (len_hist && C <= 0) fail(SYZGPU_EINVAL, "len_hist needs C > 0");
-    corpus_minimize_end(*reinterpret_cast<Corpus*>(cp), C, selected, len_hist, (hipStream_t)stream);
-  })
-}
-
-}  // extern "C"

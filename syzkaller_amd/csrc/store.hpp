@@ -115,7 +115,6 @@ struct Corpus {
   DevArr<uint32_t> group, members, member_of, nwin, dict, gtabs, vmem;
   DevArr<uint32_t> gtchunks, gtdone;  // work items per shared window table, and their arrivals
   DevArr<uint16_t> prog_len, ids16;
-  DevArr<uint32_t> pcs;  // the raw covers (CSR with off), kept so an append can rebuild the store
   DevArr<VecWork> work;  // work items of the big call groups first, then those of the small ones
   std::vector<VecWork> hwork;
   size_t nbig_work = 0;                        // work items of the big call groups
@@ -136,8 +135,34 @@ struct Corpus {
     corpus_stats_free(stats);
     off.free(); gstart.free(); gdict.free(); el0.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
     gtchunks.free(); gtdone.free(); count_hist.free(); xg.free(); xo.free();
-    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free(); pcs.free();
+    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free();
   }
 };
+
+// ---- the index (minimize.hip) ----
+Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
+                          size_t n, uint32_t G, hipStream_t s);
+void corpus_set_parts(Corpus& K, const uint16_t* part, const uint16_t* nparts, const uint8_t* count_hist,
+                      hipStream_t s);
+void corpus_minimize_begin(Corpus& K, hipStream_t s);
+void corpus_minimize_end(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s);
+void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s);
+void corpus_sel_xchg(Corpus& K, const uint32_t* groups, const uint64_t* offsets, uint32_t ng, uint8_t* buf,
+                     int import, hipStream_t s);
+void sel_bits_bytes_dev(const uint32_t* bits, size_t n, uint8_t* out, hipStream_t s);
+
+// Device buffer that keeps its first `used` elements when it grows (appends); 1.5x headroom.
+template <class T>
+void grow_keep(Grow<T>& g, size_t used, size_t need, hipStream_t s) {
+  if (need <= g.cap && g.p) return;
+  const size_t want = need + need / 2 + 16;
+  T* p = nullptr;
+  SYZ_HIP(hipMalloc(&p, want * sizeof(T)));
+  if (used && g.p) SYZ_HIP(hipMemcpyAsync(p, g.p, used * sizeof(T), hipMemcpyDeviceToDevice, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (g.p) (void)hipFree(g.p);
+  g.p = p;
+  g.cap = want;
+}
 
 }  // namespace syz

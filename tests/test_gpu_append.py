@@ -1,6 +1,9 @@
-"""Appending to the resident store (syzgpu_corpus_append[_dev]): mgr.corpus = append(mgr.corpus, ...)
-on NewInput (syz-manager/manager.go:609-616), then minimizeCorpus (manager.go:507-527) over the grown
-store must equal the oracle's minimizeCorpus over the whole corpus."""
+"""The resident corpus's lifecycle, following mgr.corpus: appends on NewInput
+(syz-manager/manager.go:609-616, syzgpu_corpus_append[_dev], in place), minimizeCorpus
+(manager.go:507-527) and mgr.corpus = newCorpus (manager.go:529, syzgpu_corpus_keep /
+_minimize_keep_dev). After every step the store's minimizeCorpus (on the stale-index raw pipeline or
+on a rebuilt index) and its cover analytics must equal the oracle's over the same corpus, rebuilt
+host-side by the same sequence of appends and keeps."""
 import os
 import sys
 
@@ -65,3 +68,142 @@ def test_append_rejects_bad_group_and_keeps_store():
     after, agoff = st.Minimize()  # the old handle is still valid after a failed append
     assert np.array_equal(before, after) and np.array_equal(bgoff, agoff)
     st.close()
+
+
+class HostCorpus:
+    """The same corpus on the host (list of covers, call ids, program lengths)."""
+
+    def __init__(self, c, a, b):
+        self.covs = [c.pcs[int(c.off[i]):int(c.off[i + 1])] for i in range(a, b)]
+        self.group = list(c.group[a:b])
+        self.plen = list(c.prog_len[a:b])
+
+    def append(self, c, a, b):
+        other = HostCorpus(c, a, b)
+        self.covs += other.covs
+        self.group += other.group
+        self.plen += other.plen
+
+    def keep(self, idx):
+        self.covs = [self.covs[i] for i in idx]
+        self.group = [self.group[i] for i in idx]
+        self.plen = [self.plen[i] for i in idx]
+
+    def csr(self):
+        pcs, off = oracle.to_csr(self.covs)
+        return pcs, off, np.array(self.group, np.uint32), np.array(self.plen, np.uint16)
+
+
+def _check(st, hc, G):
+    pcs, off, grp, _ = hc.csr()
+    want, wgoff = oracle.minimize_grouped(pcs, off, grp, G)
+    got, goff = st.Minimize()
+    assert np.array_equal(wgoff, goff) and np.array_equal(want, got)
+    return want
+
+
+def test_manager_cycle_append_minimize_keep_vs_oracle():
+    import torch
+    c = synth.corpus(0x5EED00A4, 60_000, 41, 300_000)
+    G = c.ngroups
+    C = int(c.prog_len.max())
+    st = cover.CoverStore(*_part(c, 0, 20_000)[:3], G, _part(c, 0, 20_000)[3])
+    hc = HostCorpus(c, 0, 20_000)
+    assert st.info()["indexed"] == 1
+    s = torch.cuda.current_stream().cuda_stream
+    # NewInput x2 (host and device pointers): in place, the index goes stale
+    st.append(*_part(c, 20_000, 30_000))
+    hc.append(c, 20_000, 30_000)
+    p, o, g, l = (_dev(x) for x in _part(c, 30_000, 40_000))
+    st.append_device(p, o, g, l, 10_000, s)
+    hc.append(c, 30_000, 40_000)
+    assert st.info()["indexed"] == 0 and st.info()["entries"] == 40_000
+    _check(st, hc, G)  # raw pipeline on the stale corpus
+    # minimizeCorpus + mgr.corpus = newCorpus in one call
+    n0 = st.n
+    sel = torch.zeros(n0, dtype=torch.uint8, device="cuda")
+    hist = torch.zeros(C + 1, dtype=torch.int64, device="cuda")
+    out = torch.zeros(n0, dtype=torch.int64, device="cuda")
+    goff = torch.zeros(G + 1, dtype=torch.int64, device="cuda")
+    kept = st.MinimizeKeep(C, sel, hist, out, goff, s)
+    pcs, off, grp, pl = hc.csr()
+    want, wgoff = oracle.minimize_grouped(pcs, off, grp, G)
+    assert kept == want.size and np.array_equal(out.cpu().numpy()[:kept], want)
+    assert np.array_equal(goff.cpu().numpy().astype(np.uint64), wgoff)
+    assert np.array_equal(hist.cpu().numpy(), np.bincount(pl[want], minlength=C + 1))
+    wsel = np.zeros(n0, np.uint8)
+    wsel[want] = 1
+    assert np.array_equal(sel.cpu().numpy(), wsel)
+    hc.keep(want)
+    assert st.info()["entries"] == kept and st.info()["pcs"] == sum(len(x) for x in hc.covs)
+    _check(st, hc, G)  # the kept corpus minimizes to itself (every input was kept for a new PC)
+    # more inputs after the keep, then an explicit keep in another order, then a reindex
+    st.append(*_part(c, 40_000, 60_000))
+    hc.append(c, 40_000, 60_000)
+    _check(st, hc, G)
+    perm = np.random.default_rng(1).permutation(len(hc.covs))[: len(hc.covs) // 2]
+    st.keep(perm)
+    hc.keep(perm)
+    _check(st, hc, G)
+    st.reindex()
+    assert st.info()["indexed"] == 1
+    _check(st, hc, G)
+    # the analytics rebuild the index of the current covers themselves
+    st.append(*_part(c, 0, 3_000))
+    hc.append(c, 0, 3_000)
+    pcs, off, grp, _ = hc.csr()
+    w = oracle.cover_stats(pcs, off, grp, G)
+    g = st.CoverStats()
+    for k in ("call_inputs", "call_cover", "call_unique", "input_unique"):
+        assert np.array_equal(np.asarray(g[k]), w[k]), k
+    assert [g["cover"], g["unique_per_call"], g["unique_per_input"]] == [int(x) for x in w["totals"]]
+    st.close()
+
+
+def test_keep_rejects_out_of_range_and_keeps_corpus():
+    c = synth.corpus(0x5EED00A5, 3_000, 7, 20_000)
+    st = cover.CoverStore(c.pcs, c.off, c.group, c.ngroups, c.prog_len)
+    st.append(*_part(c, 0, 100))
+    before, bgoff = st.Minimize()
+    with pytest.raises(Exception):
+        st.keep(np.array([0, 5, c.n + 100], np.int64))
+    after, agoff = st.Minimize()
+    assert np.array_equal(before, after) and np.array_equal(bgoff, agoff)
+    st.keep(np.zeros(0, np.int64))  # an empty corpus is a corpus
+    got, goff = st.Minimize()
+    assert got.size == 0 and np.array_equal(goff, np.zeros(c.ngroups + 1, np.uint64))
+    st.close()
+
+
+def test_key_parts_survive_append_and_keep():
+    # set_parts is a property of the corpus (ADVICE r1): after an append and a keep the rebuilt index
+    # still runs only this rank's windows and counts only its groups, so two ranks' selections OR to the
+    # full one and their histograms add up to the full histogram
+    c = synth.corpus(0x5EED00A6, 40_000, 9, 200_000)
+    G, C = c.ngroups, int(c.prog_len.max())
+    import torch
+    s = torch.cuda.current_stream().cuda_stream
+    nparts = np.full(G, 2, np.uint16)
+    ranks = []
+    for r in range(2):
+        st = cover.CoverStore(*_part(c, 0, 25_000)[:3], G, _part(c, 0, 25_000)[3])
+        st.set_parts(np.full(G, r, np.uint16), nparts, (np.arange(G) % 2 == r).astype(np.uint8))
+        st.append(*_part(c, 25_000, 40_000))
+        st.keep(np.arange(0, 40_000, 2))
+        st.append(*_part(c, 1, 2))
+        sel = torch.zeros(st.n, dtype=torch.uint8, device="cuda")
+        hist = torch.zeros(C + 1, dtype=torch.int64, device="cuda")
+        st.minimize_begin(s)
+        st.minimize_end(C, sel, hist, s)
+        torch.cuda.synchronize()
+        ranks.append((sel.cpu().numpy(), hist.cpu().numpy()))
+        st.close()
+    hc = HostCorpus(c, 0, 40_000)
+    hc.keep(list(range(0, 40_000, 2)))
+    hc.append(c, 1, 2)
+    pcs, off, grp, pl = hc.csr()
+    want, _ = oracle.minimize_grouped(pcs, off, grp, G)
+    wsel = np.zeros(len(hc.covs), np.uint8)
+    wsel[want] = 1
+    assert np.array_equal(ranks[0][0] | ranks[1][0], wsel)
+    assert np.array_equal(ranks[0][1] + ranks[1][1], np.bincount(pl[want], minlength=C + 1))
