@@ -9,6 +9,13 @@ real exchange is CalculatePriorities (prio.go:29-38) over ALL kept programs: it 
 len(p.Calls), so ranks all-reduce a (C+1)-entry int64 histogram of the kept programs'
 lengths and each rank then computes the C x C priorities / ChoiceTable itself.
 
+The fuzzer's new-coverage check (syz-fuzzer/fuzzer.go:446-470; NewInput, manager.go:609-613) shards
+the other way, by PC value (SURVEY.md §8e "shard the PC-bitmap space"): a cover is new iff one of its
+PCs occurs first at it (not in maxCover, not a flake), a property of each (call, PC) key alone, so
+each rank runs the batch restricted to its PC range, the per-cover flags OR together (MAX all-reduce of
+one byte per cover) and the updated maxCover tables are the concatenation of the ranks' ranges
+(novelty_shard).
+
 The module holds the host logic only: group assignment, shard extraction, the histogram all-reduce
 and the assembly of the global group-major selection. Compute is passed in (the GPU store path in
 bench.py; tests drive the same logic with a checker on CPU under gloo).
@@ -237,3 +244,76 @@ def assemble_selection(kept_global, group, ngroups, dist=None):
     goff = np.zeros(ngroups + 1, np.uint64)
     np.cumsum(np.bincount(g, minlength=ngroups), out=goff[1:])
     return ids, goff
+
+
+# ---- PC-space sharding of the new-coverage check -----------------------------------
+SENTINEL = 0xFFFFFFFF
+
+
+def pc_bounds(sample, nparts):
+    """nparts + 1 ascending PC bounds [0, ..., 2^32] at equal-count quantiles of a PC sample (rank r
+    owns PCs in [b[r], b[r+1] - 1]); a pure function of the sample, identical on every rank."""
+    sample = np.sort(np.asarray(sample, np.uint64))
+    b = [0]
+    for j in range(1, nparts):
+        q = int(sample[min(sample.size - 1, sample.size * j // nparts)]) if sample.size else (1 << 32) * j // nparts
+        b.append(max(b[-1] + 1, q))
+    b.append(1 << 32)
+    return np.array(b, np.uint64)
+
+
+def slice_csr(pcs, off, lo, hi):
+    """Each (sorted) cover of a CSR batch restricted to PCs in [lo, hi]: (pcs', off')."""
+    pcs = np.asarray(pcs, np.uint32)
+    off = np.asarray(off, np.uint64)
+    n = off.size - 1
+    lens = np.diff(off).astype(np.int64)
+    # covers are sorted, so (cover index, pc) is sorted over the whole batch
+    key = (np.repeat(np.arange(n, dtype=np.uint64), lens) << np.uint64(32)) | pcs.astype(np.uint64)
+    idx = np.arange(n, dtype=np.uint64) << np.uint64(32)
+    a = np.searchsorted(key, idx | np.uint64(lo), side="left")
+    b = np.searchsorted(key, idx | np.uint64(hi), side="right")
+    keep = np.zeros(key.size + 1, np.int64)
+    np.add.at(keep, a, 1)
+    np.add.at(keep, b, -1)
+    mask = np.cumsum(keep[:-1]) > 0
+    off2 = np.zeros(n + 1, np.uint64)
+    np.cumsum(b - a, out=off2[1:])
+    return pcs[mask], off2
+
+
+def novelty_shard(pcs, off, group, ngroups, mc, mc_off, flakes, rank, world, bounds, run, dist=None):
+    """One rank's share of a new-coverage batch (fuzzer.go:446-470 per cover, in order) sharded by PC
+    value: the batch, the maxCover tables and the flakes restricted to [bounds[rank], bounds[rank+1]-1],
+    run(...) -> (is_new u8[n], table pcs, table offsets) on that slice (the GPU, or a checker), then the
+    OR of the flags over ranks and the ranks' table parts concatenated per call in PC order. A call's
+    table loses the 0xFFFFFFFF sentinel when any rank updated it (Union drops it over the whole table,
+    cover.go:63-70). Returns (is_new, tables, offsets), identical on every rank."""
+    import torch
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1]) - 1
+    p_r, o_r = slice_csr(pcs, off, lo, hi)
+    m_r, mo_r = slice_csr(mc, mc_off, lo, hi)
+    flakes = np.asarray(flakes, np.uint32)
+    f_r = flakes[(flakes >= lo) & (flakes <= hi)]
+    is_new_r, tab_r, toff_r = run(p_r, o_r, group, ngroups, m_r, mo_r, f_r)
+    group = np.asarray(group, np.int64)
+    updated = np.zeros(ngroups, np.uint8)
+    if is_new_r.size:
+        np.maximum.at(updated, group[np.asarray(is_new_r, bool)], 1)
+    flags = torch.from_numpy(np.concatenate([np.asarray(is_new_r, np.uint8), updated]))
+    allreduce_max_u8(flags, dist)
+    is_new, updated = flags[:is_new_r.size].numpy(), flags[is_new_r.size:].numpy()
+    parts = [(tab_r, toff_r)]
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, (np.asarray(tab_r, np.uint32), np.asarray(toff_r, np.uint64)))
+    tabs, lens = [], np.zeros(ngroups, np.int64)
+    for g in range(ngroups):
+        t = np.concatenate([np.asarray(p[0][int(p[1][g]):int(p[1][g + 1])], np.uint32) for p in parts])
+        if updated[g]:
+            t = t[t != SENTINEL]
+        tabs.append(t)
+        lens[g] = t.size
+    toff = np.zeros(ngroups + 1, np.uint64)
+    np.cumsum(lens, out=toff[1:])
+    return is_new, (np.concatenate(tabs) if tabs else np.zeros(0, np.uint32)), toff

@@ -234,3 +234,176 @@ def test_key_parts_or_to_the_full_minimize_world2():
             assert np.array_equal(ids, w), (rank, g)
             seen.add(g)
     assert seen == set(np.unique(c.group).tolist())
+
+
+# ---- the bench's own plan: plan_parts' PC-range key split, end to end (world 2 and 4) -------------
+def _split_corpus():
+    # a dominant call group (17k of 30k entries): plan_parts splits it at world 2 and 4
+    return synth.corpus(0x5EED0011, 30_000, 3, 100_000, prog_len_max=40)
+
+
+def _raw_job_cpu(covers, lo, hi):
+    """CPU restatement of one rank's MinimizeJob on a call group (panels.hip with key_lo/key_hi):
+    Go-sort positions from the FULL cover lengths (every holder sorts the whole group), each cover
+    restricted to PCs in [lo, hi] (k_slices), a byte per sorted position = some restricted PC first
+    occurs there. Returns (sel by position, order: position -> member)."""
+    import oracle
+    lens = np.array([len(x) for x in covers], np.uint64)
+    order = oracle.minimize_order(lens)
+    sel = np.zeros(len(covers), np.uint8)
+    seen = set()
+    for pos, m in enumerate(order):
+        cov = covers[m]
+        part = cov[(cov >= lo) & (cov <= hi)]
+        if any(int(x) not in seen for x in part):
+            sel[pos] = 1
+        seen.update(int(x) for x in part)
+    return sel, order
+
+
+def _plan_rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = _split_corpus()
+        G = c.ngroups
+        # bench.py's plan, shard and key ranges
+        e, w = sharding.layout_stats(c.group, c.off, G)
+        plan = sharding.plan_parts(e, w, world)
+        ids = plan.local_entries(c.group, rank)
+        local = synth.Corpus(*_sub(c, ids), G)
+        key_lo, key_hi = plan.key_ranges(rank, sharding.split_bounds(plan, local, rank))
+        _, _, count_hist = plan.store_parts(rank)
+        gs, offs, nbytes = plan.split_groups()
+        buf = torch.zeros(max(nbytes, 1), dtype=torch.uint8)
+        jobs = {}
+        for g in range(G):
+            if not plan.held(rank)[g]:
+                continue
+            mem = np.nonzero(local.group == g)[0]
+            covers = [local.cover(int(i)) for i in mem]
+            sel, order = _raw_job_cpu(covers, int(key_lo[g]), int(key_hi[g]))
+            jobs[g] = (mem, sel, order)
+            if g in gs:  # export the split group's bytes (one per group-relative rank)
+                j = int(np.nonzero(gs == g)[0][0])
+                buf[int(offs[j]):int(offs[j]) + mem.size] = torch.from_numpy(sel)
+        sharding.allreduce_max_u8(buf, dist)
+        hist = torch.zeros(C + 1, dtype=torch.int64)
+        kept_primary = []
+        for g, (mem, sel, order) in jobs.items():
+            if g in gs:  # import: OR the other holders' bytes back
+                j = int(np.nonzero(gs == g)[0][0])
+                sel = np.maximum(sel, buf[int(offs[j]):int(offs[j]) + mem.size].numpy())
+            kept_local = mem[order[sel == 1]]  # selection order
+            if count_hist[g]:
+                hist += torch.from_numpy(np.bincount(local.prog_len[kept_local], minlength=C + 1).astype(np.int64))
+                kept_primary.append(ids[kept_local])
+        sharding.allreduce_hist(hist, dist)
+        kp = np.concatenate(kept_primary) if kept_primary else np.zeros(0, np.int64)
+        sel_all, goff = sharding.assemble_selection(kp, c.group, G, dist)
+        q.put((rank, hist.numpy().copy(), sel_all, goff, len(gs)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _sub(c, ids):
+    lens = np.diff(c.off)[ids].astype(np.uint64)
+    off = np.zeros(ids.size + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    pcs = np.concatenate([c.cover(int(i)) for i in ids]) if ids.size else np.zeros(0, np.uint32)
+    return pcs, off, c.group[ids], c.prog_len[ids]
+
+
+def _spawn(target, world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_plan_key_split_matches_single_process(world):
+    import oracle
+    res = _spawn(_plan_rank, world)
+    c = _split_corpus()
+    want, wgoff = oracle.minimize_grouped(c.pcs, c.off, c.group, c.ngroups)
+    want_hist = np.bincount(c.prog_len[want], minlength=C + 1)
+    for rank, hist, sel, goff, nsplit in res:
+        assert nsplit >= 1  # the plan really split a group
+        assert np.array_equal(hist, want_hist), rank
+        assert np.array_equal(goff, wgoff), rank
+        assert np.array_equal(sel, want), rank
+
+
+# ---- the new-coverage batch sharded by PC value (world 2 and 3) -------------------------------------
+def _novelty_inputs():
+    S = 0xFFFFFFFF
+    base = synth.corpus(0x5EED0012, 800, 13, 20_000)
+    fresh = synth.corpus(0x5EED0013, 4_000, 13, 20_000)
+    mc = []
+    for g in range(13):
+        ids = np.nonzero(base.group == g)[0]
+        t = np.unique(np.concatenate([base.cover(int(i)) for i in ids])) if ids.size else np.zeros(0, np.uint32)
+        if g % 5 == 0:
+            t = np.append(t[t != S], np.uint32(S))  # a table holding the sentinel
+        mc.append(t.astype(np.uint32))
+    import oracle
+    mcp, mco = oracle.to_csr(mc)
+    covs = [fresh.cover(i).copy() for i in range(fresh.n)]
+    for i in range(0, fresh.n, 29):
+        covs[i] = np.append(covs[i][covs[i] != S], np.uint32(S)).astype(np.uint32)
+    for i in range(3, fresh.n, 31):
+        covs[i] = np.zeros(0, np.uint32)
+    pcs, off = oracle.to_csr(covs)
+    flakes = np.unique(pcs[::53][pcs[::53] != S]).astype(np.uint32)
+    return pcs, off, fresh.group, 13, mcp, mco, flakes
+
+
+def _novelty_rank(rank, world, port, q):
+    import torch.distributed as dist
+    import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pcs, off, grp, G, mcp, mco, flakes = _novelty_inputs()
+        bounds = sharding.pc_bounds(pcs[::7], world)
+        out = sharding.novelty_shard(pcs, off, grp, G, mcp, mco, flakes, rank, world, bounds, oracle.novelty, dist)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_novelty_pc_space_shards_match_single_process(world):
+    import oracle
+    res = _spawn(_novelty_rank, world)
+    pcs, off, grp, G, mcp, mco, flakes = _novelty_inputs()
+    w_new, w_mc, w_off = oracle.novelty(pcs, off, grp, G, mcp, mco, flakes)
+    assert 0 < w_new.sum() < w_new.size
+    for rank, (is_new, tab, toff) in res:
+        assert np.array_equal(is_new, w_new), rank
+        assert np.array_equal(toff, w_off), rank
+        assert np.array_equal(tab, w_mc), rank
+
+
+def test_slice_csr_and_bounds():
+    pcs = np.array([1, 5, 9, 2, 3, 7, 0xFFFFFFFF], np.uint32)
+    off = np.array([0, 3, 3, 7], np.uint64)
+    p, o = sharding.slice_csr(pcs, off, 3, 8)
+    assert list(p) == [5, 3, 7] and list(o) == [0, 1, 1, 3]
+    p, o = sharding.slice_csr(pcs, off, 8, 0xFFFFFFFF)
+    assert list(p) == [9, 0xFFFFFFFF] and list(o) == [0, 1, 1, 2]
+    b = sharding.pc_bounds(np.arange(1000), 4)
+    assert b[0] == 0 and b[-1] == 1 << 32 and np.all(np.diff(b.astype(np.int64)) > 0)
