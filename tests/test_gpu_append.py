@@ -177,23 +177,36 @@ def test_keep_rejects_out_of_range_and_keeps_corpus():
 
 def test_key_parts_survive_append_and_keep():
     # set_parts is a property of the corpus: after an append and a keep the rebuilt index
-    # still runs only this rank's windows and counts only its groups, so two ranks' selections OR to the
-    # full one and their histograms add up to the full histogram
+    # still runs only this rank's windows and counts only its groups, so after the selection exchange
+    # (export, MAX, import) both ranks hold the full selection and their histograms add up to the full one
     c = synth.corpus(0x5EED00A6, 40_000, 9, 200_000)
     G, C = c.ngroups, int(c.prog_len.max())
     import torch
     s = torch.cuda.current_stream().cuda_stream
     nparts = np.full(G, 2, np.uint16)
-    ranks = []
+    stores = []
     for r in range(2):
         st = cover.CoverStore(*_part(c, 0, 25_000)[:3], G, _part(c, 0, 25_000)[3])
         st.set_parts(np.full(G, r, np.uint16), nparts, (np.arange(G) % 2 == r).astype(np.uint8))
         st.append(*_part(c, 25_000, 40_000))
         st.keep(np.arange(0, 40_000, 2))
         st.append(*_part(c, 1, 2))
+        st.minimize_begin(s)
+        stores.append(st)
+    # the selection exchange of every (split) group: export, MAX across the two "ranks", import
+    groups = np.arange(G, dtype=np.uint32)
+    ent = np.bincount(np.concatenate([c.group[0:40_000:2], c.group[1:2]]).astype(np.int64), minlength=G)
+    offs = np.zeros(G, np.uint64)
+    np.cumsum(ent[:-1], out=offs[1:])
+    bufs = [torch.zeros(int(ent.sum()), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    for st, b in zip(stores, bufs):
+        st.export_sel(groups, offs, b, s)
+    both = torch.maximum(bufs[0], bufs[1])
+    ranks = []
+    for st in stores:
+        st.import_sel(groups, offs, both, s)
         sel = torch.zeros(st.n, dtype=torch.uint8, device="cuda")
         hist = torch.zeros(C + 1, dtype=torch.int64, device="cuda")
-        st.minimize_begin(s)
         st.minimize_end(C, sel, hist, s)
         torch.cuda.synchronize()
         ranks.append((sel.cpu().numpy(), hist.cpu().numpy()))
@@ -205,5 +218,5 @@ def test_key_parts_survive_append_and_keep():
     want, _ = oracle.minimize_grouped(pcs, off, grp, G)
     wsel = np.zeros(len(hc.covs), np.uint8)
     wsel[want] = 1
-    assert np.array_equal(ranks[0][0] | ranks[1][0], wsel)
+    assert np.array_equal(ranks[0][0], wsel) and np.array_equal(ranks[1][0], wsel)
     assert np.array_equal(ranks[0][1] + ranks[1][1], np.bincount(pl[want], minlength=C + 1))
