@@ -324,7 +324,7 @@ def main():
             "novelty_config3": nov,
             "cover_analytics": ana,
             "hub_ingest_config5": hubr,
-            "store_append": app,
+            "manager_cycle": app,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -357,37 +357,54 @@ def store_leg(args, L, corp, d_pcs, d_off, d_grp, d_len, d_sel, d_hist, C, G, sp
 
 
 def append_leg(args, dev, store, sptr, C, d_hist):
-    """NewInput (manager.go:609-616) on the resident store: mgr.corpus = append(mgr.corpus, inputs) for
-    a batch of fresh programs (device-resident), then one minimizeCorpus over the grown store. The
-    append rebuilds the store on the device from its kept covers (syzgpu_corpus_append_dev)."""
+    """The manager's corpus cycle on the resident store: NewInput appends (manager.go:609-616,
+    mgr.corpus = append(...), in place, O(new)) of `--append` fresh programs in batches of 1000, then
+    minimizeCorpus with mgr.corpus = newCorpus (manager.go:507-529, syzgpu_corpus_minimize_keep_dev: the
+    raw pipeline, since the appends made the index stale, then the gather of the kept covers), then
+    CalculatePriorities + BuildChoiceTable on the kept length histogram. Two cycles; the second starts
+    from the first one's kept corpus."""
     import torch
     from syzkaller_amd import _lib, synth
+    L = _lib.lib()
     b = synth.corpus(args.seed + 0x40, args.append, args.ngroups, args.npcs)
 
     def t(a):
         view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64, np.dtype(np.uint16): np.int16}
         return torch.from_numpy(np.ascontiguousarray(a).view(view.get(a.dtype, a.dtype))).to(dev)
-    d = [t(b.pcs), t(b.off), t(b.group), t(b.prog_len)]
-    n0 = store.n
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    store.append_device(d[0], d[1], d[2], d[3], b.n, sptr)
-    torch.cuda.synchronize()
-    app_s = time.perf_counter() - t0
-    sel = torch.zeros(store.n, dtype=torch.uint8, device=dev)
-    t0 = time.perf_counter()
-    _lib.check(_lib.lib().syzgpu_corpus_minimize_dev(store.handle, C, sel.data_ptr(), d_hist.data_ptr(), sptr))
-    torch.cuda.synchronize()
-    first_ms = (time.perf_counter() - t0) * 1e3
-    t0 = time.perf_counter()
-    _lib.check(_lib.lib().syzgpu_corpus_minimize_dev(store.handle, C, sel.data_ptr(), d_hist.data_ptr(), sptr))
-    torch.cuda.synchronize()
-    again_ms = (time.perf_counter() - t0) * 1e3
-    return {"what": "syzgpu_corpus_append_dev of %d fresh programs onto the %d-program store, then "
-                    "minimizeCorpus over the grown store" % (b.n, n0),
-            "append_s": round(app_s, 4), "entries_after": int(store.n),
-            "kept_after": int(sel.sum().item()),
-            "minimize_ms_first": round(first_ms, 3), "minimize_ms": round(again_ms, 3)}
+    batch = 1000
+    parts = []
+    for a in range(0, b.n, batch):
+        e = min(b.n, a + batch)
+        o = b.off[a:e + 1].astype(np.uint64)
+        parts.append((t(b.pcs[int(o[0]):int(o[-1])]), t(o - o[0]), t(b.group[a:e]), t(b.prog_len[a:e]), e - a))
+    uses = static_usage(C)
+    d_uses = t(uses)
+    d_static = torch.empty((C, C), dtype=torch.float32, device=dev)
+    d_prios = torch.empty((C, C), dtype=torch.float32, device=dev)
+    d_run = torch.empty((C, C), dtype=torch.int64, device=dev)
+    cycles = []
+    for _ in range(2):
+        n0 = store.n
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for d in parts:
+            store.append_device(*d, sptr)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        kept = store.MinimizeKeep(C, None, d_hist, None, None, sptr)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        _lib.check(L.syzgpu_static_priorities_dev(d_uses.data_ptr(), uses.shape[0], C, d_static.data_ptr(), sptr))
+        _lib.check(L.syzgpu_prio_choice_dev(d_static.data_ptr(), d_hist.data_ptr(), C, None, d_prios.data_ptr(),
+                                            d_run.data_ptr(), None, sptr))
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        cycles.append({"entries_before": int(n0), "appended": int(b.n), "kept": int(kept),
+                       "append_ms": round((t1 - t0) * 1e3, 3), "minimize_keep_ms": round((t2 - t1) * 1e3, 3),
+                       "prio_ms": round((t3 - t2) * 1e3, 3), "cycle_ms": round((t3 - t0) * 1e3, 3)})
+    return {"what": "manager cycle on the resident store: %d NewInput appends of %d programs, minimizeCorpus + "
+                    "keep (mgr.corpus = newCorpus), CalculatePriorities + ChoiceTable; two cycles"
+                    % (len(parts), batch), "cycles": cycles}
 
 
 def text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step):

@@ -37,13 +37,23 @@ constexpr int PP_BLOCK = 1024;
 constexpr int PP_WAVES = PP_BLOCK / 64;
 constexpr int PP_U = 4;     // 64-PC tiles per wave in flight in k_part's passes
 constexpr int PP_TPW2 = 20;  // 64-PC tiles per wave in k_part2 (all in flight)
-constexpr uint32_t HS = 16384;   // open-addressing slots of a sparse-window table (128 KB with the ranks)
-constexpr uint32_t HCAP = 16384; // PCs per round of a sparse window (distinct keys <= PCs: at most full;
-                                 // calls repeat PCs, so tables are typically half full)
+#ifndef SYZ_HS_BITS
+#define SYZ_HS_BITS 14
+#endif
+constexpr uint32_t HS_BITS = SYZ_HS_BITS;
+constexpr uint32_t HS = 1u << HS_BITS;  // open-addressing slots of a sparse-window table (8 B each)
+#ifndef SYZ_HCAP
+#define SYZ_HCAP 16384
+#endif
+#ifndef SYZ_HTARGET
+#define SYZ_HTARGET 16384
+#endif
+constexpr uint32_t HCAP = SYZ_HCAP;  // PCs per round of a sparse window (distinct keys <= PCs: at most
+                                     // full; 8192 measured slower: every window is read twice)
 constexpr uint32_t HPROBE = 128; // a longer probe run means the table is full after all
 constexpr uint32_t HBM_WORDS = 2048;  // LDS winner bitmap of the sparse kernel (65536 ranks per pass)
 constexpr uint32_t DENSE = 8192;      // PCs per 32K-address window above which a call is direct-mode
-constexpr uint32_t HTARGET = 16384;   // PCs per window a sparse call's window size aims at
+constexpr uint32_t HTARGET = SYZ_HTARGET;  // PCs per window a sparse call's window size aims at
 
 
 // ---- per-entry statistics: PCs per call group and the PC span --------------------------------------
@@ -470,6 +480,160 @@ __global__ __launch_bounds__(PP_BLOCK) void k_part2(const uint32_t* __restrict__
   }
 }
 
+// ---- P, register form (k_part3): each PC read from HBM once ----------------------------------------
+// One workgroup per chunk, as k_part, but every wave loads all of its tiles' PCs into registers up
+// front (PP_TPW2 loads in flight per lane), so the second pass needs no second read; and the LDS
+// atomics of both passes are taken once per RUN: the 64 lanes of a tile hold consecutive PCs of one
+// (sorted) cover, so neighbouring lanes mostly share a window; a run's head lane adds the run's
+// length to the window's count (pass 1) or reserves its slots (pass 2) and the run's lanes write
+// consecutive LDS words. 74 KB of LDS: two workgroups per CU.
+struct TileRun {
+  uint32_t start, len;
+  bool head;
+};
+
+// lanes with `valid` (of a tile) and their window w: the maximal runs of equal w between invalid lanes
+__device__ __forceinline__ TileRun tile_run(uint32_t w, bool valid, unsigned lane) {
+  const uint32_t wp = __shfl_up(w, 1, 64);
+  const uint64_t vm = __ballot(valid);
+  const bool pv = lane > 0 && ((vm >> (lane - 1)) & 1ull);
+  const bool head = valid && (!pv || wp != w);
+  const uint64_t hm = __ballot(head);
+  const uint64_t le = (2ull << lane) - 1;  // lanes <= this one (all 64 for lane 63)
+  TileRun r;
+  r.head = head;
+  r.start = 63u - (uint32_t)__clzll(hm & le);
+  const uint64_t stop = (hm | ~vm) & ~le;
+  r.len = (stop ? (uint32_t)__ffsll((unsigned long long)stop) - 1u : 64u) - r.start;
+  return r;
+}
+
+// BLOCK threads per chunk; each wave holds TPW tiles of PCs in registers. 512 threads x 40 tiles:
+// two workgroups (74 KB of LDS each) share a CU, so one's dependent metadata loads overlap the
+// other's passes.
+template <int BLOCK, int TPW>
+__global__ __launch_bounds__(BLOCK) void k_part3(
+    const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
+    const uint64_t* __restrict__ mpos, const uint32_t* __restrict__ sbeg, const PChunk* chunks,
+    const uint64_t* nchunks_dev, const PGroup* pg, const uint64_t* gchunk, const uint64_t* gdesc, uint32_t lo,
+    uint32_t* __restrict__ elems, uint16_t* __restrict__ desc, int* err) {
+  constexpr int WAVES = BLOCK / 64;
+  static_assert(TMAX <= (uint32_t)(TPW * WAVES), "k_part3: tiles per wave");
+  __shared__ uint32_t obuf[PCAP];
+  __shared__ uint32_t hist[WMAX + 1];
+  __shared__ uint32_t tpre[MEMB + 1];
+  __shared__ uint32_t mlo[MEMB], mhi[MEMB];
+  __shared__ uint64_t mraw[MEMB];
+  __shared__ uint32_t red[WAVES + 1];
+  __shared__ uint4 tinfo[TMAX];
+  const uint64_t c = blockIdx.x;
+  if (c >= *nchunks_dev) return;
+  const int wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  const PChunk ch = chunks[c];
+  const PGroup gp = pg[ch.g];
+  const uint32_t S = gp.S, W = gp.W;
+  const uint32_t cb = ch.sub, ce = ch.sub + ch.len;
+  if (threadIdx.x < 64) {
+    const uint32_t m = threadIdx.x;
+    uint32_t nt = 0;
+    if (m < ch.nmem) {
+      const uint64_t p0 = mpos[ch.mb], a = mpos[ch.mb + m] - p0, b = mpos[ch.mb + m + 1] - p0;
+      const uint32_t x = (uint32_t)max<uint64_t>(a, cb), y = (uint32_t)min<uint64_t>(b, ce);
+      mlo[m] = x;
+      mhi[m] = y;
+      mraw[m] = off[members[ch.mb + m]] + (sbeg ? sbeg[ch.mb + m] : 0u) - a;
+      nt = y > x ? (y - x + 63) / 64 : 0;
+    }
+    const uint32_t inc = wave_incl_scan<uint32_t>(nt);
+    tpre[m] = inc - nt;
+    if (m == 63) tpre[64] = inc;
+  }
+  for (uint32_t i = threadIdx.x; i <= W; i += BLOCK) hist[i] = 0;
+  __syncthreads();
+  const uint32_t ntiles = tpre[64];
+  for (uint32_t t = threadIdx.x; t < ntiles; t += BLOCK) {
+    uint32_t lo_m = 0, hi_m = ch.nmem;  // largest m < nmem with tpre[m] <= t
+    while (hi_m - lo_m > 1) {
+      const uint32_t mid = (lo_m + hi_m) >> 1;
+      if (tpre[mid] <= t)
+        lo_m = mid;
+      else
+        hi_m = mid;
+    }
+    const uint32_t m = lo_m;
+    const uint32_t q0 = mlo[m] + (t - tpre[m]) * 64;
+    const uint64_t base = mraw[m] + q0;
+    tinfo[t] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), min(64u, mhi[m] - q0) | (m << 8), 0u);
+  }
+  __syncthreads();
+  // every tile of this wave: t = wv + WAVES k; its PCs into registers, all loads in flight
+  uint32_t v[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; k++) {
+    const uint32_t t = wv + WAVES * k;
+    v[k] = 0;
+    if (t < ntiles) {
+      const uint4 ti = tinfo[t];
+      if (lane < (ti.z & 0xFFu)) v[k] = pcs[(((uint64_t)ti.y << 32) | ti.x) + lane];
+    }
+  }
+  // pass 1: window histogram, one LDS atomic per run
+#pragma unroll
+  for (int k = 0; k < TPW; k++) {
+    const uint32_t t = wv + WAVES * k;
+    if (t >= ntiles) break;  // wave-uniform
+    const uint32_t cnt = tinfo[t].z & 0xFFu;
+    const uint32_t w = (v[k] - lo) >> S;
+    const bool in = lane < cnt;
+    if (in && w >= W) atomicOr(err, 1);  // outside [lo, hi]: an unsorted cover; redone on exact bounds
+    const TileRun r = tile_run(w, in && w < W, lane);
+    if (r.head) atomicAdd(&hist[w], r.len);
+  }
+  __syncthreads();
+  // window starts (exclusive scan) -> desc row and cursors
+  uint16_t* drow = desc + gdesc[ch.g] + (c - gchunk[ch.g]) * (uint64_t)(W + 1);
+  {
+    uint32_t run = 0;
+    for (uint32_t b0 = 0; b0 <= W; b0 += BLOCK) {
+      const uint32_t i = b0 + threadIdx.x;
+      const uint32_t x = i < W ? hist[i] : 0;
+      uint32_t tot;
+      const uint32_t pre = block_excl_scan<BLOCK>(x, red, &tot) + run;
+      if (i <= W) {
+        drow[i] = (uint16_t)pre;
+        hist[i] = pre;
+      }
+      run += tot;
+    }
+  }
+  __syncthreads();
+  // pass 2: element = offset in window | member tag, window-major into obuf, a run's slots reserved
+  // by its head
+  const uint32_t omask = (1u << S) - 1;
+#pragma unroll
+  for (int k = 0; k < TPW; k++) {
+    const uint32_t t = wv + WAVES * k;
+    if (t >= ntiles) break;
+    const uint32_t z = tinfo[t].z;
+    const uint32_t d = v[k] - lo, w = d >> S;
+    const bool in = lane < (z & 0xFFu) && w < W;
+    const TileRun r = tile_run(w, in, lane);
+    uint32_t base = r.head ? atomicAdd(&hist[w], r.len) : 0u;
+    base = (uint32_t)__shfl((int)base, (int)r.start, 64);
+    if (in) obuf[base + (lane - r.start)] = (d & omask) | ((z >> 8) << S);
+  }
+  __syncthreads();
+  uint32_t* dst = elems + ch.elem;
+  for (uint32_t i = threadIdx.x; i < ch.len; i += BLOCK) dst[i] = obuf[i];
+}
+
+#ifndef SYZ_P3_BLOCK
+#define SYZ_P3_BLOCK 512
+#endif
+constexpr int P3_BLOCK = SYZ_P3_BLOCK;
+constexpr int P3_TPW = (int)((TMAX + P3_BLOCK / 64 - 1) / (P3_BLOCK / 64));
+
 // Winners of a window table -> sel8[rank] = 1 with plain byte stores (no atomics: a byte written by
 // several tables is written with the same value). Ranks of call g lie in [gbase, gbase + ng); the
 // first BMW*32 of them are deduplicated through an LDS bitmap first, so each kept input costs one
@@ -510,7 +674,10 @@ __device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t 
 // ranks of the run's 64-member block into a register (lane m = member m), and the run's elements are
 // loaded one per lane; an element's rank is then a register shuffle by its member tag. RB runs'
 // loads are in flight together.
-constexpr int RB = 16;
+#ifndef SYZ_RB
+#define SYZ_RB 16
+#endif
+constexpr int RB = SYZ_RB;
 constexpr int TU = 4;  // slices in flight per long run
 template <class F>
 __device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* __restrict__ chunks,
@@ -590,7 +757,106 @@ __device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* _
   }
 }
 
-__global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
+// The same walk balanced by element tiles instead of runs: a window's runs are taken RUNB at a time;
+// their 64-element tiles are numbered (a workgroup scan in LDS) and every wave streams a contiguous
+// share of the tiles, TT tiles in flight per lane (one element load and one 256-byte rank-block load
+// each, independent), so a window of a few long runs (the sparse calls) keeps every wave and as many
+// loads in flight as one of thousands of short runs (the dense ones). `scratch` holds RUNB * 20 bytes
+// of LDS (the caller's winner bitmap, unused until the emit).
+constexpr uint32_t RUNB = 512;
+constexpr int TT = 8;
+template <class F>
+__device__ __forceinline__ void for_window_tiles(const PItem it, const PChunk* __restrict__ chunks,
+                                                 const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
+                                                 const uint16_t* __restrict__ desc,
+                                                 const uint32_t* __restrict__ elems,
+                                                 const uint32_t* __restrict__ rank_of_member, uint32_t nmem_total,
+                                                 uint32_t* scratch, uint32_t* red, F f) {
+  const uint32_t g = it.g, w = it.w;
+  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
+  const uint32_t W = pg[g].W, S = pg[g].S;
+  const uint32_t omask = (1u << S) - 1;
+  const uint16_t* d0 = desc + gdesc[g] + w;
+  uint64_t* relem = reinterpret_cast<uint64_t*>(scratch);  // RUNB (scratch is 16-byte aligned)
+  uint32_t* rstart = scratch + 2 * RUNB;                     // RUNB + 1
+  uint32_t* rlen = rstart + RUNB + 1;                        // RUNB
+  uint32_t* rmb = rlen + RUNB;                               // RUNB
+  const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  const uint32_t last_m = nmem_total ? nmem_total - 1 : 0;
+  for (uint64_t b0 = c0; b0 < c1; b0 += RUNB) {
+    const uint32_t nb = (uint32_t)min<uint64_t>(RUNB, c1 - b0);
+    uint32_t tiles = 0;
+    if (threadIdx.x < nb) {
+      const uint64_t c = b0 + threadIdx.x;
+      const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
+      const uint32_t s0 = d[0], len = (uint32_t)d[1] - s0;
+      rlen[threadIdx.x] = len;
+      relem[threadIdx.x] = chunks[c].elem + s0;
+      rmb[threadIdx.x] = chunks[c].mb;
+      tiles = (len + 63) / 64;
+    }
+    uint32_t T;
+    const uint32_t pre = block_excl_scan<1024>(tiles, red, &T);
+    if (threadIdx.x < nb) rstart[threadIdx.x] = pre;
+    if (threadIdx.x == 0) rstart[nb] = T;
+    __syncthreads();
+    // this wave's tiles [ta, tb), 64 at a time: lane l finds the run of tile tb0 + l (a binary search
+    // in LDS, all lanes at once), then the tiles are broadcast from their lanes, TT loads in flight
+    const uint32_t ta = (uint32_t)((uint64_t)T * wv / nw), tb = (uint32_t)((uint64_t)T * (wv + 1) / nw);
+    for (uint32_t tb0 = ta; tb0 < tb; tb0 += 64) {
+      const uint32_t t = tb0 + lane;
+      uint32_t r = 0, hi = nb;  // largest r < nb with rstart[r] <= t
+      while (hi - r > 1) {
+        const uint32_t mid = (r + hi) >> 1;
+        if (rstart[mid] <= t)
+          r = mid;
+        else
+          hi = mid;
+      }
+      const uint32_t k = (t - rstart[r]) * 64;
+      const uint32_t tcnt = t < tb ? min(64u, rlen[r] - k) : 0u;
+      const uint64_t taddr = relem[r] + k;
+      const uint32_t tmb = rmb[r];
+      const uint32_t ntl = min(64u, tb - tb0);
+      for (uint32_t u0 = 0; u0 < ntl; u0 += TT) {
+        uint32_t e[TT], rk[TT], cnt[TT];
+#pragma unroll
+        for (int u = 0; u < TT; u++) {
+          const uint32_t jl = u0 + u;  // wave-uniform lane index
+          cnt[u] = jl < ntl ? (uint32_t)__builtin_amdgcn_readlane((int)tcnt, (int)jl) : 0u;
+          e[u] = 0;
+          rk[u] = 0;
+          if (cnt[u]) {
+            const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(taddr >> 32), (int)jl)
+                                << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)taddr, (int)jl);
+            const uint32_t mb = (uint32_t)__builtin_amdgcn_readlane((int)tmb, (int)jl);
+            rk[u] = rank_of_member[min(mb + lane, last_m)];
+            if (lane < cnt[u]) e[u] = elems[a + lane];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < TT; u++) {
+          const uint32_t R = (uint32_t)__shfl((int)rk[u], (int)(e[u] >> S), 64);
+          if (lane < cnt[u]) f(e[u] & omask, R);
+        }
+      }
+    }
+    __syncthreads();  // the run table is rewritten by the next batch
+  }
+}
+
+static bool pmin_tiles() {
+  static const bool v = getenv("SYZGPU_PMIN_TILES") && atoi(getenv("SYZGPU_PMIN_TILES")) != 0;
+  return v;
+}
+
+#ifndef SYZ_PMIN_WPE
+#define SYZ_PMIN_WPE 1  // waves per SIMD the first-occurrence kernels' registers aim at (8: 2 per CU)
+#endif
+template <bool TILES>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_PMIN_WPE, 8))) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
                                                       const uint64_t* gchunk, const uint64_t* gdesc,
                                                       const PGroup* pg, const uint16_t* __restrict__ desc,
                                                       const uint32_t* __restrict__ elems,
@@ -598,17 +864,23 @@ __global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const 
                                                       uint32_t nmem_total, const uint64_t* gstart,
                                                       uint8_t* sel8, int dbg) {
   __shared__ uint32_t tab[1u << DS];
-  __shared__ uint32_t bm[BM_WORDS];
+  __shared__ __align__(16) uint32_t bm[BM_WORDS];  // also the tile walk's run table until the emit
+  __shared__ uint32_t red[1024 / 64 + 1];
+  static_assert(BM_WORDS >= RUNB * 5 + 1, "run table in the bitmap");
   const PItem it = items[blockIdx.x];
   for (uint32_t i = threadIdx.x; i < (1u << DS); i += 1024) tab[i] = RANK_NONE;
   __syncthreads();
   uint32_t acc = 0;
-  for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, [&](uint32_t o, uint32_t R) {
+  auto upd = [&](uint32_t o, uint32_t R) {
     if (dbg & 1)
       acc ^= o * 31 + R;
     else if (tab[o] > R)
       atomicMin(&tab[o], R);
-  });
+  };
+  if constexpr (TILES)
+    for_window_tiles(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, bm, red, upd);
+  else
+    for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, upd);
   __syncthreads();
   if (acc == 0x9E3779B9u) sel8[0] = 1;
   if (dbg & 2) return;
@@ -630,23 +902,28 @@ __device__ uint32_t window_elem_count(const PItem it, const uint64_t* gchunk, co
   return block_sum<1024>(s, red);
 }
 
-__device__ __forceinline__ uint32_t hslot14(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - 14); }
-static_assert(HS == 16384, "hslot14");
+__device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - HS_BITS); }
 
 // Sparse windows: open addressing keyed by the window offset, kept at most half full: a window with
 // more than HCAP PCs is done in R = ceil(PCs / HCAP) rounds, each taking the keys of one residue of
 // another hash (so each round holds at most about HCAP distinct keys). A probe run longer than
 // HPROBE means the table is full after all: every round is redone with twice as many; a winner
 // marked by a finished round stays valid (marks are idempotent stores of exact winners).
-__global__ __launch_bounds__(1024) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
+#ifndef SYZ_PMIN_WPE
+#define SYZ_PMIN_WPE 1  // waves per SIMD the first-occurrence kernels' registers aim at (8: 2 per CU)
+#endif
+template <bool TILES>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_PMIN_WPE, 8))) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
                                                     const uint64_t* gchunk, const uint64_t* gdesc,
                                                     const PGroup* pg, const uint16_t* __restrict__ desc,
                                                     const uint32_t* __restrict__ elems,
                                                     const uint32_t* __restrict__ rank_of_member,
-                                                    uint32_t nmem_total, const uint64_t* gstart, uint8_t* sel8) {
+                                                    uint32_t nmem_total, const uint64_t* gstart, uint8_t* sel8,
+                                                    int dbg) {
   __shared__ uint32_t keys[HS];
   __shared__ uint32_t vals[HS];
   __shared__ uint32_t bm[HBM_WORDS];
+  __shared__ __align__(16) uint32_t rtab[RUNB * 5 + 1];  // the tile walk's run table
   __shared__ uint32_t red[1024 / 64 + 1];
   __shared__ int full;
   const PItem it = items[blockIdx.x];
@@ -662,10 +939,14 @@ __global__ __launch_bounds__(1024) void k_pmin_hash(const PItem* items, const PC
     if (threadIdx.x == 0) full = 0;
     __syncthreads();
     const uint32_t RR = R, rr = round;
-    for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16,
-                     [&](uint32_t o, uint32_t Rk) {
+    uint32_t acc = 0;
+    auto upd = [&](uint32_t o, uint32_t Rk) {
+                       if (dbg & 64) {
+                         acc ^= o * 31 + Rk;
+                         return;
+                       }
                        if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
-                       uint32_t h = hslot14(o);
+                       uint32_t h = hslot(o);
                        for (uint32_t probes = 0; probes < HPROBE; probes++) {
                          uint32_t k = keys[h];
                          if (k == 0xFFFFFFFFu) {
@@ -679,7 +960,12 @@ __global__ __launch_bounds__(1024) void k_pmin_hash(const PItem* items, const PC
                          h = (h + 1) & (HS - 1);
                        }
                        full = 1;
-                     });
+                     };
+    if constexpr (TILES)
+      for_window_tiles(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, rtab, red, upd);
+    else
+      for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, upd);
+    if (acc == 0x9E3779B9u) sel8[0] = 1;
     __syncthreads();
     if (full) {
       R *= 2;
@@ -784,14 +1070,15 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
 
 // diagnostic switches (SYZGPU_PM_DBG, timing experiments only; results are wrong when set):
 // 1 = direct tables not updated, 2 = no winner emit, 4 = no open-addressing windows,
-// 8 = P without its second pass, 16 = P without the element stores
+// 8 = P without its second pass, 16 = P without the element stores, 64 = sparse windows walked but
+// not probed
 static unsigned part_grid() {
   static const unsigned v = getenv("SYZGPU_PART_GRID") ? (unsigned)atoi(getenv("SYZGPU_PART_GRID")) : (1u << 30);
   return v ? v : 1u;
 }
 
 static int part_kind() {
-  static const int v = getenv("SYZGPU_PART") ? atoi(getenv("SYZGPU_PART")) : 1;
+  static const int v = getenv("SYZGPU_PART") ? atoi(getenv("SYZGPU_PART")) : 3;
   return v;
 }
 
@@ -1023,6 +1310,9 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, std::min<unsigned>(part_grid(), c.ncu));
       k_part2<<<grid, PP_BLOCK, 0, pq>>>(a.pcs, chunks, cstart + B, tiles, ntiles, dpg, gchunk, gdesc, lo, elems,
                                          desc, err);
+    } else if (part_kind() == 3) {
+      k_part3<P3_BLOCK, P3_TPW><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg,
+                                                        gchunk, gdesc, lo, elems, desc, err);
     } else {
       const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, part_grid());
       k_part<<<grid, PP_BLOCK, 0, pq>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc,
@@ -1042,13 +1332,15 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     SYZ_HIP(hipStreamWaitEvent(q, c.ev_part1, 0));
     ProfScope ps(tag, q, 0);
     if (nd) {
-      k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + first_d, chunks, gchunk, gdesc, dpg, desc, elems,
-                                                  rank_of_member, (uint32_t)n, gstart, sel8, pm_dbg());
+      auto* kd = pmin_tiles() ? k_pmin_direct<true> : k_pmin_direct<false>;
+      kd<<<(unsigned)nd, 1024, 0, q>>>(ditems + first_d, chunks, gchunk, gdesc, dpg, desc, elems, rank_of_member,
+                                       (uint32_t)n, gstart, sel8, pm_dbg());
       SYZ_LAUNCHED();
     }
     if (nh && !(pm_dbg() & 4)) {
-      k_pmin_hash<<<(unsigned)nh, 1024, 0, q>>>(ditems + first_h, chunks, gchunk, gdesc, dpg, desc, elems,
-                                                    rank_of_member, (uint32_t)n, gstart, sel8);
+      auto* kh = pmin_tiles() ? k_pmin_hash<true> : k_pmin_hash<false>;
+      kh<<<(unsigned)nh, 1024, 0, q>>>(ditems + first_h, chunks, gchunk, gdesc, dpg, desc, elems, rank_of_member,
+                                       (uint32_t)n, gstart, sel8, pm_dbg());
       SYZ_LAUNCHED();
     }
   };
