@@ -1488,10 +1488,13 @@ void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ng
   SYZ_HIP(hipMalloc(&P.small, (small.size() + 1) * sizeof(Seg)));
   SYZ_HIP(hipMalloc(&P.packs, (packs.size() + 1) * sizeof(Pack)));
   SYZ_HIP(hipMalloc(&P.big, (big.size() + 1) * sizeof(Seg)));
-  if (!small.empty()) SYZ_HIP(hipMemcpy(P.small, small.data(), small.size() * sizeof(Seg), hipMemcpyHostToDevice));
-  if (!packs.empty()) SYZ_HIP(hipMemcpy(P.packs, packs.data(), packs.size() * sizeof(Pack), hipMemcpyHostToDevice));
-  if (!big.empty()) SYZ_HIP(hipMemcpy(P.big, big.data(), big.size() * sizeof(Seg), hipMemcpyHostToDevice));
-  (void)s;
+  // on the caller's stream, never the legacy one: another thread's graph capture may be running
+  if (!small.empty())
+    SYZ_HIP(hipMemcpyAsync(P.small, small.data(), small.size() * sizeof(Seg), hipMemcpyHostToDevice, s));
+  if (!packs.empty())
+    SYZ_HIP(hipMemcpyAsync(P.packs, packs.data(), packs.size() * sizeof(Pack), hipMemcpyHostToDevice, s));
+  if (!big.empty()) SYZ_HIP(hipMemcpyAsync(P.big, big.data(), big.size() * sizeof(Seg), hipMemcpyHostToDevice, s));
+  SYZ_HIP(hipStreamSynchronize(s));  // the host vectors are temporaries
 }
 
 void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const std::vector<uint64_t>& hstart, uint32_t ngroups,

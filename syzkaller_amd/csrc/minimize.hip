@@ -1099,7 +1099,8 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   }
   if (n && prog_len) {  // len(p.Calls) > C is rejected per call without a device round trip
     std::vector<uint16_t> hl(n);
-    SYZ_HIP(hipMemcpy(hl.data(), prog_len, n * 2, hipMemcpyDeviceToHost));
+    SYZ_HIP(hipMemcpyAsync(hl.data(), prog_len, n * 2, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
     K.max_prog_len = *std::max_element(hl.begin(), hl.end());
   }
   return cp.release();

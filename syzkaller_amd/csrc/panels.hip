@@ -38,7 +38,7 @@ constexpr int PP_WAVES = PP_BLOCK / 64;
 constexpr int PP_U = 4;     // 64-PC tiles per wave in flight in k_part's passes
 constexpr int PP_TPW2 = 20;  // 64-PC tiles per wave in k_part2 (all in flight)
 #ifndef SYZ_HS_BITS
-#define SYZ_HS_BITS 14
+#define SYZ_HS_BITS 13
 #endif
 constexpr uint32_t HS_BITS = SYZ_HS_BITS;
 constexpr uint32_t HS = 1u << HS_BITS;  // open-addressing slots of a sparse-window table (8 B each)
@@ -46,10 +46,11 @@ constexpr uint32_t HS = 1u << HS_BITS;  // open-addressing slots of a sparse-win
 #define SYZ_HCAP 16384
 #endif
 #ifndef SYZ_HTARGET
-#define SYZ_HTARGET 16384
+#define SYZ_HTARGET 8192
 #endif
-constexpr uint32_t HCAP = SYZ_HCAP;  // PCs per round of a sparse window (distinct keys <= PCs: at most
-                                     // full; 8192 measured slower: every window is read twice)
+constexpr uint32_t HCAP = SYZ_HCAP;  // PCs per round of a sparse window: twice the slots, i.e. the table
+                                     // fills only if no PC repeats (then the probe limit redoes the
+                                     // window in more rounds); a tighter cap reads most windows twice
 constexpr uint32_t HPROBE = 128; // a longer probe run means the table is full after all
 constexpr uint32_t HBM_WORDS = 2048;  // LDS winner bitmap of the sparse kernel (65536 ranks per pass)
 constexpr uint32_t DENSE = 8192;      // PCs per 32K-address window above which a call is direct-mode
@@ -679,7 +680,7 @@ __device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t 
 #endif
 constexpr int RB = SYZ_RB;
 constexpr int TU = 4;  // slices in flight per long run
-template <class F>
+template <int RBN = RB, class F>
 __device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* __restrict__ chunks,
                                                  const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
                                                  const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems,
@@ -709,11 +710,11 @@ __device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* _
       mb = chunks[c].mb;
     }
     const uint32_t nr = (uint32_t)min<uint64_t>(64, (nrun - b0 + nwaves - 1) / nwaves);
-    for (uint32_t r0 = 0; r0 < nr; r0 += RB) {
-      uint32_t rk[RB], e0[RB], e1[RB], ln[RB];
-      uint64_t sts[RB];
+    for (uint32_t r0 = 0; r0 < nr; r0 += RBN) {
+      uint32_t rk[RBN], e0[RBN], e1[RBN], ln[RBN];
+      uint64_t sts[RBN];
 #pragma unroll
-      for (int r = 0; r < RB; r++) {
+      for (int r = 0; r < RBN; r++) {
         const uint32_t j = r0 + r;
         ln[r] = j < nr ? (uint32_t)__builtin_amdgcn_readlane((int)len, (int)j) : 0u;
         const uint32_t mbj = (uint32_t)__builtin_amdgcn_readlane((int)mb, (int)j);
@@ -729,7 +730,7 @@ __device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* _
         }
       }
 #pragma unroll
-      for (int r = 0; r < RB; r++) {
+      for (int r = 0; r < RBN; r++) {
         if (!ln[r]) continue;
         {
           const uint32_t R = (uint32_t)__shfl((int)rk[r], (int)(e0[r] >> S), 64);
@@ -852,11 +853,8 @@ static bool pmin_tiles() {
   return v;
 }
 
-#ifndef SYZ_PMIN_WPE
-#define SYZ_PMIN_WPE 1  // waves per SIMD the first-occurrence kernels' registers aim at (8: 2 per CU)
-#endif
 template <bool TILES>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_PMIN_WPE, 8))) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
+__global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
                                                       const uint64_t* gchunk, const uint64_t* gdesc,
                                                       const PGroup* pg, const uint16_t* __restrict__ desc,
                                                       const uint32_t* __restrict__ elems,
@@ -909,11 +907,16 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 // another hash (so each round holds at most about HCAP distinct keys). A probe run longer than
 // HPROBE means the table is full after all: every round is redone with twice as many; a winner
 // marked by a finished round stays valid (marks are idempotent stores of exact winners).
-#ifndef SYZ_PMIN_WPE
-#define SYZ_PMIN_WPE 1  // waves per SIMD the first-occurrence kernels' registers aim at (8: 2 per CU)
+// 72 KB of LDS at 8192 slots: two workgroups per CU (registers held to 64 per lane, 4 runs in
+// flight per wave), so one window's table init and emit overlap the other's loads
+#ifndef SYZ_HASH_RB
+#define SYZ_HASH_RB 4
+#endif
+#ifndef SYZ_HASH_WPE
+#define SYZ_HASH_WPE 8
 #endif
 template <bool TILES>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_PMIN_WPE, 8))) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_HASH_WPE, 8))) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
                                                     const uint64_t* gchunk, const uint64_t* gdesc,
                                                     const PGroup* pg, const uint16_t* __restrict__ desc,
                                                     const uint32_t* __restrict__ elems,
@@ -964,7 +967,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_PMIN_W
     if constexpr (TILES)
       for_window_tiles(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, rtab, red, upd);
     else
-      for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, upd);
+      for_window_elems<SYZ_HASH_RB>(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, upd);
     if (acc == 0x9E3779B9u) sel8[0] = 1;
     __syncthreads();
     if (full) {

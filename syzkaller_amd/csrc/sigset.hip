@@ -42,10 +42,12 @@ struct SigSet {
     SYZ_HIP(hipMalloc(&owner, c * 4));
     SYZ_HIP(hipMalloc(&seq, c * 8));
     SYZ_HIP(hipMalloc(&dead, c * 4));
-    SYZ_HIP(hipMemset(tag, 0, c * 8));
-    SYZ_HIP(hipMemset(claim, 0, c * 4));
-    SYZ_HIP(hipMemset(owner, 0xFF, c * 4));
-    SYZ_HIP(hipMemset(dead, 0, c * 4));
+    hipStream_t s = ctx().stream;  // stream-ordered: another thread's graph capture may be running
+    SYZ_HIP(hipMemsetAsync(tag, 0, c * 8, s));
+    SYZ_HIP(hipMemsetAsync(claim, 0, c * 4, s));
+    SYZ_HIP(hipMemsetAsync(owner, 0xFF, c * 4, s));
+    SYZ_HIP(hipMemsetAsync(dead, 0, c * 4, s));
+    SYZ_HIP(hipStreamSynchronize(s));
   }
   void free_all() {
     for (void* p : {(void*)tag, (void*)key, (void*)claim, (void*)owner, (void*)seq, (void*)dead})
