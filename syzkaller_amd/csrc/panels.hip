@@ -28,15 +28,30 @@
 
 namespace syz {
 
-constexpr uint32_t PCAP = 16384;  // PCs per chunk (the LDS staging buffer of k_part)
+#ifndef SYZ_PCAP
+#define SYZ_PCAP 16384
+#endif
+constexpr uint32_t PCAP = SYZ_PCAP;  // PCs per chunk (the LDS staging buffer of the transpose)
 constexpr uint32_t MEMB = 64;     // members per block: a 6-bit member tag in each element
 constexpr uint32_t WMAX = 1024;   // windows per call group
-constexpr uint32_t DS = 15;       // direct-mode window bits: a 32768-entry u32 min table
+#ifndef SYZ_DS
+#define SYZ_DS 15
+#endif
+#ifndef SYZ_PBM_WORDS
+#define SYZ_PBM_WORDS 6144
+#endif
+#ifndef SYZ_DIRECT_RB
+#define SYZ_DIRECT_RB 16
+#endif
+#ifndef SYZ_DIRECT_WPE
+#define SYZ_DIRECT_WPE 1
+#endif
+constexpr uint32_t DS = SYZ_DS;  // direct-mode window bits: a 2^DS-entry u32 min table
+constexpr uint32_t PBM_WORDS = SYZ_PBM_WORDS;  // LDS winner bitmap of the direct kernel
 constexpr uint32_t SMAX = 26;     // 32 - 6 tag bits
 constexpr int PP_BLOCK = 1024;
 constexpr int PP_WAVES = PP_BLOCK / 64;
 constexpr int PP_U = 4;     // 64-PC tiles per wave in flight in k_part's passes
-constexpr int PP_TPW2 = 20;  // 64-PC tiles per wave in k_part2 (all in flight)
 #ifndef SYZ_HS_BITS
 #define SYZ_HS_BITS 13
 #endif
@@ -53,7 +68,7 @@ constexpr uint32_t HCAP = SYZ_HCAP;  // PCs per round of a sparse window: twice 
                                      // window in more rounds); a tighter cap reads most windows twice
 constexpr uint32_t HPROBE = 128; // a longer probe run means the table is full after all
 constexpr uint32_t HBM_WORDS = 2048;  // LDS winner bitmap of the sparse kernel (65536 ranks per pass)
-constexpr uint32_t DENSE = 8192;      // PCs per 32K-address window above which a call is direct-mode
+constexpr uint32_t DENSE = 8192u >> (15 - DS);  // PCs per window (per 32K addresses: 8192) above which a call is direct-mode
 constexpr uint32_t HTARGET = SYZ_HTARGET;  // PCs per window a sparse call's window size aims at
 
 
@@ -303,187 +318,11 @@ __global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))
   }
 }
 
-// ---- P, pipelined form (k_part2): tile tables precomputed, one persistent workgroup per CU ----------
-// k_tiles: a wave per chunk writes its tile table (raw address, valid lanes | member tag << 8, chunk
-// position of the tile's first PC) into a fixed TMAX-entry slot. k_part2 keeps three chunks in flight:
-// while chunk c is rewritten LDS-to-LDS and stored, the PCs of chunk c+G are loading into registers
-// and the tile table of chunk c+2G into LDS (G = grid), so each CU streams HBM while it works in LDS.
 constexpr uint32_t TMAX = PCAP / 64 + MEMB;  // tiles per chunk
-static_assert(TMAX <= PP_TPW2 * (PP_BLOCK / 64), "k_part2: tiles per wave");
-
-__global__ __launch_bounds__(256) void k_tiles(const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
-                                               const uint64_t* __restrict__ mpos, const uint32_t* __restrict__ sbeg,
-                                               const PChunk* chunks, const uint64_t* nchunks_dev, uint4* tiles,
-                                               uint32_t* ntiles) {
-  const uint64_t nch = *nchunks_dev;
-  const unsigned lane = __lane_id();
-  for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nch;
-       c += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
-    const PChunk ch = chunks[c];
-    const uint32_t cb = ch.sub, ce = ch.sub + ch.len;
-    const uint32_t m = lane;
-    uint32_t nt = 0, x = 0, y = 0;
-    uint64_t raw = 0;
-    if (m < ch.nmem) {
-      const uint64_t p0 = mpos[ch.mb], a = mpos[ch.mb + m] - p0, b = mpos[ch.mb + m + 1] - p0;
-      x = (uint32_t)max<uint64_t>(a, cb);
-      y = (uint32_t)min<uint64_t>(b, ce);
-      raw = off[members[ch.mb + m]] + (sbeg ? sbeg[ch.mb + m] : 0u) - a;
-      nt = y > x ? (y - x + 63) / 64 : 0;
-    }
-    const uint32_t inc = wave_incl_scan<uint32_t>(nt);
-    const uint32_t pre = inc - nt;
-    const uint32_t total = __shfl(inc, 63, 64);
-    if (lane == 0) ntiles[c] = total;
-    uint4* tc = tiles + c * TMAX;
-    for (uint32_t t0 = 0; t0 < total; t0 += 64) {  // wave-uniform: the shuffles need every lane
-      const uint32_t t = t0 + lane;
-      uint32_t j = 0;  // the last member whose tiles start at or before t
-#pragma unroll
-      for (int s = 32; s >= 1; s >>= 1) {
-        const uint32_t pj = __shfl(pre, (int)(j + s) & 63, 64);
-        if (j + s < ch.nmem && pj <= t) j += s;
-      }
-      const uint32_t xj = __shfl(x, (int)j, 64), yj = __shfl(y, (int)j, 64), pj = __shfl(pre, (int)j, 64);
-      const uint64_t rj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(raw >> 32), (int)j, 64) << 32) |
-                          (uint32_t)__shfl((int)(uint32_t)raw, (int)j, 64);
-      const uint32_t q0 = xj + (t - pj) * 64;
-      const uint64_t base = rj + q0;
-      if (t < total) tc[t] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), min(64u, yj - q0) | (j << 8), q0 - cb);
-    }
-  }
-}
-
-struct PHead {  // the chunk a tile-table buffer holds
-  uint64_t elem, drow;
-  uint32_t S, W, len, nt, g, pad;
-};
-
-__global__ __launch_bounds__(PP_BLOCK) void k_part2(const uint32_t* __restrict__ pcs, const PChunk* chunks,
-                                                    const uint64_t* nchunks_dev, const uint4* __restrict__ tiles,
-                                                    const uint32_t* __restrict__ ntiles_c, const PGroup* pg,
-                                                    const uint64_t* gchunk, const uint64_t* gdesc, uint32_t lo,
-                                                    uint32_t* __restrict__ elems, uint16_t* __restrict__ desc,
-                                                    int* err) {
-  __shared__ uint32_t ibuf[PCAP];
-  __shared__ uint32_t obuf[PCAP];
-  __shared__ uint32_t hist[WMAX + 1];
-  __shared__ uint4 tt[3][TMAX];
-  __shared__ PHead hd[3];
-  __shared__ uint32_t red[PP_WAVES + 1];
-  const uint64_t nch = *nchunks_dev;
-  const int wv = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  const uint64_t G = gridDim.x;
-  // tile table + header of chunk cc into buffer b (every thread takes part; no barrier inside)
-  auto load_table = [&](uint64_t cc, int b) {
-    if (cc >= nch) return;
-    const uint32_t nt = ntiles_c[cc];
-    const uint4* src = tiles + cc * TMAX;
-    for (uint32_t t = threadIdx.x; t < nt; t += PP_BLOCK) tt[b][t] = src[t];
-    if (threadIdx.x == 0) {
-      const PChunk ch = chunks[cc];
-      const PGroup gp = pg[ch.g];
-      hd[b] = PHead{ch.elem, gdesc[ch.g] + (cc - gchunk[ch.g]) * (uint64_t)(gp.W + 1), gp.S, gp.W, ch.len, nt, ch.g, 0};
-    }
-  };
-  uint64_t c = blockIdx.x;
-  if (c >= nch) return;
-  for (uint32_t i = threadIdx.x; i <= WMAX; i += PP_BLOCK) hist[i] = 0;
-  load_table(c, 0);
-  load_table(c + G, 1);
-  __syncthreads();
-  uint32_t v[PP_TPW2];
-  {  // PCs of the first chunk: tile t = wv + PP_WAVES k of this wave
-    constexpr int B_ = 0;
-    const uint32_t nt_ = hd[B_].nt;
-#pragma unroll
-    for (int k = 0; k < PP_TPW2; k++) {
-      const uint32_t t = wv + PP_WAVES * k;
-      v[k] = 0;
-      if (t < nt_) {
-        const uint4 ti = tt[B_][t];
-        if (lane < (ti.z & 0xFFu)) v[k] = pcs[(((uint64_t)ti.y << 32) | ti.x) + lane];
-      }
-    }
-  }
-#pragma nounroll
-  for (uint32_t it = 0;; it++) {
-    const int b = (int)(it % 3), b1 = (int)((it + 1) % 3), b2 = (int)((it + 2) % 3);
-    const PHead h = hd[b];
-    const uint32_t S = h.S, W = h.W;
-    // pass 1: the chunk's PCs (registers) -> ibuf at their chunk positions, window histogram
-#pragma unroll
-    for (int k = 0; k < PP_TPW2; k++) {
-      const uint32_t t = wv + PP_WAVES * k;
-      if (t < h.nt) {
-        const uint4 ti = tt[b][t];
-        if (lane < (ti.z & 0xFFu)) {
-          ibuf[ti.w + lane] = v[k];
-          const uint32_t w = (v[k] - lo) >> S;
-          if (w < W)
-            atomicAdd(&hist[w], 1u);
-          else
-            atomicOr(err, 1);  // outside [lo, hi]: an unsorted cover; redone on exact bounds
-        }
-      }
-    }
-    load_table(c + 2 * G, b2);
-    __syncthreads();
-    // the next chunk's PCs start loading while this one is scanned, rewritten and stored
-    uint32_t vn[PP_TPW2];
-    {
-      const uint32_t nt_ = c + G < nch ? hd[b1].nt : 0u;
-#pragma unroll
-      for (int k = 0; k < PP_TPW2; k++) {
-        const uint32_t t = wv + PP_WAVES * k;
-        vn[k] = 0;
-        if (t < nt_) {
-          const uint4 ti = tt[b1][t];
-          if (lane < (ti.z & 0xFFu)) vn[k] = pcs[(((uint64_t)ti.y << 32) | ti.x) + lane];
-        }
-      }
-    }
-    {
-      uint16_t* drow = desc + h.drow;
-      uint32_t run = 0;
-      for (uint32_t b0 = 0; b0 <= W; b0 += PP_BLOCK) {
-        const uint32_t i = b0 + threadIdx.x;
-        const uint32_t x = i < W ? hist[i] : 0;
-        uint32_t tot;
-        const uint32_t pre = block_excl_scan<PP_BLOCK>(x, red, &tot) + run;
-        if (i <= W) {
-          drow[i] = (uint16_t)pre;
-          hist[i] = pre;
-        }
-        run += tot;
-      }
-    }
-    __syncthreads();
-    // pass 2: element = offset in window | member tag, window-major into obuf
-    const uint32_t omask = (1u << S) - 1;
-    for (uint32_t t = wv; t < h.nt; t += PP_WAVES) {
-      const uint4 ti = tt[b][t];
-      if (lane < (ti.z & 0xFFu)) {
-        const uint32_t d = ibuf[ti.w + lane] - lo, w = d >> S;
-        if (w < W) obuf[atomicAdd(&hist[w], 1u)] = (d & omask) | ((ti.z >> 8) << S);
-      }
-    }
-    __syncthreads();
-    uint32_t* dst = elems + h.elem;
-    for (uint32_t i = threadIdx.x; i < h.len; i += PP_BLOCK) dst[i] = obuf[i];
-    for (uint32_t i = threadIdx.x; i <= W; i += PP_BLOCK) hist[i] = 0;
-    __syncthreads();
-    c += G;
-    if (c >= nch) break;
-#pragma unroll
-    for (int k = 0; k < PP_TPW2; k++) v[k] = vn[k];
-  }
-}
 
 // ---- P, register form (k_part3): each PC read from HBM once ----------------------------------------
 // One workgroup per chunk, as k_part, but every wave loads all of its tiles' PCs into registers up
-// front (PP_TPW2 loads in flight per lane), so the second pass needs no second read; and the LDS
+// front (all of them in flight per lane), so the second pass needs no second read; and the LDS
 // atomics of both passes are taken once per RUN: the 64 lanes of a tile hold consecutive PCs of one
 // (sorted) cover, so neighbouring lanes mostly share a window; a run's head lane adds the run's
 // length to the window's count (pass 1) or reserves its slots (pass 2) and the run's lanes write
@@ -854,7 +693,7 @@ static bool pmin_tiles() {
 }
 
 template <bool TILES>
-__global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_DIRECT_WPE, 8))) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
                                                       const uint64_t* gchunk, const uint64_t* gdesc,
                                                       const PGroup* pg, const uint16_t* __restrict__ desc,
                                                       const uint32_t* __restrict__ elems,
@@ -862,9 +701,9 @@ __global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const 
                                                       uint32_t nmem_total, const uint64_t* gstart,
                                                       uint8_t* sel8, int dbg) {
   __shared__ uint32_t tab[1u << DS];
-  __shared__ __align__(16) uint32_t bm[BM_WORDS];  // also the tile walk's run table until the emit
+  __shared__ __align__(16) uint32_t bm[PBM_WORDS];  // also the tile walk's run table until the emit
   __shared__ uint32_t red[1024 / 64 + 1];
-  static_assert(BM_WORDS >= RUNB * 5 + 1, "run table in the bitmap");
+  static_assert(PBM_WORDS >= RUNB * 5 + 1, "run table in the bitmap");
   const PItem it = items[blockIdx.x];
   for (uint32_t i = threadIdx.x; i < (1u << DS); i += 1024) tab[i] = RANK_NONE;
   __syncthreads();
@@ -878,12 +717,12 @@ __global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const 
   if constexpr (TILES)
     for_window_tiles(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, bm, red, upd);
   else
-    for_window_elems(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, upd);
+    for_window_elems<SYZ_DIRECT_RB>(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, upd);
   __syncthreads();
   if (acc == 0x9E3779B9u) sel8[0] = 1;
   if (dbg & 2) return;
   const uint64_t gb = gstart[it.g];
-  emit_winner_bytes<BM_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, bm, sel8);
+  emit_winner_bytes<PBM_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, bm, sel8);
 }
 
 // PCs of one (call, window) over all its chunks' runs (metadata only)
@@ -1276,8 +1115,6 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint64_t* gdesc = sc.get<uint64_t>("pm_gdesc", G + 1);
   uint16_t* desc = sc.get<uint16_t>("pm_desc", desc_bound + 1);
   uint32_t* elems = sc.get<uint32_t>("pm_elems", total_pcs + 1);
-  uint4* tiles = part_kind() == 2 ? sc.get<uint4>("pm_tiles", chunk_bound * TMAX + 1) : nullptr;
-  uint32_t* ntiles = part_kind() == 2 ? sc.get<uint32_t>("pm_ntiles", chunk_bound + 1) : nullptr;
   if (B) {
     k_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, gstart, mpos, nsub);
     SYZ_LAUNCHED();
@@ -1291,9 +1128,20 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_LAUNCHED();
   // ---- P on its own stream, beside the Go sort ----
   if (!c.part) {
-    int least = 0, greatest = 0;
-    SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
+    // SYZGPU_PART_RESERVE=k: P's stream may not use k of every 32 CUs, which stay free for the Go
+    // sort's latency-bound rounds (the step's other branch); 0: the whole chip, lowest priority
+    static const int reserve = getenv("SYZGPU_PART_RESERVE") ? atoi(getenv("SYZGPU_PART_RESERVE")) : 0;
+    if (reserve > 0 && reserve < 32) {
+      if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+      std::vector<uint32_t> mask((c.ncu + 31) / 32, 0);
+      for (int cu = 0; cu < c.ncu; cu++)
+        if (cu % 32 >= reserve) mask[cu / 32] |= 1u << (cu % 32);
+      SYZ_HIP(hipExtStreamCreateWithCUMask(&c.part, (uint32_t)mask.size() * 32, mask.data()));
+    } else {
+      int least = 0, greatest = 0;
+      SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
+    }
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
   }
@@ -1305,15 +1153,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     ProfScope ps("part", pq, total_pcs * 8 + (uint64_t)n * 24);
     // one workgroup per chunk: workgroups retire all along, so the Go sort's kernels (on normal-priority
     // streams, this one is the lowest) get CUs while P still runs
-    if (part_kind() == 2) {
-      if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
-      k_tiles<<<(unsigned)std::min<uint64_t>((chunk_bound + 3) / 4, 16384), 256, 0, pq>>>(
-          a.off, members, mpos, sbeg, chunks, cstart + B, tiles, ntiles);
-      SYZ_LAUNCHED();
-      const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, std::min<unsigned>(part_grid(), c.ncu));
-      k_part2<<<grid, PP_BLOCK, 0, pq>>>(a.pcs, chunks, cstart + B, tiles, ntiles, dpg, gchunk, gdesc, lo, elems,
-                                         desc, err);
-    } else if (part_kind() == 3) {
+    if (part_kind() == 3) {
       k_part3<P3_BLOCK, P3_TPW><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg,
                                                         gchunk, gdesc, lo, elems, desc, err);
     } else {
