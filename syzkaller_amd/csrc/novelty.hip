@@ -486,6 +486,224 @@ __global__ __launch_bounds__(KT_PAGE_WORDS) void k_kt_clear(u64a* bm, const uint
   bm[(uint64_t)plist[blockIdx.x] * KT_PAGE_WORDS + threadIdx.x] = 0;
 }
 
+// ---- per-call keys (SYZGPU_NOVELTY=keys): T is indexed by the (call, PC) pairs that occur, not by
+// G x (P+1) ------------------------------------------------------------------------------------------
+// B[g] is a bitmap over the dense PC ids d (P+1 columns, column P = the table sentinel) marking the
+// keys call g holds (in a cover or in maxCover0[g]); BR[g][w] = {bits, rank of bit 0 over every row}
+// turns (g, d) into e, the key's index in T (E2 = every call's distinct keys, ≈ a tenth of G x (P+1)
+// at config 3), and row order stays PC order, so the emit is still an ordered compaction.
+struct Bw {  // one 64-key word of B with the rank of its first key
+  u64a bits;
+  uint64_t rank;
+};
+
+__device__ __forceinline__ uint64_t kb_key(const Bw* __restrict__ br, uint64_t wpr, uint32_t g, uint32_t d) {
+  const Bw q = br[(uint64_t)g * wpr + (d >> 6)];
+  return q.rank + (uint64_t)__popcll(q.bits & ((1ull << (d & 63)) - 1));
+}
+
+// B from the covers (PCs other than 0xFFFFFFFF) ...
+__global__ __launch_bounds__(KT_TB) void k_kb_mark_cov(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ group, size_t n, uint64_t L,
+                                                       uint32_t G, const uint64_t* __restrict__ tile_k0,
+                                                       const uint2* __restrict__ dw, uint64_t wpr, u64a* B) {
+  __shared__ uint64_t soff[KT_TOFF + 1];
+  KtTile T;
+  kt_tile_stage(off, n, tile_k0, soff, T, blockIdx.x);
+  const uint64_t j0 = blockIdx.x * KT_TILE + (uint64_t)threadIdx.x * KT_TPC;
+  uint32_t pc[KT_TPC], kk[KT_TPC];
+  const int cnt = kt_tile_load(pcs, L, n, T, j0, pc, kk);
+  if (!cnt) return;
+  uint2 q2[KT_TPC];
+#pragma unroll
+  for (int q = 0; q < KT_TPC; q++) q2[q] = dw[pc[q] >> 5];
+  uint32_t last_k = ~0u, last_g = 0;
+  uint64_t w[KT_TPC];
+  u64a bit[KT_TPC], cur[KT_TPC];
+#pragma unroll
+  for (int q = 0; q < KT_TPC; q++) {
+    if (kk[q] != last_k) last_k = kk[q], last_g = group[kk[q]];
+    const bool ok = q < cnt && pc[q] != SENT && last_g < G;
+    const uint32_t d = q2[q].y + (uint32_t)__popc(q2[q].x & ((1u << (pc[q] & 31)) - 1));
+    w[q] = ok ? (uint64_t)last_g * wpr + (d >> 6) : ~0ull;
+    bit[q] = 1ull << (d & 63);
+    cur[q] = ok ? B[w[q]] : ~0ull;
+  }
+#pragma unroll
+  for (int q = 0; q < KT_TPC; q++)
+    if (!(cur[q] & bit[q])) atomicOr(&B[w[q]], bit[q]);  // a stale 0 only costs a redundant atomic
+}
+
+// ... and from maxCover0 (its 0xFFFFFFFF in column P)
+__global__ void k_kb_mark_mc(const uint32_t* mc, const uint64_t* mc_off, uint32_t G, uint64_t M,
+                             const uint2* __restrict__ dw, uint64_t P, uint64_t wpr, u64a* B) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < M; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = (uint32_t)upper_bound_dev<uint64_t>(mc_off, 0, G + 1, j) - 1;
+    const uint32_t pc = mc[j];
+    const uint64_t d = pc == SENT ? P : kt_dense(dw, pc);
+    atomicOr(&B[(uint64_t)g * wpr + (d >> 6)], 1ull << (d & 63));
+  }
+}
+
+__global__ void k_kb_popc(const u64a* __restrict__ B, uint64_t nw, uint32_t* cnt) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x)
+    cnt[i] = (uint32_t)__popcll(B[i]);
+}
+
+__global__ void k_kb_words(const u64a* __restrict__ B, const uint64_t* __restrict__ pre, uint64_t nw, Bw* br) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x)
+    br[i] = Bw{B[i], pre[i]};
+}
+
+// flakes -> FLAKE where the call holds the key (run first), then maxCover0 keys -> OLD
+__global__ void k_kb_init_flakes(const uint32_t* fl, uint64_t nfl, uint32_t G, const uint2* __restrict__ dw,
+                                 const Bw* __restrict__ br, uint64_t wpr, uint32_t* tab) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nfl * G; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t pc = fl[j % nfl];
+    const uint32_t g = (uint32_t)(j / nfl);
+    if (pc == SENT) continue;
+    const uint32_t d = kt_dense(dw, pc);
+    const Bw q = br[(uint64_t)g * wpr + (d >> 6)];
+    if ((q.bits >> (d & 63)) & 1ull) tab[q.rank + (uint64_t)__popcll(q.bits & ((1ull << (d & 63)) - 1))] = KT_FLAKE;
+  }
+}
+
+__global__ void k_kb_init_mc(const uint32_t* mc, const uint64_t* mc_off, uint32_t G, uint64_t M,
+                             const uint2* __restrict__ dw, uint64_t P, const Bw* __restrict__ br, uint64_t wpr,
+                             uint32_t* tab) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < M; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = (uint32_t)upper_bound_dev<uint64_t>(mc_off, 0, G + 1, j) - 1;
+    const uint32_t pc = mc[j];
+    tab[kb_key(br, wpr, g, pc == SENT ? (uint32_t)P : kt_dense(dw, pc))] = KT_OLD;
+  }
+}
+
+// T[e(g, d)] = min(T, KT_COVER + k) over the covers' keys
+__global__ __launch_bounds__(KT_TB) void k_kb_first(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ group, size_t n, uint64_t L, uint32_t G,
+                                                    const uint64_t* __restrict__ tile_k0, const uint2* __restrict__ dw,
+                                                    const Bw* __restrict__ br, uint64_t wpr, uint32_t* tab) {
+  __shared__ uint64_t soff[KT_TOFF + 1];
+  KtTile T;
+  kt_tile_stage(off, n, tile_k0, soff, T, blockIdx.x);
+  const uint64_t j0 = blockIdx.x * KT_TILE + (uint64_t)threadIdx.x * KT_TPC;
+  uint32_t pc[KT_TPC], kk[KT_TPC];
+  const int cnt = kt_tile_load(pcs, L, n, T, j0, pc, kk);
+  if (!cnt) return;
+  uint2 q2[KT_TPC];
+#pragma unroll
+  for (int q = 0; q < KT_TPC; q++) q2[q] = dw[pc[q] >> 5];
+  uint32_t last_k = ~0u, last_g = 0;
+  Bw bq[KT_TPC];
+  uint32_t dd[KT_TPC];
+  bool ok[KT_TPC];
+#pragma unroll
+  for (int q = 0; q < KT_TPC; q++) {
+    if (kk[q] != last_k) last_k = kk[q], last_g = group[kk[q]];
+    ok[q] = q < cnt && pc[q] != SENT && last_g < G;
+    dd[q] = q2[q].y + (uint32_t)__popc(q2[q].x & ((1u << (pc[q] & 31)) - 1));
+    bq[q] = ok[q] ? br[(uint64_t)last_g * wpr + (dd[q] >> 6)] : Bw{0, 0};
+  }
+  uint64_t idx[KT_TPC];
+  uint32_t cur[KT_TPC];
+#pragma unroll
+  for (int q = 0; q < KT_TPC; q++) {
+    idx[q] = bq[q].rank + (uint64_t)__popcll(bq[q].bits & ((1ull << (dd[q] & 63)) - 1));
+    cur[q] = ok[q] ? tab[idx[q]] : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < KT_TPC; q++) {
+    const uint32_t me = kk[q] + KT_COVER;
+    if (ok[q] && cur[q] > me) atomicMin(&tab[idx[q]], me);
+  }
+}
+
+// per chunk of KB_WORDS words of B: kept keys, is_new of the winning covers, updated rows
+constexpr int KB_ITEMS = 4;  // B words per thread
+constexpr uint64_t KB_CHUNK = (uint64_t)KT_BLOCK * KB_ITEMS;
+__global__ __launch_bounds__(KT_BLOCK) void k_kb_count(const Bw* __restrict__ br, uint64_t nw, uint64_t wpr,
+                                                       const uint32_t* __restrict__ tab, uint8_t* is_new, uint8_t* upd,
+                                                       uint32_t* cnt) {
+  __shared__ uint32_t lds[KT_BLOCK / 64 + 1];
+  const uint64_t w0 = blockIdx.x * KB_CHUNK + (uint64_t)threadIdx.x * KB_ITEMS;
+  uint32_t c = 0;
+  for (int q = 0; q < KB_ITEMS; q++) {
+    const uint64_t w = w0 + q;
+    if (w >= nw) break;
+    const Bw b = br[w];
+    const int nb = __popcll(b.bits);
+    for (int i = 0; i < nb; i++) {
+      const uint32_t v = tab[b.rank + i];
+      if (v != KT_FLAKE && v != KT_EMPTY) {
+        c++;
+        if (v != KT_OLD) {
+          is_new[v - KT_COVER] = 1;
+          upd[w / wpr] = 1;
+        }
+      }
+    }
+  }
+  const uint32_t tot = block_sum<KT_BLOCK>(c, lds);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+
+// a table that took a Union loses its 0xFFFFFFFF entry (column P)
+__global__ void k_kb_sentfix(const Bw* __restrict__ br, uint64_t wpr, uint64_t P, uint32_t G, const uint8_t* upd,
+                             uint32_t* tab, uint32_t* cnt) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+    const uint64_t w = (uint64_t)g * wpr + (P >> 6);
+    const Bw b = br[w];
+    if (!((b.bits >> (P & 63)) & 1ull)) continue;
+    const uint64_t e = b.rank + (uint64_t)__popcll(b.bits & ((1ull << (P & 63)) - 1));
+    if (upd[g] && tab[e] == KT_OLD) {
+      tab[e] = KT_FLAKE;  // dropped like a flake
+      atomicSub(&cnt[w / KB_CHUNK], 1u);
+    }
+  }
+}
+
+// per chunk: the kept keys in (g, pc) order, row starts into ooff
+__global__ __launch_bounds__(KT_BLOCK) void k_kb_emit(const Bw* __restrict__ br, uint64_t nw, uint64_t wpr, uint32_t G,
+                                                      const uint32_t* __restrict__ tab, const uint64_t* cpre,
+                                                      uint64_t nchunks, const uint32_t* __restrict__ pc_of, uint32_t* out,
+                                                      uint64_t cap, uint64_t* ooff, int* err) {
+  __shared__ uint32_t lds[KT_BLOCK / 64 + 1];
+  const uint64_t w0 = blockIdx.x * KB_CHUNK + (uint64_t)threadIdx.x * KB_ITEMS;
+  uint32_t c = 0;
+  for (int q = 0; q < KB_ITEMS; q++) {
+    const uint64_t w = w0 + q;
+    if (w >= nw) break;
+    const Bw b = br[w];
+    const int nb = __popcll(b.bits);
+    for (int i = 0; i < nb; i++) c += tab[b.rank + i] < KT_EMPTY && tab[b.rank + i] != KT_FLAKE;
+  }
+  uint32_t tot;
+  uint64_t pos = cpre[blockIdx.x] + block_excl_scan<KT_BLOCK>(c, lds, &tot);
+  for (int q = 0; q < KB_ITEMS; q++) {
+    const uint64_t w = w0 + q;
+    if (w >= nw) break;
+    if (w % wpr == 0) ooff[w / wpr] = pos;
+    const Bw b = br[w];
+    u64a m = b.bits;
+    uint64_t e = b.rank;
+    while (m) {
+      const int i = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const uint32_t v = tab[e++];
+      if (v != KT_FLAKE && v != KT_EMPTY) {
+        if (pos < cap)
+          out[pos] = pc_of[(w % wpr) * 64 + i];
+        else
+          atomicOr(err, 8);
+        pos++;
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) ooff[G] = cpre[nchunks];
+}
+
+static int strategy();
+
 static bool novelty_table(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_t* d_grp, size_t n, uint64_t L,
                           uint32_t G,
                           const uint32_t* d_mc, const uint64_t* d_mco, uint64_t M, const uint32_t* d_fl,
@@ -534,7 +752,9 @@ static bool novelty_table(const uint32_t* d_pcs, const uint64_t* d_off, const ui
   const uint64_t P = hP[0];
   const uint64_t E = (uint64_t)G * (P + 1);
   const uint64_t nchunks = (E + KT_CHUNK - 1) / KT_CHUNK;
-  if (nchunks * KT_CHUNK * 4 > table_budget) {  // too many keys for a direct table: clean up, sort instead
+  const uint64_t wpr = (P + 1 + 63) / 64, nw = (uint64_t)G * wpr;  // per-call keys: B words
+  const bool grid = strategy() != 3;  // SYZGPU_NOVELTY=keys: per-call keys
+  auto release = [&]() {  // the bitmap and its summary back to zero
     if (npages) {
       k_kt_clear<<<npages, KT_PAGE_WORDS, 0, s>>>(bm, plist);
       SYZ_LAUNCHED();
@@ -543,7 +763,83 @@ static bool novelty_table(const uint32_t* d_pcs, const uint64_t* d_off, const ui
     SYZ_HIP(hipStreamSynchronize(s));
     sc.put_clean("kt_bm");
     sc.put_clean("kt_sum");
+  };
+  if (grid ? nchunks * KT_CHUNK * 4 > table_budget : nw * 36 > table_budget) {  // too big: sort instead
+    release();
     return false;
+  }
+  if (!grid) {
+    uint32_t* pc_of = sc.get<uint32_t>("kt_pcof", P + 1);
+    u64a* B = sc.get<u64a>("kb_b", nw + 1);
+    Bw* br = sc.get<Bw>("kb_br", nw + 1);
+    uint32_t* wc = sc.get<uint32_t>("kb_wc", nw + 1);
+    uint64_t* wpre = sc.get<uint64_t>("kb_wpre", nw + 1);
+    uint8_t* upd = sc.get<uint8_t>("kt_upd", G + 1);
+    const uint64_t nch = (nw + KB_CHUNK - 1) / KB_CHUNK;
+    uint32_t* cnt = sc.get<uint32_t>("kt_cnt", nch + 1);
+    uint64_t* cpre = sc.get<uint64_t>("kt_cpre", nch + 1);
+    SYZ_HIP(hipMemsetAsync(upd, 0, G + 1, s));
+    SYZ_HIP(hipMemsetAsync(B, 0, nw * 8, s));
+    {
+      ProfScope ps("novelty_dense", s, (M + nflakes) * 4 + nw * 40);
+      if (npages) {
+        k_kt_dense<<<npages, KT_PAGE_WORDS, 0, s>>>(bm, plist, ppre, dw, pc_of);
+        SYZ_LAUNCHED();
+      }
+      SYZ_HIP(hipMemsetD32Async((hipDeviceptr_t)(pc_of + P), (int)SENT, 1, s));
+    }
+    {
+      ProfScope ps("novelty_keys", s, L * 4 + n * 12 + 8 + M * 4);
+      if (ntiles) {
+        k_kb_mark_cov<<<(unsigned)ntiles, KT_TB, 0, s>>>(d_pcs, d_off, d_grp, n, L, G, tile_k0, dw, wpr, B);
+        SYZ_LAUNCHED();
+      }
+      if (M) {
+        k_kb_mark_mc<<<grid_for(M, 256, 16384), 256, 0, s>>>(d_mc, d_mco, G, M, dw, P, wpr, B);
+        SYZ_LAUNCHED();
+      }
+      k_kb_popc<<<grid_for(nw, 256, 16384), 256, 0, s>>>(B, nw, wc);
+      SYZ_LAUNCHED();
+      exclusive_scan_u32(wc, wpre, nw, s);
+      k_kb_words<<<grid_for(nw, 256, 16384), 256, 0, s>>>(B, wpre, nw, br);
+      SYZ_LAUNCHED();
+    }
+    SYZ_HIP(hipMemcpyAsync(hP, wpre + nw, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    const uint64_t E2 = hP[0];
+    if (E2 * 4 > table_budget) {
+      release();
+      return false;
+    }
+    uint32_t* tab = sc.get<uint32_t>("kb_tab", E2 + 1);
+    SYZ_HIP(hipMemsetAsync(tab, 0xFF, (E2 + 1) * 4, s));
+    {
+      ProfScope ps("novelty_first", s, L * 4 + n * 12 + 8);
+      if (nflakes) {
+        k_kb_init_flakes<<<grid_for(nflakes * G, 256, 16384), 256, 0, s>>>(d_fl, nflakes, G, dw, br, wpr, tab);
+        SYZ_LAUNCHED();
+      }
+      if (M) {
+        k_kb_init_mc<<<grid_for(M, 256, 16384), 256, 0, s>>>(d_mc, d_mco, G, M, dw, P, br, wpr, tab);
+        SYZ_LAUNCHED();
+      }
+      if (ntiles) {
+        k_kb_first<<<(unsigned)ntiles, KT_TB, 0, s>>>(d_pcs, d_off, d_grp, n, L, G, tile_k0, dw, br, wpr, tab);
+        SYZ_LAUNCHED();
+      }
+    }
+    {
+      ProfScope ps("novelty_emit", s, nw * 16 + E2 * 8);
+      k_kb_count<<<(unsigned)nch, KT_BLOCK, 0, s>>>(br, nw, wpr, tab, d_new, upd, cnt);
+      SYZ_LAUNCHED();
+      k_kb_sentfix<<<grid_for(G, 256, 64), 256, 0, s>>>(br, wpr, P, G, upd, tab, cnt);
+      SYZ_LAUNCHED();
+      exclusive_scan_u32(cnt, cpre, nch, s);
+      k_kb_emit<<<(unsigned)nch, KT_BLOCK, 0, s>>>(br, nw, wpr, G, tab, cpre, nch, pc_of, d_out, out_cap, d_ooff, err);
+      SYZ_LAUNCHED();
+    }
+    release();
+    return true;
   }
   uint32_t* pc_of = sc.get<uint32_t>("kt_pcof", P + 1);
   uint32_t* tab = sc.get_clean<uint32_t>("kt_tab", nchunks * KT_CHUNK, 0xFF, s);
@@ -584,23 +880,19 @@ static bool novelty_table(const uint32_t* d_pcs, const uint64_t* d_off, const ui
     k_kt_emit<<<(unsigned)nchunks, KT_BLOCK, 0, s>>>(tab, E, P, G, cpre, nchunks, pc_of, d_out, out_cap, d_ooff, err);
     SYZ_LAUNCHED();
   }
-  if (npages) {
-    k_kt_clear<<<npages, KT_PAGE_WORDS, 0, s>>>(bm, plist);
-    SYZ_LAUNCHED();
-  }
-  SYZ_HIP(hipMemsetAsync(sum, 0, KT_SUM_WORDS * 8, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  sc.put_clean("kt_bm");
-  sc.put_clean("kt_sum");
+  release();
   sc.put_clean("kt_tab");
   return true;
 }
 
-// SYZGPU_NOVELTY=sort forces the radix-sort strategy, =table the keyed table (tests run both).
+// SYZGPU_NOVELTY=sort forces the radix-sort strategy, =table the keyed table over G x (P+1), =keys the
+// keyed table over per-call keys (opt-in: measured 31.3 vs 14.6 ms at config 3, one more dependent
+// gather per PC in each of two passes). Tests run every strategy.
 static int strategy() {
   const char* e = getenv("SYZGPU_NOVELTY");
   if (e && !strcmp(e, "sort")) return 1;
   if (e && !strcmp(e, "table")) return 2;
+  if (e && !strcmp(e, "keys")) return 3;
   return 0;
 }
 
@@ -609,7 +901,7 @@ static uint64_t table_budget() {
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
   const uint64_t b = fr / 4;
-  return strategy() == 2 ? ~0ull : std::min<uint64_t>(b, 64ull << 30);
+  return strategy() >= 2 ? ~0ull : std::min<uint64_t>(b, 64ull << 30);
 }
 
 static void check_errors(int* err, hipStream_t s);

@@ -22,7 +22,7 @@ from syzkaller_amd import _lib, cover, synth  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["table", "sort"])
+@pytest.fixture(autouse=True, params=["table", "keys", "sort"])
 def strategy(request, monkeypatch):
     """Both device strategies: the keyed first-occurrence table (default) and the stable radix sort
     (used when the table would not fit). SYZGPU_NOVELTY is read by the library on every call."""
