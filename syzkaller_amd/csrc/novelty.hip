@@ -885,14 +885,15 @@ static bool novelty_table(const uint32_t* d_pcs, const uint64_t* d_off, const ui
   return true;
 }
 
-// SYZGPU_NOVELTY=sort forces the radix-sort strategy, =table the keyed table over G x (P+1), =keys the
-// keyed table over per-call keys (opt-in: measured 31.3 vs 14.6 ms at config 3, one more dependent
-// gather per PC in each of two passes). Tests run every strategy.
+// Default: PC windows (novelty_win.hip) when the span fits them, else the keyed table over G x (P+1),
+// else the radix sort. SYZGPU_NOVELTY=windows|table|sort|keys forces one (keys: the keyed table over
+// per-call keys, measured 31.3 vs 14.6 ms for the G x (P+1) table at config 3). Tests run every one.
 static int strategy() {
   const char* e = getenv("SYZGPU_NOVELTY");
   if (e && !strcmp(e, "sort")) return 1;
   if (e && !strcmp(e, "table")) return 2;
   if (e && !strcmp(e, "keys")) return 3;
+  if (e && !strcmp(e, "windows")) return 4;
   return 0;
 }
 
@@ -905,6 +906,10 @@ static uint64_t table_budget() {
 }
 
 static void check_errors(int* err, hipStream_t s);
+
+bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_t* d_grp, size_t n, uint32_t G,
+                     const uint32_t* d_mc, const uint64_t* d_mco, const uint32_t* d_fl, size_t nfl, uint8_t* d_new,
+                     uint32_t* d_out, size_t out_cap, uint64_t* d_ooff, int* err, hipStream_t s);
 
 // The batch on device-resident inputs: L = off[n] PCs in the covers, M = mc_off[G] in the tables.
 // Writes is_new[n], out_mc[<= out_cap] and out_mc_off[G+1] on the device; the call returns after the
@@ -920,6 +925,16 @@ void novelty_dev(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_t* d
   int* err = sc.get<int>("nv_err", 2);
   SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
   if (n) SYZ_HIP(hipMemsetAsync(d_new, 0, n, s));
+  if (strategy() == 0 || strategy() == 4) {
+    if (nflakes > 1) {
+      k_nov_check_flakes<<<grid_for(nflakes, 256, 1024), 256, 0, s>>>(d_fl, nflakes, err);
+      SYZ_LAUNCHED();
+    }
+    if (novelty_windows(d_pcs, d_off, d_grp, n, G, d_mc, d_mco, d_fl, nflakes, d_new, d_out, out_cap, d_ooff, err, s)) {
+      check_errors(err, s);
+      return;
+    }
+  }
   if (strategy() != 1 && novelty_table(d_pcs, d_off, d_grp, n, L, G, d_mc, d_mco, M, d_fl, nflakes, d_new, d_out, out_cap,
                                        d_ooff, err, table_budget(), s)) {
     check_errors(err, s);

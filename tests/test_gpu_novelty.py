@@ -22,10 +22,12 @@ from syzkaller_amd import _lib, cover, synth  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["table", "keys", "sort"])
+@pytest.fixture(autouse=True, params=["windows", "table", "keys", "sort"])
 def strategy(request, monkeypatch):
-    """Both device strategies: the keyed first-occurrence table (default) and the stable radix sort
-    (used when the table would not fit). SYZGPU_NOVELTY is read by the library on every call."""
+    """Every device strategy: PC windows on the Minimize pipeline (default while the PC span fits
+    1024 windows of 32K addresses), the keyed first-occurrence table over G x (P+1) (the default
+    beyond), the keyed table over per-call keys, and the stable radix sort (when no table fits).
+    SYZGPU_NOVELTY is read by the library on every call."""
     monkeypatch.setenv("SYZGPU_NOVELTY", request.param)
     return request.param
 
@@ -154,6 +156,33 @@ def test_novelty_full_pc_space():
         _check(pcs, off, grp, G, mcp, mco, flakes)
 
 
+def test_novelty_window_edges():
+    # a span of exactly 1024 windows ending at the top of the u32 space: PCs on window boundaries,
+    # 0xFFFFFFFE, flakes on boundaries and inside tables, a table of only the sentinel, a call with
+    # only its table, covers of only the sentinel, long covers crossing chunks (> 16384 PCs)
+    rnd = np.random.default_rng(21)
+    base = 0xFE000000
+    bounds = np.array([base, base + 32767, base + 32768, base + 65535, 0xFFFF7FFF, 0xFFFF8000, 0xFFFFFFFE],
+                      np.uint32)
+    G = 6
+    for _ in range(3):
+        pool = np.unique(np.concatenate([bounds, (base + rnd.integers(0, 2**25 - 1, size=40_000)).astype(np.uint32)]))
+        n = 300
+        covs = [np.unique(rnd.choice(pool, size=int(rnd.integers(0, 60)))) for _ in range(n)]
+        covs[5] = np.unique(rnd.choice(pool, size=30_000))
+        covs[6] = np.array([0xFFFFFFFF], np.uint32)
+        covs[7] = np.append(np.unique(rnd.choice(pool, size=20)), np.uint32(0xFFFFFFFF))
+        grp = rnd.integers(0, G - 1, size=n).astype(np.uint32)  # call G-1: its table only
+        mc = [np.unique(rnd.choice(pool, size=int(rnd.integers(0, 3000)))) for _ in range(G)]
+        mc[1] = np.append(mc[1], np.uint32(0xFFFFFFFF))
+        mc[3] = np.array([0xFFFFFFFF], np.uint32)
+        mc[4] = np.unique(rnd.choice(pool, size=25_000))
+        flakes = np.unique(np.concatenate([bounds[:3], rnd.choice(pool, size=50), mc[0][:5]]))
+        pcs, off = oracle.to_csr(covs)
+        mcp, mco = oracle.to_csr(mc)
+        _check(pcs, off, grp, G, mcp, mco, flakes)
+
+
 def test_novelty_good_batch_after_rejected_one():
     pcs = np.array([2, 1, 3], np.uint32)  # not canonical
     off = np.array([0, 3], np.uint64)
@@ -188,6 +217,30 @@ def test_novelty_rejects_bad_input(what):
     with pytest.raises(_lib.SyzGpuError) as e:
         cover.NoveltyBatch(pcs, off, grp, 2, mcp, mco, fl)
     assert e.value.code == _lib.EINVAL
+
+
+@pytest.mark.parametrize("where", ["cover", "table"])
+@pytest.mark.parametrize("at", [1, 63, 64, 16383, 16384, 19998])
+def test_novelty_rejects_unsorted_anywhere(where, at):
+    # one swapped pair inside a long list: inside a 64-PC tile, across tiles, across the 16384-PC
+    # chunks of the window transpose, at the end; then an equal pair (not strictly increasing)
+    good = (0x81000000 + 4 * np.arange(20_000)).astype(np.uint32)
+    for kind in ("swap", "dup"):
+        bad = good.copy()
+        if kind == "swap":
+            bad[at - 1], bad[at] = bad[at], bad[at - 1]
+        else:
+            bad[at] = bad[at - 1]
+        covs = [good[:100], bad if where == "cover" else good]
+        mc = [bad if where == "table" else good[::3], np.zeros(0, np.uint32)]
+        pcs, off = oracle.to_csr(covs)
+        mcp, mco = oracle.to_csr(mc)
+        with pytest.raises(_lib.SyzGpuError) as e:
+            cover.NoveltyBatch(pcs, off, np.array([1, 0], np.uint32), 2, mcp, mco, np.zeros(0, np.uint32))
+        assert e.value.code == _lib.EINVAL
+    pcs, off = oracle.to_csr([good[:100], good])
+    mcp, mco = oracle.to_csr([good[::3], np.zeros(0, np.uint32)])
+    _check(pcs, off, np.array([1, 0], np.uint32), 2, mcp, mco, np.zeros(0, np.uint32))
 
 
 def test_novelty_capacity_error():
