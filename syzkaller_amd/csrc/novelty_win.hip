@@ -11,7 +11,7 @@
 // rank is its position in that list, so the table is the group's smallest rank.
 //
 //   G  group partition (stable) + members + lengths (a trailing 0xFFFFFFFF dropped) + the PC span
-//   P  k_part3<NOV>: the members' PCs transposed into 2^DS-address windows (one HBM read per PC), every
+//   P  k_part3<NOV>: the members' PCs transposed into 2^SB-address windows (one HBM read per PC), every
 //      list checked strictly increasing on the way
 //   M  k_nw_min: a workgroup per (call, window): direct min-rank table in LDS, then one pass over it in
 //      PC order: a key is kept if the table holds it or a non-flake cover does (flakes of the window in
@@ -21,9 +21,10 @@
 //      tables, sorted by (call, PC)), a table's 0xFFFFFFFF last unless the call took a Union
 //
 // Integer work throughout; bit-exact by construction. Windows are direct-mapped only, so the PC span
-// must fit WMAX windows (2^DS x 1024 = 32M addresses); a wider span (or G > 4096) falls back to the
+// must fit WMAX windows (2^15 x 1024 = 32M addresses); a wider span (or G > 4096) falls back to the
 // keyed table (novelty.hip).
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
 
 #include "panels_dev.hpp"
@@ -31,9 +32,18 @@
 
 namespace syz {
 
-constexpr uint32_t NW_BITS = 1u << DS;          // addresses per window
-constexpr uint32_t NW_WORDS64 = NW_BITS / 64;   // u64 words of a window's kept bitmap
-constexpr uint32_t NW_FLK_WORDS = NW_BITS / 32; // LDS flake bitmap words
+// window bits SB: 15 = 32K-entry tables (128 KB of LDS, one 1024-thread workgroup per CU), 14 = 16K-entry
+// tables (64 KB, two 512-thread workgroups per CU, so one's metadata and table set-up overlap the
+// other's walk)
+template <uint32_t SB>
+struct NwCfg {
+  static constexpr uint32_t BITS = 1u << SB;      // addresses per window
+  static constexpr uint32_t WORDS64 = BITS / 64;  // u64 words of a window's kept bitmap
+  static constexpr uint32_t FLK = BITS / 32;      // LDS flake bitmap words
+  static constexpr int BLOCK = SB >= 15 ? 1024 : 512;
+  static constexpr uint32_t BMW = SB >= 15 ? PBM_WORDS : 2048;  // LDS rank bitmap words (winner dedup)
+  static constexpr int EBLOCK = (int)(WORDS64 / 2);              // k_nw_emit: two words per thread
+};
 
 // combined members: call g's list is [table g (entry id n + g), its covers in batch order]
 __global__ void k_nw_members(const uint32_t* members, const uint64_t* gstart, const uint32_t* group, size_t n,
@@ -85,46 +95,48 @@ __global__ __launch_bounds__(256) void k_nw_meta(const uint32_t* pcs, const uint
 
 // M: one (call, window). tab = min member position per window offset; the table's position cstart[g]
 // is OLD.
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_nw_min(
+template <uint32_t SB>
+__global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
     const PItem* items, const PChunk* __restrict__ chunks, const uint64_t* gchunk, const uint64_t* gdesc,
     const PGroup* pg, const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems, const uint64_t* cstart,
-    uint32_t lo, const uint32_t* __restrict__ fl, uint64_t nfl, unsigned long long* kbits, uint32_t* wcount,
-    uint8_t* sel8, uint8_t* upd) {
-  __shared__ uint32_t tab[NW_BITS];
-  __shared__ uint32_t bm[PBM_WORDS];
-  __shared__ uint32_t flk[NW_FLK_WORDS];
-  __shared__ uint32_t red[1024 / 64 + 1];
+    uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart, unsigned long long* kbits,
+    uint32_t* wcount, uint8_t* sel8, uint8_t* upd, int dbg) {
+  using K = NwCfg<SB>;
+  constexpr int BLOCK = K::BLOCK;
+  __shared__ uint32_t tab[K::BITS];
+  __shared__ uint32_t bm[K::BMW];
+  __shared__ uint32_t flk[K::FLK];
+  __shared__ uint32_t red[BLOCK / 64 + 1];
   const PItem it = items[blockIdx.x];
   const uint32_t g = it.g, w = it.w, W = pg[g].W;
-  for (uint32_t i = threadIdx.x; i < NW_BITS; i += 1024) tab[i] = RANK_NONE;
-  for (uint32_t i = threadIdx.x; i < NW_FLK_WORDS; i += 1024) flk[i] = 0;
+  for (uint32_t i = threadIdx.x; i < K::BITS; i += BLOCK) tab[i] = RANK_NONE;
+  for (uint32_t i = threadIdx.x; i < K::FLK; i += BLOCK) flk[i] = 0;
   __syncthreads();
-  // the flakes inside this window's addresses
-  const uint64_t wlo = (uint64_t)lo + ((uint64_t)w << DS), whi = wlo + NW_BITS;
-  if (nfl) {
-    const uint64_t i0 = lower_bound_dev<uint32_t>(fl, 0, nfl, (uint32_t)wlo);
-    for (uint64_t i = i0 + threadIdx.x; i < nfl && fl[i] < whi; i += 1024) {
-      const uint32_t o = fl[i] - (uint32_t)wlo;
-      atomicOr(&flk[o >> 5], 1u << (o & 31));
-    }
+  // the flakes inside this window's addresses: fl[fstart[w], fstart[w + 1])
+  const uint32_t wlo = lo + (w << SB);
+  for (uint32_t i = fstart[w] + threadIdx.x; i < fstart[w + 1]; i += BLOCK) {
+    const uint32_t o = fl[i] - wlo;
+    atomicOr(&flk[o >> 5], 1u << (o & 31));
   }
-  for_window_elems<SYZ_DIRECT_RB, true>(it, chunks, gchunk, gdesc, pg, desc, elems, nullptr, 0u, 16,
-                                        [&](uint32_t o, uint32_t R) {
-                                          if (tab[o] > R) atomicMin(&tab[o], R);
-                                        });
+  if (!(dbg & 1))
+    for_window_elems<SYZ_DIRECT_RB, true>(it, chunks, gchunk, gdesc, pg, desc, elems, nullptr, 0u, BLOCK / 64,
+                                          [&](uint32_t o, uint32_t R) {
+                                            if (tab[o] > R) atomicMin(&tab[o], R);
+                                          });
+  if (dbg & 2) return;
   const uint64_t gb = cstart[g], ng = cstart[g + 1] - gb;
-  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)PBM_WORDS * 32, ng);
+  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)K::BMW * 32, ng);
   const uint32_t words = (span + 31) / 32;
-  for (uint32_t i = threadIdx.x; i < words; i += 1024) bm[i] = 0;
+  for (uint32_t i = threadIdx.x; i < words; i += BLOCK) bm[i] = 0;
   __syncthreads();
   // in PC order: kept keys as bitmap words, new covers marked
   const unsigned lane = __lane_id();
-  const uint64_t slot_bits = ((uint64_t)g * W + w) * NW_WORDS64;
+  const uint64_t slot_bits = ((uint64_t)g * W + w) * K::WORDS64;
   uint32_t cnt = 0;
   int anynew = 0;
 #pragma unroll 4
-  for (uint32_t i = 0; i < NW_BITS / 1024; i++) {
-    const uint32_t o = i * 1024 + threadIdx.x;
+  for (uint32_t i = 0; i < K::BITS / BLOCK; i++) {
+    const uint32_t o = i * BLOCK + threadIdx.x;
     const uint32_t r = tab[o];
     const bool old = r == (uint32_t)gb;
     const bool flake = (flk[o >> 5] >> (o & 31)) & 1u;
@@ -145,16 +157,24 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 8))) vo
       }
     }
   }
-  const uint32_t tot = block_sum<1024>(cnt, red);
+  const uint32_t tot = block_sum<BLOCK>(cnt, red);
   if (threadIdx.x == 0) wcount[(uint64_t)g * (W + 1) + w] = tot;
   if (__syncthreads_or(anynew) && threadIdx.x == 0) upd[g] = 1;
-  for (uint32_t i = threadIdx.x; i < words; i += 1024) {
+  for (uint32_t i = threadIdx.x; i < words; i += BLOCK) {
     uint32_t v = bm[i];
     while (v) {
       const uint32_t b = __ffs(v) - 1;
       sel8[gb + 32ull * i + b] = 1;
       v &= v - 1;
     }
+  }
+}
+
+// fstart[w] = the first flake at or above window w's first address (w in [0, W]; nfl past the span)
+__global__ void k_nw_fstart(const uint32_t* fl, uint64_t nfl, uint32_t lo, uint32_t W, uint32_t sb, uint32_t* fstart) {
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w <= W; w += gridDim.x * blockDim.x) {
+    const uint64_t a = (uint64_t)lo + ((uint64_t)w << sb);
+    fstart[w] = a > 0xFFFFFFFFull ? (uint32_t)nfl : (uint32_t)lower_bound_dev<uint32_t>(fl, 0, nfl, (uint32_t)a);
   }
 }
 
@@ -166,12 +186,13 @@ __global__ void k_nw_sent(const uint8_t* has_sent, const uint8_t* upd, uint32_t 
 }
 
 // E: one slot per workgroup; the window's kept bitmap -> its PCs at wpos[slot]
-constexpr int NE_BLOCK = 256;
-static_assert(NW_WORDS64 == 2 * NE_BLOCK, "k_nw_emit: two bitmap words per thread");
-__global__ __launch_bounds__(NE_BLOCK) void k_nw_emit(const unsigned long long* __restrict__ kbits,
+template <uint32_t SB>
+__global__ __launch_bounds__(NwCfg<SB>::EBLOCK) void k_nw_emit(const unsigned long long* __restrict__ kbits,
                                                       const uint64_t* __restrict__ wpos, uint32_t G, uint32_t W,
                                                       uint32_t lo, uint32_t* out, uint64_t cap, uint64_t* ooff,
                                                       int* err) {
+  using K = NwCfg<SB>;
+  constexpr int NE_BLOCK = K::EBLOCK;
   __shared__ uint32_t red[NE_BLOCK / 64 + 1];
   const uint64_t slot = blockIdx.x;
   const uint32_t g = (uint32_t)(slot / (W + 1)), w = (uint32_t)(slot % (W + 1));
@@ -189,11 +210,11 @@ __global__ __launch_bounds__(NE_BLOCK) void k_nw_emit(const unsigned long long* 
     if (threadIdx.x == 0) out[p0] = SENT;
     return;
   }
-  const uint64_t base = ((uint64_t)g * W + w) * NW_WORDS64 + 2 * threadIdx.x;
+  const uint64_t base = ((uint64_t)g * W + w) * K::WORDS64 + 2 * threadIdx.x;
   const unsigned long long b0 = kbits[base], b1 = kbits[base + 1];
   uint32_t tot;
   uint64_t p = p0 + block_excl_scan<NE_BLOCK>((uint32_t)(__popcll(b0) + __popcll(b1)), red, &tot);
-  const uint32_t a0 = lo + (w << DS) + 128u * threadIdx.x;
+  const uint32_t a0 = lo + (w << SB) + 128u * threadIdx.x;
   for (int h = 0; h < 2; h++) {
     unsigned long long m = h ? b1 : b0;
     while (m) {
@@ -209,6 +230,18 @@ __global__ void k_nw_isnew(const uint32_t* cmem, const uint8_t* sel8, size_t nm,
     const uint32_t e = cmem[i];
     if (e < n1) is_new[e] = sel8[i];
   }
+}
+
+// timing experiments only (results are wrong when set): SYZGPU_NW_DBG 1 = tables not walked, 2 = no emit
+static int nw_dbg() {
+  static const int v = getenv("SYZGPU_NW_DBG") ? atoi(getenv("SYZGPU_NW_DBG")) : 0;
+  return v;
+}
+
+// SYZGPU_NW_BITS=14|15: window bits (default: 14 while the span fits 1024 such windows, else 15)
+static uint32_t nw_bits_forced() {
+  static const uint32_t v = getenv("SYZGPU_NW_BITS") ? (uint32_t)atoi(getenv("SYZGPU_NW_BITS")) : 0u;
+  return v == 14 || v == 15 ? v : 0u;
 }
 
 // false: the span does not fit the direct windows (or G is too large): use another strategy. err gets
@@ -260,10 +293,13 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   const uint64_t total = hbuf[G + 1];
   uint32_t lo = reinterpret_cast<uint32_t*>(hbuf + G + 2)[0], hi = reinterpret_cast<uint32_t*>(hbuf + G + 2)[1];
   if (lo > hi) lo = hi = 0;  // no PCs outside the sentinel
-  lo &= ~(NW_BITS - 1);      // windows on 2^DS boundaries: a window's addresses never wrap
-  const uint64_t W64 = (((uint64_t)hi - lo) >> DS) + 1;
-  if (W64 > WMAX) return false;
-  const uint32_t W = (uint32_t)W64;
+  auto nwin = [&](uint32_t sb) { return (((uint64_t)hi - (lo & ~((1u << sb) - 1))) >> sb) + 1; };
+  uint32_t SB = nw_bits_forced();
+  if (!SB) SB = nwin(14) <= WMAX ? 14 : 15;
+  if (nwin(SB) > WMAX) return false;
+  lo &= ~((1u << SB) - 1);  // windows on 2^SB boundaries: a window's addresses never wrap
+  const uint32_t W = (uint32_t)nwin(SB);
+  const uint32_t words64 = (1u << SB) / 64;
   // ---- plan: every call direct-mapped on W windows; blocks of 64 members; work items ----
   std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
   for (uint32_t g = 0; g < G; g++) {
@@ -290,7 +326,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   {
     uint8_t* p = stage;
     PGroup* hp = reinterpret_cast<PGroup*>(p);
-    for (uint32_t g = 0; g < G; g++) hp[g] = PGroup{DS, W, PMODE_DIRECT, 0};
+    for (uint32_t g = 0; g < G; g++) hp[g] = PGroup{SB, W, PMODE_DIRECT, 0};
     SYZ_HIP(hipMemcpyAsync(dpg, p, G * sizeof(PGroup), hipMemcpyHostToDevice, s));
     p += (G + 1) * sizeof(PGroup);
     std::memcpy(p, hgblock.data(), (G + 1) * 4);
@@ -315,7 +351,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   uint16_t* desc = sc.get<uint16_t>("nw_desc", desc_bound + 1);
   uint32_t* elems = sc.get<uint32_t>("pm_elems", total + 1);
   const size_t nslots = (size_t)G * (W + 1);
-  unsigned long long* kbits = sc.get<unsigned long long>("nw_kbits", nitems * NW_WORDS64 + 1);
+  unsigned long long* kbits = sc.get<unsigned long long>("nw_kbits", nitems * words64 + 1);
   uint32_t* wcount = sc.get<uint32_t>("nw_wcount", nslots + 1);
   uint64_t* wpos = sc.get<uint64_t>("nw_wpos", nslots + 1);
   uint8_t* sel8 = sc.get<uint8_t>("nw_sel8", nm + 1);
@@ -341,18 +377,28 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
         d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, gchunk, gdesc, lo, elems, desc, err, ns);
     SYZ_LAUNCHED();
   }
+  uint32_t* fstart = sc.get<uint32_t>("nw_fstart", (size_t)W + 2);
   {
-    ProfScope ps("novelty_min", s, total * 4 + nitems * NW_WORDS64 * 8);
-    k_nw_min<<<(unsigned)nitems, 1024, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems, cstart, lo, d_fl, nfl,
-                                               kbits, wcount, sel8, upd);
+    ProfScope ps("novelty_min", s, total * 4 + nitems * words64 * 8);
+    k_nw_fstart<<<grid_for(W + 1, 256, 64), 256, 0, s>>>(d_fl, nfl, lo, W, SB, fstart);
+    SYZ_LAUNCHED();
+    if (SB == 14)
+      k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems, cstart,
+                                                                 lo, d_fl, fstart, kbits, wcount, sel8, upd, nw_dbg());
+    else
+      k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems, cstart,
+                                                                 lo, d_fl, fstart, kbits, wcount, sel8, upd, nw_dbg());
     SYZ_LAUNCHED();
   }
   {
-    ProfScope ps("novelty_emit", s, nitems * NW_WORDS64 * 8 + (uint64_t)nm * 6);
+    ProfScope ps("novelty_emit", s, nitems * words64 * 8 + (uint64_t)nm * 6);
     k_nw_sent<<<grid_for(G, 256, 64), 256, 0, s>>>(has_sent, upd, G, W, wcount);
     SYZ_LAUNCHED();
     exclusive_scan_u32(wcount, wpos, nslots, s);
-    k_nw_emit<<<(unsigned)nslots, NE_BLOCK, 0, s>>>(kbits, wpos, G, W, lo, d_out, out_cap, d_ooff, err);
+    if (SB == 14)
+      k_nw_emit<14><<<(unsigned)nslots, NwCfg<14>::EBLOCK, 0, s>>>(kbits, wpos, G, W, lo, d_out, out_cap, d_ooff, err);
+    else
+      k_nw_emit<15><<<(unsigned)nslots, NwCfg<15>::EBLOCK, 0, s>>>(kbits, wpos, G, W, lo, d_out, out_cap, d_ooff, err);
     SYZ_LAUNCHED();
     k_nw_isnew<<<grid_for(nm, 256, 8192), 256, 0, s>>>(cmem, sel8, nm, (uint32_t)n, d_new);
     SYZ_LAUNCHED();

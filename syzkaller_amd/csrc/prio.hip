@@ -37,19 +37,20 @@ __global__ __launch_bounds__(256) void k_len_hist(const uint16_t* prog_len, cons
     if (lh[i]) atomicAdd((unsigned long long*)&hist[i], lh[i]);
 }
 
-// H(k) = sum_{L > k} hist[L], clamped to 2^24 (the float32 accumulator's fixed point), as float.
-__device__ __forceinline__ void block_suffix(const int64_t* hist, int32_t C, float* Hf, int64_t* red) {
-  // process from the top: H(k) = total - sum_{L <= k} hist[L]
+// H(k) = sum_{L > k} hist[L], clamped to 2^24 (the float32 accumulator's fixed point), as float, for
+// k in [k0, C): a row block of k_prio_row only reads H(max(i, j)) >= H(i), so it builds [i, C) alone.
+__device__ __forceinline__ void block_suffix(const int64_t* hist, int32_t C, float* Hf, int64_t* red, int32_t k0 = 0) {
+  // process from k0 up: H(k) = total - sum_{k0 < L <= k} hist[L], total = sum_{L > k0} hist[L]
   int64_t carry = 0;
   int64_t total = 0;
-  for (int32_t base = 0; base <= C; base += PR_BLOCK) {
+  for (int32_t base = k0 + 1; base <= C; base += PR_BLOCK) {
     const int32_t i = base + threadIdx.x;
     total += i <= C ? hist[i] : 0;
   }
   total = block_sum<PR_BLOCK>(total, red);
-  for (int32_t base = 0; base < C; base += PR_BLOCK) {
+  for (int32_t base = k0; base < C; base += PR_BLOCK) {
     const int32_t k = base + threadIdx.x;
-    const int64_t v = k < C ? hist[k] : 0;
+    const int64_t v = k < C && k > k0 ? hist[k] : 0;
     int64_t tot;
     const int64_t incl = block_excl_scan<PR_BLOCK>(v, red, &tot) + v + carry;
     if (k < C) {
@@ -75,8 +76,8 @@ __device__ __forceinline__ int64_t go_f32_to_int(float x) {
 // mode 0: dynamic from Hf (+ optional static multiply); mode 1: prios given (ChoiceTable only);
 // mode 2: calcStaticPriorities' tail on the pair sums in prios_in (static_prio.hip): the diagonal
 // becomes the row's maximum (prio.go:124-132), then normalizePrio, written to prios_out (may alias).
-// mode 0 with hist: every row block builds H in LDS itself (no separate suffix launch on the step's
-// critical path; the same integer sums, so the same floats)
+// mode 0 with hist: every row block builds H(k), k >= its row, in LDS itself (no separate suffix launch
+// on the step's critical path; the same integer sums, so the same floats)
 __global__ __launch_bounds__(PR_BLOCK) void k_prio_row(int mode, const float* Hf, const float* static_prios,
                                                        const float* prios_in, int32_t C, const uint8_t* enabled,
                                                        float* prios_out, int64_t* run, uint8_t* present,
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(PR_BLOCK) void k_prio_row(int mode, const float* Hf
   extern __shared__ float Hs[];
   __shared__ int64_t sred[PR_BLOCK / 64 + 1];
   if (mode == 0 && hist) {
-    block_suffix(hist, C, Hs, sred);
+    block_suffix(hist, C, Hs, sred, (int32_t)blockIdx.x);
     __syncthreads();
     Hf = Hs;
   }

@@ -321,6 +321,29 @@ def test_priorities_bit_exact(C, nprogs):
         assert np.array_equal(wrun[wpres == 1], ct.run_matrix[wpres == 1])
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("C,nlong", [(4096, 60), (16384, 12)])
+def test_priorities_bit_exact_large_c(C, nlong):
+    # a few program lengths over the whole [0, C] range, so every row's suffix sums H(k >= i) are
+    # non-trivial (each row block of the fused kernel builds only its own [i, C) range); the oracle's
+    # calcDynamicPrio is the literal O(sum len^2) loop, hence few long programs beside many short ones
+    rnd = np.random.default_rng(C)
+    plen = np.concatenate([rnd.integers(0, C + 1, size=nlong), rnd.integers(0, 41, size=20_000)]).astype(np.uint16)
+    dyn_want = oracle.dynamic_prio(plen, C)
+    dyn_got = prog.calcDynamicPrio(plen, C)
+    assert np.array_equal(dyn_want.view(np.uint32), dyn_got.view(np.uint32))
+    del dyn_want, dyn_got
+    st = _static(C, C)
+    want = oracle.calculate_priorities(st, plen)
+    got = prog.CalculatePriorities(st, plen)
+    assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
+    del want
+    wrun, wpres = oracle.build_choice_table(got, None)
+    ct = prog.BuildChoiceTable(got, None)
+    assert np.array_equal(wpres, ct.present)
+    assert np.array_equal(wrun, ct.run_matrix)
+
+
 def test_choice_table_special_values():
     C = 16
     p = np.random.default_rng(3).random((C, C)).astype(np.float32)
