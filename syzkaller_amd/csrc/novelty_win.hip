@@ -13,10 +13,11 @@
 //   G  group partition (stable) + members + lengths (a trailing 0xFFFFFFFF dropped) + the PC span
 //   P  k_part3<NOV>: the members' PCs transposed into 2^SB-address windows (one HBM read per PC), every
 //      list checked strictly increasing on the way
-//   M  k_nw_min: a workgroup per (call, window): direct min-rank table in LDS, then one pass over it in
-//      PC order: a key is kept if the table holds it or a non-flake cover does (flakes of the window in
-//      an LDS bitmap), a cover that wins a kept key is new (byte stores, deduplicated by an LDS rank
-//      bitmap); the kept keys leave as a 4 KB bitmap per window, their count beside it
+//   M  k_nw_min: a workgroup per (call, window): direct min-rank table in LDS (and a presence bitmap
+//      the element that first lowers an entry sets), then one pass over the present keys in PC order:
+//      a key is kept if the table holds it or a non-flake cover does (flakes of the window in an LDS
+//      bitmap), a cover that wins a kept key is new (byte stores, deduplicated by an LDS rank bitmap);
+//      the kept keys leave as a bitmap per window (2^SB bits), their count beside it
 //   E  scan of the counts, then every window's bitmap expands to its PCs at its offset (the updated
 //      tables, sorted by (call, PC)), a table's 0xFFFFFFFF last unless the call took a Union
 //
@@ -32,53 +33,80 @@
 
 namespace syz {
 
-// window bits SB: 15 = 32K-entry tables (128 KB of LDS, one 1024-thread workgroup per CU), 14 = 16K-entry
-// tables (64 KB, two 512-thread workgroups per CU, so one's metadata and table set-up overlap the
-// other's walk)
+// Direct windows (calls with many PCs per window): 2^DB addresses, a 2^DB-entry min table. DB = 14: 64 KB
+// of LDS, two 512-thread workgroups per CU, so one's metadata and table set-up overlap the other's walk
+// (15 when the span needs it: 128 KB, one 1024-thread workgroup).
 template <uint32_t SB>
 struct NwCfg {
   static constexpr uint32_t BITS = 1u << SB;      // addresses per window
-  static constexpr uint32_t WORDS64 = BITS / 64;  // u64 words of a window's kept bitmap
-  static constexpr uint32_t FLK = BITS / 32;      // LDS flake bitmap words
+  static constexpr uint32_t FLK = BITS / 32;      // u32 words of a window's bitmaps
   static constexpr int BLOCK = SB >= 15 ? 1024 : 512;
-  static constexpr uint32_t BMW = SB >= 15 ? PBM_WORDS : 2048;  // LDS rank bitmap words (winner dedup)
-  static constexpr int EBLOCK = (int)(WORDS64 / 2);              // k_nw_emit: two words per thread
+  static constexpr uint32_t BMW = SB >= 15 ? 5120 : 2048;  // LDS rank bitmap words (winner dedup)
+};
+// Hashed windows (the other calls): 2^S addresses, S in (DB, NH_MAXB], sized so a window holds about
+// NH_TARGET PCs; an NH_SLOTS-slot open-addressing min table (rounds by key residue when it fills) and
+// an LDS kept bitmap of the window, so the kept keys still leave in PC order.
+constexpr uint32_t NH_MAXB = 17;
+constexpr uint32_t NH_SLOTS_BITS = 12;
+constexpr uint32_t NH_SLOTS = 1u << NH_SLOTS_BITS;
+constexpr uint32_t NH_CAP = NH_SLOTS * 3 / 4;  // PCs per round
+constexpr uint32_t NH_TARGET = 2048;           // PCs per window a hashed call aims at
+constexpr uint32_t NH_PROBE = 64;
+constexpr uint32_t NH_FLCAP = 1024;            // flakes of a window staged in LDS
+constexpr int NH_BLOCK = 512;
+constexpr int NE_BLOCK = 256;                  // k_nw_emit
+
+// per call: window layout of the kept bitmaps (u32 words) and of the count slots
+struct NwGroup {
+  uint64_t kbase;  // first kept-bitmap word of the call's window 0
+  uint64_t sbase;  // first count slot (W + 1 slots: the windows, then the table's 0xFFFFFFFF)
 };
 
-// combined members: call g's list is [table g (entry id n + g), its covers in batch order]
+// combined members: call g's list is [table g (entry id n + g), its covers in batch order]; inv[e] = the
+// position of entry e (covers and tables) in that order
 __global__ void k_nw_members(const uint32_t* members, const uint64_t* gstart, const uint32_t* group, size_t n,
-                             uint32_t G, uint32_t* cmem, uint64_t* cstart) {
+                             uint32_t G, uint32_t* cmem, uint64_t* cstart, uint32_t* inv) {
   const size_t tot = n > (size_t)G + 1 ? n : (size_t)G + 1;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
     if (i < n) {
       const uint32_t e = members[i];
       const uint32_t g = group[e] < G ? group[e] : 0u;  // an invalid id was counted in group 0
       cmem[i + g + 1] = e;
+      inv[e] = (uint32_t)(i + g + 1);
     }
-    if (i < G) cmem[gstart[i] + i] = (uint32_t)n + (uint32_t)i;
+    if (i < G) {
+      cmem[gstart[i] + i] = (uint32_t)n + (uint32_t)i;
+      inv[n + i] = (uint32_t)(gstart[i] + i);
+    }
     if (i <= G) cstart[i] = gstart[i] + i;
   }
 }
 
 // member lengths without a trailing 0xFFFFFFFF (foreach never matches it, cover.go:81-102; a table's
-// is put back after the windows), which tables had one, and the span of the other PCs
+// is put back after the windows), which tables had one, and the span of the other PCs; in entry order
+// (coalesced offsets, the first and last PC of neighbouring entries on neighbouring lines)
 __global__ __launch_bounds__(256) void k_nw_meta(const uint32_t* pcs, const uint64_t* off, const uint32_t* mc,
-                                                 const uint64_t* mc_off, const uint32_t* cmem, size_t nm, uint32_t n1,
+                                                 const uint64_t* mc_off, const uint32_t* inv, size_t n, uint32_t G,
                                                  uint32_t* mlen, uint8_t* has_sent, uint32_t* span) {
   uint32_t lo = 0xFFFFFFFFu, hi = 0;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t e = cmem[i];
-    const bool tab = e >= n1;
-    const uint32_t* src = tab ? mc + mc_off[e - n1] : pcs + off[e];
-    uint64_t len = tab ? mc_off[e - n1 + 1] - mc_off[e - n1] : off[e + 1] - off[e];
-    if (len && src[len - 1] == SENT) {
-      len--;
-      if (tab) has_sent[e - n1] = 1;
-    }
-    mlen[i] = (uint32_t)len;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + G; i += (size_t)gridDim.x * blockDim.x) {
+    const bool tab = i >= n;
+    const uint32_t* src = tab ? mc + mc_off[i - n] : pcs + off[i];
+    uint64_t len = tab ? mc_off[i - n + 1] - mc_off[i - n] : off[i + 1] - off[i];
+    uint32_t first = 0, last = 0;
     if (len) {
-      lo = min(lo, src[0]);
-      hi = max(hi, src[len - 1]);
+      first = src[0];
+      last = src[len - 1];
+      if (last == SENT) {
+        len--;
+        if (tab) has_sent[i - n] = 1;
+        if (len) last = src[len - 1];
+      }
+    }
+    mlen[inv[i]] = (uint32_t)len;
+    if (len) {
+      lo = min(lo, first);
+      hi = max(hi, last);
     }
   }
   lo = wave_min(lo);
@@ -93,35 +121,127 @@ __global__ __launch_bounds__(256) void k_nw_meta(const uint32_t* pcs, const uint
   }
 }
 
+// The walk of a direct table with its LDS updates batched: every run of a group of RBN issues its
+// ds_min (with return) first, one wait, then the lanes that found the entry empty set its presence bit
+// — instead of a read, a wait and a conditional atomic per run.
+template <int RBN>
+__device__ __forceinline__ void nw_walk_direct(const PItem it, const PChunk* __restrict__ chunks, const uint64_t* gchunk,
+                                               const uint64_t* gdesc, const PGroup* pg,
+                                               const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems,
+                                               int nwaves, uint32_t* tab, uint32_t* pres) {
+  const uint32_t g = it.g, w = it.w;
+  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
+  const uint32_t W = pg[g].W, S = pg[g].S;
+  const uint32_t omask = (1u << S) - 1;
+  const uint16_t* d0 = desc + gdesc[g] + w;
+  const int wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  auto upd_one = [&](uint32_t e, uint32_t mbj) {
+    const uint32_t o = e & omask;
+    if (atomicMin(&tab[o], mbj + (e >> S)) == RANK_NONE) atomicOr(&pres[o >> 5], 1u << (o & 31));
+  };
+  const uint64_t nrun = c1 - c0;
+  for (uint64_t b0 = (uint64_t)wv; b0 < nrun; b0 += (uint64_t)nwaves * 64) {
+    const uint64_t c = c0 + b0 + (uint64_t)lane * nwaves;
+    uint32_t len = 0, mb = 0, stl = 0, sth = 0;
+    if (c < c1) {
+      const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
+      const uint32_t s0 = d[0], s1 = d[1];
+      len = s1 - s0;
+      const uint64_t st = chunks[c].elem + s0;
+      stl = (uint32_t)st;
+      sth = (uint32_t)(st >> 32);
+      mb = chunks[c].mb;
+    }
+    const uint32_t nr = (uint32_t)min<uint64_t>(64, (nrun - b0 + nwaves - 1) / nwaves);
+    for (uint32_t r0 = 0; r0 < nr; r0 += RBN) {
+      uint32_t e0[RBN], ln[RBN], mbr[RBN], old[RBN];
+      uint64_t sts[RBN];
+#pragma unroll
+      for (int r = 0; r < RBN; r++) {
+        const uint32_t j = r0 + r;
+        ln[r] = j < nr ? (uint32_t)__builtin_amdgcn_readlane((int)len, (int)j) : 0u;
+        mbr[r] = (uint32_t)__builtin_amdgcn_readlane((int)mb, (int)j);
+        sts[r] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sth, (int)j) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane((int)stl, (int)j);
+        e0[r] = lane < ln[r] ? elems[sts[r] + lane] : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < RBN; r++)
+        old[r] = lane < ln[r] ? atomicMin(&tab[e0[r] & omask], mbr[r] + (e0[r] >> S)) : 0u;
+#pragma unroll
+      for (int r = 0; r < RBN; r++)
+        if (lane < ln[r] && old[r] == RANK_NONE) {
+          const uint32_t o = e0[r] & omask;
+          atomicOr(&pres[o >> 5], 1u << (o & 31));
+        }
+#pragma unroll
+      for (int r = 0; r < RBN; r++) {
+        for (uint32_t k = 64; k < ln[r]; k += 64 * TU) {  // long runs: TU 64-PC slices in flight
+          uint32_t x[TU];
+#pragma unroll
+          for (int u = 0; u < TU; u++) {
+            const uint32_t i = k + 64 * u + lane;
+            x[u] = i < ln[r] ? elems[sts[r] + i] : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < TU; u++)
+            if (k + 64 * u + lane < ln[r]) upd_one(x[u], mbr[r]);
+        }
+      }
+    }
+  }
+}
+
+// SYZGPU_NW_WALK=0 (A/B): the direct tables through for_window_elems (read, compare, atomic per run)
+static int nw_walk_kind() {
+  static const int v = getenv("SYZGPU_NW_WALK") ? atoi(getenv("SYZGPU_NW_WALK")) : 1;
+  return v;
+}
+
 // M: one (call, window). tab = min member position per window offset; the table's position cstart[g]
 // is OLD.
 template <uint32_t SB>
 __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
     const PItem* items, const PChunk* __restrict__ chunks, const uint64_t* gchunk, const uint64_t* gdesc,
     const PGroup* pg, const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems, const uint64_t* cstart,
-    uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart, unsigned long long* kbits,
-    uint32_t* wcount, uint8_t* sel8, uint8_t* upd, int dbg) {
+    uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart, const NwGroup* ng_,
+    uint32_t* kbits, uint32_t* wcount, uint8_t* sel8, uint8_t* upd, int dbg, int walk) {
   using K = NwCfg<SB>;
   constexpr int BLOCK = K::BLOCK;
-  __shared__ uint32_t tab[K::BITS];
+  __shared__ __align__(16) uint32_t tab[K::BITS];
   __shared__ uint32_t bm[K::BMW];
   __shared__ uint32_t flk[K::FLK];
+  __shared__ uint32_t pres[K::FLK];  // offsets some member holds (set by the element that lowers NONE)
   __shared__ uint32_t red[BLOCK / 64 + 1];
   const PItem it = items[blockIdx.x];
-  const uint32_t g = it.g, w = it.w, W = pg[g].W;
-  for (uint32_t i = threadIdx.x; i < K::BITS; i += BLOCK) tab[i] = RANK_NONE;
-  for (uint32_t i = threadIdx.x; i < K::FLK; i += BLOCK) flk[i] = 0;
+  const uint32_t g = it.g, w = it.w;
+  {
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+    const uint4 none4 = make_uint4(RANK_NONE, RANK_NONE, RANK_NONE, RANK_NONE);
+    for (uint32_t i = threadIdx.x; i < K::BITS / 4; i += BLOCK) t4[i] = none4;
+  }
+  for (uint32_t i = threadIdx.x; i < K::FLK; i += BLOCK) {
+    flk[i] = 0;
+    pres[i] = 0;
+  }
   __syncthreads();
   // the flakes inside this window's addresses: fl[fstart[w], fstart[w + 1])
   const uint32_t wlo = lo + (w << SB);
   for (uint32_t i = fstart[w] + threadIdx.x; i < fstart[w + 1]; i += BLOCK) {
-    const uint32_t o = fl[i] - wlo;
-    atomicOr(&flk[o >> 5], 1u << (o & 31));
+    const uint32_t o = fl[i] - wlo;  // flakes not increasing (rejected after the batch) land anywhere
+    if (o < K::BITS) atomicOr(&flk[o >> 5], 1u << (o & 31));
   }
-  if (!(dbg & 1))
+  if (!(dbg & 1) && walk == 1)
+    nw_walk_direct<SYZ_DIRECT_RB>(it, chunks, gchunk, gdesc, pg, desc, elems, BLOCK / 64, tab, pres);
+  else if (!(dbg & 1))
     for_window_elems<SYZ_DIRECT_RB, true>(it, chunks, gchunk, gdesc, pg, desc, elems, nullptr, 0u, BLOCK / 64,
                                           [&](uint32_t o, uint32_t R) {
-                                            if (tab[o] > R) atomicMin(&tab[o], R);
+                                            if (tab[o] > R) {
+                                              atomicMin(&tab[o], R);
+                                              const uint32_t bit = 1u << (o & 31);
+                                              if (!(pres[o >> 5] & bit)) atomicOr(&pres[o >> 5], bit);
+                                            }
                                           });
   if (dbg & 2) return;
   const uint64_t gb = cstart[g], ng = cstart[g + 1] - gb;
@@ -129,36 +249,38 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
   const uint32_t words = (span + 31) / 32;
   for (uint32_t i = threadIdx.x; i < words; i += BLOCK) bm[i] = 0;
   __syncthreads();
-  // in PC order: kept keys as bitmap words, new covers marked
-  const unsigned lane = __lane_id();
-  const uint64_t slot_bits = ((uint64_t)g * W + w) * K::WORDS64;
+  // the present offsets in PC order, a 32-offset word per thread: kept keys as bitmap words (coalesced
+  // u32 stores), new covers marked
+  const NwGroup gl = ng_[g];
+  uint32_t* kb32 = kbits + gl.kbase + (uint64_t)w * K::FLK;
   uint32_t cnt = 0;
   int anynew = 0;
-#pragma unroll 4
-  for (uint32_t i = 0; i < K::BITS / BLOCK; i++) {
-    const uint32_t o = i * BLOCK + threadIdx.x;
-    const uint32_t r = tab[o];
-    const bool old = r == (uint32_t)gb;
-    const bool flake = (flk[o >> 5] >> (o & 31)) & 1u;
-    const bool keep = r != RANK_NONE && (old || !flake);
-    const uint64_t bal = __ballot(keep);
-    if (lane == 0) {
-      kbits[slot_bits + (o >> 6)] = bal;
-      cnt += (uint32_t)__popcll(bal);
-    }
-    if (keep && !old) {
-      anynew = 1;
-      const uint64_t lr = (uint64_t)r - gb;
-      if (lr < span) {
-        const uint32_t bit = 1u << (lr & 31);
-        if (!(bm[lr >> 5] & bit)) atomicOr(&bm[lr >> 5], bit);
-      } else {
-        sel8[r] = 1;
+  for (uint32_t wd = threadIdx.x; wd < K::FLK; wd += BLOCK) {
+    uint32_t m = pres[wd], kw = 0;
+    const uint32_t fw = flk[wd];
+    while (m) {
+      const uint32_t b = __ffs(m) - 1;
+      m &= m - 1;
+      const uint32_t r = tab[32 * wd + b];
+      const bool old = r == (uint32_t)gb;
+      if (!old && ((fw >> b) & 1u)) continue;  // a flake no table holds: never new, never kept
+      kw |= 1u << b;
+      if (!old) {
+        anynew = 1;
+        const uint64_t lr = (uint64_t)r - gb;
+        if (lr < span) {
+          const uint32_t bit = 1u << (lr & 31);
+          if (!(bm[lr >> 5] & bit)) atomicOr(&bm[lr >> 5], bit);
+        } else {
+          sel8[r] = 1;
+        }
       }
     }
+    kb32[wd] = kw;
+    cnt += (uint32_t)__popc(kw);
   }
   const uint32_t tot = block_sum<BLOCK>(cnt, red);
-  if (threadIdx.x == 0) wcount[(uint64_t)g * (W + 1) + w] = tot;
+  if (threadIdx.x == 0) wcount[gl.sbase + w] = tot;
   if (__syncthreads_or(anynew) && threadIdx.x == 0) upd[g] = 1;
   for (uint32_t i = threadIdx.x; i < words; i += BLOCK) {
     uint32_t v = bm[i];
@@ -170,7 +292,144 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
   }
 }
 
-// fstart[w] = the first flake at or above window w's first address (w in [0, W]; nfl past the span)
+// PCs of one (call, window) over all its chunks' runs (metadata only)
+template <int BLOCK>
+__device__ uint32_t nw_window_elems(const PItem it, const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
+                                    const uint16_t* __restrict__ desc, uint32_t* red) {
+  const uint32_t g = it.g, w = it.w, W = pg[g].W;
+  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
+  const uint16_t* d0 = desc + gdesc[g] + w;
+  uint32_t s = 0;
+  for (uint64_t c = c0 + threadIdx.x; c < c1; c += BLOCK) {
+    const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
+    s += (uint32_t)d[1] - d[0];
+  }
+  return block_sum<BLOCK>(s, red);
+}
+
+__device__ __forceinline__ uint32_t nh_slot(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - NH_SLOTS_BITS); }
+
+// M, hashed: one (call, window) of 2^S addresses (S = pg[g].S, at most NH_MAXB)
+__global__ __launch_bounds__(NH_BLOCK) void k_nw_hmin(
+    const PItem* items, const PChunk* __restrict__ chunks, const uint64_t* gchunk, const uint64_t* gdesc,
+    const PGroup* pg, const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems, const uint64_t* cstart,
+    uint32_t lo, uint32_t db, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart, uint32_t wdb,
+    const NwGroup* ng_, uint32_t* kbits, uint32_t* wcount, uint8_t* sel8, uint8_t* upd) {
+  constexpr int BLOCK = NH_BLOCK;
+  constexpr uint32_t KW = (1u << NH_MAXB) / 32;
+  constexpr uint32_t BMW = 2048;
+  __shared__ uint32_t keys[NH_SLOTS];
+  __shared__ uint32_t vals[NH_SLOTS];
+  __shared__ uint32_t kept[KW];
+  __shared__ uint32_t bm[BMW];
+  __shared__ uint32_t flist[NH_FLCAP];
+  __shared__ uint32_t red[BLOCK / 64 + 1];
+  __shared__ int full;
+  const PItem it = items[blockIdx.x];
+  const uint32_t g = it.g, w = it.w, S = pg[g].S;
+  const uint32_t nkw = (1u << S) / 32;
+  const uint32_t wlo = lo + (w << S);
+  const uint64_t gb = cstart[g], ng = cstart[g + 1] - gb;
+  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BMW * 32, ng);
+  const uint32_t words = (span + 31) / 32;
+  // the window's flakes: those of its direct-size sub-windows
+  const uint32_t f0 = fstart[min(w << (S - db), wdb)], f1 = fstart[min((w + 1) << (S - db), wdb)];
+  const bool fl_lds = f1 - f0 <= NH_FLCAP;
+  for (uint32_t i = threadIdx.x; i < nkw; i += BLOCK) kept[i] = 0;
+  for (uint32_t i = threadIdx.x; i < words; i += BLOCK) bm[i] = 0;
+  if (fl_lds)
+    for (uint32_t i = f0 + threadIdx.x; i < f1; i += BLOCK) flist[i - f0] = fl[i];
+  const uint32_t E = nw_window_elems<BLOCK>(it, gchunk, gdesc, pg, desc, red);  // (synchronizes)
+  int anynew = 0;
+  uint32_t R = E ? (E + NH_CAP - 1) / NH_CAP : 0;
+  for (uint32_t round = 0; round < R;) {
+    for (uint32_t i = threadIdx.x; i < NH_SLOTS; i += BLOCK) {
+      keys[i] = 0xFFFFFFFFu;
+      vals[i] = RANK_NONE;
+    }
+    if (threadIdx.x == 0) full = 0;
+    __syncthreads();
+    const uint32_t RR = R, rr = round;
+    for_window_elems<4, true>(it, chunks, gchunk, gdesc, pg, desc, elems, nullptr, 0u, BLOCK / 64,
+                              [&](uint32_t o, uint32_t Rk) {
+                                if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
+                                uint32_t h = nh_slot(o);
+                                for (uint32_t probes = 0; probes < NH_PROBE; probes++) {
+                                  uint32_t k = keys[h];
+                                  if (k == 0xFFFFFFFFu) {
+                                    k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
+                                    if (k == 0xFFFFFFFFu) k = o;
+                                  }
+                                  if (k == o) {
+                                    if (vals[h] > Rk) atomicMin(&vals[h], Rk);
+                                    return;
+                                  }
+                                  h = (h + 1) & (NH_SLOTS - 1);
+                                }
+                                full = 1;
+                              });
+    __syncthreads();
+    if (full) {  // redo every round with twice as many (marks already made are exact and idempotent)
+      R *= 2;
+      round = 0;
+      __syncthreads();
+      continue;
+    }
+    // this round's keys: kept bit unless a flake no table holds; the first cover of a kept key is new
+    for (uint32_t i = threadIdx.x; i < NH_SLOTS; i += BLOCK) {
+      const uint32_t o = keys[i];
+      if (o == 0xFFFFFFFFu) continue;
+      const uint32_t r = vals[i];
+      const bool old = r == (uint32_t)gb;
+      if (!old) {
+        const uint32_t pc = wlo + o;
+        bool flake;
+        if (fl_lds) {
+          const uint32_t j = (uint32_t)lower_bound_dev<uint32_t>(flist, 0, f1 - f0, pc);
+          flake = j < f1 - f0 && flist[j] == pc;
+        } else {
+          const uint64_t j = lower_bound_dev<uint32_t>(fl, f0, f1, pc);
+          flake = j < f1 && fl[j] == pc;
+        }
+        if (flake) continue;
+        anynew = 1;
+        const uint64_t lr = (uint64_t)r - gb;
+        if (lr < span) {
+          const uint32_t bit = 1u << (lr & 31);
+          if (!(bm[lr >> 5] & bit)) atomicOr(&bm[lr >> 5], bit);
+        } else {
+          sel8[r] = 1;
+        }
+      }
+      atomicOr(&kept[o >> 5], 1u << (o & 31));
+    }
+    round++;
+    __syncthreads();
+  }
+  __syncthreads();
+  const NwGroup gl = ng_[g];
+  uint32_t* kb32 = kbits + gl.kbase + (uint64_t)w * nkw;
+  uint32_t cnt = 0;
+  for (uint32_t i = threadIdx.x; i < nkw; i += BLOCK) {
+    const uint32_t v = kept[i];
+    kb32[i] = v;
+    cnt += (uint32_t)__popc(v);
+  }
+  const uint32_t tot = block_sum<BLOCK>(cnt, red);
+  if (threadIdx.x == 0) wcount[gl.sbase + w] = tot;
+  if (__syncthreads_or(anynew) && threadIdx.x == 0) upd[g] = 1;
+  for (uint32_t i = threadIdx.x; i < words; i += BLOCK) {
+    uint32_t v = bm[i];
+    while (v) {
+      const uint32_t b = __ffs(v) - 1;
+      sel8[gb + 32ull * i + b] = 1;
+      v &= v - 1;
+    }
+  }
+}
+
+// fstart[w] = the first flake at or above direct-size window w's first address (w in [0, W]; nfl past
+// the span)
 __global__ void k_nw_fstart(const uint32_t* fl, uint64_t nfl, uint32_t lo, uint32_t W, uint32_t sb, uint32_t* fstart) {
   for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w <= W; w += gridDim.x * blockDim.x) {
     const uint64_t a = (uint64_t)lo + ((uint64_t)w << sb);
@@ -178,28 +437,35 @@ __global__ void k_nw_fstart(const uint32_t* fl, uint64_t nfl, uint32_t lo, uint3
   }
 }
 
-// slot W of every call: its table's 0xFFFFFFFF stays unless the call took a Union (Union goes through
-// foreach, cover.go:81-102)
-__global__ void k_nw_sent(const uint8_t* has_sent, const uint8_t* upd, uint32_t G, uint32_t W, uint32_t* wcount) {
+// the last slot of every call: its table's 0xFFFFFFFF stays unless the call took a Union (Union goes
+// through foreach, cover.go:81-102)
+__global__ void k_nw_sent(const uint8_t* has_sent, const uint8_t* upd, const NwGroup* ng_, uint32_t G, uint32_t* wcount) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x)
-    wcount[(uint64_t)g * (W + 1) + W] = has_sent[g] && !upd[g] ? 1u : 0u;
+    wcount[ng_[g + 1].sbase - 1] = has_sent[g] && !upd[g] ? 1u : 0u;
 }
 
 // E: one slot per workgroup; the window's kept bitmap -> its PCs at wpos[slot]
-template <uint32_t SB>
-__global__ __launch_bounds__(NwCfg<SB>::EBLOCK) void k_nw_emit(const unsigned long long* __restrict__ kbits,
-                                                      const uint64_t* __restrict__ wpos, uint32_t G, uint32_t W,
-                                                      uint32_t lo, uint32_t* out, uint64_t cap, uint64_t* ooff,
-                                                      int* err) {
-  using K = NwCfg<SB>;
-  constexpr int NE_BLOCK = K::EBLOCK;
+__global__ __launch_bounds__(NE_BLOCK) void k_nw_emit(const uint32_t* __restrict__ kbits,
+                                                      const uint64_t* __restrict__ wpos, const NwGroup* ng_,
+                                                      const PGroup* pg, uint32_t G, uint32_t lo, uint32_t* out,
+                                                      uint64_t cap, uint64_t* ooff, int* err) {
   __shared__ uint32_t red[NE_BLOCK / 64 + 1];
   const uint64_t slot = blockIdx.x;
-  const uint32_t g = (uint32_t)(slot / (W + 1)), w = (uint32_t)(slot % (W + 1));
+  uint32_t g0 = 0, g1 = G;  // the call: last g with sbase <= slot
+  while (g1 - g0 > 1) {
+    const uint32_t mid = (g0 + g1) >> 1;
+    if (ng_[mid].sbase <= slot)
+      g0 = mid;
+    else
+      g1 = mid;
+  }
+  const uint32_t g = g0;
+  const NwGroup gl = ng_[g];
+  const uint32_t w = (uint32_t)(slot - gl.sbase), W = pg[g].W, S = pg[g].S;
   const uint64_t p0 = wpos[slot], c = wpos[slot + 1] - p0;
   if (threadIdx.x == 0 && w == 0) {
     ooff[g] = p0;
-    if (g + 1 == G) ooff[G] = wpos[(uint64_t)G * (W + 1)];
+    if (g + 1 == G) ooff[G] = wpos[ng_[G].sbase];
   }
   if (c == 0) return;
   if (p0 + c > cap) {
@@ -210,17 +476,19 @@ __global__ __launch_bounds__(NwCfg<SB>::EBLOCK) void k_nw_emit(const unsigned lo
     if (threadIdx.x == 0) out[p0] = SENT;
     return;
   }
-  const uint64_t base = ((uint64_t)g * W + w) * K::WORDS64 + 2 * threadIdx.x;
-  const unsigned long long b0 = kbits[base], b1 = kbits[base + 1];
+  const uint32_t q = (1u << S) / 32 / NE_BLOCK;  // words per thread (2 .. 16)
+  const uint32_t* kb = kbits + gl.kbase + (uint64_t)w * ((1u << S) / 32) + (uint64_t)threadIdx.x * q;
+  uint32_t pc = 0;
+  for (uint32_t i = 0; i < q; i++) pc += (uint32_t)__popc(kb[i]);
   uint32_t tot;
-  uint64_t p = p0 + block_excl_scan<NE_BLOCK>((uint32_t)(__popcll(b0) + __popcll(b1)), red, &tot);
-  const uint32_t a0 = lo + (w << SB) + 128u * threadIdx.x;
-  for (int h = 0; h < 2; h++) {
-    unsigned long long m = h ? b1 : b0;
+  uint64_t p = p0 + block_excl_scan<NE_BLOCK>(pc, red, &tot);
+  const uint32_t a0 = lo + (w << S) + 32u * q * threadIdx.x;
+  for (uint32_t i = 0; i < q; i++) {
+    uint32_t m = kb[i];
     while (m) {
-      const int i = __ffsll(m) - 1;
+      const uint32_t b = __ffs(m) - 1;
       m &= m - 1;
-      out[p++] = a0 + 64u * h + (uint32_t)i;
+      out[p++] = a0 + 32u * i + b;
     }
   }
 }
@@ -238,10 +506,22 @@ static int nw_dbg() {
   return v;
 }
 
-// SYZGPU_NW_BITS=14|15: window bits (default: 14 while the span fits 1024 such windows, else 15)
+// SYZGPU_NW_BITS=14|15: direct window bits (default: 14 while the span fits 1024 such windows, else 15)
 static uint32_t nw_bits_forced() {
   static const uint32_t v = getenv("SYZGPU_NW_BITS") ? (uint32_t)atoi(getenv("SYZGPU_NW_BITS")) : 0u;
   return v == 14 || v == 15 ? v : 0u;
+}
+
+// SYZGPU_NW_HASH=1: hashed windows for the calls with few PCs (A/B; measured 2.65 vs 2.47 ms for all
+// direct at config 3)
+static bool nw_hash() {
+  static const bool v = getenv("SYZGPU_NW_HASH") && atoi(getenv("SYZGPU_NW_HASH")) != 0;
+  return v;
+}
+
+__global__ void k_nw_gpcs(const uint64_t* mpos, const uint64_t* cstart, uint32_t G, uint64_t* gpcs) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x)
+    gpcs[g] = mpos[cstart[g + 1]] - mpos[cstart[g]];
 }
 
 // false: the span does not fit the direct windows (or G is too large): use another strategy. err gets
@@ -259,6 +539,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
   uint32_t* cmem = sc.get<uint32_t>("nw_cmem", nm + 1);
   uint32_t* mlen = sc.get<uint32_t>("nw_mlen", nm + 1);
+  uint32_t* inv = sc.get<uint32_t>("nw_inv", nm + 1);
   uint64_t* mpos = sc.get<uint64_t>("nw_mpos", nm + 1);
   uint8_t* has_sent = sc.get<uint8_t>("nw_has_sent", G + 1);
   uint8_t* upd = sc.get<uint8_t>("nw_upd", G + 1);
@@ -275,60 +556,90 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     ProfScope ps("novelty_group", s, (uint64_t)n * 28 + (uint64_t)nm * 24);
     group_partition_dev(d_grp, d_off, n, G, gstart, members, el, perr, s);
     k_nw_members<<<grid_for(std::max<size_t>(n, G + 1), 256, 8192), 256, 0, s>>>(members, gstart, d_grp, n, G, cmem,
-                                                                                 cstart);
+                                                                                 cstart, inv);
     SYZ_LAUNCHED();
-    k_nw_meta<<<grid_for(nm, 256, 4096), 256, 0, s>>>(d_pcs, d_off, d_mc, d_mco, cmem, nm, (uint32_t)n, mlen, has_sent,
-                                                      span);
+    k_nw_meta<<<grid_for(nm, 256, 4096), 256, 0, s>>>(d_pcs, d_off, d_mc, d_mco, inv, n, G, mlen, has_sent, span);
     SYZ_LAUNCHED();
     exclusive_scan_u32(mlen, mpos, nm, s);
   }
-  uint64_t* hbuf = c.pinned.get<uint64_t>((size_t)G + 8);
+  uint64_t* gpcs = sc.get<uint64_t>("nw_gpcs", G + 1);
+  k_nw_gpcs<<<grid_for(G, 256, 64), 256, 0, s>>>(mpos, cstart, G, gpcs);
+  SYZ_LAUNCHED();
+  uint64_t* hbuf = c.pinned.get<uint64_t>(2 * (size_t)G + 8);
   SYZ_HIP(hipMemcpyAsync(hbuf, cstart, (G + 1) * 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipMemcpyAsync(hbuf + G + 1, mpos + nm, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipMemcpyAsync(hbuf + G + 2, span, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipMemcpyAsync(hbuf + G + 3, perr, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hbuf + G + 4, gpcs, G * 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   if (*reinterpret_cast<int*>(hbuf + G + 3)) fail(SYZGPU_EINVAL, "group id >= ngroups");
-  const std::vector<uint64_t> hstart(hbuf, hbuf + G + 1);
+  const std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 4, hbuf + 2 * G + 4);
   const uint64_t total = hbuf[G + 1];
   uint32_t lo = reinterpret_cast<uint32_t*>(hbuf + G + 2)[0], hi = reinterpret_cast<uint32_t*>(hbuf + G + 2)[1];
   if (lo > hi) lo = hi = 0;  // no PCs outside the sentinel
-  auto nwin = [&](uint32_t sb) { return (((uint64_t)hi - (lo & ~((1u << sb) - 1))) >> sb) + 1; };
-  uint32_t SB = nw_bits_forced();
-  if (!SB) SB = nwin(14) <= WMAX ? 14 : 15;
-  if (nwin(SB) > WMAX) return false;
-  lo &= ~((1u << SB) - 1);  // windows on 2^SB boundaries: a window's addresses never wrap
-  const uint32_t W = (uint32_t)nwin(SB);
-  const uint32_t words64 = (1u << SB) / 64;
-  // ---- plan: every call direct-mapped on W windows; blocks of 64 members; work items ----
+  // windows on 2^NH_MAXB boundaries (a window's addresses never wrap, and every size nests)
+  lo &= ~((1u << NH_MAXB) - 1);
+  auto nwin = [&](uint32_t sb) { return (((uint64_t)hi - lo) >> sb) + 1; };
+  uint32_t DB = nw_bits_forced();
+  if (!DB) DB = nwin(14) <= WMAX ? 14 : 15;
+  if (nwin(DB) > WMAX) return false;
+  const uint32_t WD = (uint32_t)nwin(DB);
+  // ---- plan: per call direct (DB) or hashed windows (S in (DB, NH_MAXB]); blocks; work items ----
+  std::vector<PGroup> hpg(G);
+  std::vector<NwGroup> hng(G + 1);
+  uint64_t kw = 0, slots = 0;
+  for (uint32_t g = 0; g < G; g++) {
+    uint32_t S = DB;
+    if (nw_hash() && hpcs[g] < (uint64_t)NH_TARGET * WD) {  // fewer than NH_TARGET PCs per direct window
+      S = DB + 1;
+      while (S < NH_MAXB && hpcs[g] <= (uint64_t)NH_TARGET * nwin(S + 1)) S++;
+    }
+    const uint32_t W = (uint32_t)nwin(S);
+    hpg[g] = PGroup{S, W, S == DB ? (uint32_t)PMODE_DIRECT : (uint32_t)PMODE_HASH, 0};
+    hng[g] = NwGroup{kw, slots};
+    kw += (uint64_t)W << (S - 5);
+    slots += W + 1;
+  }
+  hng[G] = NwGroup{kw, slots};
   std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
+  uint64_t desc_bound = 0;
   for (uint32_t g = 0; g < G; g++) {
     const uint32_t nb = (uint32_t)((hstart[g + 1] - hstart[g] + MEMB - 1) / MEMB);
     hgblock[g + 1] = hgblock[g] + nb;
     hbgroup.insert(hbgroup.end(), nb, g);
+    desc_bound += (nb + hpcs[g] / PCAP + 1) * (uint64_t)(hpg[g].W + 1);  // chunks of g <= nb + PCs / PCAP + 1
   }
   const uint32_t B = hgblock[G];
-  const uint64_t chunk_bound = B + total / PCAP + 1;
-  const uint64_t desc_bound = chunk_bound * (W + 1);
-  // items: larger calls first (their windows are the long ones), so the grid's tail is short
+  const uint64_t chunk_bound = B + total / PCAP + G + 1;
+  // items: direct and hashed, each larger calls first (their windows are the long ones)
   std::vector<uint32_t> order(G);
   std::iota(order.begin(), order.end(), 0u);
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
-    return hstart[x + 1] - hstart[x] > hstart[y + 1] - hstart[y];
-  });
-  const size_t nitems = (size_t)G * W;
-  const size_t stage_bytes = (G + 1) * sizeof(PGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 + nitems * sizeof(PItem);
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hpcs[x] > hpcs[y]; });
+  std::vector<PItem> hitems;
+  size_t ndirect = 0;
+  for (int mode = 0; mode < 2; mode++) {
+    for (uint32_t g : order)
+      if (hpg[g].mode == (uint32_t)mode)
+        for (uint32_t w = 0; w < hpg[g].W; w++) hitems.push_back(PItem{g, w});
+    if (mode == 0) ndirect = hitems.size();
+  }
+  const size_t nitems = hitems.size(), nhash = nitems - ndirect;
+  const size_t stage_bytes = (G + 1) * sizeof(PGroup) + (G + 1) * sizeof(NwGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 +
+                             nitems * sizeof(PItem);
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
   PGroup* dpg = sc.get<PGroup>("nw_pg", G + 1);
+  NwGroup* dng = sc.get<NwGroup>("nw_ng", G + 1);
   uint32_t* dgblock = sc.get<uint32_t>("nw_gblock", G + 1);
   uint32_t* dbgroup = sc.get<uint32_t>("nw_bgroup", (size_t)B + 1);
   PItem* ditems = sc.get<PItem>("nw_items", nitems + 1);
   {
     uint8_t* p = stage;
-    PGroup* hp = reinterpret_cast<PGroup*>(p);
-    for (uint32_t g = 0; g < G; g++) hp[g] = PGroup{SB, W, PMODE_DIRECT, 0};
+    std::memcpy(p, hpg.data(), G * sizeof(PGroup));
     SYZ_HIP(hipMemcpyAsync(dpg, p, G * sizeof(PGroup), hipMemcpyHostToDevice, s));
     p += (G + 1) * sizeof(PGroup);
+    std::memcpy(p, hng.data(), (G + 1) * sizeof(NwGroup));
+    SYZ_HIP(hipMemcpyAsync(dng, p, (G + 1) * sizeof(NwGroup), hipMemcpyHostToDevice, s));
+    p += (G + 1) * sizeof(NwGroup);
     std::memcpy(p, hgblock.data(), (G + 1) * 4);
     SYZ_HIP(hipMemcpyAsync(dgblock, p, (G + 1) * 4, hipMemcpyHostToDevice, s));
     p += (G + 1) * 4;
@@ -337,11 +648,10 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
       SYZ_HIP(hipMemcpyAsync(dbgroup, p, (size_t)B * 4, hipMemcpyHostToDevice, s));
     }
     p += ((size_t)B + 1) * 4;
-    PItem* hi_ = reinterpret_cast<PItem*>(p);
-    size_t k = 0;
-    for (uint32_t g : order)
-      for (uint32_t w = 0; w < W; w++) hi_[k++] = PItem{g, w};
-    SYZ_HIP(hipMemcpyAsync(ditems, p, nitems * sizeof(PItem), hipMemcpyHostToDevice, s));
+    if (nitems) {
+      std::memcpy(p, hitems.data(), nitems * sizeof(PItem));
+      SYZ_HIP(hipMemcpyAsync(ditems, p, nitems * sizeof(PItem), hipMemcpyHostToDevice, s));
+    }
   }
   uint32_t* nsub = sc.get<uint32_t>("nw_nsub", (size_t)B + 1);
   uint64_t* cstartb = sc.get<uint64_t>("nw_cstartb", (size_t)B + 1);
@@ -350,10 +660,9 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   uint64_t* gdesc = sc.get<uint64_t>("nw_gdesc", G + 1);
   uint16_t* desc = sc.get<uint16_t>("nw_desc", desc_bound + 1);
   uint32_t* elems = sc.get<uint32_t>("pm_elems", total + 1);
-  const size_t nslots = (size_t)G * (W + 1);
-  unsigned long long* kbits = sc.get<unsigned long long>("nw_kbits", nitems * words64 + 1);
-  uint32_t* wcount = sc.get<uint32_t>("nw_wcount", nslots + 1);
-  uint64_t* wpos = sc.get<uint64_t>("nw_wpos", nslots + 1);
+  uint32_t* kbits = sc.get<uint32_t>("nw_kbits", kw + 1);
+  uint32_t* wcount = sc.get<uint32_t>("nw_wcount", slots + 1);
+  uint64_t* wpos = sc.get<uint64_t>("nw_wpos", slots + 1);
   uint8_t* sel8 = sc.get<uint8_t>("nw_sel8", nm + 1);
   SYZ_HIP(hipMemsetAsync(sel8, 0, nm + 1, s));
   {
@@ -377,28 +686,34 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
         d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, gchunk, gdesc, lo, elems, desc, err, ns);
     SYZ_LAUNCHED();
   }
-  uint32_t* fstart = sc.get<uint32_t>("nw_fstart", (size_t)W + 2);
+  uint32_t* fstart = sc.get<uint32_t>("nw_fstart", (size_t)WD + 2);
   {
-    ProfScope ps("novelty_min", s, total * 4 + nitems * words64 * 8);
-    k_nw_fstart<<<grid_for(W + 1, 256, 64), 256, 0, s>>>(d_fl, nfl, lo, W, SB, fstart);
+    ProfScope ps("novelty_min", s, total * 4 + kw * 4);
+    k_nw_fstart<<<grid_for(WD + 1, 256, 64), 256, 0, s>>>(d_fl, nfl, lo, WD, DB, fstart);
     SYZ_LAUNCHED();
-    if (SB == 14)
-      k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems, cstart,
-                                                                 lo, d_fl, fstart, kbits, wcount, sel8, upd, nw_dbg());
-    else
-      k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems, cstart,
-                                                                 lo, d_fl, fstart, kbits, wcount, sel8, upd, nw_dbg());
-    SYZ_LAUNCHED();
+    if (ndirect) {
+      if (DB == 14)
+        k_nw_min<14><<<(unsigned)ndirect, NwCfg<14>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems,
+                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
+                                                                    upd, nw_dbg(), nw_walk_kind());
+      else
+        k_nw_min<15><<<(unsigned)ndirect, NwCfg<15>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems,
+                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
+                                                                    upd, nw_dbg(), nw_walk_kind());
+      SYZ_LAUNCHED();
+    }
+    if (nhash) {
+      k_nw_hmin<<<(unsigned)nhash, NH_BLOCK, 0, s>>>(ditems + ndirect, chunks, gchunk, gdesc, dpg, desc, elems, cstart,
+                                                     lo, DB, d_fl, fstart, WD, dng, kbits, wcount, sel8, upd);
+      SYZ_LAUNCHED();
+    }
   }
   {
-    ProfScope ps("novelty_emit", s, nitems * words64 * 8 + (uint64_t)nm * 6);
-    k_nw_sent<<<grid_for(G, 256, 64), 256, 0, s>>>(has_sent, upd, G, W, wcount);
+    ProfScope ps("novelty_emit", s, kw * 4 + (uint64_t)nm * 6);
+    k_nw_sent<<<grid_for(G, 256, 64), 256, 0, s>>>(has_sent, upd, dng, G, wcount);
     SYZ_LAUNCHED();
-    exclusive_scan_u32(wcount, wpos, nslots, s);
-    if (SB == 14)
-      k_nw_emit<14><<<(unsigned)nslots, NwCfg<14>::EBLOCK, 0, s>>>(kbits, wpos, G, W, lo, d_out, out_cap, d_ooff, err);
-    else
-      k_nw_emit<15><<<(unsigned)nslots, NwCfg<15>::EBLOCK, 0, s>>>(kbits, wpos, G, W, lo, d_out, out_cap, d_ooff, err);
+    exclusive_scan_u32(wcount, wpos, slots, s);
+    k_nw_emit<<<(unsigned)slots, NE_BLOCK, 0, s>>>(kbits, wpos, dng, dpg, G, lo, d_out, out_cap, d_ooff, err);
     SYZ_LAUNCHED();
     k_nw_isnew<<<grid_for(nm, 256, 8192), 256, 0, s>>>(cmem, sel8, nm, (uint32_t)n, d_new);
     SYZ_LAUNCHED();

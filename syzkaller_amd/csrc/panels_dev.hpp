@@ -155,6 +155,7 @@ __global__ __launch_bounds__(BLOCK) void k_part3(
   __shared__ uint32_t red[WAVES + 1];
   __shared__ uint4 tinfo[TMAX];
   __shared__ uint32_t tlast[NOV ? TMAX : 1];  // NOV: the last PC of every tile
+  __shared__ uint8_t mtab[NOV ? MEMB : 1];    // NOV: the member is a table
   const uint64_t c = blockIdx.x;
   if (c >= *nchunks_dev) return;
   const int wv = threadIdx.x >> 6;
@@ -174,9 +175,10 @@ __global__ __launch_bounds__(BLOCK) void k_part3(
       mhi[m] = y;
       const uint32_t e = members[ch.mb + m];
       const uint32_t* src;
-      if constexpr (NOV)
+      if constexpr (NOV) {
         src = e >= ns.n1 ? ns.mc + ns.mc_off[e - ns.n1] : pcs + off[e];
-      else
+        mtab[m] = e >= ns.n1;
+      } else
         src = pcs + off[e] + (sbeg ? sbeg[ch.mb + m] : 0u);
       mraw[m] = (uint64_t)(uintptr_t)src - a * 4;
       nt = y > x ? (y - x + 63) / 64 : 0;
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(BLOCK) void k_part3(
     const uint64_t base = mraw[m] + (uint64_t)q0 * 4;
     uint32_t fl = 0;
     if constexpr (NOV)  // bit 0: a table; bit 1: the member's previous tile is tile t - 1 of this chunk
-      fl = (members[ch.mb + m] >= ns.n1 ? 1u : 0u) | (t > tpre[m] ? 2u : 0u);
+      fl = (mtab[m] ? 1u : 0u) | (t > tpre[m] ? 2u : 0u);
     tinfo[t] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), min(64u, mhi[m] - q0) | (m << 8), fl);
   }
   __syncthreads();

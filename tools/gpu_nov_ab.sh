@@ -16,8 +16,11 @@ for SET in "" "$@"; do
   rc=$?; [ $rc -eq 0 ] || { echo "run $i rc=$rc"; tail -5 $OUT/ab$i.err; exit $rc; }
   python3 -c "import json,sys; d=json.load(open('$OUT/ab$i.json')); print(d['ms_per_batch'], d['kernels_ms_per_batch'])" | tee -a $OUT/ab.log
 done
-[ -n "$NOPMC" ] && exit 0
 cd /tmp
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/tools/nov_bench.py 2 > $OUT/trace.log 2>&1
+rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+f=$(find $OUT/trace -name "*kernel_stats.csv" | head -1); cut -d, -f1-4 "$f" | head -30
+[ -n "$NOPMC" ] && exit 0
 p=0
 for CTR in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU" \
            "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_BUSY_CYCLES" \
