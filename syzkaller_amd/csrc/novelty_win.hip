@@ -11,19 +11,21 @@
 // rank is its position in that list, so the table is the group's smallest rank.
 //
 //   G  group partition (stable) + members + lengths (a trailing 0xFFFFFFFF dropped) + the PC span
-//   P  k_part3<NOV>: the members' PCs transposed into 2^SB-address windows (one HBM read per PC), every
+//   P  k_part3<NOV>: the members' PCs transposed into 2^DB-address windows (one HBM read per PC), every
 //      list checked strictly increasing on the way
-//   M  k_nw_min: a workgroup per (call, window): direct min-rank table in LDS (and a presence bitmap
-//      the element that first lowers an entry sets), then one pass over the present keys in PC order:
-//      a key is kept if the table holds it or a non-flake cover does (flakes of the window in an LDS
-//      bitmap), a cover that wins a kept key is new (byte stores, deduplicated by an LDS rank bitmap);
-//      the kept keys leave as a bitmap per window (2^SB bits), their count beside it
+//   M  k_nw_min: a workgroup per (call, window): a direct min-rank table in LDS (and a presence bitmap
+//      the element that finds an entry empty sets), the LDS updates of 16 runs issued before one
+//      wait; then the present keys in PC order: a key is kept if the table holds it or a non-flake
+//      cover does (the window's flakes in an LDS bitmap), a cover that wins a kept key is new (byte
+//      stores, deduplicated by an LDS rank bitmap); the kept keys leave as a bitmap per window (2^DB
+//      bits), their count beside it
 //   E  scan of the counts, then every window's bitmap expands to its PCs at its offset (the updated
 //      tables, sorted by (call, PC)), a table's 0xFFFFFFFF last unless the call took a Union
 //
-// Integer work throughout; bit-exact by construction. Windows are direct-mapped only, so the PC span
-// must fit WMAX windows (2^15 x 1024 = 32M addresses); a wider span (or G > 4096) falls back to the
-// keyed table (novelty.hip).
+// Integer work throughout; bit-exact by construction. Windows are direct-mapped, so the PC span must
+// fit WMAX windows (2^15 x 1024 = 32M addresses); a wider span (or G > 4096) falls back to the keyed
+// table (novelty.hip). Measured and dropped (profiles/r02_ab/novelty_ab.md): hashed windows for calls
+// with few PCs per window, persistent workgroups with the next item prefetched, branch-free batches.
 #include <algorithm>
 #include <cstdlib>
 #include <numeric>
@@ -43,18 +45,7 @@ struct NwCfg {
   static constexpr int BLOCK = SB >= 15 ? 1024 : 512;
   static constexpr uint32_t BMW = SB >= 15 ? 5120 : 2048;  // LDS rank bitmap words (winner dedup)
 };
-// Hashed windows (the other calls): 2^S addresses, S in (DB, NH_MAXB], sized so a window holds about
-// NH_TARGET PCs; an NH_SLOTS-slot open-addressing min table (rounds by key residue when it fills) and
-// an LDS kept bitmap of the window, so the kept keys still leave in PC order.
-constexpr uint32_t NH_MAXB = 17;
-constexpr uint32_t NH_SLOTS_BITS = 12;
-constexpr uint32_t NH_SLOTS = 1u << NH_SLOTS_BITS;
-constexpr uint32_t NH_CAP = NH_SLOTS * 3 / 4;  // PCs per round
-constexpr uint32_t NH_TARGET = 2048;           // PCs per window a hashed call aims at
-constexpr uint32_t NH_PROBE = 64;
-constexpr uint32_t NH_FLCAP = 1024;            // flakes of a window staged in LDS
-constexpr int NH_BLOCK = 512;
-constexpr int NE_BLOCK = 256;                  // k_nw_emit
+constexpr int NE_BLOCK = 256;  // k_nw_emit
 
 // per call: window layout of the kept bitmaps (u32 words) and of the count slots
 struct NwGroup {
@@ -292,142 +283,6 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
   }
 }
 
-// PCs of one (call, window) over all its chunks' runs (metadata only)
-template <int BLOCK>
-__device__ uint32_t nw_window_elems(const PItem it, const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
-                                    const uint16_t* __restrict__ desc, uint32_t* red) {
-  const uint32_t g = it.g, w = it.w, W = pg[g].W;
-  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
-  const uint16_t* d0 = desc + gdesc[g] + w;
-  uint32_t s = 0;
-  for (uint64_t c = c0 + threadIdx.x; c < c1; c += BLOCK) {
-    const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
-    s += (uint32_t)d[1] - d[0];
-  }
-  return block_sum<BLOCK>(s, red);
-}
-
-__device__ __forceinline__ uint32_t nh_slot(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - NH_SLOTS_BITS); }
-
-// M, hashed: one (call, window) of 2^S addresses (S = pg[g].S, at most NH_MAXB)
-__global__ __launch_bounds__(NH_BLOCK) void k_nw_hmin(
-    const PItem* items, const PChunk* __restrict__ chunks, const uint64_t* gchunk, const uint64_t* gdesc,
-    const PGroup* pg, const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems, const uint64_t* cstart,
-    uint32_t lo, uint32_t db, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart, uint32_t wdb,
-    const NwGroup* ng_, uint32_t* kbits, uint32_t* wcount, uint8_t* sel8, uint8_t* upd) {
-  constexpr int BLOCK = NH_BLOCK;
-  constexpr uint32_t KW = (1u << NH_MAXB) / 32;
-  constexpr uint32_t BMW = 2048;
-  __shared__ uint32_t keys[NH_SLOTS];
-  __shared__ uint32_t vals[NH_SLOTS];
-  __shared__ uint32_t kept[KW];
-  __shared__ uint32_t bm[BMW];
-  __shared__ uint32_t flist[NH_FLCAP];
-  __shared__ uint32_t red[BLOCK / 64 + 1];
-  __shared__ int full;
-  const PItem it = items[blockIdx.x];
-  const uint32_t g = it.g, w = it.w, S = pg[g].S;
-  const uint32_t nkw = (1u << S) / 32;
-  const uint32_t wlo = lo + (w << S);
-  const uint64_t gb = cstart[g], ng = cstart[g + 1] - gb;
-  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BMW * 32, ng);
-  const uint32_t words = (span + 31) / 32;
-  // the window's flakes: those of its direct-size sub-windows
-  const uint32_t f0 = fstart[min(w << (S - db), wdb)], f1 = fstart[min((w + 1) << (S - db), wdb)];
-  const bool fl_lds = f1 - f0 <= NH_FLCAP;
-  for (uint32_t i = threadIdx.x; i < nkw; i += BLOCK) kept[i] = 0;
-  for (uint32_t i = threadIdx.x; i < words; i += BLOCK) bm[i] = 0;
-  if (fl_lds)
-    for (uint32_t i = f0 + threadIdx.x; i < f1; i += BLOCK) flist[i - f0] = fl[i];
-  const uint32_t E = nw_window_elems<BLOCK>(it, gchunk, gdesc, pg, desc, red);  // (synchronizes)
-  int anynew = 0;
-  uint32_t R = E ? (E + NH_CAP - 1) / NH_CAP : 0;
-  for (uint32_t round = 0; round < R;) {
-    for (uint32_t i = threadIdx.x; i < NH_SLOTS; i += BLOCK) {
-      keys[i] = 0xFFFFFFFFu;
-      vals[i] = RANK_NONE;
-    }
-    if (threadIdx.x == 0) full = 0;
-    __syncthreads();
-    const uint32_t RR = R, rr = round;
-    for_window_elems<4, true>(it, chunks, gchunk, gdesc, pg, desc, elems, nullptr, 0u, BLOCK / 64,
-                              [&](uint32_t o, uint32_t Rk) {
-                                if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
-                                uint32_t h = nh_slot(o);
-                                for (uint32_t probes = 0; probes < NH_PROBE; probes++) {
-                                  uint32_t k = keys[h];
-                                  if (k == 0xFFFFFFFFu) {
-                                    k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
-                                    if (k == 0xFFFFFFFFu) k = o;
-                                  }
-                                  if (k == o) {
-                                    if (vals[h] > Rk) atomicMin(&vals[h], Rk);
-                                    return;
-                                  }
-                                  h = (h + 1) & (NH_SLOTS - 1);
-                                }
-                                full = 1;
-                              });
-    __syncthreads();
-    if (full) {  // redo every round with twice as many (marks already made are exact and idempotent)
-      R *= 2;
-      round = 0;
-      __syncthreads();
-      continue;
-    }
-    // this round's keys: kept bit unless a flake no table holds; the first cover of a kept key is new
-    for (uint32_t i = threadIdx.x; i < NH_SLOTS; i += BLOCK) {
-      const uint32_t o = keys[i];
-      if (o == 0xFFFFFFFFu) continue;
-      const uint32_t r = vals[i];
-      const bool old = r == (uint32_t)gb;
-      if (!old) {
-        const uint32_t pc = wlo + o;
-        bool flake;
-        if (fl_lds) {
-          const uint32_t j = (uint32_t)lower_bound_dev<uint32_t>(flist, 0, f1 - f0, pc);
-          flake = j < f1 - f0 && flist[j] == pc;
-        } else {
-          const uint64_t j = lower_bound_dev<uint32_t>(fl, f0, f1, pc);
-          flake = j < f1 && fl[j] == pc;
-        }
-        if (flake) continue;
-        anynew = 1;
-        const uint64_t lr = (uint64_t)r - gb;
-        if (lr < span) {
-          const uint32_t bit = 1u << (lr & 31);
-          if (!(bm[lr >> 5] & bit)) atomicOr(&bm[lr >> 5], bit);
-        } else {
-          sel8[r] = 1;
-        }
-      }
-      atomicOr(&kept[o >> 5], 1u << (o & 31));
-    }
-    round++;
-    __syncthreads();
-  }
-  __syncthreads();
-  const NwGroup gl = ng_[g];
-  uint32_t* kb32 = kbits + gl.kbase + (uint64_t)w * nkw;
-  uint32_t cnt = 0;
-  for (uint32_t i = threadIdx.x; i < nkw; i += BLOCK) {
-    const uint32_t v = kept[i];
-    kb32[i] = v;
-    cnt += (uint32_t)__popc(v);
-  }
-  const uint32_t tot = block_sum<BLOCK>(cnt, red);
-  if (threadIdx.x == 0) wcount[gl.sbase + w] = tot;
-  if (__syncthreads_or(anynew) && threadIdx.x == 0) upd[g] = 1;
-  for (uint32_t i = threadIdx.x; i < words; i += BLOCK) {
-    uint32_t v = bm[i];
-    while (v) {
-      const uint32_t b = __ffs(v) - 1;
-      sel8[gb + 32ull * i + b] = 1;
-      v &= v - 1;
-    }
-  }
-}
-
 // fstart[w] = the first flake at or above direct-size window w's first address (w in [0, W]; nfl past
 // the span)
 __global__ void k_nw_fstart(const uint32_t* fl, uint64_t nfl, uint32_t lo, uint32_t W, uint32_t sb, uint32_t* fstart) {
@@ -512,13 +367,6 @@ static uint32_t nw_bits_forced() {
   return v == 14 || v == 15 ? v : 0u;
 }
 
-// SYZGPU_NW_HASH=1: hashed windows for the calls with few PCs (A/B; measured 2.65 vs 2.47 ms for all
-// direct at config 3)
-static bool nw_hash() {
-  static const bool v = getenv("SYZGPU_NW_HASH") && atoi(getenv("SYZGPU_NW_HASH")) != 0;
-  return v;
-}
-
 __global__ void k_nw_gpcs(const uint64_t* mpos, const uint64_t* cstart, uint32_t G, uint64_t* gpcs) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x)
     gpcs[g] = mpos[cstart[g + 1]] - mpos[cstart[g]];
@@ -577,28 +425,21 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   const uint64_t total = hbuf[G + 1];
   uint32_t lo = reinterpret_cast<uint32_t*>(hbuf + G + 2)[0], hi = reinterpret_cast<uint32_t*>(hbuf + G + 2)[1];
   if (lo > hi) lo = hi = 0;  // no PCs outside the sentinel
-  // windows on 2^NH_MAXB boundaries (a window's addresses never wrap, and every size nests)
-  lo &= ~((1u << NH_MAXB) - 1);
+  lo &= ~((1u << 15) - 1);  // windows on 2^15 boundaries: a window's addresses never wrap
   auto nwin = [&](uint32_t sb) { return (((uint64_t)hi - lo) >> sb) + 1; };
   uint32_t DB = nw_bits_forced();
   if (!DB) DB = nwin(14) <= WMAX ? 14 : 15;
   if (nwin(DB) > WMAX) return false;
   const uint32_t WD = (uint32_t)nwin(DB);
-  // ---- plan: per call direct (DB) or hashed windows (S in (DB, NH_MAXB]); blocks; work items ----
+  // ---- plan: every call on WD direct windows of 2^DB addresses; blocks; work items ----
   std::vector<PGroup> hpg(G);
   std::vector<NwGroup> hng(G + 1);
   uint64_t kw = 0, slots = 0;
   for (uint32_t g = 0; g < G; g++) {
-    uint32_t S = DB;
-    if (nw_hash() && hpcs[g] < (uint64_t)NH_TARGET * WD) {  // fewer than NH_TARGET PCs per direct window
-      S = DB + 1;
-      while (S < NH_MAXB && hpcs[g] <= (uint64_t)NH_TARGET * nwin(S + 1)) S++;
-    }
-    const uint32_t W = (uint32_t)nwin(S);
-    hpg[g] = PGroup{S, W, S == DB ? (uint32_t)PMODE_DIRECT : (uint32_t)PMODE_HASH, 0};
+    hpg[g] = PGroup{DB, WD, (uint32_t)PMODE_DIRECT, 0};
     hng[g] = NwGroup{kw, slots};
-    kw += (uint64_t)W << (S - 5);
-    slots += W + 1;
+    kw += (uint64_t)WD << (DB - 5);
+    slots += WD + 1;
   }
   hng[G] = NwGroup{kw, slots};
   std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
@@ -611,19 +452,15 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   }
   const uint32_t B = hgblock[G];
   const uint64_t chunk_bound = B + total / PCAP + G + 1;
-  // items: direct and hashed, each larger calls first (their windows are the long ones)
+  // items: larger calls first (their windows are the long ones), so the grid's tail is short
   std::vector<uint32_t> order(G);
   std::iota(order.begin(), order.end(), 0u);
   std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hpcs[x] > hpcs[y]; });
   std::vector<PItem> hitems;
-  size_t ndirect = 0;
-  for (int mode = 0; mode < 2; mode++) {
-    for (uint32_t g : order)
-      if (hpg[g].mode == (uint32_t)mode)
-        for (uint32_t w = 0; w < hpg[g].W; w++) hitems.push_back(PItem{g, w});
-    if (mode == 0) ndirect = hitems.size();
-  }
-  const size_t nitems = hitems.size(), nhash = nitems - ndirect;
+  hitems.reserve((size_t)G * WD);
+  for (uint32_t g : order)
+    for (uint32_t w = 0; w < WD; w++) hitems.push_back(PItem{g, w});
+  const size_t nitems = hitems.size();
   const size_t stage_bytes = (G + 1) * sizeof(PGroup) + (G + 1) * sizeof(NwGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 +
                              nitems * sizeof(PItem);
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
@@ -691,20 +528,15 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     ProfScope ps("novelty_min", s, total * 4 + kw * 4);
     k_nw_fstart<<<grid_for(WD + 1, 256, 64), 256, 0, s>>>(d_fl, nfl, lo, WD, DB, fstart);
     SYZ_LAUNCHED();
-    if (ndirect) {
+    if (nitems) {
       if (DB == 14)
-        k_nw_min<14><<<(unsigned)ndirect, NwCfg<14>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems,
-                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
-                                                                    upd, nw_dbg(), nw_walk_kind());
+        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems,
+                                                                   cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
+                                                                   upd, nw_dbg(), nw_walk_kind());
       else
-        k_nw_min<15><<<(unsigned)ndirect, NwCfg<15>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems,
-                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
-                                                                    upd, nw_dbg(), nw_walk_kind());
-      SYZ_LAUNCHED();
-    }
-    if (nhash) {
-      k_nw_hmin<<<(unsigned)nhash, NH_BLOCK, 0, s>>>(ditems + ndirect, chunks, gchunk, gdesc, dpg, desc, elems, cstart,
-                                                     lo, DB, d_fl, fstart, WD, dng, kbits, wcount, sel8, upd);
+        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems,
+                                                                   cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
+                                                                   upd, nw_dbg(), nw_walk_kind());
       SYZ_LAUNCHED();
     }
   }
