@@ -194,7 +194,7 @@ static int nw_walk_kind() {
 // is OLD.
 template <uint32_t SB>
 __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
-    const PItem* items, const PChunk* __restrict__ chunks, const uint64_t* gchunk, const uint64_t* gdesc,
+    const uint32_t* order, uint32_t W, const PChunk* __restrict__ chunks, const uint64_t* gchunk, const uint64_t* gdesc,
     const PGroup* pg, const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems, const uint64_t* cstart,
     uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart, const NwGroup* ng_,
     uint32_t* kbits, uint32_t* wcount, uint8_t* sel8, uint8_t* upd, int dbg, int walk) {
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
   __shared__ uint32_t flk[K::FLK];
   __shared__ uint32_t pres[K::FLK];  // offsets some member holds (set by the element that lowers NONE)
   __shared__ uint32_t red[BLOCK / 64 + 1];
-  const PItem it = items[blockIdx.x];
+  const PItem it{order[blockIdx.x / W], blockIdx.x % W};
   const uint32_t g = it.g, w = it.w;
   {
     uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -367,6 +367,12 @@ static uint32_t nw_bits_forced() {
   return v == 14 || v == 15 ? v : 0u;
 }
 
+// block b -> its call: the last g with gblock[g] <= b
+__global__ void k_nw_bgroup(const uint32_t* gblock, uint32_t G, uint32_t B, uint32_t* bgroup) {
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
+    bgroup[b] = (uint32_t)upper_bound_dev<uint32_t>(gblock, 0, G + 1, b) - 1;
+}
+
 __global__ void k_nw_gpcs(const uint64_t* mpos, const uint64_t* cstart, uint32_t G, uint64_t* gpcs) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x)
     gpcs[g] = mpos[cstart[g + 1]] - mpos[cstart[g]];
@@ -442,53 +448,39 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     slots += WD + 1;
   }
   hng[G] = NwGroup{kw, slots};
-  std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
+  std::vector<uint32_t> hgblock(G + 1, 0);
   uint64_t desc_bound = 0;
   for (uint32_t g = 0; g < G; g++) {
     const uint32_t nb = (uint32_t)((hstart[g + 1] - hstart[g] + MEMB - 1) / MEMB);
     hgblock[g + 1] = hgblock[g] + nb;
-    hbgroup.insert(hbgroup.end(), nb, g);
     desc_bound += (nb + hpcs[g] / PCAP + 1) * (uint64_t)(hpg[g].W + 1);  // chunks of g <= nb + PCs / PCAP + 1
   }
   const uint32_t B = hgblock[G];
   const uint64_t chunk_bound = B + total / PCAP + G + 1;
-  // items: larger calls first (their windows are the long ones), so the grid's tail is short
+  // items (call, window), larger calls first (their windows are the long ones) so the grid's tail is
+  // short: item i is window i % WD of call order[i / WD], generated on the device
   std::vector<uint32_t> order(G);
   std::iota(order.begin(), order.end(), 0u);
   std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hpcs[x] > hpcs[y]; });
-  std::vector<PItem> hitems;
-  hitems.reserve((size_t)G * WD);
-  for (uint32_t g : order)
-    for (uint32_t w = 0; w < WD; w++) hitems.push_back(PItem{g, w});
-  const size_t nitems = hitems.size();
-  const size_t stage_bytes = (G + 1) * sizeof(PGroup) + (G + 1) * sizeof(NwGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 +
-                             nitems * sizeof(PItem);
+  const size_t nitems = (size_t)G * WD;
+  // one staging copy: PGroup[G+1], NwGroup[G+1], gblock[G+1], order[G+1]
+  const size_t o_ng = (G + 1) * sizeof(PGroup), o_gb = o_ng + (G + 1) * sizeof(NwGroup), o_or = o_gb + (G + 1) * 4;
+  const size_t stage_bytes = o_or + (G + 1) * 4;
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
-  PGroup* dpg = sc.get<PGroup>("nw_pg", G + 1);
-  NwGroup* dng = sc.get<NwGroup>("nw_ng", G + 1);
-  uint32_t* dgblock = sc.get<uint32_t>("nw_gblock", G + 1);
+  uint8_t* dstage = sc.get<uint8_t>("nw_stage", stage_bytes + 64);
+  std::memcpy(stage, hpg.data(), G * sizeof(PGroup));
+  std::memcpy(stage + o_ng, hng.data(), (G + 1) * sizeof(NwGroup));
+  std::memcpy(stage + o_gb, hgblock.data(), (G + 1) * 4);
+  std::memcpy(stage + o_or, order.data(), G * 4);
+  SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
+  const PGroup* dpg = reinterpret_cast<const PGroup*>(dstage);
+  const NwGroup* dng = reinterpret_cast<const NwGroup*>(dstage + o_ng);
+  const uint32_t* dgblock = reinterpret_cast<const uint32_t*>(dstage + o_gb);
+  const uint32_t* dorder = reinterpret_cast<const uint32_t*>(dstage + o_or);
   uint32_t* dbgroup = sc.get<uint32_t>("nw_bgroup", (size_t)B + 1);
-  PItem* ditems = sc.get<PItem>("nw_items", nitems + 1);
-  {
-    uint8_t* p = stage;
-    std::memcpy(p, hpg.data(), G * sizeof(PGroup));
-    SYZ_HIP(hipMemcpyAsync(dpg, p, G * sizeof(PGroup), hipMemcpyHostToDevice, s));
-    p += (G + 1) * sizeof(PGroup);
-    std::memcpy(p, hng.data(), (G + 1) * sizeof(NwGroup));
-    SYZ_HIP(hipMemcpyAsync(dng, p, (G + 1) * sizeof(NwGroup), hipMemcpyHostToDevice, s));
-    p += (G + 1) * sizeof(NwGroup);
-    std::memcpy(p, hgblock.data(), (G + 1) * 4);
-    SYZ_HIP(hipMemcpyAsync(dgblock, p, (G + 1) * 4, hipMemcpyHostToDevice, s));
-    p += (G + 1) * 4;
-    if (B) {
-      std::memcpy(p, hbgroup.data(), (size_t)B * 4);
-      SYZ_HIP(hipMemcpyAsync(dbgroup, p, (size_t)B * 4, hipMemcpyHostToDevice, s));
-    }
-    p += ((size_t)B + 1) * 4;
-    if (nitems) {
-      std::memcpy(p, hitems.data(), nitems * sizeof(PItem));
-      SYZ_HIP(hipMemcpyAsync(ditems, p, nitems * sizeof(PItem), hipMemcpyHostToDevice, s));
-    }
+  if (B) {
+    k_nw_bgroup<<<grid_for(B, 256, 4096), 256, 0, s>>>(dgblock, G, B, dbgroup);
+    SYZ_LAUNCHED();
   }
   uint32_t* nsub = sc.get<uint32_t>("nw_nsub", (size_t)B + 1);
   uint64_t* cstartb = sc.get<uint64_t>("nw_cstartb", (size_t)B + 1);
@@ -530,11 +522,11 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     SYZ_LAUNCHED();
     if (nitems) {
       if (DB == 14)
-        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems,
+        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, chunks, gchunk, gdesc, dpg, desc, elems,
                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
                                                                    upd, nw_dbg(), nw_walk_kind());
       else
-        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(ditems, chunks, gchunk, gdesc, dpg, desc, elems,
+        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, chunks, gchunk, gdesc, dpg, desc, elems,
                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
                                                                    upd, nw_dbg(), nw_walk_kind());
       SYZ_LAUNCHED();
