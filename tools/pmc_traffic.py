@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Parse the FETCH_SIZE / WRITE_SIZE passes of tools/gpu_pmc.sh into profiles/pmc_traffic.json.
 
-FETCH_SIZE and WRITE_SIZE are KiB per dispatch. The two vec_min launches of a step (big call groups on
-the main stream, small ones on the side stream) are told apart by their template argument. On gfx950 FETCH_SIZE reports half the bytes of a wide
+FETCH_SIZE and WRITE_SIZE are KiB per dispatch; a kernel's dispatches (e.g. the two pmin classes of a
+step) are averaged. On gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced streaming read (MI355X_MICROARCH.md §HBM), so it is doubled; WRITE_SIZE is exact for 16-B
 stores and taken as is. Per kernel: the mean over its dispatches of the bench command (3 timed + 1
 warmup steps), as HBM bytes per launch.
@@ -13,9 +13,10 @@ import json
 import os
 import sys
 
-SHORT = {"k_vec_min": "vec_min", "k_select_store": "select_out", "k_gr_count": "gosort_round",
+SHORT = {"k_part3": "part", "k_pmin_direct": "pmin", "k_pmin_hash": "pmin_hash", "k_grp_scatter": "group_partition",
+         "k_sel_flags": "select_out", "k_vec_min": "vec_min", "k_gr_count": "gosort_round",
          "k_gr_lists": "gosort_round", "k_gr_swap": "gosort_round", "k_ls_sort": "gosort_lds",
-         "k_prio_row": "prio_choice", "k_ranks": "ranks", "k_el_init": "el_init"}
+         "k_prio_row": "prio_choice", "k_st_gram": "static_prio", "k_ranks": "ranks"}
 
 
 def short(name, grid):
