@@ -924,8 +924,7 @@ void novelty_dev(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_t* d
   const uint64_t ni = L + M;
   int* err = sc.get<int>("nv_err", 2);
   SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
-  if (n) SYZ_HIP(hipMemsetAsync(d_new, 0, n, s));
-  if (strategy() == 0 || strategy() == 4) {
+  if (strategy() == 0 || strategy() == 4) {  // (writes every is_new flag itself)
     if (nflakes > 1) {
       k_nov_check_flakes<<<grid_for(nflakes, 256, 1024), 256, 0, s>>>(d_fl, nflakes, err);
       SYZ_LAUNCHED();
@@ -935,6 +934,7 @@ void novelty_dev(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_t* d
       return;
     }
   }
+  if (n) SYZ_HIP(hipMemsetAsync(d_new, 0, n, s));
   if (strategy() != 1 && novelty_table(d_pcs, d_off, d_grp, n, L, G, d_mc, d_mco, M, d_fl, nflakes, d_new, d_out, out_cap,
                                        d_ooff, err, table_budget(), s)) {
     check_errors(err, s);

@@ -53,21 +53,37 @@ struct NwGroup {
   uint64_t sbase;  // first count slot (W + 1 slots: the windows, then the table's 0xFFFFFFFF)
 };
 
-// combined members: call g's list is [table g (entry id n + g), its covers in batch order]; inv[e] = the
-// position of entry e (covers and tables) in that order
+// the per-call state of one batch: error word, sentinel and Union flags, kept ranks, the span
+__global__ void k_nw_init(int* perr, uint8_t* has_sent, uint8_t* upd, uint32_t G, uint8_t* sel8, size_t nsel,
+                          uint32_t* span) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsel; i += (size_t)gridDim.x * blockDim.x) {
+    sel8[i] = 0;
+    if (i <= G) {
+      has_sent[i] = 0;
+      upd[i] = 0;
+    }
+    if (i < 2) {
+      perr[i] = 0;
+      span[i] = i ? 0u : 0xFFFFFFFFu;
+    }
+  }
+}
+
+// combined members: call g's list is [table g (entry id n + g), its covers in batch order], with the
+// members' lengths gathered from the entry-order lengths (elen: covers, then tables)
 __global__ void k_nw_members(const uint32_t* members, const uint64_t* gstart, const uint32_t* group, size_t n,
-                             uint32_t G, uint32_t* cmem, uint64_t* cstart, uint32_t* inv) {
+                             uint32_t G, const uint32_t* elen, uint32_t* cmem, uint64_t* cstart, uint32_t* mlen) {
   const size_t tot = n > (size_t)G + 1 ? n : (size_t)G + 1;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
     if (i < n) {
       const uint32_t e = members[i];
       const uint32_t g = group[e] < G ? group[e] : 0u;  // an invalid id was counted in group 0
       cmem[i + g + 1] = e;
-      inv[e] = (uint32_t)(i + g + 1);
+      mlen[i + g + 1] = elen[e];
     }
     if (i < G) {
       cmem[gstart[i] + i] = (uint32_t)n + (uint32_t)i;
-      inv[n + i] = (uint32_t)(gstart[i] + i);
+      mlen[gstart[i] + i] = elen[n + i];
     }
     if (i <= G) cstart[i] = gstart[i] + i;
   }
@@ -75,10 +91,10 @@ __global__ void k_nw_members(const uint32_t* members, const uint64_t* gstart, co
 
 // member lengths without a trailing 0xFFFFFFFF (foreach never matches it, cover.go:81-102; a table's
 // is put back after the windows), which tables had one, and the span of the other PCs; in entry order
-// (coalesced offsets, the first and last PC of neighbouring entries on neighbouring lines)
+// (coalesced offsets and lengths, the first and last PC of neighbouring entries on neighbouring lines)
 __global__ __launch_bounds__(256) void k_nw_meta(const uint32_t* pcs, const uint64_t* off, const uint32_t* mc,
-                                                 const uint64_t* mc_off, const uint32_t* inv, size_t n, uint32_t G,
-                                                 uint32_t* mlen, uint8_t* has_sent, uint32_t* span) {
+                                                 const uint64_t* mc_off, size_t n, uint32_t G, uint32_t* elen,
+                                                 uint8_t* has_sent, uint32_t* span) {
   uint32_t lo = 0xFFFFFFFFu, hi = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + G; i += (size_t)gridDim.x * blockDim.x) {
     const bool tab = i >= n;
@@ -94,7 +110,7 @@ __global__ __launch_bounds__(256) void k_nw_meta(const uint32_t* pcs, const uint
         if (len) last = src[len - 1];
       }
     }
-    mlen[inv[i]] = (uint32_t)len;
+    elen[i] = (uint32_t)len;
     if (len) {
       lo = min(lo, first);
       hi = max(hi, last);
@@ -393,26 +409,22 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
   uint32_t* cmem = sc.get<uint32_t>("nw_cmem", nm + 1);
   uint32_t* mlen = sc.get<uint32_t>("nw_mlen", nm + 1);
-  uint32_t* inv = sc.get<uint32_t>("nw_inv", nm + 1);
+  uint32_t* elen = sc.get<uint32_t>("nw_elen", nm + 1);
   uint64_t* mpos = sc.get<uint64_t>("nw_mpos", nm + 1);
   uint8_t* has_sent = sc.get<uint8_t>("nw_has_sent", G + 1);
   uint8_t* upd = sc.get<uint8_t>("nw_upd", G + 1);
   uint32_t* span = sc.get<uint32_t>("nw_span", 4);
   int* perr = sc.get<int>("nw_perr", 2);
-  SYZ_HIP(hipMemsetAsync(perr, 0, 8, s));
-  SYZ_HIP(hipMemsetAsync(has_sent, 0, G + 1, s));
-  SYZ_HIP(hipMemsetAsync(upd, 0, G + 1, s));
-  uint32_t* hinit = c.pinned.get<uint32_t>(16);
-  hinit[0] = 0xFFFFFFFFu;
-  hinit[1] = 0;
-  SYZ_HIP(hipMemcpyAsync(span, hinit, 8, hipMemcpyHostToDevice, s));
+  uint8_t* sel8 = sc.get<uint8_t>("nw_sel8", nm + 1);
+  k_nw_init<<<grid_for(nm + 1, 256, 1024), 256, 0, s>>>(perr, has_sent, upd, G, sel8, nm + 1, span);
+  SYZ_LAUNCHED();
   {
     ProfScope ps("novelty_group", s, (uint64_t)n * 28 + (uint64_t)nm * 24);
     group_partition_dev(d_grp, d_off, n, G, gstart, members, el, perr, s);
-    k_nw_members<<<grid_for(std::max<size_t>(n, G + 1), 256, 8192), 256, 0, s>>>(members, gstart, d_grp, n, G, cmem,
-                                                                                 cstart, inv);
+    k_nw_meta<<<grid_for(nm, 256, 4096), 256, 0, s>>>(d_pcs, d_off, d_mc, d_mco, n, G, elen, has_sent, span);
     SYZ_LAUNCHED();
-    k_nw_meta<<<grid_for(nm, 256, 4096), 256, 0, s>>>(d_pcs, d_off, d_mc, d_mco, inv, n, G, mlen, has_sent, span);
+    k_nw_members<<<grid_for(std::max<size_t>(n, G + 1), 256, 8192), 256, 0, s>>>(members, gstart, d_grp, n, G, elen,
+                                                                                 cmem, cstart, mlen);
     SYZ_LAUNCHED();
     exclusive_scan_u32(mlen, mpos, nm, s);
   }
@@ -492,8 +504,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   uint32_t* kbits = sc.get<uint32_t>("nw_kbits", kw + 1);
   uint32_t* wcount = sc.get<uint32_t>("nw_wcount", slots + 1);
   uint64_t* wpos = sc.get<uint64_t>("nw_wpos", slots + 1);
-  uint8_t* sel8 = sc.get<uint8_t>("nw_sel8", nm + 1);
-  SYZ_HIP(hipMemsetAsync(sel8, 0, nm + 1, s));
+
   {
     ProfScope ps("novelty_part", s, total * 8 + (uint64_t)nm * 24);
     if (B) {
