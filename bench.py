@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--append", type=int, default=10_000,
                     help="also time a NewInput append of this many programs to the store at N=1 (0: off)")
     ap.add_argument("--novelty-cpu-sample", type=int, default=20_000)
+    ap.add_argument("--cooccurrence", type=int, default=1,
+                    help="also time the call-ID co-occurrence X^T X on int8 MFMA (SURVEY.md F1/K9) at N=1")
     ap.add_argument("--split-largest", type=int, default=0,
                     help="rehearsal: force the largest call group into this many PC-key parts")
     ap.add_argument("--emulate", default="", help="W:r — rehearsal: run rank r's shard of a W-rank job on this "
@@ -290,6 +292,7 @@ def main():
             store_leg_res, store = store_leg(args, L, corp, d_pcs, d_off, d_grp, d_len, d_sel, d_hist, C, G, sptr)
         tail = text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step) if args.text and solo else None
         nov = novelty_leg(args, dev, L, read_prof) if args.novelty and solo else None
+        cooc = cooccurrence_leg(args, dev, L, read_prof, corp, C) if args.cooccurrence and solo else None
         hubr = hub_leg(args, dev, L, read_prof, corp, sptr) if args.hub and solo else None
         ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr) if args.analytics and solo else None
         app = append_leg(args, dev, store, sptr, C, d_hist) if args.append and solo else None  # last: replaces
@@ -322,6 +325,7 @@ def main():
             "store_reuse": store_leg_res,
             "minimize_corpus_tail": tail,
             "novelty_config3": nov,
+            "call_cooccurrence": cooc,
             "cover_analytics": ana,
             "hub_ingest_config5": hubr,
             "manager_cycle": app,
@@ -633,6 +637,58 @@ def hub_leg(args, dev, L, read_prof, corp, sptr):
 def _lib_check(rc):
     from syzkaller_amd import _lib
     _lib.check(rc)
+
+
+I8_PEAK_TOPS = 5000.0  # MI355X dense int8 MFMA: 2x the ~2.5 PF dense BF16 rate (MI355X_MICROARCH.md, MFMA table)
+
+
+def cooccurrence_leg(args, dev, L, read_prof, corp, C):
+    """The call-ID co-occurrence X^T X (syzgpu_call_cooccurrence_dev, int8 MFMA; SURVEY.md F1/K9 — not the
+    reference's position-indexed calcDynamicPrio) over the bench corpus's programs: len(p.Calls) from the
+    corpus, call ids Zipf(1.2) over C, seeded. Roofline: the int8 ops of the upper-triangle tiles the GEMM
+    runs (2 * 128^2 * Kp per tile) over its launch time against the dense int8 MFMA peak."""
+    import torch
+    rnd = np.random.default_rng(args.seed + 0x77)
+    lens = corp.prog_len.astype(np.uint64)
+    off = np.zeros(corp.n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    w = 1.0 / np.arange(1, C + 1) ** 1.2
+    calls = rnd.choice(C, size=int(off[-1]), p=w / w.sum()).astype(np.uint16)
+    dc = torch.from_numpy(calls.view(np.int16)).to(dev)
+    do = torch.from_numpy(off.view(np.int64)).to(dev)
+    out = torch.empty((C, C), dtype=torch.int32, device=dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        _lib_check(L.syzgpu_call_cooccurrence_dev(dc.data_ptr(), do.data_ptr(), corp.n, C, out.data_ptr(), sptr))
+    step()
+    torch.cuda.synchronize()
+    steps = max(1, args.steps // 2)
+    L.syzgpu_profile_only(None)
+    L.syzgpu_profile_enable(1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ev = read_prof()
+    L.syzgpu_profile_enable(0)
+    T = (C + 127) // 128
+    Kp = (corp.n + 31) // 32 * 32
+    res = {"what": "call-ID co-occurrence X^T X - diag (int32 C x C) of %d programs (%d calls, ids Zipf(1.2) over "
+                   "C=%d); not the reference's position-indexed calcDynamicPrio (SURVEY.md F1)" % (corp.n, int(off[-1]), C),
+           "ms": round(el / steps * 1e3, 3),
+           "kernels_ms": {k: round(e["ms"] / steps, 4) for k, e in ev.items()},
+           "pairs": int(out.sum().item())}
+    g = ev.get("cooc_gemm")
+    if g:
+        ms = g["ms"] / g["launches"]
+        ops = 2.0 * (T * (T + 1) // 2) * 128 * 128 * Kp  # the upper-triangle tiles the kernel runs
+        res["roofline"] = {"bound": "mfma", "kernel": "cooc_gemm (v_mfma_i32_32x32x32_i8)",
+                           "achieved": round(ops / (ms * 1e-3) / 1e12, 1), "peak": I8_PEAK_TOPS, "unit": "TOP/s",
+                           "frac": round(ops / (ms * 1e-3) / 1e12 / I8_PEAK_TOPS, 4), "avg_launch_ms": round(ms, 4),
+                           "ops_per_launch": int(ops)}
+    return res
 
 
 def novelty_leg(args, dev, L, read_prof):

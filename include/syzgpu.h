@@ -137,6 +137,16 @@ int syzgpu_prog_scan_dev(const uint8_t* data, const uint64_t* off, size_t n, con
  * corpus program i (the only property the reference reads). out: C*C float32. */
 int syzgpu_dynamic_prio(const uint16_t* prog_len, size_t nprogs, int32_t C, float* out);
 
+/* The call-ID co-occurrence XᵀX (int8 MFMA, int32 accumulation): the north_star's dense-contraction
+ * reading of prio.go:142-151 with call IDs in place of positions. NOT what the
+ * reference computes (it indexes by position: syzgpu_dynamic_prio); an analytics entry of its own.
+ * calls/off: the CSR of every program's call ids (< C); out (C*C int32): out[a][b] = the number of
+ * ordered pairs of distinct positions of one program with calls (a, b), summed over programs.
+ * SYZGPU_EINVAL if a call id >= C or a call occurs more than 127 times in one program. */
+int syzgpu_call_cooccurrence(const uint16_t* calls, const uint64_t* off, size_t nprogs, int32_t C, int32_t* out);
+int syzgpu_call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t nprogs, int32_t C,
+                                 int32_t* out, void* stream);
+
 /* prog/prio.go:40-135 calcStaticPriorities. uses[k*C + c] = the weight call c uses usage key k with
  * (the `uses` map of prio.go:41-104 as a dense nkeys x C float32 matrix, 0 = unused; at most 8
  * distinct non-zero finite weights, SYZGPU_EINVAL otherwise; syzkaller_amd/sysdesc.py builds it from

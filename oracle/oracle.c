@@ -397,6 +397,25 @@ int oracle_dynamic_prio(const uint16_t* prog_len, size_t nprogs, int32_t C, floa
   return 0;
 }
 
+/* The call-ID form of prio.go:142-151 (not the reference's quantity): for every
+ * program, += 1 at [calls[i0]][calls[i1]] for every ordered pair of distinct positions i0 != i1. The
+ * literal loop, exact int32 counts; the checker of syzgpu_call_cooccurrence. */
+int oracle_call_cooccurrence(const uint16_t* calls, const uint64_t* off, size_t nprogs, int32_t C, int32_t* out) {
+  if (C <= 0) return 1;
+  memset(out, 0, sizeof(int32_t) * (size_t)C * (size_t)C);
+  for (size_t p = 0; p < nprogs; p++) {
+    const uint64_t b = off[p], e = off[p + 1];
+    for (uint64_t i0 = b; i0 < e; i0++) {
+      if ((int32_t)calls[i0] >= C) return 1;
+      for (uint64_t i1 = b; i1 < e; i1++) {
+        if (i0 == i1) continue;
+        out[(size_t)calls[i0] * C + calls[i1]] += 1;
+      }
+    }
+  }
+  return 0;
+}
+
 int oracle_calculate_priorities(const float* static_prios, const uint16_t* prog_len, size_t nprogs,
                                 int32_t C, float* out) {
   int rc = oracle_dynamic_prio(prog_len, nprogs, C, out); /* prio.go:31 */

@@ -47,6 +47,7 @@ int oracle_minimize_order(const uint64_t* lens, size_t n, int64_t* perm);
 /* prog/prio.go:137-154 calcDynamicPrio + :158-192 normalizePrio. prog_len[i] = len(p.Calls).
  * out is C*C row-major float32. */
 int oracle_dynamic_prio(const uint16_t* prog_len, size_t nprogs, int32_t C, float* out);
+int oracle_call_cooccurrence(const uint16_t* calls, const uint64_t* off, size_t nprogs, int32_t C, int32_t* out);
 
 /* prog/prio.go:158-192 normalizePrio on a C*C matrix in place. */
 void oracle_normalize_prio(float* prios, int32_t C);

@@ -39,6 +39,8 @@ def lib():
                                               _u64p]
         L.oracle_minimize_order.argtypes = [_u64p, ctypes.c_size_t, _i64p]
         L.oracle_dynamic_prio.argtypes = [_u16p, ctypes.c_size_t, ctypes.c_int32, _f32p]
+        L.oracle_call_cooccurrence.argtypes = [_u16p, _u64p, ctypes.c_size_t, ctypes.c_int32,
+                                               ctypes.POINTER(ctypes.c_int32)]
         L.oracle_normalize_prio.argtypes = [_f32p, ctypes.c_int32]
         L.oracle_normalize_prio.restype = None
         L.oracle_calculate_priorities.argtypes = [_f32p, _u16p, ctypes.c_size_t, ctypes.c_int32, _f32p]
@@ -134,6 +136,16 @@ def dynamic_prio(prog_len, C):
     prog_len = np.ascontiguousarray(prog_len, dtype=np.uint16)
     out = np.empty((C, C), dtype=np.float32)
     _check(lib().oracle_dynamic_prio(_p(prog_len, _u16p), prog_len.size, C, _p(out, _f32p)), "dynamic_prio")
+    return out
+
+
+def call_cooccurrence(calls, off, C):
+    """The call-ID form of prio.go:142-151: int32 C x C pair counts."""
+    calls = np.ascontiguousarray(calls, dtype=np.uint16)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    out = np.empty((C, C), dtype=np.int32)
+    _check(lib().oracle_call_cooccurrence(_p(calls, _u16p), _p(off, _u64p), off.size - 1, C,
+                                          out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "call_cooccurrence")
     return out
 
 

@@ -40,6 +40,8 @@ SIGNATURES = {
     "syzgpu_prog_scan": (_c.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
     "syzgpu_prog_scan_dev": (_c.c_int, [_vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_dynamic_prio": (_c.c_int, [_vp, _sz, _c.c_int32, _vp]),
+    "syzgpu_call_cooccurrence": (_c.c_int, [_vp, _vp, _sz, _c.c_int32, _vp]),
+    "syzgpu_call_cooccurrence_dev": (_c.c_int, [_vp, _vp, _sz, _c.c_int32, _vp, _vp]),
     "syzgpu_calculate_priorities": (_c.c_int, [_vp, _vp, _sz, _c.c_int32, _vp]),
     "syzgpu_static_priorities": (_c.c_int, [_vp, _sz, _c.c_int32, _vp]),
     "syzgpu_static_priorities_dev": (_c.c_int, [_vp, _sz, _c.c_int32, _vp, _vp]),

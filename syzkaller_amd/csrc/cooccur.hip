@@ -1,0 +1,209 @@
+// Call co-occurrence XᵀX on int8 MFMA: the north_star's "true dense contraction" reading of
+// calcDynamicPrio (prog/prio.go:137-152). The reference adds 1 to prios[i0][i1]
+// for every pair of distinct call POSITIONS i0 != i1 of a program (so its result depends only on the
+// program lengths; syzgpu_dynamic_prio reproduces that bit-exactly). This entry computes the call-ID
+// form the loop was meant to have: out[a][b] = the number of ordered pairs of distinct positions of a
+// program whose calls are (a, b), summed over the corpus — with X[a][p] = occurrences of call a in
+// program p, out = XᵀX - diag(total occurrences). It is NOT the reference's quantity; it is exact
+// integer work (int8 operands, int32 accumulation), checked bit-exact by tests/test_gpu_cooccur.py.
+//
+//   build  X in K-blocks of 32 programs, Xb[kb][c][32] int8 (a 32-row operand of one K-block is 1 KB
+//          contiguous), one program per thread (byte counts through u32 atomics), and the total
+//          occurrences per call through an LDS histogram
+//   gemm   a wave per 64x64 output tile (2x2 v_mfma_i32_32x32x32_i8), four waves per 128x128
+//          workgroup tile, the upper triangle of tiles only (an off-diagonal tile adds its transpose
+//          too), the K blocks split over KS workgroups (int32 atomics into out); every
+//          lane's operand is 16 consecutive program bytes of one call, so A and B agree on the K
+//          order inside a step (as in static_prio.hip)
+//   diag   out[a][a] -= occurrences of a
+#include <algorithm>
+
+#include "pipeline.hpp"
+
+namespace syz {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int CO_KB = 32;     // programs per K block
+constexpr int CO_TILE = 128;  // output rows/columns per workgroup
+
+// one program per thread; err: 1 = call id >= C, 2 = a call occurs more than 127 times in a program
+__global__ __launch_bounds__(256) void k_co_build(const uint16_t* __restrict__ calls, const uint64_t* __restrict__ off,
+                                                  size_t n, int32_t C, uint32_t Cp, uint32_t* Xw,
+                                                  unsigned long long* occ, int* err) {
+  extern __shared__ uint32_t lh[];
+  for (int32_t c = threadIdx.x; c < C; c += blockDim.x) lh[c] = 0;
+  __syncthreads();
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    const uint64_t b = off[p], e = off[p + 1];
+    const uint64_t kb = p / CO_KB;
+    const uint32_t kk = (uint32_t)(p % CO_KB);
+    if (e - b > 127) {
+      // a call could repeat more than an int8 holds: count this program's repeats first
+      for (uint64_t j = b; j < e; j++) {
+        uint32_t cnt = 0;
+        for (uint64_t i = b; i < e; i++) cnt += calls[i] == calls[j];
+        if (cnt > 127) atomicOr(err, 2);
+      }
+    }
+    for (uint64_t j = b; j < e; j++) {
+      const uint32_t c = calls[j];
+      if ((int32_t)c >= C) {
+        atomicOr(err, 1);
+        continue;
+      }
+      const size_t byte = ((size_t)kb * Cp + c) * CO_KB + kk;
+      atomicAdd(&Xw[byte >> 2], 1u << (8 * (byte & 3)));
+      atomicAdd(&lh[c], 1u);
+    }
+  }
+  __syncthreads();
+  for (int32_t c = threadIdx.x; c < C; c += blockDim.x)
+    if (lh[c]) atomicAdd(&occ[c], (unsigned long long)lh[c]);
+}
+
+// grid (T (T + 1) / 2, KS) over the upper triangle of the T x T workgroup tiles (XᵀX is symmetric: an
+// off-diagonal tile also adds its transpose); a wave's tile: rows r0 + [0, 64), columns c0 + [0, 64)
+__global__ __launch_bounds__(256) void k_co_gemm(const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t T,
+                                                 uint32_t nkb, uint32_t kb_per, int* __restrict__ out) {
+  uint32_t ty = 0, t = blockIdx.x;  // t -> (ty, tx), tx >= ty
+  while (t >= T - ty) t -= T - ty++;
+  const uint32_t tx = ty + t;
+  const int wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  const uint32_t r0 = ty * CO_TILE + (wv >> 1) * 64, c0 = tx * CO_TILE + (wv & 1) * 64;
+  const uint32_t kb0 = blockIdx.y * kb_per, kb1 = min(nkb, kb0 + kb_per);
+  v16i acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) acc[i][j] = v16i{};
+  // lane l: 16 bytes [16 (l >> 5), +16) of row (l & 31) of a 32-row operand
+  const size_t lo = (size_t)(lane & 31) * CO_KB + 16 * (lane >> 5);
+  const size_t kstride = (size_t)Cp * CO_KB;
+  const int8_t* pa = X + (size_t)r0 * CO_KB + lo;
+  const int8_t* pb = X + (size_t)c0 * CO_KB + lo;
+  if (kb0 < kb1) {
+    v4i a0 = *reinterpret_cast<const v4i*>(pa + kb0 * kstride);
+    v4i a1 = *reinterpret_cast<const v4i*>(pa + kb0 * kstride + 32 * CO_KB);
+    v4i b0 = *reinterpret_cast<const v4i*>(pb + kb0 * kstride);
+    v4i b1 = *reinterpret_cast<const v4i*>(pb + kb0 * kstride + 32 * CO_KB);
+    for (uint32_t kb = kb0; kb < kb1; kb++) {
+      // the next block's operands in flight while this one's four MFMAs run
+      v4i na0 = a0, na1 = a1, nb0 = b0, nb1 = b1;
+      if (kb + 1 < kb1) {
+        const size_t o = (size_t)(kb + 1) * kstride;
+        na0 = *reinterpret_cast<const v4i*>(pa + o);
+        na1 = *reinterpret_cast<const v4i*>(pa + o + 32 * CO_KB);
+        nb0 = *reinterpret_cast<const v4i*>(pb + o);
+        nb1 = *reinterpret_cast<const v4i*>(pb + o + 32 * CO_KB);
+      }
+      acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
+      a0 = na0, a1 = na1, b0 = nb0, b1 = nb1;
+    }
+  }
+  // result register r of lane l: row (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31 (gfx950 32x32)
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t col = c0 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const uint32_t row = r0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int v = acc[i][j][r];
+        if ((int32_t)row < C && (int32_t)col < C && v) {
+          atomicAdd(&out[(size_t)row * C + col], v);
+          if (tx != ty) atomicAdd(&out[(size_t)col * C + row], v);
+        }
+      }
+    }
+}
+
+__global__ void k_co_diag(const unsigned long long* occ, int32_t C, int* out) {
+  for (int32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < C; a += gridDim.x * blockDim.x)
+    out[(size_t)a * C + a] -= (int)occ[a];
+}
+
+// SYZGPU_CO_KS=k forces the K split (tests; read on every call)
+static uint32_t co_splits() {
+  const char* e = getenv("SYZGPU_CO_KS");
+  return e ? (uint32_t)std::max(1, atoi(e)) : 0u;
+}
+
+// out (C x C int32, device) = the call-ID co-occurrence of the programs' call lists (device CSR)
+void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n, int32_t C, int32_t* out,
+                           hipStream_t s) {
+  if (C <= 0 || C > 16384) fail(SYZGPU_EINVAL, "C out of range");
+  if (!out || (n && !off)) fail(SYZGPU_EINVAL, "null pointer");
+  Context& c = ctx();
+  Scratch& sc = c.scratch;
+  const uint32_t Cp = ((uint32_t)C + CO_TILE - 1) / CO_TILE * CO_TILE;
+  const uint32_t nkb = (uint32_t)((n + CO_KB - 1) / CO_KB);
+  const size_t xbytes = (size_t)std::max<uint32_t>(nkb, 1) * Cp * CO_KB;
+  uint32_t* Xw = sc.get<uint32_t>("co_x", xbytes / 4 + 1);
+  unsigned long long* occ = sc.get<unsigned long long>("co_occ", (size_t)C + 1);
+  int* err = sc.get<int>("co_err", 2);
+  SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
+  SYZ_HIP(hipMemsetAsync(occ, 0, ((size_t)C + 1) * 8, s));
+  SYZ_HIP(hipMemsetAsync(out, 0, (size_t)C * C * 4, s));
+  {
+    ProfScope ps("cooc_build", s, xbytes);
+    SYZ_HIP(hipMemsetAsync(Xw, 0, xbytes, s));
+    if (n) {
+      k_co_build<<<grid_for(n, 256, 1024), 256, (size_t)C * 4, s>>>(calls, off, n, C, Cp, Xw, occ, err);
+      SYZ_LAUNCHED();
+    }
+  }
+  {
+    // K split: enough workgroups for every CU a few times over
+    if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+    const uint32_t T = Cp / CO_TILE, tiles = T * (T + 1) / 2;
+    uint32_t ks = co_splits();
+    if (!ks) ks = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(nkb, 1), (4u * c.ncu + tiles - 1) / tiles));
+    const uint32_t kb_per = (std::max<uint32_t>(nkb, 1) + ks - 1) / ks;
+    ProfScope ps("cooc_gemm", s, 2ull * C * C * (uint64_t)nkb * CO_KB);  // (ops, not bytes)
+    k_co_gemm<<<dim3(tiles, ks), 256, 0, s>>>(reinterpret_cast<const int8_t*>(Xw), C, Cp, T, nkb, kb_per, out);
+    SYZ_LAUNCHED();
+    k_co_diag<<<grid_for(C, 256, 64), 256, 0, s>>>(occ, C, out);
+    SYZ_LAUNCHED();
+  }
+  int* h = c.pinned.get<int>(2);
+  SYZ_HIP(hipMemcpyAsync(h, err, 4, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (h[0] & 1) fail(SYZGPU_EINVAL, "call id >= C");
+  if (h[0] & 2) fail(SYZGPU_EINVAL, "a call occurs more than 127 times in one program (int8 operand)");
+}
+
+}  // namespace syz
+
+extern "C" int syzgpu_call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n, int32_t C,
+                                            int32_t* out, void* stream) {
+  SYZ_API_BODY({ syz::call_cooccurrence_dev(calls, off, n, C, out, (hipStream_t)stream); })
+}
+
+extern "C" int syzgpu_call_cooccurrence(const uint16_t* calls, const uint64_t* off, size_t n, int32_t C,
+                                        int32_t* out) {
+  SYZ_API_BODY({
+    if (!off || !out) syz::fail(SYZGPU_EINVAL, "null pointer");
+    if (off[0] != 0) syz::fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
+    for (size_t i = 0; i < n; i++)
+      if (off[i + 1] < off[i]) syz::fail(SYZGPU_EINVAL, "CSR offsets must be non-decreasing");
+    if (C <= 0 || C > 16384) syz::fail(SYZGPU_EINVAL, "C out of range");
+    syz::Context& c = syz::ctx();
+    hipStream_t s = c.stream;
+    const uint64_t L = off[n];
+    uint16_t* dc = c.scratch.get<uint16_t>("co_calls", L + 1);
+    uint64_t* doff = c.scratch.get<uint64_t>("co_off", n + 1);
+    int32_t* dout = c.scratch.get<int32_t>("co_out", (size_t)C * C + 1);
+    if (L) SYZ_HIP(hipMemcpyAsync(dc, calls, L * 2, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    syz::call_cooccurrence_dev(dc, doff, n, C, dout, s);
+    SYZ_HIP(hipMemcpyAsync(out, dout, (size_t)C * C * 4, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+  })
+}

@@ -29,6 +29,17 @@ def calcDynamicPrio(prog_lens, C):
     return out
 
 
+def CallCooccurrence(calls, off, C):
+    """The call-ID co-occurrence XᵀX on int8 MFMA (not the reference's calcDynamicPrio,
+    which counts call positions): int32 C x C, [a][b] = ordered pairs of distinct positions with calls
+    (a, b) in one program, summed over the programs of the CSR (calls, off)."""
+    calls = np.ascontiguousarray(calls, dtype=np.uint16)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    out = np.empty((C, C), dtype=np.int32)
+    check(lib().syzgpu_call_cooccurrence(ptr(calls), ptr(off), off.size - 1, C, ptr(out)))
+    return out
+
+
 def calcStaticPriorities(usage=None):
     """prio.go:40-135 for the calls of `usage` (sysdesc.Usage; default: the bundled sys/*.txt)."""
     if usage is None:

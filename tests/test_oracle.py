@@ -204,3 +204,21 @@ def test_novelty_first_occurrence_equals_literal(nth):
     g = oracle.novelty_mt(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes, nth)
     assert all(np.array_equal(a, b) for a, b in zip(w, g))
     assert 0 < w[0].sum() < fresh.n
+
+
+def test_oracle_call_cooccurrence_literal_pairs():
+    # the oracle's pair loop against a direct Python restatement of the call-ID form of
+    # prio.go:142-151 (for i0, for i1 != i0: prios[id(i0)][id(i1)] += 1)
+    rnd = np.random.default_rng(9)
+    C = 12
+    progs = [list(rnd.integers(0, C, size=int(rnd.integers(0, 9)))) for _ in range(60)]
+    want = np.zeros((C, C), np.int32)
+    for p in progs:
+        for i0 in range(len(p)):
+            for i1 in range(len(p)):
+                if i0 != i1:
+                    want[p[i0], p[i1]] += 1
+    off = np.zeros(len(progs) + 1, np.uint64)
+    np.cumsum([len(p) for p in progs], out=off[1:])
+    calls = np.array([c for p in progs for c in p], np.uint16)
+    assert np.array_equal(oracle.call_cooccurrence(calls, off, C), want)
