@@ -63,17 +63,30 @@ __global__ __launch_bounds__(256) void k_co_build(const uint16_t* __restrict__ c
     if (lh[c]) atomicAdd(&occ[c], (unsigned long long)lh[c]);
 }
 
-// grid (T (T + 1) / 2, KS) over the upper triangle of the T x T workgroup tiles (XᵀX is symmetric: an
-// off-diagonal tile also adds its transpose); a wave's tile: rows r0 + [0, 64), columns c0 + [0, 64)
-__global__ __launch_bounds__(256) void k_co_gemm(const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t T,
-                                                 uint32_t nkb, uint32_t kb_per, int* __restrict__ out) {
-  uint32_t ty = 0, t = blockIdx.x;  // t -> (ty, tx), tx >= ty
+// tiles x KS workgroups over the upper triangle of the T x T workgroup tiles (XᵀX is symmetric: an
+// off-diagonal tile also adds its transpose) and KS ranges of K blocks; a wave's tile: rows
+// r0 + [0, 64), columns c0 + [0, 64). XCD-aware when KS % 8 == 0: workgroups are dealt to the 8 XCDs
+// round-robin, so block b runs on XCD b % 8; every tile of one K range is placed on the same XCD,
+// so each X block is fetched from HBM into one L2 and re-read there by the tiles that share its rows
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_co_gemm(const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t T,
+                                                 uint32_t tiles, uint32_t ks, uint32_t nkb, uint32_t kb_per,
+                                                 int* __restrict__ out) {
+  uint32_t t, kg;
+  if (ks % 8 == 0) {
+    const uint32_t j = blockIdx.x >> 3;
+    t = j % tiles;
+    kg = (j / tiles) * 8 + (blockIdx.x & 7);
+  } else {
+    t = blockIdx.x % tiles;
+    kg = blockIdx.x / tiles;
+  }
+  uint32_t ty = 0;  // t -> (ty, tx), tx >= ty
   while (t >= T - ty) t -= T - ty++;
   const uint32_t tx = ty + t;
   const int wv = threadIdx.x >> 6;
   const unsigned lane = __lane_id();
   const uint32_t r0 = ty * CO_TILE + (wv >> 1) * 64, c0 = tx * CO_TILE + (wv & 1) * 64;
-  const uint32_t kb0 = blockIdx.y * kb_per, kb1 = min(nkb, kb0 + kb_per);
+  const uint32_t kb0 = kg * kb_per, kb1 = min(nkb, kb0 + kb_per);
   v16i acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; i++)
@@ -132,7 +145,7 @@ __global__ void k_co_diag(const unsigned long long* occ, int32_t C, int* out) {
 // SYZGPU_CO_KS=k forces the K split (tests; read on every call)
 static uint32_t co_splits() {
   const char* e = getenv("SYZGPU_CO_KS");
-  return e ? (uint32_t)std::max(1, atoi(e)) : 0u;
+  return e && *e ? (uint32_t)std::max(1, atoi(e)) : 0u;
 }
 
 // out (C x C int32, device) = the call-ID co-occurrence of the programs' call lists (device CSR)
@@ -160,14 +173,19 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
     }
   }
   {
-    // K split: enough workgroups for every CU a few times over
+    // K split: about two workgroups per CU (all resident at once), in multiples of 8 K ranges (one
+    // set of ranges per XCD) once there are enough K blocks for that
     if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
     const uint32_t T = Cp / CO_TILE, tiles = T * (T + 1) / 2;
     uint32_t ks = co_splits();
-    if (!ks) ks = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(nkb, 1), (4u * c.ncu + tiles - 1) / tiles));
+    if (!ks) {
+      ks = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(nkb, 1), (2u * c.ncu + tiles - 1) / tiles));
+      if (nkb >= 64) ks = std::min<uint32_t>((ks + 7) / 8 * 8, nkb / 8 * 8);
+    }
     const uint32_t kb_per = (std::max<uint32_t>(nkb, 1) + ks - 1) / ks;
     ProfScope ps("cooc_gemm", s, 2ull * C * C * (uint64_t)nkb * CO_KB);  // (ops, not bytes)
-    k_co_gemm<<<dim3(tiles, ks), 256, 0, s>>>(reinterpret_cast<const int8_t*>(Xw), C, Cp, T, nkb, kb_per, out);
+    k_co_gemm<<<tiles * ks, 256, 0, s>>>(reinterpret_cast<const int8_t*>(Xw), C, Cp, T, tiles, ks, nkb, kb_per,
+                                          out);
     SYZ_LAUNCHED();
     k_co_diag<<<grid_for(C, 256, 64), 256, 0, s>>>(occ, C, out);
     SYZ_LAUNCHED();

@@ -67,11 +67,12 @@ def test_cooccurrence_edges():
 
 def test_cooccurrence_k_tail_and_splits(monkeypatch):
     # program counts around the 32-program K blocks, with the K split forced to several values
-    C = 96
-    for n in (31, 32, 33, 1023, 4097):
+    # (KS a multiple of 8 takes the XCD-aware block mapping; C = 300 has 6 upper-triangle tiles)
+    cases = [(96, n) for n in (31, 32, 33, 1023, 4097)] + [(300, 4097), (300, 20000)]
+    for C, n in cases:
         calls, off = corpus_calls(n, n, C)
         want = oracle.call_cooccurrence(calls, off, C)
-        for ks in ("1", "3", "64"):
+        for ks in ("1", "3", "16", "64"):
             monkeypatch.setenv("SYZGPU_CO_KS", ks)
             assert np.array_equal(prog.CallCooccurrence(calls, off, C), want)
 
