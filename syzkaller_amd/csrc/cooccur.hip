@@ -68,6 +68,7 @@ __global__ __launch_bounds__(256) void k_co_build(const uint16_t* __restrict__ c
 // r0 + [0, 64), columns c0 + [0, 64). XCD-aware when KS % 8 == 0: workgroups are dealt to the 8 XCDs
 // round-robin, so block b runs on XCD b % 8; every tile of one K range is placed on the same XCD,
 // so each X block is fetched from HBM into one L2 and re-read there by the tiles that share its rows
+template <int PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_co_gemm(const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t T,
                                                  uint32_t tiles, uint32_t ks, uint32_t nkb, uint32_t kb_per,
                                                  int* __restrict__ out) {
@@ -97,29 +98,136 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const size_t kstride = (size_t)Cp * CO_KB;
   const int8_t* pa = X + (size_t)r0 * CO_KB + lo;
   const int8_t* pb = X + (size_t)c0 * CO_KB + lo;
-  if (kb0 < kb1) {
-    v4i a0 = *reinterpret_cast<const v4i*>(pa + kb0 * kstride);
-    v4i a1 = *reinterpret_cast<const v4i*>(pa + kb0 * kstride + 32 * CO_KB);
-    v4i b0 = *reinterpret_cast<const v4i*>(pb + kb0 * kstride);
-    v4i b1 = *reinterpret_cast<const v4i*>(pb + kb0 * kstride + 32 * CO_KB);
-    for (uint32_t kb = kb0; kb < kb1; kb++) {
-      // the next block's operands in flight while this one's four MFMAs run
-      v4i na0 = a0, na1 = a1, nb0 = b0, nb1 = b1;
-      if (kb + 1 < kb1) {
-        const size_t o = (size_t)(kb + 1) * kstride;
-        na0 = *reinterpret_cast<const v4i*>(pa + o);
-        na1 = *reinterpret_cast<const v4i*>(pa + o + 32 * CO_KB);
-        nb0 = *reinterpret_cast<const v4i*>(pb + o);
-        nb1 = *reinterpret_cast<const v4i*>(pb + o + 32 * CO_KB);
+  // PF K blocks of operands in flight: stage i holds block kb + i while block kb's MFMAs run
+  v4i st[PF][4];
+#pragma unroll
+  for (int i = 0; i < PF; i++)
+    if (kb0 + i < kb1) {
+      const size_t o = (size_t)(kb0 + i) * kstride;
+      st[i][0] = *reinterpret_cast<const v4i*>(pa + o);
+      st[i][1] = *reinterpret_cast<const v4i*>(pa + o + 32 * CO_KB);
+      st[i][2] = *reinterpret_cast<const v4i*>(pb + o);
+      st[i][3] = *reinterpret_cast<const v4i*>(pb + o + 32 * CO_KB);
+    }
+  for (uint32_t kb = kb0; kb < kb1; kb += PF) {
+#pragma unroll
+    for (int i = 0; i < PF; i++) {
+      if (kb + i >= kb1) break;
+      const v4i a0 = st[i][0], a1 = st[i][1], b0 = st[i][2], b1 = st[i][3];
+      if (kb + i + PF < kb1) {
+        const size_t o = (size_t)(kb + i + PF) * kstride;
+        st[i][0] = *reinterpret_cast<const v4i*>(pa + o);
+        st[i][1] = *reinterpret_cast<const v4i*>(pa + o + 32 * CO_KB);
+        st[i][2] = *reinterpret_cast<const v4i*>(pb + o);
+        st[i][3] = *reinterpret_cast<const v4i*>(pb + o + 32 * CO_KB);
       }
       acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
-      a0 = na0, a1 = na1, b0 = nb0, b1 = nb1;
     }
   }
   // result register r of lane l: row (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31 (gfx950 32x32)
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t col = c0 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const uint32_t row = r0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int v = acc[i][j][r];
+        if ((int32_t)row < C && (int32_t)col < C && v) {
+          atomicAdd(&out[(size_t)row * C + col], v);
+          if (tx != ty) atomicAdd(&out[(size_t)col * C + row], v);
+        }
+      }
+    }
+}
+
+// LDS-staged form: a workgroup of (TILE / 64)^2 waves stages each K block's A rows [ty TILE, +TILE) and
+// B rows [tx TILE, +TILE) (TILE x 32 bytes each, contiguous in Xb) through double-buffered LDS, one
+// 16-byte global load per thread per operand; each wave then reads its 2 + 2 operands from LDS
+// (ds_read_b128). The two 16-byte halves of row r sit swapped when bit 3 of r is set, so the lane
+// groups of a ds_read_b128 (rows {0-3, 12-15, 20-27}, ...) hit 16 distinct 4-bank sets.
+template <int TILE>
+__global__ __launch_bounds__(TILE* TILE / 64) __attribute__((amdgpu_waves_per_eu(4))) void k_co_gemm_lds(
+    const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t T, uint32_t tiles, uint32_t ks, uint32_t nkb,
+    uint32_t kb_per, int* __restrict__ out) {
+  constexpr int NT = TILE * TILE / 64;        // threads
+  constexpr int OPB = TILE * CO_KB;           // bytes of one operand tile per K block
+  constexpr int LPT = 2 * OPB / 16 / NT;      // 16-byte loads per thread per K block (A and B)
+  static_assert(LPT >= 1 && (2 * OPB / 16) % NT == 0, "staging split");
+  __shared__ __align__(16) int8_t sm[2][2 * OPB];  // [buffer][A tile | B tile]
+  uint32_t t, kg;
+  if (ks % 8 == 0) {
+    const uint32_t j = blockIdx.x >> 3;
+    t = j % tiles;
+    kg = (j / tiles) * 8 + (blockIdx.x & 7);
+  } else {
+    t = blockIdx.x % tiles;
+    kg = blockIdx.x / tiles;
+  }
+  uint32_t ty = 0;
+  while (t >= T - ty) t -= T - ty++;
+  const uint32_t tx = ty + t;
+  const int wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  constexpr int WPR = TILE / 64;  // waves per tile row
+  const uint32_t wr = (wv / WPR) * 64, wc = (wv % WPR) * 64;
+  const uint32_t kb0 = kg * kb_per, kb1 = min(nkb, kb0 + kb_per);
+  const size_t kstride = (size_t)Cp * CO_KB;
+  // staging: chunk q = threadIdx.x + i NT of [A tile | B tile]; its row and half, swizzled LDS offset
+  const int8_t* gsrc[LPT];
+  int soff[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; i++) {
+    const int q = threadIdx.x + i * NT;
+    const int isb = q >= OPB / 16, qq = isb ? q - OPB / 16 : q;
+    const int row = qq >> 1, half = qq & 1;
+    gsrc[i] = X + (size_t)((isb ? tx : ty) * TILE + row) * CO_KB + 16 * half;
+    soff[i] = isb * OPB + row * CO_KB + 16 * (half ^ ((row >> 3) & 1));
+  }
+  // operand reads: lane l takes half (l >> 5) of row (l & 31) of a 32-row block
+  const int lrow = lane & 31, lhalf = lane >> 5;
+  int aoff[2], boff[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int ra = wr + 32 * i + lrow, rb = wc + 32 * i + lrow;
+    aoff[i] = ra * CO_KB + 16 * (lhalf ^ ((ra >> 3) & 1));
+    boff[i] = OPB + rb * CO_KB + 16 * (lhalf ^ ((rb >> 3) & 1));
+  }
+  v16i acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) acc[i][j] = v16i{};
+  if (kb0 < kb1) {
+    v4i g[LPT];
+#pragma unroll
+    for (int i = 0; i < LPT; i++) g[i] = *reinterpret_cast<const v4i*>(gsrc[i] + kb0 * kstride);
+    int cur = 0;
+    for (uint32_t kb = kb0; kb < kb1; kb++) {
+#pragma unroll
+      for (int i = 0; i < LPT; i++) *reinterpret_cast<v4i*>(&sm[cur][soff[i]]) = g[i];
+      __syncthreads();
+      if (kb + 1 < kb1) {
+        const size_t o = (size_t)(kb + 1) * kstride;
+#pragma unroll
+        for (int i = 0; i < LPT; i++) g[i] = *reinterpret_cast<const v4i*>(gsrc[i] + o);
+      }
+      const v4i a0 = *reinterpret_cast<const v4i*>(&sm[cur][aoff[0]]);
+      const v4i a1 = *reinterpret_cast<const v4i*>(&sm[cur][aoff[1]]);
+      const v4i b0 = *reinterpret_cast<const v4i*>(&sm[cur][boff[0]]);
+      const v4i b1 = *reinterpret_cast<const v4i*>(&sm[cur][boff[1]]);
+      acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
+      cur ^= 1;
+    }
+  }
+  const uint32_t r0 = ty * TILE + wr, c0 = tx * TILE + wc;
 #pragma unroll
   for (int i = 0; i < 2; i++)
 #pragma unroll
@@ -148,6 +256,13 @@ static uint32_t co_splits() {
   return e && *e ? (uint32_t)std::max(1, atoi(e)) : 0u;
 }
 
+// A/B knobs, read on every call: SYZGPU_CO_FORM=0|1|2 (direct operand loads with 128 tiles, LDS-staged
+// 128, LDS-staged 256), SYZGPU_CO_PF=1..3 (K blocks in flight in the direct form)
+static int co_env(const char* name, int def, int lo, int hi) {
+  const char* e = getenv(name);
+  return e && *e ? std::min(hi, std::max(lo, atoi(e))) : def;
+}
+
 // out (C x C int32, device) = the call-ID co-occurrence of the programs' call lists (device CSR)
 void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n, int32_t C, int32_t* out,
                            hipStream_t s) {
@@ -155,7 +270,7 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
   if (!out || (n && !off)) fail(SYZGPU_EINVAL, "null pointer");
   Context& c = ctx();
   Scratch& sc = c.scratch;
-  const uint32_t Cp = ((uint32_t)C + CO_TILE - 1) / CO_TILE * CO_TILE;
+  const uint32_t Cp = ((uint32_t)C + 255) / 256 * 256;  // rows per K block: a multiple of every tile size
   const uint32_t nkb = (uint32_t)((n + CO_KB - 1) / CO_KB);
   const size_t xbytes = (size_t)std::max<uint32_t>(nkb, 1) * Cp * CO_KB;
   uint32_t* Xw = sc.get<uint32_t>("co_x", xbytes / 4 + 1);
@@ -176,7 +291,10 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
     // K split: about two workgroups per CU (all resident at once), in multiples of 8 K ranges (one
     // set of ranges per XCD) once there are enough K blocks for that
     if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
-    const uint32_t T = Cp / CO_TILE, tiles = T * (T + 1) / 2;
+    const int pf = co_env("SYZGPU_CO_PF", 1, 1, 3);
+    const int form = co_env("SYZGPU_CO_FORM", 0, 0, 2);  // 0 direct operand loads (128 tiles), 1 LDS-staged 128, 2 LDS-staged 256
+    const uint32_t tile = form == 2 ? 256 : CO_TILE;
+    const uint32_t T = Cp / tile, tiles = T * (T + 1) / 2;
     uint32_t ks = co_splits();
     if (!ks) {
       ks = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(nkb, 1), (2u * c.ncu + tiles - 1) / tiles));
@@ -184,8 +302,17 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
     }
     const uint32_t kb_per = (std::max<uint32_t>(nkb, 1) + ks - 1) / ks;
     ProfScope ps("cooc_gemm", s, 2ull * C * C * (uint64_t)nkb * CO_KB);  // (ops, not bytes)
-    k_co_gemm<<<tiles * ks, 256, 0, s>>>(reinterpret_cast<const int8_t*>(Xw), C, Cp, T, tiles, ks, nkb, kb_per,
-                                          out);
+    const int8_t* Xb = reinterpret_cast<const int8_t*>(Xw);
+    if (form == 2)
+      k_co_gemm_lds<256><<<tiles * ks, 1024, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+    else if (form == 1)
+      k_co_gemm_lds<128><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+    else if (pf == 3)
+      k_co_gemm<3><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+    else if (pf == 2)
+      k_co_gemm<2><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+    else
+      k_co_gemm<1><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
     SYZ_LAUNCHED();
     k_co_diag<<<grid_for(C, 256, 64), 256, 0, s>>>(occ, C, out);
     SYZ_LAUNCHED();
