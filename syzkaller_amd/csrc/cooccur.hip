@@ -12,10 +12,10 @@
 //          occurrences per call through an LDS histogram
 //   gemm   a wave per 64x64 output tile (2x2 v_mfma_i32_32x32x32_i8), four waves per 128x128
 //          workgroup tile, the upper triangle of tiles only (an off-diagonal tile adds its transpose
-//          too), the K blocks split over KS workgroups (int32 atomics into out); every
+//          too), the K blocks split over KS workgroups, each storing its partial tile; every
 //          lane's operand is 16 consecutive program bytes of one call, so A and B agree on the K
 //          order inside a step (as in static_prio.hip)
-//   diag   out[a][a] -= occurrences of a
+//   reduce out = the sum of the KS partials (and its transpose), out[a][a] -= occurrences of a
 #include <algorithm>
 
 #include "pipeline.hpp"
@@ -63,6 +63,25 @@ __global__ __launch_bounds__(256) void k_co_build(const uint16_t* __restrict__ c
     if (lh[c]) atomicAdd(&occ[c], (unsigned long long)lh[c]);
 }
 
+// a wave's 64x64 accumulators into its workgroup's partial tile P[kg][tile][TILE][TILE] (plain stores:
+// the KS partials are summed by k_co_reduce). Result register r of lane l: row (r & 3) + 8 (r >> 2) +
+// 4 (l >> 5), column l & 31 (gfx950 32x32).
+template <int TILE>
+__device__ __forceinline__ void co_store_partial(const v16i (&acc)[2][2], int* __restrict__ P, size_t tbase,
+                                                 uint32_t wr, uint32_t wc, unsigned lane) {
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const uint32_t col = wc + 32 * j + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const uint32_t row = wr + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        P[tbase + (size_t)row * TILE + col] = acc[i][j][r];
+      }
+    }
+}
+
 // tiles x KS workgroups over the upper triangle of the T x T workgroup tiles (XᵀX is symmetric: an
 // off-diagonal tile also adds its transpose) and KS ranges of K blocks; a wave's tile: rows
 // r0 + [0, 64), columns c0 + [0, 64). XCD-aware when KS % 8 == 0: workgroups are dealt to the 8 XCDs
@@ -71,7 +90,7 @@ __global__ __launch_bounds__(256) void k_co_build(const uint16_t* __restrict__ c
 template <int PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_co_gemm(const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t T,
                                                  uint32_t tiles, uint32_t ks, uint32_t nkb, uint32_t kb_per,
-                                                 int* __restrict__ out) {
+                                                 int* __restrict__ P) {
   uint32_t t, kg;
   if (ks % 8 == 0) {
     const uint32_t j = blockIdx.x >> 3;
@@ -81,6 +100,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     t = blockIdx.x % tiles;
     kg = blockIdx.x / tiles;
   }
+  const uint32_t tid = t;
   uint32_t ty = 0;  // t -> (ty, tx), tx >= ty
   while (t >= T - ty) t -= T - ty++;
   const uint32_t tx = ty + t;
@@ -127,22 +147,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
     }
   }
-  // result register r of lane l: row (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31 (gfx950 32x32)
-#pragma unroll
-  for (int i = 0; i < 2; i++)
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const uint32_t col = c0 + 32 * j + (lane & 31);
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const uint32_t row = r0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int v = acc[i][j][r];
-        if ((int32_t)row < C && (int32_t)col < C && v) {
-          atomicAdd(&out[(size_t)row * C + col], v);
-          if (tx != ty) atomicAdd(&out[(size_t)col * C + row], v);
-        }
-      }
-    }
+  co_store_partial<CO_TILE>(acc, P, ((size_t)kg * tiles + tid) * CO_TILE * CO_TILE, (wv >> 1) * 64, (wv & 1) * 64, lane);
 }
 
 // LDS-staged form: a workgroup of (TILE / 64)^2 waves stages each K block's A rows [ty TILE, +TILE) and
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 template <int TILE>
 __global__ __launch_bounds__(TILE* TILE / 64) __attribute__((amdgpu_waves_per_eu(4))) void k_co_gemm_lds(
     const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t T, uint32_t tiles, uint32_t ks, uint32_t nkb,
-    uint32_t kb_per, int* __restrict__ out) {
+    uint32_t kb_per, int* __restrict__ P) {
   constexpr int NT = TILE * TILE / 64;        // threads
   constexpr int OPB = TILE * CO_KB;           // bytes of one operand tile per K block
   constexpr int LPT = 2 * OPB / 16 / NT;      // 16-byte loads per thread per K block (A and B)
@@ -168,6 +173,7 @@ __global__ __launch_bounds__(TILE* TILE / 64) __attribute__((amdgpu_waves_per_eu
     t = blockIdx.x % tiles;
     kg = blockIdx.x / tiles;
   }
+  const uint32_t tid = t;
   uint32_t ty = 0;
   while (t >= T - ty) t -= T - ty++;
   const uint32_t tx = ty + t;
@@ -227,27 +233,29 @@ __global__ __launch_bounds__(TILE* TILE / 64) __attribute__((amdgpu_waves_per_eu
       cur ^= 1;
     }
   }
-  const uint32_t r0 = ty * TILE + wr, c0 = tx * TILE + wc;
-#pragma unroll
-  for (int i = 0; i < 2; i++)
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const uint32_t col = c0 + 32 * j + (lane & 31);
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const uint32_t row = r0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int v = acc[i][j][r];
-        if ((int32_t)row < C && (int32_t)col < C && v) {
-          atomicAdd(&out[(size_t)row * C + col], v);
-          if (tx != ty) atomicAdd(&out[(size_t)col * C + row], v);
-        }
-      }
-    }
+  co_store_partial<TILE>(acc, P, ((size_t)kg * tiles + tid) * TILE * TILE, wr, wc, lane);
 }
 
-__global__ void k_co_diag(const unsigned long long* occ, int32_t C, int* out) {
-  for (int32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < C; a += gridDim.x * blockDim.x)
-    out[(size_t)a * C + a] -= (int)occ[a];
+// out[row][col] = the sum of the KS partials of (row, col), minus the occurrences of row on the
+// diagonal; one thread per element of an upper-triangle tile, which writes the element and, off the
+// diagonal tiles, its transpose (so every element of out is written exactly once)
+__global__ __launch_bounds__(256) void k_co_reduce(const int* __restrict__ P, uint32_t tiles, uint32_t ks,
+                                                   uint32_t T, uint32_t tile, int32_t C,
+                                                   const unsigned long long* __restrict__ occ, int* __restrict__ out) {
+  uint32_t t = blockIdx.x;
+  const uint32_t e = blockIdx.y * blockDim.x + threadIdx.x;
+  const size_t tt = (size_t)tile * tile;
+  const size_t base = (size_t)t * tt + e;
+  uint32_t ty = 0;
+  while (t >= T - ty) t -= T - ty++;
+  const uint32_t tx = ty + t;
+  const uint32_t row = ty * tile + e / tile, col = tx * tile + e % tile;
+  if ((int32_t)row >= C || (int32_t)col >= C) return;
+  int v = 0;
+  for (uint32_t kg = 0; kg < ks; kg++) v += P[(size_t)kg * tiles * tt + base];
+  if (row == col) v -= (int)occ[row];
+  out[(size_t)row * C + col] = v;
+  if (tx != ty) out[(size_t)col * C + row] = v;
 }
 
 // SYZGPU_CO_KS=k forces the K split (tests; read on every call)
@@ -278,7 +286,6 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
   int* err = sc.get<int>("co_err", 2);
   SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
   SYZ_HIP(hipMemsetAsync(occ, 0, ((size_t)C + 1) * 8, s));
-  SYZ_HIP(hipMemsetAsync(out, 0, (size_t)C * C * 4, s));
   {
     ProfScope ps("cooc_build", s, xbytes);
     SYZ_HIP(hipMemsetAsync(Xw, 0, xbytes, s));
@@ -300,21 +307,27 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
       ks = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(nkb, 1), (2u * c.ncu + tiles - 1) / tiles));
       if (nkb >= 64) ks = std::min<uint32_t>((ks + 7) / 8 * 8, nkb / 8 * 8);
     }
+    // the partial tiles stay within 2 GiB
+    ks = std::min<uint32_t>(ks, std::max<uint64_t>(1, (1ull << 29) / ((uint64_t)tiles * tile * tile)));
     const uint32_t kb_per = (std::max<uint32_t>(nkb, 1) + ks - 1) / ks;
-    ProfScope ps("cooc_gemm", s, 2ull * C * C * (uint64_t)nkb * CO_KB);  // (ops, not bytes)
     const int8_t* Xb = reinterpret_cast<const int8_t*>(Xw);
+    int* P = sc.get<int>("co_part", (size_t)ks * tiles * tile * tile);
+    {
+    ProfScope ps("cooc_gemm", s, 2ull * C * C * (uint64_t)nkb * CO_KB);  // (ops, not bytes)
     if (form == 2)
-      k_co_gemm_lds<256><<<tiles * ks, 1024, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+      k_co_gemm_lds<256><<<tiles * ks, 1024, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     else if (form == 1)
-      k_co_gemm_lds<128><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+      k_co_gemm_lds<128><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     else if (pf == 3)
-      k_co_gemm<3><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+      k_co_gemm<3><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     else if (pf == 2)
-      k_co_gemm<2><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+      k_co_gemm<2><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     else
-      k_co_gemm<1><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, out);
+      k_co_gemm<1><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     SYZ_LAUNCHED();
-    k_co_diag<<<grid_for(C, 256, 64), 256, 0, s>>>(occ, C, out);
+    }
+    ProfScope ps("cooc_reduce", s, (uint64_t)ks * tiles * tile * tile * 4 + (uint64_t)C * C * 4);
+    k_co_reduce<<<dim3(tiles, tile * tile / 256), 256, 0, s>>>(P, tiles, ks, T, tile, C, occ, out);
     SYZ_LAUNCHED();
   }
   int* h = c.pinned.get<int>(2);
