@@ -250,6 +250,33 @@ __device__ __forceinline__ T wave_min(T x) {
   return x;
 }
 
+// Folds every thread's [lo, hi] into span[0] (min) and span[1] (max): reduced across the workgroup
+// first, and each atomic skipped when the running span already covers the block's value (same-address
+// atomics from every wave of a large grid serialize). Every thread of the block must call it.
+template <int BLOCK>
+__device__ __forceinline__ void block_span_update(uint32_t lo, uint32_t hi, uint32_t* span) {
+  __shared__ uint32_t red[2][BLOCK / 64];
+  lo = wave_min(lo);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t y = __shfl_xor(hi, d, 64);
+    hi = y > hi ? y : hi;
+  }
+  if (__lane_id() == 0) {
+    red[0][threadIdx.x >> 6] = lo;
+    red[1][threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < BLOCK / 64; i++) {
+      lo = min(lo, red[0][i]);
+      hi = max(hi, red[1][i]);
+    }
+    if (lo < __hip_atomic_load(&span[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&span[0], lo);
+    if (hi > __hip_atomic_load(&span[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&span[1], hi);
+  }
+}
+
 // Exclusive scan across a workgroup of BLOCK threads. lds needs BLOCK/64 + 1 slots. Every thread
 // reads the (at most 16) wave totals itself: two barriers, no serial pass.
 template <int BLOCK, class T>

@@ -86,6 +86,9 @@ __global__ __launch_bounds__(256) void k_grp_scatter(const uint32_t* group, cons
     // an invalid id goes to group 0, exactly as k_grp_count counted it, so every slot stays inside
     // [0, n) until the host reports the error
     const uint32_t g = valid && group[i] < G ? group[i] : 0;
+    // the round's lengths are loaded once, up front: inside the leader loop below a load would be
+    // waited for once per distinct group of the round (~60 at G = 289)
+    const uint64_t len = valid ? off[i + 1] - off[i] : 0;
     uint64_t todo = __ballot(valid);
     while (todo) {
       const int leader = __ffsll((unsigned long long)todo) - 1;
@@ -95,7 +98,6 @@ __global__ __launch_bounds__(256) void k_grp_scatter(const uint32_t* group, cons
       if (valid && g == gl) {
         const uint32_t pos = b0 + __popcll(mask & lanemask_lt());
         members[pos] = (uint32_t)i;
-        const uint64_t len = off[i + 1] - off[i];
         el[pos] = (len << 32) | pos;
       }
       wave_sync();

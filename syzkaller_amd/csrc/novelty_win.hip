@@ -116,16 +116,7 @@ __global__ __launch_bounds__(256) void k_nw_meta(const uint32_t* pcs, const uint
       hi = max(hi, last);
     }
   }
-  lo = wave_min(lo);
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t y = __shfl_xor(hi, d, 64);
-    hi = y > hi ? y : hi;
-  }
-  if (__lane_id() == 0) {
-    atomicMin(&span[0], lo);
-    atomicMax(&span[1], hi);
-  }
+  block_span_update<256>(lo, hi, span);
 }
 
 // The walk of a direct table with its LDS updates batched: every run of a group of RBN issues its

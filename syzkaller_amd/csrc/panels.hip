@@ -79,16 +79,7 @@ __global__ __launch_bounds__(256) void k_minmax(const uint32_t* pcs, size_t L, u
     lo = min(lo, v);
     hi = max(hi, v);
   }
-  lo = wave_min(lo);
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t y = __shfl_xor(hi, d, 64);
-    hi = y > hi ? y : hi;
-  }
-  if (__lane_id() == 0) {
-    atomicMin(&span[0], lo);
-    atomicMax(&span[1], hi);
-  }
+  block_span_update<256>(lo, hi, span);
 }
 
 __global__ void k_mlen(const uint64_t* el, size_t n, uint32_t* mlen) {
