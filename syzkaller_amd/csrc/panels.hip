@@ -29,16 +29,18 @@
 namespace syz {
 
 
+// workgroups of k_span_sums: each adds its G per-group sums to gpcs with global atomics, G x blocks
+// of them on G addresses; SYZGPU_SPAN_BLOCKS overrides (A/B)
+static unsigned span_blocks() {
+  const char* e = getenv("SYZGPU_SPAN_BLOCKS");
+  return e && *e ? (unsigned)std::max(1, atoi(e)) : 512u;
+}
+
 // ---- per-entry statistics: PCs per call group and the PC span --------------------------------------
 __global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                                                    size_t n, uint32_t G, uint64_t* gpcs, uint32_t* span) {
   extern __shared__ unsigned long long lsum[];
-  __shared__ uint32_t slo, shi;
   for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) lsum[g] = 0;
-  if (threadIdx.x == 0) {
-    slo = 0xFFFFFFFFu;
-    shi = 0;
-  }
   __syncthreads();
   uint32_t lo = 0xFFFFFFFFu, hi = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -52,23 +54,9 @@ __global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const ui
       hi = max(hi, pcs[b - 1]);
     }
   }
-  lo = wave_min(lo);
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t y = __shfl_xor(hi, d, 64);
-    hi = y > hi ? y : hi;
-  }
-  if (__lane_id() == 0) {
-    atomicMin(&slo, lo);
-    atomicMax(&shi, hi);
-  }
-  __syncthreads();
+  block_span_update<256>(lo, hi, span);  // (its barrier also completes lsum)
   for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
     if (lsum[g]) atomicAdd((unsigned long long*)&gpcs[g], lsum[g]);
-  if (threadIdx.x == 0) {
-    atomicMin(&span[0], slo);
-    atomicMax(&span[1], shi);
-  }
 }
 
 // exact bounds (the slow path when some cover is not sorted)
@@ -672,7 +660,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     ProfScope ps("group_partition", s, (uint64_t)n * 28);
     group_partition_dev(a.group, a.off, n, G, gstart, members, el, err, s);
     if (n) {
-      k_span_sums<<<grid_for(n, 256, 2048), 256, G * 8, s>>>(a.pcs, a.off, a.group, n, G, gpcs, span);
+      k_span_sums<<<grid_for(n, 256, span_blocks()), 256, G * 8, s>>>(a.pcs, a.off, a.group, n, G, gpcs, span);
       SYZ_LAUNCHED();
       if (krange)
         k_slices<<<grid_for(n, 256, 4096), 256, 0, s>>>(a.pcs, a.off, members, el, a.group, n, krange, sbeg, mlen);
