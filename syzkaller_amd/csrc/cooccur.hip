@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 // 16-byte global load per thread per operand; each wave then reads its 2 + 2 operands from LDS
 // (ds_read_b128). The two 16-byte halves of row r sit swapped when bit 3 of r is set, so the lane
 // groups of a ds_read_b128 (rows {0-3, 12-15, 20-27}, ...) hit 16 distinct 4-bank sets.
-template <int TILE>
+template <int TILE, int KPB>
 __global__ __launch_bounds__(TILE* TILE / 64) __attribute__((amdgpu_waves_per_eu(4))) void k_co_gemm_lds(
     const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t T, uint32_t tiles, uint32_t ks, uint32_t nkb,
     uint32_t kb_per, int* __restrict__ P) {
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(TILE* TILE / 64) __attribute__((amdgpu_waves_per_eu
   constexpr int OPB = TILE * CO_KB;           // bytes of one operand tile per K block
   constexpr int LPT = 2 * OPB / 16 / NT;      // 16-byte loads per thread per K block (A and B)
   static_assert(LPT >= 1 && (2 * OPB / 16) % NT == 0, "staging split");
-  __shared__ __align__(16) int8_t sm[2][2 * OPB];  // [buffer][A tile | B tile]
+  __shared__ __align__(16) int8_t sm[2][KPB][2 * OPB];  // [buffer][K block of the stage][A tile | B tile]
   uint32_t t, kg;
   if (ks % 8 == 0) {
     const uint32_t j = blockIdx.x >> 3;
@@ -208,28 +208,40 @@ __global__ __launch_bounds__(TILE* TILE / 64) __attribute__((amdgpu_waves_per_eu
   for (int i = 0; i < 2; i++)
 #pragma unroll
     for (int j = 0; j < 2; j++) acc[i][j] = v16i{};
+  // KPB K blocks per stage (one barrier per stage); loads past the range's last block re-read it and
+  // their MFMAs are branched around
   if (kb0 < kb1) {
-    v4i g[LPT];
+    const uint32_t klast = kb1 - 1;
+    v4i g[KPB][LPT];
 #pragma unroll
-    for (int i = 0; i < LPT; i++) g[i] = *reinterpret_cast<const v4i*>(gsrc[i] + kb0 * kstride);
+    for (int q = 0; q < KPB; q++)
+#pragma unroll
+      for (int i = 0; i < LPT; i++)
+        g[q][i] = *reinterpret_cast<const v4i*>(gsrc[i] + (size_t)min(kb0 + q, klast) * kstride);
     int cur = 0;
-    for (uint32_t kb = kb0; kb < kb1; kb++) {
+    for (uint32_t kb = kb0; kb < kb1; kb += KPB) {
 #pragma unroll
-      for (int i = 0; i < LPT; i++) *reinterpret_cast<v4i*>(&sm[cur][soff[i]]) = g[i];
+      for (int q = 0; q < KPB; q++)
+#pragma unroll
+        for (int i = 0; i < LPT; i++) *reinterpret_cast<v4i*>(&sm[cur][q][soff[i]]) = g[q][i];
       __syncthreads();
-      if (kb + 1 < kb1) {
-        const size_t o = (size_t)(kb + 1) * kstride;
 #pragma unroll
-        for (int i = 0; i < LPT; i++) g[i] = *reinterpret_cast<const v4i*>(gsrc[i] + o);
+      for (int q = 0; q < KPB; q++)
+#pragma unroll
+        for (int i = 0; i < LPT; i++)
+          g[q][i] = *reinterpret_cast<const v4i*>(gsrc[i] + (size_t)min(kb + KPB + q, klast) * kstride);
+#pragma unroll
+      for (int q = 0; q < KPB; q++) {
+        if (kb + q >= kb1) break;
+        const v4i a0 = *reinterpret_cast<const v4i*>(&sm[cur][q][aoff[0]]);
+        const v4i a1 = *reinterpret_cast<const v4i*>(&sm[cur][q][aoff[1]]);
+        const v4i b0 = *reinterpret_cast<const v4i*>(&sm[cur][q][boff[0]]);
+        const v4i b1 = *reinterpret_cast<const v4i*>(&sm[cur][q][boff[1]]);
+        acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
       }
-      const v4i a0 = *reinterpret_cast<const v4i*>(&sm[cur][aoff[0]]);
-      const v4i a1 = *reinterpret_cast<const v4i*>(&sm[cur][aoff[1]]);
-      const v4i b0 = *reinterpret_cast<const v4i*>(&sm[cur][boff[0]]);
-      const v4i b1 = *reinterpret_cast<const v4i*>(&sm[cur][boff[1]]);
-      acc[0][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, acc[1][1], 0, 0, 0);
       cur ^= 1;
     }
   }
@@ -265,7 +277,8 @@ static uint32_t co_splits() {
 }
 
 // A/B knobs, read on every call: SYZGPU_CO_FORM=0|1|2 (direct operand loads with 128 tiles, LDS-staged
-// 128, LDS-staged 256), SYZGPU_CO_PF=1..3 (K blocks in flight in the direct form)
+// 128 (default), LDS-staged 256), SYZGPU_CO_PF=1..3 (K blocks in flight in the direct form; in form 1, >= 2
+// stages 4 K blocks per barrier instead of 2)
 static int co_env(const char* name, int def, int lo, int hi) {
   const char* e = getenv(name);
   return e && *e ? std::min(hi, std::max(lo, atoi(e))) : def;
@@ -299,7 +312,7 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
     // set of ranges per XCD) once there are enough K blocks for that
     if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
     const int pf = co_env("SYZGPU_CO_PF", 1, 1, 3);
-    const int form = co_env("SYZGPU_CO_FORM", 0, 0, 2);  // 0 direct operand loads (128 tiles), 1 LDS-staged 128, 2 LDS-staged 256
+    const int form = co_env("SYZGPU_CO_FORM", 1, 0, 2);  // default: LDS-staged, 2 K blocks per barrier  // 0 direct operand loads (128 tiles), 1 LDS-staged 128, 2 LDS-staged 256
     const uint32_t tile = form == 2 ? 256 : CO_TILE;
     const uint32_t T = Cp / tile, tiles = T * (T + 1) / 2;
     uint32_t ks = co_splits();
@@ -315,9 +328,11 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
     {
     ProfScope ps("cooc_gemm", s, 2ull * C * C * (uint64_t)nkb * CO_KB);  // (ops, not bytes)
     if (form == 2)
-      k_co_gemm_lds<256><<<tiles * ks, 1024, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
+      k_co_gemm_lds<256, 1><<<tiles * ks, 1024, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
+    else if (form == 1 && pf >= 2)
+      k_co_gemm_lds<128, 4><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     else if (form == 1)
-      k_co_gemm_lds<128><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
+      k_co_gemm_lds<128, 2><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     else if (pf == 3)
       k_co_gemm<3><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     else if (pf == 2)
