@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "corpus progs/sec: cover.Minimize + calcDynamicPrio, 1M progs, 1/2/4/8 GPUs"
-ROOF_KERNEL = "part"  # the window transpose of the raw covers
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured copy)
 
 
@@ -66,41 +66,30 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_model(name, corp, info, C):
-    """(bound, algorithmic bytes per launch) of a kernel of the step, DESIGN.md §3.
-    part: the window transpose reads every PC once and writes it once as a 4-byte element, plus the
-          per-member offsets it reads (members, mpos, off, slice: 24 B per entry);
-    pmin / pmin_small: the first-occurrence tables read every element once (4 B per PC), the groups
-          sorted by the global rounds / the small ones (their PCs are not split out: the byte model
-          uses the step's PCs in proportion to the launch time of the two).
-    prio_choice: static in + prios out + run out (16 B per matrix cell).
-    static_prio: latency-bound (a 1159 x 1159 x 395 int8 Gram per weight-class pair, ~10 MOP each)."""
-    n, pcs = corp.n, info["pcs"]
-    if name == "part":
-        return "hbm", 8 * pcs + 24 * n
-    if name == "select_out":
-        return "hbm", 10 * n
-    if name == "prio_choice":
-        return "hbm", 16 * C * C
-    return "latency", None  # gosort_* (dependent partitions), pmin (split by class below), helpers
+def dominant_kernel(kern):
+    """The step's dominant kernel: the kernel scope (named after its HIP kernel, as in the rocprofv3
+    summary) with the most time in the untimed per-kernel pass, among those carrying an algorithmic
+    byte model: k_part4 8 B per PC + 24 B per entry; k_pmin_direct / k_pmin_hash 4 B per
+    PC of the groups they walk; select_out, prio_choice as recorded. Phase scopes (gosort_*, m_big,
+    group_partition) span several kernels and are not candidates."""
+    rows = [(d["ms"], name) for name, d in kern.items() if name.startswith("k_") and d["bytes"] > 0]
+    return max(rows)[1] if rows else None
 
 
-def roofline(kern, corp, info, C):
-    """Roofline of the dominant HBM-bound kernel (time from HIP events on the launch stream)."""
-    rows = []
-    for name, d in kern.items():
-        bound, alg = kernel_model(name, corp, info, C)
-        rows.append((d["ms"], name, bound, alg, d))
-    rows.sort(reverse=True)
-    hbm = [r for r in rows if r[2] == "hbm"]
-    if not hbm:
+def roofline(name, ev, peak_gbs=None):
+    """Roofline of one kernel from its HIP events in the timed region (on its launch stream): achieved =
+    its recorded algorithmic bytes / its time; traffic = HBM bytes per launch from the committed PMC
+    passes (profiles/pmc_traffic.json, FETCH_SIZE doubled + WRITE_SIZE) when they name this kernel."""
+    d = ev.get(name)
+    if not d or not d["ms"]:
         return None
-    _, name, bound, alg, d = hbm[0]
     avg_ms = d["ms"] / d["launches"]
+    alg = d["bytes"] / d["launches"]
     ach = alg / (avg_ms * 1e-3) / 1e9
-    out = {"bound": bound, "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_ms": round(avg_ms, 4),
-           "algorithmic_bytes_per_launch": int(alg), "dominant_kernel_overall": rows[0][1]}
+    peak = peak_gbs or HBM_PEAK_GBS
+    out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
+           "frac": round(ach / peak, 4), "traffic": None, "avg_launch_ms": round(avg_ms, 4),
+           "launches_per_step": None, "algorithmic_bytes_per_launch": int(alg)}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
@@ -237,9 +226,20 @@ def main():
             e["bytes"] += int(by[i])
         return out
 
-    # timed region: HIP events (on the launch stream) around the roofline kernel only
+    # per-kernel breakdown first (untimed: events around every kernel), which names the dominant kernel
+    kern = {}
     if args.profile:
-        L.syzgpu_profile_only(ROOF_KERNEL.encode())
+        L.syzgpu_profile_only(None)
+        L.syzgpu_profile_enable(1)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        kern = read_prof()
+        L.syzgpu_profile_enable(0)
+    roof_kernel = dominant_kernel(kern) if kern else None
+    # timed region: HIP events (on the launch stream) around the dominant kernel only
+    if roof_kernel:
+        L.syzgpu_profile_only(roof_kernel.encode())
         L.syzgpu_profile_enable(1)
     if world > 1:
         dist.barrier()
@@ -251,19 +251,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    roof_ev = read_prof() if args.profile else {}
+    roof_ev = read_prof() if roof_kernel else {}
     L.syzgpu_profile_enable(0)
     job_info = job.info()
-    # per-kernel breakdown: a separate, untimed pass with events around every kernel
-    kern = {}
-    if args.profile:
-        L.syzgpu_profile_only(None)
-        L.syzgpu_profile_enable(1)
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        kern = read_prof()
-        L.syzgpu_profile_enable(0)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         sharding.allreduce(t, dist, dist.ReduceOp.MAX)
@@ -277,11 +267,10 @@ def main():
     out = None
     if rank == 0:
         # roofline of the dominant kernel: algorithmic bytes over its measured time
-        roof = None
-        if roof_ev:
-            roof = roofline(roof_ev, corp, job_info, C)
-            if roof and kern:
-                roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
+        roof = roofline(roof_kernel, roof_ev) if roof_kernel else None
+        if roof:
+            roof["launches_per_step"] = round(roof_ev[roof_kernel]["launches"] / args.steps, 2)
+            roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
         path_bytes = 4 * int(off[-1]) + 10 * total_progs + 16 * C * C  # SURVEY.md §8(d), whole job
         cpu = None
         if args.cpu_baseline and world == 1:

@@ -14,8 +14,11 @@
 //          workgroup tile, the upper triangle of tiles only (an off-diagonal tile adds its transpose
 //          too), the K blocks split over KS workgroups, each storing its partial tile; every
 //          lane's operand is 16 consecutive program bytes of one call, so A and B agree on the K
-//          order inside a step (as in static_prio.hip)
-//   reduce out = the sum of the KS partials (and its transpose), out[a][a] -= occurrences of a
+//          order inside a step (as in static_prio.hip). Default: both 128-row operand tiles of two
+//          K blocks staged through double-buffered LDS per barrier (k_co_gemm_lds<128, 2>);
+//          SYZGPU_CO_FORM=0 loads the operands per wave instead (k_co_gemm<1>)
+//   reduce out = the sum of the KS partials (and its transpose), out[a][a] -= occurrences of a, in
+//          int64; a count that cannot fit int32 is an error, never a wrapped value
 #include <algorithm>
 
 #include "pipeline.hpp"
@@ -28,10 +31,11 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int CO_KB = 32;     // programs per K block
 constexpr int CO_TILE = 128;  // output rows/columns per workgroup
 
-// one program per thread; err: 1 = call id >= C, 2 = a call occurs more than 127 times in a program
+// one program per thread; err: 1 = call id >= C, 2 = a call occurs more than 127 times in a program;
+// kbound[kb] = sum of len^2 over the K block's programs (a bound on any cell's count from the block)
 __global__ __launch_bounds__(256) void k_co_build(const uint16_t* __restrict__ calls, const uint64_t* __restrict__ off,
                                                   size_t n, int32_t C, uint32_t Cp, uint32_t* Xw,
-                                                  unsigned long long* occ, int* err) {
+                                                  unsigned long long* occ, unsigned long long* kbound, int* err) {
   extern __shared__ uint32_t lh[];
   for (int32_t c = threadIdx.x; c < C; c += blockDim.x) lh[c] = 0;
   __syncthreads();
@@ -39,6 +43,8 @@ __global__ __launch_bounds__(256) void k_co_build(const uint16_t* __restrict__ c
     const uint64_t b = off[p], e = off[p + 1];
     const uint64_t kb = p / CO_KB;
     const uint32_t kk = (uint32_t)(p % CO_KB);
+    // every count this program adds to one cell is at most cnt_a * cnt_b <= len^2: the K block's bound
+    if (e > b) atomicAdd(&kbound[kb], (unsigned long long)(e - b) * (e - b));
     if (e - b > 127) {
       // a call could repeat more than an int8 holds: count this program's repeats first
       for (uint64_t j = b; j < e; j++) {
@@ -248,12 +254,24 @@ __global__ __launch_bounds__(TILE* TILE / 64) __attribute__((amdgpu_waves_per_eu
   co_store_partial<TILE>(acc, P, ((size_t)kg * tiles + tid) * TILE * TILE, wr, wc, lane);
 }
 
+// A K range's partial cells are exact int32 while the range's sum of len^2 stays below 2^31 (every
+// cell adds at most len^2 per program); err 4 otherwise (the caller gets an error, never a wrapped count)
+__global__ void k_co_ranges(const unsigned long long* kbound, uint32_t nkb, uint32_t ks, uint32_t kb_per, int* err) {
+  for (uint32_t kg = blockIdx.x * blockDim.x + threadIdx.x; kg < ks; kg += gridDim.x * blockDim.x) {
+    unsigned long long t = 0;
+    for (uint32_t kb = kg * kb_per; kb < nkb && kb < (kg + 1) * kb_per; kb++) t += kbound[kb];
+    if (t >= (1ull << 31)) atomicOr(err, 4);
+  }
+}
+
 // out[row][col] = the sum of the KS partials of (row, col), minus the occurrences of row on the
-// diagonal; one thread per element of an upper-triangle tile, which writes the element and, off the
-// diagonal tiles, its transpose (so every element of out is written exactly once)
+// diagonal, summed in int64 (err 8 when it leaves int32); one thread per element of an upper-triangle
+// tile, which writes the element and, off the diagonal tiles, its transpose (so every element of out
+// is written exactly once)
 __global__ __launch_bounds__(256) void k_co_reduce(const int* __restrict__ P, uint32_t tiles, uint32_t ks,
                                                    uint32_t T, uint32_t tile, int32_t C,
-                                                   const unsigned long long* __restrict__ occ, int* __restrict__ out) {
+                                                   const unsigned long long* __restrict__ occ, int* __restrict__ out,
+                                                   int* err) {
   uint32_t t = blockIdx.x;
   const uint32_t e = blockIdx.y * blockDim.x + threadIdx.x;
   const size_t tt = (size_t)tile * tile;
@@ -263,11 +281,12 @@ __global__ __launch_bounds__(256) void k_co_reduce(const int* __restrict__ P, ui
   const uint32_t tx = ty + t;
   const uint32_t row = ty * tile + e / tile, col = tx * tile + e % tile;
   if ((int32_t)row >= C || (int32_t)col >= C) return;
-  int v = 0;
+  long long v = 0;
   for (uint32_t kg = 0; kg < ks; kg++) v += P[(size_t)kg * tiles * tt + base];
-  if (row == col) v -= (int)occ[row];
-  out[(size_t)row * C + col] = v;
-  if (tx != ty) out[(size_t)col * C + row] = v;
+  if (row == col) v -= (long long)occ[row];
+  if (v > 0x7FFFFFFFll || v < -0x80000000ll) atomicOr(err, 8);
+  out[(size_t)row * C + col] = (int)v;
+  if (tx != ty) out[(size_t)col * C + row] = (int)v;
 }
 
 // SYZGPU_CO_KS=k forces the K split (tests; read on every call)
@@ -276,9 +295,8 @@ static uint32_t co_splits() {
   return e && *e ? (uint32_t)std::max(1, atoi(e)) : 0u;
 }
 
-// A/B knobs, read on every call: SYZGPU_CO_FORM=0|1|2 (direct operand loads with 128 tiles, LDS-staged
-// 128 (default), LDS-staged 256), SYZGPU_CO_PF=1..3 (K blocks in flight in the direct form; in form 1, >= 2
-// stages 4 K blocks per barrier instead of 2)
+// A/B knob, read on every call: SYZGPU_CO_FORM=0 the direct form (per-wave operand loads, TA-bound:
+// profiles/r02_ab/cooccur_ab.md), 1 (default) the LDS-staged form
 static int co_env(const char* name, int def, int lo, int hi) {
   const char* e = getenv(name);
   return e && *e ? std::min(hi, std::max(lo, atoi(e))) : def;
@@ -296,14 +314,16 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
   const size_t xbytes = (size_t)std::max<uint32_t>(nkb, 1) * Cp * CO_KB;
   uint32_t* Xw = sc.get<uint32_t>("co_x", xbytes / 4 + 1);
   unsigned long long* occ = sc.get<unsigned long long>("co_occ", (size_t)C + 1);
+  unsigned long long* kbound = sc.get<unsigned long long>("co_kbound", (size_t)nkb + 1);
   int* err = sc.get<int>("co_err", 2);
   SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
+  SYZ_HIP(hipMemsetAsync(kbound, 0, ((size_t)nkb + 1) * 8, s));
   SYZ_HIP(hipMemsetAsync(occ, 0, ((size_t)C + 1) * 8, s));
   {
     ProfScope ps("cooc_build", s, xbytes);
     SYZ_HIP(hipMemsetAsync(Xw, 0, xbytes, s));
     if (n) {
-      k_co_build<<<grid_for(n, 256, 1024), 256, (size_t)C * 4, s>>>(calls, off, n, C, Cp, Xw, occ, err);
+      k_co_build<<<grid_for(n, 256, 1024), 256, (size_t)C * 4, s>>>(calls, off, n, C, Cp, Xw, occ, kbound, err);
       SYZ_LAUNCHED();
     }
   }
@@ -311,9 +331,8 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
     // K split: about two workgroups per CU (all resident at once), in multiples of 8 K ranges (one
     // set of ranges per XCD) once there are enough K blocks for that
     if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
-    const int pf = co_env("SYZGPU_CO_PF", 1, 1, 3);
-    const int form = co_env("SYZGPU_CO_FORM", 1, 0, 2);  // default: LDS-staged, 2 K blocks per barrier  // 0 direct operand loads (128 tiles), 1 LDS-staged 128, 2 LDS-staged 256
-    const uint32_t tile = form == 2 ? 256 : CO_TILE;
+    const int form = co_env("SYZGPU_CO_FORM", 1, 0, 1);
+    const uint32_t tile = CO_TILE;
     const uint32_t T = Cp / tile, tiles = T * (T + 1) / 2;
     uint32_t ks = co_splits();
     if (!ks) {
@@ -327,22 +346,16 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
     int* P = sc.get<int>("co_part", (size_t)ks * tiles * tile * tile);
     {
     ProfScope ps("cooc_gemm", s, 2ull * C * C * (uint64_t)nkb * CO_KB);  // (ops, not bytes)
-    if (form == 2)
-      k_co_gemm_lds<256, 1><<<tiles * ks, 1024, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
-    else if (form == 1 && pf >= 2)
-      k_co_gemm_lds<128, 4><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
-    else if (form == 1)
+    if (form == 1)
       k_co_gemm_lds<128, 2><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
-    else if (pf == 3)
-      k_co_gemm<3><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
-    else if (pf == 2)
-      k_co_gemm<2><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     else
       k_co_gemm<1><<<tiles * ks, 256, 0, s>>>(Xb, C, Cp, T, tiles, ks, nkb, kb_per, P);
     SYZ_LAUNCHED();
     }
     ProfScope ps("cooc_reduce", s, (uint64_t)ks * tiles * tile * tile * 4 + (uint64_t)C * C * 4);
-    k_co_reduce<<<dim3(tiles, tile * tile / 256), 256, 0, s>>>(P, tiles, ks, T, tile, C, occ, out);
+    k_co_ranges<<<grid_for(ks, 256, 64), 256, 0, s>>>(kbound, nkb, ks, kb_per, err);
+    SYZ_LAUNCHED();
+    k_co_reduce<<<dim3(tiles, tile * tile / 256), 256, 0, s>>>(P, tiles, ks, T, tile, C, occ, out, err);
     SYZ_LAUNCHED();
   }
   int* h = c.pinned.get<int>(2);
@@ -350,6 +363,8 @@ void call_cooccurrence_dev(const uint16_t* calls, const uint64_t* off, size_t n,
   SYZ_HIP(hipStreamSynchronize(s));
   if (h[0] & 1) fail(SYZGPU_EINVAL, "call id >= C");
   if (h[0] & 2) fail(SYZGPU_EINVAL, "a call occurs more than 127 times in one program (int8 operand)");
+  if (h[0] & 4) fail(SYZGPU_EINVAL, "a K range's sum of len^2 reaches 2^31: its int32 partial counts could wrap");
+  if (h[0] & 8) fail(SYZGPU_EINVAL, "a co-occurrence count exceeds int32");
 }
 
 }  // namespace syz

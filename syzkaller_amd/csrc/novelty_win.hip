@@ -491,7 +491,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   uint64_t* gchunk = sc.get<uint64_t>("nw_gchunk", G + 1);
   uint64_t* gdesc = sc.get<uint64_t>("nw_gdesc", G + 1);
   uint16_t* desc = sc.get<uint16_t>("nw_desc", desc_bound + 1);
-  uint32_t* elems = sc.get<uint32_t>("pm_elems", total + 1);
+  uint32_t* elems = sc.get<uint32_t>("pm_elems", elem_bound(total, chunk_bound));
   uint32_t* kbits = sc.get<uint32_t>("nw_kbits", kw + 1);
   uint32_t* wcount = sc.get<uint32_t>("nw_wcount", slots + 1);
   uint64_t* wpos = sc.get<uint64_t>("nw_wpos", slots + 1);

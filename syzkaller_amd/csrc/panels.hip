@@ -70,159 +70,33 @@ __global__ __launch_bounds__(256) void k_minmax(const uint32_t* pcs, size_t L, u
   block_span_update<256>(lo, hi, span);
 }
 
+// PCs of each call group this job reads (its members' slices): the exact byte model of the kernels
+__global__ void k_gslice(const uint64_t* gstart, const uint64_t* mpos, uint32_t G, uint64_t* gsl) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x)
+    gsl[g] = mpos[gstart[g + 1]] - mpos[gstart[g]];
+}
+
 __global__ void k_mlen(const uint64_t* el, size_t n, uint32_t* mlen) {
   for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x)
     mlen[m] = (uint32_t)(el[m] >> 32);
 }
 
-// ---- P: transpose the covers into windows ---------------------------------------------------------
-__global__ __launch_bounds__(PP_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_part(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ members,
-                                                      const uint64_t* __restrict__ mpos,
-                                                      const uint32_t* __restrict__ sbeg, const PChunk* chunks,
-                                                      const uint64_t* nchunks_dev, const PGroup* pg,
-                                                      const uint64_t* gchunk, const uint64_t* gdesc, uint32_t lo,
-                                                      uint32_t* __restrict__ elems, uint16_t* __restrict__ desc,
-                                                      int* err, int dbg) {
-  __shared__ uint32_t obuf[PCAP];
-  __shared__ uint32_t hist[WMAX + 1];
-  __shared__ uint32_t tpre[MEMB + 1];   // tiles before member m
-  __shared__ uint32_t mlo[MEMB], mhi[MEMB];  // the member's PCs inside this chunk, block coordinates
-  __shared__ uint64_t mraw[MEMB];            // off[entry] - block coordinate of the member's first PC
-  __shared__ uint32_t red[PP_WAVES + 1];
-  __shared__ uint4 tinfo[PCAP / 64 + MEMB];
-  const uint64_t nch = *nchunks_dev;
-  const int wv = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {  // one chunk per workgroup (grid = chunk bound)
-    const PChunk ch = chunks[c];
-    const PGroup gp = pg[ch.g];
-    const uint32_t S = gp.S, W = gp.W;
-    const uint32_t cb = ch.sub, ce = ch.sub + ch.len;
-    // member ranges and tiles
-    if (threadIdx.x < 64) {
-      const uint32_t m = threadIdx.x;
-      uint32_t nt = 0;
-      if (m < ch.nmem) {
-        const uint64_t p0 = mpos[ch.mb], a = mpos[ch.mb + m] - p0, b = mpos[ch.mb + m + 1] - p0;
-        const uint32_t x = (uint32_t)max<uint64_t>(a, cb), y = (uint32_t)min<uint64_t>(b, ce);
-        mlo[m] = x;
-        mhi[m] = y;
-        mraw[m] = off[members[ch.mb + m]] + (sbeg ? sbeg[ch.mb + m] : 0u) - a;
-        nt = y > x ? (y - x + 63) / 64 : 0;
-      }
-      const uint32_t inc = wave_incl_scan<uint32_t>(nt);
-      tpre[m] = inc - nt;
-      if (m == 63) tpre[64] = inc;
-    }
-    for (uint32_t i = threadIdx.x; i <= W; i += PP_BLOCK) hist[i] = 0;
-    __syncthreads();
-    const uint32_t ntiles = tpre[64];
-    const uint32_t nm = ch.nmem;
-    // tile table: per 64-PC tile its member, valid lanes and raw address (built once per chunk, so the
-    // passes read one 16-byte broadcast per tile)
-    for (uint32_t t = threadIdx.x; t < ntiles; t += PP_BLOCK) {
-      uint32_t lo_m = 0, hi_m = nm;  // largest m < nm with tpre[m] <= t
-      while (hi_m - lo_m > 1) {
-        const uint32_t mid = (lo_m + hi_m) >> 1;
-        if (tpre[mid] <= t)
-          lo_m = mid;
-        else
-          hi_m = mid;
-      }
-      const uint32_t m = lo_m;
-      const uint32_t q0 = mlo[m] + (t - tpre[m]) * 64;
-      const uint64_t base = mraw[m] + q0;
-      tinfo[t] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), min(64u, mhi[m] - q0) | (m << 8), 0u);
-    }
-    __syncthreads();
-    auto tile = [&](uint32_t t, uint32_t& m, uint64_t& addr) -> bool {
-      const uint4 ti = tinfo[t];
-      m = ti.z >> 8;
-      addr = (((uint64_t)ti.y << 32) | ti.x) + lane;
-      return lane < (ti.z & 0xFFu);
-    };
-    // pass 1: window histogram (PP_U tiles per wave in flight)
-    for (uint32_t t0 = wv; t0 < ntiles; t0 += PP_WAVES * PP_U) {
-      uint32_t v[PP_U];
-      bool ok[PP_U];
-#pragma unroll
-      for (int k = 0; k < PP_U; k++) {
-        const uint32_t t = t0 + PP_WAVES * k;
-        uint32_t m;
-        uint64_t ad;
-        ok[k] = t < ntiles && tile(t, m, ad);
-        v[k] = ok[k] ? pcs[ad] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < PP_U; k++) {
-        if (!ok[k]) continue;
-        const uint32_t w = (v[k] - lo) >> S;
-        if (w < W)
-          atomicAdd(&hist[w], 1u);
-        else
-          atomicOr(err, 1);  // outside [lo, hi]: an unsorted cover; redone on exact bounds
-      }
-    }
-    __syncthreads();
-    // window starts (exclusive scan) -> desc row and cursors
-    uint16_t* drow = desc + gdesc[ch.g] + (c - gchunk[ch.g]) * (uint64_t)(W + 1);
-    {
-      uint32_t run = 0;
-      for (uint32_t b0 = 0; b0 <= W; b0 += PP_BLOCK) {
-        const uint32_t i = b0 + threadIdx.x;
-        const uint32_t x = i < W ? hist[i] : 0;
-        uint32_t tot;
-        const uint32_t pre = block_excl_scan<PP_BLOCK>(x, red, &tot) + run;
-        if (i <= W) {
-          drow[i] = (uint16_t)pre;
-          hist[i] = pre;
-        }
-        run += tot;
-      }
-    }
-    __syncthreads();
-    // pass 2 (the chunk again, from L2): element = offset in window | member tag, window-major in LDS
-    const uint32_t omask = (1u << S) - 1;
-    for (uint32_t t0 = wv; t0 < ntiles && !(dbg & 8); t0 += PP_WAVES * PP_U) {
-      uint32_t v[PP_U], mm[PP_U];
-      bool ok[PP_U];
-#pragma unroll
-      for (int k = 0; k < PP_U; k++) {
-        const uint32_t t = t0 + PP_WAVES * k;
-        uint64_t ad;
-        ok[k] = t < ntiles && tile(t, mm[k], ad);
-        v[k] = ok[k] ? pcs[ad] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < PP_U; k++) {
-        if (!ok[k]) continue;
-        const uint32_t d = v[k] - lo, w = d >> S;
-        if (w < W) obuf[atomicAdd(&hist[w], 1u)] = (d & omask) | (mm[k] << S);
-      }
-    }
-    __syncthreads();
-    uint32_t* dst = elems + ch.elem;
-    if (!(dbg & 16))
-      for (uint32_t i = threadIdx.x; i < ch.len; i += PP_BLOCK) dst[i] = obuf[i];
-    __syncthreads();
-  }
-}
-
-
 // Winners of a window table -> sel8[rank] = 1 with plain byte stores (no atomics: a byte written by
 // several tables is written with the same value). Ranks of call g lie in [gbase, gbase + ng); the
 // first BMW*32 of them are deduplicated through an LDS bitmap first, so each kept input costs one
 // store per table, not one per key it wins.
-template <uint32_t BMW>
+struct RankIdentity {
+  __device__ uint32_t operator()(uint32_t v) const { return v; }
+};
+template <uint32_t BMW, class D = RankIdentity>
 __device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
-                                                  uint32_t* bm, uint8_t* sel8) {
+                                                  uint32_t* bm, uint8_t* sel8, D decode = D{}) {
   const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BMW * 32, ng);
   const uint32_t words = (span + 31) / 32;
   for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
-    const uint32_t r = tab[i];
+    const uint32_t r = decode(tab[i]);
     if (r == RANK_NONE) continue;
     const uint64_t lr = (uint64_t)r - gbase;
     if (lr < span) {
@@ -245,132 +119,34 @@ __device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t 
 }
 
 
-// The same walk balanced by element tiles instead of runs: a window's runs are taken RUNB at a time;
-// their 64-element tiles are numbered (a workgroup scan in LDS) and every wave streams a contiguous
-// share of the tiles, TT tiles in flight per lane (one element load and one 256-byte rank-block load
-// each, independent), so a window of a few long runs (the sparse calls) keeps every wave and as many
-// loads in flight as one of thousands of short runs (the dense ones). `scratch` holds RUNB * 20 bytes
-// of LDS (the caller's winner bitmap, unused until the emit).
-constexpr uint32_t RUNB = 512;
-constexpr int TT = 8;
-template <class F>
-__device__ __forceinline__ void for_window_tiles(const PItem it, const PChunk* __restrict__ chunks,
-                                                 const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
-                                                 const uint16_t* __restrict__ desc,
-                                                 const uint32_t* __restrict__ elems,
-                                                 const uint32_t* __restrict__ rank_of_member, uint32_t nmem_total,
-                                                 uint32_t* scratch, uint32_t* red, F f) {
-  const uint32_t g = it.g, w = it.w;
-  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
-  const uint32_t W = pg[g].W, S = pg[g].S;
-  const uint32_t omask = (1u << S) - 1;
-  const uint16_t* d0 = desc + gdesc[g] + w;
-  uint64_t* relem = reinterpret_cast<uint64_t*>(scratch);  // RUNB (scratch is 16-byte aligned)
-  uint32_t* rstart = scratch + 2 * RUNB;                     // RUNB + 1
-  uint32_t* rlen = rstart + RUNB + 1;                        // RUNB
-  uint32_t* rmb = rlen + RUNB;                               // RUNB
-  const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  const uint32_t last_m = nmem_total ? nmem_total - 1 : 0;
-  for (uint64_t b0 = c0; b0 < c1; b0 += RUNB) {
-    const uint32_t nb = (uint32_t)min<uint64_t>(RUNB, c1 - b0);
-    uint32_t tiles = 0;
-    if (threadIdx.x < nb) {
-      const uint64_t c = b0 + threadIdx.x;
-      const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
-      const uint32_t s0 = d[0], len = (uint32_t)d[1] - s0;
-      rlen[threadIdx.x] = len;
-      relem[threadIdx.x] = chunks[c].elem + s0;
-      rmb[threadIdx.x] = chunks[c].mb;
-      tiles = (len + 63) / 64;
-    }
-    uint32_t T;
-    const uint32_t pre = block_excl_scan<1024>(tiles, red, &T);
-    if (threadIdx.x < nb) rstart[threadIdx.x] = pre;
-    if (threadIdx.x == 0) rstart[nb] = T;
-    __syncthreads();
-    // this wave's tiles [ta, tb), 64 at a time: lane l finds the run of tile tb0 + l (a binary search
-    // in LDS, all lanes at once), then the tiles are broadcast from their lanes, TT loads in flight
-    const uint32_t ta = (uint32_t)((uint64_t)T * wv / nw), tb = (uint32_t)((uint64_t)T * (wv + 1) / nw);
-    for (uint32_t tb0 = ta; tb0 < tb; tb0 += 64) {
-      const uint32_t t = tb0 + lane;
-      uint32_t r = 0, hi = nb;  // largest r < nb with rstart[r] <= t
-      while (hi - r > 1) {
-        const uint32_t mid = (r + hi) >> 1;
-        if (rstart[mid] <= t)
-          r = mid;
-        else
-          hi = mid;
-      }
-      const uint32_t k = (t - rstart[r]) * 64;
-      const uint32_t tcnt = t < tb ? min(64u, rlen[r] - k) : 0u;
-      const uint64_t taddr = relem[r] + k;
-      const uint32_t tmb = rmb[r];
-      const uint32_t ntl = min(64u, tb - tb0);
-      for (uint32_t u0 = 0; u0 < ntl; u0 += TT) {
-        uint32_t e[TT], rk[TT], cnt[TT];
-#pragma unroll
-        for (int u = 0; u < TT; u++) {
-          const uint32_t jl = u0 + u;  // wave-uniform lane index
-          cnt[u] = jl < ntl ? (uint32_t)__builtin_amdgcn_readlane((int)tcnt, (int)jl) : 0u;
-          e[u] = 0;
-          rk[u] = 0;
-          if (cnt[u]) {
-            const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(taddr >> 32), (int)jl)
-                                << 32) |
-                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)taddr, (int)jl);
-            const uint32_t mb = (uint32_t)__builtin_amdgcn_readlane((int)tmb, (int)jl);
-            rk[u] = rank_of_member[min(mb + lane, last_m)];
-            if (lane < cnt[u]) e[u] = elems[a + lane];
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < TT; u++) {
-          const uint32_t R = (uint32_t)__shfl((int)rk[u], (int)(e[u] >> S), 64);
-          if (lane < cnt[u]) f(e[u] & omask, R);
-        }
-      }
-    }
-    __syncthreads();  // the run table is rewritten by the next batch
-  }
-}
-
-static bool pmin_tiles() {
-  static const bool v = getenv("SYZGPU_PMIN_TILES") && atoi(getenv("SYZGPU_PMIN_TILES")) != 0;
-  return v;
-}
-
-template <bool TILES>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_DIRECT_WPE, 8))) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
+// Dense windows: a 2^DS-entry direct min table in LDS (128 KB: one workgroup per CU), the packed walk
+// (panels_dev.hpp), then the winners as byte stores; the walk's LDS scratch is the emit's rank bitmap.
+__global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
                                                       const uint64_t* gchunk, const uint64_t* gdesc,
                                                       const PGroup* pg, const uint16_t* __restrict__ desc,
                                                       const uint32_t* __restrict__ elems,
                                                       const uint32_t* __restrict__ rank_of_member,
-                                                      uint32_t nmem_total, const uint64_t* gstart,
-                                                      uint8_t* sel8, int dbg) {
-  __shared__ uint32_t tab[1u << DS];
-  __shared__ __align__(16) uint32_t bm[PBM_WORDS];  // also the tile walk's run table until the emit
-  __shared__ uint32_t red[1024 / 64 + 1];
-  static_assert(PBM_WORDS >= RUNB * 5 + 1, "run table in the bitmap");
+                                                      const uint64_t* gstart, uint8_t* sel8, int dbg) {
+  __shared__ __align__(16) uint32_t tab[1u << DS];
+  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];
+  __shared__ uint64_t red64[1024 / 64 + 1];
+  SYZ_STAMP(1, 0);
   const PItem it = items[blockIdx.x];
-  for (uint32_t i = threadIdx.x; i < (1u << DS); i += 1024) tab[i] = RANK_NONE;
+  {
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+    const uint4 none4 = make_uint4(RANK_NONE, RANK_NONE, RANK_NONE, RANK_NONE);
+    for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
+  }
   __syncthreads();
-  uint32_t acc = 0;
-  auto upd = [&](uint32_t o, uint32_t R) {
-    if (dbg & 1)
-      acc ^= o * 31 + R;
-    else if (tab[o] > R)
-      atomicMin(&tab[o], R);
-  };
-  if constexpr (TILES)
-    for_window_tiles(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, bm, red, upd);
-  else
-    for_window_elems<SYZ_DIRECT_RB>(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, upd);
+  SYZ_STAMP(1, 1);
+  for_window_packed<SYZ_PK_U, false>(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, wsc, red64,
+                                     [&](uint32_t o, uint32_t R) { atomicMin(&tab[o], R); });
   __syncthreads();
-  if (acc == 0x9E3779B9u) sel8[0] = 1;
+  SYZ_STAMP(1, 2);
   if (dbg & 2) return;
   const uint64_t gb = gstart[it.g];
-  emit_winner_bytes<PBM_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, bm, sel8);
+  emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, wsc, sel8);
+  SYZ_STAMP(1, 3);
 }
 
 // PCs of one (call, window) over all its chunks' runs (metadata only)
@@ -396,65 +172,84 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 // marked by a finished round stays valid (marks are idempotent stores of exact winners).
 // 72 KB of LDS at 8192 slots: two workgroups per CU (registers held to 64 per lane, 4 runs in
 // flight per wave), so one window's table init and emit overlap the other's loads
-#ifndef SYZ_HASH_RB
-#define SYZ_HASH_RB 4
+#ifndef SYZ_PK_HU
+#define SYZ_PK_HU 4
 #endif
-#ifndef SYZ_HASH_WPE
-#define SYZ_HASH_WPE 8
-#endif
-template <bool TILES>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_HASH_WPE, 8))) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
+// Sparse windows: open addressing keyed by the window offset, kept at most half full: a window with
+// more than HCAP PCs is done in R = ceil(PCs / HCAP) rounds, each taking the keys of one residue of
+// another hash (so each round holds at most about HCAP distinct keys). A probe run longer than
+// HPROBE means the table is full after all: every round is redone with twice as many; a winner
+// marked by a finished round stays valid (marks are idempotent stores of exact winners).
+// PACKED (call groups of < 2^13 entries, windows of <= 2^19 addresses): a slot is one u32,
+// offset << 13 | rank - the group's first rank, inserted by CAS and lowered by atomicMin (equal high
+// bits, so the min is the min rank), 16K slots in the 64 KB of the 8K key/value pairs.
+template <bool PACKED>
+__global__ __launch_bounds__(1024) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
                                                     const uint64_t* gchunk, const uint64_t* gdesc,
                                                     const PGroup* pg, const uint16_t* __restrict__ desc,
                                                     const uint32_t* __restrict__ elems,
                                                     const uint32_t* __restrict__ rank_of_member,
-                                                    uint32_t nmem_total, const uint64_t* gstart, uint8_t* sel8,
-                                                    int dbg) {
-  __shared__ uint32_t keys[HS];
-  __shared__ uint32_t vals[HS];
-  __shared__ uint32_t bm[HBM_WORDS];
-  __shared__ __align__(16) uint32_t rtab[RUNB * 5 + 1];  // the tile walk's run table
-  __shared__ uint32_t red[1024 / 64 + 1];
+                                                    const uint64_t* gstart, uint8_t* sel8, int dbg) {
+  constexpr uint32_t NS = PACKED ? PHS : HS;  // slots
+  constexpr uint32_t CAP = PACKED ? PHCAP : HCAP;
+  __shared__ uint32_t tabs[2 * HS];
+  static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
+  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];  // the walk's scratch, then the emit bitmap
+  __shared__ uint64_t red64[1024 / 64 + 1];
   __shared__ int full;
+  uint32_t* keys = tabs;       // PACKED: the slots
+  uint32_t* vals = tabs + HS;
   const PItem it = items[blockIdx.x];
   const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
-  const uint32_t E = window_elem_count(it, gchunk, gdesc, pg, desc, red);
+  const uint32_t E = window_elem_count(it, gchunk, gdesc, pg, desc, reinterpret_cast<uint32_t*>(red64));
   if (E == 0) return;
-  uint32_t R = (E + HCAP - 1) / HCAP;
+  uint32_t R = (E + CAP - 1) / CAP;
   for (uint32_t round = 0; round < R;) {
-    for (uint32_t i = threadIdx.x; i < HS; i += 1024) {
-      keys[i] = 0xFFFFFFFFu;
-      vals[i] = RANK_NONE;
-    }
+    for (uint32_t i = threadIdx.x; i < 2 * HS; i += 1024) tabs[i] = (PACKED || i < HS) ? 0xFFFFFFFFu : RANK_NONE;
     if (threadIdx.x == 0) full = 0;
     __syncthreads();
     const uint32_t RR = R, rr = round;
     uint32_t acc = 0;
-    auto upd = [&](uint32_t o, uint32_t Rk) {
-                       if (dbg & 64) {
-                         acc ^= o * 31 + Rk;
-                         return;
-                       }
-                       if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
-                       uint32_t h = hslot(o);
-                       for (uint32_t probes = 0; probes < HPROBE; probes++) {
-                         uint32_t k = keys[h];
-                         if (k == 0xFFFFFFFFu) {
-                           k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
-                           if (k == 0xFFFFFFFFu) k = o;
-                         }
-                         if (k == o) {
-                           if (vals[h] > Rk) atomicMin(&vals[h], Rk);
-                           return;
-                         }
-                         h = (h + 1) & (HS - 1);
-                       }
-                       full = 1;
-                     };
-    if constexpr (TILES)
-      for_window_tiles(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, rtab, red, upd);
-    else
-      for_window_elems<SYZ_HASH_RB>(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, nmem_total, 16, upd);
+    for_window_packed<SYZ_PK_HU, false>(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, wsc, red64,
+                                       [&](uint32_t o, uint32_t Rk) {
+                                         if (Rk == RANK_NONE) return;  // a lane past the window
+                                         if (dbg & 64) {
+                                           acc ^= o * 31 + Rk;
+                                           return;
+                                         }
+                                         if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
+                                         if constexpr (PACKED) {
+                                           const uint32_t pk = (o << PK_RBITS) | (uint32_t)(Rk - gb);
+                                           uint32_t h = (o * 0x9E3779B1u) >> (32 - PHS_BITS);
+                                           for (uint32_t probes = 0; probes < HPROBE; probes++) {
+                                             uint32_t k = keys[h];
+                                             if (k == 0xFFFFFFFFu) {
+                                               k = atomicCAS(&keys[h], 0xFFFFFFFFu, pk);
+                                               if (k == 0xFFFFFFFFu) return;
+                                             }
+                                             if ((k >> PK_RBITS) == o) {
+                                               if (k > pk) atomicMin(&keys[h], pk);
+                                               return;
+                                             }
+                                             h = (h + 1) & (PHS - 1);
+                                           }
+                                         } else {
+                                           uint32_t h = hslot(o);
+                                           for (uint32_t probes = 0; probes < HPROBE; probes++) {
+                                             uint32_t k = keys[h];
+                                             if (k == 0xFFFFFFFFu) {
+                                               k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
+                                               if (k == 0xFFFFFFFFu) k = o;
+                                             }
+                                             if (k == o) {
+                                               atomicMin(&vals[h], Rk);
+                                               return;
+                                             }
+                                             h = (h + 1) & (HS - 1);
+                                           }
+                                         }
+                                         full = 1;
+                                       });
     if (acc == 0x9E3779B9u) sel8[0] = 1;
     __syncthreads();
     if (full) {
@@ -463,7 +258,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SYZ_HASH_W
       __syncthreads();
       continue;
     }
-    emit_winner_bytes<HBM_WORDS>(vals, HS, gb, ng, bm, sel8);
+    if constexpr (PACKED) {
+      const uint32_t g32 = (uint32_t)gb;  // ranks fit 32 bits (n < 2^32)
+      emit_winner_bytes<PK_SCRATCH_WORDS>(keys, NS, gb, ng, wsc, sel8, [g32](uint32_t v) {
+        return v == 0xFFFFFFFFu ? RANK_NONE : g32 + (v & ((1u << PK_RBITS) - 1));
+      });
+    } else {
+      emit_winner_bytes<PK_SCRATCH_WORDS>(vals, HS, gb, ng, wsc, sel8);
+    }
     round++;
   }
 }
@@ -530,7 +332,7 @@ __global__ void k_slices(const uint32_t* pcs, const uint64_t* off, const uint32_
 
 // ---- host orchestration ---------------------------------------------------------------------------------
 
-void plan_windows(uint64_t span, const uint64_t* gpcs, uint32_t G, std::vector<PGroup>& pg) {
+void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, uint32_t G, std::vector<PGroup>& pg) {
   pg.assign(G, PGroup{});
   auto nwin = [&](uint32_t S) { return (span + (1ull << S) - 1) >> S; };
   uint32_t smin = DS;
@@ -545,30 +347,28 @@ void plan_windows(uint64_t span, const uint64_t* gpcs, uint32_t G, std::vector<P
       p.mode = PMODE_DIRECT;
       continue;
     }
-    // sparse: the widest window (<= 2^SMAX addresses) that still gives about HTARGET PCs per window
-    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(WMAX, (E + HTARGET - 1) / HTARGET));
+    // sparse: the widest window (<= 2^SMAX addresses) that still gives about HTARGET PCs per window;
+    // a group of < 2^13 entries whose windows fit 2^19 addresses takes the packed table (2x the PCs)
+    const bool small = gstart[g + 1] - gstart[g] < (1u << PK_RBITS);
+    const uint64_t tgt = small ? PHTARGET : HTARGET;
+    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(WMAX, (E + tgt - 1) / tgt));
     uint32_t S = std::max(smin, DS);
     while (S < SMAX && nwin(S + 1) >= want) S++;
     if (S > SMAX) S = SMAX;
+    if (small && S > PSMAX && nwin(PSMAX) <= WMAX) S = PSMAX;
     p.S = S;
     p.W = (uint32_t)std::max<uint64_t>(1, nwin(S));
-    p.mode = PMODE_HASH;
+    p.mode = small && S <= PSMAX ? PMODE_PACKED : PMODE_HASH;
   }
 }
 
 static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span);
 
 // diagnostic switches (SYZGPU_PM_DBG, timing experiments only; results are wrong when set):
-// 1 = direct tables not updated, 2 = no winner emit, 4 = no open-addressing windows,
-// 8 = P without its second pass, 16 = P without the element stores, 64 = sparse windows walked but
+// 2 = no winner emit (direct windows), 4 = no open-addressing windows, 64 = sparse windows walked but
 // not probed
-static unsigned part_grid() {
-  static const unsigned v = getenv("SYZGPU_PART_GRID") ? (unsigned)atoi(getenv("SYZGPU_PART_GRID")) : (1u << 30);
-  return v ? v : 1u;
-}
-
 static int part_kind() {
-  static const int v = getenv("SYZGPU_PART") ? atoi(getenv("SYZGPU_PART")) : 3;
+  static const int v = getenv("SYZGPU_PART") ? atoi(getenv("SYZGPU_PART")) : 4;
   return v;
 }
 
@@ -639,6 +439,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint32_t* mlen = sc.get<uint32_t>("pm_mlen", n + 1);
   uint32_t* sbeg = a.key_lo ? sc.get<uint32_t>("pm_sbeg", n + 1) : nullptr;
   uint64_t* mpos = sc.get<uint64_t>("pm_mpos", n + 1);
+  uint64_t* gsl = sc.get<uint64_t>("pm_gsl", G + 1);
   SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
   SYZ_HIP(hipMemsetAsync(gpcs, 0, (G + 1) * 8, s));
   uint32_t* hinit = c.pinned.get<uint32_t>(16);
@@ -669,15 +470,19 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       SYZ_LAUNCHED();
     }
     exclusive_scan_u32(mlen, mpos, n, s);
+    k_gslice<<<grid_for(G, 256, 64), 256, 0, s>>>(gstart, mpos, G, gsl);
+    SYZ_LAUNCHED();
   }
-  uint64_t* hbuf = c.pinned.get<uint64_t>(2 * (size_t)G + 8);
+  uint64_t* hbuf = c.pinned.get<uint64_t>(3 * (size_t)G + 8);
   SYZ_HIP(hipMemcpyAsync(hbuf, gstart, (G + 1) * 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipMemcpyAsync(hbuf + G + 1, gpcs, G * 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipMemcpyAsync(hbuf + 2 * G + 1, span, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipMemcpyAsync(hbuf + 2 * G + 2, err, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hbuf + 2 * G + 3, gsl, G * 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   if (*reinterpret_cast<int*>(hbuf + 2 * G + 2)) fail(SYZGPU_EINVAL, "group id >= ngroups");
   std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
+  const uint64_t* hsl = hbuf + 2 * G + 3;  // PCs this job reads per group (key parts: the slices)
   uint32_t lo = reinterpret_cast<uint32_t*>(hbuf + 2 * G + 1)[0], hi = reinterpret_cast<uint32_t*>(hbuf + 2 * G + 1)[1];
   if (exact_span) {
     lo = exact_span[0];
@@ -688,7 +493,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   const uint64_t spanw = (uint64_t)hi - lo + 1;
   // ---- plan: window size per call group, blocks, chunk bound, work items ----
   std::vector<PGroup> hpg;
-  plan_windows(spanw, hpcs.data(), G, hpg);
+  plan_windows(spanw, hpcs.data(), hstart.data(), G, hpg);
   std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
   uint64_t chunk_bound = 0, desc_bound = 0, total_pcs = 0;
   for (uint32_t g = 0; g < G; g++) {
@@ -699,7 +504,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     const uint64_t cb = nb + (hpcs[g] + PCAP - 1) / PCAP;  // a key part holds at most the whole group
     chunk_bound += cb;
     desc_bound += cb * (hpg[g].W + 1);
-    total_pcs += hpcs[g];
+    total_pcs += hsl[g];
   }
   const uint32_t B = hgblock[G];
   // work items: (call, window), the big groups (sorted by the global rounds) first, each class by
@@ -710,7 +515,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
     return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W;
   });
-  std::vector<PItem> items[2][2];  // [big][mode]
+  std::vector<PItem> items[2][3];  // [big][mode]
+  uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};  // PCs the items of each class walk (the M byte models)
   for (uint32_t g : order) {
     if (!hpcs[g]) continue;
     uint32_t w0 = 0, w1 = hpg[g].W;
@@ -722,6 +528,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     }
     auto& v = items[is_big(g) ? 1 : 0][hpg[g].mode];
     for (uint32_t w = w0; w < w1; w++) v.push_back(PItem{g, w});
+    item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
   }
   PGroup* dpg = sc.get<PGroup>("pm_pg", G + 1);
   uint32_t* dgblock = sc.get<uint32_t>("pm_gblock", G + 1);
@@ -762,7 +569,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint64_t* gchunk = sc.get<uint64_t>("pm_gchunk", G + 1);
   uint64_t* gdesc = sc.get<uint64_t>("pm_gdesc", G + 1);
   uint16_t* desc = sc.get<uint16_t>("pm_desc", desc_bound + 1);
-  uint32_t* elems = sc.get<uint32_t>("pm_elems", total_pcs + 1);
+  uint32_t* elems = sc.get<uint32_t>("pm_elems", elem_bound(total_pcs, chunk_bound));
   if (B) {
     k_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, gstart, mpos, nsub);
     SYZ_LAUNCHED();
@@ -798,40 +605,56 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_HIP(hipEventRecord(c.ev_part0, s));
   SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
   if (chunk_bound) {
-    ProfScope ps("part", pq, total_pcs * 8 + (uint64_t)n * 24);
+    // byte model: every PC read once and written once as a 4-byte element, plus 24 B of member
+    // metadata per entry (members, mpos, off, slice)
+    ProfScope ps(part_kind() == 3 ? "k_part3" : "k_part4", pq, total_pcs * 8 + (uint64_t)n * 24);
     // one workgroup per chunk: workgroups retire all along, so the Go sort's kernels (on normal-priority
     // streams, this one is the lowest) get CUs while P still runs
-    if (part_kind() == 3) {
-      k_part3<P3_BLOCK, P3_TPW><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg,
-                                                        gchunk, gdesc, lo, elems, desc, err);
-    } else {
-      const unsigned grid = (unsigned)std::min<uint64_t>(chunk_bound, part_grid());
-      k_part<<<grid, PP_BLOCK, 0, pq>>>(a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc,
-                                        lo, elems, desc, err, pm_dbg());
-    }
+    // SYZGPU_PART=3 (A/B): round 2's transpose (run-detecting, per-lane tile addresses)
+    if (part_kind() == 3)
+      k_part3<P3_BLOCK, P3_TPW><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
+          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc, lo, elems, desc, err);
+    else
+      k_part4<P3_BLOCK, P3_TPW><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
+          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc, lo, elems, desc, err);
     SYZ_LAUNCHED();
   }
   SYZ_HIP(hipEventRecord(c.ev_part1, pq));
   // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
   uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
   SYZ_HIP(hipMemsetAsync(sel8, 0, (n + 31) / 32 * 32 + 64, s));
-  const size_t nd_small = items[0][PMODE_DIRECT].size(), nh_small = items[0][PMODE_HASH].size();
-  const size_t nd_big = items[1][PMODE_DIRECT].size(), nh_big = items[1][PMODE_HASH].size();
-  const size_t off_small_d = 0, off_small_h = nd_small, off_big_d = nd_small + nh_small,
-               off_big_h = off_big_d + nd_big;
-  auto run_m = [&](hipStream_t q, size_t first_d, size_t nd, size_t first_h, size_t nh, const char* tag) {
+  // ditems holds the classes in order (small, big), each as its direct, hash, packed items
+  size_t ifirst[2][3];
+  {
+    size_t k = 0;
+    for (int b = 0; b < 2; b++)
+      for (int m = 0; m < 3; m++) {
+        ifirst[b][m] = k;
+        k += items[b][m].size();
+      }
+  }
+  // byte model of M: every element read once (4 B per PC of the class's groups)
+  auto run_m = [&](hipStream_t q, int big) {
     SYZ_HIP(hipStreamWaitEvent(q, c.ev_part1, 0));
-    ProfScope ps(tag, q, 0);
+    ProfScope ps(big ? "m_big" : "m_small", q, 0);
+    const size_t nd = items[big][PMODE_DIRECT].size(), nh = items[big][PMODE_HASH].size(),
+                 np = items[big][PMODE_PACKED].size();
     if (nd) {
-      auto* kd = pmin_tiles() ? k_pmin_direct<true> : k_pmin_direct<false>;
-      kd<<<(unsigned)nd, 1024, 0, q>>>(ditems + first_d, chunks, gchunk, gdesc, dpg, desc, elems, rank_of_member,
-                                       (uint32_t)n, gstart, sel8, pm_dbg());
+      ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
+      k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], chunks, gchunk, gdesc, dpg,
+                                                   desc, elems, rank_of_member, gstart, sel8, pm_dbg());
       SYZ_LAUNCHED();
     }
     if (nh && !(pm_dbg() & 4)) {
-      auto* kh = pmin_tiles() ? k_pmin_hash<true> : k_pmin_hash<false>;
-      kh<<<(unsigned)nh, 1024, 0, q>>>(ditems + first_h, chunks, gchunk, gdesc, dpg, desc, elems, rank_of_member,
-                                       (uint32_t)n, gstart, sel8, pm_dbg());
+      ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
+      k_pmin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[big][PMODE_HASH], chunks, gchunk, gdesc,
+                                                        dpg, desc, elems, rank_of_member, gstart, sel8, pm_dbg());
+      SYZ_LAUNCHED();
+    }
+    if (np && !(pm_dbg() & 4)) {
+      ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
+      k_pmin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], chunks, gchunk, gdesc,
+                                                       dpg, desc, elems, rank_of_member, gstart, sel8, pm_dbg());
       SYZ_LAUNCHED();
     }
   };
@@ -844,11 +667,11 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
   auto small_done = [&](hipStream_t q) {
     if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);
-    run_m(q, off_small_d, nd_small, off_small_h, nh_small, "pmin_small");
+    run_m(q, 0);
   };
   auto big_done = [&](hipStream_t q) {
     if (P.nbig) ranks_big(el, perm, P, members, rank_of_member, ent_of_rank, q);
-    run_m(q, off_big_d, nd_big, off_big_h, nh_big, "pmin");
+    run_m(q, 1);
   };
   if (n) {
     gosort_run(el, perm, n, P, s, small_done, big_done);
@@ -860,8 +683,9 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   J.stats_total_pcs = total_pcs;
-  J.stats_items_direct = nd_small + nd_big;
-  J.stats_items_hash = nh_small + nh_big;
+  J.stats_items_direct = items[0][PMODE_DIRECT].size() + items[1][PMODE_DIRECT].size();
+  J.stats_items_hash = items[0][PMODE_HASH].size() + items[1][PMODE_HASH].size() + items[0][PMODE_PACKED].size() +
+                       items[1][PMODE_PACKED].size();
   if (herr[0] & 1) {
     if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
     return false;
@@ -1096,6 +920,17 @@ int syzgpu_mz_fetch(syzgpu_mz* job, int64_t* out_idx, uint64_t* group_out_off) {
     minimize_raw_fetch(J, out_idx, group_out_off);
   })
 }
+
+#ifdef SYZ_STAMPS
+// diagnostic build only: the phase stamps of the last k_part4 (which = 0) / k_pmin_direct (1) launch
+int syzgpu_debug_stamps(int which, uint64_t* out, size_t cap) {
+  SYZ_API_BODY({
+    const size_t n = std::min<size_t>(cap, (size_t)STAMP_WG * 8);
+    SYZ_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), n * 8, (size_t)which * STAMP_WG * 8 * 8,
+                                hipMemcpyDeviceToHost));
+  })
+}
+#endif
 
 int syzgpu_mz_info(syzgpu_mz* job, uint64_t* info, size_t cap) {
   SYZ_API_BODY({

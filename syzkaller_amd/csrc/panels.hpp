@@ -10,7 +10,7 @@ namespace syz {
 
 constexpr uint32_t MAX_GROUPS_PM = 4096;
 
-enum { PMODE_DIRECT = 0, PMODE_HASH = 1 };
+enum { PMODE_DIRECT = 0, PMODE_HASH = 1, PMODE_PACKED = 2 };
 
 struct PGroup {          // per call group: window bits, windows, table kind
   uint32_t S, W, mode, pad;
@@ -73,7 +73,7 @@ void minimize_raw_xchg(MinJob& J, const uint32_t* groups, const uint64_t* offset
                        int import, hipStream_t s);
 void minimize_raw_end(MinJob& J, const RawEndArgs& e);
 void minimize_raw_fetch(MinJob& J, int64_t* out_idx, uint64_t* group_out_off);
-void plan_windows(uint64_t span, const uint64_t* gpcs, uint32_t G, std::vector<PGroup>& pg);
+void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, uint32_t G, std::vector<PGroup>& pg);
 // group-major kept list (device) from a rank bitmap
 void sel_compact_dev(const uint8_t* sel8, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
                      int64_t* out_idx, uint64_t* group_out_off, hipStream_t s);

@@ -282,31 +282,32 @@ def slice_csr(pcs, off, lo, hi):
     return pcs[mask], off2
 
 
-def novelty_shard(pcs, off, group, ngroups, mc, mc_off, flakes, rank, world, bounds, run, dist=None):
-    """One rank's share of a new-coverage batch (fuzzer.go:446-470 per cover, in order) sharded by PC
-    value: the batch, the maxCover tables and the flakes restricted to [bounds[rank], bounds[rank+1]-1],
-    run(...) -> (is_new u8[n], table pcs, table offsets) on that slice (the GPU, or a checker), then the
-    OR of the flags over ranks and the ranks' table parts concatenated per call in PC order. A call's
-    table loses the 0xFFFFFFFF sentinel when any rank updated it (Union drops it over the whole table,
-    cover.go:63-70). Returns (is_new, tables, offsets), identical on every rank."""
-    import torch
-    lo, hi = int(bounds[rank]), int(bounds[rank + 1]) - 1
+def novelty_slice(pcs, off, mc, mc_off, flakes, lo, hi):
+    """A rank's inputs of a PC-range shard of the new-coverage check: the batch, the maxCover tables and
+    the flakes restricted to PCs in [lo, hi]."""
     p_r, o_r = slice_csr(pcs, off, lo, hi)
     m_r, mo_r = slice_csr(mc, mc_off, lo, hi)
     flakes = np.asarray(flakes, np.uint32)
-    f_r = flakes[(flakes >= lo) & (flakes <= hi)]
-    is_new_r, tab_r, toff_r = run(p_r, o_r, group, ngroups, m_r, mo_r, f_r)
+    return p_r, o_r, m_r, mo_r, flakes[(flakes >= lo) & (flakes <= hi)]
+
+
+def novelty_flags(is_new_r, group, ngroups):
+    """A rank's exchange bytes: its per-cover flags and per-call "updated" flags, u8[n + G] (the MAX
+    all-reduce of these over ranks is the whole exchange of the flags)."""
     group = np.asarray(group, np.int64)
     updated = np.zeros(ngroups, np.uint8)
-    if is_new_r.size:
+    if np.asarray(is_new_r).size:
         np.maximum.at(updated, group[np.asarray(is_new_r, bool)], 1)
-    flags = torch.from_numpy(np.concatenate([np.asarray(is_new_r, np.uint8), updated]))
-    allreduce_max_u8(flags, dist)
-    is_new, updated = flags[:is_new_r.size].numpy(), flags[is_new_r.size:].numpy()
-    parts = [(tab_r, toff_r)]
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
-        parts = [None] * world
-        dist.all_gather_object(parts, (np.asarray(tab_r, np.uint32), np.asarray(toff_r, np.uint64)))
+    return np.concatenate([np.asarray(is_new_r, np.uint8), updated])
+
+
+def novelty_merge(flags, parts, n, ngroups):
+    """The batch's result from the MAX-reduced flags (u8[n + G]) and every rank's table part
+    [(tables, offsets)] in rank (= PC range) order: each call's table is the concatenation of its
+    parts, without the 0xFFFFFFFF sentinel when any rank updated it (Union drops it over the whole
+    table, cover.go:63-70). Returns (is_new, tables, offsets)."""
+    flags = np.asarray(flags, np.uint8)
+    is_new, updated = flags[:n], flags[n:n + ngroups]
     tabs, lens = [], np.zeros(ngroups, np.int64)
     for g in range(ngroups):
         t = np.concatenate([np.asarray(p[0][int(p[1][g]):int(p[1][g + 1])], np.uint32) for p in parts])
@@ -317,3 +318,23 @@ def novelty_shard(pcs, off, group, ngroups, mc, mc_off, flakes, rank, world, bou
     toff = np.zeros(ngroups + 1, np.uint64)
     np.cumsum(lens, out=toff[1:])
     return is_new, (np.concatenate(tabs) if tabs else np.zeros(0, np.uint32)), toff
+
+
+def novelty_shard(pcs, off, group, ngroups, mc, mc_off, flakes, rank, world, bounds, run, dist=None):
+    """One rank's share of a new-coverage batch (fuzzer.go:446-470 per cover, in order) sharded by PC
+    value: the batch, the maxCover tables and the flakes restricted to [bounds[rank], bounds[rank+1]-1]
+    (novelty_slice), run(...) -> (is_new u8[n], table pcs, table offsets) on that slice (the GPU, or a
+    checker), then the MAX all-reduce of the flags (novelty_flags: n + G bytes) and the ranks' table
+    parts concatenated per call in PC order (novelty_merge). Returns (is_new, tables, offsets),
+    identical on every rank."""
+    import torch
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1]) - 1
+    p_r, o_r, m_r, mo_r, f_r = novelty_slice(pcs, off, mc, mc_off, flakes, lo, hi)
+    is_new_r, tab_r, toff_r = run(p_r, o_r, group, ngroups, m_r, mo_r, f_r)
+    flags = torch.from_numpy(novelty_flags(is_new_r, group, ngroups))
+    allreduce_max_u8(flags, dist)
+    parts = [(tab_r, toff_r)]
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, (np.asarray(tab_r, np.uint32), np.asarray(toff_r, np.uint64)))
+    return novelty_merge(flags.numpy(), parts, np.asarray(is_new_r).size, ngroups)

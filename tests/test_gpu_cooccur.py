@@ -72,9 +72,30 @@ def test_cooccurrence_k_tail_and_splits(monkeypatch):
     for C, n in cases:
         calls, off = corpus_calls(n, n, C)
         want = oracle.call_cooccurrence(calls, off, C)
-        for ks in ("1", "3", "16", "64"):
-            monkeypatch.setenv("SYZGPU_CO_KS", ks)
-            assert np.array_equal(prog.CallCooccurrence(calls, off, C), want)
+        for form in ("0", "1"):  # the direct operand loads and the LDS-staged default
+            monkeypatch.setenv("SYZGPU_CO_FORM", form)
+            for ks in ("1", "3", "16", "64"):
+                monkeypatch.setenv("SYZGPU_CO_KS", ks)
+                assert np.array_equal(prog.CallCooccurrence(calls, off, C), want)
+
+
+@pytest.mark.parametrize("ks", ["1", "64"])
+def test_cooccurrence_int32_overflow_is_an_error(monkeypatch, ks):
+    # 140k programs of 127 calls 3: out[3][3] = 140k * 127 * 126 > 2^31 - 1. One K range: its partial
+    # could wrap (sum of len^2 >= 2^31, err 4); 64 ranges: the partials are exact, the int64 sum is not
+    # an int32 (err 8). Either way an error, never a wrapped count.
+    n = 140_000
+    off = (np.arange(n + 1, dtype=np.uint64) * 127).astype(np.uint64)
+    calls = np.full(n * 127, 3, np.uint16)
+    monkeypatch.setenv("SYZGPU_CO_KS", ks)
+    with pytest.raises(_lib.SyzGpuError) as e:
+        prog.CallCooccurrence(calls, off, 8)
+    assert e.value.code == _lib.EINVAL
+    # just below the limit, with the default K split: exact
+    monkeypatch.delenv("SYZGPU_CO_KS")
+    m = (2**31 - 1) // (127 * 126)
+    got = prog.CallCooccurrence(calls[:m * 127], off[:m + 1], 8)
+    assert int(got[3, 3]) == m * 127 * 126
 
 
 @pytest.mark.parametrize("bad", ["call_id", "repeats"])

@@ -13,20 +13,14 @@ import json
 import os
 import sys
 
-SHORT = {"k_part3": "part", "k_pmin_direct": "pmin", "k_pmin_hash": "pmin_hash", "k_grp_scatter": "group_partition",
-         "k_sel_flags": "select_out", "k_vec_min": "vec_min", "k_gr_count": "gosort_round",
-         "k_gr_lists": "gosort_round", "k_gr_swap": "gosort_round", "k_ls_sort": "gosort_lds",
-         "k_prio_row": "prio_choice", "k_st_gram": "static_prio", "k_ranks": "ranks",
-         "k_co_gemm": "cooc_gemm", "k_co_build": "cooc_build"}
-
 
 def short(name, grid):
-    if "k_vec_min<true>" in name:
-        return "vec_min_small"
-    for k, v in SHORT.items():
-        if k in name:
-            return v
-    return None
+    """The kernel's base name (`void syz::k_part4<512, 40, false>(...)` -> `k_part4`): the names the
+    bench's per-kernel scopes use."""
+    base = name.split("(")[0].split("<")[0].split("::")[-1].strip()
+    if base.startswith("void "):
+        base = base[5:]
+    return base or None
 
 
 def read(d, counter):
