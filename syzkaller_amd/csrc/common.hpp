@@ -158,7 +158,8 @@ struct ProfScope {
 // ---- device-wide scans (scan.hip) ----------------------------------------------------------
 // out[i] = sum(in[0..i)), out[n] = total. in may be uint8_t / uint32_t / uint64_t.
 void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s);
-void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s);
+// tag: a distinct scratch name for scans that may run on another stream at the same time
+void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s, const char* tag = "");
 void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s);
 
 inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {

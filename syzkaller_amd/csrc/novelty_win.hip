@@ -119,92 +119,24 @@ __global__ __launch_bounds__(256) void k_nw_meta(const uint32_t* pcs, const uint
   block_span_update<256>(lo, hi, span);
 }
 
-// The walk of a direct table with its LDS updates batched: every run of a group of RBN issues its
-// ds_min (with return) first, one wait, then the lanes that found the entry empty set its presence bit
-// — instead of a read, a wait and a conditional atomic per run.
-template <int RBN>
-__device__ __forceinline__ void nw_walk_direct(const PItem it, const PChunk* __restrict__ chunks, const uint64_t* gchunk,
-                                               const uint64_t* gdesc, const PGroup* pg,
-                                               const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems,
-                                               int nwaves, uint32_t* tab, uint32_t* pres) {
-  const uint32_t g = it.g, w = it.w;
-  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
-  const uint32_t W = pg[g].W, S = pg[g].S;
-  const uint32_t omask = (1u << S) - 1;
-  const uint16_t* d0 = desc + gdesc[g] + w;
-  const int wv = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  auto upd_one = [&](uint32_t e, uint32_t mbj) {
-    const uint32_t o = e & omask;
-    if (atomicMin(&tab[o], mbj + (e >> S)) == RANK_NONE) atomicOr(&pres[o >> 5], 1u << (o & 31));
-  };
-  const uint64_t nrun = c1 - c0;
-  for (uint64_t b0 = (uint64_t)wv; b0 < nrun; b0 += (uint64_t)nwaves * 64) {
-    const uint64_t c = c0 + b0 + (uint64_t)lane * nwaves;
-    uint32_t len = 0, mb = 0, stl = 0, sth = 0;
-    if (c < c1) {
-      const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
-      const uint32_t s0 = d[0], s1 = d[1];
-      len = s1 - s0;
-      const uint64_t st = chunks[c].elem + s0;
-      stl = (uint32_t)st;
-      sth = (uint32_t)(st >> 32);
-      mb = chunks[c].mb;
-    }
-    const uint32_t nr = (uint32_t)min<uint64_t>(64, (nrun - b0 + nwaves - 1) / nwaves);
-    for (uint32_t r0 = 0; r0 < nr; r0 += RBN) {
-      uint32_t e0[RBN], ln[RBN], mbr[RBN], old[RBN];
-      uint64_t sts[RBN];
-#pragma unroll
-      for (int r = 0; r < RBN; r++) {
-        const uint32_t j = r0 + r;
-        ln[r] = j < nr ? (uint32_t)__builtin_amdgcn_readlane((int)len, (int)j) : 0u;
-        mbr[r] = (uint32_t)__builtin_amdgcn_readlane((int)mb, (int)j);
-        sts[r] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sth, (int)j) << 32) |
-                 (uint32_t)__builtin_amdgcn_readlane((int)stl, (int)j);
-        e0[r] = lane < ln[r] ? elems[sts[r] + lane] : 0u;
-      }
-#pragma unroll
-      for (int r = 0; r < RBN; r++)
-        old[r] = lane < ln[r] ? atomicMin(&tab[e0[r] & omask], mbr[r] + (e0[r] >> S)) : 0u;
-#pragma unroll
-      for (int r = 0; r < RBN; r++)
-        if (lane < ln[r] && old[r] == RANK_NONE) {
-          const uint32_t o = e0[r] & omask;
-          atomicOr(&pres[o >> 5], 1u << (o & 31));
-        }
-#pragma unroll
-      for (int r = 0; r < RBN; r++) {
-        for (uint32_t k = 64; k < ln[r]; k += 64 * TU) {  // long runs: TU 64-PC slices in flight
-          uint32_t x[TU];
-#pragma unroll
-          for (int u = 0; u < TU; u++) {
-            const uint32_t i = k + 64 * u + lane;
-            x[u] = i < ln[r] ? elems[sts[r] + i] : 0u;
-          }
-#pragma unroll
-          for (int u = 0; u < TU; u++)
-            if (k + 64 * u + lane < ln[r]) upd_one(x[u], mbr[r]);
-        }
-      }
-    }
-  }
+// a table slot: the window offset rotated right by 2 bits, so PCs on 4-byte boundaries spread over
+// every LDS bank
+template <uint32_t SB>
+__device__ __forceinline__ uint32_t nw_index(uint32_t o) {
+  return ((o >> 2) | (o << (SB - 2))) & ((1u << SB) - 1);
 }
 
-// SYZGPU_NW_WALK=0 (A/B): the direct tables through for_window_elems (read, compare, atomic per run)
-static int nw_walk_kind() {
-  static const int v = getenv("SYZGPU_NW_WALK") ? atoi(getenv("SYZGPU_NW_WALK")) : 1;
-  return v;
-}
+#ifndef SYZ_RG_NU
+#define SYZ_RG_NU 2
+#endif
 
 // M: one (call, window). tab = min member position per window offset; the table's position cstart[g]
 // is OLD.
 template <uint32_t SB>
 __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
-    const uint32_t* order, uint32_t W, const PChunk* __restrict__ chunks, const uint64_t* gchunk, const uint64_t* gdesc,
-    const PGroup* pg, const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems, const uint64_t* cstart,
-    uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart, const NwGroup* ng_,
-    uint32_t* kbits, uint32_t* wcount, uint8_t* sel8, uint8_t* upd, int dbg, int walk) {
+    const uint32_t* order, uint32_t W, const PGroup* pg, const uint64_t* rstart, const uint32_t* elems,
+    const uint64_t* cstart, uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart,
+    const NwGroup* ng_, uint32_t* kbits, uint32_t* wcount, uint8_t* sel8, uint8_t* upd, int dbg) {
   using K = NwCfg<SB>;
   constexpr int BLOCK = K::BLOCK;
   __shared__ __align__(16) uint32_t tab[K::BITS];
@@ -230,17 +162,12 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
     const uint32_t o = fl[i] - wlo;  // flakes not increasing (rejected after the batch) land anywhere
     if (o < K::BITS) atomicOr(&flk[o >> 5], 1u << (o & 31));
   }
-  if (!(dbg & 1) && walk == 1)
-    nw_walk_direct<SYZ_DIRECT_RB>(it, chunks, gchunk, gdesc, pg, desc, elems, BLOCK / 64, tab, pres);
-  else if (!(dbg & 1))
-    for_window_elems<SYZ_DIRECT_RB, true>(it, chunks, gchunk, gdesc, pg, desc, elems, nullptr, 0u, BLOCK / 64,
-                                          [&](uint32_t o, uint32_t R) {
-                                            if (tab[o] > R) {
-                                              atomicMin(&tab[o], R);
-                                              const uint32_t bit = 1u << (o & 31);
-                                              if (!(pres[o >> 5] & bit)) atomicOr(&pres[o >> 5], bit);
-                                            }
-                                          });
+  // the window's regions; a member's rank is its position (the table first, then batch order)
+  if (!(dbg & 1))
+    for_region<SYZ_RG_NU, true>(it, pg, cstart, rstart, elems, nullptr, [&](uint32_t o, uint32_t R) {
+      if (R != RANK_NONE && atomicMin(&tab[nw_index<SB>(o)], R) == RANK_NONE) atomicOr(&pres[o >> 5], 1u << (o & 31));
+    });
+  __syncthreads();
   if (dbg & 2) return;
   const uint64_t gb = cstart[g], ng = cstart[g + 1] - gb;
   const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)K::BMW * 32, ng);
@@ -259,7 +186,7 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
     while (m) {
       const uint32_t b = __ffs(m) - 1;
       m &= m - 1;
-      const uint32_t r = tab[32 * wd + b];
+      const uint32_t r = tab[nw_index<SB>(32 * wd + b)];
       const bool old = r == (uint32_t)gb;
       if (!old && ((fw >> b) & 1u)) continue;  // a flake no table holds: never new, never kept
       kw |= 1u << b;
@@ -444,12 +371,21 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   std::vector<PGroup> hpg(G);
   std::vector<NwGroup> hng(G + 1);
   uint64_t kw = 0, slots = 0;
+  uint64_t nreg = 0;
+  std::vector<ColItem> hcol;
   for (uint32_t g = 0; g < G; g++) {
-    hpg[g] = PGroup{DB, WD, (uint32_t)PMODE_DIRECT, 0};
+    // regions: one per (member segment of 2^(32 - DB) members, window)
+    const uint64_t ngm = hstart[g + 1] - hstart[g];
+    const uint32_t nseg = (uint32_t)((ngm + (1ull << (32 - DB)) - 1) >> (32 - DB));
+    hpg[g] = PGroup{DB, WD, (uint32_t)PMODE_DIRECT, (uint32_t)nreg};
+    nreg += (uint64_t)nseg * WD;
+    for (uint32_t sg = 0; sg < nseg; sg++)
+      for (uint32_t w0 = 0; w0 < WD; w0 += 64) hcol.push_back(ColItem{g, sg, w0, 0});
     hng[g] = NwGroup{kw, slots};
     kw += (uint64_t)WD << (DB - 5);
     slots += WD + 1;
   }
+  if (nreg >= (1ull << 31)) return false;
   hng[G] = NwGroup{kw, slots};
   std::vector<uint32_t> hgblock(G + 1, 0);
   uint64_t desc_bound = 0;
@@ -468,18 +404,21 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   const size_t nitems = (size_t)G * WD;
   // one staging copy: PGroup[G+1], NwGroup[G+1], gblock[G+1], order[G+1]
   const size_t o_ng = (G + 1) * sizeof(PGroup), o_gb = o_ng + (G + 1) * sizeof(NwGroup), o_or = o_gb + (G + 1) * 4;
-  const size_t stage_bytes = o_or + (G + 1) * 4;
+  const size_t o_ci = o_or + (G + 1) * 4;
+  const size_t stage_bytes = o_ci + (hcol.size() + 1) * sizeof(ColItem);
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
   uint8_t* dstage = sc.get<uint8_t>("nw_stage", stage_bytes + 64);
   std::memcpy(stage, hpg.data(), G * sizeof(PGroup));
   std::memcpy(stage + o_ng, hng.data(), (G + 1) * sizeof(NwGroup));
   std::memcpy(stage + o_gb, hgblock.data(), (G + 1) * 4);
   std::memcpy(stage + o_or, order.data(), G * 4);
+  if (!hcol.empty()) std::memcpy(stage + o_ci, hcol.data(), hcol.size() * sizeof(ColItem));
   SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
   const PGroup* dpg = reinterpret_cast<const PGroup*>(dstage);
   const NwGroup* dng = reinterpret_cast<const NwGroup*>(dstage + o_ng);
   const uint32_t* dgblock = reinterpret_cast<const uint32_t*>(dstage + o_gb);
   const uint32_t* dorder = reinterpret_cast<const uint32_t*>(dstage + o_or);
+  const ColItem* dcol = reinterpret_cast<const ColItem*>(dstage + o_ci);
   uint32_t* dbgroup = sc.get<uint32_t>("nw_bgroup", (size_t)B + 1);
   if (B) {
     k_nw_bgroup<<<grid_for(B, 256, 4096), 256, 0, s>>>(dgblock, G, B, dbgroup);
@@ -490,14 +429,17 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   PChunk* chunks = sc.get<PChunk>("nw_chunks", chunk_bound + 1);
   uint64_t* gchunk = sc.get<uint64_t>("nw_gchunk", G + 1);
   uint64_t* gdesc = sc.get<uint64_t>("nw_gdesc", G + 1);
-  uint16_t* desc = sc.get<uint16_t>("nw_desc", desc_bound + 1);
-  uint32_t* elems = sc.get<uint32_t>("pm_elems", elem_bound(total, chunk_bound));
+  uint16_t* cnt = sc.get<uint16_t>("nw_cnt", desc_bound + 1);
+  uint32_t* colpre = sc.get<uint32_t>("nw_colpre", desc_bound + 1);
+  uint32_t* elems = sc.get<uint32_t>("pm_elems", total + 8);
+  uint32_t* rtot = sc.get<uint32_t>("nw_rtot", nreg + 1);
+  uint64_t* rstart = sc.get<uint64_t>("nw_rstart", nreg + 2);
   uint32_t* kbits = sc.get<uint32_t>("nw_kbits", kw + 1);
   uint32_t* wcount = sc.get<uint32_t>("nw_wcount", slots + 1);
   uint64_t* wpos = sc.get<uint64_t>("nw_wpos", slots + 1);
 
   {
-    ProfScope ps("novelty_part", s, total * 8 + (uint64_t)nm * 24);
+    ProfScope ps("novelty_part", s, total * 12 + (uint64_t)nm * 48);
     if (B) {
       k_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, cstart, mpos, nsub);
       SYZ_LAUNCHED();
@@ -513,8 +455,17 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     ns.mc = d_mc;
     ns.mc_off = d_mco;
     ns.n1 = (uint32_t)n;
-    k_part3<P3_BLOCK, P3_TPW, true><<<(unsigned)chunk_bound, P3_BLOCK, 0, s>>>(
-        d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, gchunk, gdesc, lo, elems, desc, err, ns);
+    k_region<P3_BLOCK, P3_TPW, true, true><<<(unsigned)chunk_bound, P3_BLOCK, 0, s>>>(
+        d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, cstart, gchunk, gdesc, lo, cnt, nullptr,
+        nullptr, nullptr, err, ns);
+    SYZ_LAUNCHED();
+    k_colscan<<<(unsigned)hcol.size(), CS_BLOCK, 0, s>>>(dcol, dpg, cstart, dgblock, cstartb, gchunk, gdesc, cnt,
+                                                        colpre, rtot);
+    SYZ_LAUNCHED();
+    exclusive_scan_u32(rtot, rstart, nreg, s);
+    k_region<P3_BLOCK, P3_TPW, true, false><<<(unsigned)chunk_bound, P3_BLOCK, 0, s>>>(
+        d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, cstart, gchunk, gdesc, lo, nullptr, colpre,
+        rstart, elems, err, ns);
     SYZ_LAUNCHED();
   }
   uint32_t* fstart = sc.get<uint32_t>("nw_fstart", (size_t)WD + 2);
@@ -524,13 +475,11 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     SYZ_LAUNCHED();
     if (nitems) {
       if (DB == 14)
-        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, chunks, gchunk, gdesc, dpg, desc, elems,
-                                                                   cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
-                                                                   upd, nw_dbg(), nw_walk_kind());
+        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, dpg, rstart, elems, cstart, lo, d_fl,
+                                                                   fstart, dng, kbits, wcount, sel8, upd, nw_dbg());
       else
-        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, chunks, gchunk, gdesc, dpg, desc, elems,
-                                                                   cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
-                                                                   upd, nw_dbg(), nw_walk_kind());
+        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, dpg, rstart, elems, cstart, lo, d_fl,
+                                                                   fstart, dng, kbits, wcount, sel8, upd, nw_dbg());
       SYZ_LAUNCHED();
     }
   }

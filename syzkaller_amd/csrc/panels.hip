@@ -119,18 +119,20 @@ __device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t 
 }
 
 
-// Dense windows: a 2^DS-entry direct min table in LDS (128 KB: one workgroup per CU), the packed walk
-// (panels_dev.hpp), then the winners as byte stores; the walk's LDS scratch is the emit's rank bitmap.
-__global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const PChunk* __restrict__ chunks,
-                                                      const uint64_t* gchunk, const uint64_t* gdesc,
-                                                      const PGroup* pg, const uint16_t* __restrict__ desc,
-                                                      const uint32_t* __restrict__ elems,
+// Dense windows: a 2^DS-entry direct min table in LDS (128 KB: one workgroup per CU), the window's
+// regions streamed (panels_dev.hpp for_region), then the winners as byte stores.
+#ifndef SYZ_RG_U
+#define SYZ_RG_U 2
+#endif
+// The direct table's index: the offset rotated right by 2 bits inside the window, so PCs on 4-byte
+// instruction boundaries (arm64, and the synthetic corpora) fill every LDS bank, not a quarter of them
+__device__ __forceinline__ uint32_t tab_index(uint32_t o) { return ((o >> 2) | (o << (DS - 2))) & ((1u << DS) - 1); }
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_pmin_direct(const PItem* items, const PGroup* pg, const uint64_t* rstart,
+                                                      const uint32_t* elems,
                                                       const uint32_t* __restrict__ rank_of_member,
                                                       const uint64_t* gstart, uint8_t* sel8, int dbg) {
   __shared__ __align__(16) uint32_t tab[1u << DS];
-  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];
-  __shared__ uint64_t red64[1024 / 64 + 1];
-  SYZ_STAMP(1, 0);
+  __shared__ uint32_t bm[PK_SCRATCH_WORDS];
   const PItem it = items[blockIdx.x];
   {
     uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -138,29 +140,37 @@ __global__ __launch_bounds__(1024) void k_pmin_direct(const PItem* items, const 
     for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
   }
   __syncthreads();
-  SYZ_STAMP(1, 1);
-  for_window_packed<SYZ_PK_U, false>(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, wsc, red64,
-                                     [&](uint32_t o, uint32_t R) { atomicMin(&tab[o], R); });
+  if (dbg & 1) {  // timing only: the walk without its table updates
+    uint32_t acc = 0;
+    for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, elems, rank_of_member,
+                                [&](uint32_t o, uint32_t R) { acc += o ^ R; });
+    if (acc == 0x9E3779B9u) sel8[0] = 1;
+  } else if (dbg & 8) {  // timing only: no rank gathers
+    for_region<SYZ_RG_U, true>(it, pg, gstart, rstart, elems, nullptr,
+                               [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
+  } else {
+    for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, elems, rank_of_member,
+                                [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
+  }
   __syncthreads();
-  SYZ_STAMP(1, 2);
   if (dbg & 2) return;
   const uint64_t gb = gstart[it.g];
-  emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, wsc, sel8);
-  SYZ_STAMP(1, 3);
+  emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, bm, sel8);
 }
 
-// PCs of one (call, window) over all its chunks' runs (metadata only)
-__device__ uint32_t window_elem_count(const PItem it, const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
-                                      const uint16_t* __restrict__ desc, uint32_t* red) {
-  const uint32_t g = it.g, w = it.w, W = pg[g].W;
-  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
-  const uint16_t* d0 = desc + gdesc[g] + w;
-  uint32_t s = 0;
-  for (uint64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
-    const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
-    s += (uint32_t)d[1] - d[0];
+// PCs of one (call, window): the lengths of its segments' regions
+__device__ __forceinline__ uint32_t window_elem_count(const PItem it, const PGroup* pg, const uint64_t* gstart,
+                                                     const uint64_t* rstart) {
+  const PGroup p = pg[it.g];
+  const uint32_t sb = 32 - p.S;
+  const uint64_t ng = gstart[it.g + 1] - gstart[it.g];
+  const uint32_t nseg = (uint32_t)((ng + (1ull << sb) - 1) >> sb);
+  uint64_t e = 0;
+  for (uint32_t s = 0; s < nseg; s++) {
+    const uint32_t r = p.rb + s * p.W + it.w;
+    e += rstart[r + 1] - rstart[r];
   }
-  return block_sum<1024>(s, red);
+  return (uint32_t)e;
 }
 
 __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - HS_BITS); }
@@ -173,7 +183,7 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 // 72 KB of LDS at 8192 slots: two workgroups per CU (registers held to 64 per lane, 4 runs in
 // flight per wave), so one window's table init and emit overlap the other's loads
 #ifndef SYZ_PK_HU
-#define SYZ_PK_HU 4
+#define SYZ_PK_HU 1
 #endif
 // Sparse windows: open addressing keyed by the window offset, kept at most half full: a window with
 // more than HCAP PCs is done in R = ceil(PCs / HCAP) rounds, each taking the keys of one residue of
@@ -184,24 +194,21 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 // offset << 13 | rank - the group's first rank, inserted by CAS and lowered by atomicMin (equal high
 // bits, so the min is the min rank), 16K slots in the 64 KB of the 8K key/value pairs.
 template <bool PACKED>
-__global__ __launch_bounds__(1024) void k_pmin_hash(const PItem* items, const PChunk* __restrict__ chunks,
-                                                    const uint64_t* gchunk, const uint64_t* gdesc,
-                                                    const PGroup* pg, const uint16_t* __restrict__ desc,
-                                                    const uint32_t* __restrict__ elems,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pmin_hash(const PItem* items, const PGroup* pg, const uint64_t* rstart,
+                                                    const uint32_t* elems,
                                                     const uint32_t* __restrict__ rank_of_member,
                                                     const uint64_t* gstart, uint8_t* sel8, int dbg) {
   constexpr uint32_t NS = PACKED ? PHS : HS;  // slots
   constexpr uint32_t CAP = PACKED ? PHCAP : HCAP;
   __shared__ uint32_t tabs[2 * HS];
   static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
-  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];  // the walk's scratch, then the emit bitmap
-  __shared__ uint64_t red64[1024 / 64 + 1];
+  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];  // the emit bitmap
   __shared__ int full;
   uint32_t* keys = tabs;       // PACKED: the slots
   uint32_t* vals = tabs + HS;
   const PItem it = items[blockIdx.x];
   const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
-  const uint32_t E = window_elem_count(it, gchunk, gdesc, pg, desc, reinterpret_cast<uint32_t*>(red64));
+  const uint32_t E = window_elem_count(it, pg, gstart, rstart);
   if (E == 0) return;
   uint32_t R = (E + CAP - 1) / CAP;
   for (uint32_t round = 0; round < R;) {
@@ -210,8 +217,7 @@ __global__ __launch_bounds__(1024) void k_pmin_hash(const PItem* items, const PC
     __syncthreads();
     const uint32_t RR = R, rr = round;
     uint32_t acc = 0;
-    for_window_packed<SYZ_PK_HU, false>(it, chunks, gchunk, gdesc, pg, desc, elems, rank_of_member, wsc, red64,
-                                       [&](uint32_t o, uint32_t Rk) {
+    for_region<SYZ_PK_HU, false>(it, pg, gstart, rstart, elems, rank_of_member, [&](uint32_t o, uint32_t Rk) {
                                          if (Rk == RANK_NONE) return;  // a lane past the window
                                          if (dbg & 64) {
                                            acc ^= o * 31 + Rk;
@@ -365,15 +371,18 @@ void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, u
 static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span);
 
 // diagnostic switches (SYZGPU_PM_DBG, timing experiments only; results are wrong when set):
-// 2 = no winner emit (direct windows), 4 = no open-addressing windows, 64 = sparse windows walked but
+// 1 = direct walk without table updates, 2 = no winner emit (direct windows), 4 = no open-addressing
+// windows, 8 = direct walk without rank gathers, 64 = sparse windows walked but
 // not probed
-static int part_kind() {
-  static const int v = getenv("SYZGPU_PART") ? atoi(getenv("SYZGPU_PART")) : 4;
-  return v;
-}
 
 static bool pm_serial() {
   static const bool v = getenv("SYZGPU_PM_SERIAL") && atoi(getenv("SYZGPU_PM_SERIAL")) != 0;
+  return v;
+}
+
+// SYZGPU_RG_DBG (timing only, results wrong): 16 = P loads only, 32 = scatter without pass 2, 64 = no stores
+static int rg_dbg() {
+  static const int v = getenv("SYZGPU_RG_DBG") ? atoi(getenv("SYZGPU_RG_DBG")) : 0;
   return v;
 }
 
@@ -495,7 +504,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   std::vector<PGroup> hpg;
   plan_windows(spanw, hpcs.data(), hstart.data(), G, hpg);
   std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
-  uint64_t chunk_bound = 0, desc_bound = 0, total_pcs = 0;
+  uint64_t chunk_bound = 0, total_pcs = 0, nreg = 0, desc_bound = 0;
+  std::vector<ColItem> hcol;  // column-scan items: (group, segment, 64 windows)
   for (uint32_t g = 0; g < G; g++) {
     const uint64_t ng = hstart[g + 1] - hstart[g];
     const uint32_t nb = (uint32_t)((ng + MEMB - 1) / MEMB);
@@ -505,6 +515,15 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     chunk_bound += cb;
     desc_bound += cb * (hpg[g].W + 1);
     total_pcs += hsl[g];
+    // regions: one per (member segment, window); a group's PCs must fit 32-bit places
+    if (hpcs[g] >= (1ull << 32)) fail(SYZGPU_EINVAL, "a call group with 2^32 or more PCs");
+    const uint32_t sb = 32 - hpg[g].S;
+    const uint32_t nseg = (uint32_t)((ng + (1ull << sb) - 1) >> sb);
+    hpg[g].rb = (uint32_t)nreg;
+    nreg += (uint64_t)nseg * hpg[g].W;
+    if (nreg >= (1ull << 31)) fail(SYZGPU_EINVAL, "too many PC regions");
+    for (uint32_t sg = 0; sg < nseg; sg++)
+      for (uint32_t w0 = 0; w0 < hpg[g].W; w0 += 64) hcol.push_back(ColItem{g, sg, w0, 0});
   }
   const uint32_t B = hgblock[G];
   // work items: (call, window), the big groups (sorted by the global rounds) first, each class by
@@ -538,8 +557,9 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     for (auto& v : r) nitems += v.size();
   PItem* ditems = sc.get<PItem>("pm_items", nitems + 1);
   // host staging in pinned memory: one synchronous point below covers the copies
-  const size_t stage_bytes =
-      (G + 1) * sizeof(PGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 + (nitems + 1) * sizeof(PItem);
+  ColItem* dcol = sc.get<ColItem>("pm_colitems", hcol.size() + 1);
+  const size_t stage_bytes = (G + 1) * sizeof(PGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 +
+                             (nitems + 1) * sizeof(PItem) + (hcol.size() + 1) * sizeof(ColItem);
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
   {
     uint8_t* p = stage;
@@ -561,6 +581,11 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
         k += v.size();
       }
     if (nitems) SYZ_HIP(hipMemcpyAsync(ditems, p, nitems * sizeof(PItem), hipMemcpyHostToDevice, s));
+    p += (nitems + 1) * sizeof(PItem);
+    if (!hcol.empty()) {
+      std::memcpy(p, hcol.data(), hcol.size() * sizeof(ColItem));
+      SYZ_HIP(hipMemcpyAsync(dcol, p, hcol.size() * sizeof(ColItem), hipMemcpyHostToDevice, s));
+    }
   }
   // ---- blocks -> chunks ----
   uint32_t* nsub = sc.get<uint32_t>("pm_nsub", (size_t)B + 1);
@@ -568,8 +593,11 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   PChunk* chunks = sc.get<PChunk>("pm_chunks", chunk_bound + 1);
   uint64_t* gchunk = sc.get<uint64_t>("pm_gchunk", G + 1);
   uint64_t* gdesc = sc.get<uint64_t>("pm_gdesc", G + 1);
-  uint16_t* desc = sc.get<uint16_t>("pm_desc", desc_bound + 1);
-  uint32_t* elems = sc.get<uint32_t>("pm_elems", elem_bound(total_pcs, chunk_bound));
+  uint16_t* cnt = sc.get<uint16_t>("pm_cnt", desc_bound + 1);
+  uint32_t* colpre = sc.get<uint32_t>("pm_colpre", desc_bound + 1);
+  uint32_t* elems = sc.get<uint32_t>("pm_elems", total_pcs + 8);
+  uint32_t* rtot = sc.get<uint32_t>("pm_rtot", nreg + 1);
+  uint64_t* rstart = sc.get<uint64_t>("pm_rstart", nreg + 2);
   if (B) {
     k_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, gstart, mpos, nsub);
     SYZ_LAUNCHED();
@@ -605,19 +633,29 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_HIP(hipEventRecord(c.ev_part0, s));
   SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
   if (chunk_bound) {
-    // byte model: every PC read once and written once as a 4-byte element, plus 24 B of member
-    // metadata per entry (members, mpos, off, slice)
-    ProfScope ps(part_kind() == 3 ? "k_part3" : "k_part4", pq, total_pcs * 8 + (uint64_t)n * 24);
-    // one workgroup per chunk: workgroups retire all along, so the Go sort's kernels (on normal-priority
-    // streams, this one is the lowest) get CUs while P still runs
-    // SYZGPU_PART=3 (A/B): round 2's transpose (run-detecting, per-lane tile addresses)
-    if (part_kind() == 3)
-      k_part3<P3_BLOCK, P3_TPW><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
-          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc, lo, elems, desc, err);
-    else
-      k_part4<P3_BLOCK, P3_TPW><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
-          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gchunk, gdesc, lo, elems, desc, err);
-    SYZ_LAUNCHED();
+    // byte model: every PC read twice (count, scatter) and written once as a 4-byte element, plus 24 B
+    // of member metadata per entry per pass (members, mpos, off, slice)
+    {
+      ProfScope ps("k_region_count", pq, total_pcs * 4 + (uint64_t)n * 24);
+      k_region<P3_BLOCK, P3_TPW, false, true><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
+          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gstart, gchunk, gdesc, lo, cnt, nullptr,
+          nullptr, nullptr, err, NovSrc{}, rg_dbg());
+      SYZ_LAUNCHED();
+    }
+    {
+      ProfScope ps("k_colscan", pq, desc_bound * 8);
+      k_colscan<<<(unsigned)hcol.size(), CS_BLOCK, 0, pq>>>(dcol, dpg, gstart, dgblock, cstart, gchunk, gdesc, cnt,
+                                                           colpre, rtot);
+      SYZ_LAUNCHED();
+    }
+    exclusive_scan_u32(rtot, rstart, nreg, pq, "rg");
+    {
+      ProfScope ps("k_region", pq, total_pcs * 8 + (uint64_t)n * 24);
+      k_region<P3_BLOCK, P3_TPW, false, false><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
+          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gstart, gchunk, gdesc, lo, nullptr, colpre,
+          rstart, elems, err, NovSrc{}, rg_dbg());
+      SYZ_LAUNCHED();
+    }
   }
   SYZ_HIP(hipEventRecord(c.ev_part1, pq));
   // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
@@ -641,20 +679,20 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
                  np = items[big][PMODE_PACKED].size();
     if (nd) {
       ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
-      k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], chunks, gchunk, gdesc, dpg,
-                                                   desc, elems, rank_of_member, gstart, sel8, pm_dbg());
+      k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], dpg, rstart, elems,
+                                                   rank_of_member, gstart, sel8, pm_dbg());
       SYZ_LAUNCHED();
     }
     if (nh && !(pm_dbg() & 4)) {
       ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
-      k_pmin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[big][PMODE_HASH], chunks, gchunk, gdesc,
-                                                        dpg, desc, elems, rank_of_member, gstart, sel8, pm_dbg());
+      k_pmin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[big][PMODE_HASH], dpg, rstart, elems,
+                                                        rank_of_member, gstart, sel8, pm_dbg());
       SYZ_LAUNCHED();
     }
     if (np && !(pm_dbg() & 4)) {
       ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
-      k_pmin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], chunks, gchunk, gdesc,
-                                                       dpg, desc, elems, rank_of_member, gstart, sel8, pm_dbg());
+      k_pmin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dpg, rstart, elems,
+                                                       rank_of_member, gstart, sel8, pm_dbg());
       SYZ_LAUNCHED();
     }
   };

@@ -13,7 +13,7 @@ constexpr uint32_t MAX_GROUPS_PM = 4096;
 enum { PMODE_DIRECT = 0, PMODE_HASH = 1, PMODE_PACKED = 2 };
 
 struct PGroup {          // per call group: window bits, windows, table kind
-  uint32_t S, W, mode, pad;
+  uint32_t S, W, mode, rb;  // rb: first region of the group (region form: rb + segment * W + window)
 };
 struct PItem {           // one (call group, window) min-rank table
   uint32_t g, w;

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const T* in, size_t n
 __global__ void k_zero_total(uint64_t* out) { out[0] = 0; }
 
 template <class T>
-static void scan_impl(const T* in, uint64_t* out, size_t n, hipStream_t s, int depth) {
+static void scan_impl(const T* in, uint64_t* out, size_t n, hipStream_t s, int depth, const char* tag = "") {
   if (n == 0) {
     k_zero_total<<<1, 1, 0, s>>>(out);
     SYZ_LAUNCHED();
@@ -252,14 +252,14 @@ static void scan_impl(const T* in, uint64_t* out, size_t n, hipStream_t s, int d
   }
   const size_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
   Scratch& sc = ctx().scratch;
-  uint64_t* sums = sc.get<uint64_t>("scan_sums" + std::to_string(depth), tiles + 1);
-  uint64_t* offs = sc.get<uint64_t>("scan_offs" + std::to_string(depth), tiles + 1);
+  uint64_t* sums = sc.get<uint64_t>(std::string("scan_sums") + tag + std::to_string(depth), tiles + 1);
+  uint64_t* offs = sc.get<uint64_t>(std::string("scan_offs") + tag + std::to_string(depth), tiles + 1);
   if (tiles == 1) {
     SYZ_HIP(hipMemsetAsync(offs, 0, sizeof(uint64_t), s));
   } else {
     k_scan_reduce<T><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, sums);
     SYZ_LAUNCHED();
-    scan_impl<uint64_t>(sums, offs, tiles, s, depth + 1);
+    scan_impl<uint64_t>(sums, offs, tiles, s, depth + 1, tag);
   }
   k_scan_apply<T><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, offs, out, 1);
   SYZ_LAUNCHED();
@@ -268,8 +268,8 @@ static void scan_impl(const T* in, uint64_t* out, size_t n, hipStream_t s, int d
 void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s) {
   scan_impl<uint8_t>(in, out, n, s, 0);
 }
-void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s) {
-  scan_impl<uint32_t>(in, out, n, s, 0);
+void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s, const char* tag) {
+  scan_impl<uint32_t>(in, out, n, s, 0, tag);
 }
 void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) {
   scan_impl<uint64_t>(in, out, n, s, 0);

@@ -17,12 +17,12 @@ job = cover.MinimizeJob()
 s = torch.cuda.current_stream().cuda_stream
 def step():
     job.begin(d[0], d[1], d[2], c.n, 289, d[3], stream=s)
-for _ in range(3):
+for _ in range(int(os.environ.get("PM_W", "3"))):
     step()
 torch.cuda.synchronize()
 L.syzgpu_profile_only(None)
 L.syzgpu_profile_enable(1)
-K = 5
+K = int(os.environ.get("PM_K", "5"))
 t0 = time.perf_counter()
 for _ in range(K):
     step()
