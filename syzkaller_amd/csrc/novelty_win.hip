@@ -464,7 +464,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     SYZ_LAUNCHED();
     exclusive_scan_u32(rtot, rstart, nreg, s);
     k_region<P3_BLOCK, P3_TPW, true, false><<<(unsigned)chunk_bound, P3_BLOCK, 0, s>>>(
-        d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, cstart, gchunk, gdesc, lo, nullptr, colpre,
+        d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, cstart, gchunk, gdesc, lo, cnt, colpre,
         rstart, elems, err, ns);
     SYZ_LAUNCHED();
   }

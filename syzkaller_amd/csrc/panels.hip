@@ -652,7 +652,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     {
       ProfScope ps("k_region", pq, total_pcs * 8 + (uint64_t)n * 24);
       k_region<P3_BLOCK, P3_TPW, false, false><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
-          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gstart, gchunk, gdesc, lo, nullptr, colpre,
+          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gstart, gchunk, gdesc, lo, cnt, colpre,
           rstart, elems, err, NovSrc{}, rg_dbg());
       SYZ_LAUNCHED();
     }

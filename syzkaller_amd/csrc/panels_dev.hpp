@@ -638,15 +638,16 @@ __global__ __launch_bounds__(BLOCK) void k_region(
     if (acc == 0x9E3779B9u) err[1] = 1;
     return;
   }
-  // pass 1: window histogram, one LDS atomic per run of equal windows in a tile
+  if constexpr (COUNT) {
+    // window histogram: one LDS atomic per PC where the tile's PCs mostly sit in windows of their own
+    // (sparse covers), one per run of equal windows otherwise (dense covers: no same-address pile-up)
 #pragma unroll
-  for (int k = 0; k < TPW; k++) {
-    const uint32_t t = wv + WAVES * k;
-    if (t >= ntiles) break;  // wave-uniform
-    const uint32_t cnt = tinfo[t].z & 0xFFu;
-    const uint32_t w = (v[k] - lo) >> S;
-    const bool in = lane < cnt;
-    if constexpr (COUNT) {  // the checks (the scatter pass only skips what they report)
+    for (int k = 0; k < TPW; k++) {
+      const uint32_t t = wv + WAVES * k;
+      if (t >= ntiles) break;  // wave-uniform
+      const uint32_t cnt = tinfo[t].z & 0xFFu;
+      const uint32_t w = (v[k] - lo) >> S;
+      const bool in = lane < cnt;
       if constexpr (NOV) {
         const uint32_t pv = __shfl_up(v[k], 1, 64);
         const uint32_t eb = (tinfo[t].w & 1u) ? 1u : 4u;
@@ -655,9 +656,18 @@ __global__ __launch_bounds__(BLOCK) void k_region(
       } else {
         if (in && w >= W) bad |= 1;  // outside [lo, hi]: an unsorted cover; redone on exact bounds
       }
+      const bool ok = in && w < W;
+      const TileRun r = tile_run(w, ok, lane);
+      const uint32_t runs = (uint32_t)__popcll(__ballot(r.head)), pcs = (uint32_t)__popcll(__ballot(ok));
+      if (2 * runs > pcs) {
+        if (ok) atomicAdd(&hist[w], 1u);
+      } else if (r.head) {
+        atomicAdd(&hist[w], r.len);
+      }
     }
-    const TileRun r = tile_run(w, in && w < W, lane);
-    if (r.head) atomicAdd(&hist[w], r.len);
+  } else {
+    // the count pass's histogram of this chunk
+    for (uint32_t w = threadIdx.x; w < W; w += BLOCK) hist[w] = cnt[row + w];
   }
   __syncthreads();
   if constexpr (NOV && COUNT) {  // the member's previous tile ends below this tile's first PC
@@ -669,7 +679,7 @@ __global__ __launch_bounds__(BLOCK) void k_region(
       if (lane == 0 && (f & 2u) && tlast[t - 1] >= v[k]) bad |= (f & 1u) ? 1 : 4;
     }
   }
-  {
+  if constexpr (COUNT) {
     const uint64_t bm = __ballot(bad != 0);
     if (bm) {
       int all = bad;
@@ -677,8 +687,6 @@ __global__ __launch_bounds__(BLOCK) void k_region(
       for (int dd = 32; dd >= 1; dd >>= 1) all |= __shfl_xor(all, dd, 64);
       if (lane == (unsigned)(__ffsll((unsigned long long)bm) - 1)) atomicOr(err, all);
     }
-  }
-  if constexpr (COUNT) {
     for (uint32_t w = threadIdx.x; w < W; w += BLOCK) cnt[row + w] = (uint16_t)hist[w];
   } else {
     // window starts (exclusive scan) -> LDS cursors
@@ -692,8 +700,9 @@ __global__ __launch_bounds__(BLOCK) void k_region(
       run += tot;
     }
     __syncthreads();
-    if (dbg & 32) return;  // timing only: no pass 2, no stores
-    // pass 2: element = member in segment << S | offset in window, window-major into obuf
+    if (dbg & 32) return;  // timing only: no staging, no stores
+    // element = member in segment << S | offset in window, window-major into obuf: a slot per PC from a
+    // returning LDS atomic, or per run (dense covers) broadcast from the run's head
     const uint32_t omask = (1u << S) - 1;
 #pragma unroll
     for (int k = 0; k < TPW; k++) {
@@ -702,20 +711,48 @@ __global__ __launch_bounds__(BLOCK) void k_region(
       const uint32_t z = tinfo[t].z;
       const uint32_t d = v[k] - lo, w = d >> S;
       const bool in = lane < (z & 0xFFu) && w < W;
+      const uint32_t el = (d & omask) | ((mseg0 + (z >> 8)) << S);
       const TileRun r = tile_run(w, in, lane);
-      uint32_t base = r.head ? atomicAdd(&hist[w], r.len) : 0u;
-      base = (uint32_t)__shfl((int)base, (int)r.start, 64);
-      if (in) obuf[base + (lane - r.start)] = (d & omask) | ((mseg0 + (z >> 8)) << S);
+      const uint32_t runs = (uint32_t)__popcll(__ballot(r.head)), pcs = (uint32_t)__popcll(__ballot(in));
+      if (2 * runs > pcs) {
+        if (in) obuf[atomicAdd(&hist[w], 1u)] = el;
+      } else {
+        uint32_t base = r.head ? atomicAdd(&hist[w], r.len) : 0u;
+        base = (uint32_t)__shfl((int)base, (int)r.start, 64);
+        if (in) obuf[base + (lane - r.start)] = el;
+      }
     }
     __syncthreads();
     if (dbg & 64) return;  // timing only: no stores
-    // one contiguous run per window at its place (hist[w] is now window w's end)
+    // one contiguous run per window at its place (hist[w] is now window w's end): wave wv takes windows
+    // wv, wv + WAVES, ...; 64 of them at a time have their start, length and place read at once, and
+    // four runs' first 64 elements are read before their stores
     uint32_t* gel = elems + rstart[gp.rb];
-    for (uint32_t w = wv; w < W; w += WAVES) {
-      const uint32_t a = w ? hist[w - 1] : 0u, n = hist[w] - a;
-      if (!n) continue;
-      uint32_t* dst = gel + posl[w];
-      for (uint32_t i = lane; i < n; i += 64) dst[i] = obuf[a + i];
+    for (uint32_t j0 = 0; wv + WAVES * j0 < W; j0 += 64) {
+      const uint32_t wl = wv + WAVES * (j0 + lane);
+      uint32_t a = 0, n = 0, ps = 0;
+      if (wl < W) {
+        a = wl ? hist[wl - 1] : 0u;
+        n = hist[wl] - a;
+        ps = posl[wl];
+      }
+      const uint32_t nj = min(64u, (W - wv + WAVES - 1) / WAVES - j0);
+      for (uint32_t j = 0; j < nj; j += 4) {
+        uint32_t x[4], aj[4], njj[4], pj[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int jj = (int)min(j + u, 63u);
+          aj[u] = (uint32_t)__builtin_amdgcn_readlane((int)a, jj);
+          njj[u] = j + u < nj ? (uint32_t)__builtin_amdgcn_readlane((int)n, jj) : 0u;
+          pj[u] = (uint32_t)__builtin_amdgcn_readlane((int)ps, jj);
+          x[u] = lane < njj[u] ? obuf[aj[u] + lane] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (lane < njj[u]) gel[pj[u] + lane] = x[u];
+          for (uint32_t i = lane + 64; i < njj[u]; i += 64) gel[pj[u] + i] = obuf[aj[u] + i];
+        }
+      }
     }
   }
 }

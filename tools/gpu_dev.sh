@@ -7,8 +7,8 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 if [ "$TESTS" != "none" ]; then
-  timeout -k 10 600 python -u -m pytest $TESTS -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
-  rc=$?; tail -15 $OUT/pytest.log; [ $rc -eq 0 ] || { echo "pytest failed rc=$rc"; exit $rc; }
+  timeout -k 10 600 python -u -m pytest $TESTS -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+  rc=$?; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || { echo "pytest failed rc=$rc"; exit $rc; }
 fi
 env "$@" SYZGPU_PM_SERIAL=1 timeout -k 10 120 python3 tools/pm_time.py > $OUT/pm.log 2>&1 || { tail -5 $OUT/pm.log; exit 1; }
 env "$@" timeout -k 10 120 python3 tools/pm_time.py >> $OUT/pm.log 2>&1 || { tail -5 $OUT/pm.log; exit 1; }
