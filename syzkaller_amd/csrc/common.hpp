@@ -109,6 +109,8 @@ struct Context {
   uint32_t gr_resident = 0;  // workgroups of k_gr_persist resident at once (occupancy x CUs)
   hipStream_t part = nullptr;  // the raw Minimize's transpose pass, beside the Go sort
   hipEvent_t ev_part0 = nullptr, ev_part1 = nullptr;
+  hipStream_t part2 = nullptr;  // its scatter passes, batch after batch beside the next batch's count
+  std::vector<hipEvent_t> ev_cnt, ev_sct;  // per batch: count done, scatter done
   int ncu = 0;  // compute units of the device
   std::shared_ptr<struct GosortPlan> raw_plan;  // Go-sort plan of the last raw corpus layout
   std::vector<uint64_t> raw_plan_key;

@@ -134,7 +134,8 @@ __device__ __forceinline__ uint32_t nw_index(uint32_t o) {
 // is OLD.
 template <uint32_t SB>
 __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
-    const uint32_t* order, uint32_t W, const PGroup* pg, const uint64_t* rstart, const uint32_t* elems,
+    const uint32_t* order, uint32_t W, const PGroup* pg, const uint64_t* rstart, const uint32_t* rtot,
+    const uint32_t* elems,
     const uint64_t* cstart, uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart,
     const NwGroup* ng_, uint32_t* kbits, uint32_t* wcount, uint8_t* sel8, uint8_t* upd, int dbg) {
   using K = NwCfg<SB>;
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
   }
   // the window's regions; a member's rank is its position (the table first, then batch order)
   if (!(dbg & 1))
-    for_region<SYZ_RG_NU, true>(it, pg, cstart, rstart, elems, nullptr, [&](uint32_t o, uint32_t R) {
+    for_region<SYZ_RG_NU, true>(it, pg, cstart, rstart, rtot, elems, nullptr, [&](uint32_t o, uint32_t R) {
       if (R != RANK_NONE && atomicMin(&tab[nw_index<SB>(o)], R) == RANK_NONE) atomicOr(&pres[o >> 5], 1u << (o & 31));
     });
   __syncthreads();
@@ -456,7 +457,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     ns.mc_off = d_mco;
     ns.n1 = (uint32_t)n;
     k_region<P3_BLOCK, P3_TPW, true, true><<<(unsigned)chunk_bound, P3_BLOCK, 0, s>>>(
-        d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, cstart, gchunk, gdesc, lo, cnt, nullptr,
+        d_pcs, d_off, cmem, mpos, nullptr, chunks, 0u, G, dpg, cstart, gchunk, gdesc, lo, cnt, nullptr,
         nullptr, nullptr, err, ns);
     SYZ_LAUNCHED();
     k_colscan<<<(unsigned)hcol.size(), CS_BLOCK, 0, s>>>(dcol, dpg, cstart, dgblock, cstartb, gchunk, gdesc, cnt,
@@ -464,7 +465,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     SYZ_LAUNCHED();
     exclusive_scan_u32(rtot, rstart, nreg, s);
     k_region<P3_BLOCK, P3_TPW, true, false><<<(unsigned)chunk_bound, P3_BLOCK, 0, s>>>(
-        d_pcs, d_off, cmem, mpos, nullptr, chunks, cstartb + B, dpg, cstart, gchunk, gdesc, lo, cnt, colpre,
+        d_pcs, d_off, cmem, mpos, nullptr, chunks, 0u, G, dpg, cstart, gchunk, gdesc, lo, cnt, colpre,
         rstart, elems, err, ns);
     SYZ_LAUNCHED();
   }
@@ -475,10 +476,10 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     SYZ_LAUNCHED();
     if (nitems) {
       if (DB == 14)
-        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, dpg, rstart, elems, cstart, lo, d_fl,
+        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, dpg, rstart, rtot, elems, cstart, lo, d_fl,
                                                                    fstart, dng, kbits, wcount, sel8, upd, nw_dbg());
       else
-        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, dpg, rstart, elems, cstart, lo, d_fl,
+        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, dpg, rstart, rtot, elems, cstart, lo, d_fl,
                                                                    fstart, dng, kbits, wcount, sel8, upd, nw_dbg());
       SYZ_LAUNCHED();
     }

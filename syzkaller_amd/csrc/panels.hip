@@ -20,6 +20,7 @@
 // (syzgpu_minimize_grouped's output) are produced on the device in the same call.
 // Integer work throughout: bit-exact by construction (F2); tests/test_gpu_raw.py checks every output.
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <memory>
 #include <numeric>
@@ -127,7 +128,7 @@ __device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t 
 // The direct table's index: the offset rotated right by 2 bits inside the window, so PCs on 4-byte
 // instruction boundaries (arm64, and the synthetic corpora) fill every LDS bank, not a quarter of them
 __device__ __forceinline__ uint32_t tab_index(uint32_t o) { return ((o >> 2) | (o << (DS - 2))) & ((1u << DS) - 1); }
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_pmin_direct(const PItem* items, const PGroup* pg, const uint64_t* rstart,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_pmin_direct(const PItem* items, const PGroup* pg, const uint64_t* rstart, const uint32_t* rtot,
                                                       const uint32_t* elems,
                                                       const uint32_t* __restrict__ rank_of_member,
                                                       const uint64_t* gstart, uint8_t* sel8, int dbg) {
@@ -142,14 +143,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 4))) vo
   __syncthreads();
   if (dbg & 1) {  // timing only: the walk without its table updates
     uint32_t acc = 0;
-    for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, elems, rank_of_member,
+    for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, rtot, elems, rank_of_member,
                                 [&](uint32_t o, uint32_t R) { acc += o ^ R; });
     if (acc == 0x9E3779B9u) sel8[0] = 1;
   } else if (dbg & 8) {  // timing only: no rank gathers
-    for_region<SYZ_RG_U, true>(it, pg, gstart, rstart, elems, nullptr,
+    for_region<SYZ_RG_U, true>(it, pg, gstart, rstart, rtot, elems, nullptr,
                                [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
   } else {
-    for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, elems, rank_of_member,
+    for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, rtot, elems, rank_of_member,
                                 [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
   }
   __syncthreads();
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 4))) vo
 
 // PCs of one (call, window): the lengths of its segments' regions
 __device__ __forceinline__ uint32_t window_elem_count(const PItem it, const PGroup* pg, const uint64_t* gstart,
-                                                     const uint64_t* rstart) {
+                                                     const uint32_t* rtot) {
   const PGroup p = pg[it.g];
   const uint32_t sb = 32 - p.S;
   const uint64_t ng = gstart[it.g + 1] - gstart[it.g];
@@ -168,7 +169,7 @@ __device__ __forceinline__ uint32_t window_elem_count(const PItem it, const PGro
   uint64_t e = 0;
   for (uint32_t s = 0; s < nseg; s++) {
     const uint32_t r = p.rb + s * p.W + it.w;
-    e += rstart[r + 1] - rstart[r];
+    e += rtot[r];
   }
   return (uint32_t)e;
 }
@@ -194,7 +195,7 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 // offset << 13 | rank - the group's first rank, inserted by CAS and lowered by atomicMin (equal high
 // bits, so the min is the min rank), 16K slots in the 64 KB of the 8K key/value pairs.
 template <bool PACKED>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pmin_hash(const PItem* items, const PGroup* pg, const uint64_t* rstart,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pmin_hash(const PItem* items, const PGroup* pg, const uint64_t* rstart, const uint32_t* rtot,
                                                     const uint32_t* elems,
                                                     const uint32_t* __restrict__ rank_of_member,
                                                     const uint64_t* gstart, uint8_t* sel8, int dbg) {
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
   uint32_t* vals = tabs + HS;
   const PItem it = items[blockIdx.x];
   const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
-  const uint32_t E = window_elem_count(it, pg, gstart, rstart);
+  const uint32_t E = window_elem_count(it, pg, gstart, rtot);
   if (E == 0) return;
   uint32_t R = (E + CAP - 1) / CAP;
   for (uint32_t round = 0; round < R;) {
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     __syncthreads();
     const uint32_t RR = R, rr = round;
     uint32_t acc = 0;
-    for_region<SYZ_PK_HU, false>(it, pg, gstart, rstart, elems, rank_of_member, [&](uint32_t o, uint32_t Rk) {
+    for_region<SYZ_PK_HU, false>(it, pg, gstart, rstart, rtot, elems, rank_of_member, [&](uint32_t o, uint32_t Rk) {
                                          if (Rk == RANK_NONE) return;  // a lane past the window
                                          if (dbg & 64) {
                                            acc ^= o * 31 + Rk;
@@ -386,6 +387,18 @@ static int rg_dbg() {
   return v;
 }
 
+// SYZGPU_PM_BATCHES: batches of call groups the raw pipeline is cut into (default 1: more batches
+// were measured slower, the overlapping passes compete for the same CUs and slow the Go sort)
+static uint32_t pm_batches() {
+  static const uint32_t v = getenv("SYZGPU_PM_BATCHES") ? (uint32_t)std::max(1, atoi(getenv("SYZGPU_PM_BATCHES"))) : 1u;
+  return v;
+}
+
+static bool pm_p2() {
+  static const bool v = getenv("SYZGPU_PM_P2") && atoi(getenv("SYZGPU_PM_P2")) != 0;
+  return v;
+}
+
 static int pm_dbg() {
   static const int v = getenv("SYZGPU_PM_DBG") ? atoi(getenv("SYZGPU_PM_DBG")) : 0;
   return v;
@@ -504,6 +517,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   std::vector<PGroup> hpg;
   plan_windows(spanw, hpcs.data(), hstart.data(), G, hpg);
   std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
+  std::vector<uint64_t> hgel(G + 1, 0), hcb(G, 0);  // a group's first element; its chunk bound
+  std::vector<size_t> hcolg(G + 1, 0);              // a group's first column-scan item
   uint64_t chunk_bound = 0, total_pcs = 0, nreg = 0, desc_bound = 0;
   std::vector<ColItem> hcol;  // column-scan items: (group, segment, 64 windows)
   for (uint32_t g = 0; g < G; g++) {
@@ -512,8 +527,10 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     hgblock[g + 1] = hgblock[g] + nb;
     hbgroup.insert(hbgroup.end(), nb, g);
     const uint64_t cb = nb + (hpcs[g] + PCAP - 1) / PCAP;  // a key part holds at most the whole group
+    hcb[g] = cb;
     chunk_bound += cb;
     desc_bound += cb * (hpg[g].W + 1);
+    hgel[g] = total_pcs;
     total_pcs += hsl[g];
     // regions: one per (member segment, window); a group's PCs must fit 32-bit places
     if (hpcs[g] >= (1ull << 32)) fail(SYZGPU_EINVAL, "a call group with 2^32 or more PCs");
@@ -522,19 +539,48 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     hpg[g].rb = (uint32_t)nreg;
     nreg += (uint64_t)nseg * hpg[g].W;
     if (nreg >= (1ull << 31)) fail(SYZGPU_EINVAL, "too many PC regions");
+    hcolg[g] = hcol.size();
     for (uint32_t sg = 0; sg < nseg; sg++)
       for (uint32_t w0 = 0; w0 < hpg[g].W; w0 += 64) hcol.push_back(ColItem{g, sg, w0, 0});
   }
+  hgel[G] = total_pcs;
+  hcolg[G] = hcol.size();
   const uint32_t B = hgblock[G];
-  // work items: (call, window), the big groups (sorted by the global rounds) first, each class by
-  // mode, largest expected window first so the tail of the grid is short; a key part only its windows
+  // batches: contiguous ranges of call groups of similar size (no group split), taken from the last
+  // group to the first; each batch's P (count, column scan, region starts, scatter) and M run as soon
+  // as their inputs are ready, so one batch's scatter overlaps the next one's count and the previous
+  // one's M
+  struct Batch {
+    uint32_t g0, g1;
+    uint64_t cb;
+  };
+  std::vector<Batch> batches;
+  {
+    const uint64_t target = std::max<uint64_t>(1, (chunk_bound + pm_batches() - 1) / pm_batches());
+    uint32_t g1 = G;
+    uint64_t acc = 0;
+    for (uint32_t g = G; g-- > 0;) {
+      acc += hcb[g];
+      if (acc >= target || g == 0) {
+        batches.push_back(Batch{g, g1, acc});
+        g1 = g;
+        acc = 0;
+      }
+    }
+  }
+  const size_t NB = batches.size();
+  std::vector<uint32_t> gbatch(G, 0);
+  for (size_t b = 0; b < NB; b++)
+    for (uint32_t g = batches[b].g0; g < batches[b].g1; g++) gbatch[g] = (uint32_t)b;
+  // work items: (call, window) per batch, class (big groups: sorted by the global rounds) and mode,
+  // largest expected window first so the tail of the grid is short; a key part only its windows
   const auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
   std::vector<uint32_t> order(G);
   std::iota(order.begin(), order.end(), 0u);
   std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
     return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W;
   });
-  std::vector<PItem> items[2][3];  // [big][mode]
+  std::vector<std::array<std::array<std::vector<PItem>, 3>, 2>> items(NB);  // [batch][big][mode]
   uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};  // PCs the items of each class walk (the M byte models)
   for (uint32_t g : order) {
     if (!hpcs[g]) continue;
@@ -545,22 +591,25 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       w0 = (klo - lo) >> hpg[g].S;
       w1 = std::min<uint32_t>(hpg[g].W, ((khi - lo) >> hpg[g].S) + 1);
     }
-    auto& v = items[is_big(g) ? 1 : 0][hpg[g].mode];
+    auto& v = items[gbatch[g]][is_big(g) ? 1 : 0][hpg[g].mode];
     for (uint32_t w = w0; w < w1; w++) v.push_back(PItem{g, w});
     item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
   }
   PGroup* dpg = sc.get<PGroup>("pm_pg", G + 1);
   uint32_t* dgblock = sc.get<uint32_t>("pm_gblock", G + 1);
   uint32_t* dbgroup = sc.get<uint32_t>("pm_bgroup", (size_t)B + 1);
+  uint64_t* dgel = sc.get<uint64_t>("pm_gel0", G + 1);
   size_t nitems = 0;
-  for (auto& r : items)
-    for (auto& v : r) nitems += v.size();
+  for (auto& bi : items)
+    for (auto& r : bi)
+      for (auto& v : r) nitems += v.size();
   PItem* ditems = sc.get<PItem>("pm_items", nitems + 1);
   // host staging in pinned memory: one synchronous point below covers the copies
   ColItem* dcol = sc.get<ColItem>("pm_colitems", hcol.size() + 1);
-  const size_t stage_bytes = (G + 1) * sizeof(PGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 +
+  const size_t stage_bytes = (G + 1) * sizeof(PGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 + (G + 1) * 8 +
                              (nitems + 1) * sizeof(PItem) + (hcol.size() + 1) * sizeof(ColItem);
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
+  std::vector<std::array<std::array<size_t, 3>, 2>> ifirst(NB);  // first item of [batch][big][mode]
   {
     uint8_t* p = stage;
     std::memcpy(p, hpg.data(), G * sizeof(PGroup));
@@ -574,12 +623,18 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       SYZ_HIP(hipMemcpyAsync(dbgroup, p, (size_t)B * 4, hipMemcpyHostToDevice, s));
     }
     p += ((size_t)B + 1) * 4;
+    std::memcpy(p, hgel.data(), (G + 1) * 8);
+    SYZ_HIP(hipMemcpyAsync(dgel, p, (G + 1) * 8, hipMemcpyHostToDevice, s));
+    p += (G + 1) * 8;
     size_t k = 0;
-    for (auto& r : items)
-      for (auto& v : r) {
-        if (!v.empty()) std::memcpy(p + k * sizeof(PItem), v.data(), v.size() * sizeof(PItem));
-        k += v.size();
-      }
+    for (size_t b = 0; b < NB; b++)
+      for (int big = 0; big < 2; big++)
+        for (int m = 0; m < 3; m++) {
+          const auto& v = items[b][big][m];
+          ifirst[b][big][m] = k;
+          if (!v.empty()) std::memcpy(p + k * sizeof(PItem), v.data(), v.size() * sizeof(PItem));
+          k += v.size();
+        }
     if (nitems) SYZ_HIP(hipMemcpyAsync(ditems, p, nitems * sizeof(PItem), hipMemcpyHostToDevice, s));
     p += (nitems + 1) * sizeof(PItem);
     if (!hcol.empty()) {
@@ -609,91 +664,96 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   }
   k_gchunk<<<1, 1024, 0, s>>>(dgblock, G, cstart, dpg, gchunk, gdesc);
   SYZ_LAUNCHED();
-  // ---- P on its own stream, beside the Go sort ----
+  // ---- P on two streams of their own (count, scatter), beside the Go sort ----
   if (!c.part) {
-    // SYZGPU_PART_RESERVE=k: P's stream may not use k of every 32 CUs, which stay free for the Go
-    // sort's latency-bound rounds (the step's other branch); 0: the whole chip, lowest priority
-    static const int reserve = getenv("SYZGPU_PART_RESERVE") ? atoi(getenv("SYZGPU_PART_RESERVE")) : 0;
-    if (reserve > 0 && reserve < 32) {
-      if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
-      std::vector<uint32_t> mask((c.ncu + 31) / 32, 0);
-      for (int cu = 0; cu < c.ncu; cu++)
-        if (cu % 32 >= reserve) mask[cu / 32] |= 1u << (cu % 32);
-      SYZ_HIP(hipExtStreamCreateWithCUMask(&c.part, (uint32_t)mask.size() * 32, mask.data()));
-    } else {
-      int least = 0, greatest = 0;
-      SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
-    }
+    int least = 0, greatest = 0;
+    SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
+    // (a fourth stream costs the Go sort its hardware-queue share even while idle: only when asked for)
+    if (pm_p2()) SYZ_HIP(hipStreamCreateWithPriority(&c.part2, hipStreamNonBlocking, least));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
   }
+  while (c.ev_cnt.size() < NB) {
+    hipEvent_t e1, e2;
+    SYZ_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+    c.ev_cnt.push_back(e1);
+    c.ev_sct.push_back(e2);
+  }
   // SYZGPU_PM_SERIAL=1 (timing experiments): P on the main stream, before the sort
-  hipStream_t pq = pm_serial() ? s : c.part;
+  // SYZGPU_PM_P2=1: the scatter passes on a second stream (a fourth hardware queue: measured slower,
+  // the Go sort's latency-bound rounds lose their queue share)
+  hipStream_t pq = pm_serial() ? s : c.part, pq2 = pm_serial() ? s : (pm_p2() ? c.part2 : c.part);
   SYZ_HIP(hipEventRecord(c.ev_part0, s));
   SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
-  if (chunk_bound) {
+  if (c.part2) SYZ_HIP(hipStreamWaitEvent(c.part2, c.ev_part0, 0));
+  for (size_t b = 0; b < NB; b++) {
+    const Batch bt = batches[b];
+    const uint64_t bpcs = hgel[bt.g1] - hgel[bt.g0], bn = hstart[bt.g1] - hstart[bt.g0];
     // byte model: every PC read twice (count, scatter) and written once as a 4-byte element, plus 24 B
     // of member metadata per entry per pass (members, mpos, off, slice)
-    {
-      ProfScope ps("k_region_count", pq, total_pcs * 4 + (uint64_t)n * 24);
-      k_region<P3_BLOCK, P3_TPW, false, true><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
-          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gstart, gchunk, gdesc, lo, cnt, nullptr,
+    if (bt.cb) {
+      ProfScope ps("k_region_count", pq, bpcs * 4 + bn * 24);
+      k_region<P3_BLOCK, P3_TPW, false, true><<<(unsigned)bt.cb, P3_BLOCK, 0, pq>>>(
+          a.pcs, a.off, members, mpos, sbeg, chunks, bt.g0, bt.g1, dpg, gstart, gchunk, gdesc, lo, cnt, nullptr,
           nullptr, nullptr, err, NovSrc{}, rg_dbg());
       SYZ_LAUNCHED();
     }
     {
-      ProfScope ps("k_colscan", pq, desc_bound * 8);
-      k_colscan<<<(unsigned)hcol.size(), CS_BLOCK, 0, pq>>>(dcol, dpg, gstart, dgblock, cstart, gchunk, gdesc, cnt,
-                                                           colpre, rtot);
+      const size_t ncol = hcolg[bt.g1] - hcolg[bt.g0];
+      ProfScope ps("k_colscan", pq, 0);
+      if (ncol) {
+        k_colscan<<<(unsigned)ncol, CS_BLOCK, 0, pq>>>(dcol + hcolg[bt.g0], dpg, gstart, dgblock, cstart, gchunk,
+                                                       gdesc, cnt, colpre, rtot);
+        SYZ_LAUNCHED();
+      }
+      k_rstart<<<bt.g1 - bt.g0, RS_BLOCK, 0, pq>>>(bt.g0, dpg, gstart, dgel, rtot, rstart);
       SYZ_LAUNCHED();
     }
-    exclusive_scan_u32(rtot, rstart, nreg, pq, "rg");
-    {
-      ProfScope ps("k_region", pq, total_pcs * 8 + (uint64_t)n * 24);
-      k_region<P3_BLOCK, P3_TPW, false, false><<<(unsigned)chunk_bound, P3_BLOCK, 0, pq>>>(
-          a.pcs, a.off, members, mpos, sbeg, chunks, cstart + B, dpg, gstart, gchunk, gdesc, lo, cnt, colpre,
+    if (pq2 != pq) {
+      SYZ_HIP(hipEventRecord(c.ev_cnt[b], pq));
+      SYZ_HIP(hipStreamWaitEvent(pq2, c.ev_cnt[b], 0));
+    }
+    if (bt.cb) {
+      ProfScope ps("k_region", pq2, bpcs * 8 + bn * 24);
+      k_region<P3_BLOCK, P3_TPW, false, false><<<(unsigned)bt.cb, P3_BLOCK, 0, pq2>>>(
+          a.pcs, a.off, members, mpos, sbeg, chunks, bt.g0, bt.g1, dpg, gstart, gchunk, gdesc, lo, cnt, colpre,
           rstart, elems, err, NovSrc{}, rg_dbg());
       SYZ_LAUNCHED();
     }
+    SYZ_HIP(hipEventRecord(c.ev_sct[b], pq2));
   }
-  SYZ_HIP(hipEventRecord(c.ev_part1, pq));
-  // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
+  SYZ_HIP(hipEventRecord(c.ev_part1, pq2));
+  // ---- Go-sort ranks, then M per class and batch as soon as its own sort and scatter are done ----
   uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
   SYZ_HIP(hipMemsetAsync(sel8, 0, (n + 31) / 32 * 32 + 64, s));
-  // ditems holds the classes in order (small, big), each as its direct, hash, packed items
-  size_t ifirst[2][3];
-  {
-    size_t k = 0;
-    for (int b = 0; b < 2; b++)
-      for (int m = 0; m < 3; m++) {
-        ifirst[b][m] = k;
-        k += items[b][m].size();
-      }
-  }
   // byte model of M: every element read once (4 B per PC of the class's groups)
   auto run_m = [&](hipStream_t q, int big) {
-    SYZ_HIP(hipStreamWaitEvent(q, c.ev_part1, 0));
     ProfScope ps(big ? "m_big" : "m_small", q, 0);
-    const size_t nd = items[big][PMODE_DIRECT].size(), nh = items[big][PMODE_HASH].size(),
-                 np = items[big][PMODE_PACKED].size();
-    if (nd) {
-      ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
-      k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], dpg, rstart, elems,
-                                                   rank_of_member, gstart, sel8, pm_dbg());
-      SYZ_LAUNCHED();
-    }
-    if (nh && !(pm_dbg() & 4)) {
-      ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
-      k_pmin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[big][PMODE_HASH], dpg, rstart, elems,
-                                                        rank_of_member, gstart, sel8, pm_dbg());
-      SYZ_LAUNCHED();
-    }
-    if (np && !(pm_dbg() & 4)) {
-      ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
-      k_pmin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dpg, rstart, elems,
-                                                       rank_of_member, gstart, sel8, pm_dbg());
-      SYZ_LAUNCHED();
+    for (size_t b = 0; b < NB; b++) {
+      const auto& it = items[b][big];
+      const size_t nd = it[PMODE_DIRECT].size(), nh = it[PMODE_HASH].size(), np = it[PMODE_PACKED].size();
+      if (!nd && !nh && !np) continue;
+      SYZ_HIP(hipStreamWaitEvent(q, c.ev_sct[b], 0));
+      if (nd) {
+        ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
+        k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[b][big][PMODE_DIRECT], dpg, rstart, rtot, elems,
+                                                     rank_of_member, gstart, sel8, pm_dbg());
+        SYZ_LAUNCHED();
+      }
+      if (nh && !(pm_dbg() & 4)) {
+        ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
+        k_pmin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[b][big][PMODE_HASH], dpg, rstart, rtot,
+                                                          elems, rank_of_member, gstart, sel8, pm_dbg());
+        SYZ_LAUNCHED();
+      }
+      if (np && !(pm_dbg() & 4)) {
+        ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
+        k_pmin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[b][big][PMODE_PACKED], dpg, rstart, rtot,
+                                                         elems, rank_of_member, gstart, sel8, pm_dbg());
+        SYZ_LAUNCHED();
+      }
     }
   };
   if (!J.plan || J.plan_key != hstart) {
@@ -721,9 +781,12 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   J.stats_total_pcs = total_pcs;
-  J.stats_items_direct = items[0][PMODE_DIRECT].size() + items[1][PMODE_DIRECT].size();
-  J.stats_items_hash = items[0][PMODE_HASH].size() + items[1][PMODE_HASH].size() + items[0][PMODE_PACKED].size() +
-                       items[1][PMODE_PACKED].size();
+  J.stats_items_direct = J.stats_items_hash = 0;
+  for (const auto& bi : items)
+    for (int big = 0; big < 2; big++) {
+      J.stats_items_direct += bi[big][PMODE_DIRECT].size();
+      J.stats_items_hash += bi[big][PMODE_HASH].size() + bi[big][PMODE_PACKED].size();
+    }
   if (herr[0] & 1) {
     if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
     return false;

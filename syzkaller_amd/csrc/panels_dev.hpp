@@ -541,7 +541,7 @@ template <int BLOCK, int TPW, bool NOV = false, bool COUNT = false>
 __global__ __launch_bounds__(BLOCK) void k_region(
     const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
     const uint64_t* __restrict__ mpos, const uint32_t* __restrict__ sbeg, const PChunk* chunks,
-    const uint64_t* nchunks_dev, const PGroup* pg, const uint64_t* gstart, const uint64_t* gchunk,
+    uint32_t g0, uint32_t g1, const PGroup* pg, const uint64_t* gstart, const uint64_t* gchunk,
     const uint64_t* gdesc, uint32_t lo, uint16_t* cnt, const uint32_t* colpre, const uint64_t* rstart,
     uint32_t* __restrict__ elems, int* err, NovSrc ns = NovSrc{}, int dbg = 0) {
   constexpr int WAVES = BLOCK / 64;
@@ -556,8 +556,8 @@ __global__ __launch_bounds__(BLOCK) void k_region(
   __shared__ uint4 tinfo[TMAX];
   __shared__ uint32_t tlast[NOV && COUNT ? TMAX : 1];
   __shared__ uint8_t mtab[NOV ? MEMB : 1];
-  const uint64_t c = blockIdx.x;
-  if (c >= *nchunks_dev) return;
+  const uint64_t c = gchunk[g0] + blockIdx.x;  // the chunks of call groups [g0, g1)
+  if (c >= gchunk[g1]) return;
   const int wv = threadIdx.x >> 6;
   const unsigned lane = __lane_id();
   const PChunk ch = chunks[c];
@@ -757,6 +757,29 @@ __global__ __launch_bounds__(BLOCK) void k_region(
   }
 }
 
+// Region starts of call groups [g0, g1) (one workgroup per group): the group's first element (gel0, its
+// place in the element buffer) + the exclusive scan of its regions' totals.
+constexpr int RS_BLOCK = 1024;
+static __global__ __launch_bounds__(RS_BLOCK) void k_rstart(uint32_t g0, const PGroup* pg, const uint64_t* gstart,
+                                                           const uint64_t* gel0, const uint32_t* rtot,
+                                                           uint64_t* rstart) {
+  __shared__ uint64_t red[RS_BLOCK / 64 + 1];
+  const uint32_t g = g0 + blockIdx.x;
+  const PGroup gp = pg[g];
+  const uint32_t sb = 32 - gp.S;
+  const uint64_t ng = gstart[g + 1] - gstart[g];
+  const uint32_t nr = (uint32_t)((ng + (1ull << sb) - 1) >> sb) * gp.W;
+  uint64_t run = gel0[g];
+  for (uint32_t b0 = 0; b0 < nr; b0 += RS_BLOCK) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint64_t x = i < nr ? rtot[gp.rb + i] : 0;
+    uint64_t tot;
+    const uint64_t pre = block_excl_scan<RS_BLOCK>(x, red, &tot) + run;
+    if (i < nr) rstart[gp.rb + i] = pre;
+    run += tot;
+  }
+}
+
 // Column scan of the COUNT rows: one workgroup per (group, member segment, 64 windows); lane = window,
 // wave k takes the k-th slice of the segment's chunks. colpre[row(c) + w] = PCs of window w in the
 // segment's chunks before c; rtot[region] = the column's total.
@@ -829,7 +852,7 @@ static __global__ __launch_bounds__(CS_BLOCK) void k_colscan(const ColItem* item
 // a copy between them would wait for the loads), so a wave waits on its gathers with loads in flight.
 template <int U, bool IDENT, class F>
 __device__ __forceinline__ void for_region(const PItem it, const PGroup* pg, const uint64_t* gstart,
-                                           const uint64_t* rstart, const uint32_t* elems,
+                                           const uint64_t* rstart, const uint32_t* rtot, const uint32_t* elems,
                                            const uint32_t* __restrict__ rank_of_member, F f) {
   const uint32_t g = it.g, w = it.w;
   const PGroup p = pg[g];
@@ -839,7 +862,7 @@ __device__ __forceinline__ void for_region(const PItem it, const PGroup* pg, con
   const uint32_t BD = blockDim.x;
   for (uint32_t s = 0; s < nseg; s++) {
     const uint32_t r = p.rb + s * p.W + w;
-    const uint64_t a = rstart[r], b = rstart[r + 1];
+    const uint64_t a = rstart[r], b = a + rtot[r];
     if (a == b) continue;
     const uint64_t a4 = a & ~3ull;
     const uint32_t lo4 = (uint32_t)(a - a4), hi4 = (uint32_t)(b - a4);  // valid slots [lo4, hi4)
