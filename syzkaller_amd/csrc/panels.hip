@@ -71,10 +71,38 @@ __global__ __launch_bounds__(256) void k_minmax(const uint32_t* pcs, size_t L, u
   block_span_update<256>(lo, hi, span);
 }
 
-// PCs of each call group this job reads (its members' slices): the exact byte model of the kernels
-__global__ void k_gslice(const uint64_t* gstart, const uint64_t* mpos, uint32_t G, uint64_t* gsl) {
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x)
-    gsl[g] = mpos[gstart[g + 1]] - mpos[gstart[g]];
+// the job's per-step state: error word, per-group PC sums, the PC span
+__global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x) {
+    gpcs[g] = 0;
+    if (g < 2) {
+      err[g] = 0;
+      span[g] = g ? 0u : 0xFFFFFFFFu;
+    }
+  }
+}
+
+// What the host plans the windows from, in one buffer (one copy back): gstart[G + 1], the PCs of each
+// call group gpcs[G], the span, the error word, and the PCs of each call group this job reads (its
+// members' slices: the exact byte model of the kernels) gsl[G]
+__global__ void k_gpack(const uint64_t* gstart, const uint64_t* gpcs, const uint32_t* span, const int* err,
+                        const uint64_t* mpos, uint32_t G, uint64_t* out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * G + 3; i += gridDim.x * blockDim.x) {
+    uint64_t v;
+    if (i <= G)
+      v = gstart[i];
+    else if (i < 2 * G + 1)
+      v = gpcs[i - G - 1];
+    else if (i == 2 * G + 1)
+      v = ((uint64_t)span[1] << 32) | span[0];
+    else if (i == 2 * G + 2)
+      v = ((uint64_t)(uint32_t)err[1] << 32) | (uint32_t)err[0];
+    else {
+      const uint32_t g = i - 2 * G - 3;
+      v = mpos[gstart[g + 1]] - mpos[gstart[g]];
+    }
+    out[i] = v;
+  }
 }
 
 __global__ void k_mlen(const uint64_t* el, size_t n, uint32_t* mlen) {
@@ -461,13 +489,9 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint32_t* mlen = sc.get<uint32_t>("pm_mlen", n + 1);
   uint32_t* sbeg = a.key_lo ? sc.get<uint32_t>("pm_sbeg", n + 1) : nullptr;
   uint64_t* mpos = sc.get<uint64_t>("pm_mpos", n + 1);
-  uint64_t* gsl = sc.get<uint64_t>("pm_gsl", G + 1);
-  SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
-  SYZ_HIP(hipMemsetAsync(gpcs, 0, (G + 1) * 8, s));
-  uint32_t* hinit = c.pinned.get<uint32_t>(16);
-  hinit[0] = 0xFFFFFFFFu;
-  hinit[1] = 0;
-  SYZ_HIP(hipMemcpyAsync(span, hinit, 8, hipMemcpyHostToDevice, s));
+  uint64_t* gpack = sc.get<uint64_t>("pm_gpack", 3 * (size_t)G + 4);
+  k_pm_init<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(err, gpcs, G, span);
+  SYZ_LAUNCHED();
   uint32_t* krange = nullptr;
   if (a.key_lo) {
     std::vector<uint32_t> kr(2 * (size_t)G);
@@ -492,15 +516,11 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       SYZ_LAUNCHED();
     }
     exclusive_scan_u32(mlen, mpos, n, s);
-    k_gslice<<<grid_for(G, 256, 64), 256, 0, s>>>(gstart, mpos, G, gsl);
+    k_gpack<<<grid_for(3 * (size_t)G + 3, 256, 64), 256, 0, s>>>(gstart, gpcs, span, err, mpos, G, gpack);
     SYZ_LAUNCHED();
   }
   uint64_t* hbuf = c.pinned.get<uint64_t>(3 * (size_t)G + 8);
-  SYZ_HIP(hipMemcpyAsync(hbuf, gstart, (G + 1) * 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(hbuf + G + 1, gpcs, G * 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(hbuf + 2 * G + 1, span, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(hbuf + 2 * G + 2, err, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(hbuf + 2 * G + 3, gsl, G * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hbuf, gpack, (3 * (size_t)G + 3) * 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   if (*reinterpret_cast<int*>(hbuf + 2 * G + 2)) fail(SYZGPU_EINVAL, "group id >= ngroups");
   std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
@@ -595,52 +615,42 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     for (uint32_t w = w0; w < w1; w++) v.push_back(PItem{g, w});
     item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
   }
-  PGroup* dpg = sc.get<PGroup>("pm_pg", G + 1);
-  uint32_t* dgblock = sc.get<uint32_t>("pm_gblock", G + 1);
-  uint32_t* dbgroup = sc.get<uint32_t>("pm_bgroup", (size_t)B + 1);
-  uint64_t* dgel = sc.get<uint64_t>("pm_gel0", G + 1);
   size_t nitems = 0;
   for (auto& bi : items)
     for (auto& r : bi)
       for (auto& v : r) nitems += v.size();
-  PItem* ditems = sc.get<PItem>("pm_items", nitems + 1);
-  // host staging in pinned memory: one synchronous point below covers the copies
-  ColItem* dcol = sc.get<ColItem>("pm_colitems", hcol.size() + 1);
-  const size_t stage_bytes = (G + 1) * sizeof(PGroup) + (G + 1) * 4 + ((size_t)B + 1) * 4 + (G + 1) * 8 +
-                             (nitems + 1) * sizeof(PItem) + (hcol.size() + 1) * sizeof(ColItem);
+  // the plan goes over in one copy: PGroup[G + 1], gblock[G + 1], bgroup[B + 1], gel0[G + 1],
+  // items[nitems + 1], column-scan items (16-byte aligned parts)
+  auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
+  const size_t o_gb = al16((G + 1) * sizeof(PGroup)), o_bg = o_gb + al16((G + 1) * 4),
+               o_ge = o_bg + al16(((size_t)B + 1) * 4), o_it = o_ge + al16((G + 1) * 8),
+               o_co = o_it + al16((nitems + 1) * sizeof(PItem)),
+               stage_bytes = o_co + al16((hcol.size() + 1) * sizeof(ColItem));
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
+  uint8_t* dstage = sc.get<uint8_t>("pm_stage", stage_bytes + 64);
+  PGroup* dpg = reinterpret_cast<PGroup*>(dstage);
+  uint32_t* dgblock = reinterpret_cast<uint32_t*>(dstage + o_gb);
+  uint32_t* dbgroup = reinterpret_cast<uint32_t*>(dstage + o_bg);
+  uint64_t* dgel = reinterpret_cast<uint64_t*>(dstage + o_ge);
+  PItem* ditems = reinterpret_cast<PItem*>(dstage + o_it);
+  ColItem* dcol = reinterpret_cast<ColItem*>(dstage + o_co);
   std::vector<std::array<std::array<size_t, 3>, 2>> ifirst(NB);  // first item of [batch][big][mode]
   {
-    uint8_t* p = stage;
-    std::memcpy(p, hpg.data(), G * sizeof(PGroup));
-    SYZ_HIP(hipMemcpyAsync(dpg, p, G * sizeof(PGroup), hipMemcpyHostToDevice, s));
-    p += (G + 1) * sizeof(PGroup);
-    std::memcpy(p, hgblock.data(), (G + 1) * 4);
-    SYZ_HIP(hipMemcpyAsync(dgblock, p, (G + 1) * 4, hipMemcpyHostToDevice, s));
-    p += (G + 1) * 4;
-    if (B) {
-      std::memcpy(p, hbgroup.data(), (size_t)B * 4);
-      SYZ_HIP(hipMemcpyAsync(dbgroup, p, (size_t)B * 4, hipMemcpyHostToDevice, s));
-    }
-    p += ((size_t)B + 1) * 4;
-    std::memcpy(p, hgel.data(), (G + 1) * 8);
-    SYZ_HIP(hipMemcpyAsync(dgel, p, (G + 1) * 8, hipMemcpyHostToDevice, s));
-    p += (G + 1) * 8;
+    std::memcpy(stage, hpg.data(), G * sizeof(PGroup));
+    std::memcpy(stage + o_gb, hgblock.data(), (G + 1) * 4);
+    if (B) std::memcpy(stage + o_bg, hbgroup.data(), (size_t)B * 4);
+    std::memcpy(stage + o_ge, hgel.data(), (G + 1) * 8);
     size_t k = 0;
     for (size_t b = 0; b < NB; b++)
       for (int big = 0; big < 2; big++)
         for (int m = 0; m < 3; m++) {
           const auto& v = items[b][big][m];
           ifirst[b][big][m] = k;
-          if (!v.empty()) std::memcpy(p + k * sizeof(PItem), v.data(), v.size() * sizeof(PItem));
+          if (!v.empty()) std::memcpy(stage + o_it + k * sizeof(PItem), v.data(), v.size() * sizeof(PItem));
           k += v.size();
         }
-    if (nitems) SYZ_HIP(hipMemcpyAsync(ditems, p, nitems * sizeof(PItem), hipMemcpyHostToDevice, s));
-    p += (nitems + 1) * sizeof(PItem);
-    if (!hcol.empty()) {
-      std::memcpy(p, hcol.data(), hcol.size() * sizeof(ColItem));
-      SYZ_HIP(hipMemcpyAsync(dcol, p, hcol.size() * sizeof(ColItem), hipMemcpyHostToDevice, s));
-    }
+    if (!hcol.empty()) std::memcpy(stage + o_co, hcol.data(), hcol.size() * sizeof(ColItem));
+    SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
   }
   // ---- blocks -> chunks ----
   uint32_t* nsub = sc.get<uint32_t>("pm_nsub", (size_t)B + 1);
@@ -685,6 +695,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   // SYZGPU_PM_P2=1: the scatter passes on a second stream (a fourth hardware queue: measured slower,
   // the Go sort's latency-bound rounds lose their queue share)
   hipStream_t pq = pm_serial() ? s : c.part, pq2 = pm_serial() ? s : (pm_p2() ? c.part2 : c.part);
+  int* herr = c.pinned.get<int>(4);
   SYZ_HIP(hipEventRecord(c.ev_part0, s));
   SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
   if (c.part2) SYZ_HIP(hipStreamWaitEvent(c.part2, c.ev_part0, 0));
@@ -711,8 +722,12 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       k_rstart<<<bt.g1 - bt.g0, RS_BLOCK, 0, pq>>>(bt.g0, dpg, gstart, dgel, rtot, rstart);
       SYZ_LAUNCHED();
     }
-    if (pq2 != pq) {
+    if (b + 1 == NB) {  // the count passes' error word, as soon as the last one is done
+      SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, pq));
       SYZ_HIP(hipEventRecord(c.ev_cnt[b], pq));
+    }
+    if (pq2 != pq) {
+      if (b + 1 != NB) SYZ_HIP(hipEventRecord(c.ev_cnt[b], pq));
       SYZ_HIP(hipStreamWaitEvent(pq2, c.ev_cnt[b], 0));
     }
     if (bt.cb) {
@@ -777,9 +792,12 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     small_done(s);
     big_done(s);
   }
-  int* herr = c.pinned.get<int>(4);
-  SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
+  // the only error the passes report (a PC outside the planned windows) comes from the count passes:
+  // wait for their error word, not for the scatter and M (end() and the exchange queue behind M on
+  // their streams)
+  SYZ_HIP(hipEventSynchronize(c.ev_cnt[NB - 1]));
+  if (!J.done) SYZ_HIP(hipEventCreateWithFlags(&J.done, hipEventDisableTiming));
+  SYZ_HIP(hipEventRecord(J.done, s));  // (s has joined the small class's M)
   J.stats_total_pcs = total_pcs;
   J.stats_items_direct = J.stats_items_hash = 0;
   for (const auto& bi : items)
@@ -828,6 +846,7 @@ void minimize_raw_xchg(MinJob& J, const uint32_t* groups, const uint64_t* offset
     SYZ_HIP(hipStreamSynchronize(s));
     J.xkey = key;
   }
+  SYZ_HIP(hipStreamWaitEvent(s, J.done, 0));
   const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>(1, (maxn + 1023) / 1024), 1024);
   k_job_xchg<<<dim3(gx, ng), 256, 0, s>>>(J.sel8.p, J.gstart.p, J.xg.p, J.xo.p, buf, import);
   SYZ_LAUNCHED();
@@ -893,6 +912,7 @@ void minimize_raw_end(MinJob& J, const RawEndArgs& e) {
   const uint32_t G = J.G;
   hipStream_t s = e.s;
   int* err = sc.get<int>("mz_err", 2);
+  SYZ_HIP(hipStreamWaitEvent(s, J.done, 0));
   SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
   const uint8_t* dcount = nullptr;
   if (e.count_hist) {

@@ -66,6 +66,10 @@ struct MinJob {
   std::vector<uint64_t> plan_key;
   uint64_t stats_total_pcs = 0;
   size_t stats_items_direct = 0, stats_items_hash = 0;
+  hipEvent_t done = nullptr;  // begin's last work (M) on its stream: end / exchange / fetch wait for it
+  ~MinJob() {
+    if (done) (void)hipEventDestroy(done);
+  }
 };
 
 void minimize_raw_begin(MinJob& J, const RawMinArgs& a);
