@@ -200,6 +200,13 @@ def main():
             sharding.allreduce_max_u8(d_x, dist)
             if xg.size:
                 job.import_sel(xg, xo, d_x, sptr)
+        if world == 1:
+            # minimizeCorpus's tail in one call (manager.go:523-536): kept flags / list / length
+            # histogram, calcStaticPriorities (int8 MFMA) beside them, CalculatePriorities +
+            # BuildChoiceTable; one wait for the error checks
+            job.end_prio(C, d_uses, uses.shape[0], d_static, d_prios, d_run, count_hist if parts else None,
+                         d_sel, d_hist, d_out, d_goff, d_pres, sptr)
+            return
         job.end(C, count_hist if parts else None, d_sel, d_hist, d_out, d_goff, sptr)
         sharding.allreduce_hist(d_hist, dist)  # kept-length histogram: (C+1) int64
         # CalculatePriorities (prio.go:29-38): calcStaticPriorities (int8 MFMA) x normalized dynamic

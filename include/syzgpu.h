@@ -212,6 +212,14 @@ int syzgpu_mz_import_sel_dev(syzgpu_mz* job, const uint32_t* groups, const uint6
                              const uint8_t* buf, void* stream);
 int syzgpu_mz_end_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist, uint8_t* selected, int64_t* len_hist,
                       int64_t* out_idx, uint64_t* group_out_off, void* stream);
+/* minimizeCorpus's tail (syz-manager/manager.go:523-536) in one call: syzgpu_mz_end_dev's outputs (len_hist
+ * required), calcStaticPriorities of the usage matrix (prog/prio.go:40-135) into static_prios, and
+ * CalculatePriorities + BuildChoiceTable from the histogram (prio.go:29-38, 137-192, 202-228) into
+ * prios / run / row_present (may be NULL); the three error checks after one wait. */
+int syzgpu_mz_end_prio_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist, uint8_t* selected,
+                           int64_t* len_hist, int64_t* out_idx, uint64_t* group_out_off, const float* uses,
+                           size_t nkeys, float* static_prios, float* prios, int64_t* run, uint8_t* row_present,
+                           void* stream);
 int syzgpu_mz_fetch(syzgpu_mz* job, int64_t* out_idx, uint64_t* group_out_off);
 int syzgpu_mz_info(syzgpu_mz* job, uint64_t* info, size_t cap);
 

@@ -55,6 +55,8 @@ SIGNATURES = {
     "syzgpu_mz_export_sel_dev": (_c.c_int, [_vp, _vp, _vp, _c.c_uint32, _vp, _vp]),
     "syzgpu_mz_import_sel_dev": (_c.c_int, [_vp, _vp, _vp, _c.c_uint32, _vp, _vp]),
     "syzgpu_mz_end_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "syzgpu_mz_end_prio_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp,
+                                          _vp]),
     "syzgpu_mz_fetch": (_c.c_int, [_vp, _vp, _vp]),
     "syzgpu_mz_info": (_c.c_int, [_vp, _vp, _sz]),
     "syzgpu_prio_choice_dev": (_c.c_int, [_vp, _vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp]),

@@ -146,6 +146,15 @@ class MinimizeJob:
         check(lib().syzgpu_mz_end_dev(self._h, C, ptr(ch), ptr(d_selected), ptr(d_len_hist), ptr(d_out_idx),
                                       ptr(d_group_out_off), stream))
 
+    def end_prio(self, C, d_uses, nkeys, d_static, d_prios, d_run, count_hist=None, d_selected=None,
+                 d_len_hist=None, d_out_idx=None, d_group_out_off=None, d_row_present=None, stream=0):
+        """minimizeCorpus's tail (manager.go:523-536): end() + calcStaticPriorities + CalculatePriorities
+        + BuildChoiceTable in one call, on device buffers."""
+        ch = None if count_hist is None else np.ascontiguousarray(count_hist, np.uint8)
+        check(lib().syzgpu_mz_end_prio_dev(self._h, C, ptr(ch), ptr(d_selected), ptr(d_len_hist), ptr(d_out_idx),
+                                           ptr(d_group_out_off), ptr(d_uses), nkeys, ptr(d_static), ptr(d_prios),
+                                           ptr(d_run), ptr(d_row_present), stream))
+
     def fetch(self, n, ngroups):
         out = np.empty(max(n, 1), np.int64)
         goff = np.zeros(ngroups + 1, np.uint64)

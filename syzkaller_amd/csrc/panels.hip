@@ -26,6 +26,7 @@
 #include <numeric>
 
 #include "panels_dev.hpp"
+#include "pipeline.hpp"
 
 namespace syz {
 
@@ -929,12 +930,16 @@ void minimize_raw_end(MinJob& J, const RawEndArgs& e) {
     SYZ_LAUNCHED();
   }
   if (e.out_idx || e.group_out_off) sel_compact_dev(J.sel8.p, J.ent_of_rank.p, J.gstart.p, n, G, e.out_idx, e.group_out_off, s);
-  if (e.len_hist) {  // len(p.Calls) > C is Go's index-out-of-range panic (prio.go:148)
+  if (e.len_hist && !e.defer_check) {  // len(p.Calls) > C is Go's index-out-of-range panic (prio.go:148)
     int* herr = c.pinned.get<int>(4);
     SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
-    if (herr[0] & 2) fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
+    minimize_raw_end_check(herr[0]);
   }
+}
+
+void minimize_raw_end_check(int err) {
+  if (err & 2) fail(SYZGPU_EINVAL, "len(p.Calls) > C (prog/prio.go:148 would panic)");
 }
 
 // host copies of the group-major kept list (the syzgpu_minimize_grouped outputs)
@@ -1030,6 +1035,53 @@ int syzgpu_mz_end_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist, uint
     e.group_out_off = group_out_off;
     e.s = (hipStream_t)stream;
     minimize_raw_end(J, e);
+  })
+}
+
+// minimizeCorpus's tail in one call (manager.go:523-536): the kept flags, list and length histogram of
+// the job (syzgpu_mz_end_dev), calcStaticPriorities of the usage matrix on a second stream beside
+// them, then CalculatePriorities + BuildChoiceTable from the histogram (syzgpu_prio_choice_dev); the
+// error checks of all three after one wait.
+int syzgpu_mz_end_prio_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist, uint8_t* selected,
+                           int64_t* len_hist, int64_t* out_idx, uint64_t* group_out_off, const float* uses,
+                           size_t nkeys, float* static_prios, float* prios, int64_t* run, uint8_t* row_present,
+                           void* stream) {
+  SYZ_API_BODY({
+    if (!job) fail(SYZGPU_EINVAL, "null job");
+    if (!len_hist || !static_prios || !prios || !run) fail(SYZGPU_EINVAL, "null pointer");
+    MinJob& J = *reinterpret_cast<MinJob*>(job);
+    std::lock_guard<std::recursive_mutex> hl_(J.mu);
+    Context& c = ctx();
+    hipStream_t s = (hipStream_t)stream;
+    // calcStaticPriorities depends on the usage matrix only: on the side stream (idle once the small
+    // call groups' Minimize is done), joined before CalculatePriorities
+    hipStream_t ss = c.side ? c.side : s;
+    if (ss != s) {
+      SYZ_HIP(hipEventRecord(c.ev_fork, s));
+      SYZ_HIP(hipStreamWaitEvent(ss, c.ev_fork, 0));
+    }
+    const uint32_t* dserr = static_priorities_enqueue(uses, nkeys, C, static_prios, ss);
+    RawEndArgs e;
+    e.C = C;
+    e.count_hist = count_hist;
+    e.selected = selected;
+    e.len_hist = len_hist;
+    e.out_idx = out_idx;
+    e.group_out_off = group_out_off;
+    e.s = s;
+    e.defer_check = true;
+    minimize_raw_end(J, e);
+    if (ss != s) {
+      SYZ_HIP(hipEventRecord(c.ev_join, ss));
+      SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
+    }
+    prio_choice_dev(static_prios, len_hist, nullptr, C, nullptr, prios, run, row_present, s);
+    uint32_t* h = c.pinned.get<uint32_t>(8);
+    SYZ_HIP(hipMemcpyAsync(h, c.scratch.get<int>("mz_err", 2), 4, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipMemcpyAsync(h + 1, dserr, 4, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    minimize_raw_end_check((int)h[0]);
+    static_prio_check(h[1]);
   })
 }
 

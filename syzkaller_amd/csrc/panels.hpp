@@ -44,6 +44,7 @@ struct RawEndArgs {
   int64_t* out_idx = nullptr;           // device, kept entries group-major in selection order
   uint64_t* group_out_off = nullptr;    // device, G+1
   hipStream_t s = nullptr;
+  bool defer_check = false;             // leave the len(p.Calls) > C check to the caller (minimize_raw_end_check)
 };
 
 // One minimizeCorpus job (the raw path): its selection lives here between begin and end, so a
@@ -76,6 +77,7 @@ void minimize_raw_begin(MinJob& J, const RawMinArgs& a);
 void minimize_raw_xchg(MinJob& J, const uint32_t* groups, const uint64_t* offsets, uint32_t ng, uint8_t* buf,
                        int import, hipStream_t s);
 void minimize_raw_end(MinJob& J, const RawEndArgs& e);
+void minimize_raw_end_check(int err);  // the deferred check of end's device error word (mz_err)
 void minimize_raw_fetch(MinJob& J, int64_t* out_idx, uint64_t* group_out_off);
 void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, uint32_t G, std::vector<PGroup>& pg);
 // group-major kept list (device) from a rank bitmap

@@ -56,6 +56,9 @@ void canonicalize_batch_dev(uint32_t* pcs, const uint64_t* off, const uint64_t* 
 // prio.hip
 void len_hist_dev(const uint16_t* prog_len, const uint8_t* sel, size_t n, int32_t C, int64_t* hist, int* err,
                   hipStream_t s);
+// calcStaticPriorities (static_prio.hip): enqueue only, and the check of its device error word
+const uint32_t* static_priorities_enqueue(const float* uses, size_t nkeys, int32_t C, float* prios, hipStream_t s);
+void static_prio_check(uint32_t err);
 void prio_choice_dev(const float* static_prios, const int64_t* len_hist, const float* prios_in, int32_t C,
                      const uint8_t* enabled, float* prios_out, int64_t* run, uint8_t* present, hipStream_t s);
 

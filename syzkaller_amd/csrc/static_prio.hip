@@ -151,8 +151,9 @@ __global__ __launch_bounds__(64) void k_st_gram(const int8_t* __restrict__ X, in
 
 void static_prio_rows_dev(float* prios, int32_t C, hipStream_t s);  // prio.hip
 
-// prios = calcStaticPriorities() of the usage matrix (device pointers); returns after the error check
-void static_priorities_dev(const float* uses, size_t nkeys, int32_t C, float* prios, hipStream_t s) {
+// prios = calcStaticPriorities() of the usage matrix (device pointers), enqueued on s; returns the device
+// word whose bits static_prio_check reads (after s has run)
+const uint32_t* static_priorities_enqueue(const float* uses, size_t nkeys, int32_t C, float* prios, hipStream_t s) {
   if (C <= 0 || C > 16384) fail(SYZGPU_EINVAL, "C out of range");
   if (nkeys >= (1u << 24)) fail(SYZGPU_EINVAL, "too many usage keys");
   if (!prios || (nkeys && !uses)) fail(SYZGPU_EINVAL, "null pointer");
@@ -178,11 +179,21 @@ void static_priorities_dev(const float* uses, size_t nkeys, int32_t C, float* pr
   k_st_gram<<<dim3(Cp / 32, Cp / 32), 64, 0, s>>>(X, C, Cp, Kp, cl, prios);
   SYZ_LAUNCHED();
   static_prio_rows_dev(prios, C, s);
-  uint32_t* h = c.pinned.get<uint32_t>(4);
-  SYZ_HIP(hipMemcpyAsync(h, &cl->err, 4, hipMemcpyDeviceToHost, s));
+  return &cl->err;
+}
+
+void static_prio_check(uint32_t err) {
+  if (err & 2) fail(SYZGPU_EINVAL, "non-finite usage weight");
+  if (err & 1) fail(SYZGPU_EINVAL, "more than 8 distinct usage weights");
+}
+
+// the same, returning after the error check
+void static_priorities_dev(const float* uses, size_t nkeys, int32_t C, float* prios, hipStream_t s) {
+  const uint32_t* derr = static_priorities_enqueue(uses, nkeys, C, prios, s);
+  uint32_t* h = ctx().pinned.get<uint32_t>(4);
+  SYZ_HIP(hipMemcpyAsync(h, derr, 4, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
-  if (h[0] & 2) fail(SYZGPU_EINVAL, "non-finite usage weight");
-  if (h[0] & 1) fail(SYZGPU_EINVAL, "more than 8 distinct usage weights");
+  static_prio_check(h[0]);
 }
 
 }  // namespace syz

@@ -182,3 +182,53 @@ def test_len_hist_rejects_long_programs(torch):
     pl[:] = 99  # every kept program is longer than C
     with pytest.raises(_lib.SyzGpuError):
         run_dev(torch, c.pcs, c.off, c.group, 5, pl, 40)
+
+
+def test_end_prio_fused_tail_matches_oracle(torch):
+    # syzgpu_mz_end_prio_dev: minimizeCorpus's tail (manager.go:523-536) in one call — kept list, flags
+    # and length histogram of the job, calcStaticPriorities of the bundled sys/ usage matrix, then
+    # CalculatePriorities + BuildChoiceTable — against the oracle of each piece
+    from syzkaller_amd import sysdesc
+    u = sysdesc.bundled()
+    C = u.C
+    c = synth.corpus(0x5EED0021, 30_000, 97, 200_000)
+    want_kept, want_goff = oracle.minimize_grouped(c.pcs, c.off, c.group, 97)
+    want_hist = np.bincount(c.prog_len[want_kept], minlength=C + 1).astype(np.int64)
+    st = oracle.static_priorities(u.weights, exact=True)
+    want_p = oracle.calculate_priorities(st, c.prog_len[want_kept])
+    want_run, want_pres = oracle.build_choice_table(want_p)
+    s = torch.cuda.current_stream().cuda_stream
+    d = [_dev(torch, x) for x in (c.pcs, c.off, c.group, c.prog_len)]
+    sel = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+    hist = torch.zeros(C + 1, dtype=torch.int64, device="cuda")
+    out = torch.zeros(c.n, dtype=torch.int64, device="cuda")
+    goff = torch.zeros(98, dtype=torch.int64, device="cuda")
+    d_w = torch.from_numpy(u.weights).cuda()
+    d_st = torch.empty((C, C), dtype=torch.float32, device="cuda")
+    d_p = torch.empty((C, C), dtype=torch.float32, device="cuda")
+    d_run = torch.empty((C, C), dtype=torch.int64, device="cuda")
+    d_pres = torch.empty(C, dtype=torch.uint8, device="cuda")
+    job = cover.MinimizeJob()
+    for _ in range(2):  # the second step reuses the job and the lane's streams
+        job.begin(d[0], d[1], d[2], c.n, 97, d[3], stream=s)
+        job.end_prio(C, d_w, u.weights.shape[0], d_st, d_p, d_run, None, sel, hist, out, goff, d_pres, s)
+        torch.cuda.synchronize()
+        g = goff.cpu().numpy().astype(np.uint64)
+        assert np.array_equal(g, want_goff)
+        assert np.array_equal(out.cpu().numpy()[: int(g[-1])], want_kept)
+        assert np.array_equal(hist.cpu().numpy(), want_hist)
+        assert np.array_equal(d_st.cpu().numpy().view(np.uint32), st.view(np.uint32))
+        assert np.array_equal(d_p.cpu().numpy().view(np.uint32), want_p.view(np.uint32))
+        assert np.array_equal(d_run.cpu().numpy(), want_run)
+        assert np.array_equal(d_pres.cpu().numpy(), want_pres)
+    # the deferred checks still raise: a kept program longer than C, and a non-finite usage weight
+    long_len = _dev(torch, np.full(c.n, C + 5, np.uint16))
+    job.begin(d[0], d[1], d[2], c.n, 97, long_len, stream=s)
+    with pytest.raises(_lib.SyzGpuError):
+        job.end_prio(C, d_w, u.weights.shape[0], d_st, d_p, d_run, None, sel, hist, out, goff, d_pres, s)
+    bad = u.weights.copy()
+    bad[0, 0] = np.nan
+    d_bad = torch.from_numpy(bad).cuda()
+    job.begin(d[0], d[1], d[2], c.n, 97, d[3], stream=s)
+    with pytest.raises(_lib.SyzGpuError):
+        job.end_prio(C, d_bad, u.weights.shape[0], d_st, d_p, d_run, None, sel, hist, out, goff, d_pres, s)
