@@ -338,3 +338,33 @@ def novelty_shard(pcs, off, group, ngroups, mc, mc_off, flakes, rank, world, bou
         parts = [None] * world
         dist.all_gather_object(parts, (np.asarray(tab_r, np.uint32), np.asarray(toff_r, np.uint64)))
     return novelty_merge(flags.numpy(), parts, np.asarray(is_new_r).size, ngroups)
+
+
+# ---- the call co-occurrence XᵀX, sharded by corpus rows (north_star) --------------
+def cooccurrence_rows(nprogs, world):
+    """Row shards of the co-occurrence: rank r takes programs [b[r], b[r+1]) (equal counts, in corpus
+    order). XᵀX is a sum over programs, so the shards' partial matrices add up to the whole."""
+    return np.linspace(0, nprogs, world + 1).round().astype(np.int64)
+
+
+def cooccurrence_slice(calls, off, lo, hi):
+    """Programs [lo, hi) of the CSR (calls, off) as their own CSR."""
+    off = np.asarray(off, np.uint64)
+    a, b = int(off[lo]), int(off[hi])
+    return np.asarray(calls)[a:b], (off[lo:hi + 1] - off[lo]).astype(np.uint64)
+
+
+def cooccurrence_shard(calls, off, C, rank, world, run, dist=None):
+    """One rank's share of the call co-occurrence: run(calls, off, C) -> int32 C x C on this rank's row
+    shard (the GPU entry, or a checker), then one SUM all-reduce of the C x C partials. The sum is
+    taken in int64 and must fit int32 like the single-device result (the entry's ERANGE): an overflow
+    raises OverflowError. Returns the int32 C x C matrix, identical on every rank."""
+    import torch
+    b = cooccurrence_rows(np.asarray(off).size - 1, world)
+    part = np.asarray(run(*cooccurrence_slice(calls, off, int(b[rank]), int(b[rank + 1])), C), np.int32)
+    t = torch.from_numpy(part.astype(np.int64))
+    allreduce(t, dist)
+    tot = t.numpy()
+    if tot.size and (tot.max() > np.iinfo(np.int32).max or tot.min() < np.iinfo(np.int32).min):
+        raise OverflowError("call co-occurrence count outside int32")
+    return tot.astype(np.int32)

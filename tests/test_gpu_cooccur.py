@@ -131,3 +131,21 @@ def test_cooccurrence_device_entry():
                                                        torch.cuda.current_stream(dev).cuda_stream))
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_cooccurrence_row_shards_on_gpu(world):
+    # the north_star's multi-GPU form: corpus rows sharded over the ranks, each rank's XᵀX on the int8
+    # matrix cores, one SUM all-reduce of the C x C partials (sharding.cooccurrence_shard); here the
+    # ranks run one after another in this process and the partials are summed exactly as the
+    # all-reduce sums them (int64, checked against int32)
+    from syzkaller_amd import sharding
+    C = 1159
+    calls, off = corpus_calls(41, 200_000, C)
+    want = oracle.call_cooccurrence(calls, off, C)
+    b = sharding.cooccurrence_rows(off.size - 1, world)
+    tot = np.zeros((C, C), np.int64)
+    for r in range(world):
+        tot += prog.CallCooccurrence(*sharding.cooccurrence_slice(calls, off, int(b[r]), int(b[r + 1])), C)
+    assert tot.max() <= np.iinfo(np.int32).max
+    assert np.array_equal(tot.astype(np.int32), want)

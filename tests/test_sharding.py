@@ -407,3 +407,50 @@ def test_slice_csr_and_bounds():
     assert list(p) == [9, 0xFFFFFFFF] and list(o) == [0, 1, 1, 2]
     b = sharding.pc_bounds(np.arange(1000), 4)
     assert b[0] == 0 and b[-1] == 1 << 32 and np.all(np.diff(b.astype(np.int64)) > 0)
+
+
+# ---- the call co-occurrence sharded by corpus rows: SUM all-reduce of the C x C partials --------------
+def _cooc_rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    import oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls, off, C = _cooc_corpus()
+        got = sharding.cooccurrence_shard(calls, off, C, rank, world, oracle.call_cooccurrence, dist)
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def _cooc_corpus():
+    rnd = np.random.default_rng(77)
+    n, C = 3000, 61
+    lens = np.minimum(rnd.geometric(0.3, size=n), 40).astype(np.uint64)
+    lens[::50] = 0  # empty programs
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    calls = rnd.integers(0, C, size=int(off[-1])).astype(np.uint16)
+    return calls, off, C
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cooccurrence_row_shards_sum_to_the_whole(world):
+    import torch.multiprocessing as mp
+
+    import oracle
+    calls, off, C = _cooc_corpus()
+    want = oracle.call_cooccurrence(calls, off, C)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cooc_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    for _, got in res:
+        assert np.array_equal(got, want)

@@ -17,9 +17,12 @@ import sys
 def short(name, grid):
     """The kernel's base name (`void syz::k_part4<512, 40, false>(...)` -> `k_part4`): the names the
     bench's per-kernel scopes use."""
-    base = name.split("(")[0].split("<")[0].split("::")[-1].strip()
+    head = name.split("(")[0]
+    base = head.split("<")[0].split("::")[-1].strip()
     if base.startswith("void "):
         base = base[5:]
+    if base == "k_region" and head.replace(" ", "").endswith(",true>"):
+        base = "k_region_count"  # the count pass (bench scope name), k_region<.., COUNT = true>
     return base or None
 
 
