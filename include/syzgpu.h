@@ -360,7 +360,8 @@ int syzgpu_sigset_erase_dev(syzgpu_sigset* set, const uint8_t* sigs, size_t n, u
                             uint64_t* nerased, void* stream);
 
 /* Per-kernel timing of the last *_dev call (HIP events on the call's stream), for the benchmark's
- * roofline. names/ms arrays of capacity cap; returns the number of kernels recorded. */
+ * roofline. names/ms arrays of capacity cap; returns the number of kernels recorded. on = 2 also runs
+ * the raw minimize's passes one after another (each scope then times its kernels alone). */
 int syzgpu_profile_enable(int on);
 /* Restrict the recording to the scopes named `name` (NULL: all), so that the timed region of the
  * benchmark carries one event pair per step for its roofline kernel only. */

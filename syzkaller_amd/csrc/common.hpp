@@ -129,6 +129,8 @@ struct LaneGuard {
 // Kernel timing (bench roofline). Records named events around launches when enabled.
 struct Prof {
   bool on = false;
+  bool serial = false;  // (syzgpu_profile_enable(2)) the raw minimize's passes one after another, so each
+                        // scope times its kernels alone (the bench's per-kernel pass)
   std::string only;  // when non-empty, only scopes of this name are recorded
   bool match(const char* name) const { return only.empty() || only == name; }
   struct Rec {

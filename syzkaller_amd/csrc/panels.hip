@@ -407,7 +407,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
 
 static bool pm_serial() {
   static const bool v = getenv("SYZGPU_PM_SERIAL") && atoi(getenv("SYZGPU_PM_SERIAL")) != 0;
-  return v;
+  return v || (prof().on && prof().serial);
 }
 
 // SYZGPU_RG_DBG (timing only, results wrong): 16 = P loads only, 32 = scatter without pass 2, 64 = no stores

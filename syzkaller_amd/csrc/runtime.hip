@@ -329,6 +329,7 @@ const char* syzgpu_version(void) { return "syzgpu 0.1 gfx950"; }
 
 int syzgpu_profile_enable(int on) {
   prof().on = on != 0;
+  prof().serial = on == 2;
   prof().reset();
   return SYZGPU_OK;
 }

@@ -24,5 +24,5 @@ for E in "$@"; do
   python3 -c "
 import json
 d=json.loads([l for l in open('$OUT/b$i.log') if l.startswith('{')][-1])
-print('step', d['ms_per_step'], {k: v for k, v in list(d['kernels_ms_per_step_untimed_pass'].items())[:8]})" | tee -a $OUT/ab.log
+print('step', d['ms_per_step'], {k: v for k, v in list(d['kernels_ms_per_step_serialized_pass'].items())[:8]})" | tee -a $OUT/ab.log
 done

@@ -7,6 +7,6 @@ for cfg in "SYZGPU_GR_PERSIST=0" "SYZGPU_GR_PERSIST=1 SYZGPU_GR_PGRID=64" "SYZGP
   python3 -c "
 import json
 d=json.loads([l for l in open('gpurun_out/ab/b.log') if l.startswith('{')][-1])
-k=d['kernels_ms_per_step_untimed_pass']
+k=d['kernels_ms_per_step_serialized_pass']
 print('$cfg', d['ms_per_step'], 'level', k['gosort_level'], 'lds_small', k['gosort_lds_small'], 'vmin', k['vec_min'])"
 done

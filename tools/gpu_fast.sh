@@ -15,5 +15,5 @@ python3 -c "
 import json,sys
 d=json.loads([l for l in open('$OUT/bench.log') if l.startswith('{')][-1])
 print('ms_per_step', d['ms_per_step'], 'value', d['value'], 'roof', d['roofline']['kernel'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])
-print(json.dumps(d['kernels_ms_per_step_untimed_pass']))
+print(json.dumps(d['kernels_ms_per_step_serialized_pass']))
 "

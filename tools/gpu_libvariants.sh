@@ -10,6 +10,6 @@ for t in "$@"; do
   python3 -c "
 import json
 d=json.loads([l for l in open('gpurun_out/variants/b_$t.log') if l.startswith('{')][-1])
-k=d['kernels_ms_per_step_untimed_pass']
+k=d['kernels_ms_per_step_serialized_pass']
 print('$t', d['ms_per_step'], 'gosort_level', k['gosort_level'], 'vec_min', k['vec_min'])"
 done

@@ -15,5 +15,5 @@ for SET in "" "$@"; do
   python3 -c "
 import json
 d=json.loads([l for l in open('$OUT/b$i.log') if l.startswith('{')][-1])
-print(d['ms_per_step'], {k: v for k, v in d['kernels_ms_per_step_untimed_pass'].items()})" | tee -a $OUT/ab.log
+print(d['ms_per_step'], {k: v for k, v in d['kernels_ms_per_step_serialized_pass'].items()})" | tee -a $OUT/ab.log
 done

@@ -12,5 +12,5 @@ for SET in "$A" "$B" "$A" "$B"; do
   python3 -c "
 import json
 d=json.loads([l for l in open('$OUT/b$i.log') if l.startswith('{')][-1])
-print('[$SET]', d['ms_per_step'], d['kernels_ms_per_step_untimed_pass'].get('pmin'), d['kernels_ms_per_step_untimed_pass'].get('pmin_small'))" | tee -a $OUT/ab.log
+print('[$SET]', d['ms_per_step'], d['kernels_ms_per_step_serialized_pass'].get('pmin'), d['kernels_ms_per_step_serialized_pass'].get('pmin_small'))" | tee -a $OUT/ab.log
 done

@@ -8,5 +8,5 @@ for cv in ${@:-32768 65536 131072}; do
   python3 -c "
 import json
 d=json.loads([l for l in open('gpurun_out/sweep/cv_$cv.log') if l.startswith('{')][-1])
-print($cv, d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['kernels_ms_per_step_untimed_pass']['vec_min_small'])"
+print($cv, d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['kernels_ms_per_step_serialized_pass']['vec_min_small'])"
 done
