@@ -49,8 +49,10 @@ def parse():
     ap.add_argument("--profile", type=int, default=1, help="per-kernel HIP event timing in the timed region")
     ap.add_argument("--store", type=int, default=1, help="also time the resident-store side leg at N=1")
     ap.add_argument("--text", type=int, default=1, help="also time the text pass over the kept programs at N=1")
-    ap.add_argument("--novelty", type=int, default=1, help="also time config 3 (triage batch) at N=1")
+    ap.add_argument("--novelty", type=int, default=1, help="also time config 3 (triage batch): at N=1 whole, at N>1 sharded by PC range")
     ap.add_argument("--novelty-covers", type=int, default=1_000_000)
+    ap.add_argument("--novelty-wide", type=int, default=1,
+                    help="also time the novelty batch with its PC span stretched 34x (272M addresses)")
     ap.add_argument("--hub", type=int, default=1, help="also time config 5's hub ingest (scan + SHA-1 + dedup) at N=1")
     ap.add_argument("--analytics", type=int, default=1, help="also time the manager's cover analytics at N=1")
     ap.add_argument("--analytics-cpu-sample", type=int, default=10_000)
@@ -273,6 +275,11 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_progs * args.steps / elapsed
 
+    # configs[2] on N GPUs: every rank takes its PC range of the batch (collectives inside)
+    nov_sh = None
+    if world > 1 and args.novelty and not args.emulate:
+        nov_sh = novelty_leg_sharded(args, dev, L, dist, rank, world)
+
     out = None
     if rank == 0:
         # roofline of the dominant kernel: algorithmic bytes over its measured time
@@ -324,7 +331,7 @@ def main():
             "gen_s": round(gen_s, 2),
             "store_reuse": store_leg_res,
             "minimize_corpus_tail": tail,
-            "novelty_config3": nov,
+            "novelty_config3": nov if nov is not None else nov_sh,
             "call_cooccurrence": cooc,
             "cover_analytics": ana,
             "hub_ingest_config5": hubr,
@@ -743,6 +750,36 @@ def novelty_leg(args, dev, L, read_prof):
            "path_roofline": {"bytes_per_batch": alg_batch, "achieved": round(alg_batch / (el / steps) / 1e9, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(alg_batch / (el / steps) / 1e9 / HBM_PEAK_GBS, 4)}}
+    if args.novelty_wide:
+        # the same batch with its PC space spread over 34x the addresses (8M -> 272M span: past the
+        # direct windows' 32M, so the hashed windows run); same outputs up to the monotone map
+        base = 0x81000000
+
+        def stretch(x):
+            y = (x.to(torch.int64) & 0xFFFFFFFF) - base
+            return (y * 34 + base).to(torch.int32)
+        dw = [stretch(d[0]), d[1], d[2], stretch(d[3]), d[4], stretch(d[5])]
+
+        def step_w():
+            cover.NoveltyBatchDev(dw[0], dw[1], dw[2], b.n, G, dw[3], dw[4], int(mco[-1]), dw[5], flakes.size,
+                                  int(b.off[-1]), is_new, out, cap, ooff, sptr)
+        step_w()
+        torch.cuda.synchronize()
+        L.syzgpu_profile_enable(1)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step_w()
+        torch.cuda.synchronize()
+        elw = time.perf_counter() - t0
+        evw = read_prof()
+        L.syzgpu_profile_enable(0)
+        del dw
+        res["wide_span"] = {"span_addresses": int(34 * (int(max(b.pcs.max(), mcp.max())) - base)),
+                            "ms_per_batch": round(elw / steps * 1e3, 3),
+                            "ratio_vs_default_span": round(elw / el, 3),
+                            "new_covers": int(is_new.sum().item()),
+                            "kernels_ms_per_batch": {k: round(e["ms"] / steps, 4)
+                                                     for k, e in sorted(evw.items(), key=lambda x: -x[1]["ms"])}}
     if ev:
         dom, e = max(ev.items(), key=lambda x: x[1]["ms"])
         ms = e["ms"] / e["launches"]
@@ -762,6 +799,81 @@ def novelty_leg(args, dev, L, read_prof):
                                "sample": "first %d covers of the batch; oracle/liboracle.so literal per-cover "
                                          "Difference/Union (fuzzer.go:446-470), %.2f s" % (k, dt)}
     return res
+
+
+def novelty_leg_sharded(args, dev, L, dist, rank, world):
+    """configs[2] on N GPUs (every rank runs it): the same 1M-cover batch and maxCover0 as
+    novelty_leg, sharded by PC value (sharding.novelty_shard's plan: equal-count PC ranges from a
+    sample, identical on every rank). Each rank holds its range's slice of the batch, of the tables and
+    of the flakes in HBM (sliced on the device before the timed loop, as a PC-sharded maxCover would be
+    kept); a step = syzgpu_novelty_batch_dev on the slice, the per-call "updated" flags, and one RCCL
+    MAX all-reduce of n + G bytes (is_new + updated). The updated tables stay sharded (each rank's
+    range is all the next batch needs). Strong scaling: the batch is fixed."""
+    import torch
+    from syzkaller_amd import cover, sharding, synth
+    G = args.ngroups
+    base = synth.corpus(args.seed + 0x30, 100_000, G, args.npcs)
+    _, mcp, mco = cover.NoveltyBatch(base.pcs, base.off, base.group, G, np.zeros(0, np.uint32),
+                                     np.zeros(G + 1, np.uint64), np.zeros(0, np.uint32))
+    rnd = np.random.default_rng(3)
+    flakes = np.unique(rnd.choice(base.pcs, 5000, replace=False))
+    b = synth.corpus(args.seed + 0x31, args.novelty_covers, G, args.npcs)
+    bounds = sharding.pc_bounds(b.pcs[:: max(1, b.pcs.size // 200_000)], world)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1]) - 1
+
+    def t(a):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+        return torch.from_numpy(np.ascontiguousarray(a).view(view.get(a.dtype, a.dtype))).to(dev)
+
+    def dslice(pcs, off):
+        # [lo, hi] of every sorted list, on the device: mask, compaction, per-list counts
+        u = pcs.to(torch.int64) & 0xFFFFFFFF
+        m = (u >= lo) & (u <= hi)
+        cs = torch.zeros(m.numel() + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(m, 0, out=cs[1:])
+        o2 = cs[off] - cs[off[:1]]
+        return pcs[m].contiguous(), o2.contiguous()
+    p_r, o_r = dslice(t(b.pcs), t(b.off))
+    m_r, mo_r = dslice(t(mcp), t(mco))
+    f_r = flakes[(flakes >= lo) & (flakes <= hi)]
+    d_f, d_grp = t(f_r), t(b.group)
+    g64 = d_grp.to(torch.int64)
+    nl, nm = int(o_r[-1].item()), int(mo_r[-1].item())
+    cap = nm + nl + 1
+    flags = torch.zeros(b.n + G, dtype=torch.uint8, device=dev)
+    is_new = flags[: b.n]
+    out = torch.empty(cap, dtype=torch.int32, device=dev)
+    ooff = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        cover.NoveltyBatchDev(p_r, o_r, d_grp, b.n, G, m_r, mo_r, nm, d_f, f_r.size, nl, is_new, out, cap, ooff,
+                              sptr)
+        flags[b.n:].zero_()
+        flags[b.n:].scatter_reduce_(0, g64, is_new, "amax")
+        sharding.allreduce_max_u8(flags, dist)
+    step()
+    torch.cuda.synchronize()
+    steps = max(1, args.steps // 2)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    sharding.allreduce(el, dist, dist.ReduceOp.MAX)
+    el = float(el.item())
+    new = int(is_new.sum().item())
+    tab = torch.tensor([int(ooff[-1].item())], dtype=torch.int64, device=dev)
+    sharding.allreduce(tab, dist)
+    return {"workload": "config3: 1M fresh covers (%d PCs) vs maxCover0 of a 100k corpus (%d PCs), %d flakes; "
+                        "sharded by PC range over %d ranks" % (int(b.off[-1]), int(mco[-1]), flakes.size, world),
+            "metric": "triage covers/sec", "value": round(b.n * steps / el, 1), "ms_per_batch": round(el / steps * 1e3, 3),
+            "scaling": "strong", "new_covers": new, "maxcover_out_pcs": int(tab.item()),
+            "rank0_slice_pcs": nl, "exchange_bytes_per_batch": b.n + G,
+            "exchange": "one MAX all-reduce of n + G bytes (is_new + per-call updated); tables stay sharded"}
 
 
 def cpu_baseline(corp, uses, n_sample):

@@ -894,6 +894,7 @@ static int strategy() {
   if (e && !strcmp(e, "table")) return 2;
   if (e && !strcmp(e, "keys")) return 3;
   if (e && !strcmp(e, "windows")) return 4;
+  if (e && !strcmp(e, "hwindows")) return 5;  // the windows, hashed whatever the span
   return 0;
 }
 
@@ -909,7 +910,7 @@ static void check_errors(int* err, hipStream_t s);
 
 bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_t* d_grp, size_t n, uint32_t G,
                      const uint32_t* d_mc, const uint64_t* d_mco, const uint32_t* d_fl, size_t nfl, uint8_t* d_new,
-                     uint32_t* d_out, size_t out_cap, uint64_t* d_ooff, int* err, hipStream_t s);
+                     uint32_t* d_out, size_t out_cap, uint64_t* d_ooff, int* err, bool force_hash, hipStream_t s);
 
 // The batch on device-resident inputs: L = off[n] PCs in the covers, M = mc_off[G] in the tables.
 // Writes is_new[n], out_mc[<= out_cap] and out_mc_off[G+1] on the device; the call returns after the
@@ -924,15 +925,18 @@ void novelty_dev(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_t* d
   const uint64_t ni = L + M;
   int* err = sc.get<int>("nv_err", 2);
   SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
-  if (strategy() == 0 || strategy() == 4) {  // (writes every is_new flag itself)
+  if (strategy() == 0 || strategy() >= 4) {  // (writes every is_new flag itself)
     if (nflakes > 1) {
       k_nov_check_flakes<<<grid_for(nflakes, 256, 1024), 256, 0, s>>>(d_fl, nflakes, err);
       SYZ_LAUNCHED();
     }
-    if (novelty_windows(d_pcs, d_off, d_grp, n, G, d_mc, d_mco, d_fl, nflakes, d_new, d_out, out_cap, d_ooff, err, s)) {
+    if (novelty_windows(d_pcs, d_off, d_grp, n, G, d_mc, d_mco, d_fl, nflakes, d_new, d_out, out_cap, d_ooff, err,
+                        strategy() == 5, s)) {
       check_errors(err, s);
       return;
     }
+    // forced: no silent change of strategy
+    if (strategy() >= 4) fail(SYZGPU_EINVAL, "novelty: the windows strategy cannot take this batch (ngroups > 4096)");
   }
   if (n) SYZ_HIP(hipMemsetAsync(d_new, 0, n, s));
   if (strategy() != 1 && novelty_table(d_pcs, d_off, d_grp, n, L, G, d_mc, d_mco, M, d_fl, nflakes, d_new, d_out, out_cap,
@@ -1002,6 +1006,7 @@ static void check_errors(int* err, hipStream_t s) {
   if (herr[0] & 4) fail(SYZGPU_EINVAL, "covers must be canonical (strictly increasing)");
   if (herr[0] & 16) fail(SYZGPU_EINVAL, "flakes must be canonical (strictly increasing)");
   if (herr[0] & 8) fail(SYZGPU_ECAPACITY, "out_mc capacity too small");
+  if (herr[0] & 32) fail(SYZGPU_EINTERNAL, "novelty: a hashed window's table overflowed at one address per round");
 }
 
 void novelty_batch(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n, uint32_t G,

@@ -22,10 +22,12 @@
 //   E  scan of the counts, then every window's bitmap expands to its PCs at its offset (the updated
 //      tables, sorted by (call, PC)), a table's 0xFFFFFFFF last unless the call took a Union
 //
-// Integer work throughout; bit-exact by construction. Windows are direct-mapped, so the PC span must
-// fit WMAX windows (2^15 x 1024 = 32M addresses); a wider span (or G > 4096) falls back to the keyed
-// table (novelty.hip). Measured and dropped (profiles/r02_ab/novelty_ab.md): hashed windows for calls
-// with few PCs per window, persistent workgroups with the next item prefetched, branch-free batches.
+// Integer work throughout; bit-exact by construction. Direct windows need the PC span to fit WMAX
+// windows (2^15 x 1024 = 32M addresses); a wider span takes hashed windows (k_nw_hash: a window size
+// per call, an open-addressing LDS table, the kept keys sorted per address sub-range and stored as a
+// list), up to the whole u32 space. Only G > 4096 falls back to the keyed table (novelty.hip).
+// Measured and dropped (profiles/r02_ab/novelty_ab.md): hashed windows for the calls with few PCs per
+// window inside a narrow span, persistent workgroups with the next item prefetched, branch-free batches.
 #include <algorithm>
 #include <cstdlib>
 #include <numeric>
@@ -234,14 +236,25 @@ __global__ void k_nw_sent(const uint8_t* has_sent, const uint8_t* upd, const NwG
     wcount[ng_[g + 1].sbase - 1] = has_sent[g] && !upd[g] ? 1u : 0u;
 }
 
-// E: one slot per workgroup; the window's kept bitmap -> its PCs at wpos[slot]
-__global__ __launch_bounds__(NE_BLOCK) void k_nw_emit(const uint32_t* __restrict__ kbits,
-                                                      const uint64_t* __restrict__ wpos, const NwGroup* ng_,
-                                                      const PGroup* pg, uint32_t G, uint32_t lo, uint32_t* out,
-                                                      uint64_t cap, uint64_t* ooff, int* err) {
-  __shared__ uint32_t red[NE_BLOCK / 64 + 1];
-  const uint64_t slot = blockIdx.x;
-  uint32_t g0 = 0, g1 = G;  // the call: last g with sbase <= slot
+// ---- wide spans: hashed windows -----------------------------------------------------------------
+// When the span does not fit 1024 direct windows, every call gets its own window size (2^S addresses,
+// S in [15, 26], about NW_HTARGET PCs per window, <= 1024 windows) and a workgroup per (call, window)
+// keeps an open-addressing table in LDS: key = window offset, value = min member position. The
+// window's offsets are done in R contiguous address sub-ranges (R a power of two, doubled and the
+// unfinished sub-ranges redone when a probe run exceeds HPROBE), so each round's kept keys, sorted in
+// LDS (bitonic), extend the window's PC-ordered kept list at hkeys[hbase[slot]]: no bitmap of 2^S bits.
+constexpr uint32_t NW_HTARGET = 8192;
+constexpr int NH_BLOCK = 512;             // two workgroups per CU (74 KB of LDS each)
+constexpr uint32_t NH_PER = HS / NH_BLOCK;  // table slots per thread at compaction
+constexpr uint32_t NH_FLK = 512;         // flakes of a window kept in LDS for the lookup
+constexpr uint32_t NH_OBITS = 19;       // sub-ranges up to 2^19 addresses are ordered by a bitmap (64 KB)
+static_assert((1u << (NH_OBITS - 5)) <= 2 * HS, "the order bitmap fits the table's space");
+
+__device__ __forceinline__ uint32_t hslot_nw(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - HS_BITS); }
+
+// the call of count slot `slot`: the last g with sbase <= slot
+__device__ __forceinline__ uint32_t nw_slot_group(const NwGroup* ng_, uint32_t G, uint64_t slot) {
+  uint32_t g0 = 0, g1 = G;
   while (g1 - g0 > 1) {
     const uint32_t mid = (g0 + g1) >> 1;
     if (ng_[mid].sbase <= slot)
@@ -249,7 +262,243 @@ __global__ __launch_bounds__(NE_BLOCK) void k_nw_emit(const uint32_t* __restrict
     else
       g1 = mid;
   }
-  const uint32_t g = g0;
+  return g0;
+}
+
+// PCs of (call g, window w): its regions' lengths over the member segments
+__device__ __forceinline__ uint32_t nw_window_pcs(uint32_t g, uint32_t w, const PGroup* pg, const uint64_t* cstart,
+                                                  const uint32_t* rtot) {
+  const PGroup p = pg[g];
+  const uint32_t sb = 32 - p.S;
+  const uint64_t ng = cstart[g + 1] - cstart[g];
+  const uint32_t nseg = (uint32_t)((ng + (1ull << sb) - 1) >> sb);
+  uint32_t e = 0;
+  for (uint32_t s = 0; s < nseg; s++) e += rtot[p.rb + s * p.W + w];
+  return e;
+}
+
+// capacity of every count slot's kept list (its window's PCs; 0 for the table-sentinel slot)
+__global__ void k_nw_hcap(const NwGroup* ng_, const PGroup* pg, const uint64_t* cstart, const uint32_t* rtot,
+                          uint32_t G, uint64_t slots, uint32_t* hcap) {
+  for (uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; sl < slots; sl += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t g = nw_slot_group(ng_, G, sl);
+    const uint32_t w = (uint32_t)(sl - ng_[g].sbase);
+    hcap[sl] = w < pg[g].W ? nw_window_pcs(g, w, pg, cstart, rtot) : 0u;
+  }
+}
+
+// M (hashed): item i is window i - iofs[j] of call order[j] (larger calls first)
+__global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, const uint32_t* iofs, uint32_t G,
+                                                  const PGroup* pg, const uint64_t* rstart, const uint32_t* rtot,
+                                                  const uint32_t* elems, const uint64_t* cstart, uint32_t lo,
+                                                  const uint32_t* __restrict__ fl, uint64_t nfl, const NwGroup* ng_,
+                                                  const uint64_t* hbase, uint32_t* hkeys, uint32_t* wcount,
+                                                  uint8_t* sel8, uint8_t* upd, int* err, int dbg) {
+  __shared__ uint32_t tabs[2 * HS];  // keys, values; then the sub-range's kept-offset bitmap
+  __shared__ uint32_t bm[HBM_WORDS];
+  __shared__ uint32_t red[NH_BLOCK / 64 + 1];
+  __shared__ uint32_t flk[NH_FLK];  // the window's flakes (when they fit)
+  __shared__ int full;
+  uint32_t* keys = tabs;
+  uint32_t* vals = tabs + HS;
+  const uint32_t j = (uint32_t)upper_bound_dev<uint32_t>(iofs, 0, G + 1, blockIdx.x) - 1;
+  const uint32_t g = order[j], w = blockIdx.x - iofs[j];
+  const PItem it{g, w};
+  const uint32_t S = pg[g].S;
+  const uint64_t gb = cstart[g], ng = cstart[g + 1] - gb;
+  const uint64_t slot = ng_[g].sbase + w;
+  const uint32_t E = nw_window_pcs(g, w, pg, cstart, rtot);
+  if (E == 0) {
+    if (threadIdx.x == 0) wcount[slot] = 0;
+    return;
+  }
+  // the flakes inside the window's addresses [wlo, wlo + 2^S)
+  const uint32_t wlo = lo + (w << S);
+  const uint64_t whi = (uint64_t)wlo + (1ull << S);
+  const uint64_t f0 = lower_bound_dev<uint32_t>(fl, 0, nfl, wlo);
+  const uint64_t f1 = whi > 0xFFFFFFFFull ? nfl : lower_bound_dev<uint32_t>(fl, f0, nfl, (uint32_t)whi);
+  const bool flds = f1 - f0 <= NH_FLK;  // searched in LDS, else in the global list
+  const uint32_t nf = flds ? (uint32_t)(f1 - f0) : 0u;
+  for (uint32_t i = threadIdx.x; i < nf; i += NH_BLOCK) flk[i] = fl[f0 + i];
+  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)HBM_WORDS * 32, ng);
+  const uint32_t words = (span + 31) / 32;
+  for (uint32_t i = threadIdx.x; i < words; i += NH_BLOCK) bm[i] = 0;
+  uint32_t* out = hkeys + hbase[slot];
+  uint32_t lr2 = 0;  // log2 R: one round unless the table fills
+  uint32_t kc = 0;
+  int anynew = 0;
+  for (uint32_t round = 0; round < (1u << lr2);) {
+    for (uint32_t i = threadIdx.x; i < HS; i += NH_BLOCK) {
+      keys[i] = 0xFFFFFFFFu;
+      vals[i] = RANK_NONE;
+    }
+    if (threadIdx.x == 0) full = 0;
+    __syncthreads();
+    const uint32_t sh = S - lr2, rr = round;
+    const bool split = lr2 > 0;
+    uint32_t acc = 0;
+    for_region<SYZ_RG_NU, true>(it, pg, cstart, rstart, rtot, elems, nullptr, [&](uint32_t o, uint32_t R) {
+      if (R == RANK_NONE || (split && (o >> sh) != rr)) return;
+      if (dbg & 1) {
+        acc += o ^ R;
+        return;
+      }
+      uint32_t h = hslot_nw(o);
+      for (uint32_t probes = 0; probes < HPROBE; probes++) {
+        uint32_t k = keys[h];
+        if (k == 0xFFFFFFFFu) {
+          k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
+          if (k == 0xFFFFFFFFu) k = o;
+        }
+        if (k == o) {
+          atomicMin(&vals[h], R);
+          return;
+        }
+        h = (h + 1) & (HS - 1);
+      }
+      full = 1;
+    });
+    if (acc == 0x9E3779B9u) sel8[0] = 1;
+    __syncthreads();
+    if (dbg & 2) return;
+    if (full) {  // twice the sub-ranges; the finished ones stay done
+      if (lr2 == S) {
+        if (threadIdx.x == 0) atomicOr(err, 32);
+        return;
+      }
+      lr2++;
+      round *= 2;
+      __syncthreads();
+      continue;
+    }
+    // the kept keys of this sub-range: held by the table, or by a cover when not a flake
+    uint32_t kk[NH_PER];
+    bool kp[NH_PER];
+#pragma unroll
+    for (uint32_t q = 0; q < NH_PER; q++) {
+      const uint32_t i = threadIdx.x + q * NH_BLOCK;
+      kp[q] = false;
+      kk[q] = keys[i];
+      if (kk[q] == 0xFFFFFFFFu) continue;
+      const uint32_t v = vals[i];
+      const bool old = v == (uint32_t)gb;
+      if (!old && f1 > f0) {  // a flake no table holds: never new, never kept
+        const uint32_t pc = wlo + kk[q];
+        if (flds) {
+          const uint32_t x = (uint32_t)lower_bound_dev<uint32_t>(flk, 0, nf, pc);
+          if (x < nf && flk[x] == pc) continue;
+        } else {
+          const uint64_t x = lower_bound_dev<uint32_t>(fl, f0, f1, pc);
+          if (x < f1 && fl[x] == pc) continue;
+        }
+      }
+      kp[q] = true;
+      if (!old) {
+        anynew = 1;
+        const uint64_t lr = (uint64_t)v - gb;
+        if (lr < span) {
+          const uint32_t bit = 1u << (lr & 31);
+          if (!(bm[lr >> 5] & bit)) atomicOr(&bm[lr >> 5], bit);
+        } else {
+          sel8[v] = 1;
+        }
+      }
+    }
+    __syncthreads();  // the table is read: its space takes the order
+    const uint32_t sbase = split ? rr << sh : 0u;
+    if (sh <= NH_OBITS) {
+      // a sub-range of <= 2^19 addresses: a presence bitmap over it, read out in address order
+      const uint32_t nw = sh >= 5 ? 1u << (sh - 5) : 1u;
+      for (uint32_t i = threadIdx.x; i < nw; i += NH_BLOCK) tabs[i] = 0;
+      __syncthreads();
+#pragma unroll
+      for (uint32_t q = 0; q < NH_PER; q++)
+        if (kp[q]) {
+          const uint32_t o = kk[q] - sbase;
+          atomicOr(&tabs[o >> 5], 1u << (o & 31));
+        }
+      __syncthreads();
+      // each wave a contiguous range of words, read lane-strided (no bank conflicts): its count, the
+      // waves' prefix, then the bits in order, 64 words at a time with a wave scan for positions
+      constexpr uint32_t NWV = NH_BLOCK / 64;
+      const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
+      const uint32_t per = (nw + NWV - 1) / NWV, w0 = min(nw, wv * per), w1 = min(nw, w0 + per);
+      uint32_t c = 0;
+      for (uint32_t i = w0 + lane; i < w1; i += 64) c += (uint32_t)__popc(tabs[i]);
+      uint32_t tot;
+      uint32_t p = kc + block_excl_scan<NH_BLOCK>(c, red, &tot);  // lane order = word order mod 64 only
+      p = __shfl(p, 0, 64);  // the wave's first position (lane 0's exclusive prefix)
+      for (uint32_t i0 = w0; i0 < w1; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        uint32_t m = i < w1 ? tabs[i] : 0u;
+        const uint32_t cm = (uint32_t)__popc(m);
+        const uint32_t inc = wave_incl_scan(cm);
+        uint32_t q = p + inc - cm;
+        while (m) {
+          const uint32_t b = __ffs(m) - 1;
+          m &= m - 1;
+          out[q++] = sbase + 32u * i + b;
+        }
+        p += __shfl(inc, 63, 64);
+      }
+      kc += tot;
+    } else {
+      // wider (calls with few PCs per window): the kept offsets compacted, then a bitonic sort
+      uint32_t c = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < NH_PER; q++) c += kp[q] ? 1u : 0u;
+      uint32_t nk;
+      uint32_t p = block_excl_scan<NH_BLOCK>(c, red, &nk);
+      uint32_t P = 1;
+      while (P < nk) P <<= 1;
+#pragma unroll
+      for (uint32_t q = 0; q < NH_PER; q++)
+        if (kp[q]) keys[p++] = kk[q];
+      for (uint32_t i = nk + threadIdx.x; i < P; i += NH_BLOCK) keys[i] = 0xFFFFFFFFu;
+      __syncthreads();
+      for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+          for (uint32_t i = threadIdx.x; i < P; i += NH_BLOCK) {
+            const uint32_t l = i ^ jj;
+            if (l > i) {
+              const uint32_t a = keys[i], b = keys[l];
+              if ((a > b) == ((i & k) == 0)) {
+                keys[i] = b;
+                keys[l] = a;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      for (uint32_t i = threadIdx.x; i < nk; i += NH_BLOCK) out[kc + i] = keys[i];
+      kc += nk;
+    }
+    round++;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) wcount[slot] = kc;
+  if (__syncthreads_or(anynew) && threadIdx.x == 0) upd[g] = 1;
+  for (uint32_t i = threadIdx.x; i < words; i += NH_BLOCK) {
+    uint32_t v = bm[i];
+    while (v) {
+      const uint32_t b = __ffs(v) - 1;
+      sel8[gb + 32ull * i + b] = 1;
+      v &= v - 1;
+    }
+  }
+}
+
+// E: one slot per workgroup; the window's kept bitmap (or, hashed windows, its sorted kept offsets at
+// hkeys[hbase[slot]]) -> its PCs at wpos[slot]
+__global__ __launch_bounds__(NE_BLOCK) void k_nw_emit(const uint32_t* __restrict__ kbits,
+                                                      const uint64_t* __restrict__ wpos, const NwGroup* ng_,
+                                                      const PGroup* pg, uint32_t G, uint32_t lo, uint32_t* out,
+                                                      uint64_t cap, uint64_t* ooff, int* err,
+                                                      const uint64_t* __restrict__ hbase,
+                                                      const uint32_t* __restrict__ hkeys) {
+  __shared__ uint32_t red[NE_BLOCK / 64 + 1];
+  const uint64_t slot = blockIdx.x;
+  const uint32_t g = nw_slot_group(ng_, G, slot);
   const NwGroup gl = ng_[g];
   const uint32_t w = (uint32_t)(slot - gl.sbase), W = pg[g].W, S = pg[g].S;
   const uint64_t p0 = wpos[slot], c = wpos[slot + 1] - p0;
@@ -264,6 +513,12 @@ __global__ __launch_bounds__(NE_BLOCK) void k_nw_emit(const uint32_t* __restrict
   }
   if (w == W) {
     if (threadIdx.x == 0) out[p0] = SENT;
+    return;
+  }
+  if (hbase) {
+    const uint32_t wlo = lo + (w << S);
+    const uint32_t* src = hkeys + hbase[slot];
+    for (uint64_t i = threadIdx.x; i < c; i += NE_BLOCK) out[p0 + i] = wlo + src[i];
     return;
   }
   const uint32_t q = (1u << S) / 32 / NE_BLOCK;  // words per thread (2 .. 16)
@@ -296,6 +551,13 @@ static int nw_dbg() {
   return v;
 }
 
+// timing experiments only (results are wrong when set): SYZGPU_NWH_DBG 1 = hashed windows walked
+// without table updates, 2 = tables built, nothing after
+static int nwh_dbg() {
+  static const int v = getenv("SYZGPU_NWH_DBG") ? atoi(getenv("SYZGPU_NWH_DBG")) : 0;
+  return v;
+}
+
 // SYZGPU_NW_BITS=14|15: direct window bits (default: 14 while the span fits 1024 such windows, else 15)
 static uint32_t nw_bits_forced() {
   static const uint32_t v = getenv("SYZGPU_NW_BITS") ? (uint32_t)atoi(getenv("SYZGPU_NW_BITS")) : 0u;
@@ -313,11 +575,12 @@ __global__ void k_nw_gpcs(const uint64_t* mpos, const uint64_t* cstart, uint32_t
     gpcs[g] = mpos[cstart[g + 1]] - mpos[cstart[g]];
 }
 
-// false: the span does not fit the direct windows (or G is too large): use another strategy. err gets
-// novelty.hip's bits (1 table, 2 group id, 4 cover, 8 capacity).
+// Direct windows while the span fits 1024 of them, else (or force_hash) hashed windows. false: G is
+// too large (or the batch too long) for the windows: use another strategy. err gets novelty.hip's bits
+// (1 table, 2 group id, 4 cover, 8 capacity, 32 internal).
 bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_t* d_grp, size_t n, uint32_t G,
                      const uint32_t* d_mc, const uint64_t* d_mco, const uint32_t* d_fl, size_t nfl, uint8_t* d_new,
-                     uint32_t* d_out, size_t out_cap, uint64_t* d_ooff, int* err, hipStream_t s) {
+                     uint32_t* d_out, size_t out_cap, uint64_t* d_ooff, int* err, bool force_hash, hipStream_t s) {
   if (G == 0 || G > MAX_GROUPS_PM || (uint64_t)n + G >= 0xFFFFFFF0ull) return false;
   Context& c = ctx();
   Scratch& sc = c.scratch;
@@ -366,25 +629,35 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   auto nwin = [&](uint32_t sb) { return (((uint64_t)hi - lo) >> sb) + 1; };
   uint32_t DB = nw_bits_forced();
   if (!DB) DB = nwin(14) <= WMAX ? 14 : 15;
-  if (nwin(DB) > WMAX) return false;
-  const uint32_t WD = (uint32_t)nwin(DB);
-  // ---- plan: every call on WD direct windows of 2^DB addresses; blocks; work items ----
+  const bool hashed = force_hash || nwin(DB) > WMAX;
+  uint32_t smin = 15;  // hashed windows: the narrowest size whose windows fit WMAX
+  while (nwin(smin) > WMAX) smin++;
+  const uint32_t WD = hashed ? 0u : (uint32_t)nwin(DB);
+  // ---- plan: direct — every call on WD windows of 2^DB addresses; hashed — a window size per call
+  // (about NW_HTARGET PCs per window); regions, blocks, work items ----
   std::vector<PGroup> hpg(G);
   std::vector<NwGroup> hng(G + 1);
   uint64_t kw = 0, slots = 0;
   uint64_t nreg = 0;
   std::vector<ColItem> hcol;
   for (uint32_t g = 0; g < G; g++) {
-    // regions: one per (member segment of 2^(32 - DB) members, window)
+    uint32_t S = DB, W = WD;
+    if (hashed) {
+      const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(WMAX, (hpcs[g] + NW_HTARGET - 1) / NW_HTARGET));
+      S = smin;
+      while (S < SMAX && nwin(S + 1) >= want) S++;
+      W = (uint32_t)nwin(S);
+    }
+    // regions: one per (member segment of 2^(32 - S) members, window)
     const uint64_t ngm = hstart[g + 1] - hstart[g];
-    const uint32_t nseg = (uint32_t)((ngm + (1ull << (32 - DB)) - 1) >> (32 - DB));
-    hpg[g] = PGroup{DB, WD, (uint32_t)PMODE_DIRECT, (uint32_t)nreg};
-    nreg += (uint64_t)nseg * WD;
+    const uint32_t nseg = (uint32_t)((ngm + (1ull << (32 - S)) - 1) >> (32 - S));
+    hpg[g] = PGroup{S, W, (uint32_t)(hashed ? PMODE_HASH : PMODE_DIRECT), (uint32_t)nreg};
+    nreg += (uint64_t)nseg * W;
     for (uint32_t sg = 0; sg < nseg; sg++)
-      for (uint32_t w0 = 0; w0 < WD; w0 += 64) hcol.push_back(ColItem{g, sg, w0, 0});
+      for (uint32_t w0 = 0; w0 < W; w0 += 64) hcol.push_back(ColItem{g, sg, w0, 0});
     hng[g] = NwGroup{kw, slots};
-    kw += (uint64_t)WD << (DB - 5);
-    slots += WD + 1;
+    if (!hashed) kw += (uint64_t)W << (S - 5);
+    slots += W + 1;
   }
   if (nreg >= (1ull << 31)) return false;
   hng[G] = NwGroup{kw, slots};
@@ -402,10 +675,12 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   std::vector<uint32_t> order(G);
   std::iota(order.begin(), order.end(), 0u);
   std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hpcs[x] > hpcs[y]; });
-  const size_t nitems = (size_t)G * WD;
-  // one staging copy: PGroup[G+1], NwGroup[G+1], gblock[G+1], order[G+1]
+  std::vector<uint32_t> iofs(G + 1, 0);  // hashed: the items of order[j] are [iofs[j], iofs[j + 1])
+  for (uint32_t j = 0; j < G; j++) iofs[j + 1] = iofs[j] + hpg[order[j]].W;
+  const size_t nitems = hashed ? (size_t)iofs[G] : (size_t)G * WD;
+  // one staging copy: PGroup[G+1], NwGroup[G+1], gblock[G+1], order[G+1], iofs[G+1], ColItem[]
   const size_t o_ng = (G + 1) * sizeof(PGroup), o_gb = o_ng + (G + 1) * sizeof(NwGroup), o_or = o_gb + (G + 1) * 4;
-  const size_t o_ci = o_or + (G + 1) * 4;
+  const size_t o_io = o_or + (G + 1) * 4, o_ci = o_io + (G + 1) * 4;
   const size_t stage_bytes = o_ci + (hcol.size() + 1) * sizeof(ColItem);
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
   uint8_t* dstage = sc.get<uint8_t>("nw_stage", stage_bytes + 64);
@@ -413,12 +688,14 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   std::memcpy(stage + o_ng, hng.data(), (G + 1) * sizeof(NwGroup));
   std::memcpy(stage + o_gb, hgblock.data(), (G + 1) * 4);
   std::memcpy(stage + o_or, order.data(), G * 4);
+  std::memcpy(stage + o_io, iofs.data(), (G + 1) * 4);
   if (!hcol.empty()) std::memcpy(stage + o_ci, hcol.data(), hcol.size() * sizeof(ColItem));
   SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
   const PGroup* dpg = reinterpret_cast<const PGroup*>(dstage);
   const NwGroup* dng = reinterpret_cast<const NwGroup*>(dstage + o_ng);
   const uint32_t* dgblock = reinterpret_cast<const uint32_t*>(dstage + o_gb);
   const uint32_t* dorder = reinterpret_cast<const uint32_t*>(dstage + o_or);
+  const uint32_t* diofs = reinterpret_cast<const uint32_t*>(dstage + o_io);
   const ColItem* dcol = reinterpret_cast<const ColItem*>(dstage + o_ci);
   uint32_t* dbgroup = sc.get<uint32_t>("nw_bgroup", (size_t)B + 1);
   if (B) {
@@ -469,8 +746,24 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
         rstart, elems, err, ns);
     SYZ_LAUNCHED();
   }
+  uint64_t* hbase = nullptr;
+  uint32_t* hkeys = nullptr;
+  if (hashed) {
+    ProfScope ps("novelty_min_hash", s, total * 8 + slots * 20);
+    uint32_t* hcap = sc.get<uint32_t>("nw_hcap", slots + 1);
+    hbase = sc.get<uint64_t>("nw_hbase", slots + 1);
+    hkeys = sc.get<uint32_t>("nw_hkeys", total + 8);
+    k_nw_hcap<<<grid_for(slots, 256, 4096), 256, 0, s>>>(dng, dpg, cstart, rtot, G, slots, hcap);
+    SYZ_LAUNCHED();
+    exclusive_scan_u32(hcap, hbase, slots, s);
+    if (nitems) {
+      k_nw_hash<<<(unsigned)nitems, NH_BLOCK, 0, s>>>(dorder, diofs, G, dpg, rstart, rtot, elems, cstart, lo, d_fl, nfl,
+                                                  dng, hbase, hkeys, wcount, sel8, upd, err, nwh_dbg());
+      SYZ_LAUNCHED();
+    }
+  }
   uint32_t* fstart = sc.get<uint32_t>("nw_fstart", (size_t)WD + 2);
-  {
+  if (!hashed) {
     ProfScope ps("novelty_min", s, total * 4 + kw * 4);
     k_nw_fstart<<<grid_for(WD + 1, 256, 64), 256, 0, s>>>(d_fl, nfl, lo, WD, DB, fstart);
     SYZ_LAUNCHED();
@@ -489,7 +782,8 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     k_nw_sent<<<grid_for(G, 256, 64), 256, 0, s>>>(has_sent, upd, dng, G, wcount);
     SYZ_LAUNCHED();
     exclusive_scan_u32(wcount, wpos, slots, s);
-    k_nw_emit<<<(unsigned)slots, NE_BLOCK, 0, s>>>(kbits, wpos, dng, dpg, G, lo, d_out, out_cap, d_ooff, err);
+    k_nw_emit<<<(unsigned)slots, NE_BLOCK, 0, s>>>(kbits, wpos, dng, dpg, G, lo, d_out, out_cap, d_ooff, err, hbase,
+                                                   hkeys);
     SYZ_LAUNCHED();
     k_nw_isnew<<<grid_for(nm, 256, 8192), 256, 0, s>>>(cmem, sel8, nm, (uint32_t)n, d_new);
     SYZ_LAUNCHED();

@@ -22,12 +22,13 @@ from syzkaller_amd import _lib, cover, synth  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["windows", "table", "keys", "sort"])
+@pytest.fixture(autouse=True, params=["windows", "hwindows", "table", "keys", "sort"])
 def strategy(request, monkeypatch):
-    """Every device strategy: PC windows on the Minimize pipeline (default while the PC span fits
-    1024 windows of 32K addresses), the keyed first-occurrence table over G x (P+1) (the default
-    beyond), the keyed table over per-call keys, and the stable radix sort (when no table fits).
-    SYZGPU_NOVELTY is read by the library on every call."""
+    """Every device strategy: PC windows on the Minimize pipeline (the default: direct windows while
+    the PC span fits 1024 windows of 32K addresses, hashed windows beyond), the hashed windows forced
+    whatever the span, the keyed first-occurrence table over G x (P+1) (the default for G > 4096),
+    the keyed table over per-call keys, and the stable radix sort (when no table fits). A forced
+    windows strategy fails rather than fall back. SYZGPU_NOVELTY is read by the library on every call."""
     monkeypatch.setenv("SYZGPU_NOVELTY", request.param)
     return request.param
 
@@ -127,6 +128,91 @@ def test_novelty_config3_full_size():
     fresh, mcp, mco, flakes = _config3(100_000, 1_000_000, 2_000_000)
     w_new, w_mc, w_off = oracle.novelty_mt(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes, 16)
     g_new, g_mc, g_off = cover.NoveltyBatch(fresh.pcs, fresh.off, fresh.group, 289, mcp, mco, flakes)
+    assert np.array_equal(w_off, g_off)
+    assert np.array_equal(w_mc, g_mc)
+    assert np.array_equal(w_new, g_new)
+    assert 0 < g_new.sum() < fresh.n
+
+
+def _scopes(fn):
+    """Run fn with the library's profiling scopes on; the set of scope names it recorded."""
+    import ctypes
+    L = _lib.lib()
+    L.syzgpu_profile_only(None)
+    L.syzgpu_profile_enable(1)
+    try:
+        res = fn()
+    finally:
+        cap = 4096
+        names = ctypes.create_string_buffer(48 * cap)
+        ms = np.zeros(cap, np.float32)
+        by = np.zeros(cap, np.uint64)
+        k = L.syzgpu_profile_read(names, ms.ctypes.data, by.ctypes.data, cap)
+        L.syzgpu_profile_enable(0)
+    return res, {names.raw[48 * i:48 * (i + 1)].split(b"\0")[0].decode() for i in range(k)}
+
+
+def _stretch(pcs, base, k, add=0):
+    """The monotone map base + (pc - base) * k + add (keeps every list strictly increasing)."""
+    return (np.uint64(add) + np.uint64(base) + (pcs.astype(np.uint64) - np.uint64(base)) * np.uint64(k)).astype(np.uint32)
+
+
+def _with_extremes(mcp, mco):
+    """The tables with PC 0 first in call 0's and 0xFFFFFFFE last in the last call's."""
+    add0 = not (mco[1] > 0 and mcp[0] == 0)
+    out = np.concatenate([np.zeros(int(add0), np.uint32), mcp, np.array([0xFFFFFFFE], np.uint32)])
+    mco = mco.copy()
+    mco[1:] += np.uint64(add0)
+    mco[-1] += np.uint64(1)
+    return out, mco
+
+
+@pytest.mark.parametrize("span", ["256M", "u32"])
+def test_novelty_wide_span_small_vs_literal_oracle(span, strategy):
+    # configs[2]-shaped data spread over a 280M-address span (past the direct windows' 32M) and over
+    # the whole u32 space (0 and 0xFFFFFFFE held): the default strategy must stay on the windows
+    # (hashed) and match the literal oracle
+    if strategy not in ("windows", "hwindows"):
+        pytest.skip("the windowed strategies' span coverage")
+    fresh, mcp, mco, flakes = _config3(1_000, 8_000, 100_000)
+    base = 0x81000000
+    if span == "256M":
+        f = lambda a: _stretch(a, base, 700)
+    else:  # v = (pc - base) / 4 in [0, 100000) -> v * 42949: [0, 0xFFFE...]
+        f = lambda a: ((a.astype(np.uint64) - np.uint64(base)) // np.uint64(4) * np.uint64(42949)).astype(np.uint32)
+    pcs, mcp2, fl2 = f(fresh.pcs), f(mcp), f(flakes)
+    mcp2, mco2 = _with_extremes(mcp2, mco)
+    lo, hi = int(min(pcs.min(), mcp2.min())), int(max(pcs.max(), mcp2.max()))
+    assert hi - lo >= (256 << 20)
+    if span == "u32":
+        assert lo == 0 and hi == 0xFFFFFFFE
+    new, sc = _scopes(lambda: _check(pcs, fresh.off, fresh.group, 289, mcp2, mco2, fl2))
+    assert "novelty_min_hash" in sc and "novelty_min" not in sc
+    assert 0 < new.sum() < fresh.n
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("span", ["256M", "u32"])
+def test_novelty_config3_full_size_wide_span(span, strategy):
+    # configs[2] at full size (1M fresh covers, 422M PCs) with the 2M-PC space spread over 272M
+    # addresses and over the whole u32 space: hashed windows, bit-exact against oracle_novelty_mt
+    if strategy != "windows":
+        pytest.skip("the default strategy's span coverage")
+    fresh, mcp, mco, flakes = _config3(100_000, 1_000_000, 2_000_000)
+    base = 0x81000000
+    if span == "256M":
+        f = lambda a: _stretch(a, base, 34)
+    else:  # v in [0, 2M) -> v * 2147 (<= 0xFFF...)
+        f = lambda a: ((a.astype(np.uint64) - np.uint64(base)) // np.uint64(4) * np.uint64(2147)).astype(np.uint32)
+    pcs, mcp2, fl2 = f(fresh.pcs), f(mcp), f(flakes)
+    mco2 = mco
+    if span == "u32":
+        mcp2, mco2 = _with_extremes(mcp2, mco)
+    lo, hi = int(min(pcs.min(), mcp2.min())), int(max(pcs.max(), mcp2.max()))
+    assert hi - lo >= (256 << 20)
+    w_new, w_mc, w_off = oracle.novelty_mt(pcs, fresh.off, fresh.group, 289, mcp2, mco2, fl2, 16)
+    (g_new, g_mc, g_off), sc = _scopes(lambda: cover.NoveltyBatch(pcs, fresh.off, fresh.group, 289, mcp2, mco2, fl2))
+    assert "novelty_min_hash" in sc
     assert np.array_equal(w_off, g_off)
     assert np.array_equal(w_mc, g_mc)
     assert np.array_equal(w_new, g_new)
