@@ -68,14 +68,43 @@ def parse():
     return ap.parse_args()
 
 
+# the round's committed rocprofv3 kernel summary of this bench command (tools/gpu_final.sh): its top
+# kernel by total GPU time names the roofline kernel
+ROCPROF_STATS = os.path.join(ROOT, "profiles", "r03_kernel_stats.csv")
+# rocprofv3 kernel name -> the library's profiling scope around that kernel
+ROCPROF_SCOPE = [("k_region<512, 40, false, false>", "k_region"), ("k_region<512, 40, false, true>", "k_region_count"),
+                 ("k_pmin_direct", "k_pmin_direct"), ("k_pmin_hash<false>", "k_pmin_hash"),
+                 ("k_pmin_hash<true>", "k_pmin_packed"), ("k_colscan", "k_colscan")]
+
+
+def rocprof_top(path=ROCPROF_STATS):
+    """(scope, kernel name) of the first row of the committed rocprofv3 --stats summary (rows are
+    sorted by total duration), or None."""
+    import csv
+    try:
+        rows = list(csv.DictReader(open(path)))
+    except OSError:
+        return None
+    if not rows:
+        return None
+    top = rows[0]["Name"]
+    for pat, scope in ROCPROF_SCOPE:
+        if pat in top:
+            return scope, top
+    return None
+
+
 def dominant_kernel(kern):
-    """The step's dominant kernel: the kernel scope (named after its HIP kernel, as in the rocprofv3
-    summary) with the most time in the untimed per-kernel pass, among those carrying an algorithmic
-    byte model: k_region (the scatter) 8 B per PC + 24 B per entry, k_region_count 4 B
-    per PC + 24 B per entry, k_pmin_direct / k_pmin_hash / k_pmin_packed 4 B per PC of the groups they
-    walk. That pass runs the raw pipeline's passes one after another (syzgpu_profile_enable(2)), so
-    each scope times its kernels alone and concurrent classes do not inflate each other. Phase scopes
-    (gosort_*, m_big, group_partition) span several kernels and are not candidates."""
+    """The step's dominant kernel: the top kernel of the committed rocprofv3 summary of this command
+    (ROCPROF_STATS) when it maps to a byte-modelled scope; else the kernel scope with the most time in
+    the untimed per-kernel pass among those carrying an algorithmic byte model:
+    k_region (the scatter) 8 B per PC + 24 B per entry, k_region_count 4 B per PC + 24 B per entry,
+    k_pmin_direct / k_pmin_hash / k_pmin_packed 4 B per PC of the groups they walk. That pass runs the
+    raw pipeline's passes one after another (syzgpu_profile_enable(2)), so each scope times its kernels
+    alone. Phase scopes (gosort_*, m_big, group_partition) span several kernels and are not candidates."""
+    top = rocprof_top()
+    if top and top[0] in kern and kern[top[0]]["bytes"] > 0:
+        return top[0]
     rows = [(d["ms"], name) for name, d in kern.items() if name.startswith("k_") and d["bytes"] > 0]
     return max(rows)[1] if rows else None
 
@@ -287,8 +316,11 @@ def main():
         if roof:
             roof["launches_per_step"] = round(roof_ev[roof_kernel]["launches"] / args.steps, 2)
             roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
-            roof["selection"] = ("the byte-modelled kernel with the most time in the serialized per-kernel "
-                                 "pass; achieved from its HIP events in the (concurrent) timed region")
+            top = rocprof_top()
+            roof["selection"] = (("the top kernel of the committed rocprofv3 summary %s (%s)"
+                                  % (os.path.relpath(ROCPROF_STATS, ROOT), top[1][:60])) if top and top[0] == roof_kernel
+                                 else "the byte-modelled kernel with the most time in the serialized per-kernel pass")
+            roof["selection"] += "; achieved from its HIP events in the (concurrent) timed region"
         path_bytes = 4 * int(off[-1]) + 10 * total_progs + 16 * C * C  # SURVEY.md §8(d), whole job
         cpu = None
         if args.cpu_baseline and world == 1:

@@ -247,8 +247,9 @@ constexpr uint32_t NW_HTARGET = 8192;
 constexpr int NH_BLOCK = 512;             // two workgroups per CU (74 KB of LDS each)
 constexpr uint32_t NH_PER = HS / NH_BLOCK;  // table slots per thread at compaction
 constexpr uint32_t NH_FLK = 512;         // flakes of a window kept in LDS for the lookup
-constexpr uint32_t NH_OBITS = 19;       // sub-ranges up to 2^19 addresses are ordered by a bitmap (64 KB)
-static_assert((1u << (NH_OBITS - 5)) <= 2 * HS, "the order bitmap fits the table's space");
+constexpr uint32_t NH_NB_BITS = 11;      // order buckets of a sub-range: 2048
+constexpr uint32_t NH_NB = 1u << NH_NB_BITS;
+static_assert(NH_NB + HS <= 2 * HS && NH_NB % NH_BLOCK == 0, "bucket counts and list in the table's space");
 
 __device__ __forceinline__ uint32_t hslot_nw(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - HS_BITS); }
 
@@ -405,72 +406,49 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
       }
     }
     __syncthreads();  // the table is read: its space takes the order
+    // Order: 2048 buckets by the top address bits of the sub-range (counts, a scan, the keys listed
+    // by bucket), then a key's place = its bucket's start + the keys of its bucket below it (buckets
+    // hold a few keys: PCs are spread over the window's addresses)
+    uint32_t* bcnt = tabs;               // [NH_NB] keys per bucket, then their starts
+    uint32_t* blist = tabs + NH_NB;      // [HS] the keys, bucket by bucket
+    const uint32_t bsh = sh > NH_NB_BITS ? sh - NH_NB_BITS : 0u;
     const uint32_t sbase = split ? rr << sh : 0u;
-    if (sh <= NH_OBITS) {
-      // a sub-range of <= 2^19 addresses: a presence bitmap over it, read out in address order
-      const uint32_t nw = sh >= 5 ? 1u << (sh - 5) : 1u;
-      for (uint32_t i = threadIdx.x; i < nw; i += NH_BLOCK) tabs[i] = 0;
-      __syncthreads();
+    for (uint32_t i = threadIdx.x; i < NH_NB; i += NH_BLOCK) bcnt[i] = 0;
+    __syncthreads();
+    uint32_t pib[NH_PER];  // place inside the bucket, or none
 #pragma unroll
-      for (uint32_t q = 0; q < NH_PER; q++)
-        if (kp[q]) {
-          const uint32_t o = kk[q] - sbase;
-          atomicOr(&tabs[o >> 5], 1u << (o & 31));
-        }
-      __syncthreads();
-      // each wave a contiguous range of words, read lane-strided (no bank conflicts): its count, the
-      // waves' prefix, then the bits in order, 64 words at a time with a wave scan for positions
-      constexpr uint32_t NWV = NH_BLOCK / 64;
-      const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
-      const uint32_t per = (nw + NWV - 1) / NWV, w0 = min(nw, wv * per), w1 = min(nw, w0 + per);
-      uint32_t c = 0;
-      for (uint32_t i = w0 + lane; i < w1; i += 64) c += (uint32_t)__popc(tabs[i]);
-      uint32_t tot;
-      uint32_t p = kc + block_excl_scan<NH_BLOCK>(c, red, &tot);  // lane order = word order mod 64 only
-      p = __shfl(p, 0, 64);  // the wave's first position (lane 0's exclusive prefix)
-      for (uint32_t i0 = w0; i0 < w1; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        uint32_t m = i < w1 ? tabs[i] : 0u;
-        const uint32_t cm = (uint32_t)__popc(m);
-        const uint32_t inc = wave_incl_scan(cm);
-        uint32_t q = p + inc - cm;
-        while (m) {
-          const uint32_t b = __ffs(m) - 1;
-          m &= m - 1;
-          out[q++] = sbase + 32u * i + b;
-        }
-        p += __shfl(inc, 63, 64);
+    for (uint32_t q = 0; q < NH_PER; q++)
+      pib[q] = kp[q] ? atomicAdd(&bcnt[(kk[q] - sbase) >> bsh], 1u) : 0xFFFFFFFFu;
+    __syncthreads();
+    {
+      constexpr uint32_t PERB = NH_NB / NH_BLOCK;  // buckets per thread
+      uint32_t x[PERB], c = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < PERB; k++) {
+        x[k] = bcnt[threadIdx.x * PERB + k];
+        c += x[k];
       }
-      kc += tot;
-    } else {
-      // wider (calls with few PCs per window): the kept offsets compacted, then a bitonic sort
-      uint32_t c = 0;
-#pragma unroll
-      for (uint32_t q = 0; q < NH_PER; q++) c += kp[q] ? 1u : 0u;
       uint32_t nk;
-      uint32_t p = block_excl_scan<NH_BLOCK>(c, red, &nk);
-      uint32_t P = 1;
-      while (P < nk) P <<= 1;
+      uint32_t pre = block_excl_scan<NH_BLOCK>(c, red, &nk);
+#pragma unroll
+      for (uint32_t k = 0; k < PERB; k++) {
+        bcnt[threadIdx.x * PERB + k] = pre;
+        pre += x[k];
+      }
+      __syncthreads();
 #pragma unroll
       for (uint32_t q = 0; q < NH_PER; q++)
-        if (kp[q]) keys[p++] = kk[q];
-      for (uint32_t i = nk + threadIdx.x; i < P; i += NH_BLOCK) keys[i] = 0xFFFFFFFFu;
+        if (pib[q] != 0xFFFFFFFFu) blist[bcnt[(kk[q] - sbase) >> bsh] + pib[q]] = kk[q];
       __syncthreads();
-      for (uint32_t k = 2; k <= P; k <<= 1)
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-          for (uint32_t i = threadIdx.x; i < P; i += NH_BLOCK) {
-            const uint32_t l = i ^ jj;
-            if (l > i) {
-              const uint32_t a = keys[i], b = keys[l];
-              if ((a > b) == ((i & k) == 0)) {
-                keys[i] = b;
-                keys[l] = a;
-              }
-            }
-          }
-          __syncthreads();
+#pragma unroll
+      for (uint32_t q = 0; q < NH_PER; q++)
+        if (pib[q] != 0xFFFFFFFFu) {
+          const uint32_t bk = (kk[q] - sbase) >> bsh;
+          const uint32_t b0 = bcnt[bk], b1 = bk + 1 < NH_NB ? bcnt[bk + 1] : nk;
+          uint32_t r = b0;
+          for (uint32_t i = b0; i < b1; i++) r += blist[i] < kk[q] ? 1u : 0u;
+          out[kc + r] = kk[q];
         }
-      for (uint32_t i = threadIdx.x; i < nk; i += NH_BLOCK) out[kc + i] = keys[i];
       kc += nk;
     }
     round++;
