@@ -44,16 +44,17 @@ def lpt_assign(weights, nranks):
 
 
 # ---- key-space sharding: call groups split over ranks by dense-PC windows ----------
-# Cost model of one rank's step, calibrated on MI355X with the bench workload: the
-# Go-sort latency of its largest big call group (global rounds + LDS sort, grows by a level per
-# doubling), plus the first-occurrence stream over its big groups' PCs, plus the per-entry passes
-# (sort rounds over every held entry, ranks, selection output). Small groups (<= 8192 entries) sort
-# in LDS packs and stream on the side stream, overlapped; their PCs are charged a fraction. A split
-# group costs every holder its full sort (latency and entries) but only its share of the PCs.
+# Cost model of one rank's step (ms = LAT + per-entry + per-PC terms), fitted on MI355X to the 8-rank
+# rehearsal of the bench workload (tools/gpu_emulate.sh 8:0..8:7, profiles/r03_emu8/: residuals
+# <= 0.2 ms): a fixed 0.29 ms once a rank holds a big call group (the Go sort's dependent rounds and
+# the pipeline's launches), 1.24 ns per held entry (partition, sort, ranks, selection: a split group
+# costs every holder all its entries) and 4.26 ps per PC streamed (transpose + first-occurrence
+# tables: a split group costs each holder only its share). Small groups (<= 8192 entries) sort in LDS
+# packs and stream on the side stream, overlapped; their PCs are charged a fraction.
 SMALL_GROUP = 8192
-LAT_REF_N, LAT_REF_US, LAT_PER_DOUBLING_US = 203_000, 520.0, 73.0
-US_PER_PC = 0.92e-6
-US_PER_ENTRY = 8.0e-5
+LAT_REF_N, LAT_REF_US, LAT_PER_DOUBLING_US = 203_000, 290.0, 0.0
+US_PER_PC = 4.26e-3
+US_PER_ENTRY = 1.24
 SMALL_PC_FRACTION = 0.3
 
 
