@@ -240,9 +240,13 @@ int syzgpu_minimize_grouped_fetch(int64_t* out_idx, uint64_t* group_out_off, siz
  * freed). create also builds the dense-id index (per call every distinct PC gets an id, covers become
  * id lists split at 32768-id windows), which minimizeCorpus, the cover analytics and key parts run on;
  * create therefore needs canonical covers (sorted, duplicate-free: what the executor produces,
- * executor.cc:572-585). Appends and keeps make the index stale: Minimize then runs on the raw
- * pipeline over the covers (same results, no rebuild), the analytics and set_parts rebuild it, and
- * syzgpu_corpus_reindex rebuilds it on request. */
+ * executor.cc:572-585). Appends and keeps update the index in place (corpus_inc.hip: new PCs get the
+ * next ids of their call, appended id vectors join the stream's tail, a keep is applied by the index's
+ * next user as one relayout of the stream), so Minimize stays on it; if an update cannot be made
+ * (non-canonical appended covers, an entry kept twice, key parts set) the index is dropped and
+ * Minimize runs on the raw pipeline over the covers (same results). The analytics rebuild an updated
+ * index from the covers (its id -> PC table is not extended), set_parts and syzgpu_corpus_reindex
+ * rebuild it on request. */
 typedef struct syzgpu_corpus syzgpu_corpus;
 int syzgpu_corpus_create(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                          const uint16_t* prog_len /* may be NULL */, size_t n, uint32_t ngroups,
@@ -253,8 +257,9 @@ int syzgpu_corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uin
 int syzgpu_corpus_destroy(syzgpu_corpus* c);
 /* mgr.corpus = append(mgr.corpus, inputs...) (NewInput, syz-manager/manager.go:609-616): appends n
  * covers (CSR, offsets from 0; group ids < the store's ngroups, checked by the next minimize) in
- * place, O(new covers): one device copy plus a host read of two offsets. *out (may be NULL) receives
- * the same handle. Batch the inputs of an RPC into one call: every call synchronises its stream. */
+ * place, O(new covers): one device copy plus a host read of two offsets, and the index update (O(new
+ * covers + the stream's tail), plus the group partition). *out (may be NULL) receives the same
+ * handle. Batch the inputs of an RPC into one call: every call synchronises its stream. */
 int syzgpu_corpus_append(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                          const uint16_t* prog_len /* may be NULL */, size_t n, syzgpu_corpus** out);
 int syzgpu_corpus_append_dev(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
@@ -276,12 +281,12 @@ int syzgpu_corpus_minimize_ordered_dev(syzgpu_corpus* c, int32_t C, uint8_t* sel
  * may be NULL) = the new corpus's size. Returns after the keep. */
 int syzgpu_corpus_minimize_keep_dev(syzgpu_corpus* c, int32_t C, uint8_t* selected, int64_t* len_hist,
                                     int64_t* out_idx, uint64_t* group_out_off, void* stream, uint64_t* kept);
-/* Rebuild the dense-id index now if appends or keeps made it stale. */
+/* Rebuild the dense-id index now if there is none (or apply a recorded keep to it). */
 int syzgpu_corpus_reindex(syzgpu_corpus* c, void* stream);
 /* info[0..11] = entries, calls, PCs, distinct (call, PC) ids, work items, shared window tables,
  * 16-byte id vectors of the stream, entries and PCs of the call groups sorted by the global rounds
  * (more than 8192 entries), id vectors of those groups in this store's key parts / in all, and 1 if
- * the index is current (fields 3..10 are 0 while it is stale) */
+ * an index is kept (fields 3..10 are 0 without one) */
 int syzgpu_corpus_info(const syzgpu_corpus* c, uint64_t* info, size_t cap);
 
 /* Key-space sharding of minimizeCorpus over ranks (the multi-GPU form of manager.go:523-527; no

@@ -363,7 +363,7 @@ int syzgpu_corpus_cover_stats_dev(syzgpu_corpus* cp, uint64_t* call_inputs, uint
     if (!cp) fail(SYZGPU_EINVAL, "null corpus");
     CorpusHandle& H = *reinterpret_cast<CorpusHandle*>(cp);
     std::lock_guard<std::recursive_mutex> hl_(H.mu);
-    corpus_cover_stats_dev(corpus_index(H, (hipStream_t)stream), call_inputs, call_cover, call_unique, totals,
+    corpus_cover_stats_dev(corpus_index_full(H, (hipStream_t)stream), call_inputs, call_cover, call_unique, totals,
                            input_unique, (hipStream_t)stream);
   })
 }
@@ -375,7 +375,7 @@ int syzgpu_corpus_cover_stats(syzgpu_corpus* cp, uint64_t* call_inputs, uint64_t
     CorpusHandle& H = *reinterpret_cast<CorpusHandle*>(cp);
     std::lock_guard<std::recursive_mutex> hl_(H.mu);
     hipStream_t s = C_.stream;
-    Corpus& K = corpus_index(H, s);
+    Corpus& K = corpus_index_full(H, s);
     const uint32_t G = K.G;
     const size_t n = K.n;
     uint64_t* d = C_.scratch.get<uint64_t>("cs_out", 3ull * G + 4);
@@ -398,7 +398,7 @@ int syzgpu_corpus_cover(syzgpu_corpus* cp, int64_t call, int unique, uint32_t* o
     CorpusHandle& H = *reinterpret_cast<CorpusHandle*>(cp);
     std::lock_guard<std::recursive_mutex> hl_(H.mu);
     hipStream_t s = C_.stream;
-    Corpus& K = corpus_index(H, s);
+    Corpus& K = corpus_index_full(H, s);
     uint32_t* d = C_.scratch.get<uint32_t>("cs_list", K.total_ids + 1);
     const uint64_t len = corpus_cover(K, call, unique, d, K.total_ids + 1, s);
     *out_n = len;

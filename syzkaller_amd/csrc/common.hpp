@@ -1,6 +1,9 @@
 // Shared runtime pieces of libsyzgpu.so: error handling, the per-device context with grow-only
 // scratch buffers, and wave64 / workgroup primitives used by every kernel.
 #pragma once
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -164,6 +167,22 @@ struct ProfScope {
 void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s);
 // tag: a distinct scratch name for scans that may run on another stream at the same time
 void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s, const char* tag = "");
+
+// Host-side phase timing for development (SYZGPU_PHASE_TIMING=1: each mark drains the stream and
+// prints the wall time since the previous mark to stderr); off, a mark costs nothing.
+struct PhaseTimer {
+  bool on;
+  const char* what;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseTimer(const char* w) : on(getenv("SYZGPU_PHASE_TIMING") != nullptr), what(w), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* name, hipStream_t s) {
+    if (!on) return;
+    (void)hipStreamSynchronize(s);
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[phase] %s.%s %.3f ms\n", what, name, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
 void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s);
 
 inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {

@@ -84,12 +84,39 @@ static void swap_grow(Grow<T>& a, Grow<T>& b) {
 }
 
 Corpus& corpus_index(CorpusHandle& H, hipStream_t s) {
+  if (H.index && H.index->keep_pending) {
+    try {
+      corpus_index_sync(*H.index, H, s);
+    } catch (...) {
+      H.index.reset();
+    }
+  }
   if (!H.index) {
     H.index.reset(corpus_create_dev(H.pcs.p, H.off.p, H.group.p, H.prog_len.p, H.n, H.G, s));
     if (H.parts_set)
       corpus_set_parts(*H.index, H.part.data(), H.nparts.data(), H.has_count_hist ? H.count_hist.data() : nullptr, s);
   }
   return *H.index;
+}
+
+Corpus& corpus_index_full(CorpusHandle& H, hipStream_t s) {
+  if (H.index && H.index->incremental) H.index.reset();
+  return corpus_index(H, s);
+}
+
+// the index (if any) follows a change of H's covers, or is dropped
+template <class F>
+static void index_follow(CorpusHandle& H, F f) {
+  if (!H.index) return;
+  if (H.parts_set || getenv("SYZGPU_NO_INC_INDEX")) {
+    H.index.reset();
+    return;
+  }
+  try {
+    f(*H.index);
+  } catch (...) {
+    H.index.reset();
+  }
 }
 
 static uint32_t max_len_dev(const uint16_t* a, size_t n, hipStream_t s) {
@@ -124,7 +151,9 @@ static void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* 
   const uint64_t Lm = h[1];
   if (Lm && !pcs) fail(SYZGPU_EINVAL, "null pointer");
   const size_t n = H.n, nt = n + m;
+  const uint64_t L0 = H.L;
   if (nt >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
+  index_follow(H, [&](Corpus& K) { corpus_index_sync(K, H, s); });  // a recorded keep first
   grow_keep(H.pcs, H.L, H.L + Lm + 1, s);
   grow_keep(H.off, n + 1, nt + 1, s);
   grow_keep(H.group, n, nt + 1, s);
@@ -138,8 +167,8 @@ static void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* 
   H.max_prog_len = std::max(H.max_prog_len, prog_len ? max_len_dev(prog_len, m, s) : 0u);
   H.n = nt;
   H.L += Lm;
-  H.index.reset();
   H.path = 0;
+  index_follow(H, [&](Corpus& K) { corpus_index_append(K, H, n, L0, s); });
 }
 
 static CorpusHandle* handle_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
@@ -147,15 +176,18 @@ static CorpusHandle* handle_create_dev(const uint32_t* pcs, const uint64_t* off,
   if (G == 0 || G > 4096) fail(SYZGPU_EINVAL, "ngroups out of range (1..4096)");
   std::unique_ptr<CorpusHandle> H(new CorpusHandle());
   H->G = G;
-  append_covers(*H, pcs, off, group, prog_len, n, s);
+  append_covers(*H, pcs, off, group, prog_len, n, s);  // (no index yet: nothing to follow)
   corpus_index(*H, s);  // validates the covers (canonical, group ids) and serves minimize at once
   SYZ_HIP(hipStreamSynchronize(s));
   return H.release();
 }
 
 // mgr.corpus = the entries idx[0..m) (device int64), in that order
-static void keep_entries(CorpusHandle& H, const int64_t* idx, size_t m, hipStream_t s) {
+// distinct: idx is minimize's kept list (in range, no entry twice), so the kept PCs fit the old
+// count and the gather goes out before the one wait
+static void keep_entries(CorpusHandle& H, const int64_t* idx, size_t m, hipStream_t s, bool distinct = false) {
   if (m && !idx) fail(SYZGPU_EINVAL, "null pointer");
+  index_follow(H, [&](Corpus& K) { corpus_index_sync(K, H, s); });  // a recorded keep first
   Scratch& sc = ctx().scratch;
   uint32_t* len = sc.get<uint32_t>("co_len", m + 1);
   uint32_t* info = sc.get<uint32_t>("co_info", 2);
@@ -170,27 +202,37 @@ static void keep_entries(CorpusHandle& H, const int64_t* idx, size_t m, hipStrea
   }
   exclusive_scan_u32(len, H.off2.p, m, s);
   uint64_t* h = ctx().pinned.get<uint64_t>(2);
+  if (distinct) {
+    H.pcs2.ensure(H.L + 1);
+    if (m) {
+      k_keep_pcs<<<grid_for(m * 64, 256, 65536), 256, 0, s>>>(idx, m, H.n, H.pcs.p, H.off.p, H.off2.p, H.pcs2.p);
+      SYZ_LAUNCHED();
+    }
+  }
   SYZ_HIP(hipMemcpyAsync(&h[0], H.off2.p + m, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipMemcpyAsync(&h[1], info, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   const uint32_t* hi = reinterpret_cast<const uint32_t*>(&h[1]);
   if (hi[0]) fail(SYZGPU_EINVAL, "kept entry index out of range");
   const uint64_t L2 = m ? h[0] : 0;
-  H.pcs2.ensure(L2 + 1);
-  if (m && L2) {
-    k_keep_pcs<<<grid_for(m * 64, 256, 65536), 256, 0, s>>>(idx, m, H.n, H.pcs.p, H.off.p, H.off2.p, H.pcs2.p);
-    SYZ_LAUNCHED();
+  if (!distinct) {
+    H.pcs2.ensure(L2 + 1);
+    if (m && L2) {
+      k_keep_pcs<<<grid_for(m * 64, 256, 65536), 256, 0, s>>>(idx, m, H.n, H.pcs.p, H.off.p, H.off2.p, H.pcs2.p);
+      SYZ_LAUNCHED();
+    }
+    SYZ_HIP(hipStreamSynchronize(s));  // the old covers are the next keep's target
   }
-  SYZ_HIP(hipStreamSynchronize(s));  // the old covers are the next keep's target
   swap_grow(H.pcs, H.pcs2);
   swap_grow(H.off, H.off2);
   swap_grow(H.group, H.group2);
   swap_grow(H.prog_len, H.prog_len2);
+  const size_t n0 = H.n;
   H.n = m;
   H.L = L2;
   H.max_prog_len = hi[1];
-  H.index.reset();
   H.path = 0;
+  index_follow(H, [&](Corpus& K) { corpus_index_keep(K, H, idx, m, n0, s); });
 }
 
 static void handle_begin(CorpusHandle& H, hipStream_t s) {
@@ -244,15 +286,19 @@ static void handle_end(CorpusHandle& H, int32_t C, uint8_t* selected, int64_t* l
 static uint64_t minimize_keep(CorpusHandle& H, int32_t C, uint8_t* selected, int64_t* len_hist, int64_t* out_idx,
                               uint64_t* group_out_off, hipStream_t s) {
   Scratch& sc = ctx().scratch;
+  PhaseTimer pt("minimize_keep");
   int64_t* out = out_idx ? out_idx : sc.get<int64_t>("co_out", H.n + 1);
   uint64_t* goff = group_out_off ? group_out_off : sc.get<uint64_t>("co_goff", H.G + 1);
   handle_begin(H, s);
+  pt.mark(H.path == 1 ? "begin_index" : "begin_raw", s);
   handle_end(H, C, selected, len_hist, out, goff, s);
+  pt.mark("end", s);
   uint64_t* h = ctx().pinned.get<uint64_t>(1);
   SYZ_HIP(hipMemcpyAsync(h, goff + H.G, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   const uint64_t m = *h;
-  keep_entries(H, out, m, s);
+  keep_entries(H, out, m, s, true);
+  pt.mark("keep", s);
   return m;
 }
 
@@ -425,6 +471,7 @@ int syzgpu_corpus_info(const syzgpu_corpus* cp, uint64_t* info, size_t cap) {
     if (!info) fail(SYZGPU_EINVAL, "null pointer");
     CorpusHandle& H = H_of(const_cast<syzgpu_corpus*>(cp));
     std::lock_guard<std::recursive_mutex> hl_(H.mu);
+    if (H.index && H.index->keep_pending) corpus_index(H, C_.stream);  // a recorded keep applied
     uint64_t v[12] = {H.n, H.G, H.L, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (H.index) {
       const Corpus& K = *H.index;

@@ -11,9 +11,10 @@ namespace syz {
 // mgr.corpus (manager.go:52-65) as device-resident CSR covers: the source of truth. NewInput appends
 // to it in place (manager.go:609-616, O(new covers)); minimizeCorpus replaces it by its kept entries
 // in Go's order (mgr.corpus = newCorpus, manager.go:523-529, one gather). Minimize runs on the
-// dense-id index (Corpus, ≈0.7 ms at 1M programs) while that matches the covers, and on the raw
-// pipeline (panels.hip, no build) once appends or a keep have made it stale; the index is rebuilt
-// only for what needs it: the cover analytics, key-space parts, or an explicit reindex.
+// dense-id index (Corpus, ≈0.7 ms at 1M programs), which appends and keeps update in place
+// (corpus_inc.hip); without an index (never built, or dropped by a failed update or key-space parts)
+// on the raw pipeline (panels.hip, no build). The index is built for what needs it: the cover
+// analytics, key-space parts, or an explicit reindex.
 struct CorpusHandle {
   std::recursive_mutex mu;  // one call on a corpus at a time (mgr.mu serialises them in the reference)
   size_t n = 0;
@@ -37,5 +38,14 @@ struct CorpusHandle {
 
 // The index of H's current covers, built (with H's key parts) if stale.
 Corpus& corpus_index(CorpusHandle& H, hipStream_t s);
+// The same with its id -> PC dictionary complete (rebuilt if appends or keeps were applied to it
+// incrementally): the cover analytics' form.
+Corpus& corpus_index_full(CorpusHandle& H, hipStream_t s);
+// corpus_inc.hip: the index brought up to H after an append (H's entries from n0 and PCs from L0 are
+// new) or a keep (H = the old entries idx[0..m) of n0); they throw on failure (the caller drops it)
+void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L0, hipStream_t s);
+void corpus_index_keep(Corpus& K, const CorpusHandle& H, const int64_t* idx, size_t m, size_t n0, hipStream_t s);
+// a recorded keep applied (the index's users call it first: corpus_index does)
+void corpus_index_sync(Corpus& K, const CorpusHandle& H, hipStream_t s);
 
 }  // namespace syz

@@ -1458,6 +1458,16 @@ GosortPlan::~GosortPlan() {
 }
 
 void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ngroups, hipStream_t s) {
+  // a plan may be re-made for a new layout (the incremental corpus index): the old arrays go first
+  // (their last users ran on s), the learned round count stays as a hint
+  if (P.small || P.packs || P.big) SYZ_HIP(hipStreamSynchronize(s));
+  if (P.small) (void)hipFree(P.small);
+  if (P.packs) (void)hipFree(P.packs);
+  if (P.big) (void)hipFree(P.big);
+  P.small = nullptr;
+  P.packs = nullptr;
+  P.big = nullptr;
+  P.big_max = 0;
   std::vector<Seg> big, small;
   std::vector<Pack> packs;
   for (uint32_t g = 0; g < ngroups; g++) {

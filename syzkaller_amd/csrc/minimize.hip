@@ -716,6 +716,7 @@ __global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict_
       }
     }
     for (; v < w.vend; v += VM_BLOCK) vec_update(tab, ids16[v], rank_of_member[vmem[v]]);
+    for (v = w.tbeg + threadIdx.x; v < w.tend; v += VM_BLOCK) vec_update(tab, ids16[v], rank_of_member[vmem[v]]);
     __syncthreads();
     if (w.gtab == RANK_NONE) {
       const uint64_t gb = gstart[w.g];
@@ -798,7 +799,7 @@ __global__ void k_gather_u64(const uint64_t* src, const uint64_t* idx, size_t n,
 // Orders this rank's work items and uploads them: big call groups (sorted by the global rounds)
 // first, small ones (LDS packs, sorted on the side stream) after, so each class's Minimize runs as
 // soon as its own sort is done; largest first inside a class, so the tail of the grid is short.
-static void corpus_upload_work(Corpus& K, hipStream_t s) {
+void corpus_upload_work(Corpus& K, hipStream_t s) {
   const std::vector<uint64_t>& hstart = K.hstart;
   auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
   std::stable_sort(K.hwork.begin(), K.hwork.end(), [&](const VecWork& x, const VecWork& y) {
@@ -810,7 +811,7 @@ static void corpus_upload_work(Corpus& K, hipStream_t s) {
   K.big_vecs = 0;
   while (K.nbig_work < K.hwork.size() && is_big(K.hwork[K.nbig_work].g))
     K.big_vecs += K.hwork[K.nbig_work].vend - K.hwork[K.nbig_work].vbeg, K.nbig_work++;
-  K.work.alloc(K.hwork.size());
+  K.work.ensure(K.hwork.size());
   if (!K.hwork.empty())
     SYZ_HIP(hipMemcpyAsync(K.work.p, K.hwork.data(), K.hwork.size() * sizeof(VecWork), hipMemcpyHostToDevice, s));
   // work items per shared table: the vec_min chunk that brings the count to it emits the table
@@ -995,6 +996,8 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   }
   hgdict[G] = hds[nbuckets];
   K.total_ids = hds[nbuckets];
+  K.hnids.assign(G, 0);
+  for (uint32_t g = 0; g < G; g++) K.hnids[g] = hgdict[g + 1] - hgdict[g];
   K.dict.alloc(K.total_ids);
   K.gdict.alloc(G + 1);
   K.nwin.alloc(G);
@@ -1072,6 +1075,7 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   uint64_t chunk_vecs = std::min<uint64_t>(
       CHUNK_VECS_MAX, std::max<uint64_t>(CHUNK_VECS_MIN, (K.total_vecs / 300 + 4095) / 4096 * 4096));
   if (const char* cv = getenv("SYZGPU_CHUNK_VECS")) chunk_vecs = std::max<uint64_t>(1, strtoull(cv, nullptr, 10));
+  K.chunk_vecs = chunk_vecs;
   size_t pi = 0;
   for (uint32_t g = 0; g < G; g++) {
     const uint64_t p_g = hgdict[g + 1] - hgdict[g];
@@ -1120,6 +1124,61 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   return cp.release();
 }
 
+
+// The group partition of K's current entries (K.off, K.group, K.n): members, gstart, member_of, the
+// Go-sort keys el0, hstart and the Go-sort plan; hpcs = PCs per call. The incremental index
+// (corpus_inc.hip) re-runs it after an append or a keep; it is corpus_create_dev's step 1.
+void corpus_partition(Corpus& K, std::vector<uint64_t>& hpcs, hipStream_t s) {
+  Scratch& sc = ctx().scratch;
+  const size_t n = K.n;
+  const uint32_t G = K.G;
+  const uint32_t pw = grp_pw(n, G);
+  const uint32_t nchunks = (uint32_t)((n + pw - 1) / pw);
+  int* err = sc.get<int>("cs_err", 2);
+  uint32_t* cnt = sc.get<uint32_t>("mz_cnt", (size_t)G * nchunks + 1);
+  uint64_t* cnt_scan = sc.get<uint64_t>("mz_cnt_scan", (size_t)G * nchunks + 1);
+  uint64_t* gpcs = sc.get<uint64_t>("mz_gpcs", G + 1);
+  K.members.ensure(n + 1);
+  K.member_of.ensure(n + 1);
+  K.el0.ensure(n + 1);
+  if (!K.gstart.p) K.gstart.alloc(G + 1);
+  SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
+  SYZ_HIP(hipMemsetAsync(cnt, 0, ((size_t)G * nchunks + 1) * 4, s));
+  SYZ_HIP(hipMemsetAsync(gpcs, 0, (G + 1) * 8, s));
+  if (n) {
+    const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
+    k_grp_count<<<wg, 256, 4 * G * 4, s>>>(K.group.p, n, G, nchunks, pw, cnt, err);
+    SYZ_LAUNCHED();
+    k_grp_sumlen<<<grid_for(n, 256, 2048), 256, G * 8, s>>>(K.group.p, K.off.p, n, G, gpcs);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(cnt, cnt_scan, (size_t)G * nchunks, s);
+  k_grp_starts<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(cnt_scan, G, nchunks, n, K.gstart.p);
+  SYZ_LAUNCHED();
+  if (n) {
+    const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
+    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(K.group.p, K.off.p, n, G, nchunks, pw, cnt_scan, K.members.p, K.el0.p);
+    SYZ_LAUNCHED();
+    k_invert<<<grid_for(n, 256, 4096), 256, 0, s>>>(K.members.p, n, K.member_of.p);
+    SYZ_LAUNCHED();
+  }
+  std::vector<uint64_t> hstart(G + 1);
+  hpcs.assign(G, 0);
+  int herr[2];
+  SYZ_HIP(hipMemcpyAsync(hstart.data(), K.gstart.p, (G + 1) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hpcs.data(), gpcs, G * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (herr[0]) fail(SYZGPU_EINVAL, "group id >= ngroups");
+  K.hstart = hstart;
+  K.big_entries = K.big_pcs = 0;
+  for (uint32_t g = 0; g < G; g++)
+    if (hstart[g + 1] - hstart[g] > GS_T_SEG) {
+      K.big_entries += hstart[g + 1] - hstart[g];
+      K.big_pcs += hpcs[g];
+    }
+  gosort_plan(K.gsplan, hstart, G, s);
+}
 
 // minimizeCorpus, first half: the Go-sort ranks and the first-occurrence pass into the rank bitmap
 // (this rank's key parts only, see corpus_set_parts).

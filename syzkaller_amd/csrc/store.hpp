@@ -1,6 +1,7 @@
 // The resident corpus store (the device analog of syz-manager's mgr.corpus, manager.go:52-65),
 // shared by Minimize (minimize.hip) and the manager's cover analytics (analytics.hip).
 #pragma once
+#include <map>
 #include <vector>
 
 #include "pipeline.hpp"
@@ -28,6 +29,7 @@ struct VecWork {
   uint64_t vbeg, vend;
   uint32_t gtab;  // RANK_NONE: sole chunk of its panel, emit directly; else index of a global table
   uint32_t win;   // id window of the panel (the unit of key-space sharding)
+  uint64_t tbeg = 0, tend = 0;  // the panel's appended vectors (incremental index), walked after vbeg..vend
 };
 
 // the cover analytics of a store (analytics.hip), computed on first use and kept with it
@@ -78,6 +80,10 @@ struct DevArr {
     free();
     n = count;
     SYZ_HIP(hipMalloc(&p, (count ? count : 1) * sizeof(T)));
+  }
+  void ensure(size_t count) {  // at least count elements; the contents are not kept
+    if (p && count <= n) return;
+    alloc(count + count / 4 + 16);
   }
   void free() {
     if (p) (void)hipFree(p);
@@ -131,11 +137,27 @@ struct Corpus {
   uint32_t max_prog_len = 0;
   uint32_t ngtabs = 0;
   CoverStats* stats = nullptr;
+  // incremental maintenance (corpus_inc.hip): ids per call, the (call, PC) -> id lookup sorted by
+  // call << 32 | PC, and whether appends/keeps have left dict/gdict behind (the analytics rebuild)
+  std::vector<uint64_t> hnids;
+  DevArr<uint64_t> sd_key;
+  DevArr<uint32_t> sd_id;
+  size_t sd_n = 0;
+  bool sd_built = false, incremental = false;
+  std::vector<VecWork> hmain;  // the items over the panel-major body of the stream (no tails)
+  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint64_t>> ptail;  // panel -> appended range
+  uint64_t tail0 = 0, chunk_vecs = 0;  // first appended vector (the tail), work-item size of the body
+  DevArr<uint16_t> ids16b;             // relayout targets (swapped in)
+  DevArr<uint32_t> vmemb;
+  bool keep_pending = false;           // a keep not yet applied: mgr.corpus = the old entries keep_idx
+  size_t keep_m = 0, keep_n0 = 0;
+  DevArr<int64_t> keep_idx;
   ~Corpus() {
     corpus_stats_free(stats);
     off.free(); gstart.free(); gdict.free(); el0.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
     gtchunks.free(); gtdone.free(); count_hist.free(); xg.free(); xo.free();
-    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free();
+    gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free(); sd_key.free(); sd_id.free();
+    ids16b.free(); vmemb.free(); keep_idx.free();
   }
 };
 
@@ -150,6 +172,8 @@ void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
 void corpus_sel_xchg(Corpus& K, const uint32_t* groups, const uint64_t* offsets, uint32_t ng, uint8_t* buf,
                      int import, hipStream_t s);
 void sel_bits_bytes_dev(const uint32_t* bits, size_t n, uint8_t* out, hipStream_t s);
+void corpus_partition(Corpus& K, std::vector<uint64_t>& hpcs, hipStream_t s);
+void corpus_upload_work(Corpus& K, hipStream_t s);
 
 // Device buffer that keeps its first `used` elements when it grows (appends); 1.5x headroom.
 template <class T>

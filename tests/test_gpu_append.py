@@ -111,14 +111,14 @@ def test_manager_cycle_append_minimize_keep_vs_oracle():
     hc = HostCorpus(c, 0, 20_000)
     assert st.info()["indexed"] == 1
     s = torch.cuda.current_stream().cuda_stream
-    # NewInput x2 (host and device pointers): in place, the index goes stale
+    # NewInput x2 (host and device pointers): in place, the index follows (corpus_inc.hip)
     st.append(*_part(c, 20_000, 30_000))
     hc.append(c, 20_000, 30_000)
     p, o, g, l = (_dev(x) for x in _part(c, 30_000, 40_000))
     st.append_device(p, o, g, l, 10_000, s)
     hc.append(c, 30_000, 40_000)
-    assert st.info()["indexed"] == 0 and st.info()["entries"] == 40_000
-    _check(st, hc, G)  # raw pipeline on the stale corpus
+    assert st.info()["indexed"] == 1 and st.info()["entries"] == 40_000
+    _check(st, hc, G)  # on the appended index
     # minimizeCorpus + mgr.corpus = newCorpus in one call
     n0 = st.n
     sel = torch.zeros(n0, dtype=torch.uint8, device="cuda")
@@ -136,6 +136,7 @@ def test_manager_cycle_append_minimize_keep_vs_oracle():
     assert np.array_equal(sel.cpu().numpy(), wsel)
     hc.keep(want)
     assert st.info()["entries"] == kept and st.info()["pcs"] == sum(len(x) for x in hc.covs)
+    assert st.info()["indexed"] == 1  # the keep compacted the index rather than dropping it
     _check(st, hc, G)  # the kept corpus minimizes to itself (every input was kept for a new PC)
     # more inputs after the keep, then an explicit keep in another order, then a reindex
     st.append(*_part(c, 40_000, 60_000))
@@ -157,6 +158,51 @@ def test_manager_cycle_append_minimize_keep_vs_oracle():
     for k in ("call_inputs", "call_cover", "call_unique", "input_unique"):
         assert np.array_equal(np.asarray(g[k]), w[k]), k
     assert [g["cover"], g["unique_per_call"], g["unique_per_input"]] == [int(x) for x in w["totals"]]
+    st.close()
+
+
+@pytest.mark.parametrize("inc", [True, False])
+def test_incremental_index_new_pcs_and_windows(inc, monkeypatch):
+    # appends bring PCs the index has never seen (a wider PC space, few calls: their dense ids open
+    # new 32K-id windows), keeps drop and reorder entries, one keep repeats an entry (the index cannot
+    # follow it: it is dropped and built afresh); after every step the store minimizes like the oracle,
+    # on the maintained index (inc) or on the raw pipeline (SYZGPU_NO_INC_INDEX=1)
+    import torch
+    if not inc:
+        monkeypatch.setenv("SYZGPU_NO_INC_INDEX", "1")
+    G = 5
+    a = synth.corpus(0x5EED00B1, 8_000, G, 30_000)
+    b = synth.corpus(0x5EED00B2, 12_000, G, 400_000)
+    C = int(max(a.prog_len.max(), b.prog_len.max()))
+    st = cover.CoverStore(a.pcs, a.off, a.group, G, a.prog_len)
+    hc = HostCorpus(a, 0, a.n)
+    s = torch.cuda.current_stream().cuda_stream
+    for lo, hi in ((0, 3_000), (3_000, 3_001), (3_001, 3_001), (3_001, 9_000)):
+        st.append(*_part(b, lo, hi))
+        hc.append(b, lo, hi)
+        assert st.info()["indexed"] == (1 if inc else 0)
+        _check(st, hc, G)
+    assert st.info()["entries"] == len(hc.covs)
+    want = _check(st, hc, G)
+    kept = st.MinimizeKeep(C, None, torch.zeros(C + 1, dtype=torch.int64, device="cuda"), None, None, s)
+    assert kept == want.size
+    hc.keep(want)
+    _check(st, hc, G)
+    st.append(*_part(b, 9_000, 12_000))
+    hc.append(b, 9_000, 12_000)
+    _check(st, hc, G)
+    rnd = np.random.default_rng(5)
+    perm = rnd.permutation(len(hc.covs))[: 2 * len(hc.covs) // 3]
+    st.keep(perm)
+    hc.keep(perm)
+    _check(st, hc, G)
+    st.append(*_part(a, 0, 500))
+    hc.append(a, 0, 500)
+    _check(st, hc, G)
+    dup = np.concatenate([np.arange(100), [7]])  # entry 7 twice: the update fails, the index is rebuilt
+    st.keep(dup)
+    hc.keep(list(dup))
+    _check(st, hc, G)
     st.close()
 
 
