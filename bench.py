@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--novelty-covers", type=int, default=1_000_000)
     ap.add_argument("--novelty-wide", type=int, default=1,
                     help="also time the novelty batch with its PC span stretched 34x (272M addresses)")
+    ap.add_argument("--setops", type=int, default=1,
+                    help="also time the batched set ops on config-3 covers (triage pairs) at N=1")
     ap.add_argument("--hub", type=int, default=1, help="also time config 5's hub ingest (scan + SHA-1 + dedup) at N=1")
     ap.add_argument("--analytics", type=int, default=1, help="also time the manager's cover analytics at N=1")
     ap.add_argument("--analytics-cpu-sample", type=int, default=10_000)
@@ -332,6 +334,7 @@ def main():
         tail = text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step) if args.text and solo else None
         nov = novelty_leg(args, dev, L, read_prof) if args.novelty and solo else None
         cooc = cooccurrence_leg(args, dev, L, read_prof, corp, C) if args.cooccurrence and solo else None
+        sops = setops_leg(args, dev, L) if args.setops and solo else None
         hubr = hub_leg(args, dev, L, read_prof, corp, sptr) if args.hub and solo else None
         ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr) if args.analytics and solo else None
         app = append_leg(args, dev, store, sptr, C, d_hist) if args.append and solo else None  # last: replaces
@@ -365,6 +368,7 @@ def main():
             "minimize_corpus_tail": tail,
             "novelty_config3": nov if nov is not None else nov_sh,
             "call_cooccurrence": cooc,
+            "setops_triage": sops,
             "cover_analytics": ana,
             "hub_ingest_config5": hubr,
             "manager_cycle": app,
@@ -830,6 +834,55 @@ def novelty_leg(args, dev, L, read_prof):
         res["cpu_baseline"] = {"value": round(k / dt, 1), "unit": "covers/s", "cores": 1, "kind": "port",
                                "sample": "first %d covers of the batch; oracle/liboracle.so literal per-cover "
                                          "Difference/Union (fuzzer.go:446-470), %.2f s" % (k, dt)}
+    return res
+
+
+def setops_leg(args, dev, L):
+    """The cover set algebra in batch (cover/cover.go:42-102; triage users fuzzer.go:374-375,
+    389-406): 1M pairs (config 3's fresh covers, each against a second run of the same input with 5 %
+    of its PCs missing), device-resident; one launch sequence per op over all pairs
+    (syzgpu_setop_batch_dev). Algorithmic bytes: both inputs and their offsets read, the output and
+    its offsets written."""
+    import torch
+    from syzkaller_amd import cover, synth
+    G = args.ngroups
+    c = synth.corpus(args.seed + 0x31, args.novelty_covers, G, args.npcs)
+    n = c.n
+
+    def t(a):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+        return torch.from_numpy(np.ascontiguousarray(a).view(view.get(a.dtype, a.dtype))).to(dev)
+    da, dao = t(c.pcs), t(c.off)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    keep = torch.rand(da.numel(), generator=gen, device=dev) > 0.05
+    db = da[keep].contiguous()
+    cs = torch.zeros(keep.numel() + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(keep, 0, out=cs[1:])
+    dbo = (cs[dao] - cs[dao[:1]]).contiguous()
+    del keep, cs
+    na, nb = int(da.numel()), int(db.numel())
+    cap = na + nb + 1
+    out = torch.empty(cap, dtype=torch.int32, device=dev)
+    ooff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    res = {"workload": "1M pairs: config-3 covers (%d PCs) vs a second run with 5%% of the PCs dropped (%d PCs)"
+                       % (na, nb), "ops": {}}
+    steps = max(1, args.steps // 2)
+    for op in ("intersection", "difference", "union"):
+        tot = cover.SetOpBatchDev(op, da, dao, na, db, dbo, nb, n, out, cap, ooff, sptr)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tot = cover.SetOpBatchDev(op, da, dao, na, db, dbo, nb, n, out, cap, ooff, sptr)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        alg = 4 * (na + nb) + 16 * (n + 1) + 4 * tot + 8 * (n + 1)
+        res["ops"][op] = {"ms_per_batch": round(ms, 3), "out_pcs": int(tot), "pairs_per_s": round(n / ms * 1e3, 1),
+                          "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+                                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                       "algorithmic_bytes": int(alg)}}
     return res
 
 

@@ -85,6 +85,12 @@ int syzgpu_canonicalize_batch(uint32_t* pcs, const uint64_t* off, size_t ncov, u
 int syzgpu_setop_batch(int op, const uint32_t* a, const uint64_t* a_off, const uint32_t* b,
                        const uint64_t* b_off, size_t npairs, uint32_t* out, size_t out_cap,
                        uint64_t* out_off);
+/* The same on device-resident CSRs (a_off[0] = b_off[0] = 0; na = a_off[npairs], nb = b_off[npairs]
+ * from the caller): out / out_off device arrays, *total (host, may be NULL) = out_off[npairs]. Returns
+ * after the stream has drained. The triage users: fuzzer.go:374-375, 389-406. */
+int syzgpu_setop_batch_dev(int op, const uint32_t* a, const uint64_t* a_off, uint64_t na, const uint32_t* b,
+                           const uint64_t* b_off, uint64_t nb, size_t npairs, uint32_t* out, size_t out_cap,
+                           uint64_t* out_off, void* stream, uint64_t* total);
 
 /* syz-manager/manager.go:507-527 minimizeCorpus: Minimize every call group in one launch.
  * group[i] < ngroups is the call (CallName id) of corpus entry i. out_idx (capacity n) receives the

@@ -207,6 +207,17 @@ def SetOpBatch(op, a_list, b_list):
     return [out[int(ooff[i]):int(ooff[i + 1])].copy() for i in range(npairs)]
 
 
+def SetOpBatchDev(op, a, aoff, na, b, boff, nb, npairs, out, out_cap, ooff, stream=None):
+    """op(a_i, b_i) for npairs pairs of device-resident CSRs (torch tensors or device pointers):
+    out / ooff on the device; returns the total output length."""
+    import ctypes
+    code = _OPS[op] if isinstance(op, str) else int(op)
+    tot = ctypes.c_uint64(0)
+    check(lib().syzgpu_setop_batch_dev(code, ptr(a), ptr(aoff), na, ptr(b), ptr(boff), nb, npairs, ptr(out),
+                                       out_cap, ptr(ooff), stream, ctypes.byref(tot)))
+    return int(tot.value)
+
+
 def CanonicalizeBatch(pcs, off):
     """Canonicalize every cover of a CSR in place; returns the new lengths."""
     off = np.ascontiguousarray(off, dtype=np.uint64)

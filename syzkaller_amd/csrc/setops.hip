@@ -9,7 +9,7 @@
 //   Union                 keep every a[x]; keep b[y] iff rank_b >= ca
 //   SymmetricDifference   keep a[x] iff rank_a >= cb; keep b[y] iff rank_b >= ca
 // and 0xFFFFFFFF (the sentinel, cover.go:17) is never emitted. Outputs are placed by prefix sums
-// of the keep flags — one thread per element, no sequential merge.
+// of the keep flags — one lane per element (a wave per pair), no sequential merge.
 //
 // Canonicalize (cover.go:28-40): per-cover sort in LDS (bitonic, up to 16384 PCs = the kcov limit,
 // executor.cc:48) or a global bitonic network beyond, then unique with last = sentinel.
@@ -21,48 +21,60 @@ namespace syz {
 
 // ---- batched set operations -------------------------------------------------------------------
 
-__device__ __forceinline__ uint32_t pair_of(const uint64_t* off, uint32_t npairs, uint64_t x) {
-  // last p with off[p] <= x, off non-decreasing, p < npairs
-  uint32_t lo = 0, hi = npairs;
-  while (hi - lo > 1) {
-    uint32_t m = (lo + hi) >> 1;
-    if (off[m] <= x)
-      lo = m;
-    else
-      hi = m;
-  }
-  return lo;
+
+// Work unit: a segment of <= SO_SEG consecutive elements of one pair's list (a pair of n elements has
+// ceil(n / SO_SEG) segments; segoff = their exclusive scan over the pairs), one wave per segment
+// (grid-stride): the pair is found once per segment, so an element costs only its searches inside
+// the other list, whose few lines the wave's lanes share through L1; long lists still spread over
+// many waves.
+constexpr uint64_t SO_SEG = 1024;
+
+__global__ void k_setop_nseg(const uint64_t* off, uint32_t npairs, uint32_t* nseg) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += gridDim.x * blockDim.x)
+    nseg[p] = (uint32_t)((off[p + 1] - off[p] + SO_SEG - 1) / SO_SEG);
+}
+
+// segment sid -> (pair, element range)
+__device__ __forceinline__ uint32_t seg_pair(const uint64_t* segoff, uint32_t npairs, uint64_t sid, const uint64_t* off,
+                                             uint64_t* x0, uint64_t* x1) {
+  const uint32_t p = (uint32_t)upper_bound_dev<uint64_t>(segoff, 0, npairs + 1, sid) - 1;
+  *x0 = off[p] + (sid - segoff[p]) * SO_SEG;
+  *x1 = min(off[p + 1], *x0 + SO_SEG);
+  return p;
 }
 
 // side 0 classifies a-elements against b, side 1 b-elements against a.
 __global__ __launch_bounds__(256) void k_setop_classify(int op, int side, const uint32_t* a, const uint64_t* aoff,
                                                         const uint32_t* b, const uint64_t* boff, uint32_t npairs,
-                                                        uint64_t total, uint8_t* keep, int* err) {
-  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
-       x += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = pair_of(aoff, npairs, x);
-    const uint64_t beg = aoff[p], end = aoff[p + 1];
-    const uint32_t v = a[x];
-    if (x + 1 < end && a[x + 1] < v) atomicOr(err, 1);  // unsorted input
-    uint8_t k = 0;
-    if (v != SENT) {
-      uint64_t rank = 0;
-      if (x > beg && a[x - 1] == v) rank = x - lower_bound_dev<uint32_t>(a, beg, x, v);
-      const uint64_t lb = lower_bound_dev<uint32_t>(b, boff[p], boff[p + 1], v);
-      uint64_t cnt = 0;
-      if (lb < boff[p + 1] && b[lb] == v) cnt = upper_bound_dev<uint32_t>(b, lb, boff[p + 1], v) - lb;
-      if (side == 0) {
-        switch (op) {
-          case SYZGPU_DIFFERENCE:
-          case SYZGPU_SYMMETRIC_DIFFERENCE: k = rank >= cnt; break;
-          case SYZGPU_UNION: k = 1; break;
-          default: k = rank < cnt; break;
+                                                        const uint64_t* segoff, uint8_t* keep, int* err) {
+  const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6, nseg = segoff[npairs];
+  for (uint64_t sid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; sid < nseg; sid += waves) {
+    uint64_t x0, x1;
+    const uint32_t p = seg_pair(segoff, npairs, sid, aoff, &x0, &x1);
+    const uint64_t beg = aoff[p], end = aoff[p + 1], b0 = boff[p], b1 = boff[p + 1];
+    for (uint64_t x = x0 + __lane_id(); x < x1; x += 64) {
+      const uint32_t v = a[x];
+      if (x + 1 < end && a[x + 1] < v) atomicOr(err, 1);  // unsorted input
+      uint8_t k = 0;
+      if (v != SENT) {
+        uint64_t rank = 0;
+        if (x > beg && a[x - 1] == v) rank = x - lower_bound_dev<uint32_t>(a, beg, x, v);
+        const uint64_t lb = lower_bound_dev<uint32_t>(b, b0, b1, v);
+        uint64_t cnt = 0;
+        if (lb < b1 && b[lb] == v) cnt = upper_bound_dev<uint32_t>(b, lb, b1, v) - lb;
+        if (side == 0) {
+          switch (op) {
+            case SYZGPU_DIFFERENCE:
+            case SYZGPU_SYMMETRIC_DIFFERENCE: k = rank >= cnt; break;
+            case SYZGPU_UNION: k = 1; break;
+            default: k = rank < cnt; break;
+          }
+        } else {
+          k = (op == SYZGPU_UNION || op == SYZGPU_SYMMETRIC_DIFFERENCE) ? (rank >= cnt) : 0;
         }
-      } else {
-        k = (op == SYZGPU_UNION || op == SYZGPU_SYMMETRIC_DIFFERENCE) ? (rank >= cnt) : 0;
       }
+      keep[x] = k;
     }
-    keep[x] = k;
   }
 }
 
@@ -73,20 +85,24 @@ __global__ void k_setop_pairlen(const uint64_t* aoff, const uint64_t* boff, cons
 }
 
 // Scatter kept elements of one side. For side 0 (a): pos = KA(x) + KB(lb_b(v)); side 1 (b):
-// pos = KB(y) + KA(ub_a(w)) — equal values from a precede those from b (they are identical).
+// pos = KB(y) + KA(ub_a(w)) — equal values from a precede those from b (they are identical). One wave
+// per pair, as k_setop_classify.
 __global__ __launch_bounds__(256) void k_setop_scatter(int side, const uint32_t* a, const uint64_t* aoff,
                                                        const uint32_t* b, const uint64_t* boff, uint32_t npairs,
-                                                       uint64_t total, const uint8_t* keep, const uint64_t* ka,
+                                                       const uint64_t* segoff, const uint8_t* keep, const uint64_t* ka,
                                                        const uint64_t* kb, const uint64_t* outoff, uint32_t* out) {
-  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
-       x += (uint64_t)gridDim.x * blockDim.x) {
-    if (!keep[x]) continue;
-    const uint32_t p = pair_of(aoff, npairs, x);
-    const uint32_t v = a[x];
-    const uint64_t other = side == 0 ? lower_bound_dev<uint32_t>(b, boff[p], boff[p + 1], v)
-                                     : upper_bound_dev<uint32_t>(b, boff[p], boff[p + 1], v);
-    const uint64_t pos = outoff[p] + (ka[x] - ka[aoff[p]]) + (kb[other] - kb[boff[p]]);
-    out[pos] = v;
+  const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6, nseg = segoff[npairs];
+  for (uint64_t sid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; sid < nseg; sid += waves) {
+    uint64_t x0, x1;
+    const uint32_t p = seg_pair(segoff, npairs, sid, aoff, &x0, &x1);
+    const uint64_t beg = aoff[p], b0 = boff[p], b1 = boff[p + 1];
+    const uint64_t base = outoff[p] - ka[beg] - kb[b0];
+    for (uint64_t x = x0 + __lane_id(); x < x1; x += 64) {
+      if (!keep[x]) continue;
+      const uint32_t v = a[x];
+      const uint64_t other = side == 0 ? lower_bound_dev<uint32_t>(b, b0, b1, v) : upper_bound_dev<uint32_t>(b, b0, b1, v);
+      out[base + ka[x] + kb[other]] = v;
+    }
   }
 }
 
@@ -102,13 +118,24 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
   uint64_t* kb = c.scratch.get<uint64_t>("so_kb", nb + 1);
   uint64_t* plen = c.scratch.get<uint64_t>("so_plen", npairs + 1);
   int* err = c.scratch.get<int>("so_err", 1);
+  uint32_t* nsa = c.scratch.get<uint32_t>("so_nsa", npairs + 1);
+  uint32_t* nsb = c.scratch.get<uint32_t>("so_nsb", npairs + 1);
+  uint64_t* sga = c.scratch.get<uint64_t>("so_sga", npairs + 1);
+  uint64_t* sgb = c.scratch.get<uint64_t>("so_sgb", npairs + 1);
   SYZ_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  k_setop_nseg<<<grid_for(npairs, 256, 4096), 256, 0, s>>>(aoff, npairs, nsa);
+  SYZ_LAUNCHED();
+  k_setop_nseg<<<grid_for(npairs, 256, 4096), 256, 0, s>>>(boff, npairs, nsb);
+  SYZ_LAUNCHED();
+  exclusive_scan_u32(nsa, sga, npairs, s);
+  exclusive_scan_u32(nsb, sgb, npairs, s);
+  const uint64_t sega = npairs + na / SO_SEG + 1, segb = npairs + nb / SO_SEG + 1;  // segment bounds
   if (na) {
-    k_setop_classify<<<grid_for(na, 256, 65536), 256, 0, s>>>(op, 0, a, aoff, b, boff, npairs, na, keepa, err);
+    k_setop_classify<<<grid_for(sega * 64, 256, 65536), 256, 0, s>>>(op, 0, a, aoff, b, boff, npairs, sga, keepa, err);
     SYZ_LAUNCHED();
   }
   if (nb) {
-    k_setop_classify<<<grid_for(nb, 256, 65536), 256, 0, s>>>(op, 1, b, boff, a, aoff, npairs, nb, keepb, err);
+    k_setop_classify<<<grid_for(segb * 64, 256, 65536), 256, 0, s>>>(op, 1, b, boff, a, aoff, npairs, sgb, keepb, err);
     SYZ_LAUNCHED();
   }
   exclusive_scan_u8(keepa, ka, na, s);
@@ -125,13 +152,13 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
   const uint64_t total = *htot;
   if (total > out_cap) fail(SYZGPU_ECAPACITY, "set operation output capacity too small");
   if (na) {
-    k_setop_scatter<<<grid_for(na, 256, 65536), 256, 0, s>>>(0, a, aoff, b, boff, npairs, na, keepa, ka, kb,
-                                                             out_off_dev, out);
+    k_setop_scatter<<<grid_for(sega * 64, 256, 65536), 256, 0, s>>>(0, a, aoff, b, boff, npairs, sga, keepa, ka, kb,
+                                                                    out_off_dev, out);
     SYZ_LAUNCHED();
   }
   if (nb) {
-    k_setop_scatter<<<grid_for(nb, 256, 65536), 256, 0, s>>>(1, b, boff, a, aoff, npairs, nb, keepb, kb, ka,
-                                                             out_off_dev, out);
+    k_setop_scatter<<<grid_for(segb * 64, 256, 65536), 256, 0, s>>>(1, b, boff, a, aoff, npairs, sgb, keepb, kb, ka,
+                                                                    out_off_dev, out);
     SYZ_LAUNCHED();
   }
   return total;
@@ -351,6 +378,26 @@ int syzgpu_setop_batch(int op, const uint32_t* a, const uint64_t* a_off, const u
     if (tot) SYZ_HIP(hipMemcpyAsync(out, dout, tot * 4, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipMemcpyAsync(out_off, doo, (npairs + 1) * 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
+  })
+}
+
+int syzgpu_setop_batch_dev(int op, const uint32_t* a, const uint64_t* a_off, uint64_t na, const uint32_t* b,
+                           const uint64_t* b_off, uint64_t nb, size_t npairs, uint32_t* out, size_t out_cap,
+                           uint64_t* out_off, void* stream, uint64_t* total) {
+  SYZ_API_BODY({
+    if (op < 0 || op > 3) fail(SYZGPU_EINVAL, "bad set operation");
+    if (!a_off || !b_off || !out_off || (na && !a) || (nb && !b)) fail(SYZGPU_EINVAL, "null pointer");
+    if (npairs >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many pairs");
+    hipStream_t s = (hipStream_t)stream;
+    uint64_t tot = 0;
+    if (npairs == 0) {
+      SYZ_HIP(hipMemsetAsync(out_off, 0, 8, s));
+      SYZ_HIP(hipStreamSynchronize(s));
+    } else {
+      tot = setop_batch_dev(op, a, a_off, na, b, b_off, nb, (uint32_t)npairs, out, out_cap, out_off, s);
+      SYZ_HIP(hipStreamSynchronize(s));
+    }
+    if (total) *total = tot;
   })
 }
 

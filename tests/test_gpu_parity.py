@@ -96,6 +96,36 @@ def test_setops_large_lists():
             assert np.array_equal(g, oracle.setop(op, c, big)), op
 
 
+def test_setop_batch_device_entry_triage_shape():
+    # the device-pointer entry (bench leg setops_triage): pairs of two runs of one input's cover, the
+    # second with PCs dropped (the triage loop's Intersection, fuzzer.go:389-406), and Difference /
+    # Union / SymmetricDifference of the same pairs; plus empty pairs; bit-exact against the oracle
+    import torch
+    c = synth.corpus(0x5EED00C1, 3_000, 17, 60_000)
+    rnd = np.random.default_rng(4)
+    a_list = [c.cover(i) for i in range(c.n)]
+    b_list = [x[rnd.random(x.size) > 0.05] for x in a_list]
+    a_list[3] = np.zeros(0, np.uint32)
+    b_list[5] = np.zeros(0, np.uint32)
+    a, aoff = cover.to_csr(a_list)
+    b, boff = cover.to_csr(b_list)
+
+    def t(x):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+        return torch.from_numpy(np.ascontiguousarray(x).view(view.get(x.dtype, x.dtype))).to("cuda:0")
+    da, dao, db, dbo = t(a), t(aoff), t(b), t(boff)
+    for op in SETOPS:
+        cap = a.size + b.size + 1
+        out = torch.zeros(cap, dtype=torch.int32, device="cuda:0")
+        ooff = torch.zeros(c.n + 1, dtype=torch.int64, device="cuda:0")
+        tot = cover.SetOpBatchDev(op, da, dao, a.size, db, dbo, b.size, c.n, out, cap, ooff)
+        o = out.cpu().numpy().view(np.uint32)
+        oo = ooff.cpu().numpy().view(np.uint64)
+        assert tot == int(oo[-1])
+        for i in range(c.n):
+            assert np.array_equal(o[int(oo[i]):int(oo[i + 1])], oracle.setop(op, a_list[i], b_list[i])), (op, i)
+
+
 def test_setop_rejects_unsorted():
     with pytest.raises(_lib.SyzGpuError) as e:
         cover.Union([3, 1], [2])
