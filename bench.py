@@ -309,7 +309,10 @@ def main():
     # configs[2] on N GPUs: every rank takes its PC range of the batch (collectives inside)
     nov_sh = None
     if world > 1 and args.novelty and not args.emulate:
-        nov_sh = novelty_leg_sharded(args, dev, L, dist, rank, world)
+        try:  # a side leg: a failure that every rank sees is reported in the line, not fatal to it
+            nov_sh = novelty_leg_sharded(args, dev, L, dist, rank, world)
+        except Exception as e:  # noqa: BLE001
+            nov_sh = {"error": "%s: %s" % (type(e).__name__, e)}
 
     out = None
     if rank == 0:
