@@ -394,7 +394,7 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
         }
       }
       kp[q] = true;
-      if (!old) {
+      if (!old && !(dbg & 4)) {
         anynew = 1;
         const uint64_t lr = (uint64_t)v - gb;
         if (lr < span) {
@@ -406,6 +406,10 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
       }
     }
     __syncthreads();  // the table is read: its space takes the order
+    if (dbg & 8) {  // timing only: no order, no output
+      round++;
+      continue;
+    }
     // Order: 2048 buckets by the top address bits of the sub-range (counts, a scan, the keys listed
     // by bucket), then a key's place = its bucket's start + the keys of its bucket below it (buckets
     // hold a few keys: PCs are spread over the window's addresses)
@@ -530,7 +534,8 @@ static int nw_dbg() {
 }
 
 // timing experiments only (results are wrong when set): SYZGPU_NWH_DBG 1 = hashed windows walked
-// without table updates, 2 = tables built, nothing after
+// without table updates, 2 = tables built, nothing after, 4 = no new-cover marks, 8 = no ordered
+// output
 static int nwh_dbg() {
   static const int v = getenv("SYZGPU_NWH_DBG") ? atoi(getenv("SYZGPU_NWH_DBG")) : 0;
   return v;
