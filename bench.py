@@ -74,7 +74,9 @@ def parse():
 # kernel by total GPU time names the roofline kernel
 ROCPROF_STATS = os.path.join(ROOT, "profiles", "r03_kernel_stats.csv")
 # rocprofv3 kernel name -> the library's profiling scope around that kernel
-ROCPROF_SCOPE = [("k_region<512, 40, false, false>", "k_region"), ("k_region<512, 40, false, true>", "k_region_count"),
+ROCPROF_SCOPE = [("k_slab<", "k_slab"), ("k_smin_direct", "k_pmin_direct"), ("k_smin_hash<false>", "k_pmin_hash"),
+                 ("k_smin_hash<true>", "k_pmin_packed"),
+                 ("k_region<512, 40, false, false>", "k_region"), ("k_region<512, 40, false, true>", "k_region_count"),
                  ("k_pmin_direct", "k_pmin_direct"), ("k_pmin_hash<false>", "k_pmin_hash"),
                  ("k_pmin_hash<true>", "k_pmin_packed"), ("k_colscan", "k_colscan")]
 
@@ -99,9 +101,10 @@ def rocprof_top(path=ROCPROF_STATS):
 def dominant_kernel(kern):
     """The step's dominant kernel: the top kernel of the committed rocprofv3 summary of this command
     (ROCPROF_STATS) when it maps to a byte-modelled scope; else the kernel scope with the most time in
-    the untimed per-kernel pass among those carrying an algorithmic byte model:
-    k_region (the scatter) 8 B per PC + 24 B per entry, k_region_count 4 B per PC + 24 B per entry,
-    k_pmin_direct / k_pmin_hash / k_pmin_packed 4 B per PC of the groups they walk. That pass runs the
+    the untimed per-kernel pass among those carrying an algorithmic byte model (SURVEY.md
+    §8d: a kernel's share of the algorithm's input, never the intermediate buffers it writes): k_slab
+    (the transpose) 4 B per PC + 10 B per entry, k_pmin_direct / k_pmin_hash / k_pmin_packed 4 B per PC
+    of the groups they walk. That pass runs the
     raw pipeline's passes one after another (syzgpu_profile_enable(2)), so each scope times its kernels
     alone. Phase scopes (gosort_*, m_big, group_partition) span several kernels and are not candidates."""
     top = rocprof_top()

@@ -34,6 +34,7 @@
 
 #include "panels_dev.hpp"
 #include "pipeline.hpp"
+#include "slab_dev.hpp"
 
 namespace syz {
 
@@ -128,17 +129,16 @@ __device__ __forceinline__ uint32_t nw_index(uint32_t o) {
   return ((o >> 2) | (o << (SB - 2))) & ((1u << SB) - 1);
 }
 
-#ifndef SYZ_RG_NU
-#define SYZ_RG_NU 2
+#ifndef SYZ_NW_U
+#define SYZ_NW_U 2
 #endif
 
 // M: one (call, window). tab = min member position per window offset; the table's position cstart[g]
 // is OLD.
 template <uint32_t SB>
 __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
-    const uint32_t* order, uint32_t W, const PGroup* pg, const uint64_t* rstart, const uint32_t* rtot,
-    const uint32_t* elems,
-    const uint64_t* cstart, uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart,
+    const uint32_t* order, uint32_t W, const SGroup* sg, const uint32_t* gslab, const uint64_t* gebase,
+    const uint32_t* D, const PSlab* slabs, const uint32_t* elems, const uint64_t* cstart, uint32_t lo, const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fstart,
     const NwGroup* ng_, uint32_t* kbits, uint32_t* wcount, uint8_t* sel8, uint8_t* upd, int dbg) {
   using K = NwCfg<SB>;
   constexpr int BLOCK = K::BLOCK;
@@ -147,6 +147,8 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
   __shared__ uint32_t flk[K::FLK];
   __shared__ uint32_t pres[K::FLK];  // offsets some member holds (set by the element that lowers NONE)
   __shared__ uint32_t red[BLOCK / 64 + 1];
+  __shared__ uint64_t red64[BLOCK / 64 + 1];
+  static_assert(K::BMW >= 2 * BLOCK + 3 * PK_NBLK, "the walk's scratch in the rank bitmap");
   const PItem it{order[blockIdx.x / W], blockIdx.x % W};
   const uint32_t g = it.g, w = it.w;
   {
@@ -165,11 +167,14 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
     const uint32_t o = fl[i] - wlo;  // flakes not increasing (rejected after the batch) land anywhere
     if (o < K::BITS) atomicOr(&flk[o >> 5], 1u << (o & 31));
   }
-  // the window's regions; a member's rank is its position (the table first, then batch order)
+  // the window's slab runs; a member's rank is its position (the table first, then batch order); the
+  // rank bitmap is the walk's scratch until the walk is done
   if (!(dbg & 1))
-    for_region<SYZ_RG_NU, true>(it, pg, cstart, rstart, rtot, elems, nullptr, [&](uint32_t o, uint32_t R) {
-      if (R != RANK_NONE && atomicMin(&tab[nw_index<SB>(o)], R) == RANK_NONE) atomicOr(&pres[o >> 5], 1u << (o & 31));
-    });
+    for_slab_window<SYZ_NW_U, true>(it, sg, gslab, gebase, D, slabs, elems, nullptr, bm, red64,
+                                    [&](uint32_t o, uint32_t R) {
+                                      if (R != RANK_NONE && atomicMin(&tab[nw_index<SB>(o)], R) == RANK_NONE)
+                                        atomicOr(&pres[o >> 5], 1u << (o & 31));
+                                    });
   __syncthreads();
   if (dbg & 2) return;
   const uint64_t gb = cstart[g], ng = cstart[g + 1] - gb;
@@ -266,31 +271,20 @@ __device__ __forceinline__ uint32_t nw_slot_group(const NwGroup* ng_, uint32_t G
   return g0;
 }
 
-// PCs of (call g, window w): its regions' lengths over the member segments
-__device__ __forceinline__ uint32_t nw_window_pcs(uint32_t g, uint32_t w, const PGroup* pg, const uint64_t* cstart,
-                                                  const uint32_t* rtot) {
-  const PGroup p = pg[g];
-  const uint32_t sb = 32 - p.S;
-  const uint64_t ng = cstart[g + 1] - cstart[g];
-  const uint32_t nseg = (uint32_t)((ng + (1ull << sb) - 1) >> sb);
-  uint32_t e = 0;
-  for (uint32_t s = 0; s < nseg; s++) e += rtot[p.rb + s * p.W + w];
-  return e;
-}
-
 // capacity of every count slot's kept list (its window's PCs; 0 for the table-sentinel slot)
-__global__ void k_nw_hcap(const NwGroup* ng_, const PGroup* pg, const uint64_t* cstart, const uint32_t* rtot,
-                          uint32_t G, uint64_t slots, uint32_t* hcap) {
+__global__ void k_nw_hcap(const NwGroup* ng_, const SGroup* sg, const uint32_t* wtot, uint32_t G, uint64_t slots,
+                          uint32_t* hcap) {
   for (uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; sl < slots; sl += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t g = nw_slot_group(ng_, G, sl);
     const uint32_t w = (uint32_t)(sl - ng_[g].sbase);
-    hcap[sl] = w < pg[g].W ? nw_window_pcs(g, w, pg, cstart, rtot) : 0u;
+    hcap[sl] = w < sg[g].W ? wtot[sg[g].wbase + w] : 0u;
   }
 }
 
 // M (hashed): item i is window i - iofs[j] of call order[j] (larger calls first)
 __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, const uint32_t* iofs, uint32_t G,
-                                                  const PGroup* pg, const uint64_t* rstart, const uint32_t* rtot,
+                                                  const SGroup* sg, const uint32_t* gslab, const uint64_t* gebase,
+                                                  const uint32_t* D, const PSlab* slabs, const uint32_t* wtot,
                                                   const uint32_t* elems, const uint64_t* cstart, uint32_t lo,
                                                   const uint32_t* __restrict__ fl, uint64_t nfl, const NwGroup* ng_,
                                                   const uint64_t* hbase, uint32_t* hkeys, uint32_t* wcount,
@@ -300,15 +294,18 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
   __shared__ uint32_t red[NH_BLOCK / 64 + 1];
   __shared__ uint32_t flk[NH_FLK];  // the window's flakes (when they fit)
   __shared__ int full;
+  constexpr uint32_t NH_WBLK = 128;  // the walk's element windows: 8K elements (its scratch fits beside)
+  __shared__ uint32_t wsc[2 * NH_BLOCK + 3 * NH_WBLK];
+  __shared__ uint64_t red64[NH_BLOCK / 64 + 1];
   uint32_t* keys = tabs;
   uint32_t* vals = tabs + HS;
   const uint32_t j = (uint32_t)upper_bound_dev<uint32_t>(iofs, 0, G + 1, blockIdx.x) - 1;
   const uint32_t g = order[j], w = blockIdx.x - iofs[j];
   const PItem it{g, w};
-  const uint32_t S = pg[g].S;
+  const uint32_t S = sg[g].S;
   const uint64_t gb = cstart[g], ng = cstart[g + 1] - gb;
   const uint64_t slot = ng_[g].sbase + w;
-  const uint32_t E = nw_window_pcs(g, w, pg, cstart, rtot);
+  const uint32_t E = wtot[sg[g].wbase + w];
   if (E == 0) {
     if (threadIdx.x == 0) wcount[slot] = 0;
     return;
@@ -338,7 +335,8 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
     const uint32_t sh = S - lr2, rr = round;
     const bool split = lr2 > 0;
     uint32_t acc = 0;
-    for_region<SYZ_RG_NU, true>(it, pg, cstart, rstart, rtot, elems, nullptr, [&](uint32_t o, uint32_t R) {
+    for_slab_window<SYZ_NW_U, true, NH_WBLK>(it, sg, gslab, gebase, D, slabs, elems, nullptr, wsc, red64,
+                                             [&](uint32_t o, uint32_t R) {
       if (R == RANK_NONE || (split && (o >> sh) != rr)) return;
       if (dbg & 1) {
         acc += o ^ R;
@@ -547,12 +545,6 @@ static uint32_t nw_bits_forced() {
   return v == 14 || v == 15 ? v : 0u;
 }
 
-// block b -> its call: the last g with gblock[g] <= b
-__global__ void k_nw_bgroup(const uint32_t* gblock, uint32_t G, uint32_t B, uint32_t* bgroup) {
-  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
-    bgroup[b] = (uint32_t)upper_bound_dev<uint32_t>(gblock, 0, G + 1, b) - 1;
-}
-
 __global__ void k_nw_gpcs(const uint64_t* mpos, const uint64_t* cstart, uint32_t G, uint64_t* gpcs) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x)
     gpcs[g] = mpos[cstart[g + 1]] - mpos[cstart[g]];
@@ -621,8 +613,6 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   std::vector<PGroup> hpg(G);
   std::vector<NwGroup> hng(G + 1);
   uint64_t kw = 0, slots = 0;
-  uint64_t nreg = 0;
-  std::vector<ColItem> hcol;
   for (uint32_t g = 0; g < G; g++) {
     uint32_t S = DB, W = WD;
     if (hashed) {
@@ -631,28 +621,16 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
       while (S < SMAX && nwin(S + 1) >= want) S++;
       W = (uint32_t)nwin(S);
     }
-    // regions: one per (member segment of 2^(32 - S) members, window)
-    const uint64_t ngm = hstart[g + 1] - hstart[g];
-    const uint32_t nseg = (uint32_t)((ngm + (1ull << (32 - S)) - 1) >> (32 - S));
-    hpg[g] = PGroup{S, W, (uint32_t)(hashed ? PMODE_HASH : PMODE_DIRECT), (uint32_t)nreg};
-    nreg += (uint64_t)nseg * W;
-    for (uint32_t sg = 0; sg < nseg; sg++)
-      for (uint32_t w0 = 0; w0 < W; w0 += 64) hcol.push_back(ColItem{g, sg, w0, 0});
+    hpg[g] = PGroup{S, W, (uint32_t)(hashed ? PMODE_HASH : PMODE_DIRECT), 0};
     hng[g] = NwGroup{kw, slots};
     if (!hashed) kw += (uint64_t)W << (S - 5);
     slots += W + 1;
   }
-  if (nreg >= (1ull << 31)) return false;
   hng[G] = NwGroup{kw, slots};
-  std::vector<uint32_t> hgblock(G + 1, 0);
-  uint64_t desc_bound = 0;
-  for (uint32_t g = 0; g < G; g++) {
-    const uint32_t nb = (uint32_t)((hstart[g + 1] - hstart[g] + MEMB - 1) / MEMB);
-    hgblock[g + 1] = hgblock[g] + nb;
-    desc_bound += (nb + hpcs[g] / PCAP + 1) * (uint64_t)(hpg[g].W + 1);  // chunks of g <= nb + PCs / PCAP + 1
-  }
-  const uint32_t B = hgblock[G];
-  const uint64_t chunk_bound = B + total / PCAP + G + 1;
+  // slabs of the combined members (slab_dev.hpp); hashed windows need their per-window totals
+  SlabJob SJ;
+  slab_plan(SJ, hstart, hpcs.data(), hpg, G, hashed);
+  const uint32_t B = SJ.B;
   // items (call, window), larger calls first (their windows are the long ones) so the grid's tail is
   // short: item i is window i % WD of call order[i / WD], generated on the device
   std::vector<uint32_t> order(G);
@@ -661,74 +639,53 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   std::vector<uint32_t> iofs(G + 1, 0);  // hashed: the items of order[j] are [iofs[j], iofs[j + 1])
   for (uint32_t j = 0; j < G; j++) iofs[j + 1] = iofs[j] + hpg[order[j]].W;
   const size_t nitems = hashed ? (size_t)iofs[G] : (size_t)G * WD;
-  // one staging copy: PGroup[G+1], NwGroup[G+1], gblock[G+1], order[G+1], iofs[G+1], ColItem[]
-  const size_t o_ng = (G + 1) * sizeof(PGroup), o_gb = o_ng + (G + 1) * sizeof(NwGroup), o_or = o_gb + (G + 1) * 4;
-  const size_t o_io = o_or + (G + 1) * 4, o_ci = o_io + (G + 1) * 4;
-  const size_t stage_bytes = o_ci + (hcol.size() + 1) * sizeof(ColItem);
+  // one staging copy: PGroup[G+1], NwGroup[G+1], SGroup[G+1], gblock[G+1], bgroup[B+1], order[G+1], iofs[G+1]
+  auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
+  const size_t o_ng = al16((G + 1) * sizeof(PGroup)), o_sg = o_ng + al16((G + 1) * sizeof(NwGroup));
+  const size_t o_gb = o_sg + al16((G + 1) * sizeof(SGroup)), o_bg = o_gb + al16((G + 1) * 4);
+  const size_t o_or = o_bg + al16(((size_t)B + 1) * 4), o_io = o_or + al16((G + 1) * 4);
+  const size_t stage_bytes = o_io + al16((G + 1) * 4);
   uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
   uint8_t* dstage = sc.get<uint8_t>("nw_stage", stage_bytes + 64);
   std::memcpy(stage, hpg.data(), G * sizeof(PGroup));
   std::memcpy(stage + o_ng, hng.data(), (G + 1) * sizeof(NwGroup));
-  std::memcpy(stage + o_gb, hgblock.data(), (G + 1) * 4);
+  std::memcpy(stage + o_sg, SJ.hsg.data(), G * sizeof(SGroup));
+  std::memcpy(stage + o_gb, SJ.hgblock.data(), (G + 1) * 4);
+  if (B) std::memcpy(stage + o_bg, SJ.hbgroup.data(), (size_t)B * 4);
   std::memcpy(stage + o_or, order.data(), G * 4);
   std::memcpy(stage + o_io, iofs.data(), (G + 1) * 4);
-  if (!hcol.empty()) std::memcpy(stage + o_ci, hcol.data(), hcol.size() * sizeof(ColItem));
   SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
   const PGroup* dpg = reinterpret_cast<const PGroup*>(dstage);
   const NwGroup* dng = reinterpret_cast<const NwGroup*>(dstage + o_ng);
-  const uint32_t* dgblock = reinterpret_cast<const uint32_t*>(dstage + o_gb);
+  const SGroup* dsg = reinterpret_cast<const SGroup*>(dstage + o_sg);
+  SJ.dsg = dsg;
+  SJ.dgblock = reinterpret_cast<const uint32_t*>(dstage + o_gb);
+  SJ.dbgroup = reinterpret_cast<const uint32_t*>(dstage + o_bg);
   const uint32_t* dorder = reinterpret_cast<const uint32_t*>(dstage + o_or);
   const uint32_t* diofs = reinterpret_cast<const uint32_t*>(dstage + o_io);
-  const ColItem* dcol = reinterpret_cast<const ColItem*>(dstage + o_ci);
-  uint32_t* dbgroup = sc.get<uint32_t>("nw_bgroup", (size_t)B + 1);
-  if (B) {
-    k_nw_bgroup<<<grid_for(B, 256, 4096), 256, 0, s>>>(dgblock, G, B, dbgroup);
-    SYZ_LAUNCHED();
-  }
-  uint32_t* nsub = sc.get<uint32_t>("nw_nsub", (size_t)B + 1);
-  uint64_t* cstartb = sc.get<uint64_t>("nw_cstartb", (size_t)B + 1);
-  PChunk* chunks = sc.get<PChunk>("nw_chunks", chunk_bound + 1);
-  uint64_t* gchunk = sc.get<uint64_t>("nw_gchunk", G + 1);
-  uint64_t* gdesc = sc.get<uint64_t>("nw_gdesc", G + 1);
-  uint16_t* cnt = sc.get<uint16_t>("nw_cnt", desc_bound + 1);
-  uint32_t* colpre = sc.get<uint32_t>("nw_colpre", desc_bound + 1);
-  uint32_t* elems = sc.get<uint32_t>("pm_elems", total + 8);
-  uint32_t* rtot = sc.get<uint32_t>("nw_rtot", nreg + 1);
-  uint64_t* rstart = sc.get<uint64_t>("nw_rstart", nreg + 2);
   uint32_t* kbits = sc.get<uint32_t>("nw_kbits", kw + 1);
   uint32_t* wcount = sc.get<uint32_t>("nw_wcount", slots + 1);
   uint64_t* wpos = sc.get<uint64_t>("nw_wpos", slots + 1);
-
   {
-    ProfScope ps("novelty_part", s, total * 12 + (uint64_t)nm * 48);
-    if (B) {
-      k_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, cstart, mpos, nsub);
-      SYZ_LAUNCHED();
-    }
-    exclusive_scan_u32(nsub, cstartb, B, s);
-    if (B) {
-      k_chunks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, cstart, mpos, cstartb, chunks);
-      SYZ_LAUNCHED();
-    }
-    k_gchunk<<<1, 1024, 0, s>>>(dgblock, G, cstartb, dpg, gchunk, gdesc);
-    SYZ_LAUNCHED();
+    // byte model: every PC read once and written once as an element, 48 B of member metadata
+    ProfScope ps("novelty_part", s, total * 8 + (uint64_t)nm * 48);
+    slab_build(SJ, "nw", mlen, mpos, nm, cstart, s);
     NovSrc ns;
     ns.mc = d_mc;
     ns.mc_off = d_mco;
     ns.n1 = (uint32_t)n;
-    k_region<P3_BLOCK, P3_TPW, true, true><<<(unsigned)chunk_bound, P3_BLOCK, 0, s>>>(
-        d_pcs, d_off, cmem, mpos, nullptr, chunks, 0u, G, dpg, cstart, gchunk, gdesc, lo, cnt, nullptr,
-        nullptr, nullptr, err, ns);
-    SYZ_LAUNCHED();
-    k_colscan<<<(unsigned)hcol.size(), CS_BLOCK, 0, s>>>(dcol, dpg, cstart, dgblock, cstartb, gchunk, gdesc, cnt,
-                                                        colpre, rtot);
-    SYZ_LAUNCHED();
-    exclusive_scan_u32(rtot, rstart, nreg, s);
-    k_region<P3_BLOCK, P3_TPW, true, false><<<(unsigned)chunk_bound, P3_BLOCK, 0, s>>>(
-        d_pcs, d_off, cmem, mpos, nullptr, chunks, 0u, G, dpg, cstart, gchunk, gdesc, lo, cnt, colpre,
-        rstart, elems, err, ns);
-    SYZ_LAUNCHED();
+    if (SJ.slab_bound) {
+      k_slab<SL_BLOCK, SL_TPW, true><<<(unsigned)SJ.slab_bound, SL_BLOCK, 0, s>>>(
+          d_pcs, d_off, cmem, mlen, SJ.tpos, nullptr, SJ.slabs, SJ.cstart + B, dsg, SJ.gebase, lo, SJ.elems, SJ.D, err,
+          SJ.wtot, ns);
+      SYZ_LAUNCHED();
+    }
   }
+  const uint32_t* gslab = SJ.gslab;
+  const uint64_t* gebase = SJ.gebase;
+  const uint32_t* D = SJ.D;
+  const PSlab* slabs = SJ.slabs;
+  const uint32_t* elems = SJ.elems;
   uint64_t* hbase = nullptr;
   uint32_t* hkeys = nullptr;
   if (hashed) {
@@ -736,12 +693,13 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     uint32_t* hcap = sc.get<uint32_t>("nw_hcap", slots + 1);
     hbase = sc.get<uint64_t>("nw_hbase", slots + 1);
     hkeys = sc.get<uint32_t>("nw_hkeys", total + 8);
-    k_nw_hcap<<<grid_for(slots, 256, 4096), 256, 0, s>>>(dng, dpg, cstart, rtot, G, slots, hcap);
+    k_nw_hcap<<<grid_for(slots, 256, 4096), 256, 0, s>>>(dng, dsg, SJ.wtot, G, slots, hcap);
     SYZ_LAUNCHED();
     exclusive_scan_u32(hcap, hbase, slots, s);
     if (nitems) {
-      k_nw_hash<<<(unsigned)nitems, NH_BLOCK, 0, s>>>(dorder, diofs, G, dpg, rstart, rtot, elems, cstart, lo, d_fl, nfl,
-                                                  dng, hbase, hkeys, wcount, sel8, upd, err, nwh_dbg());
+      k_nw_hash<<<(unsigned)nitems, NH_BLOCK, 0, s>>>(dorder, diofs, G, dsg, gslab, gebase, D, slabs, SJ.wtot, elems,
+                                                      cstart, lo, d_fl, nfl, dng, hbase, hkeys, wcount, sel8, upd, err,
+                                                      nwh_dbg());
       SYZ_LAUNCHED();
     }
   }
@@ -752,11 +710,13 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     SYZ_LAUNCHED();
     if (nitems) {
       if (DB == 14)
-        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, dpg, rstart, rtot, elems, cstart, lo, d_fl,
-                                                                   fstart, dng, kbits, wcount, sel8, upd, nw_dbg());
+        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, dsg, gslab, gebase, D, slabs, elems,
+                                                                   cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
+                                                                   upd, nw_dbg());
       else
-        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, dpg, rstart, rtot, elems, cstart, lo, d_fl,
-                                                                   fstart, dng, kbits, wcount, sel8, upd, nw_dbg());
+        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, dsg, gslab, gebase, D, slabs, elems,
+                                                                   cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
+                                                                   upd, nw_dbg());
       SYZ_LAUNCHED();
     }
   }

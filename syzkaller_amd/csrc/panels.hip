@@ -27,6 +27,7 @@
 
 #include "panels_dev.hpp"
 #include "pipeline.hpp"
+#include "slab_dev.hpp"
 
 namespace syz {
 
@@ -306,6 +307,115 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
   }
 }
 
+// ---- M over slab runs (slab_dev.hpp): the same tables, the window's runs from every slab --------------
+#ifndef SYZ_SL_MU
+#define SYZ_SL_MU 4
+#endif
+__global__ __launch_bounds__(1024) void k_smin_direct(const PItem* items, const SGroup* sg, const uint32_t* gslab,
+                                                      const uint64_t* gebase, const uint32_t* D,
+                                                      const PSlab* slabs, const uint32_t* __restrict__ elems,
+                                                      const uint32_t* __restrict__ rank_of_member,
+                                                      const uint64_t* gstart, uint8_t* sel8) {
+  __shared__ __align__(16) uint32_t tab[1u << DS];
+  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];
+  __shared__ uint64_t red64[1024 / 64 + 1];
+  const PItem it = items[blockIdx.x];
+  {
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+    const uint4 none4 = make_uint4(RANK_NONE, RANK_NONE, RANK_NONE, RANK_NONE);
+    for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
+  }
+  __syncthreads();
+  for_slab_window<SYZ_SL_MU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, wsc, red64,
+                                    [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
+  __syncthreads();
+  const uint64_t gb = gstart[it.g];
+  emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, wsc, sel8);
+}
+
+#ifndef SYZ_SL_HU
+#define SYZ_SL_HU 1
+#endif
+template <bool PACKED>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_smin_hash(const PItem* items, const SGroup* sg, const uint32_t* gslab,
+                                                    const uint64_t* gebase, const uint32_t* D, const PSlab* slabs,
+                                                    const uint32_t* __restrict__ elems,
+                                                    const uint32_t* __restrict__ rank_of_member,
+                                                    const uint64_t* gstart, uint8_t* sel8) {
+  constexpr uint32_t NS = PACKED ? PHS : HS;  // slots
+  constexpr uint32_t CAP = PACKED ? PHCAP : HCAP;
+  __shared__ uint32_t tabs[2 * HS];
+  static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
+  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];  // the walk's scratch, then the emit bitmap
+  __shared__ uint64_t red64[1024 / 64 + 1];
+  __shared__ int full;
+  uint32_t* keys = tabs;  // PACKED: the slots
+  uint32_t* vals = tabs + HS;
+  const PItem it = items[blockIdx.x];
+  const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
+  const uint32_t E = slab_window_count<1024>(it, sg, gslab, D, reinterpret_cast<uint32_t*>(red64));
+  if (E == 0) return;
+  uint32_t R = (E + CAP - 1) / CAP;
+  for (uint32_t round = 0; round < R;) {
+    for (uint32_t i = threadIdx.x; i < 2 * HS; i += 1024) tabs[i] = (PACKED || i < HS) ? 0xFFFFFFFFu : RANK_NONE;
+    if (threadIdx.x == 0) full = 0;
+    __syncthreads();
+    const uint32_t RR = R, rr = round;
+    for_slab_window<SYZ_SL_HU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, wsc, red64,
+                                      [&](uint32_t o, uint32_t Rk) {
+                                        if (Rk == RANK_NONE) return;  // a lane past the window
+                                        if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
+                                        if constexpr (PACKED) {
+                                          const uint32_t pk = (o << PK_RBITS) | (uint32_t)(Rk - gb);
+                                          uint32_t h = (o * 0x9E3779B1u) >> (32 - PHS_BITS);
+                                          for (uint32_t probes = 0; probes < HPROBE; probes++) {
+                                            uint32_t k = keys[h];
+                                            if (k == 0xFFFFFFFFu) {
+                                              k = atomicCAS(&keys[h], 0xFFFFFFFFu, pk);
+                                              if (k == 0xFFFFFFFFu) return;
+                                            }
+                                            if ((k >> PK_RBITS) == o) {
+                                              if (k > pk) atomicMin(&keys[h], pk);
+                                              return;
+                                            }
+                                            h = (h + 1) & (PHS - 1);
+                                          }
+                                        } else {
+                                          uint32_t h = hslot(o);
+                                          for (uint32_t probes = 0; probes < HPROBE; probes++) {
+                                            uint32_t k = keys[h];
+                                            if (k == 0xFFFFFFFFu) {
+                                              k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
+                                              if (k == 0xFFFFFFFFu) k = o;
+                                            }
+                                            if (k == o) {
+                                              atomicMin(&vals[h], Rk);
+                                              return;
+                                            }
+                                            h = (h + 1) & (HS - 1);
+                                          }
+                                        }
+                                        full = 1;
+                                      });
+    __syncthreads();
+    if (full) {
+      R *= 2;
+      round = 0;
+      __syncthreads();
+      continue;
+    }
+    if constexpr (PACKED) {
+      const uint32_t g32 = (uint32_t)gb;
+      emit_winner_bytes<PK_SCRATCH_WORDS>(keys, NS, gb, ng, wsc, sel8, [g32](uint32_t v) {
+        return v == 0xFFFFFFFFu ? RANK_NONE : g32 + (v & ((1u << PK_RBITS) - 1));
+      });
+    } else {
+      emit_winner_bytes<PK_SCRATCH_WORDS>(vals, HS, gb, ng, wsc, sel8);
+    }
+    round++;
+  }
+}
+
 // ---- outputs: the group-major kept list in selection order ----------------------------------------
 // kept inputs per 32 ranks (bytes are 0/1)
 __global__ void k_sel_wpop(const uint8_t* sel8, size_t nw, uint32_t* cnt) {
@@ -433,6 +543,255 @@ static int pm_dbg() {
   return v;
 }
 
+void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* hpcs, const std::vector<PGroup>& hpg,
+               uint32_t G, bool want_wtot) {
+  J.G = G;
+  J.hsg.assign(G, SGroup{});
+  J.hgblock.assign(G + 1, 0);
+  J.hbgroup.clear();
+  J.slab_bound = J.dtotal = J.wtotal = J.total_pcs = J.xtotal = 0;
+  for (uint32_t g = 0; g < G; g++) {
+    const uint64_t ng = hstart[g + 1] - hstart[g];
+    const uint32_t S = hpg[g].S, W = hpg[g].W;
+    // a member's tag fits 32 - S bits, and the all-ones tag is never a member's (SL_NONE: padding)
+    const uint32_t memb = S <= 23 ? SL_MEMB : (1u << (32 - S)) - 1;
+    const uint64_t nb = (ng + memb - 1) / memb;
+    J.hgblock[g + 1] = J.hgblock[g] + (uint32_t)nb;
+    J.hbgroup.insert(J.hbgroup.end(), nb, g);
+    // slabs of a block: ceil(tiles / SL_TILES); tiles <= PCs / 64 + members
+    const uint64_t stride = (hpcs[g] / 64 + ng) / SL_TILES + nb + 1;
+    // a group's element offsets (D) are 32-bit
+    if (hpcs[g] + stride * slab_pad(W) + 8 >= (1ull << 32)) fail(SYZGPU_EINVAL, "a call group with 2^32 or more PCs");
+    J.hsg[g] = SGroup{J.dtotal, S, W, (uint32_t)stride, memb, (uint32_t)J.wtotal, 0, J.xtotal};
+    J.xtotal += stride * slab_pad(W);
+    J.dtotal += (uint64_t)(W + 1) * stride;
+    if (want_wtot) J.wtotal += W;
+    J.slab_bound += stride;
+    J.total_pcs += hpcs[g];
+  }
+  if (J.wtotal >= (1ull << 32) || J.slab_bound >= (1ull << 31)) fail(SYZGPU_EINVAL, "too many slabs");
+  J.B = J.hgblock[G];
+}
+
+void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint64_t* mpos, size_t nmem,
+                const uint64_t* gstart, hipStream_t s) {
+  Scratch& sc = ctx().scratch;
+  auto nm = [&](const char* x) { return std::string(prefix) + x; };
+  const uint32_t B = J.B, G = J.G;
+  uint32_t* mtile = sc.get<uint32_t>(nm("_sl_mtile").c_str(), nmem + 1);
+  uint32_t* nsub = sc.get<uint32_t>(nm("_sl_nsub").c_str(), (size_t)B + 1);
+  J.tpos = sc.get<uint64_t>(nm("_sl_tpos").c_str(), nmem + 2);
+  J.cstart = sc.get<uint64_t>(nm("_sl_cstart").c_str(), (size_t)B + 2);
+  J.slabs = sc.get<PSlab>(nm("_sl_slabs").c_str(), J.slab_bound + 1);
+  J.gslab = sc.get<uint32_t>(nm("_sl_gslab").c_str(), G + 1);
+  J.gebase = sc.get<uint64_t>(nm("_sl_gebase").c_str(), G + 1);
+  J.D = sc.get<uint32_t>(nm("_sl_D").c_str(), J.dtotal + 1);
+  J.elems = sc.get<uint32_t>("pm_elems", J.total_pcs + J.xtotal + 16);
+  J.wtot = nullptr;
+  ProfScope ps("slab_plan", s, 0);
+  if (J.wtotal) {
+    J.wtot = sc.get<uint32_t>(nm("_sl_wtot").c_str(), J.wtotal + 1);
+    SYZ_HIP(hipMemsetAsync(J.wtot, 0, J.wtotal * 4, s));
+  }
+  if (nmem) {
+    k_sl_tiles<<<grid_for(nmem, 256, 4096), 256, 0, s>>>(mlen, nmem, mtile);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(mtile, J.tpos, nmem, s);
+  if (B) {
+    k_sl_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(J.dbgroup, B, J.dgblock, gstart, J.dsg, J.tpos, nsub);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(nsub, J.cstart, B, s);
+  if (J.slab_bound) {
+    k_sl_slabs<<<grid_for(J.slab_bound, 256, 8192), 256, 0, s>>>(J.dbgroup, B, J.dgblock, gstart, J.dsg, J.tpos, mpos,
+                                                                  J.cstart, J.slab_bound, J.slabs);
+    SYZ_LAUNCHED();
+  }
+  k_sl_groups<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(J.dgblock, G, J.cstart, J.slabs, J.gslab, J.gebase);
+  SYZ_LAUNCHED();
+}
+
+// SYZGPU_PM_REGION=1 (A/B): round 3's region form (count pass, column scan, scatter) instead of slabs
+static bool pm_region() {
+  static const bool v = getenv("SYZGPU_PM_REGION") && atoi(getenv("SYZGPU_PM_REGION")) != 0;
+  return v;
+}
+
+// The slab form (slab_dev.hpp): one read of the covers. Inputs from begin_once's common part: the
+// group partition (members, el, mlen, mpos), the per-group PC counts and read slices, the windows.
+static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_t>& hstart,
+                       const std::vector<uint64_t>& hpcs, const uint64_t* hsl, const std::vector<PGroup>& hpg,
+                       uint32_t lo, uint32_t hi, const uint32_t* exact_span, const uint32_t* members, uint64_t* el,
+                       const uint32_t* mlen, const uint64_t* mpos, const uint32_t* sbeg, int* err) {
+  Context& c = ctx();
+  Scratch& sc = c.scratch;
+  const size_t n = a.n;
+  const uint32_t G = a.G;
+  hipStream_t s = a.s;
+  uint64_t* gstart = J.gstart.p;
+  uint32_t* rank_of_member = J.rank_of_member.p;
+  uint32_t* ent_of_rank = J.ent_of_rank.p;
+  uint8_t* sel8 = J.sel8.p;
+  SlabJob SJ;
+  slab_plan(SJ, hstart, hsl, hpg, G, false);
+  const uint64_t slab_bound = SJ.slab_bound, total_pcs = SJ.total_pcs;
+  const uint32_t B = SJ.B;
+  // work items: (call, window), class (big groups: sorted by the global rounds) and mode, largest
+  // expected window first; a key part only its windows
+  const auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
+  std::vector<uint32_t> order(G);
+  std::iota(order.begin(), order.end(), 0u);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t x, uint32_t y) { return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W; });
+  std::array<std::array<std::vector<PItem>, 3>, 2> items;  // [big][mode]
+  uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  for (uint32_t g : order) {
+    if (!hpcs[g]) continue;
+    uint32_t w0 = 0, w1 = hpg[g].W;
+    if (a.key_lo) {
+      const uint32_t klo = std::max(a.key_lo[g], lo), khi = std::min(a.key_hi[g], hi);
+      if (klo > khi) continue;
+      w0 = (klo - lo) >> hpg[g].S;
+      w1 = std::min<uint32_t>(hpg[g].W, ((khi - lo) >> hpg[g].S) + 1);
+    }
+    auto& v = items[is_big(g) ? 1 : 0][hpg[g].mode];
+    for (uint32_t w = w0; w < w1; w++) v.push_back(PItem{g, w});
+    item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
+  }
+  size_t nitems = 0;
+  for (auto& r : items)
+    for (auto& v : r) nitems += v.size();
+  // the plan goes over in one copy: SGroup[G], gblock[G + 1], bgroup[B + 1], items[nitems + 1]
+  auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
+  const size_t o_gb = al16((G + 1) * sizeof(SGroup)), o_bg = o_gb + al16((G + 1) * 4),
+               o_it = o_bg + al16(((size_t)B + 1) * 4), stage_bytes = o_it + al16((nitems + 1) * sizeof(PItem));
+  uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
+  uint8_t* dstage = sc.get<uint8_t>("pm_stage", stage_bytes + 64);
+  SGroup* dsg = reinterpret_cast<SGroup*>(dstage);
+  uint32_t* dgblock = reinterpret_cast<uint32_t*>(dstage + o_gb);
+  uint32_t* dbgroup = reinterpret_cast<uint32_t*>(dstage + o_bg);
+  PItem* ditems = reinterpret_cast<PItem*>(dstage + o_it);
+  std::array<std::array<size_t, 3>, 2> ifirst{};
+  {
+    std::memcpy(stage, SJ.hsg.data(), G * sizeof(SGroup));
+    std::memcpy(stage + o_gb, SJ.hgblock.data(), (G + 1) * 4);
+    if (B) std::memcpy(stage + o_bg, SJ.hbgroup.data(), (size_t)B * 4);
+    size_t k = 0;
+    for (int big = 0; big < 2; big++)
+      for (int m = 0; m < 3; m++) {
+        const auto& v = items[big][m];
+        ifirst[big][m] = k;
+        if (!v.empty()) std::memcpy(stage + o_it + k * sizeof(PItem), v.data(), v.size() * sizeof(PItem));
+        k += v.size();
+      }
+    SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
+  }
+  SJ.dsg = dsg;
+  SJ.dgblock = dgblock;
+  SJ.dbgroup = dbgroup;
+  slab_build(SJ, "pm", mlen, mpos, n, gstart, s);
+  const PSlab* slabs = SJ.slabs;
+  const uint32_t* gslab = SJ.gslab;
+  const uint64_t* gebase = SJ.gebase;
+  const uint32_t* D = SJ.D;
+  uint32_t* elems = SJ.elems;
+  // ---- P on its own stream, beside the Go sort ----
+  if (!c.part) {
+    int least = 0, greatest = 0;
+    SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
+  }
+  while (c.ev_cnt.size() < 1) {
+    hipEvent_t e1, e2;
+    SYZ_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+    c.ev_cnt.push_back(e1);
+    c.ev_sct.push_back(e2);
+  }
+  hipStream_t pq = pm_serial() ? s : c.part;
+  int* herr = c.pinned.get<int>(4);
+  SYZ_HIP(hipEventRecord(c.ev_part0, s));
+  SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
+  if (slab_bound) {
+    // byte model: the algorithm's input this pass reads, 4 B per PC + 10 B per entry
+    // (offset, group id); the element buffer it writes is intermediate traffic, not algorithmic bytes
+    ProfScope ps("k_slab", pq, total_pcs * 4 + (uint64_t)n * 10);
+    k_slab<SL_BLOCK, SL_TPW><<<(unsigned)slab_bound, SL_BLOCK, 0, pq>>>(
+        a.pcs, a.off, members, mlen, SJ.tpos, sbeg, slabs, SJ.cstart + B, dsg, gebase, lo, elems, SJ.D, err, nullptr,
+        NovSrc{}, rg_dbg());
+    SYZ_LAUNCHED();
+  }
+  SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, pq));
+  SYZ_HIP(hipEventRecord(c.ev_cnt[0], pq));
+  SYZ_HIP(hipEventRecord(c.ev_sct[0], pq));
+  SYZ_HIP(hipEventRecord(c.ev_part1, pq));
+  // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
+  uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
+  SYZ_HIP(hipMemsetAsync(sel8, 0, (n + 31) / 32 * 32 + 64, s));
+  auto run_m = [&](hipStream_t q, int big) {
+    ProfScope ps(big ? "m_big" : "m_small", q, 0);
+    const auto& it = items[big];
+    const size_t nd = it[PMODE_DIRECT].size(), nh = it[PMODE_HASH].size(), np = it[PMODE_PACKED].size();
+    if (!nd && !nh && !np) return;
+    SYZ_HIP(hipStreamWaitEvent(q, c.ev_sct[0], 0));
+    if (nd) {
+      ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
+      k_smin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], dsg, gslab, gebase, D, slabs,
+                                                   elems, rank_of_member, gstart, sel8);
+      SYZ_LAUNCHED();
+    }
+    if (nh) {
+      ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
+      k_smin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[big][PMODE_HASH], dsg, gslab, gebase, D, slabs,
+                                                        elems, rank_of_member, gstart, sel8);
+      SYZ_LAUNCHED();
+    }
+    if (np) {
+      ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
+      k_smin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
+                                                       elems, rank_of_member, gstart, sel8);
+      SYZ_LAUNCHED();
+    }
+  };
+  if (!J.plan || J.plan_key != hstart) {
+    J.plan = std::make_shared<GosortPlan>();
+    gosort_plan(*J.plan, hstart, G, s);
+    J.plan_key = hstart;
+  }
+  GosortPlan& P = *J.plan;
+  rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
+  auto small_done = [&](hipStream_t q) {
+    if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);
+    run_m(q, 0);
+  };
+  auto big_done = [&](hipStream_t q) {
+    if (P.nbig) ranks_big(el, perm, P, members, rank_of_member, ent_of_rank, q);
+    run_m(q, 1);
+  };
+  if (n) {
+    gosort_run(el, perm, n, P, s, small_done, big_done);
+  } else {
+    small_done(s);
+    big_done(s);
+  }
+  SYZ_HIP(hipEventSynchronize(c.ev_cnt[0]));
+  if (!J.done) SYZ_HIP(hipEventCreateWithFlags(&J.done, hipEventDisableTiming));
+  SYZ_HIP(hipEventRecord(J.done, s));
+  J.stats_total_pcs = total_pcs;
+  J.stats_items_direct = items[0][PMODE_DIRECT].size() + items[1][PMODE_DIRECT].size();
+  J.stats_items_hash = items[0][PMODE_HASH].size() + items[1][PMODE_HASH].size() + items[0][PMODE_PACKED].size() +
+                       items[1][PMODE_PACKED].size();
+  if (herr[0] & 1) {
+    if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
+    return false;
+  }
+  J.begun = true;
+  return true;
+}
+
 void minimize_raw_begin(MinJob& J, const RawMinArgs& a) {
   if (a.G == 0 || a.G > MAX_GROUPS_PM) fail(SYZGPU_EINVAL, "ngroups out of range (1..4096)");
   if (a.n >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
@@ -537,6 +896,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   // ---- plan: window size per call group, blocks, chunk bound, work items ----
   std::vector<PGroup> hpg;
   plan_windows(spanw, hpcs.data(), hstart.data(), G, hpg);
+  if (!pm_region())
+    return begin_slab(J, a, hstart, hpcs, hsl, hpg, lo, hi, exact_span, members, el, mlen, mpos, sbeg, err);
   std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
   std::vector<uint64_t> hgel(G + 1, 0), hcb(G, 0);  // a group's first element; its chunk bound
   std::vector<size_t> hcolg(G + 1, 0);              // a group's first column-scan item

@@ -25,6 +25,55 @@ struct PChunk {          // <= PCAP consecutive PCs of one 64-member block, in m
   uint32_t g, pad;
 };
 
+struct PSlab {
+  uint64_t elem;      // first element (4-aligned: the slab's passes leave as 16-byte vectors)
+  uint64_t t0;        // first tile (index into the job's tile sequence)
+  uint32_t m0, nmem;  // first member (partition index), members spanned
+  uint32_t nt, g;     // tiles, call group
+  uint32_t j, pad;    // slab index inside its call group
+};
+
+struct SGroup {       // per call group, slab form
+  uint64_t dbase;     // first D entry
+  uint32_t S, W;      // window bits, windows
+  uint32_t stride;    // D row length (>= the group's slabs)
+  uint32_t memb;      // members per block: min(SL_MEMB, 2^(32 - S))
+  uint32_t wbase;     // first per-window total (wtot, when P is asked for them)
+  uint32_t pad;
+  uint64_t xbase;     // element slots of the padding of the groups before (a slab's runs are padded to
+                      // 4 elements: it takes its PCs + 3 W + 4 slots at most)
+};
+
+// slots of padding a slab of a call with W windows may take (k_sl_slabs' spacing)
+__host__ __device__ inline uint64_t slab_pad(uint32_t W) { return 3ull * W + 4; }
+
+// The slab form's layout of one job (slab_dev.hpp), device arrays in the lane's scratch under a name
+// prefix. slab_plan (host): blocks, slab bounds, D rows; the caller stages hsg / hgblock / hbgroup to the
+// device and sets dsg / dgblock / dbgroup; slab_build (device): tiles, their prefix, the slabs, per-group
+// first slab and element; then k_slab (P) and for_slab_window (M).
+struct SlabJob {
+  uint32_t G = 0, B = 0;
+  uint64_t slab_bound = 0, dtotal = 0, wtotal = 0, total_pcs = 0, xtotal = 0;
+  std::vector<SGroup> hsg;
+  std::vector<uint32_t> hgblock, hbgroup;
+  const SGroup* dsg = nullptr;
+  const uint32_t* dgblock = nullptr;
+  const uint32_t* dbgroup = nullptr;
+  uint64_t* tpos = nullptr;
+  uint64_t* cstart = nullptr;  // cstart[B] = slabs
+  PSlab* slabs = nullptr;
+  uint32_t* gslab = nullptr;
+  uint64_t* gebase = nullptr;
+  uint32_t* D = nullptr;
+  uint32_t* elems = nullptr;
+  uint32_t* wtot = nullptr;  // per (call, window) totals, when asked for
+};
+// hpcs: PCs each call group's members hold (their slices); S, W from hpg
+void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* hpcs, const std::vector<PGroup>& hpg,
+               uint32_t G, bool want_wtot);
+void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint64_t* mpos, size_t nmem,
+                const uint64_t* gstart, hipStream_t s);
+
 struct RawMinArgs {
   const uint32_t* pcs;
   const uint64_t* off;

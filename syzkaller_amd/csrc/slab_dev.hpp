@@ -1,0 +1,511 @@
+// Slab form of the raw Minimize pipeline's transpose (P) and window walk (M): the covers are read from
+// HBM once (round 3's region form read them twice, a count pass then the scatter).
+//
+// A SLAB is up to SL_TILES tiles of one call group's members (a tile = <= 64 consecutive PCs of one
+// member's sorted cover), i.e. <= 32K PCs, cut from the group's member sequence (partition order) in
+// blocks of at most SL_MEMB (and 2^(32 - S)) members so a member's tag fits the element. One workgroup
+// per slab:
+//   * member table in LDS, each lane resolves one tile of its wave (address, count, tag) by a search,
+//     the wave's tiles are loaded with wave-uniform (scalar) addresses, all of them in flight;
+//   * window histogram by LDS atomics, an exclusive scan -> window starts inside the slab;
+//   * the slab's window-major element sequence is produced in PASSES over a 16K-element LDS buffer:
+//     pass k takes the windows that START in [k * 16K, (k + 1) * 16K) (a contiguous window range), each
+//     element's place comes from the window's LDS cursor, and the pass leaves as one contiguous run of
+//     16-byte stores; the few elements of a window running past the buffer are stored directly;
+//   * the window starts go out WINDOW-MAJOR per call group: D[dbase + w * stride + j] = element offset
+//     (from the group's first element) of window w of the group's slab j, so M reads, for its window,
+//     two contiguous rows (starts, and the next window's starts = ends).
+// M (for_slab_window) then walks one run per slab: a window's runs are ~SL_TILES * 64 / W elements long
+// (128 for a dense call of 256 windows: 512-byte runs, against round 2's 64-element chunk runs).
+#pragma once
+#include "panels_dev.hpp"
+
+namespace syz {
+
+#ifndef SYZ_SL_BLOCK
+#define SYZ_SL_BLOCK 512
+#endif
+#ifndef SYZ_SL_TPW
+#define SYZ_SL_TPW 64
+#endif
+#ifndef SYZ_SL_SKIP
+#define SYZ_SL_SKIP 1
+#endif
+#ifndef SYZ_SL_BUF_BITS
+#define SYZ_SL_BUF_BITS 14
+#endif
+constexpr int SL_BLOCK = SYZ_SL_BLOCK;
+constexpr int SL_WAVES = SL_BLOCK / 64;
+constexpr int SL_TPW = SYZ_SL_TPW;
+constexpr uint32_t SL_TILES = (uint32_t)SL_TPW * SL_WAVES;  // tiles per slab (<= 64 PCs each)
+constexpr uint32_t SL_BUF_BITS = SYZ_SL_BUF_BITS;
+constexpr uint32_t SL_BUF = 1u << SL_BUF_BITS;                 // LDS staging elements per pass
+constexpr uint32_t SL_MEMB = 512;                              // members per slab at most
+constexpr uint32_t SL_PMAX = (SL_TILES * 64 + SL_BUF - 1) / SL_BUF + 1;  // passes at most
+static_assert(SL_TPW <= 64, "a wave's tile table is one register per lane");
+constexpr uint32_t SL_NONE = 0xFFFFFFFFu;  // a padding slot: no element (no member has the all-ones tag)
+
+// ---- slab planning on the device ------------------------------------------------------------------
+static __global__ void k_sl_tiles(const uint32_t* mlen, size_t n, uint32_t* mtile) {
+  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x)
+    mtile[m] = (mlen[m] + 63) >> 6;
+}
+
+// slabs per block of memb members
+static __global__ void k_sl_blocks(const uint32_t* bgroup, uint32_t B, const uint32_t* gblock, const uint64_t* gstart,
+                            const SGroup* sg, const uint64_t* tpos, uint32_t* nsub) {
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) {
+    const uint32_t g = bgroup[b];
+    const uint32_t mb_ = sg[g].memb;
+    const uint64_t mb = gstart[g] + (uint64_t)(b - gblock[g]) * mb_;
+    const uint64_t me = min<uint64_t>(mb + mb_, gstart[g + 1]);
+    nsub[b] = (uint32_t)((tpos[me] - tpos[mb] + SL_TILES - 1) / SL_TILES);
+  }
+}
+
+// one thread per slab (grid over a bound; cstart[B] = the slabs there are)
+static __global__ void k_sl_slabs(const uint32_t* bgroup, uint32_t B, const uint32_t* gblock, const uint64_t* gstart,
+                           const SGroup* sg, const uint64_t* tpos, const uint64_t* mpos, const uint64_t* cstart,
+                           uint64_t bound, PSlab* slabs) {
+  const uint64_t ns = cstart[B];
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < min(ns, bound);
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t b = (uint32_t)upper_bound_dev<uint64_t>(cstart, 0, B + 1, c) - 1;  // cstart[b] <= c < cstart[b+1]
+    const uint32_t g = bgroup[b];
+    const uint32_t mb_ = sg[g].memb;
+    const uint64_t mb = gstart[g] + (uint64_t)(b - gblock[g]) * mb_;
+    const uint64_t me = min<uint64_t>(mb + mb_, gstart[g + 1]);
+    const uint64_t T0 = tpos[mb] + (c - cstart[b]) * SL_TILES;
+    const uint64_t T1 = min<uint64_t>(T0 + SL_TILES, tpos[me]);
+    // the member holding tile T0: the first m with tpos[m + 1] > T0; the one holding T1 - 1 likewise
+    const uint64_t m0 = upper_bound_dev<uint64_t>(tpos, mb + 1, me + 1, T0) - 1;
+    const uint64_t m1 = upper_bound_dev<uint64_t>(tpos, m0 + 1, me + 1, T1 - 1) - 1;
+    const uint64_t pcpos = mpos[m0] + 64 * (T0 - tpos[m0]);  // the slab's first PC in the slices' order
+    PSlab s;
+    // PCs before it + the padding slots of every slab before it (at most slab_pad(W) each), 4-aligned
+    const SGroup gp = sg[g];
+    s.elem = (pcpos + gp.xbase + (c - cstart[gblock[g]]) * slab_pad(gp.W) + 3) & ~3ull;
+    s.t0 = T0;
+    s.m0 = (uint32_t)m0;
+    s.nmem = (uint32_t)(m1 - m0 + 1);
+    s.nt = (uint32_t)(T1 - T0);
+    s.g = g;
+    s.j = (uint32_t)(c - cstart[gblock[g]]);
+    s.pad = 0;
+    slabs[c] = s;
+  }
+}
+
+// gslab[g] = the group's first slab (gslab[G] = all of them), gebase[g] = its first element
+static __global__ void k_sl_groups(const uint32_t* gblock, uint32_t G, const uint64_t* cstart, const PSlab* slabs,
+                            uint32_t* gslab, uint64_t* gebase) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x) {
+    const uint64_t c = cstart[gblock[g]];
+    gslab[g] = (uint32_t)c;
+    if (g < G) gebase[g] = c < cstart[gblock[g + 1]] ? slabs[c].elem : 0;
+  }
+}
+
+// ---- P: one slab per workgroup ---------------------------------------------------------------------
+// (see the file comment). err bit 1: a PC outside [lo, lo + W << S) (an unsorted cover: the job is redone
+// on exact bounds).
+// NOV: the new-coverage check's second source (members with an entry id >= ns.n1 are maxCover tables),
+// every list checked strictly increasing as it is read (err 1 for a table, 4 for a cover: lane
+// neighbours, and a tile's first PC against the member's PC before it); wtot (optional): per (call,
+// window) element totals, added up over the slabs.
+template <int BLOCK, int TPW, bool NOV = false>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_slab(
+    const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
+    const uint32_t* __restrict__ mlen, const uint64_t* __restrict__ tpos, const uint32_t* __restrict__ sbeg,
+    const PSlab* __restrict__ slabs, const uint64_t* nslab, const SGroup* __restrict__ sg,
+    const uint64_t* __restrict__ gebase, uint32_t lo, uint32_t* __restrict__ elems, uint32_t* __restrict__ D,
+    int* err, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int dbg = 0) {
+  constexpr int WAVES = BLOCK / 64;
+  static_assert((uint32_t)TPW * WAVES == SL_TILES, "slab tiles");
+  __shared__ __align__(16) uint32_t obuf[SL_BUF];
+  __shared__ uint32_t hist[WMAX + 1 + 64];  // counts, then cursors; + a dummy slot per lane
+  __shared__ int32_t mrel[SL_MEMB];         // member i's tile 0 as a slab tile index (< 0: began earlier)
+  __shared__ uint32_t mtp[SL_MEMB];         // the search keys: mrel clipped to [0, nt]
+  __shared__ uint32_t mlo[SL_MEMB], mhi[SL_MEMB], mln[SL_MEMB];
+  __shared__ uint8_t mtab[NOV ? SL_MEMB : 1];  // NOV: member i is a table
+  __shared__ uint32_t red[WAVES + 1];
+  __shared__ uint32_t pw[SL_PMAX + 2];      // first window of each pass
+  __shared__ uint32_t pa[SL_PMAX + 1];      // its start (read before any pass moves the cursors)
+  __shared__ int unsorted;                  // some tile's PCs are not ascending (Minimize allows it)
+  const uint64_t c = blockIdx.x;
+  if (c >= *nslab) return;
+  const int wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  const PSlab sl = slabs[c];
+  const SGroup gp = sg[sl.g];
+  const uint32_t S = gp.S, W = gp.W, nt = sl.nt, nmem = sl.nmem;
+  for (uint32_t i = threadIdx.x; i < nmem; i += BLOCK) {
+    const uint64_t m = (uint64_t)sl.m0 + i;
+    const int64_t r = (int64_t)tpos[m] - (int64_t)sl.t0;
+    mrel[i] = (int32_t)r;
+    mtp[i] = (uint32_t)min<int64_t>(max<int64_t>(r, 0), (int64_t)nt);
+    const uint32_t e = members[m];
+    const uint32_t* src;
+    if constexpr (NOV) {
+      src = e >= ns.n1 ? ns.mc + ns.mc_off[e - ns.n1] : pcs + off[e];
+      mtab[i] = e >= ns.n1;
+    } else {
+      src = pcs + off[e] + (sbeg ? sbeg[m] : 0u);
+    }
+    const uint64_t a = (uint64_t)(uintptr_t)src;
+    mlo[i] = (uint32_t)a;
+    mhi[i] = (uint32_t)(a >> 32);
+    mln[i] = mlen[m];
+  }
+  for (uint32_t i = threadIdx.x; i <= W; i += BLOCK) hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < SL_PMAX + 2; i += BLOCK) pw[i] = W;
+  if (threadIdx.x == 0) unsorted = 0;
+  __syncthreads();
+  // lane k of this wave: tile t = wv + WAVES k (its member by a search of the tile prefix)
+  uint32_t alo, ahi, cz;
+  {
+    const uint32_t t = wv + WAVES * lane;
+    const uint32_t tt = t < nt ? t : 0u;
+    uint32_t a = 0, b = nmem;  // largest i with mtp[i] <= tt
+    while (b - a > 1) {
+      const uint32_t mid = (a + b) >> 1;
+      if (mtp[mid] <= tt)
+        a = mid;
+      else
+        b = mid;
+    }
+    const uint32_t ti = (uint32_t)((int32_t)tt - mrel[a]);  // tile inside the member
+    const uint64_t addr = (((uint64_t)mhi[a] << 32) | mlo[a]) + 256ull * ti;
+    alo = (uint32_t)addr;
+    ahi = (uint32_t)(addr >> 32);
+    const uint32_t cnt = (t < nt && lane < (unsigned)TPW) ? min(64u, mln[a] - 64 * ti) : 0u;
+    // count | (not the member's first tile) << 7 | (a table) << 8 | member tag << 9
+    uint32_t fl = 0;
+    if constexpr (NOV) fl = (ti > 0 ? 0x80u : 0u) | (mtab[a] ? 0x100u : 0u);
+    cz = cnt | fl | (a << 9);
+  }
+  // every tile's PCs into registers, all loads in flight (a tile's address is wave-uniform)
+  uint32_t v[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; k++) {
+    const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, k);
+    const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ahi, k) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)alo, k);
+    const uint32_t cnt = z & 0x7Fu;
+    v[k] = reinterpret_cast<const uint32_t*>((uintptr_t)base)[lane < cnt ? lane : 0u];
+    if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+  int bad = 0;  // err bits this lane saw
+  if constexpr (NOV) {
+    // strictly increasing: lane neighbours inside a tile; a tile's first PC against the PC before it
+#pragma unroll
+    for (int k = 0; k < TPW; k++) {
+      const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, k);
+      const uint32_t cnt = z & 0x7Fu;
+      const int eb = (z & 0x100u) ? 1 : 4;
+      const uint32_t pv = __shfl_up(v[k], 1, 64);
+      if (lane > 0 && lane < cnt && pv >= v[k]) bad |= eb;
+      if ((z & 0x80u) && lane == 0 && cnt) {
+        const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ahi, k) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)alo, k);
+        if (reinterpret_cast<const uint32_t*>((uintptr_t)base)[-1] >= v[k]) bad |= eb;
+      }
+    }
+  }
+  if (dbg & 16) {  // timing only: the loads alone
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < TPW; k++) acc += v[k];
+    if (acc == 0x9E3779B9u) err[1] = 1;
+    return;
+  }
+  // from here on v holds the PC's offset from lo: window = v >> S, offset in it = v & omask
+  // window histogram
+  const uint32_t DUMMY = WMAX + 1 + lane;
+  bool desc = false;  // a lane below its left neighbour
+#pragma unroll
+  for (int k = 0; k < TPW; k++) {
+    const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, k);
+    const uint32_t cnt = z & 0x7Fu;
+    if constexpr (!NOV) {  // (NOV checked strict order above: an unsorted batch fails)
+      const uint32_t pv = __shfl_up(v[k], 1, 64);
+      desc |= lane > 0 && lane < cnt && pv > v[k];
+    }
+    v[k] -= lo;
+    const uint32_t w = v[k] >> S;
+    const bool in = lane < cnt;
+    // outside the windows: an unsorted cover (Minimize: redone on exact bounds; NOV: out of order)
+    bad |= (in && w >= W) ? (NOV ? ((z & 0x100u) ? 1 : 4) : 1) : 0;
+    atomicAdd(&hist[in && w < W ? w : DUMMY], 1u);
+    if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+  }
+  if (__ballot(desc) && lane == 0) unsorted = 1;
+  {
+    const uint64_t bm = __ballot(bad != 0);
+    if (bm) {
+      int all = bad;
+#pragma unroll
+      for (int dd = 32; dd >= 1; dd >>= 1) all |= __shfl_xor(all, dd, 64);
+      if (lane == (unsigned)(__ffsll((unsigned long long)bm) - 1)) atomicOr(err, all);
+    }
+  }
+  __syncthreads();
+  if (wtot)
+    for (uint32_t i = threadIdx.x; i < W; i += BLOCK)
+      if (hist[i]) atomicAdd(&wtot[gp.wbase + i], hist[i]);
+  // window starts -> cursors, D rows, pass boundaries
+  uint32_t total;
+  {
+    uint32_t run = 0;
+    const uint64_t dcol = gp.dbase + sl.j;
+    const uint32_t erel = (uint32_t)(sl.elem - gebase[sl.g]);
+    for (uint32_t b0 = 0; b0 <= W; b0 += BLOCK) {
+      const uint32_t i = b0 + threadIdx.x;
+      const uint32_t x = i < W ? (hist[i] + 3u) & ~3u : 0u;  // runs padded to 16 bytes (M's vectors)
+      uint32_t tot;
+      const uint32_t pre = block_excl_scan<BLOCK>(x, red, &tot) + run;
+      if (i <= W) {
+        hist[i] = pre;
+        D[dcol + (uint64_t)i * gp.stride] = erel + pre;
+      }
+      run += tot;
+    }
+    total = run;
+  }
+  __syncthreads();
+  // pw[k] = first window i with wst[i] >= k * BUF (window i's start is hist[i] now; hist[W] = total):
+  // the i with wst[i - 1] < k * BUF <= wst[i]
+  for (uint32_t i = threadIdx.x; i <= W; i += BLOCK) {
+    const uint32_t s1 = hist[i];
+    const uint32_t k1 = s1 >> SL_BUF_BITS;
+    const uint32_t k0 = i ? (hist[i - 1] >> SL_BUF_BITS) + 1u : 0u;
+    for (uint32_t k = k0; k <= k1 && k < SL_PMAX + 2; k++) pw[k] = i;
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k <= SL_PMAX; k += BLOCK) pa[k] = pw[k] < W ? hist[pw[k]] : total;
+  if (dbg & 32) return;  // timing only: loads, histogram, scan
+  __syncthreads();
+  const uint32_t npass = (total + SL_BUF - 1) >> SL_BUF_BITS;
+  const bool unsorted_r = unsorted != 0;
+  const uint32_t omask = (1u << S) - 1;
+  uint32_t* gel = elems + sl.elem;
+  for (uint32_t k = 0; k < npass; k++) {
+    const uint32_t wl = pw[k], wh = pw[k + 1];
+    const uint32_t base = k << SL_BUF_BITS, lim = base + SL_BUF;
+    const uint32_t a0 = pa[k];  // the pass's first element: window wl's start
+    // the buffer's padding slots (a run's last vector) hold the no-element value
+    {
+      uint4* o4 = reinterpret_cast<uint4*>(obuf);
+      const uint4 none4 = make_uint4(SL_NONE, SL_NONE, SL_NONE, SL_NONE);
+      for (uint32_t i = threadIdx.x; i < SL_BUF / 4; i += BLOCK) o4[i] = none4;
+    }
+    __syncthreads();
+    // opaque per pass, so the compiler does not hoist 64 tiles' elements out of the pass loop (VGPRs)
+    uint32_t Sp = S, om = omask;
+    asm volatile("" : "+s"(Sp), "+s"(om));
+    const bool skip_ok = SYZ_SL_SKIP && !unsorted_r;
+    // a tile's PCs are sorted, so its windows are [w(lane 0), w(last lane)]: a tile outside the pass's
+    // windows is skipped whole (most tiles fall into one pass)
+    constexpr int PB = 4;
+#pragma unroll
+    for (int k0 = 0; k0 < TPW; k0 += PB) {
+      bool any = false;
+#pragma unroll
+      for (int q = 0; q < PB; q++) {
+        const int kk = k0 + q;
+        const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, kk);
+        const uint32_t cnt = z & 0x7Fu;
+        const uint32_t wa = (uint32_t)__builtin_amdgcn_readlane((int)v[kk], 0) >> Sp;
+        const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)v[kk], (int)(cnt ? cnt - 1 : 0)) >> Sp;
+        any |= cnt && wb >= wl && wa < wh;
+      }
+      if (!any && skip_ok) continue;  // wave-uniform
+      uint32_t pos[PB], el[PB];
+      bool ok[PB];
+#pragma unroll
+      for (int q = 0; q < PB; q++) {
+        const int kk = k0 + q;
+        const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, kk);
+        const uint32_t d = v[kk], w = d >> Sp;
+        ok[q] = lane < (z & 0x7Fu) && (w - wl) < (wh - wl);
+        el[q] = (d & om) | ((z >> 9) << Sp);
+        pos[q] = 0;
+        if (ok[q]) pos[q] = atomicAdd(&hist[w], 1u);  // lanes outside the pass issue nothing
+      }
+#pragma unroll
+      for (int q = 0; q < PB; q++) {
+        if (ok[q]) {
+          if (pos[q] < lim)
+            obuf[pos[q] - base] = el[q];
+          else
+            gel[pos[q]] = el[q];  // a window running past the buffer
+        }
+      }
+    }
+    __syncthreads();
+    // a last window running past the buffer: its padding slots are stored directly
+    if (wh > wl && threadIdx.x < 3) {
+      const uint32_t e = hist[wh - 1] + threadIdx.x;
+      if (e >= lim && (e & 3u)) gel[e] = SL_NONE;
+    }
+    // the pass leaves as [a0, e0): hist[wh - 1] is the end of its last window now (+ its padding)
+    const uint32_t e0 = wh > wl ? min((hist[wh - 1] + 3u) & ~3u, lim) : a0;
+    if (e0 > a0) {
+      const uint64_t A = sl.elem + a0, E = sl.elem + e0;
+      const uint64_t q0 = A >> 2, q1 = (E + 3) >> 2;
+      uint4* g4 = reinterpret_cast<uint4*>(elems);
+      for (uint64_t q = q0 + threadIdx.x; q < q1; q += BLOCK) {
+        const uint64_t e = q << 2;
+        const uint32_t lb = (uint32_t)(e - sl.elem) - base;  // LDS index of the vector's first element
+        if (e >= A && e + 4 <= E) {
+          g4[q] = *reinterpret_cast<const uint4*>(&obuf[lb]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; u++)
+            if (e + u >= A && e + u < E) elems[e + u] = obuf[lb + u];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- M walk over a window's slab runs ---------------------------------------------------------------
+// The runs of (call g, window w): run j = [D[w][j], D[w + 1][j]) from the group's first element (both
+// multiples of 4: runs are padded to 16 bytes with SL_NONE), its members from slab j's first member.
+// Batches of blockDim runs (one per thread), numbered in 16-byte VECTORS by one workgroup scan; the
+// waves stream the concatenation in blocks of 64 vectors (a lane's run: the run holding its block's
+// first vector plus a mbcnt of the mask of runs starting inside the block), U blocks in flight per
+// wave, one 16-byte load and four elements per lane. f(offset, rank) for every element slot; rank
+// RANK_NONE for padding and lanes past the window. IDENT: rank = member position (the new-coverage
+// check). scratch: 2 * blockDim + 3 * NBLK words (callers alias it with their emit bitmap); red64: 2
+// words per wave. NBLK: blocks per element window of a batch.
+template <int U, bool IDENT, uint32_t NBLK = PK_NBLK, class F>
+__device__ __forceinline__ void for_slab_window(const PItem it, const SGroup* __restrict__ sg,
+                                                const uint32_t* __restrict__ gslab, const uint64_t* __restrict__ gebase,
+                                                const uint32_t* __restrict__ D, const PSlab* __restrict__ slabs,
+                                                const uint32_t* __restrict__ elems,
+                                                const uint32_t* __restrict__ rank_of_member, uint32_t* scratch,
+                                                uint64_t* red64, F f) {
+  const uint32_t g = it.g, w = it.w;
+  const uint32_t c0 = gslab[g], ns = gslab[g + 1] - c0;
+  if (ns == 0) return;
+  const SGroup p = sg[g];
+  const uint32_t S = p.S, omask = (1u << S) - 1;
+  const uint32_t* Dw = D + p.dbase + (uint64_t)w * p.stride;
+  const uint32_t* Dw1 = Dw + p.stride;
+  const uint4* gel4 = reinterpret_cast<const uint4*>(elems + gebase[g]);
+  const uint32_t BD = blockDim.x;        // runs per batch: one per thread
+  uint32_t* rrel = scratch;              // [BD] vector offset of run k's vector 0 - its prefix
+  uint32_t* rmb = scratch + BD;          // [BD] first member of run k's slab
+  uint32_t* bstart = scratch + 2 * BD;   // [NBLK] run holding block j's first vector
+  uint32_t* bmask = bstart + NBLK;       // [2 NBLK] runs starting inside block j (bit = offset)
+  const int nwaves = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  auto load_run = [&](uint32_t j, uint32_t& len, uint32_t& rel, uint32_t& mb) {
+    len = rel = mb = 0;
+    if (j < ns) {
+      const uint32_t a = Dw[j];
+      rel = a >> 2;
+      len = (Dw1[j] - a) >> 2;
+      mb = slabs[c0 + j].m0;
+    }
+  };
+  uint32_t nlen, nrel, nmb;
+  load_run(threadIdx.x, nlen, nrel, nmb);
+  for (uint32_t rb = 0; rb < ns; rb += BD) {
+    const uint32_t len = nlen, rel = nrel, mb = nmb;
+    uint32_t pre, k, T;
+    pk_scan(len, reinterpret_cast<uint32_t*>(red64), pre, k, T);
+    if (len) {
+      rrel[k] = rel - pre;
+      rmb[k] = mb;
+    }
+    load_run(rb + BD + threadIdx.x, nlen, nrel, nmb);
+    for (uint32_t ew = 0; ew < T; ew += 64 * NBLK) {
+      const uint32_t te = min(T, ew + 64 * NBLK);
+      for (uint32_t j = threadIdx.x; j < 2 * NBLK; j += blockDim.x) bmask[j] = 0;
+      __syncthreads();
+      if (len && pre < te && pre + len > ew) {
+        const uint32_t a = max(pre, ew) - ew, b = min(pre + len, te) - ew;
+        for (uint32_t j = (a + 63) >> 6; (j << 6) < b; j++) bstart[j] = k;
+        if (pre >= ew && (pre & 63)) {
+          const uint32_t o = pre - ew;
+          atomicOr(&bmask[2 * (o >> 6) + ((o >> 5) & 1)], 1u << (o & 31));
+        }
+      }
+      __syncthreads();
+      const uint32_t nblk = (te - ew + 63) >> 6;
+      const uint32_t step = (uint32_t)nwaves * U;
+      // a step's runs (LDS) and vector loads; a lane past the window reads its block's first vector
+      uint32_t mbr[U], mbn[U];
+      bool ok[U], okn[U];
+      uint4 ev[U];
+      auto prep_load = [&](uint32_t j0, uint32_t* mb_, bool* ok_) {
+        uint32_t vi[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t j = j0 + (uint32_t)nwaves * u, jj = min(j, nblk - 1);
+          const uint32_t r0 = bstart[jj];
+          const uint32_t mlo_ = bmask[2 * jj], mhi_ = bmask[2 * jj + 1];
+          const uint32_t slo = (mlo_ >> 1) | (mhi_ << 31), shi = mhi_ >> 1;
+          const uint32_t idx = ew + (j << 6) + lane;
+          ok_[u] = j < nblk && idx < te;
+          const uint32_t r = r0 + __builtin_amdgcn_mbcnt_hi(shi, __builtin_amdgcn_mbcnt_lo(slo, 0u));
+          const uint32_t rr = ok_[u] ? r : r0;
+          vi[u] = rrel[rr] + (ok_[u] ? idx : ew + (jj << 6));
+          mb_[u] = rmb[rr];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) ev[u] = gel4[vi[u]];
+      };
+      if ((uint32_t)wv < nblk) prep_load(wv, mbr, ok);
+      for (uint32_t j0 = wv; j0 < nblk; j0 += step) {
+        // this step's ranks (gathers) and offsets; then the next step's loads into the same registers
+        // (this step's elements are dead by then); then the updates, which wait only for the gathers
+        uint32_t R[4 * U], o[4 * U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t q[4] = {ev[u].x, ev[u].y, ev[u].z, ev[u].w};
+#pragma unroll
+          for (int t = 0; t < 4; t++) {
+            const bool val = ok[u] && q[t] != SL_NONE;
+            if constexpr (IDENT)
+              R[4 * u + t] = val ? mbr[u] + (q[t] >> S) : RANK_NONE;
+            else
+              R[4 * u + t] = rank_of_member[mbr[u] + (val ? (q[t] >> S) : 0u)];
+            o[4 * u + t] = val ? (q[t] & omask) : 0xFFFFFFFFu;
+          }
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const bool more = j0 + step < nblk;  // wave-uniform
+        if (more) prep_load(j0 + step, mbn, okn);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 4 * U; k++) f(o[k] & omask, o[k] == 0xFFFFFFFFu ? RANK_NONE : R[k]);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          mbr[u] = mbn[u];
+          ok[u] = okn[u];
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// elements of one (call, window): the lengths of its slab runs
+template <int BLOCK>
+__device__ __forceinline__ uint32_t slab_window_count(const PItem it, const SGroup* sg, const uint32_t* gslab,
+                                                      const uint32_t* D, uint32_t* red) {
+  const SGroup p = sg[it.g];
+  const uint32_t ns = gslab[it.g + 1] - gslab[it.g];
+  const uint32_t* Dw = D + p.dbase + (uint64_t)it.w * p.stride;
+  uint32_t s = 0;
+  for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) s += Dw[j + p.stride] - Dw[j];
+  return block_sum<BLOCK>(s, red);
+}
+
+}  // namespace syz

@@ -53,8 +53,8 @@ def lpt_assign(weights, nranks):
 # packs and stream on the side stream, overlapped; their PCs are charged a fraction.
 SMALL_GROUP = 8192
 LAT_REF_N, LAT_REF_US, LAT_PER_DOUBLING_US = 203_000, 290.0, 0.0
-US_PER_PC = 4.26e-3
-US_PER_ENTRY = 1.24
+US_PER_PC = 4.26e-6  # µs per streamed PC (4.26 ps)
+US_PER_ENTRY = 1.24e-3  # µs per held entry (1.24 ns)
 SMALL_PC_FRACTION = 0.3
 
 

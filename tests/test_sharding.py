@@ -138,6 +138,22 @@ def test_plan_parts_splits_the_bottleneck_group_and_is_deterministic():
     assert np.array_equal(counts, (e > 0).astype(np.int64))
 
 
+def test_cost_model_units_are_microseconds():
+    # the modelled step of one rank holding the whole bench corpus (config 4: 1M programs, 422M PCs)
+    # is the measured N=1 step's order, a few thousand microseconds (a 1000x unit slip shows here)
+    p = synth.params(0x5EED0004, 1_000_000, 289, 2_000_000)
+    group, off, _ = synth.layout(p)
+    e, w = sharding.layout_stats(group, off, 289)
+    cost = sharding.plan_parts(e, w, 1).cost
+    assert 1_000 < float(cost.max()) < 10_000
+    # and at 8 ranks over the 8M-program job every rank models a step of the same order
+    p8 = synth.params(0x5EED0004, 8_000_000, 289, 2_000_000)
+    g8, o8, _ = synth.layout(p8)
+    e8, w8 = sharding.layout_stats(g8, o8, 289)
+    c8 = sharding.plan_parts(e8, w8, 8).cost
+    assert 1_000 < float(c8.min()) <= float(c8.max()) < 10_000
+
+
 def test_plan_parts_single_rank_keeps_groups_whole():
     c = _corpus()
     e, w = sharding.layout_stats(c.group, c.off, c.ngroups)
