@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--novelty-covers", type=int, default=1_000_000)
     ap.add_argument("--novelty-wide", type=int, default=1,
                     help="also time the novelty batch with its PC span stretched 34x (272M addresses)")
+    ap.add_argument("--canonicalize", type=int, default=1,
+                    help="also time cover.Canonicalize over 1M raw execution covers (device entry) at N=1")
     ap.add_argument("--setops", type=int, default=1,
                     help="also time the batched set ops on config-3 covers (triage pairs) at N=1")
     ap.add_argument("--hub", type=int, default=1, help="also time config 5's hub ingest (scan + SHA-1 + dedup) at N=1")
@@ -65,6 +67,10 @@ def parse():
                     help="also time the call-ID co-occurrence X^T X on int8 MFMA (SURVEY.md F1/K9) at N=1")
     ap.add_argument("--split-largest", type=int, default=0,
                     help="rehearsal: force the largest call group into this many PC-key parts")
+    ap.add_argument("--total-progs", type=int, default=0,
+                    help="strong scaling: this many programs in the whole job, sharded over the N GPUs (configs[3]: "
+                         "1M over 8); default 0 = weak scaling, --progs-per-gpu on every GPU (N x 1M: configs[4]'s "
+                         "hub-merge shape at N = 8)")
     ap.add_argument("--emulate", default="", help="W:r — rehearsal: run rank r's shard of a W-rank job on this "
                     "one process (no collectives; the printed line is that rank's time, not a job value)")
     return ap.parse_args()
@@ -139,6 +145,20 @@ def roofline(name, ev, peak_gbs=None):
     return out
 
 
+def workload_label(args, world):
+    """The BASELINE.json config the line measures: configs[3] (1M programs; strong scaling over N GPUs
+    with --total-progs) or, weak scaling at N > 1, configs[4]'s hub-merge shape (N managers' corpora of
+    --progs-per-gpu programs each)."""
+    tail = "2M-PC space, 289 calls, C=1159"
+    if args.total_progs:
+        return "config4-%dk over %d GPU%s (strong scaling): %s" % (args.total_progs // 1000, world,
+                                                                  "s" if world > 1 else "", tail)
+    if world == 1:
+        return "config4-1M: %d programs on 1 GPU, %s" % (args.progs_per_gpu, tail)
+    return ("config5-shape: %d managers' corpora of %d programs (%d programs, weak scaling: %d per GPU), %s"
+            % (world, args.progs_per_gpu, args.progs_per_gpu * world, args.progs_per_gpu, tail))
+
+
 def static_usage(C):
     """calcStaticPriorities' input: the usage matrix of the reference's sys/*.txt (1159 calls, bundled
     as package data by tools/gen_sys_usage.py); other call counts take a seeded matrix of the same
@@ -186,7 +206,8 @@ def main():
     # ---- corpus (synthetic, deterministic; generated on the host, then made resident) ----
     t0 = time.time()
     C, G = args.calls, args.ngroups
-    p = synth.params(args.seed, args.progs_per_gpu * emu_world, G, args.npcs)
+    job_progs = args.total_progs or args.progs_per_gpu * emu_world  # programs of the whole job
+    p = synth.params(args.seed, job_progs, G, args.npcs)
     group, off, plen = synth.layout(p)
     # key-space sharding plan: call groups whole or split by PC-value ranges over ranks
     ent_g, pcs_g = sharding.layout_stats(group, off, G)
@@ -304,7 +325,7 @@ def main():
         sharding.allreduce(t, dist, dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_progs = args.progs_per_gpu * world
+    total_progs = args.total_progs or args.progs_per_gpu * world
     sum_pcs_all = int(off[-1])  # the whole job's corpus (a split group is held by several ranks)
     ms_step = elapsed / args.steps * 1e3
     value = total_progs * args.steps / elapsed
@@ -340,17 +361,19 @@ def main():
         tail = text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step) if args.text and solo else None
         nov = novelty_leg(args, dev, L, read_prof) if args.novelty and solo else None
         cooc = cooccurrence_leg(args, dev, L, read_prof, corp, C) if args.cooccurrence and solo else None
-        sops = setops_leg(args, dev, L) if args.setops and solo else None
+        sops = setops_leg(args, dev, L, read_prof) if args.setops and solo else None
+        canon = canonicalize_leg(args, dev, L) if args.canonicalize and solo else None
         hubr = hub_leg(args, dev, L, read_prof, corp, sptr) if args.hub and solo else None
         ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr) if args.analytics and solo else None
         app = append_leg(args, dev, store, sptr, C, d_hist) if args.append and solo else None  # last: replaces
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "progs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "higher_is_better": True, "scaling": "strong" if args.total_progs else "weak", "vs_baseline": None,
+            "dtype": "u32",
             "data": "synthetic: seeded generator (SURVEY.md §8d shapes); raw covers resident in HBM, every step "
                     "from the covers (no store or dictionary built ahead)",
-            "config": {"workload": "config4-1M: 1M programs/GPU, 2M-PC space, 289 calls, C=1159",
+            "config": {"workload": workload_label(args, world),
                        "progs_per_gpu": args.progs_per_gpu, "total_progs": total_progs,
                        "sum_pcs": sum_pcs_all, "ngroups": G, "npcs": args.npcs, "calls": C,
                        "step": "minimizeCorpus from raw covers (partition + Go-sort ranks + window transpose + "
@@ -375,6 +398,7 @@ def main():
             "novelty_config3": nov if nov is not None else nov_sh,
             "call_cooccurrence": cooc,
             "setops_triage": sops,
+            "canonicalize_raw_covers": canon,
             "cover_analytics": ana,
             "hub_ingest_config5": hubr,
             "manager_cycle": app,
@@ -843,7 +867,71 @@ def novelty_leg(args, dev, L, read_prof):
     return res
 
 
-def setops_leg(args, dev, L):
+def canonicalize_leg(args, dev, L):
+    """cover.Canonicalize over a batch (cover/cover.go:28-40; its caller syz-fuzzer/fuzzer.go:355 runs it
+    on every input's cover): config 3's 1M fresh covers as kcov returns them when the executor's
+    dedup flag is off (executor.cc:565-585), each cover's PCs in random order with ~20 % of them
+    repeated; device-resident (syzgpu_canonicalize_batch_dev, in place: the raw batch is restored by an
+    untimed device copy before each step). Algorithmic bytes: the raw PCs read, the canonical ones
+    written, offsets read and lengths written."""
+    import torch
+    from syzkaller_amd import cover, synth
+    G = args.ngroups
+    c = synth.corpus(args.seed + 0x31, args.novelty_covers, G, args.npcs)
+    n = c.n
+    pcs = torch.from_numpy(c.pcs.view(np.int32)).to(dev)
+    lens = torch.from_numpy(np.diff(c.off).astype(np.int64)).to(dev)
+    seg = torch.repeat_interleave(torch.arange(n, device=dev, dtype=torch.int64), lens)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    dup = torch.rand(pcs.numel(), generator=gen, device=dev) < 0.2
+    pcs2, seg2 = torch.cat([pcs, pcs[dup]]), torch.cat([seg, seg[dup]])
+    del pcs, seg, dup
+    key = (seg2 << 32) | torch.randint(0, 1 << 31, (seg2.numel(),), generator=gen, device=dev, dtype=torch.int64)
+    raw = pcs2[torch.argsort(key)].contiguous()
+    del key, pcs2
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(torch.bincount(seg2, minlength=n), 0, out=off[1:])
+    del seg2
+    work = torch.empty_like(raw)
+    out_len = torch.zeros(n, dtype=torch.int64, device=dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    steps = max(1, args.steps // 2)
+    tot = 0.0
+    for k in range(steps + 1):
+        work.copy_(raw)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        cover.CanonicalizeBatchDev(work, off, n, out_len, sptr)  # returns after the stream drained
+        if k:
+            tot += time.perf_counter() - t0
+    ms = tot / steps * 1e3
+    nin, nout = int(raw.numel()), int(out_len.sum().item())
+    ok = nout == int(c.off[-1])  # the raw batch canonicalizes back to the distinct PCs of each cover
+    alg = 4 * nin + 4 * nout + 8 * (n + 1) + 8 * n
+    res = {"workload": "config3's 1M covers as raw kcov output: %d PCs (random order, ~20%% repeated) -> %d"
+                       % (nin, nout),
+           "ms_per_batch": round(ms, 3), "covers_per_s": round(n / ms * 1e3, 1), "canonical_pcs_match": ok,
+           "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "algorithmic_bytes": int(alg)}}
+    if args.cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        ns = min(n, 20_000)
+        rh = raw[: int(off[ns].item())].cpu().numpy().view(np.uint32)
+        oh = off[: ns + 1].cpu().numpy()
+        t0 = time.perf_counter()
+        for i in range(ns):
+            oracle.canonicalize(rh[oh[i]:oh[i + 1]])
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(ns / el, 1), "unit": "covers/s", "cores": 1, "kind": "port",
+                               "sample": "first %d raw covers; oracle.canonicalize per cover (Go's sort + unique), "
+                                         "%.2f s" % (ns, el)}
+    return res
+
+
+def setops_leg(args, dev, L, read_prof=None):
     """The cover set algebra in batch (cover/cover.go:42-102; triage users fuzzer.go:374-375,
     389-406): 1M pairs (config 3's fresh covers, each against a second run of the same input with 5 %
     of its PCs missing), device-resident; one launch sequence per op over all pairs
@@ -883,8 +971,17 @@ def setops_leg(args, dev, L):
             tot = cover.SetOpBatchDev(op, da, dao, na, db, dbo, nb, n, out, cap, ooff, sptr)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / steps * 1e3
+        kms = None
+        if read_prof is not None:  # the count and emit passes alone (HIP events around each)
+            L.syzgpu_profile_only(None)
+            L.syzgpu_profile_enable(1)
+            cover.SetOpBatchDev(op, da, dao, na, db, dbo, nb, n, out, cap, ooff, sptr)
+            torch.cuda.synchronize()
+            kms = {k: round(v["ms"], 3) for k, v in read_prof().items()}
+            L.syzgpu_profile_enable(0)
         alg = 4 * (na + nb) + 16 * (n + 1) + 4 * tot + 8 * (n + 1)
         res["ops"][op] = {"ms_per_batch": round(ms, 3), "out_pcs": int(tot), "pairs_per_s": round(n / ms * 1e3, 1),
+                          "kernels_ms": kms,
                           "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
                                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                        "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -900,6 +997,71 @@ def novelty_leg_sharded(args, dev, L, dist, rank, world):
     kept); a step = syzgpu_novelty_batch_dev on the slice, the per-call "updated" flags, and one RCCL
     MAX all-reduce of n + G bytes (is_new + updated). The updated tables stay sharded (each rank's
     range is all the next batch needs). Strong scaling: the batch is fixed."""
+    import torch
+    from syzkaller_amd import cover, sharding, synth
+
+    def any_failed(bad):
+        # every rank reaches this collective whatever failed locally, so a failure on one rank is
+        # reported by all of them instead of leaving the others blocked in a later collective
+        f = torch.tensor([1 if bad else 0], dtype=torch.int32, device=dev)
+        sharding.allreduce(f, dist, dist.ReduceOp.MAX)
+        return int(f.item()) != 0
+
+    try:
+        prep = _novelty_shard_prepare(args, dev, rank, world)
+        err = None
+    except Exception as e:  # noqa: BLE001
+        prep, err = None, "%s: %s" % (type(e).__name__, e)
+    if any_failed(err is not None):
+        return {"error": err or "another rank failed preparing its slice"}
+    b, G, mco, flakes, p_r, o_r, m_r, mo_r, f_r, d_f, d_grp = prep
+    g64 = d_grp.to(torch.int64)
+    nl, nm = int(o_r[-1].item()), int(mo_r[-1].item())
+    cap = nm + nl + 1
+    flags = torch.zeros(b.n + G, dtype=torch.uint8, device=dev)
+    is_new = flags[: b.n]
+    out = torch.empty(cap, dtype=torch.int32, device=dev)
+    ooff = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        ok = True
+        try:
+            cover.NoveltyBatchDev(p_r, o_r, d_grp, b.n, G, m_r, mo_r, nm, d_f, f_r.size, nl, is_new, out, cap, ooff,
+                                  sptr)
+            flags[b.n:].zero_()
+            flags[b.n:].scatter_reduce_(0, g64, is_new, "amax")
+        except Exception:  # noqa: BLE001
+            ok = False
+        sharding.allreduce_max_u8(flags, dist)  # reached on every rank
+        return ok
+    if any_failed(not step()):
+        return {"error": "the sharded novelty step failed on some rank"}
+    torch.cuda.synchronize()
+    steps = max(1, args.steps // 2)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    sharding.allreduce(el, dist, dist.ReduceOp.MAX)
+    el = float(el.item())
+    new = int(is_new.sum().item())
+    tab = torch.tensor([int(ooff[-1].item())], dtype=torch.int64, device=dev)
+    sharding.allreduce(tab, dist)
+    return {"workload": "config3: 1M fresh covers (%d PCs) vs maxCover0 of a 100k corpus (%d PCs), %d flakes; "
+                        "sharded by PC range over %d ranks" % (int(b.off[-1]), int(mco[-1]), flakes.size, world),
+            "metric": "triage covers/sec", "value": round(b.n * steps / el, 1), "ms_per_batch": round(el / steps * 1e3, 3),
+            "scaling": "strong", "new_covers": new, "maxcover_out_pcs": int(tab.item()),
+            "rank0_slice_pcs": nl, "exchange_bytes_per_batch": b.n + G,
+            "exchange": "one MAX all-reduce of n + G bytes (is_new + per-call updated); tables stay sharded"}
+
+
+def _novelty_shard_prepare(args, dev, rank, world):
+    """This rank's PC-range slice of the config-3 batch, tables and flakes, on the device (no collectives)."""
     import torch
     from syzkaller_amd import cover, sharding, synth
     G = args.ngroups
@@ -928,43 +1090,7 @@ def novelty_leg_sharded(args, dev, L, dist, rank, world):
     m_r, mo_r = dslice(t(mcp), t(mco))
     f_r = flakes[(flakes >= lo) & (flakes <= hi)]
     d_f, d_grp = t(f_r), t(b.group)
-    g64 = d_grp.to(torch.int64)
-    nl, nm = int(o_r[-1].item()), int(mo_r[-1].item())
-    cap = nm + nl + 1
-    flags = torch.zeros(b.n + G, dtype=torch.uint8, device=dev)
-    is_new = flags[: b.n]
-    out = torch.empty(cap, dtype=torch.int32, device=dev)
-    ooff = torch.zeros(G + 1, dtype=torch.int64, device=dev)
-    sptr = torch.cuda.current_stream(dev).cuda_stream
-
-    def step():
-        cover.NoveltyBatchDev(p_r, o_r, d_grp, b.n, G, m_r, mo_r, nm, d_f, f_r.size, nl, is_new, out, cap, ooff,
-                              sptr)
-        flags[b.n:].zero_()
-        flags[b.n:].scatter_reduce_(0, g64, is_new, "amax")
-        sharding.allreduce_max_u8(flags, dist)
-    step()
-    torch.cuda.synchronize()
-    steps = max(1, args.steps // 2)
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    sharding.allreduce(el, dist, dist.ReduceOp.MAX)
-    el = float(el.item())
-    new = int(is_new.sum().item())
-    tab = torch.tensor([int(ooff[-1].item())], dtype=torch.int64, device=dev)
-    sharding.allreduce(tab, dist)
-    return {"workload": "config3: 1M fresh covers (%d PCs) vs maxCover0 of a 100k corpus (%d PCs), %d flakes; "
-                        "sharded by PC range over %d ranks" % (int(b.off[-1]), int(mco[-1]), flakes.size, world),
-            "metric": "triage covers/sec", "value": round(b.n * steps / el, 1), "ms_per_batch": round(el / steps * 1e3, 3),
-            "scaling": "strong", "new_covers": new, "maxcover_out_pcs": int(tab.item()),
-            "rank0_slice_pcs": nl, "exchange_bytes_per_batch": b.n + G,
-            "exchange": "one MAX all-reduce of n + G bytes (is_new + per-call updated); tables stay sharded"}
+    return b, G, mco, flakes, p_r, o_r, m_r, mo_r, f_r, d_f, d_grp
 
 
 def cpu_baseline(corp, uses, n_sample):

@@ -79,6 +79,10 @@ int syzgpu_minimize_order(const uint64_t* lens, const uint64_t* group_off, uint3
 /* ---- batched forms (one launch for many covers / pairs) ------------------------------------- */
 /* Canonicalize every cover of a CSR in place; out_len[i] = new length of cover i. */
 int syzgpu_canonicalize_batch(uint32_t* pcs, const uint64_t* off, size_t ncov, uint64_t* out_len);
+/* The same on a device-resident CSR (pcs, off, out_len device pointers; off[0] = 0), on `stream`; returns
+ * after the stream has drained. The batch caller: the fuzzer's per-execution covers
+ * (syz-fuzzer/fuzzer.go:355, cover.Canonicalize per call of every executed program). */
+int syzgpu_canonicalize_batch_dev(uint32_t* pcs, const uint64_t* off, size_t ncov, uint64_t* out_len, void* stream);
 
 /* op(a_i, b_i) for npairs pairs of CSR covers. out_off[npairs+1] is written; out must hold
  * out_cap PCs (sum of the per-op capacities above suffices). */

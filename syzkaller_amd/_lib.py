@@ -31,6 +31,7 @@ SIGNATURES = {
     "syzgpu_minimize": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
     "syzgpu_minimize_order": (_c.c_int, [_vp, _vp, _c.c_uint32, _vp]),
     "syzgpu_canonicalize_batch": (_c.c_int, [_vp, _vp, _sz, _vp]),
+    "syzgpu_canonicalize_batch_dev": (_c.c_int, [_vp, _vp, _sz, _vp, _vp]),
     "syzgpu_setop_batch": (_c.c_int, [_c.c_int, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp]),
     "syzgpu_setop_batch_dev": (_c.c_int, [_c.c_int, _vp, _vp, _c.c_uint64, _vp, _vp, _c.c_uint64, _sz, _vp, _sz, _vp,
                                           _vp, _vp]),

@@ -227,6 +227,12 @@ def CanonicalizeBatch(pcs, off):
     return lens[:n]
 
 
+def CanonicalizeBatchDev(pcs, off, ncov, out_len, stream=None):
+    """Canonicalize every cover of a device-resident CSR in place (torch tensors or device pointers);
+    out_len (device, u64[ncov]) receives the new lengths."""
+    check(lib().syzgpu_canonicalize_batch_dev(ptr(pcs), ptr(off), ncov, ptr(out_len), stream))
+
+
 def NoveltyBatch(pcs, off, group, ngroups, maxcover_pcs, maxcover_off, flakes):
     """fuzzer.go:446-470 over a batch: returns (is_new u8[n], new maxCover CSR pcs, offsets)."""
     pcs, off, group = _u32(pcs), np.ascontiguousarray(off, dtype=np.uint64), _u32(group)

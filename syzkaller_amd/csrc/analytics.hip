@@ -179,7 +179,7 @@ __global__ __launch_bounds__(CS_BLOCK) void k_cs_runs(const uint32_t* __restrict
             atomicAdd(&ghist[g], 1u);
           else
             atomicAdd((unsigned long long*)&call_unique[g], 1ull);
-          if (one_input) atomicAdd(&input_unique[members[u]], 1u);
+          if (one_input) atomicAdd(&input_unique[u], 1u);  // (the index's vectors name entries)
         }
       }
     }
@@ -279,7 +279,7 @@ static CoverStats& corpus_analyze(Corpus& K, hipStream_t s) {
       ProfScope ps("cs_runs", s, T * 9);
       const size_t lds = K.G <= CS_LDS_G ? (size_t)K.G * 4 : 0;
       // few blocks: each flushes G call counts and 3 totals with atomics (same-address atomics serialize)
-      k_cs_runs<<<grid_for(T, CS_BLOCK, 512), CS_BLOCK, lds, s>>>(S.skeys, S.svals, T, S.uq.p, K.members.p,
+      k_cs_runs<<<grid_for(T, CS_BLOCK, 512), CS_BLOCK, lds, s>>>(S.skeys, S.svals, T, S.uq.p, nullptr,
                                                                   K.gdict.p, K.G, S.sflag.p, S.tot.p, S.sentg.p,
                                                                   S.call_unique.p, S.input_unique.p);
       SYZ_LAUNCHED();
@@ -297,7 +297,7 @@ __global__ void k_cs_percall(const uint64_t* gstart, const uint64_t* gdict, cons
   }
 }
 
-// input_unique in entry order: the per-member counts were added at members[m] already
+// input_unique in entry order: the counts were added per entry already
 __global__ void k_cs_totals(const uint64_t* tot, uint64_t* totals) {
   if (threadIdx.x == 0) {
     totals[0] = tot[0];

@@ -84,7 +84,7 @@ static void swap_grow(Grow<T>& a, Grow<T>& b) {
 }
 
 Corpus& corpus_index(CorpusHandle& H, hipStream_t s) {
-  if (H.index && H.index->keep_pending) {
+  if (H.index && (H.index->keep_pending || H.index->part_stale)) {
     try {
       corpus_index_sync(*H.index, H, s);
     } catch (...) {

@@ -7,11 +7,14 @@
 //           sorted and cut at the id windows. Their vectors join the stream's TAIL (everything
 //           appended since the last relayout, itself panel-major: each append rebuilds only the
 //           tail), and each panel's tail range is walked by the workgroup of the panel's last work
-//           item after its body range (VecWork tbeg/tend): no extra items, no extra merges. The
-//           group partition is redone and every vector's member renumbered.
+//           item after its body range (VecWork tbeg/tend): no extra items, no extra merges. A vector
+//           names its ENTRY (appends never renumber entries), the unseen keys join a small sorted
+//           DELTA dictionary (merged into the main one only when it grows past a fraction of it), and
+//           the group partition and work list are redone lazily by the next user (a minimize): an
+//           append costs O(its covers + delta + tail), not O(index).
 //   keep    recorded, and applied by the next user of the index (an append, a minimize): one
 //           relayout of the whole stream, panel-major again with the tails folded in, dropping the
-//           vectors of dropped entries (flags, a scan, one copy) and renumbering the members; the
+//           vectors of dropped entries (flags, a scan, one copy) and renumbering the entries; the
 //           work items are cut afresh as a build cuts them.
 //
 // The dictionary's id -> PC table (dict/gdict) is not extended: the cover analytics rebuild the
@@ -57,7 +60,8 @@ __global__ void k_sd_init(const uint32_t* dict, const uint64_t* gdict, uint32_t 
 // one wave per new entry: each PC's id from the sorted dictionary, or a miss
 __global__ __launch_bounds__(256) void k_ci_lookup(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                                                    size_t e0, size_t m, const uint64_t* sd_key,
-                                                   const uint32_t* sd_id, uint64_t sd_n, uint64_t pbase,
+                                                   const uint32_t* sd_id, uint64_t sd_n, const uint64_t* dl_key,
+                                                   const uint32_t* dl_id, uint64_t dl_n, uint64_t pbase,
                                                    uint32_t* ids, uint32_t* miss) {
   const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
   for (size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < m; t += waves) {
@@ -66,8 +70,14 @@ __global__ __launch_bounds__(256) void k_ci_lookup(const uint32_t* pcs, const ui
     for (uint64_t p = off[e] + __lane_id(); p < off[e + 1]; p += 64) {
       const uint64_t key = (g << 32) | pcs[p];
       const uint64_t x = lower_bound_dev<uint64_t>(sd_key, 0, sd_n, key);
-      const bool hit = x < sd_n && sd_key[x] == key;
-      ids[p - pbase] = hit ? sd_id[x] : NONE32;
+      bool hit = x < sd_n && sd_key[x] == key;
+      uint32_t id = hit ? sd_id[x] : NONE32;
+      if (!hit && dl_n) {  // the keys appended since the last merge
+        const uint64_t y = lower_bound_dev<uint64_t>(dl_key, 0, dl_n, key);
+        hit = y < dl_n && dl_key[y] == key;
+        if (hit) id = dl_id[y];
+      }
+      ids[p - pbase] = id;
       miss[p - pbase] = hit ? 0u : 1u;
     }
   }
@@ -134,6 +144,24 @@ __global__ void k_ci_merge(const uint64_t* a, const uint32_t* aid, uint64_t na, 
   }
 }
 
+// merge of two sorted (key, id) lists that share no key
+__global__ void k_ci_merge2(const uint64_t* a, const uint32_t* aid, uint64_t na, const uint64_t* b,
+                            const uint32_t* bid, uint64_t nb, uint64_t* out, uint32_t* oid) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    if (i < na) {
+      const uint64_t q = i + lower_bound_dev<uint64_t>(b, 0, nb, a[i]);
+      out[q] = a[i];
+      oid[q] = aid[i];
+    } else {
+      const uint64_t j = i - na;
+      const uint64_t q = j + lower_bound_dev<uint64_t>(a, 0, na, b[j]);
+      out[q] = b[j];
+      oid[q] = bid[j];
+    }
+  }
+}
+
 // ubeg[g] = first new key of call g
 __global__ void k_ci_ubeg(const uint64_t* u, uint64_t nu, uint32_t G, uint64_t* ubeg) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x)
@@ -145,29 +173,22 @@ __global__ void k_ci_reloff(const uint64_t* off, size_t e0, size_t m, uint64_t* 
     rel[i] = off[e0 + i] - off[e0];
 }
 
-// old vectors: member index of the old partition -> of the new one (through the entry)
-__global__ void k_ci_remap(uint32_t* vmem, uint64_t nv, const uint32_t* mem_old, const uint32_t* mof_new) {
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * blockDim.x)
-    vmem[v] = mof_new[mem_old[vmem[v]]];
-}
-
 struct Slice {  // one new cover's ids in one window -> vectors [vout, vout + ceil(len / VEC))
   uint32_t e, w, s0, len;
   uint64_t vout;
 };
 
-// one wave per slice: window-relative u16 ids (padded with the last id) and the member per vector
+// one wave per slice: window-relative u16 ids (padded with the last id) and the entry per vector
 __global__ __launch_bounds__(256) void k_ci_vfill(const Slice* sl, size_t ns, const uint32_t* ids,
-                                                  const uint64_t* rel, size_t e0, const uint32_t* mof_new,
-                                                  uint16_t* ids16, uint32_t* vmem) {
+                                                  const uint64_t* rel, size_t e0, uint16_t* ids16, uint32_t* vmem) {
   const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
   for (size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < ns; t += waves) {
     const Slice x = sl[t];
     const uint32_t* src = ids + rel[x.e] + x.s0;
     const uint32_t padded = (x.len + VEC - 1) / VEC * VEC, wb = x.w << WIN_BITS;
     for (uint32_t k = __lane_id(); k < padded; k += 64) ids16[x.vout * VEC + k] = (uint16_t)(src[min(k, x.len - 1)] - wb);
-    const uint32_t m = mof_new[e0 + x.e];
-    for (uint32_t k = __lane_id(); k < padded / VEC; k += 64) vmem[x.vout + k] = m;
+    const uint32_t e = (uint32_t)(e0 + x.e);
+    for (uint32_t k = __lane_id(); k < padded / VEC; k += 64) vmem[x.vout + k] = e;
   }
 }
 
@@ -183,22 +204,9 @@ __global__ void k_ci_invcheck(const int64_t* idx, size_t m, const uint32_t* inv,
     if (inv[idx[t]] != (uint32_t)t) atomicOr(bad, 1u);
 }
 
-__global__ void k_ci_vflag(const uint32_t* vmem, uint64_t nv, const uint32_t* mem_old, const uint32_t* inv,
-                           uint32_t* f) {
+__global__ void k_ci_vflag(const uint32_t* vmem, uint64_t nv, const uint32_t* inv, uint32_t* f) {
   for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * blockDim.x)
-    f[v] = inv[mem_old[vmem[v]]] != NONE32 ? 1u : 0u;
-}
-
-__global__ void k_ci_vcompact(const uint4* ids16, const uint32_t* vmem, uint64_t nv, const uint32_t* mem_old,
-                              const uint32_t* inv, const uint32_t* mof_new, const uint64_t* pos, uint4* ids16b,
-                              uint32_t* vmemb) {
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t e = inv[mem_old[vmem[v]]];
-    if (e == NONE32) continue;
-    const uint64_t q = pos[v];
-    ids16b[q] = ids16[v];
-    vmemb[q] = mof_new[e];
-  }
+    f[v] = inv[vmem[v]] != NONE32 ? 1u : 0u;
 }
 
 __global__ void k_ci_gather(const uint64_t* pos, const uint64_t* at, size_t n, uint64_t* out) {
@@ -266,17 +274,17 @@ __global__ __launch_bounds__(256) void k_ci_copy(const VCopy* cp, size_t nc, con
 }
 
 // relayout: vector v of segment j (segments sorted by start) goes to segbase[j] + its rank among the
-// segment's kept vectors; kept = its entry survives (inv), member renumbered
+// segment's kept vectors; kept = its entry survives (inv), entry renumbered
 __global__ void k_ci_relayout(const uint4* ids16, const uint32_t* vmem, uint64_t nv, const uint64_t* segstart,
-                              uint32_t nseg, const uint64_t* segbase, const uint64_t* pos, const uint32_t* mem_old,
-                              const uint32_t* inv, const uint32_t* mof_new, uint4* ids16b, uint32_t* vmemb) {
+                              uint32_t nseg, const uint64_t* segbase, const uint64_t* pos, const uint32_t* inv,
+                              uint4* ids16b, uint32_t* vmemb) {
   for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t e = inv[mem_old[vmem[v]]];
+    const uint32_t e = inv[vmem[v]];
     if (e == NONE32) continue;
     const uint32_t j = (uint32_t)upper_bound_dev<uint64_t>(segstart, 0, nseg, v) - 1;
     const uint64_t q = segbase[j] + (pos[v] - pos[segstart[j]]);
     ids16b[q] = ids16[v];
-    vmemb[q] = mof_new[e];
+    vmemb[q] = e;
   }
 }
 
@@ -329,8 +337,6 @@ void apply_keep(Corpus& K, const CorpusHandle& H, hipStream_t s) {
     k_ci_invcheck<<<grid_for(m, 256, 4096), 256, 0, s>>>(idx, m, inv, bad);
     SYZ_LAUNCHED();
   }
-  uint32_t* mem_old = sc.get<uint32_t>("ci_memold", n0 + 1);
-  if (n0) SYZ_HIP(hipMemcpyAsync(mem_old, K.members.p, n0 * 4, hipMemcpyDeviceToDevice, s));
   // segments of the stream: body items and tails, each with its panel
   struct Seg {
     uint64_t a, b;
@@ -346,7 +352,7 @@ void apply_keep(Corpus& K, const CorpusHandle& H, hipStream_t s) {
   uint32_t* f = sc.get<uint32_t>("ci_vflag", nv + 1);
   uint64_t* pos = sc.get<uint64_t>("ci_vpos", nv + 1);
   if (nv) {
-    k_ci_vflag<<<grid_for(nv, 256, 16384), 256, 0, s>>>(K.vmem.p, nv, mem_old, inv, f);
+    k_ci_vflag<<<grid_for(nv, 256, 16384), 256, 0, s>>>(K.vmem.p, nv, inv, f);
     SYZ_LAUNCHED();
   }
   exclusive_scan_u32(f, pos, nv, s);
@@ -413,9 +419,8 @@ void apply_keep(Corpus& K, const CorpusHandle& H, hipStream_t s) {
     SYZ_HIP(hipMemcpyAsync(dss, segstart.data(), seg.size() * 8, hipMemcpyHostToDevice, s));
     SYZ_HIP(hipMemcpyAsync(dsb, segbase.data(), seg.size() * 8, hipMemcpyHostToDevice, s));
     k_ci_relayout<<<grid_for(nv, 256, 16384), 256, 0, s>>>(reinterpret_cast<const uint4*>(K.ids16.p), K.vmem.p, nv,
-                                                          dss, (uint32_t)seg.size(), dsb, pos, mem_old, inv,
-                                                          K.member_of.p, reinterpret_cast<uint4*>(K.ids16b.p),
-                                                          K.vmemb.p);
+                                                          dss, (uint32_t)seg.size(), dsb, pos, inv,
+                                                          reinterpret_cast<uint4*>(K.ids16b.p), K.vmemb.p);
     SYZ_LAUNCHED();
   }
   std::swap(K.ids16.p, K.ids16b.p);
@@ -431,13 +436,40 @@ void apply_keep(Corpus& K, const CorpusHandle& H, hipStream_t s) {
   K.gtdone.ensure(K.ngtabs + 1);
   compose_work(K, s);
   K.keep_pending = false;
+  K.part_stale = false;
   pt.mark("relayout_work", s);
+}
+
+// the keys of the delta dictionary folded into the main one (when the delta has grown)
+void merge_delta(Corpus& K, hipStream_t s) {
+  if (!K.dl_n) return;
+  Scratch& sc = ctx().scratch;
+  const uint64_t nt = K.sd_n + K.dl_n;
+  uint64_t* k2 = sc.get<uint64_t>("ci_sdk2", nt + 1);
+  uint32_t* i2 = sc.get<uint32_t>("ci_sdi2", nt + 1);
+  k_ci_merge2<<<grid_for(nt, 256, 16384), 256, 0, s>>>(K.sd_key.p, K.sd_id.p, K.sd_n, K.dl_key.p, K.dl_id.p, K.dl_n,
+                                                        k2, i2);
+  SYZ_LAUNCHED();
+  dev_grow_keep(K.sd_key, 0, nt + 1, s);
+  dev_grow_keep(K.sd_id, 0, nt + 1, s);
+  SYZ_HIP(hipMemcpyAsync(K.sd_key.p, k2, nt * 8, hipMemcpyDeviceToDevice, s));
+  SYZ_HIP(hipMemcpyAsync(K.sd_id.p, i2, nt * 4, hipMemcpyDeviceToDevice, s));
+  K.sd_n = nt;
+  K.dl_n = 0;
 }
 
 }  // namespace
 
 void corpus_index_sync(Corpus& K, const CorpusHandle& H, hipStream_t s) {
-  if (K.keep_pending) apply_keep(K, H, s);
+  if (K.keep_pending) apply_keep(K, H, s);  // (partitions and composes the work itself)
+  if (K.part_stale) {  // appends since the last partition: the group partition and the work list
+    PhaseTimer pt("index_sync");
+    std::vector<uint64_t> hpcs;
+    corpus_partition(K, hpcs, s);
+    compose_work(K, s);
+    K.part_stale = false;
+    pt.mark("partition_work", s);
+  }
 }
 
 // H has just taken m = H.n - n0 new entries (their PCs from L0). Brings K up to H's covers.
@@ -462,7 +494,8 @@ void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L
   uint64_t* mpos = sc.get<uint64_t>("ci_mpos", Lm + 1);
   const unsigned wgrid = (unsigned)std::min<size_t>((m * 64 + 255) / 256 + 1, 65536);
   if (m) {
-    k_ci_lookup<<<wgrid, 256, 0, s>>>(H.pcs.p, off, H.group.p, n0, m, K.sd_key.p, K.sd_id.p, K.sd_n, L0, ids, miss);
+    k_ci_lookup<<<wgrid, 256, 0, s>>>(H.pcs.p, off, H.group.p, n0, m, K.sd_key.p, K.sd_id.p, K.sd_n, K.dl_key.p,
+                                      K.dl_id.p, K.dl_n, L0, ids, miss);
     SYZ_LAUNCHED();
   }
   exclusive_scan_u32(miss, mpos, Lm, s);
@@ -506,17 +539,19 @@ void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L
     SYZ_LAUNCHED();
     k_ci_missid<<<wgrid, 256, 0, s>>>(H.pcs.p, off, H.group.p, n0, m, L0, u, nu, ubeg, d_nids0, ids);
     SYZ_LAUNCHED();
-    // the dictionary takes the new keys (merged, still sorted)
-    const uint64_t nt = K.sd_n + nu;
-    uint64_t* k2 = sc.get<uint64_t>("ci_sdk2", nt + 1);
-    uint32_t* i2 = sc.get<uint32_t>("ci_sdi2", nt + 1);
-    k_ci_merge<<<grid_for(nt, 256, 16384), 256, 0, s>>>(K.sd_key.p, K.sd_id.p, K.sd_n, u, nu, ubeg, d_nids0, k2, i2);
+    // the DELTA dictionary takes the new keys (merged, still sorted: O(delta + new), not O(dictionary));
+    // it is folded into the main one once it outgrows a fraction of it
+    const uint64_t nt = K.dl_n + nu;
+    uint64_t* k2 = sc.get<uint64_t>("ci_dlk2", nt + 1);
+    uint32_t* i2 = sc.get<uint32_t>("ci_dli2", nt + 1);
+    k_ci_merge<<<grid_for(nt, 256, 16384), 256, 0, s>>>(K.dl_key.p, K.dl_id.p, K.dl_n, u, nu, ubeg, d_nids0, k2, i2);
     SYZ_LAUNCHED();
-    dev_grow_keep(K.sd_key, 0, nt + 1, s);
-    dev_grow_keep(K.sd_id, 0, nt + 1, s);
-    SYZ_HIP(hipMemcpyAsync(K.sd_key.p, k2, nt * 8, hipMemcpyDeviceToDevice, s));
-    SYZ_HIP(hipMemcpyAsync(K.sd_id.p, i2, nt * 4, hipMemcpyDeviceToDevice, s));
-    K.sd_n = nt;
+    dev_grow_keep(K.dl_key, 0, nt + 1, s);
+    dev_grow_keep(K.dl_id, 0, nt + 1, s);
+    SYZ_HIP(hipMemcpyAsync(K.dl_key.p, k2, nt * 8, hipMemcpyDeviceToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(K.dl_id.p, i2, nt * 4, hipMemcpyDeviceToDevice, s));
+    K.dl_n = nt;
+    if (K.dl_n > std::max<uint64_t>(1ull << 20, K.sd_n / 8)) merge_delta(K, s);
     uint64_t* hu = ctx().pinned.get<uint64_t>(nu + 1);
     SYZ_HIP(hipMemcpyAsync(hu, u, nu * 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
@@ -543,21 +578,14 @@ void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L
     SYZ_HIP(hipMemcpyAsync(hclen.data(), clen, m * 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipMemcpyAsync(hsp.data(), splits, hsb[m] * 4, hipMemcpyDeviceToHost, s));
   }
-  // 3. the group partition of all entries; every vector's member renumbered
-  const size_t nold = K.n;
-  uint32_t* mem_old = sc.get<uint32_t>("ci_memold", nold + 1);
-  if (nold) SYZ_HIP(hipMemcpyAsync(mem_old, K.members.p, nold * 4, hipMemcpyDeviceToDevice, s));
+  // 3. the entries taken; the group partition (and the work list) are redone by the next user: the
+  // old vectors keep their entry ids
   take_entries(K, H, s);
-  std::vector<uint64_t> hpcs;
-  corpus_partition(K, hpcs, s);  // (drains the stream: hclen / hsp are in)
+  SYZ_HIP(hipStreamSynchronize(s));  // hclen / hsp are in
   for (size_t e = 0; e < m; e++)
     if (hclen[e] != hrel[e + 1] - hrel[e]) fail(SYZGPU_EINVAL, "corpus index needs canonical covers");
-  pt.mark("canon_splits_partition", s);
+  pt.mark("canon_splits", s);
   const uint64_t nv0 = K.total_vecs;
-  if (nv0) {
-    k_ci_remap<<<grid_for(nv0, 256, 16384), 256, 0, s>>>(K.vmem.p, nv0, mem_old, K.member_of.p);
-    SYZ_LAUNCHED();
-  }
   // 4. the tail rebuilt panel-major: per panel its old tail range, then its new slices
   std::vector<Slice> hsl;
   for (size_t e = 0; e < m; e++) {
@@ -619,16 +647,14 @@ void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L
     Slice* dsl = sc.get<Slice>("ci_slices", hsl.size());
     SYZ_HIP(hipMemcpyAsync(dsl, hsl.data(), hsl.size() * sizeof(Slice), hipMemcpyHostToDevice, s));
     k_ci_vfill<<<(unsigned)std::min<size_t>((hsl.size() * 64 + 255) / 256, 65536), 256, 0, s>>>(
-        dsl, hsl.size(), ids, rel, n0, K.member_of.p, K.ids16.p, K.vmem.p);
+        dsl, hsl.size(), ids, rel, n0, K.ids16.p, K.vmem.p);
     SYZ_LAUNCHED();
   }
   (void)ntail;
   K.total_vecs = nv;
   K.ptail = nt;
+  K.part_stale = true;  // 5. the work list (body items + each panel's tail) with the next partition
   pt.mark("vectors", s);
-  // 5. the work list: body items + each panel's tail
-  compose_work(K, s);
-  pt.mark("work", s);
 }
 
 // H has just become the entries idx[0..m) (device, old ids) of a corpus of n0 entries: recorded, and

@@ -145,6 +145,18 @@ __global__ void k_ranks_ranges(const uint64_t* el, const uint32_t* perm, const u
   }
 }
 
+// the same with the rank stored per ENTRY (the corpus index: its id vectors name entries, which
+// appends never renumber)
+__global__ void k_ranks_ranges_ent(const uint64_t* el, const uint32_t* perm, const uint4* ranges,
+                                   const uint32_t* members, uint32_t* rank_of_entry, uint32_t* ent_of_rank) {
+  const uint4 rg = ranges[blockIdx.y];
+  for (uint32_t r = rg.x + blockIdx.x * blockDim.x + threadIdx.x; r < rg.y; r += gridDim.x * blockDim.x) {
+    const uint32_t e = members[(uint32_t)el[perm[r]]];
+    rank_of_entry[e] = r;
+    ent_of_rank[r] = e;
+  }
+}
+
 // ---- 3. bucket passes ------------------------------------------------------------------------------
 struct Chunk {
   uint32_t g, mbeg, mend, pad;
@@ -201,8 +213,7 @@ __device__ __forceinline__ uint32_t hslot(uint32_t pc) { return (pc * 0x9E3779B1
 // ---- 5. selection outputs ------------------------------------------------------------------------
 // Store path: kept flags in ENTRY order (coalesced stores; the rank-ordered form walks a permutation)
 // and the len(p.Calls) histogram of kept programs of the groups this rank counts (count_hist[g]).
-__global__ __launch_bounds__(256) void k_select_store(const uint32_t* sel_bits, const uint32_t* member_of,
-                                                      const uint32_t* rank_of_member, size_t n,
+__global__ __launch_bounds__(256) void k_select_store(const uint32_t* sel_bits, const uint32_t* rank_of_entry, size_t n,
                                                       const uint16_t* prog_len, const uint32_t* group,
                                                       const uint8_t* count_hist, int32_t C, uint8_t* selected,
                                                       int64_t* hist, int* err) {
@@ -212,16 +223,14 @@ __global__ __launch_bounds__(256) void k_select_store(const uint32_t* sel_bits, 
     for (int32_t i = threadIdx.x; i <= C; i += blockDim.x) lh[i] = 0;
     __syncthreads();
   }
-  // SS_U entries per thread at once: the dependent gathers (member -> rank -> winner bit) of all of
-  // them are in flight together instead of one chain per grid-stride step
+  // SS_U entries per thread at once: the dependent gathers (rank -> winner bit) of all of them are in
+  // flight together instead of one chain per grid-stride step
   constexpr int SS_U = 8;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t e0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e0 < n; e0 += stride * SS_U) {
     uint32_t r[SS_U], b[SS_U];
 #pragma unroll
-    for (int k = 0; k < SS_U; k++) r[k] = e0 + k * stride < n ? member_of[e0 + k * stride] : 0;
-#pragma unroll
-    for (int k = 0; k < SS_U; k++) r[k] = e0 + k * stride < n ? rank_of_member[r[k]] : 0;
+    for (int k = 0; k < SS_U; k++) r[k] = e0 + k * stride < n ? rank_of_entry[e0 + k * stride] : 0;
 #pragma unroll
     for (int k = 0; k < SS_U; k++) b[k] = e0 + k * stride < n ? sel_bits[r[k] >> 5] : 0;
 #pragma unroll
@@ -666,9 +675,10 @@ template <bool SIDE>
 __global__ __launch_bounds__(VM_BLOCK) void k_vec_min(const VecWork* __restrict__ work, uint32_t nitems,
                                                       const uint4* __restrict__ ids16,
                                                       const uint32_t* __restrict__ vmem,
-                                                      const uint32_t* __restrict__ rank_of_member,
+                                                      const uint32_t* __restrict__ rank_of_entry,
                                                       const uint64_t* __restrict__ gstart, uint32_t* sel_bits,
                                                       uint32_t* gtabs, const uint32_t* gtchunks, uint32_t* gtdone) {
+  const uint32_t* __restrict__ rank_of_member = rank_of_entry;  // vmem names entries
   __shared__ uint32_t tab[WIN];
   __shared__ uint32_t bm[BM_WORDS];
   __shared__ uint32_t last;
@@ -785,7 +795,7 @@ __global__ __launch_bounds__(256) void k_vfill(const uint32_t* members, const ui
     const uint32_t wb = w << WIN_BITS;
     for (uint32_t k = lane; k < padded; k += 64)
       ids16[vo * VEC + k] = (uint16_t)(src[s0 + min(k, len - 1)] - wb);
-    for (uint32_t k = lane; k < padded / VEC; k += 64) vmem[vo + k] = (uint32_t)m;
+    for (uint32_t k = lane; k < padded / VEC; k += 64) vmem[vo + k] = e;  // the vector's entry
   }
 }
 
@@ -1192,7 +1202,7 @@ void corpus_minimize_begin(Corpus& K, hipStream_t s) {
   K.rom.ensure(n + 1);
   K.eor.ensure(n + 1);
   K.sel_bits.ensure(n / 32 + 2);
-  uint32_t* rank_of_member = K.rom.p;
+  uint32_t* rank_of_entry = K.rom.p;  // (the index's vectors name entries)
   uint32_t* ent_of_rank = K.eor.p;
   SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
   uint32_t* sel_bits = K.sel_bits.p;
@@ -1220,14 +1230,14 @@ void corpus_minimize_begin(Corpus& K, hipStream_t s) {
     const unsigned grid = (unsigned)std::min<size_t>(count, side ? side_cus : (1u << 20));
     auto* k = side ? k_vec_min<true> : k_vec_min<false>;
     k<<<grid, VM_BLOCK, 0, q>>>(K.work.p + first, (uint32_t)count, reinterpret_cast<const uint4*>(K.ids16.p),
-                                K.vmem.p, rank_of_member, K.gstart.p, sel_bits, K.gtabs.p, K.gtchunks.p,
+                                K.vmem.p, rank_of_entry, K.gstart.p, sel_bits, K.gtabs.p, K.gtchunks.p,
                                 K.gtdone.p);
     SYZ_LAUNCHED();
   };
   auto small_done = [&](hipStream_t q) {
     if (P.npacks) {  // a pack holds at most GS_T_SEG elements
-      k_ranks_ranges<<<dim3(GS_T_SEG / 1024, P.npacks), 256, 0, q>>>(
-          el, perm, reinterpret_cast<const uint4*>(P.packs), K.members.p, rank_of_member, ent_of_rank);
+      k_ranks_ranges_ent<<<dim3(GS_T_SEG / 1024, P.npacks), 256, 0, q>>>(
+          el, perm, reinterpret_cast<const uint4*>(P.packs), K.members.p, rank_of_entry, ent_of_rank);
       SYZ_LAUNCHED();
     }
     ProfScope ps("vec_min_small", q, (K.total_pcs - K.big_pcs) * 4 + (n - K.big_entries) * 10);
@@ -1236,8 +1246,8 @@ void corpus_minimize_begin(Corpus& K, hipStream_t s) {
   auto big_done = [&](hipStream_t q) {
     if (P.nbig) {
       const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>(1, P.big_max / 2048), 256);
-      k_ranks_ranges<<<dim3(gx, P.nbig), 256, 0, q>>>(el, perm, reinterpret_cast<const uint4*>(P.big), K.members.p,
-                                                     rank_of_member, ent_of_rank);
+      k_ranks_ranges_ent<<<dim3(gx, P.nbig), 256, 0, q>>>(el, perm, reinterpret_cast<const uint4*>(P.big),
+                                                         K.members.p, rank_of_entry, ent_of_rank);
       SYZ_LAUNCHED();
     }
     // algorithmic bytes of this rank's share: the PCs of its key parts (in proportion to their id
@@ -1304,13 +1314,13 @@ void corpus_minimize_end(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
   const size_t n = K.n;
   int* err = sc.get<int>("mz_err", 2);
   if (!K.begun) fail(SYZGPU_EINVAL, "corpus: minimize_begin first");
-  uint32_t* rank_of_member = K.rom.p;
+  uint32_t* rank_of_entry = K.rom.p;
   uint32_t* sel_bits = K.sel_bits.p;
   if (len_hist) SYZ_HIP(hipMemsetAsync(len_hist, 0, (size_t)(C + 1) * 8, s));
   ProfScope ps("select_out", s, (uint64_t)n * 8);
   if (n) {
     k_select_store<<<grid_for(n, 256, 512), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
-        sel_bits, K.member_of.p, rank_of_member, n, len_hist ? K.prog_len.p : nullptr, K.group.p,
+        sel_bits, rank_of_entry, n, len_hist ? K.prog_len.p : nullptr, K.group.p,
         K.has_count_hist ? K.count_hist.p : nullptr, C, selected, len_hist, err);
     SYZ_LAUNCHED();
   }

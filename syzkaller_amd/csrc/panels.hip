@@ -311,7 +311,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #ifndef SYZ_SL_MU
 #define SYZ_SL_MU 4
 #endif
-__global__ __launch_bounds__(1024) void k_smin_direct(const PItem* items, const SGroup* sg, const uint32_t* gslab,
+#if SYZ_DS < 15
+#define SYZ_SMIN_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))  // 64 KB tables: two workgroups per CU
+#else
+#define SYZ_SMIN_OCC
+#endif
+__global__ __launch_bounds__(1024) SYZ_SMIN_OCC void k_smin_direct(const PItem* items, const SGroup* sg, const uint32_t* gslab,
                                                       const uint64_t* gebase, const uint32_t* D,
                                                       const PSlab* slabs, const uint32_t* __restrict__ elems,
                                                       const uint32_t* __restrict__ rank_of_member,

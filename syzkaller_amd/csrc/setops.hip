@@ -106,9 +106,254 @@ __global__ __launch_bounds__(256) void k_setop_scatter(int side, const uint32_t*
   }
 }
 
+// ---- merge-path tiles (strictly increasing lists, the kcov case) --------------------------------
+// For strictly increasing lists foreach's walk (cover.go:81-102) is the stable merge (a first on ties)
+// in which an element is PAIRED iff its merged neighbour holds the same value: a[i] with the b at the
+// walk's b pointer when a[i] is taken, b[j] with the a taken just before it. So every pair's merged
+// sequence is cut into tiles of SO_T merged elements at merge-path diagonals; a tile's two sub-lists
+// (+ one halo element each) are staged in LDS with coalesced loads, each thread merges SO_VT elements
+// from its own diagonal, and the pass either counts the op's outputs per tile (count) or, after a scan
+// of the counts, stages them in LDS and stores the tile's run coalesced (emit). A pair with a repeated
+// value (allowed by Go, never produced by the executor's sort + unique) sends the batch to the
+// per-element rank path above; a descending neighbour is the Go panic (EINVAL).
+constexpr int SO_BLOCK = 256;
+constexpr int SO_VT = 4;
+constexpr uint32_t SO_T = SO_BLOCK * SO_VT;  // merged elements per tile
+
+__global__ void k_so_ntiles(const uint64_t* aoff, const uint64_t* boff, uint32_t npairs, uint32_t* nt) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += gridDim.x * blockDim.x) {
+    const uint64_t m = (aoff[p + 1] - aoff[p]) + (boff[p + 1] - boff[p]);
+    nt[p] = (uint32_t)((m + SO_T - 1) / SO_T);
+  }
+}
+
+// tpair[t] = the pair of tile t
+__global__ void k_so_tpair(const uint64_t* tstart, uint32_t npairs, uint32_t* tpair) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += gridDim.x * blockDim.x)
+    for (uint64_t t = tstart[p]; t < tstart[p + 1]; t++) tpair[t] = p;
+}
+
+// merge path over global memory by one wave: 64 candidates per round (the predicate a[i] <= b[d-i-1]
+// is true, then false), so a range of 2^12 takes two rounds of dependent loads, not twelve
+__device__ __forceinline__ uint32_t merge_path_wave(const uint32_t* A, uint32_t la, const uint32_t* B, uint32_t lb,
+                                                    uint32_t d) {
+  uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;  // answer in [lo, hi]
+  const unsigned lane = __lane_id();
+  while (hi > lo) {
+    const uint32_t n = hi - lo;
+    const uint32_t step = (n + 63) / 64;
+    const uint32_t i = lo + lane * step;
+    const bool t = i < hi && A[i] <= B[d - i - 1];
+    const uint64_t bt = __ballot(t);
+    // the predicate holds on lanes [0, k): the answer is in (lo + (k - 1) step, lo + k step]
+    const uint32_t k = (uint32_t)__popcll(bt);
+    if (k == 0) {
+      hi = lo;
+    } else {
+      const uint32_t nlo = lo + (k - 1) * step + 1;
+      hi = min(hi, lo + k * step);
+      lo = nlo;
+    }
+  }
+  return lo;
+}
+
+// merge path: the number of a-elements among the first d merged ones (a first on ties)
+template <class RA, class RB>
+__device__ __forceinline__ uint32_t merge_path(RA A, uint32_t la, RB B, uint32_t lb, uint32_t d) {
+  uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (A(mid) <= B(d - mid - 1))
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// COUNT: tcnt[tile] = outputs of the tile; flags bit 0 = a repeated value, err = descending
+// EMIT: the tile's outputs at out[tout[tile]..]
+template <bool EMIT>
+__global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __restrict__ a,
+                                                      const uint64_t* __restrict__ aoff,
+                                                      const uint32_t* __restrict__ b,
+                                                      const uint64_t* __restrict__ boff, uint32_t npairs,
+                                                      const uint64_t* __restrict__ tstart,
+                                                      const uint32_t* __restrict__ tpair, uint32_t* tcnt,
+                                                      const uint64_t* __restrict__ tout, uint32_t* out,
+                                                      int* flags, int* err) {
+  __shared__ uint32_t As[SO_T + 2], Bs[SO_T + 2];  // As[0]: a before the tile; Bs[nb]: b after it
+  __shared__ uint32_t st[EMIT ? SO_T : 1];
+  __shared__ uint32_t red[SO_BLOCK / 64 + 1];
+  __shared__ uint32_t meta[6];
+  const uint64_t tile = blockIdx.x;
+  if (tile >= tstart[npairs]) return;
+  if (threadIdx.x < 64) {  // wave 0: the tile's diagonals (a one-tile pair needs no search)
+    const uint32_t p = tpair[tile];
+    const uint64_t a0 = aoff[p], b0 = boff[p];
+    const uint32_t la = (uint32_t)(aoff[p + 1] - a0), lb = (uint32_t)(boff[p + 1] - b0);
+    const uint32_t d0 = (uint32_t)(tile - tstart[p]) * SO_T, d1 = min(d0 + SO_T, la + lb);
+    const uint32_t* A = a + a0;
+    const uint32_t* B = b + b0;
+    const uint32_t i0 = d0 == 0 ? 0u : merge_path_wave(A, la, B, lb, d0);
+    const uint32_t i1 = d1 == la + lb ? la : merge_path_wave(A, la, B, lb, d1);
+    if (threadIdx.x == 0) {
+      meta[0] = p;
+      meta[1] = i0;
+      meta[2] = i1;
+      meta[3] = d0 - i0;  // j0
+      meta[4] = d1 - i1;  // j1
+      meta[5] = 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t p = meta[0], i0 = meta[1], i1 = meta[2], j0 = meta[3], j1 = meta[4];
+  const uint64_t a0 = aoff[p], b0 = boff[p];
+  const uint32_t la = (uint32_t)(aoff[p + 1] - a0), lb = (uint32_t)(boff[p + 1] - b0);
+  const uint32_t na = i1 - i0, nb = j1 - j0;
+  // halo: the a before the tile (none: a value no b equals... the walk's "previous a" does not exist,
+  // marked by NOPREV), the b after it (the pointer past the pair: NONEXT)
+  for (uint32_t k = threadIdx.x; k < na; k += SO_BLOCK) As[k + 1] = a[a0 + i0 + k];
+  for (uint32_t k = threadIdx.x; k < nb; k += SO_BLOCK) Bs[k] = b[b0 + j0 + k];
+  if (threadIdx.x == 0) As[0] = i0 > 0 ? a[a0 + i0 - 1] : 0u;
+  if (threadIdx.x == 1) Bs[nb] = j1 < lb ? b[b0 + j1] : 0u;
+  // one element past the tile's a run (the order check across tiles)
+  const uint32_t anext = i1 < la ? a[a0 + i1] : 0xFFFFFFFFu;
+  __syncthreads();
+  const bool hasprev = i0 > 0, hasnext = j1 < lb;
+  // order checks: strictly increasing inside the tile and against the next tile's first element
+  if (!EMIT) {
+    int f = 0, e = 0;
+    for (uint32_t k = threadIdx.x; k < na; k += SO_BLOCK) {
+      const uint32_t x = As[k + 1];
+      const uint32_t nx = k + 1 < na ? As[k + 2] : (i1 < la ? anext : 0xFFFFFFFFu);
+      if (k + 1 < na || i1 < la) {
+        if (nx < x) e = 1;
+        if (nx == x) f = 1;
+      }
+    }
+    for (uint32_t k = threadIdx.x; k < nb; k += SO_BLOCK) {
+      const uint32_t x = Bs[k];
+      if (k + 1 < nb || j1 < lb) {
+        const uint32_t nx = Bs[k + 1];  // (Bs[nb] is the halo)
+        if (nx < x) e = 1;
+        if (nx == x) f = 1;
+      }
+    }
+    if (f) atomicOr(flags, 1);
+    if (e) atomicOr(err, 1);
+  }
+  // this thread's merged range [t * VT, (t + 1) * VT) of the tile
+  const uint32_t dt0 = min((uint32_t)threadIdx.x * SO_VT, na + nb), dt1 = min(dt0 + SO_VT, na + nb);
+  auto la_ = [&](uint32_t i) { return As[i + 1]; };
+  auto lb_ = [&](uint32_t j) { return Bs[j]; };
+  uint32_t i = merge_path(la_, na, lb_, nb, dt0), j = dt0 - i;
+  uint32_t outv[SO_VT];
+  uint32_t c = 0;
+  for (uint32_t d = dt0; d < dt1; d++) {
+    const bool take_a = j >= nb || (i < na && As[i + 1] <= Bs[j]);
+    uint32_t v;
+    bool paired, isa;
+    if (take_a) {
+      v = As[i + 1];
+      paired = (j < nb || hasnext) && Bs[j] == v;  // the b at the walk's pointer
+      isa = true;
+      i++;
+    } else {
+      v = Bs[j];
+      paired = (i > 0 || hasprev) && As[i] == v;  // the a taken just before
+      isa = false;
+      j++;
+    }
+    bool emit;
+    switch (op) {
+      case SYZGPU_DIFFERENCE: emit = isa && !paired; break;
+      case SYZGPU_INTERSECTION: emit = isa && paired; break;
+      case SYZGPU_UNION: emit = isa || !paired; break;
+      default: emit = !paired; break;  // symmetric difference
+    }
+    emit = emit && v != SENT;
+    if (EMIT && emit) outv[c] = v;
+    c += emit ? 1u : 0u;
+  }
+  uint32_t tot;
+  const uint32_t pre = block_excl_scan<SO_BLOCK>(c, red, &tot);
+  if (!EMIT) {
+    if (threadIdx.x == 0) tcnt[tile] = tot;
+    return;
+  }
+  for (uint32_t k = 0; k < c; k++) st[pre + k] = outv[k];
+  __syncthreads();
+  uint32_t* o = out + tout[tile];
+  for (uint32_t k = threadIdx.x; k < tot; k += SO_BLOCK) o[k] = st[k];
+}
+
+// out_off[p] = tout[tstart[p]] (a pair without tiles: the next one's start)
+__global__ void k_so_pairoff(const uint64_t* tstart, const uint64_t* tout, uint32_t npairs, uint64_t* out_off) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p <= npairs; p += gridDim.x * blockDim.x)
+    out_off[p] = tout[tstart[p]];
+}
+
+static uint64_t setop_batch_rank(int op, const uint32_t* a, const uint64_t* aoff, uint64_t na, const uint32_t* b,
+                                 const uint64_t* boff, uint64_t nb, uint32_t npairs, uint32_t* out, uint64_t out_cap,
+                                 uint64_t* out_off_dev, hipStream_t s);
+
 // Device-side batched set op. All pointers device; out_off_dev gets npairs+1 offsets.
 // Returns total output length (host), throws on unsorted input / capacity.
 uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64_t na, const uint32_t* b,
+                         const uint64_t* boff, uint64_t nb, uint32_t npairs, uint32_t* out, uint64_t out_cap,
+                         uint64_t* out_off_dev, hipStream_t s) {
+  Context& c = ctx();
+  if (getenv("SYZGPU_SETOP_RANK") && atoi(getenv("SYZGPU_SETOP_RANK")))
+    return setop_batch_rank(op, a, aoff, na, b, boff, nb, npairs, out, out_cap, out_off_dev, s);
+  const uint64_t tbound = npairs + (na + nb) / SO_T + 1;
+  uint32_t* ntile = c.scratch.get<uint32_t>("so_ntile", npairs + 1);
+  uint64_t* tstart = c.scratch.get<uint64_t>("so_tstart", npairs + 2);
+  uint32_t* tcnt = c.scratch.get<uint32_t>("so_tcnt", tbound + 1);
+  uint64_t* tout = c.scratch.get<uint64_t>("so_tout", tbound + 2);
+  int* fl = c.scratch.get<int>("so_fl", 2);
+  SYZ_HIP(hipMemsetAsync(fl, 0, 2 * sizeof(int), s));
+  uint32_t* tpair = c.scratch.get<uint32_t>("so_tpair", tbound + 1);
+  k_so_ntiles<<<grid_for(npairs, 256, 4096), 256, 0, s>>>(aoff, boff, npairs, ntile);
+  SYZ_LAUNCHED();
+  exclusive_scan_u32(ntile, tstart, npairs, s);
+  k_so_tpair<<<grid_for(npairs, 256, 4096), 256, 0, s>>>(tstart, npairs, tpair);
+  SYZ_LAUNCHED();
+  {
+    ProfScope ps("setop_count", s, 4 * (na + nb) + 16 * (uint64_t)npairs);
+    k_so_tile<false><<<(unsigned)tbound, SO_BLOCK, 0, s>>>(op, a, aoff, b, boff, npairs, tstart, tpair, tcnt, nullptr,
+                                                            nullptr, fl, fl + 1);
+    SYZ_LAUNCHED();
+  }
+  uint64_t* hnt = c.pinned.get<uint64_t>(2);
+  SYZ_HIP(hipMemcpyAsync(hnt, tstart + npairs, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  const uint64_t ntiles = *hnt;
+  exclusive_scan_u32(tcnt, tout, ntiles, s);
+  k_so_pairoff<<<grid_for(npairs + 1, 256, 4096), 256, 0, s>>>(tstart, tout, npairs, out_off_dev);
+  SYZ_LAUNCHED();
+  int* herr = c.pinned.get<int>(4);
+  uint64_t* htot = reinterpret_cast<uint64_t*>(herr + 2);
+  SYZ_HIP(hipMemcpyAsync(herr, fl, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(htot, tout + ntiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  if (herr[1]) fail(SYZGPU_EINVAL, "set operation input is not sorted ascending");
+  if (herr[0])  // a repeated value: the multiset rank path
+    return setop_batch_rank(op, a, aoff, na, b, boff, nb, npairs, out, out_cap, out_off_dev, s);
+  const uint64_t total = *htot;
+  if (total > out_cap) fail(SYZGPU_ECAPACITY, "set operation output capacity too small");
+  if (ntiles) {
+    ProfScope ps("setop_emit", s, 4 * (na + nb) + 4 * total + 8 * (uint64_t)npairs);
+    k_so_tile<true><<<(unsigned)ntiles, SO_BLOCK, 0, s>>>(op, a, aoff, b, boff, npairs, tstart, tpair, nullptr, tout, out,
+                                                          nullptr, nullptr);
+    SYZ_LAUNCHED();
+  }
+  return total;
+}
+
+// The per-element multiset rank path (any sorted input, repeated values included).
+static uint64_t setop_batch_rank(int op, const uint32_t* a, const uint64_t* aoff, uint64_t na, const uint32_t* b,
                          const uint64_t* boff, uint64_t nb, uint32_t npairs, uint32_t* out, uint64_t out_cap,
                          uint64_t* out_off_dev, hipStream_t s) {
   Context& c = ctx();
@@ -249,6 +494,138 @@ __global__ void k_unique_scatter(const uint32_t* s, uint64_t n, const uint8_t* k
 }
 __global__ void k_store_len(const uint64_t* pos, uint64_t n, uint64_t* out_len, uint32_t seg) {
   out_len[seg] = pos[n];
+}
+
+// ---- Canonicalize on a device-resident CSR (no host copy of the offsets) --------------------------
+// Covers are classed on the device by length (wave-aggregated appends to three lists): <= 512 PCs
+// take a 256-thread workgroup with a 2 KB LDS bitonic sort (eight workgroups per CU), <= 2048 a
+// 512-thread one, <= 16384 (kCoverSize) the 1024-thread k_canon_lds; longer ones (not produced by
+// kcov) go through the global network one by one. After the sort: unique with last = sentinel and
+// the in-place store of the kept prefix (cover.go:28-40), the new length to out_len.
+template <uint32_t PMAX, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_canon_cls(uint32_t* pcs, const uint64_t* off, const uint32_t* list,
+                                                     const uint32_t* nlist_dev, uint64_t* out_len) {
+  __shared__ uint32_t sh[PMAX];
+  __shared__ uint32_t red[BLOCK / 64 + 1];
+  const uint32_t nlist = *nlist_dev;
+  for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
+    const uint32_t seg = list[li];
+    const uint64_t beg = off[seg];
+    const uint32_t n = (uint32_t)(off[seg + 1] - beg);
+    uint32_t P = 64;
+    while (P < n) P <<= 1;
+    for (uint32_t i = threadIdx.x; i < P; i += BLOCK) sh[i] = i < n ? pcs[beg + i] : SENT;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        // one compare-exchange per pair (i, i ^ j), i with bit j clear: P / 2 of them
+        for (uint32_t t = threadIdx.x; t < P / 2; t += BLOCK) {
+          const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+          const uint32_t ij = i | j;
+          const uint32_t x = sh[i], y = sh[ij];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            sh[i] = y;
+            sh[ij] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    uint32_t outp = 0;
+    for (uint32_t base = 0; base < n; base += BLOCK) {
+      const uint32_t i = base + threadIdx.x;
+      uint32_t v = 0, kk = 0;
+      if (i < n) {
+        v = sh[i];
+        kk = v != (i ? sh[i - 1] : SENT);
+      }
+      uint32_t tot;
+      const uint32_t r = block_excl_scan<BLOCK>(kk, red, &tot);
+      if (kk) pcs[beg + outp + r] = v;
+      outp += tot;
+    }
+    if (threadIdx.x == 0) out_len[seg] = outp;
+    __syncthreads();
+  }
+}
+
+// cls lists: [0] <= 512, [1] <= 2048, [2] <= 16384, [3] longer; cnt[4]
+__global__ void k_canon_class(const uint64_t* off, size_t ncov, uint32_t* lists, size_t cap, uint32_t* cnt) {
+  for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < ncov; i0 += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = i0 + threadIdx.x;
+    int c = -1;
+    if (i < ncov) {
+      const uint64_t n = off[i + 1] - off[i];
+      c = n <= 512 ? 0 : n <= 2048 ? 1 : n <= (uint64_t)CANON_LDS ? 2 : 3;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint64_t m = __ballot(c == k);
+      if (!m) continue;
+      const unsigned leader = (unsigned)__ffsll((unsigned long long)m) - 1;
+      uint32_t base = 0;
+      if (__lane_id() == leader) base = atomicAdd(&cnt[k], (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, (int)leader, 64);
+      if (c == k) lists[k * cap + base + (uint32_t)__popcll(m & lanemask_lt())] = (uint32_t)i;
+    }
+  }
+}
+
+void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, uint64_t* out_len, hipStream_t s) {
+  Context& c = ctx();
+  if (ncov == 0) return;
+  if (ncov >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many covers");
+  uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", 4 * ncov);
+  uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", 4);
+  SYZ_HIP(hipMemsetAsync(cnt, 0, 16, s));
+  k_canon_class<<<grid_for(ncov, 256, 8192), 256, 0, s>>>(off, ncov, lists, ncov, cnt);
+  SYZ_LAUNCHED();
+  if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+  const unsigned ncu = (unsigned)std::max(1, c.ncu);
+  {
+    ProfScope ps("canon_small", s, 0);
+    k_canon_cls<512, 256><<<ncu * 8, 256, 0, s>>>(pcs, off, lists, cnt, out_len);
+    SYZ_LAUNCHED();
+  }
+  k_canon_cls<2048, 512><<<ncu * 4, 512, 0, s>>>(pcs, off, lists + ncov, cnt + 1, out_len);
+  SYZ_LAUNCHED();
+  k_canon_cls<CANON_LDS, CANON_BLOCK><<<ncu * 2, CANON_BLOCK, 0, s>>>(pcs, off, lists + 2 * ncov, cnt + 2, out_len);
+  SYZ_LAUNCHED();
+  // longer covers: their list back to the host, then the global network one by one
+  uint32_t* h = c.pinned.get<uint32_t>(4);
+  SYZ_HIP(hipMemcpyAsync(h, cnt, 16, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  const uint32_t nbig = h[3];
+  if (!nbig) return;
+  std::vector<uint32_t> big(nbig);
+  SYZ_HIP(hipMemcpyAsync(big.data(), lists + 3 * ncov, nbig * 4, hipMemcpyDeviceToHost, s));
+  std::vector<uint64_t> hoff(2);
+  for (uint32_t seg : big) {
+    SYZ_HIP(hipMemcpyAsync(hoff.data(), off + seg, 16, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    const uint64_t n = hoff[1] - hoff[0];
+    uint64_t P = 1;
+    while (P < n) P <<= 1;
+    uint32_t* tmp = c.scratch.get<uint32_t>("canon_big", P);
+    uint8_t* keep = c.scratch.get<uint8_t>("canon_keep", n);
+    uint64_t* pos = c.scratch.get<uint64_t>("canon_pos", n + 1);
+    const unsigned g = grid_for(P, 256, 65536);
+    k_canon_pad<<<g, 256, 0, s>>>(pcs + hoff[0], n, tmp, P);
+    SYZ_LAUNCHED();
+    for (uint64_t k = 2; k <= P; k <<= 1)
+      for (uint64_t j = k >> 1; j > 0; j >>= 1) {
+        k_bitonic_step<<<g, 256, 0, s>>>(tmp, P, k, j);
+        SYZ_LAUNCHED();
+      }
+    k_unique_flags<<<grid_for(n, 256, 65536), 256, 0, s>>>(tmp, n, keep);
+    SYZ_LAUNCHED();
+    exclusive_scan_u8(keep, pos, n, s);
+    k_unique_scatter<<<grid_for(n, 256, 65536), 256, 0, s>>>(tmp, n, keep, pos, pcs + hoff[0]);
+    SYZ_LAUNCHED();
+    k_store_len<<<1, 1, 0, s>>>(pos, n, out_len, seg);
+    SYZ_LAUNCHED();
+  }
 }
 
 // Canonicalize every cover of a device CSR in place. host_off is the host copy of off.
@@ -415,6 +792,15 @@ int syzgpu_canonicalize_batch(uint32_t* pcs, const uint64_t* off, size_t ncov, u
     canonicalize_batch_dev(dp, doff, off, ncov, dlen, s);
     if (n) SYZ_HIP(hipMemcpyAsync(pcs, dp, n * 4, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipMemcpyAsync(out_len, dlen, ncov * 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+  })
+}
+
+int syzgpu_canonicalize_batch_dev(uint32_t* pcs, const uint64_t* off, size_t ncov, uint64_t* out_len, void* stream) {
+  SYZ_API_BODY({
+    if (!off || !out_len || (ncov && !pcs)) fail(SYZGPU_EINVAL, "null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    canonicalize_batch_dev2(pcs, off, ncov, out_len, s);
     SYZ_HIP(hipStreamSynchronize(s));
   })
 }

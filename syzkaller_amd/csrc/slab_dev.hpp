@@ -29,7 +29,7 @@ namespace syz {
 #define SYZ_SL_TPW 64
 #endif
 #ifndef SYZ_SL_SKIP
-#define SYZ_SL_SKIP 1
+#define SYZ_SL_SKIP 0  // A/B knob: skip tile groups outside a pass (measured with register spills)
 #endif
 #ifndef SYZ_SL_BUF_BITS
 #define SYZ_SL_BUF_BITS 14
@@ -44,6 +44,12 @@ constexpr uint32_t SL_MEMB = 512;                              // members per sl
 constexpr uint32_t SL_PMAX = (SL_TILES * 64 + SL_BUF - 1) / SL_BUF + 1;  // passes at most
 static_assert(SL_TPW <= 64, "a wave's tile table is one register per lane");
 constexpr uint32_t SL_NONE = 0xFFFFFFFFu;  // a padding slot: no element (no member has the all-ones tag)
+
+// the value of lane - 1 (DPP wave_shr:1, a VALU op: shuffles through LDS would keep 64 tiles' results
+// in flight in registers)
+__device__ __forceinline__ uint32_t lane_prev(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x138, 0xF, 0xF, false);
+}
 
 // ---- slab planning on the device ------------------------------------------------------------------
 static __global__ void k_sl_tiles(const uint32_t* mlen, size_t n, uint32_t* mtile) {
@@ -131,9 +137,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   __shared__ uint32_t red[WAVES + 1];
   __shared__ uint32_t pw[SL_PMAX + 2];      // first window of each pass
   __shared__ uint32_t pa[SL_PMAX + 1];      // its start (read before any pass moves the cursors)
-  __shared__ int unsorted;                  // some tile's PCs are not ascending (Minimize allows it)
-  const uint64_t c = blockIdx.x;
-  if (c >= *nslab) return;
+  // one slab per workgroup (a persistent loop over slabs made the compiler keep per-slab values across
+  // iterations and spill)
+  const uint64_t nsl = *nslab;
+  if (uint64_t c = blockIdx.x; c < nsl) {
   const int wv = threadIdx.x >> 6;
   const unsigned lane = __lane_id();
   const PSlab sl = slabs[c];
@@ -159,7 +166,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   }
   for (uint32_t i = threadIdx.x; i <= W; i += BLOCK) hist[i] = 0;
   for (uint32_t i = threadIdx.x; i < SL_PMAX + 2; i += BLOCK) pw[i] = W;
-  if (threadIdx.x == 0) unsorted = 0;
   __syncthreads();
   // lane k of this wave: tile t = wv + WAVES k (its member by a search of the tile prefix)
   uint32_t alo, ahi, cz;
@@ -195,6 +201,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     v[k] = reinterpret_cast<const uint32_t*>((uintptr_t)base)[lane < cnt ? lane : 0u];
     if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
   }
+  // every wave has read its tiles' member entries (its loads' addresses depend on them): the member
+  // table's space takes the tiles' window ranges (a plain barrier: the loads stay in flight)
+  if (SYZ_SL_SKIP) __builtin_amdgcn_s_barrier();
+  uint32_t* trng = reinterpret_cast<uint32_t*>(mrel);  // a tile's windows: min | max << 16
+  static_assert(SL_TILES <= SL_MEMB, "tile windows in the member table's space");
   int bad = 0;  // err bits this lane saw
   if constexpr (NOV) {
     // strictly increasing: lane neighbours inside a tile; a tile's first PC against the PC before it
@@ -203,7 +214,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, k);
       const uint32_t cnt = z & 0x7Fu;
       const int eb = (z & 0x100u) ? 1 : 4;
-      const uint32_t pv = __shfl_up(v[k], 1, 64);
+      const uint32_t pv = lane_prev(v[k]);
       if (lane > 0 && lane < cnt && pv >= v[k]) bad |= eb;
       if ((z & 0x80u) && lane == 0 && cnt) {
         const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ahi, k) << 32) |
@@ -222,24 +233,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   // from here on v holds the PC's offset from lo: window = v >> S, offset in it = v & omask
   // window histogram
   const uint32_t DUMMY = WMAX + 1 + lane;
-  bool desc = false;  // a lane below its left neighbour
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
     const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, k);
     const uint32_t cnt = z & 0x7Fu;
-    if constexpr (!NOV) {  // (NOV checked strict order above: an unsorted batch fails)
-      const uint32_t pv = __shfl_up(v[k], 1, 64);
-      desc |= lane > 0 && lane < cnt && pv > v[k];
-    }
     v[k] -= lo;
     const uint32_t w = v[k] >> S;
     const bool in = lane < cnt;
+    if (SYZ_SL_SKIP) {  // the tile's window range (min and max over its lanes: covers may be unsorted)
+      const uint32_t wc = in ? min(w, 0xFFFFu) : 0xFFFFu;
+      const uint32_t wlo = wave_min(wc), whi = (uint32_t)wave_incl_max(in ? (int32_t)min(w, 0xFFFFu) : -1);
+      if (lane == 63) trng[wv + WAVES * k] = wlo | (min(whi, 0xFFFFu) << 16);
+    }
     // outside the windows: an unsorted cover (Minimize: redone on exact bounds; NOV: out of order)
     bad |= (in && w >= W) ? (NOV ? ((z & 0x100u) ? 1 : 4) : 1) : 0;
     atomicAdd(&hist[in && w < W ? w : DUMMY], 1u);
     if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
   }
-  if (__ballot(desc) && lane == 0) unsorted = 1;
   {
     const uint64_t bm = __ballot(bad != 0);
     if (bm) {
@@ -286,7 +296,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   if (dbg & 32) return;  // timing only: loads, histogram, scan
   __syncthreads();
   const uint32_t npass = (total + SL_BUF - 1) >> SL_BUF_BITS;
-  const bool unsorted_r = unsorted != 0;
   const uint32_t omask = (1u << S) - 1;
   uint32_t* gel = elems + sl.elem;
   for (uint32_t k = 0; k < npass; k++) {
@@ -303,23 +312,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     // opaque per pass, so the compiler does not hoist 64 tiles' elements out of the pass loop (VGPRs)
     uint32_t Sp = S, om = omask;
     asm volatile("" : "+s"(Sp), "+s"(om));
-    const bool skip_ok = SYZ_SL_SKIP && !unsorted_r;
-    // a tile's PCs are sorted, so its windows are [w(lane 0), w(last lane)]: a tile outside the pass's
-    // windows is skipped whole (most tiles fall into one pass)
-    constexpr int PB = 4;
+    constexpr int PB = 8;
 #pragma unroll
     for (int k0 = 0; k0 < TPW; k0 += PB) {
-      bool any = false;
+      if (SYZ_SL_SKIP) {  // a group of tiles with no window in this pass is skipped whole
+        bool any = false;
 #pragma unroll
-      for (int q = 0; q < PB; q++) {
-        const int kk = k0 + q;
-        const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, kk);
-        const uint32_t cnt = z & 0x7Fu;
-        const uint32_t wa = (uint32_t)__builtin_amdgcn_readlane((int)v[kk], 0) >> Sp;
-        const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)v[kk], (int)(cnt ? cnt - 1 : 0)) >> Sp;
-        any |= cnt && wb >= wl && wa < wh;
+        for (int q = 0; q < PB; q++) {
+          const uint32_t r = (uint32_t)__builtin_amdgcn_readfirstlane((int)trng[wv + WAVES * (k0 + q)]);
+          any |= (r >> 16) >= wl && (r & 0xFFFFu) < wh && (r & 0xFFFFu) <= (r >> 16);
+        }
+        if (!any) continue;  // wave-uniform
       }
-      if (!any && skip_ok) continue;  // wave-uniform
       uint32_t pos[PB], el[PB];
       bool ok[PB];
 #pragma unroll
@@ -368,6 +372,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
     __syncthreads();
   }
+  }  // slabs
 }
 
 // ---- M walk over a window's slab runs ---------------------------------------------------------------

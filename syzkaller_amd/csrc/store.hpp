@@ -140,9 +140,10 @@ struct Corpus {
   // incremental maintenance (corpus_inc.hip): ids per call, the (call, PC) -> id lookup sorted by
   // call << 32 | PC, and whether appends/keeps have left dict/gdict behind (the analytics rebuild)
   std::vector<uint64_t> hnids;
-  DevArr<uint64_t> sd_key;
-  DevArr<uint32_t> sd_id;
-  size_t sd_n = 0;
+  DevArr<uint64_t> sd_key, dl_key;  // main (sorted) and delta (sorted: the keys appended since the last
+  DevArr<uint32_t> sd_id, dl_id;    // merge) dictionaries
+  size_t sd_n = 0, dl_n = 0;
+  bool part_stale = false;  // appends since the last group partition / work list (redone lazily)
   bool sd_built = false, incremental = false;
   std::vector<VecWork> hmain;  // the items over the panel-major body of the stream (no tails)
   std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint64_t>> ptail;  // panel -> appended range
@@ -157,6 +158,7 @@ struct Corpus {
     off.free(); gstart.free(); gdict.free(); el0.free(); group.free(); members.free(); member_of.free(); nwin.free(); dict.free();
     gtchunks.free(); gtdone.free(); count_hist.free(); xg.free(); xo.free();
     gtabs.free(); vmem.free(); prog_len.free(); ids16.free(); work.free(); sd_key.free(); sd_id.free();
+    dl_key.free(); dl_id.free();
     ids16b.free(); vmemb.free(); keep_idx.free();
   }
 };

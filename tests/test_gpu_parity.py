@@ -126,6 +126,67 @@ def test_setop_batch_device_entry_triage_shape():
             assert np.array_equal(o[int(oo[i]):int(oo[i + 1])], oracle.setop(op, a_list[i], b_list[i])), (op, i)
 
 
+def _dev_setops(torch, a_list, b_list):
+    a, aoff = cover.to_csr(a_list)
+    b, boff = cover.to_csr(b_list)
+
+    def t(x):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+        return torch.from_numpy(np.ascontiguousarray(x).view(view.get(x.dtype, x.dtype))).to("cuda:0")
+    da, dao, db, dbo = t(a if a.size else np.zeros(1, np.uint32)), t(aoff), t(b if b.size else np.zeros(1, np.uint32)), t(boff)
+    res = {}
+    for op in SETOPS:
+        cap = a.size + b.size + 1
+        out = torch.zeros(cap, dtype=torch.int32, device="cuda:0")
+        ooff = torch.zeros(len(a_list) + 1, dtype=torch.int64, device="cuda:0")
+        tot = cover.SetOpBatchDev(op, da, dao, a.size, db, dbo, b.size, len(a_list), out, cap, ooff)
+        o = out.cpu().numpy().view(np.uint32)
+        oo = ooff.cpu().numpy().view(np.uint64)
+        assert tot == int(oo[-1])
+        res[op] = [o[int(oo[i]):int(oo[i + 1])] for i in range(len(a_list))]
+    return res
+
+
+def test_setop_tiles_boundaries_vs_oracle():
+    # strictly increasing pairs (the merge-path tile path): merged lengths around multiples of the
+    # 1024-element tile, equal values on both sides of tile cuts, identical / disjoint / one-sided
+    # pairs, the sentinel at the end of either list
+    import torch
+    rnd = np.random.default_rng(21)
+    a_list, b_list = [], []
+    for m in [1, 63, 64, 1023, 1024, 1025, 2047, 2048, 2049, 5000, 20000]:
+        for share in (0.0, 0.5, 1.0):
+            u = np.unique(rnd.integers(0, 1 << 31, size=m)).astype(np.uint32)
+            a = u[rnd.random(u.size) < 0.6]
+            b = np.union1d(u[rnd.random(u.size) < 0.6], a[rnd.random(a.size) < share]).astype(np.uint32)
+            a_list.append(a)
+            b_list.append(b)
+    a_list += [np.arange(0, 3000, 2, dtype=np.uint32), np.arange(3000, dtype=np.uint32),
+               np.zeros(0, np.uint32), np.arange(1500, dtype=np.uint32)]
+    b_list += [np.arange(0, 3000, 2, dtype=np.uint32), np.zeros(0, np.uint32),
+               np.arange(10, 2000, 3, dtype=np.uint32), np.arange(1500, 3100, dtype=np.uint32)]
+    a_list.append(np.append(np.arange(0, 2000, 2, dtype=np.uint32), np.uint32(0xFFFFFFFF)))
+    b_list.append(np.append(np.arange(0, 2000, 3, dtype=np.uint32), np.uint32(0xFFFFFFFF)))
+    got = _dev_setops(torch, a_list, b_list)
+    for op in SETOPS:
+        for i, (a, b) in enumerate(zip(a_list, b_list)):
+            assert np.array_equal(got[op][i], oracle.setop(op, a, b)), (op, i)
+
+
+def test_setop_batch_repeated_values_take_rank_path():
+    # one pair with a repeated value (Go allows it): the whole batch takes the multiset rank path
+    import torch
+    rnd = np.random.default_rng(22)
+    a_list = [np.unique(rnd.integers(0, 5000, size=800)).astype(np.uint32) for _ in range(50)]
+    b_list = [np.unique(rnd.integers(0, 5000, size=900)).astype(np.uint32) for _ in range(50)]
+    a_list[7] = np.array([1, 5, 5, 5, 9, 9], np.uint32)
+    b_list[7] = np.array([5, 9, 9, 9, 12], np.uint32)
+    got = _dev_setops(torch, a_list, b_list)
+    for op in SETOPS:
+        for i, (a, b) in enumerate(zip(a_list, b_list)):
+            assert np.array_equal(got[op][i], oracle.setop(op, a, b)), (op, i)
+
+
 def test_setop_rejects_unsorted():
     with pytest.raises(_lib.SyzGpuError) as e:
         cover.Union([3, 1], [2])
@@ -150,6 +211,28 @@ def test_canonicalize_random_vs_oracle():
         assert np.array_equal(got, want), i
         one = cover.Canonicalize(c.copy())
         assert np.array_equal(one, want), i
+
+
+def test_canonicalize_batch_dev_classes_vs_oracle():
+    # the device entry: every length class (<= 512, <= 2048, <= 16384, longer), duplicates, the
+    # sentinel, empty covers; in place, lengths on the device
+    import torch
+    rnd = np.random.default_rng(23)
+    sizes = [0, 1, 5, 64, 65, 300, 512, 513, 1000, 2048, 2049, 9000, 16384, 16385, 33000]
+    sizes += list(rnd.integers(1, 1500, size=300))
+    covs = [rnd.integers(0, max(2, int(sz)), size=int(sz), dtype=np.uint64).astype(np.uint32) for sz in sizes]
+    covs.append(np.full(9, 0xFFFFFFFF, np.uint32))
+    covs.append(np.array([7, 0xFFFFFFFF, 3, 0xFFFFFFFF, 7], np.uint32))
+    pcs, off = cover.to_csr(covs)
+    d_pcs = torch.from_numpy(pcs.view(np.int32).copy()).to("cuda:0")
+    d_off = torch.from_numpy(off.view(np.int64).copy()).to("cuda:0")
+    d_len = torch.zeros(len(covs), dtype=torch.int64, device="cuda:0")
+    cover.CanonicalizeBatchDev(d_pcs, d_off, len(covs), d_len)
+    work = d_pcs.cpu().numpy().view(np.uint32)
+    lens = d_len.cpu().numpy()
+    for i, c in enumerate(covs):
+        want = oracle.canonicalize(c)
+        assert np.array_equal(work[int(off[i]):int(off[i]) + int(lens[i])], want), i
 
 
 # ---- Minimize -----------------------------------------------------------------------------------------

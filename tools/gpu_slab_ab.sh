@@ -1,20 +1,23 @@
 #!/bin/bash
-# A/B of library variants (tools/build_variant.sh) on the serialized raw pipeline (pm_time.py), then
-# SQ counter passes of the default library. Usage (through gpurun): bash tools/gpu_slab_ab.sh TAG VARIANT...
+# A/B of library variants (tools/build_variant.sh) and environment settings on the raw minimize job
+# (pm_time.py, serialized and concurrent), then SQ counter passes of the default library.
+# Usage (through gpurun): bash tools/gpu_slab_ab.sh TAG [LIB[:VAR=val[,VAR=val]] ...]   (LIB base = default)
 set -o pipefail
 TAG=${1:-ab}; shift
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-for v in base "$@"; do
+for spec in base "$@"; do
+  v=${spec%%:*}; envs=""; [ "$spec" != "$v" ] && envs=$(echo ${spec#*:} | tr ',' ' ')
   lib=$R/syzkaller_amd/libsyzgpu.so; [ $v = base ] || lib=$R/syzkaller_amd/libsyzgpu_$v.so
   for e in "SYZGPU_PM_SERIAL=1" "X=0"; do
-    echo "== $v $e" >> $OUT/pm.log
-    env SYZGPU_LIB=$lib $e timeout -k 10 120 python3 $R/tools/pm_time.py 2>&1 | grep -v amdgpu.ids >> $OUT/pm.log || { tail -5 $OUT/pm.log; exit 1; }
+    echo "== $spec $e" >> $OUT/pm.log
+    env SYZGPU_LIB=$lib $envs $e timeout -k 10 120 python3 $R/tools/pm_time.py 2>&1 | grep -v amdgpu.ids >> $OUT/pm.log || { tail -5 $OUT/pm.log; exit 1; }
   done
 done
 cat $OUT/pm.log
+[ -n "$NO_PMC" ] && exit 0
 cd /tmp
 i=0
 for CTR in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU" \
