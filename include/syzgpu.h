@@ -274,6 +274,23 @@ int syzgpu_corpus_append(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* 
                          const uint16_t* prog_len /* may be NULL */, size_t n, syzgpu_corpus** out);
 int syzgpu_corpus_append_dev(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                              const uint16_t* prog_len, size_t n, void* stream, syzgpu_corpus** out);
+/* NewInput's gate on the store (syz-manager/manager.go:609-616) over a batch of n inputs (CSR from 0,
+ * canonical covers, call ids < ngroups): input k is new iff Difference(cover_k, corpusCover[call_k])
+ * is non-empty, corpusCover holding every cover the store has held (create, appends, keeps' dropped
+ * entries) and the batch's earlier new inputs; the new ones are appended in batch order
+ * (mgr.corpus = append(...)) and unioned in (corpusCover[call] = Union(...)). corpusCover is built on
+ * the store's first gate (or first explicit keep) and kept current in O(batch) by every append.
+ * is_new (n bytes, may be NULL): 1 = appended; *accepted (may be NULL) = their number. SYZGPU_EINVAL
+ * (store unchanged) for a bad call id or a non-canonical cover. Host-pointer and device forms: */
+int syzgpu_corpus_new_inputs(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                             const uint16_t* prog_len /* may be NULL */, size_t n, uint8_t* is_new,
+                             uint64_t* accepted);
+int syzgpu_corpus_new_inputs_dev(syzgpu_corpus* c, const uint32_t* pcs, const uint64_t* off,
+                                 const uint32_t* group, const uint16_t* prog_len, size_t n, uint8_t* is_new,
+                                 void* stream, uint64_t* accepted);
+/* corpusCover itself (manager.go:65): per call the sorted PCs, as host CSR (out_off: ngroups+1);
+ * *total = its size; SYZGPU_ECAPACITY (nothing written to out) when it exceeds cap. */
+int syzgpu_corpus_cover_union(syzgpu_corpus* c, uint32_t* out, uint64_t* out_off, size_t cap, uint64_t* total);
 /* mgr.corpus = newCorpus (manager.go:529): the corpus becomes entries idx[0..m) of the current one,
  * in that order (host / device int64 array); an index out of range is SYZGPU_EINVAL (corpus unchanged). */
 int syzgpu_corpus_keep(syzgpu_corpus* c, const int64_t* idx, size_t m);

@@ -74,6 +74,9 @@ SIGNATURES = {
     "syzgpu_corpus_destroy": (_c.c_int, [_vp]),
     "syzgpu_corpus_append": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "syzgpu_corpus_append_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+    "syzgpu_corpus_new_inputs": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+    "syzgpu_corpus_new_inputs_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "syzgpu_corpus_cover_union": (_c.c_int, [_vp, _vp, _vp, _sz, _vp]),
     "syzgpu_corpus_minimize": (_c.c_int, [_vp, _vp, _vp]),
     "syzgpu_corpus_minimize_dev": (_c.c_int, [_vp, _c.c_int32, _vp, _vp, _vp]),
     "syzgpu_corpus_info": (_c.c_int, [_vp, _vp, _sz]),

@@ -298,6 +298,42 @@ class CoverStore:
         self.n += n
         return self
 
+    def NewInputs(self, pcs, off, group, prog_len=None):
+        """NewInput's gate (manager.go:609-616) over a batch: inputs whose cover adds a PC to corpusCover
+        of their call (earlier new inputs of the batch included) are appended and unioned in. Returns
+        is_new (bool per input)."""
+        pcs, off, group = _u32(pcs), np.ascontiguousarray(off, dtype=np.uint64), _u32(group)
+        pl = None if prog_len is None else np.ascontiguousarray(prog_len, dtype=np.uint16)
+        n = off.size - 1
+        is_new = np.zeros(max(n, 1), dtype=np.uint8)
+        acc = np.zeros(1, dtype=np.uint64)
+        check(lib().syzgpu_corpus_new_inputs(self._h, ptr(pcs), ptr(off), ptr(group), ptr(pl), n, ptr(is_new),
+                                             ptr(acc)))
+        self.n += int(acc[0])
+        return is_new[:n].astype(bool)
+
+    def NewInputsDevice(self, d_pcs, d_off, d_group, d_prog_len, n, d_is_new=None, stream=0):
+        """NewInputs on device buffers; returns the number appended."""
+        acc = np.zeros(1, dtype=np.uint64)
+        check(lib().syzgpu_corpus_new_inputs_dev(self._h, ptr(d_pcs), ptr(d_off), ptr(d_group), ptr(d_prog_len), n,
+                                                 ptr(d_is_new), stream, ptr(acc)))
+        self.n += int(acc[0])
+        return int(acc[0])
+
+    def CorpusCover(self):
+        """mgr.corpusCover (manager.go:65): per call the sorted PCs, as (pcs, off[ngroups + 1])."""
+        tot = np.zeros(1, dtype=np.uint64)
+        off = np.zeros(self.ngroups + 1, dtype=np.uint64)
+        cap = 1 << 16
+        while True:
+            out = np.empty(cap, dtype=np.uint32)
+            rc = lib().syzgpu_corpus_cover_union(self._h, ptr(out), ptr(off), cap, ptr(tot))
+            if rc == ECAPACITY and int(tot[0]) > cap:
+                cap = int(tot[0])
+                continue
+            check(rc)
+            return out[: int(tot[0])].copy(), off
+
     def keep(self, idx):
         """mgr.corpus = newCorpus (manager.go:529): the corpus becomes entries idx, in that order."""
         idx = np.ascontiguousarray(idx, dtype=np.int64)

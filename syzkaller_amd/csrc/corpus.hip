@@ -132,8 +132,8 @@ static uint32_t max_len_dev(const uint16_t* a, size_t n, hipStream_t s) {
 }
 
 // covers (device pointers) appended after H's current ones; prog_len may be null (zeros)
-static void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
-                          const uint16_t* prog_len, size_t m, hipStream_t s) {
+void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                   const uint16_t* prog_len, size_t m, hipStream_t s, bool cc_update) {
   if (!off || (m && !group)) fail(SYZGPU_EINVAL, "null pointer");
   uint64_t* h = ctx().pinned.get<uint64_t>(3);
   uint32_t* bad = ctx().scratch.get<uint32_t>("co_bad", 1);
@@ -153,6 +153,7 @@ static void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* 
   const size_t n = H.n, nt = n + m;
   const uint64_t L0 = H.L;
   if (nt >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
+  if (cc_update) cc_add(H, pcs, off, group, m, Lm, s);  // corpusCover follows every append
   index_follow(H, [&](Corpus& K) { corpus_index_sync(K, H, s); });  // a recorded keep first
   grow_keep(H.pcs, H.L, H.L + Lm + 1, s);
   grow_keep(H.off, n + 1, nt + 1, s);
@@ -187,6 +188,9 @@ static CorpusHandle* handle_create_dev(const uint32_t* pcs, const uint64_t* off,
 // count and the gather goes out before the one wait
 static void keep_entries(CorpusHandle& H, const int64_t* idx, size_t m, hipStream_t s, bool distinct = false) {
   if (m && !idx) fail(SYZGPU_EINVAL, "null pointer");
+  // corpusCover holds every cover the store has held: taken before a keep that may drop a call's PCs
+  // (minimizeCorpus's keep without key parts cannot: Minimize keeps a first holder of every PC)
+  if (!distinct || H.parts_set) cc_ensure(H, s);
   index_follow(H, [&](Corpus& K) { corpus_index_sync(K, H, s); });  // a recorded keep first
   Scratch& sc = ctx().scratch;
   uint32_t* len = sc.get<uint32_t>("co_len", m + 1);
@@ -383,6 +387,59 @@ int syzgpu_corpus_append(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t*
     append_covers(H, dp, doff, dg, dl, n, s);
     SYZ_HIP(hipStreamSynchronize(s));
     if (out) *out = cp;
+  })
+}
+
+int syzgpu_corpus_new_inputs_dev(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t* off,
+                                 const uint32_t* group, const uint16_t* prog_len, size_t n, uint8_t* is_new,
+                                 void* stream, uint64_t* accepted) {
+  SYZ_API_BODY({
+    CorpusHandle& H = H_of(cp);
+    std::lock_guard<std::recursive_mutex> hl_(H.mu);
+    const uint64_t na = corpus_new_inputs(H, pcs, off, group, prog_len, n, is_new, (hipStream_t)stream);
+    if (accepted) *accepted = na;
+  })
+}
+
+int syzgpu_corpus_new_inputs(syzgpu_corpus* cp, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                             const uint16_t* prog_len, size_t n, uint8_t* is_new, uint64_t* accepted) {
+  SYZ_API_BODY({
+    CorpusHandle& H = H_of(cp);
+    std::lock_guard<std::recursive_mutex> hl_(H.mu);
+    if (!off || (n && !group)) fail(SYZGPU_EINVAL, "null pointer");
+    if (off[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
+    hipStream_t s = C_.stream;
+    const uint64_t tot = off[n];
+    uint32_t* dp = C_.scratch.get<uint32_t>("cc_hpcs", tot + 1);
+    uint64_t* doff = C_.scratch.get<uint64_t>("cc_hoff", n + 1);
+    uint32_t* dg = C_.scratch.get<uint32_t>("cc_hgrp", n + 1);
+    uint16_t* dl = prog_len ? C_.scratch.get<uint16_t>("cc_hlen", n + 1) : nullptr;
+    uint8_t* dn = C_.scratch.get<uint8_t>("cc_hnew", n + 1);
+    if (tot) SYZ_HIP(hipMemcpyAsync(dp, pcs, tot * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (n) SYZ_HIP(hipMemcpyAsync(dg, group, n * 4, hipMemcpyHostToDevice, s));
+    if (dl && n) SYZ_HIP(hipMemcpyAsync(dl, prog_len, n * 2, hipMemcpyHostToDevice, s));
+    const uint64_t na = corpus_new_inputs(H, dp, doff, dg, dl, n, dn, s);
+    if (is_new && n) SYZ_HIP(hipMemcpyAsync(is_new, dn, n, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (accepted) *accepted = na;
+  })
+}
+
+int syzgpu_corpus_cover_union(syzgpu_corpus* cp, uint32_t* out, uint64_t* out_off, size_t cap, uint64_t* total) {
+  SYZ_API_BODY({
+    CorpusHandle& H = H_of(cp);
+    std::lock_guard<std::recursive_mutex> hl_(H.mu);
+    if (!total || !out_off) fail(SYZGPU_EINVAL, "null pointer");
+    hipStream_t s = C_.stream;
+    uint32_t* d = C_.scratch.get<uint32_t>("cc_xout", cap + 1);
+    uint64_t* doff = C_.scratch.get<uint64_t>("cc_xoff", H.G + 1);
+    const uint64_t nt = cc_export(H, d, doff, cap, s);
+    *total = nt;
+    if (nt > cap) fail(SYZGPU_ECAPACITY, "corpusCover larger than the output");
+    if (nt && out) SYZ_HIP(hipMemcpyAsync(out, d, nt * 4, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipMemcpyAsync(out_off, doff, (H.G + 1) * 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
   })
 }
 

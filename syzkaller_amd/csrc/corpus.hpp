@@ -15,6 +15,18 @@ namespace syz {
 // (corpus_inc.hip); without an index (never built, or dropped by a failed update or key-space parts)
 // on the raw pipeline (panels.hip, no build). The index is built for what needs it: the cover
 // analytics, key-space parts, or an explicit reindex.
+// corpusCover (manager.go:65): sorted (call << 32 | PC) keys, main + sorted delta (corpus_cover.hip)
+struct CoverSet {
+  DevArr<uint64_t> key, dkey, tmp;
+  size_t n = 0, dn = 0;
+  bool built = false;
+  ~CoverSet() {
+    key.free();
+    dkey.free();
+    tmp.free();
+  }
+};
+
 struct CorpusHandle {
   std::recursive_mutex mu;  // one call on a corpus at a time (mgr.mu serialises them in the reference)
   size_t n = 0;
@@ -34,6 +46,7 @@ struct CorpusHandle {
   bool parts_set = false, has_count_hist = false;
   std::vector<uint16_t> part, nparts;
   std::vector<uint8_t> count_hist;
+  CoverSet cc;  // built on first use (cc_ensure)
 };
 
 // The index of H's current covers, built (with H's key parts) if stale.
@@ -47,5 +60,18 @@ void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L
 void corpus_index_keep(Corpus& K, const CorpusHandle& H, const int64_t* idx, size_t m, size_t n0, hipStream_t s);
 // a recorded keep applied (the index's users call it first: corpus_index does)
 void corpus_index_sync(Corpus& K, const CorpusHandle& H, hipStream_t s);
+// m covers (device CSR, offsets from 0) appended in place; cc_update: also union them into corpusCover
+// (when built)
+void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                   const uint16_t* prog_len, size_t m, hipStream_t s, bool cc_update = true);
+// corpus_cover.hip: corpusCover built from H's covers if it is not yet; the union of appended covers;
+// NewInput's gate over a batch (is_new: device bytes or null; returns the number appended)
+void cc_ensure(CorpusHandle& H, hipStream_t s);
+void cc_add(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t m,
+            uint64_t Lm, hipStream_t s);
+uint64_t corpus_new_inputs(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                           const uint16_t* prog_len, size_t m, uint8_t* is_new, hipStream_t s);
+// corpusCover as per-call CSR into device buffers (out capacity cap; returns the total)
+uint64_t cc_export(CorpusHandle& H, uint32_t* out, uint64_t* out_off, uint64_t cap, hipStream_t s);
 
 }  // namespace syz

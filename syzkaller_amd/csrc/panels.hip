@@ -309,7 +309,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 
 // ---- M over slab runs (slab_dev.hpp): the same tables, the window's runs from every slab --------------
 #ifndef SYZ_SL_MU
-#define SYZ_SL_MU 4
+#define SYZ_SL_MU 2
 #endif
 #if SYZ_DS < 15
 #define SYZ_SMIN_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))  // 64 KB tables: two workgroups per CU

@@ -266,3 +266,133 @@ def test_key_parts_survive_append_and_keep():
     wsel[want] = 1
     assert np.array_equal(ranks[0][0], wsel) and np.array_equal(ranks[1][0], wsel)
     assert np.array_equal(ranks[0][1] + ranks[1][1], np.bincount(pl[want], minlength=C + 1))
+
+
+# ---- NewInput's corpusCover gate (manager.go:609-616, syzgpu_corpus_new_inputs[_dev]) ----------------
+
+def _union_tables(covs, group, G):
+    """corpusCover per call: the sorted union of the covers, without cover.go's sentinel."""
+    per = [[] for _ in range(G)]
+    for cv, g in zip(covs, group):
+        per[int(g)].append(np.asarray(cv, np.uint32))
+    tabs = [np.unique(np.concatenate(p)) if p else np.zeros(0, np.uint32) for p in per]
+    tabs = [t[t != 0xFFFFFFFF] for t in tabs]
+    off = np.zeros(G + 1, np.uint64)
+    off[1:] = np.cumsum([t.size for t in tabs])
+    return np.concatenate(tabs).astype(np.uint32), off
+
+
+class GateModel:
+    """The manager's NewInput on the host: oracle_novelty with no flakes over corpusCover, then the
+    accepted inputs appended to the host corpus."""
+
+    def __init__(self, hc, G):
+        self.hc, self.G = hc, G
+        self.mc, self.mco = _union_tables(hc.covs, hc.group, G)
+
+    def new_inputs(self, pcs, off, grp, pl):
+        is_new, mc, mco = oracle.novelty(pcs, off, grp, self.G, self.mc, self.mco, np.zeros(0, np.uint32))
+        self.mc, self.mco = mc, mco
+        for k in np.flatnonzero(is_new):
+            self.hc.covs.append(pcs[int(off[k]):int(off[k + 1])])
+            self.hc.group.append(grp[k])
+            self.hc.plen.append(pl[k])
+        return is_new.astype(bool)
+
+
+def _gate_batch(c, lo, hi, extra=()):
+    """Inputs lo..hi of c plus extra (cover, call) inputs, as CSR."""
+    covs = [c.pcs[int(c.off[i]):int(c.off[i + 1])] for i in range(lo, hi)] + [np.asarray(x, np.uint32)
+                                                                             for x, _ in extra]
+    grp = np.concatenate([c.group[lo:hi], np.array([g for _, g in extra], np.uint32)]).astype(np.uint32)
+    pl = np.concatenate([c.prog_len[lo:hi], np.ones(len(extra), np.uint16)]).astype(np.uint16)
+    pcs, off = oracle.to_csr(covs)
+    return pcs.astype(np.uint32), off.astype(np.uint64), grp, pl
+
+
+def _check_gate(st, model):
+    got_pcs, got_off = st.CorpusCover()
+    assert np.array_equal(got_off, model.mco) and np.array_equal(got_pcs, model.mc)
+    assert st.n == len(model.hc.covs)
+    _check(st, model.hc, model.G)
+
+
+@pytest.mark.parametrize("first", ["gate", "keep"])
+def test_new_input_gate_vs_oracle_novelty(first):
+    import torch
+    G = 13
+    a = synth.corpus(0x5EED00C1, 12_000, G, 60_000)
+    b = synth.corpus(0x5EED00C2, 30_000, G, 90_000)  # a wider PC space: some inputs bring new PCs
+    st = cover.CoverStore(a.pcs, a.off, a.group, G, a.prog_len)
+    hc = HostCorpus(a, 0, a.n)
+    if first == "keep":
+        # an explicit keep before any gate: corpusCover is taken first, the dropped entries' PCs stay in it
+        model = GateModel(hc, G)
+        idx = np.arange(0, a.n, 3)
+        st.keep(idx)
+        hc.keep(list(idx))
+    else:
+        model = GateModel(hc, G)
+    # 1: the first gate builds corpusCover; a batch of one, then a large one (the radix path), with an
+    # input that repeats an earlier one of the batch, one whose only new PC is the sentinel, and an empty one
+    for lo, hi in ((0, 1), (1, 1)):
+        pcs, off, grp, pl = _gate_batch(b, lo, hi)
+        assert np.array_equal(st.NewInputs(pcs, off, grp, pl), model.new_inputs(pcs, off, grp, pl))
+    dup = b.pcs[int(b.off[5]):int(b.off[6])]
+    extra = [(dup, int(b.group[5])), (np.array([0xFFFFFFFF], np.uint32), 0), (np.zeros(0, np.uint32), 1),
+             (np.array([1, 2, 0xFFFFFFFF], np.uint32), 2), (np.array([1, 2], np.uint32), 2)]
+    pcs, off, grp, pl = _gate_batch(b, 1, 20_000, extra)
+    is_new = st.NewInputs(pcs, off, grp, pl)
+    want = model.new_inputs(pcs, off, grp, pl)
+    assert np.array_equal(is_new, want)
+    assert 0 < want.sum() < want.size and not want[-4] and not want[-3] and want[-2] and not want[-1]
+    _check_gate(st, model)
+    # 2: device pointers, a small batch (the one-workgroup path)
+    s = torch.cuda.current_stream().cuda_stream
+    pcs, off, grp, pl = _gate_batch(b, 20_000, 20_200)
+    d_new = torch.zeros(200, dtype=torch.uint8, device="cuda")
+    na = st.NewInputsDevice(*(_dev(x) for x in (pcs, off, grp, pl)), 200, d_new, s)
+    want = model.new_inputs(pcs, off, grp, pl)
+    assert na == int(want.sum()) and np.array_equal(d_new.cpu().numpy().astype(bool), want)
+    _check_gate(st, model)
+    # 3: minimizeCorpus's keep leaves corpusCover as it is; an explicit keep drops entries, not PCs
+    C = int(max(a.prog_len.max(), b.prog_len.max()))
+    kept = st.MinimizeKeep(C, None, torch.zeros(C + 1, dtype=torch.int64, device="cuda"), None, None, s)
+    pcs_h, off_h, grp_h, _ = hc.csr()
+    wk, _ = oracle.minimize_grouped(pcs_h, off_h, grp_h, G)
+    assert kept == wk.size
+    hc.keep(list(wk))
+    perm = np.random.default_rng(9).permutation(len(hc.covs))[: len(hc.covs) // 2]
+    st.keep(perm)
+    hc.keep(list(perm))
+    _check_gate(st, model)
+    # 4: an unconditional append is unioned in too; then the rest of b through the gate
+    st.append(*_part(b, 20_200, 21_000))
+    hc.append(b, 20_200, 21_000)
+    model.mc, model.mco = _union_tables(
+        [model.mc[int(model.mco[g]):int(model.mco[g + 1])] for g in range(G)]
+        + [b.pcs[int(b.off[i]):int(b.off[i + 1])] for i in range(20_200, 21_000)],
+        list(range(G)) + list(b.group[20_200:21_000]), G)
+    pcs, off, grp, pl = _gate_batch(b, 21_000, b.n)
+    assert np.array_equal(st.NewInputs(pcs, off, grp, pl), model.new_inputs(pcs, off, grp, pl))
+    _check_gate(st, model)
+    # 5: the same batch again adds nothing
+    assert not st.NewInputs(pcs, off, grp, pl).any()
+    _check_gate(st, model)
+    st.close()
+
+
+def test_new_input_gate_rejects_bad_batches():
+    G = 5
+    a = synth.corpus(0x5EED00C3, 3_000, G, 20_000)
+    st = cover.CoverStore(a.pcs, a.off, a.group, G, a.prog_len)
+    hc = HostCorpus(a, 0, a.n)
+    model = GateModel(hc, G)
+    for covs, grp in (([np.array([5, 3], np.uint32)], [0]),        # not sorted
+                      ([np.array([7, 7], np.uint32)], [1]),        # a repeated PC
+                      ([np.array([1 << 30], np.uint32)], [G])):    # call id >= ngroups
+        pcs, off = oracle.to_csr(covs)
+        with pytest.raises(Exception):
+            st.NewInputs(pcs.astype(np.uint32), off.astype(np.uint64), np.array(grp, np.uint32))
+        _check_gate(st, model)  # unchanged
+    st.close()
