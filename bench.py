@@ -434,39 +434,60 @@ def store_leg(args, L, corp, d_pcs, d_off, d_grp, d_len, d_sel, d_hist, C, G, sp
 
 
 def append_leg(args, dev, store, sptr, C, d_hist):
-    """The manager's corpus cycle on the resident store: NewInput appends (manager.go:609-616,
-    mgr.corpus = append(...), in place, O(new)) of `--append` fresh programs in batches of 1000, then
-    minimizeCorpus with mgr.corpus = newCorpus (manager.go:507-529, syzgpu_corpus_minimize_keep_dev: the
-    raw pipeline, since the appends made the index stale, then the gather of the kept covers), then
-    CalculatePriorities + BuildChoiceTable on the kept length histogram. Two cycles; the second starts
-    from the first one's kept corpus."""
+    """The manager's corpus cycle on the resident store. NewInput (manager.go:609-616) is the gate on
+    corpusCover (syzgpu_corpus_new_inputs_dev: Difference -> skip, Union + append): `--append` fresh
+    programs in batches of 1000, each batch one call; then minimizeCorpus with mgr.corpus = newCorpus
+    (manager.go:507-529, syzgpu_corpus_minimize_keep_dev), then CalculatePriorities + BuildChoiceTable on
+    the kept length histogram. Two cycles, the second from the first one's kept corpus. Beside them:
+    single-program NewInput RPCs (gated and unconditional appends) timed one by one, and the one-time
+    build of corpusCover from the store's covers (the first gate's)."""
     import torch
     from syzkaller_amd import _lib, synth
     L = _lib.lib()
     b = synth.corpus(args.seed + 0x40, args.append, args.ngroups, args.npcs)
+    one = synth.corpus(args.seed + 0x41, 64, args.ngroups, args.npcs)
 
     def t(a):
         view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64, np.dtype(np.uint16): np.int16}
         return torch.from_numpy(np.ascontiguousarray(a).view(view.get(a.dtype, a.dtype))).to(dev)
+
+    def slices(c, batch):
+        out = []
+        for a in range(0, c.n, batch):
+            e = min(c.n, a + batch)
+            o = c.off[a:e + 1].astype(np.uint64)
+            out.append((t(c.pcs[int(o[0]):int(o[-1])]), t(o - o[0]), t(c.group[a:e]), t(c.prog_len[a:e]), e - a))
+        return out
     batch = 1000
-    parts = []
-    for a in range(0, b.n, batch):
-        e = min(b.n, a + batch)
-        o = b.off[a:e + 1].astype(np.uint64)
-        parts.append((t(b.pcs[int(o[0]):int(o[-1])]), t(o - o[0]), t(b.group[a:e]), t(b.prog_len[a:e]), e - a))
+    parts = slices(b, batch)
+    singles = slices(one, 1)
+    d_new = torch.zeros(batch, dtype=torch.uint8, device=dev)
     uses = static_usage(C)
     d_uses = t(uses)
     d_static = torch.empty((C, C), dtype=torch.float32, device=dev)
     d_prios = torch.empty((C, C), dtype=torch.float32, device=dev)
     d_run = torch.empty((C, C), dtype=torch.int64, device=dev)
+    empty = (t(np.zeros(1, np.uint32)), t(np.zeros(1, np.uint64)), t(np.zeros(1, np.uint32)),
+             t(np.zeros(1, np.uint16)), 0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    store.NewInputsDevice(*empty, None, sptr)  # corpusCover built from the store's covers
+    build_ms = (time.perf_counter() - t0) * 1e3
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3, r
     cycles = []
     for _ in range(2):
         n0 = store.n
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        per, acc = [], 0
         for d in parts:
-            store.append_device(*d, sptr)
-        torch.cuda.synchronize()
+            ms, na = timed(lambda: store.NewInputsDevice(*d, d_new, sptr))
+            per.append(ms)
+            acc += na
         t1 = time.perf_counter()
         kept = store.MinimizeKeep(C, None, d_hist, None, None, sptr)
         torch.cuda.synchronize()
@@ -476,12 +497,24 @@ def append_leg(args, dev, store, sptr, C, d_hist):
                                             d_run.data_ptr(), None, sptr))
         torch.cuda.synchronize()
         t3 = time.perf_counter()
-        cycles.append({"entries_before": int(n0), "appended": int(b.n), "kept": int(kept),
-                       "append_ms": round((t1 - t0) * 1e3, 3), "minimize_keep_ms": round((t2 - t1) * 1e3, 3),
-                       "prio_ms": round((t3 - t2) * 1e3, 3), "cycle_ms": round((t3 - t0) * 1e3, 3)})
-    return {"what": "manager cycle on the resident store: %d NewInput appends of %d programs, minimizeCorpus + "
-                    "keep (mgr.corpus = newCorpus), CalculatePriorities + ChoiceTable; two cycles"
-                    % (len(parts), batch), "cycles": cycles}
+        cycles.append({"entries_before": int(n0), "offered": int(b.n), "accepted": int(acc), "kept": int(kept),
+                       "new_input_ms": round(sum(per), 3),
+                       "new_input_1000_ms_median": round(float(np.median(per)), 3),
+                       "minimize_keep_ms": round((t2 - t1) * 1e3, 3), "prio_ms": round((t3 - t2) * 1e3, 3),
+                       "cycle_ms": round(sum(per) + (t3 - t1) * 1e3, 3)})
+    # single-program RPCs on the kept store: gated, then unconditional (a stale index after each)
+    g1 = [timed(lambda: store.NewInputsDevice(*d, d_new, sptr))[0] for d in singles[:32]]
+    u1 = [timed(lambda: store.append_device(*d, sptr))[0] for d in singles[32:]]
+    u1000 = [timed(lambda: store.append_device(*d, sptr))[0] for d in parts[:5]]
+    return {"what": "manager cycle on the resident store: %d gated NewInput batches of %d programs "
+                    "(corpusCover Difference -> skip, Union + append), minimizeCorpus + keep "
+                    "(mgr.corpus = newCorpus), CalculatePriorities + ChoiceTable; two cycles; then single-"
+                    "program NewInputs (gated / unconditional append) and unconditional 1000-program appends"
+                    % (len(parts), batch),
+            "corpus_cover_build_ms": round(build_ms, 3), "cycles": cycles,
+            "new_input_1_ms_median": round(float(np.median(g1)), 4),
+            "append_1_ms_median": round(float(np.median(u1)), 4),
+            "append_1000_ms_median": round(float(np.median(u1000)), 4)}
 
 
 def text_leg(args, dev, L, read_prof, corp, d_sel, sptr, ms_step):

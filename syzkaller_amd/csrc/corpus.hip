@@ -20,21 +20,20 @@ __global__ void k_shift_off(const uint64_t* off, size_t m, uint64_t base, uint64
     out[i] = off[i] + base;
 }
 
-__global__ void k_check_groups(const uint32_t* group, size_t m, uint32_t G, uint32_t* bad) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x)
+// bad[0] |= 1 for a call id >= G; bad[1] = max(bad[1], prog_len) (prog_len may be null)
+__global__ void k_check_groups(const uint32_t* group, const uint16_t* prog_len, size_t m, uint32_t G,
+                               uint32_t* bad) {
+  uint32_t mx = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
     if (group[i] >= G) atomicOr(bad, 1u);
-}
-
-__global__ void k_max_u16(const uint16_t* a, size_t n, uint32_t* mx) {
-  uint32_t m = 0;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    m = max(m, (uint32_t)a[i]);
+    if (prog_len) mx = max(mx, (uint32_t)prog_len[i]);
+  }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t o = __shfl_xor(m, d, 64);
-    m = o > m ? o : m;
+    const uint32_t o = __shfl_xor(mx, d, 64);
+    mx = o > mx ? o : mx;
   }
-  if (__lane_id() == 0 && m) atomicMax(mx, m);
+  if (__lane_id() == 0 && mx) atomicMax(&bad[1], mx);
 }
 
 // keep, metadata: the kept entries' cover lengths, call ids and program lengths, in output order
@@ -84,7 +83,7 @@ static void swap_grow(Grow<T>& a, Grow<T>& b) {
 }
 
 Corpus& corpus_index(CorpusHandle& H, hipStream_t s) {
-  if (H.index && (H.index->keep_pending || H.index->part_stale)) {
+  if (H.index && (H.index->keep_pending || H.index->app_pending || H.index->part_stale)) {
     try {
       corpus_index_sync(*H.index, H, s);
     } catch (...) {
@@ -100,7 +99,7 @@ Corpus& corpus_index(CorpusHandle& H, hipStream_t s) {
 }
 
 Corpus& corpus_index_full(CorpusHandle& H, hipStream_t s) {
-  if (H.index && H.index->incremental) H.index.reset();
+  if (H.index && (H.index->incremental || H.index->app_pending)) H.index.reset();
   return corpus_index(H, s);
 }
 
@@ -119,42 +118,34 @@ static void index_follow(CorpusHandle& H, F f) {
   }
 }
 
-static uint32_t max_len_dev(const uint16_t* a, size_t n, hipStream_t s) {
-  if (!n) return 0;
-  uint32_t* d = ctx().scratch.get<uint32_t>("co_max", 1);
-  uint32_t* h = ctx().pinned.get<uint32_t>(1);
-  SYZ_HIP(hipMemsetAsync(d, 0, 4, s));
-  k_max_u16<<<grid_for(n, 256, 1024), 256, 0, s>>>(a, n, d);
-  SYZ_LAUNCHED();
-  SYZ_HIP(hipMemcpyAsync(h, d, 4, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  return *h;
-}
-
 // covers (device pointers) appended after H's current ones; prog_len may be null (zeros)
 void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                    const uint16_t* prog_len, size_t m, hipStream_t s, bool cc_update) {
   if (!off || (m && !group)) fail(SYZGPU_EINVAL, "null pointer");
   uint64_t* h = ctx().pinned.get<uint64_t>(3);
-  uint32_t* bad = ctx().scratch.get<uint32_t>("co_bad", 1);
-  SYZ_HIP(hipMemsetAsync(bad, 0, 4, s));
+  uint32_t* bad = ctx().scratch.get<uint32_t>("co_bad", 2);
+  SYZ_HIP(hipMemsetAsync(bad, 0, 8, s));
   if (m) {  // checked before anything changes, so a rejected append leaves the corpus as it was
-    k_check_groups<<<grid_for(m, 256, 1024), 256, 0, s>>>(group, m, H.G, bad);
+    k_check_groups<<<grid_for(m, 256, 1024), 256, 0, s>>>(group, prog_len, m, H.G, bad);
     SYZ_LAUNCHED();
   }
   SYZ_HIP(hipMemcpyAsync(&h[0], off, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipMemcpyAsync(&h[1], off + m, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(&h[2], bad, 4, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
+  SYZ_HIP(hipMemcpyAsync(&h[2], bad, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));  // the append's one wait
   if (h[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
-  if ((uint32_t)h[2]) fail(SYZGPU_EINVAL, "group id >= ngroups");
+  const uint32_t* hb = reinterpret_cast<const uint32_t*>(&h[2]);
+  if (hb[0]) fail(SYZGPU_EINVAL, "group id >= ngroups");
+  const uint32_t maxlen = hb[1];
   const uint64_t Lm = h[1];
   if (Lm && !pcs) fail(SYZGPU_EINVAL, "null pointer");
   const size_t n = H.n, nt = n + m;
   const uint64_t L0 = H.L;
   if (nt >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
   if (cc_update) cc_add(H, pcs, off, group, m, Lm, s);  // corpusCover follows every append
-  index_follow(H, [&](Corpus& K) { corpus_index_sync(K, H, s); });  // a recorded keep first
+  index_follow(H, [&](Corpus& K) {  // a recorded keep first (the appends before it are applied by it)
+    if (K.keep_pending) corpus_index_sync(K, H, s);
+  });
   grow_keep(H.pcs, H.L, H.L + Lm + 1, s);
   grow_keep(H.off, n + 1, nt + 1, s);
   grow_keep(H.group, n, nt + 1, s);
@@ -165,11 +156,11 @@ void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, co
   if (m) SYZ_HIP(hipMemcpyAsync(H.group.p + n, group, m * 4, hipMemcpyDeviceToDevice, s));
   if (m && prog_len) SYZ_HIP(hipMemcpyAsync(H.prog_len.p + n, prog_len, m * 2, hipMemcpyDeviceToDevice, s));
   if (m && !prog_len) SYZ_HIP(hipMemsetAsync(H.prog_len.p + n, 0, m * 2, s));
-  H.max_prog_len = std::max(H.max_prog_len, prog_len ? max_len_dev(prog_len, m, s) : 0u);
+  H.max_prog_len = std::max(H.max_prog_len, maxlen);
   H.n = nt;
   H.L += Lm;
   H.path = 0;
-  index_follow(H, [&](Corpus& K) { corpus_index_append(K, H, n, L0, s); });
+  index_follow(H, [&](Corpus& K) { corpus_index_note_append(K, n, L0); });
 }
 
 static CorpusHandle* handle_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
@@ -528,7 +519,7 @@ int syzgpu_corpus_info(const syzgpu_corpus* cp, uint64_t* info, size_t cap) {
     if (!info) fail(SYZGPU_EINVAL, "null pointer");
     CorpusHandle& H = H_of(const_cast<syzgpu_corpus*>(cp));
     std::lock_guard<std::recursive_mutex> hl_(H.mu);
-    if (H.index && H.index->keep_pending) corpus_index(H, C_.stream);  // a recorded keep applied
+    if (H.index && (H.index->keep_pending || H.index->app_pending)) corpus_index(H, C_.stream);  // recorded changes applied
     uint64_t v[12] = {H.n, H.G, H.L, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (H.index) {
       const Corpus& K = *H.index;

@@ -4,6 +4,7 @@
 #include <mutex>
 #include <vector>
 
+#include "keyhash.hpp"
 #include "panels.hpp"
 
 namespace syz {
@@ -15,16 +16,10 @@ namespace syz {
 // (corpus_inc.hip); without an index (never built, or dropped by a failed update or key-space parts)
 // on the raw pipeline (panels.hip, no build). The index is built for what needs it: the cover
 // analytics, key-space parts, or an explicit reindex.
-// corpusCover (manager.go:65): sorted (call << 32 | PC) keys, main + sorted delta (corpus_cover.hip)
+// corpusCover (manager.go:65): a device hash set of (call << 32 | PC) keys (corpus_cover.hip)
 struct CoverSet {
-  DevArr<uint64_t> key, dkey, tmp;
-  size_t n = 0, dn = 0;
+  KeyHash h;
   bool built = false;
-  ~CoverSet() {
-    key.free();
-    dkey.free();
-    tmp.free();
-  }
 };
 
 struct CorpusHandle {
@@ -57,6 +52,7 @@ Corpus& corpus_index_full(CorpusHandle& H, hipStream_t s);
 // corpus_inc.hip: the index brought up to H after an append (H's entries from n0 and PCs from L0 are
 // new) or a keep (H = the old entries idx[0..m) of n0); they throw on failure (the caller drops it)
 void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L0, hipStream_t s);
+void corpus_index_note_append(Corpus& K, size_t n0, uint64_t L0);
 void corpus_index_keep(Corpus& K, const CorpusHandle& H, const int64_t* idx, size_t m, size_t n0, hipStream_t s);
 // a recorded keep applied (the index's users call it first: corpus_index does)
 void corpus_index_sync(Corpus& K, const CorpusHandle& H, hipStream_t s);

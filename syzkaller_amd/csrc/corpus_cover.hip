@@ -5,19 +5,21 @@
 //     mgr.corpusCover[call] = cover.Union(mgr.corpusCover[call], a.Cover)
 //     mgr.corpus = append(mgr.corpus, a.RpcInput)
 //
-// The set is the store's: sorted (call << 32 | PC) keys, a main array plus a small sorted DELTA of the
-// keys added since the last fold (the index dictionary's scheme, corpus_inc.hip), so an update costs
-// O(batch + delta), not O(set). It holds every cover the store has held (the manager's corpus only
-// grows through NewInput), built from the store's covers on first use — the first gate, or a keep that
-// could drop a call's PCs (minimizeCorpus's own keep cannot: Minimize keeps a first holder of every PC)
-// — and kept current by every append. PC 0xFFFFFFFF (cover.go's sentinel) is never in it: foreach
-// drops it from every Difference and Union.
+// The set is the store's: a device hash set of (call << 32 | PC) keys (keyhash.hpp), so a lookup is one
+// or two loads and an update is a CAS per new key, O(batch). It holds every cover the store has held
+// (the manager's corpus only grows through NewInput), built from the store's covers on first use — the
+// first gate, or a keep that could drop a call's PCs (minimizeCorpus's own keep cannot: Minimize keeps
+// a first holder of every PC) — and kept current by every append. PC 0xFFFFFFFF (cover.go's sentinel)
+// is never in it: foreach drops it from every Difference and Union.
 //
 // The gate over a batch without the sequential loop: a key x missing from corpusCover is brought in by
 // the FIRST input of the batch holding it (at that input x is still missing, so the input is accepted
 // and unions x in; every later holder sees x covered). So input k is accepted iff it is the first
-// holder of some missing key: one binary search per PC, one sort of the missing (key, input) pairs,
-// first-of-run flags (the first-occurrence form of the fuzzer's maxCover update, without flakes).
+// holder of some missing key (the first-occurrence form of the fuzzer's maxCover update, without
+// flakes). Two passes over the batch's PCs: (1) keys missing from corpusCover claim a slot in a batch
+// table and take the least input holding them (atomicMin); (2) each missing key's least holder is
+// accepted and inserts the key into corpusCover. Batches past CC_BT_MAX PCs sort their missing
+// (key, input) pairs instead.
 #include <algorithm>
 
 #include "corpus.hpp"
@@ -25,38 +27,217 @@
 
 namespace syz {
 
+// ---- the hash table (keyhash.hpp) ----------------------------------------------------------------
+
+__global__ void k_kh_rehash(const uint64_t* ok, const uint32_t* ov, uint64_t ocap, uint64_t* nk, uint32_t* nv,
+                            uint64_t nmask) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ocap; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = ok[i];
+    if (k == KH_EMPTY) continue;
+    uint64_t slot;
+    kh_insert(nk, nmask, k, &slot);
+    if (nv) nv[slot] = ov[i];
+  }
+}
+
+__global__ void k_kh_insert(uint64_t* keys, uint32_t* vals, uint64_t mask, const uint64_t* in, const uint32_t* inv,
+                            uint64_t n, unsigned long long* count) {
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = i0 + threadIdx.x;
+    bool c = false;
+    if (i < n) {
+      uint64_t slot;
+      c = kh_insert(keys, mask, in[i], &slot);
+      if (vals) vals[slot] = inv ? inv[i] : 0u;
+    }
+    kh_count_claims(count, c);
+  }
+}
+
+__global__ void k_kh_flag(const uint64_t* keys, uint64_t cap, uint32_t* f) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x)
+    f[i] = keys[i] != KH_EMPTY ? 1u : 0u;
+}
+
+__global__ void k_kh_compact(const uint64_t* keys, uint64_t cap, const uint32_t* f, const uint64_t* pos,
+                             uint64_t* out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x)
+    if (f[i]) out[pos[i]] = keys[i];
+}
+
+static uint64_t kh_cap_for(uint64_t n) {
+  uint64_t c = 1024;
+  while (c < 2 * n + 16) c <<= 1;
+  return c;
+}
+
+void kh_init(KeyHash& H, uint64_t n, bool with_vals, hipStream_t s) {
+  H.cap = kh_cap_for(n);
+  H.with_vals = with_vals;
+  H.keys.ensure(H.cap);
+  SYZ_HIP(hipMemsetAsync(H.keys.p, 0xFF, H.cap * 8, s));
+  if (with_vals) H.vals.ensure(H.cap);
+  H.count.ensure(1);
+  SYZ_HIP(hipMemsetAsync(H.count.p, 0, 8, s));
+  H.bound = 0;
+}
+
+void kh_reserve(KeyHash& H, uint64_t more, hipStream_t s) {
+  if (2 * (H.bound + more) + 16 <= H.cap) return;
+  unsigned long long* hc = ctx().pinned.get<unsigned long long>(1);  // the exact count first
+  SYZ_HIP(hipMemcpyAsync(hc, H.count.p, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  H.bound = *hc;
+  if (2 * (H.bound + more) + 16 <= H.cap) return;
+  const uint64_t ncap = kh_cap_for(2 * (H.bound + more));  // room for as many again
+  DevArr<uint64_t> nk;
+  DevArr<uint32_t> nv;
+  nk.alloc(ncap);
+  SYZ_HIP(hipMemsetAsync(nk.p, 0xFF, ncap * 8, s));
+  if (H.with_vals) nv.alloc(ncap);
+  k_kh_rehash<<<grid_for(H.cap, 256, 16384), 256, 0, s>>>(H.keys.p, H.with_vals ? H.vals.p : nullptr, H.cap, nk.p,
+                                                         H.with_vals ? nv.p : nullptr, ncap - 1);
+  SYZ_LAUNCHED();
+  SYZ_HIP(hipStreamSynchronize(s));
+  std::swap(H.keys.p, nk.p);
+  std::swap(H.keys.n, nk.n);
+  std::swap(H.vals.p, nv.p);
+  std::swap(H.vals.n, nv.n);
+  H.cap = ncap;
+  nk.free();
+  nv.free();
+}
+
+void kh_insert_sorted(KeyHash& H, const uint64_t* keys, const uint32_t* vals, uint64_t n, hipStream_t s) {
+  if (!n) return;
+  kh_reserve(H, n, s);
+  k_kh_insert<<<grid_for(n, 256, 16384), 256, 0, s>>>(H.keys.p, H.with_vals ? H.vals.p : nullptr, H.mask(), keys,
+                                                     vals, n, H.count.p);
+  SYZ_LAUNCHED();
+  H.bound += n;
+}
+
+uint64_t kh_export_sorted(KeyHash& H, uint64_t** out, hipStream_t s) {
+  Scratch& sc = ctx().scratch;
+  uint32_t* f = sc.get<uint32_t>("kh_f", H.cap + 1);
+  uint64_t* pos = sc.get<uint64_t>("kh_pos", H.cap + 1);
+  k_kh_flag<<<grid_for(H.cap, 256, 16384), 256, 0, s>>>(H.keys.p, H.cap, f);
+  SYZ_LAUNCHED();
+  exclusive_scan_u32(f, pos, H.cap, s);
+  uint64_t* hn = ctx().pinned.get<uint64_t>(1);
+  SYZ_HIP(hipMemcpyAsync(hn, pos + H.cap, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  const uint64_t n = *hn;
+  uint64_t* k = sc.get<uint64_t>("kh_out", n + 1);
+  uint64_t* kt = sc.get<uint64_t>("kh_outt", n + 1);
+  uint32_t* v = sc.get<uint32_t>("kh_outv", n + 1);
+  uint32_t* vt = sc.get<uint32_t>("kh_outvt", n + 1);
+  k_kh_compact<<<grid_for(H.cap, 256, 16384), 256, 0, s>>>(H.keys.p, H.cap, f, pos, k);
+  SYZ_LAUNCHED();
+  SYZ_HIP(hipMemsetAsync(v, 0, n * 4 + 4, s));
+  radix_sort_pairs(k, v, kt, vt, n, 44, s);
+  *out = k;
+  return n;
+}
+
 namespace {
 
 constexpr uint32_t CC_SENT = 0xFFFFFFFFu;
-constexpr int CC_SMALL = 4096;  // missing pairs sorted in one workgroup's LDS (composite keys)
-constexpr int CC_SMALL_BLOCK = 1024;
+constexpr uint64_t CC_BT_MAX = 1ull << 22;  // batch PCs up to which the gate uses a batch table
 
-__device__ __forceinline__ bool cc_has(const uint64_t* a, uint64_t n, uint64_t key) {
-  const uint64_t x = lower_bound_dev<uint64_t>(a, 0, n, key);
-  return x < n && a[x] == key;
-}
-
-// one wave per cover: miss[p] = its (call, PC) key is in neither the main set nor the delta;
-// err |= 1 for a call id >= G, |= 2 for a cover that is not strictly increasing
-__global__ __launch_bounds__(256) void k_cc_lookup(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
-                                                   size_t m, uint32_t G, const uint64_t* key, uint64_t nk,
-                                                   const uint64_t* dkey, uint64_t ndk, int strict,
-                                                   uint32_t* miss, uint32_t* err) {
+// gate pass 1, one wave per input: err |= 1 for a call id >= G, |= 2 for a cover that is not strictly
+// increasing; a key missing from corpusCover (miss[p] = 1) claims a batch-table slot and keeps the
+// least input holding it
+__global__ __launch_bounds__(256) void k_cc_gate1(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                                  size_t m, uint32_t G, const uint64_t* cc, uint64_t ccmask,
+                                                  uint64_t* bt, uint32_t* btv, uint64_t btmask, uint8_t* miss,
+                                                  uint32_t* err) {
   const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
-  const uint64_t base = off[0];
   for (size_t e = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < m; e += waves) {
     const uint32_t g = group[e];
     const uint64_t a = off[e], b = off[e + 1];
     if (g >= G) {
       if (__lane_id() == 0) atomicOr(err, 1u);
-      for (uint64_t p = a + __lane_id(); p < b; p += 64) miss[p - base] = 0;
+      for (uint64_t p = a + __lane_id(); p < b; p += 64) miss[p] = 0;
       continue;
     }
     for (uint64_t p = a + __lane_id(); p < b; p += 64) {
       const uint32_t pc = pcs[p];
-      if (strict && p > a && pcs[p - 1] >= pc) atomicOr(err, 2u);
+      if (p > a && pcs[p - 1] >= pc) atomicOr(err, 2u);
       const uint64_t k = ((uint64_t)g << 32) | pc;
-      miss[p - base] = (pc != CC_SENT && !cc_has(key, nk, k) && !(ndk && cc_has(dkey, ndk, k))) ? 1u : 0u;
+      const bool ms = pc != CC_SENT && kh_find(cc, ccmask, k) == KH_EMPTY;
+      miss[p] = ms ? 1 : 0;
+      if (ms) {
+        uint64_t slot;
+        kh_insert(bt, btmask, k, &slot);
+        atomicMin(&btv[slot], (uint32_t)e);
+      }
+    }
+  }
+}
+
+// gate pass 2: the least holder of each missing key is accepted and puts the key into corpusCover
+__global__ __launch_bounds__(256) void k_cc_gate2(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                                  size_t m, const uint8_t* miss, const uint64_t* bt,
+                                                  const uint32_t* btv, uint64_t btmask, uint64_t* cc,
+                                                  uint64_t ccmask, unsigned long long* cccount, uint8_t* acc) {
+  const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t e = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < m; e += waves) {
+    const uint64_t g = group[e];
+    bool any = false;
+    for (uint64_t p0 = off[e]; p0 < off[e + 1]; p0 += 64) {
+      const uint64_t p = p0 + __lane_id();
+      bool claimed = false;
+      if (p < off[e + 1] && miss[p]) {
+        const uint64_t k = (g << 32) | pcs[p];
+        if (btv[kh_find(bt, btmask, k)] == (uint32_t)e) {
+          any = true;
+          uint64_t slot;
+          claimed = kh_insert(cc, ccmask, k, &slot);
+        }
+      }
+      kh_count_claims(cccount, claimed);
+    }
+    if (__ballot(any) && __lane_id() == 0) acc[e] = 1;
+  }
+}
+
+// an unconditional append: every key of the covers into corpusCover (covers need not be canonical)
+__global__ __launch_bounds__(256) void k_cc_add(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                                size_t m, uint64_t* cc, uint64_t ccmask,
+                                                unsigned long long* cccount) {
+  const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t e = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < m; e += waves) {
+    const uint64_t g = group[e];
+    for (uint64_t p0 = off[e]; p0 < off[e + 1]; p0 += 64) {
+      const uint64_t p = p0 + __lane_id();
+      bool claimed = false;
+      if (p < off[e + 1] && pcs[p] != CC_SENT) {
+        uint64_t slot;
+        claimed = kh_insert(cc, ccmask, (g << 32) | pcs[p], &slot);
+      }
+      kh_count_claims(cccount, claimed);
+    }
+  }
+}
+
+// large batches: the missing flags (u32, for the scan) and the checks of pass 1, no batch table
+__global__ __launch_bounds__(256) void k_cc_lookup(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                                                   size_t m, uint32_t G, const uint64_t* cc, uint64_t ccmask,
+                                                   uint32_t* miss, uint32_t* err) {
+  const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t e = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < m; e += waves) {
+    const uint32_t g = group[e];
+    const uint64_t a = off[e], b = off[e + 1];
+    if (g >= G) {
+      if (__lane_id() == 0) atomicOr(err, 1u);
+      for (uint64_t p = a + __lane_id(); p < b; p += 64) miss[p] = 0;
+      continue;
+    }
+    for (uint64_t p = a + __lane_id(); p < b; p += 64) {
+      const uint32_t pc = pcs[p];
+      if (p > a && pcs[p - 1] >= pc) atomicOr(err, 2u);
+      miss[p] = (pc != CC_SENT && kh_find(cc, ccmask, ((uint64_t)g << 32) | pc) == KH_EMPTY) ? 1u : 0u;
     }
   }
 }
@@ -66,67 +247,18 @@ __global__ __launch_bounds__(256) void k_cc_pairs(const uint32_t* pcs, const uin
                                                   size_t m, const uint32_t* miss, const uint64_t* mpos,
                                                   uint64_t* mk, uint32_t* mv) {
   const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
-  const uint64_t base = off[0];
   for (size_t e = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < m; e += waves) {
     const uint64_t g = group[e];
     for (uint64_t p = off[e] + __lane_id(); p < off[e + 1]; p += 64)
-      if (miss[p - base]) {
-        const uint64_t q = mpos[p - base];
+      if (miss[p]) {
+        const uint64_t q = mpos[p];
         mk[q] = (g << 32) | pcs[p];
         mv[q] = (uint32_t)e;
       }
   }
 }
 
-// small batches (n <= CC_SMALL pairs, inputs < 2^20): one workgroup sorts key << 20 | input in LDS
-// (bitonic), flags the first holder of every key (acc) and writes the distinct keys (u, *nu)
-__global__ __launch_bounds__(CC_SMALL_BLOCK) void k_cc_small(const uint64_t* mk, const uint32_t* mv, uint32_t n,
-                                                             uint32_t np2, uint8_t* acc, uint64_t* u,
-                                                             uint64_t* nu) {
-  __shared__ uint64_t s[CC_SMALL];
-  __shared__ uint32_t wsum[CC_SMALL_BLOCK / 64];
-  const uint32_t t = threadIdx.x;
-  for (uint32_t i = t; i < np2; i += CC_SMALL_BLOCK) s[i] = i < n ? (mk[i] << 20) | mv[i] : ~0ull;
-  __syncthreads();
-  for (uint32_t k = 2; k <= np2; k <<= 1)
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = t; i < np2 / 2; i += CC_SMALL_BLOCK) {
-        const uint32_t lo = 2 * j * (i / j) + (i % j), hi = lo + j;
-        const uint64_t a = s[lo], b = s[hi];
-        if ((a > b) == ((lo & k) == 0)) {
-          s[lo] = b;
-          s[hi] = a;
-        }
-      }
-      __syncthreads();
-    }
-  // each thread owns CC_SMALL / CC_SMALL_BLOCK consecutive slots
-  constexpr uint32_t PER = CC_SMALL / CC_SMALL_BLOCK;
-  uint32_t f = 0, cnt = 0;
-  for (uint32_t r = 0; r < PER; r++) {
-    const uint32_t i = t * PER + r;
-    const bool first = i < n && (i == 0 || (s[i] >> 20) != (s[i - 1] >> 20));
-    f |= (first ? 1u : 0u) << r;
-    cnt += first;
-    if (first) acc[(uint32_t)(s[i] & 0xFFFFFu)] = 1;
-  }
-  uint32_t x = cnt;  // block exclusive scan of cnt
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if ((int)__lane_id() >= d) x += y;
-  }
-  if (__lane_id() == 63) wsum[t >> 6] = x;
-  __syncthreads();
-  uint32_t wbase = 0;
-  for (uint32_t w = 0; w < (t >> 6); w++) wbase += wsum[w];
-  uint32_t pos = wbase + x - cnt;
-  for (uint32_t r = 0; r < PER; r++)
-    if ((f >> r) & 1u) u[pos++] = s[t * PER + r] >> 20;
-  if (t == CC_SMALL_BLOCK - 1) *nu = wbase + x;
-}
-
-// large batches, after a stable sort of the pairs by key: first-of-run flags and the first holders
+// after a stable sort of the pairs by key: the first of each key's run accepts its input
 __global__ void k_cc_first(const uint64_t* k, const uint32_t* v, uint64_t n, uint8_t* acc, uint32_t* f) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const bool first = i == 0 || k[i] != k[i - 1];
@@ -138,18 +270,6 @@ __global__ void k_cc_first(const uint64_t* k, const uint32_t* v, uint64_t n, uin
 __global__ void k_cc_ucompact(const uint64_t* k, uint64_t n, const uint32_t* f, const uint64_t* pos, uint64_t* u) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     if (f[i]) u[pos[i]] = k[i];
-}
-
-// merge of two sorted key lists that share no key: each key's place = its index + the other list's
-// keys below it
-__global__ void k_cc_merge(const uint64_t* a, uint64_t na, const uint64_t* b, uint64_t nb, uint64_t* out) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    if (i < na)
-      out[i + lower_bound_dev<uint64_t>(b, 0, nb, a[i])] = a[i];
-    else
-      out[i - na + lower_bound_dev<uint64_t>(a, 0, na, b[i - na])] = b[i - na];
-  }
 }
 
 // one wave per entry: its cover's keys (the sentinel PC as ~0: sorted last, dropped by the unique pass)
@@ -203,7 +323,7 @@ __global__ __launch_bounds__(256) void k_cc_gather(const uint32_t* pcs, const ui
   }
 }
 
-// corpusCover's keys as PCs, and each call's first place
+// corpusCover's sorted keys as PCs, and each call's first place
 __global__ void k_cc_export(const uint64_t* k, uint64_t n, uint32_t G, uint32_t* out, uint64_t* out_off) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + G + 1;
        i += (uint64_t)gridDim.x * blockDim.x) {
@@ -216,89 +336,80 @@ __global__ void k_cc_export(const uint64_t* k, uint64_t n, uint32_t G, uint32_t*
 
 unsigned wave_grid(size_t m) { return (unsigned)std::min<size_t>((m * 64 + 255) / 256 + 1, 65536); }
 
-void swap_arr(DevArr<uint64_t>& a, DevArr<uint64_t>& b) {
-  std::swap(a.p, b.p);
-  std::swap(a.n, b.n);
-}
-
-// the delta's keys folded into the main array
-void cc_fold(CoverSet& S, hipStream_t s) {
-  if (!S.dn) return;
-  const uint64_t nt = S.n + S.dn;
-  S.tmp.ensure(nt + 1);
-  k_cc_merge<<<grid_for(nt, 256, 16384), 256, 0, s>>>(S.key.p, S.n, S.dkey.p, S.dn, S.tmp.p);
-  SYZ_LAUNCHED();
-  swap_arr(S.key, S.tmp);
-  S.n = nt;
-  S.dn = 0;
-}
-
-// The batch's missing keys: acc[e] = 1 for the first holder of each (acc may be null: an unconditional
-// append, whose covers need not be canonical), the distinct keys left in the scratch "cc_u" (count
-// returned). Throws on bad input before anything changes.
-uint64_t cc_classify(CoverSet& S, const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t m,
-                     uint64_t Lm, uint32_t G, uint8_t* acc, hipStream_t s) {
-  Scratch& sc = ctx().scratch;
-  uint32_t* miss = sc.get<uint32_t>("cc_miss", Lm + 1);
-  uint64_t* mpos = sc.get<uint64_t>("cc_mpos", Lm + 1);
-  uint32_t* err = sc.get<uint32_t>("cc_err", 1);
-  uint64_t* dnu = sc.get<uint64_t>("cc_nu", 1);
-  SYZ_HIP(hipMemsetAsync(err, 0, 4, s));
-  if (m) {
-    k_cc_lookup<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, m, G, S.key.p, S.n, S.dkey.p, S.dn, acc != nullptr,
-                                             miss, err);
-    SYZ_LAUNCHED();
-  }
-  exclusive_scan_u32(miss, mpos, Lm, s);
-  uint64_t* h = ctx().pinned.get<uint64_t>(2);
-  SYZ_HIP(hipMemcpyAsync(&h[0], mpos + Lm, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(&h[1], err, 4, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  const uint64_t nmiss = h[0];
-  const uint32_t e = (uint32_t)h[1];
+void cc_fail(uint32_t e) {
   if (e & 1) fail(SYZGPU_EINVAL, "group id >= ngroups");
   if (e & 2) fail(SYZGPU_EINVAL, "NewInput covers must be canonical (strictly increasing)");
-  if (!nmiss) return 0;
-  uint64_t* mk = sc.get<uint64_t>("cc_mk", nmiss + 1);
-  uint32_t* mv = sc.get<uint32_t>("cc_mv", nmiss + 1);
-  uint64_t* u = sc.get<uint64_t>("cc_u", nmiss + 1);
-  uint8_t* a8 = acc ? acc : sc.get<uint8_t>("cc_acc0", m + 1);
-  k_cc_pairs<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, m, miss, mpos, mk, mv);
-  SYZ_LAUNCHED();
-  if (nmiss <= (uint64_t)CC_SMALL && m < (1u << 20)) {
-    uint32_t np2 = 64;
-    while (np2 < nmiss) np2 <<= 1;
-    k_cc_small<<<1, CC_SMALL_BLOCK, 0, s>>>(mk, mv, (uint32_t)nmiss, np2, a8, u, dnu);
-    SYZ_LAUNCHED();
-  } else {
-    uint64_t* mkt = sc.get<uint64_t>("cc_mkt", nmiss + 1);
-    uint32_t* mvt = sc.get<uint32_t>("cc_mvt", nmiss + 1);
-    radix_sort_pairs(mk, mv, mkt, mvt, nmiss, 44, s);  // stable: each key's pairs stay in input order
-    uint32_t* f = sc.get<uint32_t>("cc_f", nmiss + 1);
-    uint64_t* fpos = sc.get<uint64_t>("cc_fpos", nmiss + 1);
-    k_cc_first<<<grid_for(nmiss, 256, 8192), 256, 0, s>>>(mk, mv, nmiss, a8, f);
-    SYZ_LAUNCHED();
-    exclusive_scan_u32(f, fpos, nmiss, s);
-    k_cc_ucompact<<<grid_for(nmiss, 256, 8192), 256, 0, s>>>(mk, nmiss, f, fpos, u);
-    SYZ_LAUNCHED();
-    SYZ_HIP(hipMemcpyAsync(dnu, fpos + nmiss, 8, hipMemcpyDeviceToDevice, s));
-  }
-  SYZ_HIP(hipMemcpyAsync(&h[0], dnu, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  return h[0];
 }
 
-// the distinct missing keys of the last classify (scratch "cc_u") merged into the delta
-void cc_commit(CoverSet& S, uint64_t nu, hipStream_t s) {
-  if (!nu) return;
-  const uint64_t* u = ctx().scratch.get<uint64_t>("cc_u", nu + 1);
-  const uint64_t nt = S.dn + nu;
-  S.tmp.ensure(nt + 1);
-  k_cc_merge<<<grid_for(nt, 256, 16384), 256, 0, s>>>(S.dkey.p, S.dn, u, nu, S.tmp.p);
-  SYZ_LAUNCHED();
-  swap_arr(S.dkey, S.tmp);
-  S.dn = nt;
-  if (S.dn > std::max<uint64_t>(1ull << 20, S.n / 8)) cc_fold(S, s);
+// acc[e] = 1 for the first holder of a missing key, the keys inserted into corpusCover; returns the
+// number accepted (apos = the exclusive scan of acc). Throws on bad input before anything changes.
+uint64_t cc_gate(KeyHash& S, const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t m, uint64_t Lm,
+                 uint32_t G, uint8_t* acc, uint64_t* apos, hipStream_t s) {
+  Scratch& sc = ctx().scratch;
+  uint32_t* err = sc.get<uint32_t>("cc_err", 1);
+  uint64_t* h = ctx().pinned.get<uint64_t>(2);
+  SYZ_HIP(hipMemsetAsync(err, 0, 4, s));
+  if (m) SYZ_HIP(hipMemsetAsync(acc, 0, m, s));
+  kh_reserve(S, Lm, s);
+  if (Lm <= CC_BT_MAX) {
+    const uint64_t bcap = kh_cap_for(Lm);
+    uint64_t* bt = sc.get<uint64_t>("cc_bt", bcap);
+    uint32_t* btv = sc.get<uint32_t>("cc_btv", bcap);
+    uint8_t* miss = sc.get<uint8_t>("cc_miss8", Lm + 1);
+    SYZ_HIP(hipMemsetAsync(bt, 0xFF, bcap * 8, s));
+    SYZ_HIP(hipMemsetAsync(btv, 0xFF, bcap * 4, s));
+    if (m) {
+      k_cc_gate1<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, m, G, S.keys.p, S.mask(), bt, btv, bcap - 1, miss, err);
+      SYZ_LAUNCHED();
+    }
+    // the checks are read before pass 2 changes corpusCover (a rejected batch changes nothing)
+    SYZ_HIP(hipMemcpyAsync(&h[0], err, 4, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    cc_fail((uint32_t)h[0]);
+    if (m) {
+      k_cc_gate2<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, m, miss, bt, btv, bcap - 1, S.keys.p, S.mask(),
+                                              S.count.p, acc);
+      SYZ_LAUNCHED();
+    }
+    S.bound += Lm;
+  } else {
+    uint32_t* miss = sc.get<uint32_t>("cc_miss", Lm + 1);
+    uint64_t* mpos = sc.get<uint64_t>("cc_mpos", Lm + 1);
+    k_cc_lookup<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, m, G, S.keys.p, S.mask(), miss, err);
+    SYZ_LAUNCHED();
+    exclusive_scan_u32(miss, mpos, Lm, s);
+    SYZ_HIP(hipMemcpyAsync(&h[0], mpos + Lm, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipMemcpyAsync(&h[1], err, 4, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    cc_fail((uint32_t)h[1]);
+    const uint64_t nmiss = h[0];
+    if (nmiss) {
+      uint64_t* mk = sc.get<uint64_t>("cc_mk", nmiss + 1);
+      uint32_t* mv = sc.get<uint32_t>("cc_mv", nmiss + 1);
+      uint64_t* mkt = sc.get<uint64_t>("cc_mkt", nmiss + 1);
+      uint32_t* mvt = sc.get<uint32_t>("cc_mvt", nmiss + 1);
+      k_cc_pairs<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, m, miss, mpos, mk, mv);
+      SYZ_LAUNCHED();
+      radix_sort_pairs(mk, mv, mkt, mvt, nmiss, 44, s);  // stable: each key's pairs stay in input order
+      uint32_t* f = sc.get<uint32_t>("cc_f", nmiss + 1);
+      uint64_t* fpos = sc.get<uint64_t>("cc_fpos", nmiss + 1);
+      k_cc_first<<<grid_for(nmiss, 256, 8192), 256, 0, s>>>(mk, mv, nmiss, acc, f);
+      SYZ_LAUNCHED();
+      exclusive_scan_u32(f, fpos, nmiss, s);
+      uint64_t* u = sc.get<uint64_t>("cc_u", nmiss + 1);
+      k_cc_ucompact<<<grid_for(nmiss, 256, 8192), 256, 0, s>>>(mk, nmiss, f, fpos, u);
+      SYZ_LAUNCHED();
+      // the distinct keys are u[0, fpos[nmiss]); the rest of u is not written: insert up to nmiss with
+      // the count read first
+      SYZ_HIP(hipMemcpyAsync(&h[0], fpos + nmiss, 8, hipMemcpyDeviceToHost, s));
+      SYZ_HIP(hipStreamSynchronize(s));
+      kh_insert_sorted(S, u, nullptr, h[0], s);
+    }
+  }
+  exclusive_scan_u8(acc, apos, m, s);
+  SYZ_HIP(hipMemcpyAsync(&h[0], apos + m, 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  return h[0];
 }
 
 }  // namespace
@@ -329,23 +440,26 @@ void cc_ensure(CorpusHandle& H, hipStream_t s) {
   SYZ_HIP(hipMemcpyAsync(h, pos + L, 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   const uint64_t nu = *h;
-  S.key.ensure(nu + 1);
+  uint64_t* u = kt;  // (the sort's other buffer is free now)
   if (L) {
-    k_cc_ucompact<<<grid_for(L, 256, 8192), 256, 0, s>>>(k, L, f, pos, S.key.p);
+    k_cc_ucompact<<<grid_for(L, 256, 8192), 256, 0, s>>>(k, L, f, pos, u);
     SYZ_LAUNCHED();
   }
-  S.dkey.ensure(1024);
-  S.n = nu;
-  S.dn = 0;
+  kh_init(S.h, 2 * nu + (1u << 20), false, s);  // room to grow before the first rehash
+  kh_insert_sorted(S.h, u, nullptr, nu, s);
   S.built = true;
   SYZ_HIP(hipStreamSynchronize(s));
-  pt.mark("sort_unique", s);
+  pt.mark("sort_unique_insert", s);
 }
 
 void cc_add(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t m,
             uint64_t Lm, hipStream_t s) {
-  if (!H.cc.built) return;
-  cc_commit(H.cc, cc_classify(H.cc, pcs, off, group, m, Lm, H.G, nullptr, s), s);
+  if (!H.cc.built || !m) return;
+  KeyHash& S = H.cc.h;
+  kh_reserve(S, Lm, s);
+  k_cc_add<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, m, S.keys.p, S.mask(), S.count.p);
+  SYZ_LAUNCHED();
+  S.bound += Lm;
 }
 
 uint64_t corpus_new_inputs(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
@@ -361,55 +475,41 @@ uint64_t corpus_new_inputs(CorpusHandle& H, const uint32_t* pcs, const uint64_t*
   if (h[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
   const uint64_t Lm = h[1];
   if (Lm && !pcs) fail(SYZGPU_EINVAL, "null pointer");
-  uint8_t* acc = sc.get<uint8_t>("cc_acc", m + 1);
-  if (m) SYZ_HIP(hipMemsetAsync(acc, 0, m, s));
-  const uint64_t nu = cc_classify(H.cc, pcs, off, group, m, Lm, H.G, acc, s);
-  pt.mark("classify", s);
-  uint64_t na = 0;
-  if (nu) {
-    uint64_t* apos = sc.get<uint64_t>("cc_apos", m + 1);
-    exclusive_scan_u8(acc, apos, m, s);
-    SYZ_HIP(hipMemcpyAsync(&h[0], apos + m, 8, hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
-    na = h[0];
-    if (na == m) {
-      append_covers(H, pcs, off, group, prog_len, m, s, false);
-    } else {
-      uint32_t* len = sc.get<uint32_t>("cc_len", m + 1);
-      uint64_t* off2 = sc.get<uint64_t>("cc_off2", na + 1);
-      uint64_t* lpos = sc.get<uint64_t>("cc_lpos", m + 1);
-      k_cc_lens<<<grid_for(m, 256, 4096), 256, 0, s>>>(off, acc, m, len);
-      SYZ_LAUNCHED();
-      exclusive_scan_u32(len, lpos, m, s);
-      uint32_t* pcs2 = sc.get<uint32_t>("cc_pcs2", Lm + 1);
-      uint32_t* group2 = sc.get<uint32_t>("cc_grp2", na + 1);
-      uint16_t* pl2 = prog_len ? sc.get<uint16_t>("cc_pl2", na + 1) : nullptr;
-      k_cc_offs<<<grid_for(m + 1, 256, 4096), 256, 0, s>>>(acc, apos, lpos, m, off2);
-      SYZ_LAUNCHED();
-      k_cc_gather<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, prog_len, acc, apos, m, off2, pcs2, group2, pl2);
-      SYZ_LAUNCHED();
-      append_covers(H, pcs2, off2, group2, pl2, na, s, false);
-    }
-    cc_commit(H.cc, nu, s);
+  uint8_t* acc = is_new ? is_new : sc.get<uint8_t>("cc_acc", m + 1);
+  uint64_t* apos = sc.get<uint64_t>("cc_apos", m + 1);
+  const uint64_t na = cc_gate(H.cc.h, pcs, off, group, m, Lm, H.G, acc, apos, s);
+  pt.mark("gate", s);
+  if (na == m) {
+    append_covers(H, pcs, off, group, prog_len, m, s, false);
+  } else if (na) {
+    uint32_t* len = sc.get<uint32_t>("cc_len", m + 1);
+    uint64_t* lpos = sc.get<uint64_t>("cc_lpos", m + 1);
+    uint64_t* off2 = sc.get<uint64_t>("cc_off2", na + 1);
+    k_cc_lens<<<grid_for(m, 256, 4096), 256, 0, s>>>(off, acc, m, len);
+    SYZ_LAUNCHED();
+    exclusive_scan_u32(len, lpos, m, s);
+    uint32_t* pcs2 = sc.get<uint32_t>("cc_pcs2", Lm + 1);
+    uint32_t* group2 = sc.get<uint32_t>("cc_grp2", na + 1);
+    uint16_t* pl2 = prog_len ? sc.get<uint16_t>("cc_pl2", na + 1) : nullptr;
+    k_cc_offs<<<grid_for(m + 1, 256, 4096), 256, 0, s>>>(acc, apos, lpos, m, off2);
+    SYZ_LAUNCHED();
+    k_cc_gather<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, prog_len, acc, apos, m, off2, pcs2, group2, pl2);
+    SYZ_LAUNCHED();
+    append_covers(H, pcs2, off2, group2, pl2, na, s, false);
   }
-  if (is_new && m) SYZ_HIP(hipMemcpyAsync(is_new, acc, m, hipMemcpyDefault, s));
-  SYZ_HIP(hipStreamSynchronize(s));
   pt.mark("append", s);
   return na;
 }
 
 uint64_t cc_export(CorpusHandle& H, uint32_t* out, uint64_t* out_off, uint64_t cap, hipStream_t s) {
   cc_ensure(H, s);
-  CoverSet& S = H.cc;
-  const uint64_t nt = S.n + S.dn;
-  if (nt > cap) return nt;
-  uint64_t* all = ctx().scratch.get<uint64_t>("cc_all", nt + 1);
-  k_cc_merge<<<grid_for(nt, 256, 16384), 256, 0, s>>>(S.key.p, S.n, S.dkey.p, S.dn, all);
-  SYZ_LAUNCHED();
-  k_cc_export<<<grid_for(nt + H.G + 1, 256, 16384), 256, 0, s>>>(all, nt, H.G, out, out_off);
+  uint64_t* k = nullptr;
+  const uint64_t n = kh_export_sorted(H.cc.h, &k, s);
+  if (n > cap) return n;
+  k_cc_export<<<grid_for(n + H.G + 1, 256, 16384), 256, 0, s>>>(k, n, H.G, out, out_off);
   SYZ_LAUNCHED();
   SYZ_HIP(hipStreamSynchronize(s));
-  return nt;
+  return n;
 }
 
 }  // namespace syz

@@ -462,6 +462,10 @@ void merge_delta(Corpus& K, hipStream_t s) {
 
 void corpus_index_sync(Corpus& K, const CorpusHandle& H, hipStream_t s) {
   if (K.keep_pending) apply_keep(K, H, s);  // (partitions and composes the work itself)
+  if (K.app_pending) {  // the appends since the last user, as one batch
+    K.app_pending = false;
+    corpus_index_append(K, H, K.app_n0, K.app_L0, s);
+  }
   if (K.part_stale) {  // appends since the last partition: the group partition and the work list
     PhaseTimer pt("index_sync");
     std::vector<uint64_t> hpcs;
@@ -655,6 +659,15 @@ void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L
   K.ptail = nt;
   K.part_stale = true;  // 5. the work list (body items + each panel's tail) with the next partition
   pt.mark("vectors", s);
+}
+
+// H has just taken the entries from n0 (PCs from L0): recorded, indexed by the index's next user
+// (corpus_index_sync) together with any later appends, so a NewInput costs the covers' copy only
+void corpus_index_note_append(Corpus& K, size_t n0, uint64_t L0) {
+  if (K.app_pending) return;  // the pending range already starts earlier
+  K.app_pending = true;
+  K.app_n0 = n0;
+  K.app_L0 = L0;
 }
 
 // H has just become the entries idx[0..m) (device, old ids) of a corpus of n0 entries: recorded, and

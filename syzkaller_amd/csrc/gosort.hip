@@ -1548,18 +1548,28 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   }
   // the small call groups (packed) are independent of the big ones: sort them on the side stream
   // while the main stream runs the global levels
+  // A/B knob SYZGPU_GS_HIPRI=1: the big groups' rounds on a side stream of the greatest priority, so
+  // their short dependent launches are dispatched ahead of the transpose's workgroups as CUs free up
+  const bool hipri = getenv("SYZGPU_GS_HIPRI") != nullptr;
+  int least = 0, greatest = 0;
+  SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   if (!c.side) {
-    SYZ_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    if (hipri)
+      SYZ_HIP(hipStreamCreateWithPriority(&c.side, hipStreamNonBlocking, greatest));
+    else
+      SYZ_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
   }
   const bool fork = P.npacks && P.nbig && !getenv("SYZGPU_GS_NOFORK");
-  hipStream_t ss = fork ? c.side : s;
+  // the forked class runs on the side stream: the small groups by default, the big ones with hipri
+  hipStream_t ss = fork && !hipri ? c.side : s;
+  hipStream_t bs = fork && hipri ? c.side : s;
+  if (fork) {
+    SYZ_HIP(hipEventRecord(c.ev_fork, s));
+    SYZ_HIP(hipStreamWaitEvent(c.side, c.ev_fork, 0));
+  }
   if (P.npacks) {
-    if (fork) {
-      SYZ_HIP(hipEventRecord(c.ev_fork, s));
-      SYZ_HIP(hipStreamWaitEvent(ss, c.ev_fork, 0));
-    }
     {
       ProfScope ps("gosort_lds_small", ss, (uint64_t)n * 12);
       launch_ls<LS_SH, uint32_t>(el, perm, d_packs, P.npacks, nullptr, std::min<uint32_t>(P.npacks, 65535), d_small,
@@ -1570,7 +1580,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, ss);
   }
   if (small_done) small_done(ss);
-  if (fork) SYZ_HIP(hipEventRecord(c.ev_join, ss));
+  if (fork && !hipri) SYZ_HIP(hipEventRecord(c.ev_join, ss));
   // global levels: the host issues level after level without waiting; each level's segment count is
   // copied back asynchronously and the host stops issuing once a finished level reports zero
   // (levels issued after the last real one find nseg == 0 and return at once).
@@ -1597,10 +1607,10 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     // idle workgroups of a grid-stride kernel still cost dispatch time on every launch
     const size_t segs_max = P.big_total / tch + P.nbig + 1;
     const unsigned tgrid = (unsigned)std::min<size_t>(P.big_total / GL_TILE + segs_max, 2048);
-    ProfScope ps("gosort_level", s, 0);
+    ProfScope ps("gosort_level", bs, 0);
     const uint32_t epoch = (++c.gr_epoch & 0x7FFFu) | 0x8000u;
-    SYZ_HIP(hipMemsetAsync(lvl[0].plan, 0, sizeof(GPlan), s));
-    k_gl_init<<<std::min<uint32_t>(nbig, 1024), 64, 0, s>>>(el, P.big, nbig, lvl[0], ctl, epoch);
+    SYZ_HIP(hipMemsetAsync(lvl[0].plan, 0, sizeof(GPlan), bs));
+    k_gl_init<<<std::min<uint32_t>(nbig, 1024), 64, 0, bs>>>(el, P.big, nbig, lvl[0], ctl, epoch);
     SYZ_LAUNCHED();
     // Default: the rounds as captured graphs of 3 launches each. SYZGPU_GR_PERSIST=1: all rounds in one
     // persistent launch with grid barriers (k_gr_persist). Measured slower at config 4 (global rounds
@@ -1622,17 +1632,17 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
       const unsigned want = pg ? (unsigned)std::max(1, atoi(pg)) : 256u;
       const unsigned pgrid = std::min<unsigned>(std::min<unsigned>(tgrid, want), c.gr_resident);
       uint32_t* bar = sc.get<uint32_t>("gs_bar", 1);
-      SYZ_HIP(hipMemsetAsync(bar, 0, 4, s));
+      SYZ_HIP(hipMemsetAsync(bar, 0, 4, bs));
       constexpr uint32_t MAXR = 512;
       if (wt)
-        k_gr_persist<true><<<pgrid, GL_BLOCK, 0, s>>>(el, lvl[0], lvl[1], tcnt, A, B, VA, VB, ctl, dlds, heap, bar, MAXR);
+        k_gr_persist<true><<<pgrid, GL_BLOCK, 0, bs>>>(el, lvl[0], lvl[1], tcnt, A, B, VA, VB, ctl, dlds, heap, bar, MAXR);
       else
-        k_gr_persist<false><<<pgrid, GL_BLOCK, 0, s>>>(el, lvl[0], lvl[1], tcnt, A, B, VA, VB, ctl, dlds, heap, bar, MAXR);
+        k_gr_persist<false><<<pgrid, GL_BLOCK, 0, bs>>>(el, lvl[0], lvl[1], tcnt, A, B, VA, VB, ctl, dlds, heap, bar, MAXR);
       SYZ_LAUNCHED();
       if (getenv("SYZGPU_GS_DEBUG")) {
         GCtl h;
-        SYZ_HIP(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipStreamSynchronize(s));
+        SYZ_HIP(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, bs));
+        SYZ_HIP(hipStreamSynchronize(bs));
         fprintf(stderr, "gosort: persistent grid %u, %u rounds\n", pgrid, h.round & 0xFFFFu);
       }
     } else {
@@ -1689,7 +1699,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
       uint32_t issued = 0, seen = 0;
       auto launch = [&](uint32_t k) {
         if (issued + k > MAXR) fail(SYZGPU_EINTERNAL, "gosort: round limit");
-        SYZ_HIP(hipGraphLaunch(graph((int)(issued & 1), k), s));
+        SYZ_HIP(hipGraphLaunch(graph((int)(issued & 1), k), bs));
         issued += k;
       };
       bool done = false;
@@ -1715,7 +1725,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
           launch(RPG);
           continue;
         }
-        if (hipStreamQuery(s) == hipSuccess) {  // everything issued has run
+        if (hipStreamQuery(bs) == hipSuccess) {  // everything issued has run
           if ((done = poll())) break;
           if (seen < issued) fail(SYZGPU_EINTERNAL, "gosort: no progress word from the rounds");
           launch(RPG);
@@ -1725,23 +1735,24 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
       }
       P.rounds_hint = last_rounds;
       if (getenv("SYZGPU_GS_DEBUG")) {
-        SYZ_HIP(hipStreamSynchronize(s));
+        SYZ_HIP(hipStreamSynchronize(bs));
         fprintf(stderr, "gosort: %u rounds issued, %u with segments\n", issued, last_rounds);
       }
     }
     // children that reached the LDS size and depth-exhausted big ones: counts stay on the device
-    k_gs_heap<<<64, 64, 0, s>>>(el, heap, &ctl[0].nheap);
+    k_gs_heap<<<64, 64, 0, bs>>>(el, heap, &ctl[0].nheap);
     SYZ_LAUNCHED();
     // the LDS-sized children of all levels, one workgroup each ([0, nlds) via &ctl[0].nnext == 0);
     // running them per level beside the levels was measured slower: they take the CUs the
     // latency-bound level kernels need
     {
-      ProfScope ps2("gosort_lds", s, (uint64_t)n * 12);
-      launch_ls<LS_SH, uint32_t>(el, perm, nullptr, 0, &ctl[0].nnext, 1024, dlds, &ctl[2].nlds, bounceD, s);
+      ProfScope ps2("gosort_lds", bs, (uint64_t)n * 12);
+      launch_ls<LS_SH, uint32_t>(el, perm, nullptr, 0, &ctl[0].nnext, 1024, dlds, &ctl[2].nlds, bounceD, bs);
     }
-    launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nlds, bounceD, s);
+    launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nlds, bounceD, bs);
   }
-  if (big_done) big_done(s);
+  if (big_done) big_done(bs);
+  if (fork && hipri) SYZ_HIP(hipEventRecord(c.ev_join, bs));
   if (fork) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
   (void)dpacks;
 }

@@ -13,7 +13,7 @@ constexpr uint32_t PCAP = SYZ_PCAP;  // PCs per chunk (the LDS staging buffer of
 constexpr uint32_t MEMB = 64;     // members per block: a 6-bit member tag in each element
 constexpr uint32_t WMAX = 1024;   // windows per call group
 #ifndef SYZ_DS
-#define SYZ_DS 15
+#define SYZ_DS 14
 #endif
 #ifndef SYZ_PBM_WORDS
 #define SYZ_PBM_WORDS 6144

@@ -187,8 +187,10 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
   __shared__ uint32_t st[EMIT ? SO_T : 1];
   __shared__ uint32_t red[SO_BLOCK / 64 + 1];
   __shared__ uint32_t meta[6];
-  const uint64_t tile = blockIdx.x;
-  if (tile >= tstart[npairs]) return;
+  // a grid of a few workgroups per CU walks the tiles (one workgroup per tile made the launch's
+  // dispatch the bound: ~1M short workgroups per batch)
+  const uint64_t ntiles = tstart[npairs];
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   if (threadIdx.x < 64) {  // wave 0: the tile's diagonals (a one-tile pair needs no search)
     const uint32_t p = tpair[tile];
     const uint64_t a0 = aoff[p], b0 = boff[p];
@@ -281,12 +283,20 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
   const uint32_t pre = block_excl_scan<SO_BLOCK>(c, red, &tot);
   if (!EMIT) {
     if (threadIdx.x == 0) tcnt[tile] = tot;
-    return;
+  } else {
+    for (uint32_t k = 0; k < c; k++) st[pre + k] = outv[k];
+    __syncthreads();
+    uint32_t* o = out + tout[tile];
+    for (uint32_t k = threadIdx.x; k < tot; k += SO_BLOCK) o[k] = st[k];
   }
-  for (uint32_t k = 0; k < c; k++) st[pre + k] = outv[k];
-  __syncthreads();
-  uint32_t* o = out + tout[tile];
-  for (uint32_t k = threadIdx.x; k < tot; k += SO_BLOCK) o[k] = st[k];
+  __syncthreads();  // the tile's LDS is free for the next one
+  }  // tiles
+}
+
+// workgroups of a tile walk: enough to fill the CUs several times over (env SYZGPU_SO_GRID for A/B)
+static unsigned so_grid(uint64_t tiles) {
+  static const unsigned cap = getenv("SYZGPU_SO_GRID") ? (unsigned)atoi(getenv("SYZGPU_SO_GRID")) : 8192u;
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, cap));
 }
 
 // out_off[p] = tout[tstart[p]] (a pair without tiles: the next one's start)
@@ -322,8 +332,8 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
   SYZ_LAUNCHED();
   {
     ProfScope ps("setop_count", s, 4 * (na + nb) + 16 * (uint64_t)npairs);
-    k_so_tile<false><<<(unsigned)tbound, SO_BLOCK, 0, s>>>(op, a, aoff, b, boff, npairs, tstart, tpair, tcnt, nullptr,
-                                                            nullptr, fl, fl + 1);
+    k_so_tile<false><<<so_grid(tbound), SO_BLOCK, 0, s>>>(op, a, aoff, b, boff, npairs, tstart, tpair, tcnt, nullptr,
+                                                           nullptr, fl, fl + 1);
     SYZ_LAUNCHED();
   }
   uint64_t* hnt = c.pinned.get<uint64_t>(2);
@@ -345,8 +355,8 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
   if (total > out_cap) fail(SYZGPU_ECAPACITY, "set operation output capacity too small");
   if (ntiles) {
     ProfScope ps("setop_emit", s, 4 * (na + nb) + 4 * total + 8 * (uint64_t)npairs);
-    k_so_tile<true><<<(unsigned)ntiles, SO_BLOCK, 0, s>>>(op, a, aoff, b, boff, npairs, tstart, tpair, nullptr, tout, out,
-                                                          nullptr, nullptr);
+    k_so_tile<true><<<so_grid(ntiles), SO_BLOCK, 0, s>>>(op, a, aoff, b, boff, npairs, tstart, tpair, nullptr, tout, out,
+                                                         nullptr, nullptr);
     SYZ_LAUNCHED();
   }
   return total;
@@ -497,11 +507,12 @@ __global__ void k_store_len(const uint64_t* pos, uint64_t n, uint64_t* out_len, 
 }
 
 // ---- Canonicalize on a device-resident CSR (no host copy of the offsets) --------------------------
-// Covers are classed on the device by length (wave-aggregated appends to three lists): <= 512 PCs
-// take a 256-thread workgroup with a 2 KB LDS bitonic sort (eight workgroups per CU), <= 2048 a
-// 512-thread one, <= 16384 (kCoverSize) the 1024-thread k_canon_lds; longer ones (not produced by
-// kcov) go through the global network one by one. After the sort: unique with last = sentinel and
-// the in-place store of the kept prefix (cover.go:28-40), the new length to out_len.
+// Covers are classed on the device by length (wave-aggregated appends to five lists): <= 512 and
+// <= 1024 PCs take one wave each, in registers (k_canon_wave below; SYZGPU_CANON_LDS=1: the workgroup
+// LDS sorters instead), <= 2048 a 512-thread workgroup with an LDS bitonic sort, <= 16384 (kCoverSize)
+// a 1024-thread one; longer ones (not produced by kcov) go through the global network one by one.
+// After the sort: unique with last = sentinel and the in-place store of the kept prefix
+// (cover.go:28-40), the new length to out_len.
 template <uint32_t PMAX, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_canon_cls(uint32_t* pcs, const uint64_t* off, const uint32_t* list,
                                                      const uint32_t* nlist_dev, uint64_t* out_len) {
@@ -550,17 +561,85 @@ __global__ __launch_bounds__(BLOCK) void k_canon_cls(uint32_t* pcs, const uint64
   }
 }
 
-// cls lists: [0] <= 512, [1] <= 2048, [2] <= 16384, [3] longer; cnt[4]
+// One WAVE per cover of <= 64 R PCs, the cover in registers (element e = r * 64 + lane: coalesced loads
+// and stores): a bitonic network over the next power of two >= its length (>= 64), compare-exchanges
+// across registers in place and across lanes by xor shuffles, no LDS and no barriers; then unique
+// (cover.go:28-40: a PC is kept iff it differs from the one before, the first against the sentinel)
+// and the kept PCs stored in place at their ballot ranks. Four independent waves per workgroup walk
+// the class list.
+template <int R>
+__global__ __launch_bounds__(256) void k_canon_wave(uint32_t* pcs, const uint64_t* off, const uint32_t* list,
+                                                    const uint32_t* nlist_dev, uint64_t* out_len) {
+  const uint32_t nlist = *nlist_dev;
+  const unsigned lane = __lane_id();
+  const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t li = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); li < nlist; li += waves) {
+    const uint32_t seg = list[li];
+    const uint64_t beg = off[seg];
+    const uint32_t n = (uint32_t)(off[seg + 1] - beg);
+    uint32_t P = 64;
+    while (P < n) P <<= 1;
+    const uint32_t nr = P >> 6;  // registers in use (uniform)
+    uint32_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint32_t e = (uint32_t)r * 64 + lane;
+      x[r] = e < n ? pcs[beg + e] : SENT;
+    }
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        if (j >= 64) {  // partner register r ^ (j / 64), same lane
+          const uint32_t jr = j >> 6;
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            if ((uint32_t)r >= nr || (r & jr)) continue;
+            const int r2 = r ^ (int)jr;
+            const uint32_t a = x[r], b = x[r2];
+            const bool up = (((uint32_t)r * 64 + lane) & k) == 0;
+            x[r] = up ? min(a, b) : max(a, b);
+            x[r2] = up ? max(a, b) : min(a, b);
+          }
+        } else {  // partner lane lane ^ j, same register
+          const bool lower = (lane & j) == 0;
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            if ((uint32_t)r >= nr) continue;
+            const uint32_t y = (uint32_t)__shfl_xor((int)x[r], (int)j, 64);
+            const bool up = (((uint32_t)r * 64 + lane) & k) == 0;
+            x[r] = (lower == up) ? min(x[r], y) : max(x[r], y);
+          }
+        }
+      }
+    }
+    uint32_t kept = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if ((uint32_t)r >= nr) continue;
+      const uint32_t e = (uint32_t)r * 64 + lane;
+      uint32_t prev = (uint32_t)__shfl_up((int)x[r], 1, 64);
+      const uint32_t last = r ? (uint32_t)__builtin_amdgcn_readlane((int)x[r > 0 ? r - 1 : 0], 63) : SENT;
+      if (lane == 0) prev = last;
+      const bool keep = e < n && x[r] != prev;
+      const uint64_t b = __ballot(keep);
+      if (keep) pcs[beg + kept + (uint32_t)__popcll(b & lanemask_lt())] = x[r];
+      kept += (uint32_t)__popcll(b);
+    }
+    if (lane == 0) out_len[seg] = kept;
+  }
+}
+
+// cls lists: [0] <= 512, [1] <= 1024, [2] <= 2048, [3] <= 16384, [4] longer; cnt[5]
+constexpr int CANON_NCLS = 5;
 __global__ void k_canon_class(const uint64_t* off, size_t ncov, uint32_t* lists, size_t cap, uint32_t* cnt) {
   for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < ncov; i0 += (size_t)gridDim.x * blockDim.x) {
     const size_t i = i0 + threadIdx.x;
     int c = -1;
     if (i < ncov) {
       const uint64_t n = off[i + 1] - off[i];
-      c = n <= 512 ? 0 : n <= 2048 ? 1 : n <= (uint64_t)CANON_LDS ? 2 : 3;
+      c = n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= (uint64_t)CANON_LDS ? 3 : 4;
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < CANON_NCLS; k++) {
       const uint64_t m = __ballot(c == k);
       if (!m) continue;
       const unsigned leader = (unsigned)__ffsll((unsigned long long)m) - 1;
@@ -576,30 +655,40 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   Context& c = ctx();
   if (ncov == 0) return;
   if (ncov >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many covers");
-  uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", 4 * ncov);
-  uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", 4);
-  SYZ_HIP(hipMemsetAsync(cnt, 0, 16, s));
+  uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", CANON_NCLS * ncov);
+  uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", CANON_NCLS);
+  SYZ_HIP(hipMemsetAsync(cnt, 0, CANON_NCLS * 4, s));
   k_canon_class<<<grid_for(ncov, 256, 8192), 256, 0, s>>>(off, ncov, lists, ncov, cnt);
   SYZ_LAUNCHED();
   if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
   const unsigned ncu = (unsigned)std::max(1, c.ncu);
+  static const bool lds = getenv("SYZGPU_CANON_LDS") != nullptr;  // A/B: the workgroup LDS sorters
   {
     ProfScope ps("canon_small", s, 0);
-    k_canon_cls<512, 256><<<ncu * 8, 256, 0, s>>>(pcs, off, lists, cnt, out_len);
-    SYZ_LAUNCHED();
+    if (lds) {
+      k_canon_cls<512, 256><<<ncu * 8, 256, 0, s>>>(pcs, off, lists, cnt, out_len);
+      SYZ_LAUNCHED();
+      k_canon_cls<2048, 512><<<ncu * 4, 512, 0, s>>>(pcs, off, lists + ncov, cnt + 1, out_len);
+      SYZ_LAUNCHED();
+    } else {
+      k_canon_wave<8><<<ncu * 8, 256, 0, s>>>(pcs, off, lists, cnt, out_len);
+      SYZ_LAUNCHED();
+      k_canon_wave<16><<<ncu * 6, 256, 0, s>>>(pcs, off, lists + ncov, cnt + 1, out_len);
+      SYZ_LAUNCHED();
+    }
   }
-  k_canon_cls<2048, 512><<<ncu * 4, 512, 0, s>>>(pcs, off, lists + ncov, cnt + 1, out_len);
+  k_canon_cls<2048, 512><<<ncu * 4, 512, 0, s>>>(pcs, off, lists + 2 * ncov, cnt + 2, out_len);
   SYZ_LAUNCHED();
-  k_canon_cls<CANON_LDS, CANON_BLOCK><<<ncu * 2, CANON_BLOCK, 0, s>>>(pcs, off, lists + 2 * ncov, cnt + 2, out_len);
+  k_canon_cls<CANON_LDS, CANON_BLOCK><<<ncu * 2, CANON_BLOCK, 0, s>>>(pcs, off, lists + 3 * ncov, cnt + 3, out_len);
   SYZ_LAUNCHED();
   // longer covers: their list back to the host, then the global network one by one
-  uint32_t* h = c.pinned.get<uint32_t>(4);
-  SYZ_HIP(hipMemcpyAsync(h, cnt, 16, hipMemcpyDeviceToHost, s));
+  uint32_t* h = c.pinned.get<uint32_t>(CANON_NCLS);
+  SYZ_HIP(hipMemcpyAsync(h, cnt, CANON_NCLS * 4, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
-  const uint32_t nbig = h[3];
+  const uint32_t nbig = h[4];
   if (!nbig) return;
   std::vector<uint32_t> big(nbig);
-  SYZ_HIP(hipMemcpyAsync(big.data(), lists + 3 * ncov, nbig * 4, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(big.data(), lists + 4 * ncov, nbig * 4, hipMemcpyDeviceToHost, s));
   std::vector<uint64_t> hoff(2);
   for (uint32_t seg : big) {
     SYZ_HIP(hipMemcpyAsync(hoff.data(), off + seg, 16, hipMemcpyDeviceToHost, s));

@@ -144,6 +144,9 @@ struct Corpus {
   DevArr<uint32_t> sd_id, dl_id;    // merge) dictionaries
   size_t sd_n = 0, dl_n = 0;
   bool part_stale = false;  // appends since the last group partition / work list (redone lazily)
+  bool app_pending = false;  // entries [app_n0, the covers' n) appended, not yet indexed (next user)
+  size_t app_n0 = 0;
+  uint64_t app_L0 = 0;
   bool sd_built = false, incremental = false;
   std::vector<VecWork> hmain;  // the items over the panel-major body of the stream (no tails)
   std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint64_t>> ptail;  // panel -> appended range
