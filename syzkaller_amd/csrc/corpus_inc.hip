@@ -556,10 +556,11 @@ void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L
     SYZ_HIP(hipMemcpyAsync(K.dl_id.p, i2, nt * 4, hipMemcpyDeviceToDevice, s));
     K.dl_n = nt;
     if (K.dl_n > std::max<uint64_t>(1ull << 20, K.sd_n / 8)) merge_delta(K, s);
-    uint64_t* hu = ctx().pinned.get<uint64_t>(nu + 1);
-    SYZ_HIP(hipMemcpyAsync(hu, u, nu * 8, hipMemcpyDeviceToHost, s));
+    // the new ids per call: ubeg's differences (G + 1 words back, not the nu keys)
+    uint64_t* hub = ctx().pinned.get<uint64_t>(G + 1);
+    SYZ_HIP(hipMemcpyAsync(hub, ubeg, (G + 1) * 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
-    for (uint64_t k = 0; k < nu; k++) K.hnids[hu[k] >> 32]++;
+    for (uint32_t g = 0; g < G; g++) K.hnids[g] += hub[g + 1] - hub[g];
     K.total_ids += nu;
   }
   pt.mark("ids", s);
@@ -576,7 +577,7 @@ void corpus_index_append(Corpus& K, const CorpusHandle& H, size_t n0, uint64_t L
   std::vector<uint64_t> hclen(m);
   std::vector<uint32_t> hsp(hsb[m] + 1);
   if (m) {
-    canonicalize_batch_dev(ids, rel, hrel.data(), m, clen, s);
+    canonicalize_batch_dev2(ids, rel, m, clen, s);
     k_splits<<<grid_for(m, 256, 4096), 256, 0, s>>>(ids, rel, H.group.p + n0, m, K.nwin.p, sbase, splits);
     SYZ_LAUNCHED();
     SYZ_HIP(hipMemcpyAsync(hclen.data(), clen, m * 8, hipMemcpyDeviceToHost, s));

@@ -1548,23 +1548,16 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   }
   // the small call groups (packed) are independent of the big ones: sort them on the side stream
   // while the main stream runs the global levels
-  // A/B knob SYZGPU_GS_HIPRI=1: the big groups' rounds on a side stream of the greatest priority, so
-  // their short dependent launches are dispatched ahead of the transpose's workgroups as CUs free up
-  const bool hipri = getenv("SYZGPU_GS_HIPRI") != nullptr;
-  int least = 0, greatest = 0;
-  SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  // (the big groups' rounds on a stream of the greatest priority measured no faster beside the
+  // transpose: r04_t1, 2.988 vs 2.983 ms)
   if (!c.side) {
-    if (hipri)
-      SYZ_HIP(hipStreamCreateWithPriority(&c.side, hipStreamNonBlocking, greatest));
-    else
-      SYZ_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+    SYZ_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
   }
   const bool fork = P.npacks && P.nbig && !getenv("SYZGPU_GS_NOFORK");
-  // the forked class runs on the side stream: the small groups by default, the big ones with hipri
-  hipStream_t ss = fork && !hipri ? c.side : s;
-  hipStream_t bs = fork && hipri ? c.side : s;
+  hipStream_t ss = fork ? c.side : s;  // the small groups' stream
+  hipStream_t bs = s;                  // the big groups'
   if (fork) {
     SYZ_HIP(hipEventRecord(c.ev_fork, s));
     SYZ_HIP(hipStreamWaitEvent(c.side, c.ev_fork, 0));
@@ -1577,10 +1570,13 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     }
     // packs with a length that does not fit the u32 element (>= 2^19 PCs) were bounced: the u64
     // instantiation sorts them (a launch over an empty bounce list returns at once)
-    launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, ss);
+    // (skipped when no cover can bounce: even an empty launch of its 64 KB-LDS workgroups waits for whole
+    // CUs while the transpose runs beside the sort)
+    if (P.may_bounce)
+      launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, ss);
   }
   if (small_done) small_done(ss);
-  if (fork && !hipri) SYZ_HIP(hipEventRecord(c.ev_join, ss));
+  if (fork) SYZ_HIP(hipEventRecord(c.ev_join, ss));
   // global levels: the host issues level after level without waiting; each level's segment count is
   // copied back asynchronously and the host stops issuing once a finished level reports zero
   // (levels issued after the last real one find nseg == 0 and return at once).
@@ -1749,10 +1745,10 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
       ProfScope ps2("gosort_lds", bs, (uint64_t)n * 12);
       launch_ls<LS_SH, uint32_t>(el, perm, nullptr, 0, &ctl[0].nnext, 1024, dlds, &ctl[2].nlds, bounceD, bs);
     }
-    launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nlds, bounceD, bs);
+    if (P.may_bounce)
+      launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nlds, bounceD, bs);
   }
   if (big_done) big_done(bs);
-  if (fork && hipri) SYZ_HIP(hipEventRecord(c.ev_join, bs));
   if (fork) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
   (void)dpacks;
 }

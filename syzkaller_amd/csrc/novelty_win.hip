@@ -254,6 +254,7 @@ constexpr uint32_t NH_PER = HS / NH_BLOCK;  // table slots per thread at compact
 constexpr uint32_t NH_FLK = 512;         // flakes of a window kept in LDS for the lookup
 constexpr uint32_t NH_NB_BITS = 11;      // order buckets of a sub-range: 2048
 constexpr uint32_t NH_NB = 1u << NH_NB_BITS;
+constexpr uint32_t NH_BSCAN = 64;        // keys of a bucket placed by a scan of it; more: the sort
 static_assert(NH_NB + HS <= 2 * HS && NH_NB % NH_BLOCK == 0, "bucket counts and list in the table's space");
 
 __device__ __forceinline__ uint32_t hslot_nw(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - HS_BITS); }
@@ -297,6 +298,7 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
   constexpr uint32_t NH_WBLK = 128;  // the walk's element windows: 8K elements (its scratch fits beside)
   __shared__ uint32_t wsc[2 * NH_BLOCK + 3 * NH_WBLK];
   __shared__ uint64_t red64[NH_BLOCK / 64 + 1];
+  __shared__ uint32_t bmax;  // the largest order bucket of the sub-range
   uint32_t* keys = tabs;
   uint32_t* vals = tabs + HS;
   const uint32_t j = (uint32_t)upper_bound_dev<uint32_t>(iofs, 0, G + 1, blockIdx.x) - 1;
@@ -416,6 +418,7 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
     const uint32_t bsh = sh > NH_NB_BITS ? sh - NH_NB_BITS : 0u;
     const uint32_t sbase = split ? rr << sh : 0u;
     for (uint32_t i = threadIdx.x; i < NH_NB; i += NH_BLOCK) bcnt[i] = 0;
+    if (threadIdx.x == 0) bmax = 0;
     __syncthreads();
     uint32_t pib[NH_PER];  // place inside the bucket, or none
 #pragma unroll
@@ -424,12 +427,14 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
     __syncthreads();
     {
       constexpr uint32_t PERB = NH_NB / NH_BLOCK;  // buckets per thread
-      uint32_t x[PERB], c = 0;
+      uint32_t x[PERB], c = 0, mx = 0;
 #pragma unroll
       for (uint32_t k = 0; k < PERB; k++) {
         x[k] = bcnt[threadIdx.x * PERB + k];
         c += x[k];
+        mx = max(mx, x[k]);
       }
+      if (mx > NH_BSCAN || (dbg & 16)) atomicMax(&bmax, mx + 1);
       uint32_t nk;
       uint32_t pre = block_excl_scan<NH_BLOCK>(c, red, &nk);
 #pragma unroll
@@ -442,15 +447,35 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
       for (uint32_t q = 0; q < NH_PER; q++)
         if (pib[q] != 0xFFFFFFFFu) blist[bcnt[(kk[q] - sbase) >> bsh] + pib[q]] = kk[q];
       __syncthreads();
+      if (bmax == 0) {  // every bucket holds a few keys: a key's place by a scan of its bucket
 #pragma unroll
-      for (uint32_t q = 0; q < NH_PER; q++)
-        if (pib[q] != 0xFFFFFFFFu) {
-          const uint32_t bk = (kk[q] - sbase) >> bsh;
-          const uint32_t b0 = bcnt[bk], b1 = bk + 1 < NH_NB ? bcnt[bk + 1] : nk;
-          uint32_t r = b0;
-          for (uint32_t i = b0; i < b1; i++) r += blist[i] < kk[q] ? 1u : 0u;
-          out[kc + r] = kk[q];
-        }
+        for (uint32_t q = 0; q < NH_PER; q++)
+          if (pib[q] != 0xFFFFFFFFu) {
+            const uint32_t bk = (kk[q] - sbase) >> bsh;
+            const uint32_t b0 = bcnt[bk], b1 = bk + 1 < NH_NB ? bcnt[bk + 1] : nk;
+            uint32_t r = b0;
+            for (uint32_t i = b0; i < b1; i++) r += blist[i] < kk[q] ? 1u : 0u;
+            out[kc + r] = kk[q];
+          }
+      } else {  // clustered PCs (a bucket past NH_BSCAN keys): a bitonic sort of the sub-range's keys
+        uint32_t P = 64;
+        while (P < nk) P <<= 1;
+        for (uint32_t i = nk + threadIdx.x; i < P; i += NH_BLOCK) blist[i] = 0xFFFFFFFFu;
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1)
+          for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P / 2; t += NH_BLOCK) {
+              const uint32_t i = ((t & ~(jj - 1)) << 1) | (t & (jj - 1)), ij = i | jj;
+              const uint32_t a = blist[i], b = blist[ij];
+              if ((a > b) == ((i & k) == 0)) {
+                blist[i] = b;
+                blist[ij] = a;
+              }
+            }
+            __syncthreads();
+          }
+        for (uint32_t i = threadIdx.x; i < nk; i += NH_BLOCK) out[kc + i] = blist[i];
+      }
       kc += nk;
     }
     round++;
@@ -536,7 +561,9 @@ static int nw_dbg() {
 // output
 static int nwh_dbg() {
   static const int v = getenv("SYZGPU_NWH_DBG") ? atoi(getenv("SYZGPU_NWH_DBG")) : 0;
-  return v;
+  // SYZGPU_NWH_SORT=1 (read per call; results unchanged): every sub-range ordered by the sort
+  const char* so = getenv("SYZGPU_NWH_SORT");
+  return v | (so && atoi(so) ? 16 : 0);
 }
 
 // SYZGPU_NW_BITS=14|15: direct window bits (default: 14 while the span fits 1024 such windows, else 15)

@@ -40,15 +40,20 @@ static unsigned span_blocks() {
 }
 
 // ---- per-entry statistics: PCs per call group and the PC span --------------------------------------
+// (*mlmax: the longest cover, which tells the Go sort whether a pack can need its u64 element)
 __global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
-                                                   size_t n, uint32_t G, uint64_t* gpcs, uint32_t* span) {
+                                                   size_t n, uint32_t G, uint64_t* gpcs, uint32_t* span,
+                                                   uint32_t* mlmax) {
   extern __shared__ unsigned long long lsum[];
+  __shared__ uint32_t lmax;
   for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) lsum[g] = 0;
+  if (threadIdx.x == 0) lmax = 0;
   __syncthreads();
-  uint32_t lo = 0xFFFFFFFFu, hi = 0;
+  uint32_t lo = 0xFFFFFFFFu, hi = 0, mx = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const uint64_t a = off[i], b = off[i + 1];
     const uint32_t g = group[i];
+    mx = max(mx, (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull));
     if (b > a) {
       if (g < G) atomicAdd(&lsum[g], (unsigned long long)(b - a));
       // covers are sorted (executor.cc:572-585): the first and last PC bound them; k_part checks
@@ -57,9 +62,11 @@ __global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const ui
       hi = max(hi, pcs[b - 1]);
     }
   }
-  block_span_update<256>(lo, hi, span);  // (its barrier also completes lsum)
+  if (mx) atomicMax(&lmax, mx);
+  block_span_update<256>(lo, hi, span);  // (its barrier also completes lsum and lmax)
   for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
     if (lsum[g]) atomicAdd((unsigned long long*)&gpcs[g], lsum[g]);
+  if (threadIdx.x == 0 && lmax) atomicMax(mlmax, lmax);
 }
 
 // exact bounds (the slow path when some cover is not sorted)
@@ -88,10 +95,12 @@ __global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span) 
 // call group gpcs[G], the span, the error word, and the PCs of each call group this job reads (its
 // members' slices: the exact byte model of the kernels) gsl[G]
 __global__ void k_gpack(const uint64_t* gstart, const uint64_t* gpcs, const uint32_t* span, const int* err,
-                        const uint64_t* mpos, uint32_t G, uint64_t* out) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * G + 3; i += gridDim.x * blockDim.x) {
+                        const uint64_t* mpos, uint32_t G, const uint32_t* mlmax, uint64_t* out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * G + 4; i += gridDim.x * blockDim.x) {
     uint64_t v;
-    if (i <= G)
+    if (i == 3 * G + 3)
+      v = *mlmax;
+    else if (i <= G)
       v = gstart[i];
     else if (i < 2 * G + 1)
       v = gpcs[i - G - 1];
@@ -767,6 +776,7 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     J.plan_key = hstart;
   }
   GosortPlan& P = *J.plan;
+  P.may_bounce = J.may_bounce;
   rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
   auto small_done = [&](hipStream_t q) {
     if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);
@@ -855,6 +865,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint32_t* sbeg = a.key_lo ? sc.get<uint32_t>("pm_sbeg", n + 1) : nullptr;
   uint64_t* mpos = sc.get<uint64_t>("pm_mpos", n + 1);
   uint64_t* gpack = sc.get<uint64_t>("pm_gpack", 3 * (size_t)G + 4);
+  uint32_t* mlmax = sc.get<uint32_t>("pm_mlmax", 1);
+  SYZ_HIP(hipMemsetAsync(mlmax, 0, 4, s));
   k_pm_init<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(err, gpcs, G, span);
   SYZ_LAUNCHED();
   uint32_t* krange = nullptr;
@@ -872,7 +884,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     ProfScope ps("group_partition", s, (uint64_t)n * 28);
     group_partition_dev(a.group, a.off, n, G, gstart, members, el, err, s);
     if (n) {
-      k_span_sums<<<grid_for(n, 256, span_blocks()), 256, G * 8, s>>>(a.pcs, a.off, a.group, n, G, gpcs, span);
+      k_span_sums<<<grid_for(n, 256, span_blocks()), 256, G * 8, s>>>(a.pcs, a.off, a.group, n, G, gpcs, span,
+                                                                          mlmax);
       SYZ_LAUNCHED();
       if (krange)
         k_slices<<<grid_for(n, 256, 4096), 256, 0, s>>>(a.pcs, a.off, members, el, a.group, n, krange, sbeg, mlen);
@@ -881,12 +894,13 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       SYZ_LAUNCHED();
     }
     exclusive_scan_u32(mlen, mpos, n, s);
-    k_gpack<<<grid_for(3 * (size_t)G + 3, 256, 64), 256, 0, s>>>(gstart, gpcs, span, err, mpos, G, gpack);
+    k_gpack<<<grid_for(3 * (size_t)G + 4, 256, 64), 256, 0, s>>>(gstart, gpcs, span, err, mpos, G, mlmax, gpack);
     SYZ_LAUNCHED();
   }
   uint64_t* hbuf = c.pinned.get<uint64_t>(3 * (size_t)G + 8);
-  SYZ_HIP(hipMemcpyAsync(hbuf, gpack, (3 * (size_t)G + 3) * 8, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(hbuf, gpack, (3 * (size_t)G + 4) * 8, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
+  J.may_bounce = hbuf[3 * G + 3] >= GS_U32_LEN_LIMIT;
   if (*reinterpret_cast<int*>(hbuf + 2 * G + 2)) fail(SYZGPU_EINVAL, "group id >= ngroups");
   std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
   const uint64_t* hsl = hbuf + 2 * G + 3;  // PCs this job reads per group (key parts: the slices)
@@ -1144,6 +1158,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     J.plan_key = hstart;
   }
   GosortPlan& P = *J.plan;
+  P.may_bounce = J.may_bounce;
   rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
   auto small_done = [&](hipStream_t q) {
     if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);

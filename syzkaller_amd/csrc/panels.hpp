@@ -104,6 +104,7 @@ struct MinJob {
   size_t n = 0;
   uint32_t G = 0;
   bool begun = false;
+  bool may_bounce = true;  // a cover too long for the Go sort's u32 element (begin's length scan)
   const uint32_t* group = nullptr;     // caller's device buffers (valid from begin to end)
   const uint16_t* prog_len = nullptr;
   Grow<uint64_t> gstart;

@@ -13,7 +13,8 @@ struct Seg {
 };
 
 // gosort.hip: the element at sorted position r of the groups' ranges is el[perm[r]]
-constexpr uint32_t GS_T_SEG = 8192;  // call groups above this many entries start the global rounds
+constexpr uint32_t GS_T_SEG = 8192;
+constexpr uint64_t GS_U32_LEN_LIMIT = 1ull << 19;  // cover lengths the packed u32 sort element holds  // call groups above this many entries start the global rounds
 struct Pack;
 struct GosortPlan {
   size_t n = 0;
@@ -21,6 +22,7 @@ struct GosortPlan {
   uint64_t big_total = 0;  // elements in the groups that start the global levels
   uint64_t big_max = 0;    // elements in the largest of them
   mutable uint32_t rounds_hint = 0;  // global rounds the last run of this plan needed (issued up front)
+  mutable bool may_bounce = true;    // false: every cover length fits the u32 sort element (< 2^19)
   Seg* small = nullptr;
   Pack* packs = nullptr;
   Seg* big = nullptr;
@@ -52,6 +54,8 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
                          uint64_t* out_off_dev, hipStream_t s);
 void canonicalize_batch_dev(uint32_t* pcs, const uint64_t* off, const uint64_t* host_off, size_t ncov,
                             uint64_t* out_len, hipStream_t s);
+// the same with the covers classed on the device (no host offsets)
+void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, uint64_t* out_len, hipStream_t s);
 
 // prio.hip
 void len_hist_dev(const uint16_t* prog_len, const uint8_t* sel, size_t n, int32_t C, int64_t* hist, int* err,

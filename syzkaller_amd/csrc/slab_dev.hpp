@@ -31,10 +31,6 @@ namespace syz {
 #ifndef SYZ_SL_SKIP
 #define SYZ_SL_SKIP 0  // A/B knob: skip tile groups outside a pass (measured with register spills)
 #endif
-#ifndef SYZ_SL_RUNAGG
-#define SYZ_SL_RUNAGG 0  // A/B knob: one LDS atomic per run of equal windows in a tile (run head), not per
-                         // PC: bit 0 in the histogram, bit 1 in the passes
-#endif
 #ifndef SYZ_SL_BUF_BITS
 #define SYZ_SL_BUF_BITS 14
 #endif
@@ -237,11 +233,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   // from here on v holds the PC's offset from lo: window = v >> S, offset in it = v & omask
   // window histogram
   const uint32_t DUMMY = WMAX + 1 + lane;
-  uint32_t czh = cz;  // opaque: the loads' per-tile scalars are not kept live into the histogram
-  if (SYZ_SL_RUNAGG & 1) asm volatile("" : "+v"(czh));
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
-    const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)czh, k);
+    const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, k);
     const uint32_t cnt = z & 0x7Fu;
     v[k] -= lo;
     const uint32_t w = v[k] >> S;
@@ -253,19 +247,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
     // outside the windows: an unsorted cover (Minimize: redone on exact bounds; NOV: out of order)
     bad |= (in && w >= W) ? (NOV ? ((z & 0x100u) ? 1 : 4) : 1) : 0;
-    if (SYZ_SL_RUNAGG & 1) {  // a tile's PCs are sorted: equal windows are runs of lanes, one add per run
-      const bool ok = in && w < W;
-      const uint32_t key = ok ? w : 0xFFFFFFFFu;
-      const uint32_t pk = lane_prev(key);
-      const bool head = ok && (lane == 0 || pk != key);
-      const uint64_t bnd = __ballot(head || !ok);
-      const uint64_t above = lane < 63 ? bnd >> (lane + 1) : 0ull;
-      const uint32_t len = above ? (uint32_t)__ffsll((unsigned long long)above) : 64u - lane;
-      if (head) atomicAdd(&hist[w], len);
-      __builtin_amdgcn_sched_barrier(0);  // (tiles interleaved by the scheduler keep their ballots live)
-    } else {
-      atomicAdd(&hist[in && w < W ? w : DUMMY], 1u);
-    }
+    atomicAdd(&hist[in && w < W ? w : DUMMY], 1u);
     if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
   }
   {
@@ -330,7 +312,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     // opaque per pass, so the compiler does not hoist 64 tiles' elements out of the pass loop (VGPRs)
     uint32_t Sp = S, om = omask;
     asm volatile("" : "+s"(Sp), "+s"(om));
-    constexpr int PB = (SYZ_SL_RUNAGG & 2) ? 4 : 8;  // (a run-aggregated group holds two ballots per tile)
+    constexpr int PB = 8;
 #pragma unroll
     for (int k0 = 0; k0 < TPW; k0 += PB) {
       if (SYZ_SL_SKIP) {  // a group of tiles with no window in this pass is skipped whole
@@ -344,29 +326,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       }
       uint32_t pos[PB], el[PB];
       bool ok[PB];
-      if (SYZ_SL_RUNAGG & 2) {  // the run head takes the run's slots; its lanes read the base by a permute
-        uint32_t hl[PB];
-#pragma unroll
-        for (int q = 0; q < PB; q++) {
-          const int kk = k0 + q;
-          const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, kk);
-          const uint32_t d = v[kk], w = d >> Sp;
-          ok[q] = lane < (z & 0x7Fu) && (w - wl) < (wh - wl);
-          el[q] = (d & om) | ((z >> 9) << Sp);
-          const uint32_t key = ok[q] ? w : 0xFFFFFFFFu;
-          const uint32_t pk = lane_prev(key);
-          const bool head = ok[q] && (lane == 0 || pk != key);
-          const uint64_t hb = __ballot(head), bnd = __ballot(head || !ok[q]);
-          const uint64_t above = lane < 63 ? bnd >> (lane + 1) : 0ull;
-          const uint32_t len = above ? (uint32_t)__ffsll((unsigned long long)above) : 64u - lane;
-          const uint64_t mine = hb & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-          hl[q] = mine ? 63u - (uint32_t)__clzll((unsigned long long)mine) : 0u;
-          pos[q] = 0;
-          if (head) pos[q] = atomicAdd(&hist[w], len);
-        }
-#pragma unroll
-        for (int q = 0; q < PB; q++) pos[q] = (uint32_t)__shfl((int)pos[q], (int)hl[q], 64) + (lane - hl[q]);
-      } else {
 #pragma unroll
         for (int q = 0; q < PB; q++) {
           const int kk = k0 + q;
@@ -377,7 +336,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
           pos[q] = 0;
           if (ok[q]) pos[q] = atomicAdd(&hist[w], 1u);  // lanes outside the pass issue nothing
         }
-      }
 #pragma unroll
       for (int q = 0; q < PB; q++) {
         if (ok[q]) {

@@ -392,3 +392,32 @@ def test_novelty_identical_keys():
         mcp, mco = oracle.to_csr(mc)
         new = _check(pcs, off, grp, 1, mcp, mco, np.zeros(0, np.uint32))
         assert int(new.sum()) == (0 if mcp.size else 1)
+
+
+@pytest.mark.parametrize("force_sort", [False, True])
+def test_novelty_clustered_pcs(strategy, force_sort, monkeypatch):
+    # real kcov PCs cluster by function: dense runs of PCs at a few far-apart addresses put thousands of
+    # keys into one address bucket of a hashed window, where the kept keys are ordered by a sort instead
+    # of a scan of their bucket; both windowed strategies against the literal oracle
+    if strategy not in ("windows", "hwindows"):
+        pytest.skip("the windowed strategies' ordering")
+    if force_sort:  # every sub-range through the sort (the scan path's results, another way)
+        monkeypatch.setenv("SYZGPU_NWH_SORT", "1")
+    rnd = np.random.default_rng(41)
+    G = 3
+    bases = [0x10000000, 0x80000000, 0xF0000000]
+    pool = np.concatenate([b + 4 * np.arange(20_000, dtype=np.uint64) for b in bases]).astype(np.uint32)
+
+    def draw(k):
+        c = rnd.integers(0, 3)
+        lo = int(rnd.integers(0, 20_000 - k))
+        return np.unique(pool[c * 20_000 + lo + rnd.integers(0, 4 * k, size=k).clip(0, 20_000 - lo - 1)])
+    covs = [draw(int(rnd.integers(1, 400))) for _ in range(3_000)]
+    grp = rnd.integers(0, G, size=len(covs)).astype(np.uint32)
+    mc = [np.unique(pool[rnd.integers(0, pool.size, size=3_000)]) for _ in range(G)]
+    flakes = np.unique(pool[rnd.integers(0, pool.size, size=50)])
+    pcs, off = oracle.to_csr(covs)
+    mcp, mco = oracle.to_csr(mc)
+    new, sc = _scopes(lambda: _check(pcs, off, grp, G, mcp, mco, flakes))
+    assert "novelty_min_hash" in sc
+    assert 0 < new.sum() < len(covs)
