@@ -225,7 +225,9 @@ int syzgpu_mz_end_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist, uint
 /* minimizeCorpus's tail (syz-manager/manager.go:523-536) in one call: syzgpu_mz_end_dev's outputs (len_hist
  * required), calcStaticPriorities of the usage matrix (prog/prio.go:40-135) into static_prios, and
  * CalculatePriorities + BuildChoiceTable from the histogram (prio.go:29-38, 137-192, 202-228) into
- * prios / run / row_present (may be NULL); the three error checks after one wait. */
+ * prios / run / row_present (may be NULL); the three error checks after one wait. calcStaticPriorities
+ * runs beside the job's Minimize passes: `uses` must be ready on `stream` when the job's begin is
+ * enqueued (it is read from that point of the stream, not from this call's). */
 int syzgpu_mz_end_prio_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist, uint8_t* selected,
                            int64_t* len_hist, int64_t* out_idx, uint64_t* group_out_off, const float* uses,
                            size_t nkeys, float* static_prios, float* prios, int64_t* run, uint8_t* row_present,

@@ -112,6 +112,8 @@ struct Context {
   uint32_t gr_resident = 0;  // workgroups of k_gr_persist resident at once (occupancy x CUs)
   hipStream_t part = nullptr;  // the raw Minimize's transpose pass, beside the Go sort
   hipEvent_t ev_part0 = nullptr, ev_part1 = nullptr;
+  hipEvent_t ev_msmall = nullptr, ev_msmall2 = nullptr;  // the small groups' packed M on another stream
+  hipEvent_t ev_psmall = nullptr;  // P's slabs of the small call groups are cut
   hipStream_t part2 = nullptr;  // its scatter passes, batch after batch beside the next batch's count
   std::vector<hipEvent_t> ev_cnt, ev_sct;  // per batch: count done, scatter done
   int ncu = 0;  // compute units of the device
@@ -180,6 +182,19 @@ struct PhaseTimer {
     (void)hipStreamSynchronize(s);
     const auto n = std::chrono::steady_clock::now();
     fprintf(stderr, "[phase] %s.%s %.3f ms\n", what, name, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+// host-side time between points (SYZGPU_HOST_TIMING=1; no stream waits, unlike PhaseTimer)
+struct HostTimer {
+  bool on;
+  const char* what;
+  std::chrono::steady_clock::time_point t;
+  explicit HostTimer(const char* w) : on(getenv("SYZGPU_HOST_TIMING") != nullptr), what(w), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* name) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[host] %s.%s %.1f us\n", what, name, std::chrono::duration<double, std::micro>(n - t).count());
     t = n;
   }
 };

@@ -41,12 +41,14 @@ static unsigned span_blocks() {
 
 // ---- per-entry statistics: PCs per call group and the PC span --------------------------------------
 // (*mlmax: the longest cover, which tells the Go sort whether a pack can need its u64 element)
+// (gpcs may be null: the per-group sums come from the member prefix instead, no per-group atomics)
 __global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                                                    size_t n, uint32_t G, uint64_t* gpcs, uint32_t* span,
                                                    uint32_t* mlmax) {
   extern __shared__ unsigned long long lsum[];
   __shared__ uint32_t lmax;
-  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) lsum[g] = 0;
+  if (gpcs)
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) lsum[g] = 0;
   if (threadIdx.x == 0) lmax = 0;
   __syncthreads();
   uint32_t lo = 0xFFFFFFFFu, hi = 0, mx = 0;
@@ -55,7 +57,7 @@ __global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const ui
     const uint32_t g = group[i];
     mx = max(mx, (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull));
     if (b > a) {
-      if (g < G) atomicAdd(&lsum[g], (unsigned long long)(b - a));
+      if (gpcs && g < G) atomicAdd(&lsum[g], (unsigned long long)(b - a));
       // covers are sorted (executor.cc:572-585): the first and last PC bound them; k_part checks
       // every PC against the resulting windows and the call is redone on exact bounds otherwise
       lo = min(lo, pcs[a]);
@@ -64,8 +66,9 @@ __global__ __launch_bounds__(256) void k_span_sums(const uint32_t* pcs, const ui
   }
   if (mx) atomicMax(&lmax, mx);
   block_span_update<256>(lo, hi, span);  // (its barrier also completes lsum and lmax)
-  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
-    if (lsum[g]) atomicAdd((unsigned long long*)&gpcs[g], lsum[g]);
+  if (gpcs)
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+      if (lsum[g]) atomicAdd((unsigned long long*)&gpcs[g], lsum[g]);
   if (threadIdx.x == 0 && lmax) atomicMax(mlmax, lmax);
 }
 
@@ -547,6 +550,14 @@ static uint32_t pm_batches() {
   return v;
 }
 
+// SYZGPU_PM_PSPLIT=1 (A/B): P as two launches, the small call groups' slabs first, so their M starts
+// beside the big groups' slabs (measured slower: the big groups' LDS sort then waits for CUs behind
+// both, r04_q3 3.04 vs 2.96 ms)
+static bool pm_psplit() {
+  static const bool v = getenv("SYZGPU_PM_PSPLIT") && atoi(getenv("SYZGPU_PM_PSPLIT")) != 0;
+  return v;
+}
+
 static bool pm_p2() {
   static const bool v = getenv("SYZGPU_PM_P2") && atoi(getenv("SYZGPU_PM_P2")) != 0;
   return v;
@@ -587,14 +598,26 @@ void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* 
   J.B = J.hgblock[G];
 }
 
+// the members' tile counts and their prefix (tpos): needs no plan, so it can run before the host's
+uint64_t* slab_tiles(const uint32_t* mlen, size_t nmem, const char* prefix, hipStream_t s) {
+  Scratch& sc = ctx().scratch;
+  uint32_t* mtile = sc.get<uint32_t>((std::string(prefix) + "_sl_mtile").c_str(), nmem + 1);
+  uint64_t* tpos = sc.get<uint64_t>((std::string(prefix) + "_sl_tpos").c_str(), nmem + 2);
+  if (nmem) {
+    k_sl_tiles<<<grid_for(nmem, 256, 4096), 256, 0, s>>>(mlen, nmem, mtile);
+    SYZ_LAUNCHED();
+  }
+  exclusive_scan_u32(mtile, tpos, nmem, s);
+  return tpos;
+}
+
 void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint64_t* mpos, size_t nmem,
-                const uint64_t* gstart, hipStream_t s) {
+                const uint64_t* gstart, hipStream_t s, bool tiles_done) {
   Scratch& sc = ctx().scratch;
   auto nm = [&](const char* x) { return std::string(prefix) + x; };
   const uint32_t B = J.B, G = J.G;
-  uint32_t* mtile = sc.get<uint32_t>(nm("_sl_mtile").c_str(), nmem + 1);
   uint32_t* nsub = sc.get<uint32_t>(nm("_sl_nsub").c_str(), (size_t)B + 1);
-  J.tpos = sc.get<uint64_t>(nm("_sl_tpos").c_str(), nmem + 2);
+  J.tpos = tiles_done ? sc.get<uint64_t>(nm("_sl_tpos").c_str(), nmem + 2) : slab_tiles(mlen, nmem, prefix, s);
   J.cstart = sc.get<uint64_t>(nm("_sl_cstart").c_str(), (size_t)B + 2);
   J.slabs = sc.get<PSlab>(nm("_sl_slabs").c_str(), J.slab_bound + 1);
   J.gslab = sc.get<uint32_t>(nm("_sl_gslab").c_str(), G + 1);
@@ -607,11 +630,6 @@ void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint
     J.wtot = sc.get<uint32_t>(nm("_sl_wtot").c_str(), J.wtotal + 1);
     SYZ_HIP(hipMemsetAsync(J.wtot, 0, J.wtotal * 4, s));
   }
-  if (nmem) {
-    k_sl_tiles<<<grid_for(nmem, 256, 4096), 256, 0, s>>>(mlen, nmem, mtile);
-    SYZ_LAUNCHED();
-  }
-  exclusive_scan_u32(mtile, J.tpos, nmem, s);
   if (B) {
     k_sl_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(J.dbgroup, B, J.dgblock, gstart, J.dsg, J.tpos, nsub);
     SYZ_LAUNCHED();
@@ -647,8 +665,13 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   uint32_t* rank_of_member = J.rank_of_member.p;
   uint32_t* ent_of_rank = J.ent_of_rank.p;
   uint8_t* sel8 = J.sel8.p;
+  HostTimer ht("begin_slab");
+  // (hsl points into the lane's pinned buffer, which the plan's staging copy below reuses)
+  const std::vector<uint64_t> hslv(hsl, hsl + G);
+  hsl = hslv.data();
   SlabJob SJ;
   slab_plan(SJ, hstart, hsl, hpg, G, false);
+  ht.mark("slab_plan");
   const uint64_t slab_bound = SJ.slab_bound, total_pcs = SJ.total_pcs;
   const uint32_t B = SJ.B;
   // work items: (call, window), class (big groups: sorted by the global rounds) and mode, largest
@@ -658,8 +681,10 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   std::iota(order.begin(), order.end(), 0u);
   std::stable_sort(order.begin(), order.end(),
                    [&](uint32_t x, uint32_t y) { return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W; });
-  std::array<std::array<std::vector<PItem>, 3>, 2> items;  // [big][mode]
+  // items counted per (class, mode) first, then written straight into the pinned staging copy
   uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  size_t icount[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  std::vector<uint32_t> iw0(G, 0), iw1(G, 0);
   for (uint32_t g : order) {
     if (!hpcs[g]) continue;
     uint32_t w0 = 0, w1 = hpg[g].W;
@@ -669,13 +694,18 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
       w0 = (klo - lo) >> hpg[g].S;
       w1 = std::min<uint32_t>(hpg[g].W, ((khi - lo) >> hpg[g].S) + 1);
     }
-    auto& v = items[is_big(g) ? 1 : 0][hpg[g].mode];
-    for (uint32_t w = w0; w < w1; w++) v.push_back(PItem{g, w});
+    iw0[g] = w0;
+    iw1[g] = w1;
+    icount[is_big(g) ? 1 : 0][hpg[g].mode] += w1 - w0;
     item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
   }
+  std::array<std::array<size_t, 3>, 2> ifirst{};
   size_t nitems = 0;
-  for (auto& r : items)
-    for (auto& v : r) nitems += v.size();
+  for (int big = 0; big < 2; big++)
+    for (int m = 0; m < 3; m++) {
+      ifirst[big][m] = nitems;
+      nitems += icount[big][m];
+    }
   // the plan goes over in one copy: SGroup[G], gblock[G + 1], bgroup[B + 1], items[nitems + 1]
   auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
   const size_t o_gb = al16((G + 1) * sizeof(SGroup)), o_bg = o_gb + al16((G + 1) * 4),
@@ -686,25 +716,25 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   uint32_t* dgblock = reinterpret_cast<uint32_t*>(dstage + o_gb);
   uint32_t* dbgroup = reinterpret_cast<uint32_t*>(dstage + o_bg);
   PItem* ditems = reinterpret_cast<PItem*>(dstage + o_it);
-  std::array<std::array<size_t, 3>, 2> ifirst{};
+  for (uint32_t g = 0; g < G; g++) SJ.hsg[g].pad = is_big(g) ? 1u : 0u;
   {
     std::memcpy(stage, SJ.hsg.data(), G * sizeof(SGroup));
     std::memcpy(stage + o_gb, SJ.hgblock.data(), (G + 1) * 4);
     if (B) std::memcpy(stage + o_bg, SJ.hbgroup.data(), (size_t)B * 4);
-    size_t k = 0;
-    for (int big = 0; big < 2; big++)
-      for (int m = 0; m < 3; m++) {
-        const auto& v = items[big][m];
-        ifirst[big][m] = k;
-        if (!v.empty()) std::memcpy(stage + o_it + k * sizeof(PItem), v.data(), v.size() * sizeof(PItem));
-        k += v.size();
-      }
+    PItem* hit = reinterpret_cast<PItem*>(stage + o_it);
+    std::array<std::array<size_t, 3>, 2> at = ifirst;
+    for (uint32_t g : order) {
+      size_t& k = at[is_big(g) ? 1 : 0][hpg[g].mode];
+      for (uint32_t w = iw0[g]; w < iw1[g]; w++) hit[k++] = PItem{g, w};
+    }
     SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
   }
+  ht.mark("items_stage");
   SJ.dsg = dsg;
   SJ.dgblock = dgblock;
   SJ.dbgroup = dbgroup;
-  slab_build(SJ, "pm", mlen, mpos, n, gstart, s);
+  slab_build(SJ, "pm", mlen, mpos, n, gstart, s, true);
+  ht.mark("slab_build");
   const PSlab* slabs = SJ.slabs;
   const uint32_t* gslab = SJ.gslab;
   const uint64_t* gebase = SJ.gebase;
@@ -717,6 +747,11 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
+  }
+  if (!c.ev_msmall) {
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall2, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_psmall, hipEventDisableTiming));
   }
   while (c.ev_cnt.size() < 1) {
     hipEvent_t e1, e2;
@@ -732,11 +767,26 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   if (slab_bound) {
     // byte model: the algorithm's input this pass reads, 4 B per PC + 10 B per entry
     // (offset, group id); the element buffer it writes is intermediate traffic, not algorithmic bytes
-    ProfScope ps("k_slab", pq, total_pcs * 4 + (uint64_t)n * 10);
-    k_slab<SL_BLOCK, SL_TPW><<<(unsigned)slab_bound, SL_BLOCK, 0, pq>>>(
-        a.pcs, a.off, members, mlen, SJ.tpos, sbeg, slabs, SJ.cstart + B, dsg, gebase, lo, elems, SJ.D, err, nullptr,
-        NovSrc{}, rg_dbg());
-    SYZ_LAUNCHED();
+    // two launches: the small call groups' slabs first (their M starts once they and the small groups'
+    // sort are done, beside the big groups' slabs), then the big groups'; SYZGPU_PM_PSPLIT=0: one launch
+    const bool split = pm_psplit() && !pm_serial() && icount[0][0] + icount[0][1] + icount[0][2] > 0;
+    uint64_t cpcs[2] = {0, 0}, cent[2] = {0, 0};  // each launch's share of the byte model
+    for (uint32_t g = 0; g < G; g++) {
+      cpcs[is_big(g) ? 1 : 0] += hsl[g];
+      cent[is_big(g) ? 1 : 0] += hstart[g + 1] - hstart[g];
+    }
+    for (int cls = split ? 1 : 0; cls <= (split ? 2 : 0); cls++) {
+      const uint64_t bytes = cls ? cpcs[cls - 1] * 4 + cent[cls - 1] * 10 : total_pcs * 4 + (uint64_t)n * 10;
+      ProfScope ps("k_slab", pq, bytes);
+      k_slab<SL_BLOCK, SL_TPW><<<(unsigned)slab_bound, SL_BLOCK, 0, pq>>>(
+          a.pcs, a.off, members, mlen, SJ.tpos, sbeg, slabs, SJ.cstart + B, dsg, gebase, lo, elems, SJ.D, err,
+          nullptr, NovSrc{}, rg_dbg(), cls);
+      SYZ_LAUNCHED();
+      if (cls == 1) SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
+    }
+    if (!split) SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
+  } else {
+    SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
   }
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, pq));
   SYZ_HIP(hipEventRecord(c.ev_cnt[0], pq));
@@ -747,10 +797,10 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   SYZ_HIP(hipMemsetAsync(sel8, 0, (n + 31) / 32 * 32 + 64, s));
   auto run_m = [&](hipStream_t q, int big) {
     ProfScope ps(big ? "m_big" : "m_small", q, 0);
-    const auto& it = items[big];
-    const size_t nd = it[PMODE_DIRECT].size(), nh = it[PMODE_HASH].size(), np = it[PMODE_PACKED].size();
+    const size_t nd = icount[big][PMODE_DIRECT], nh = icount[big][PMODE_HASH], np = icount[big][PMODE_PACKED];
     if (!nd && !nh && !np) return;
-    SYZ_HIP(hipStreamWaitEvent(q, c.ev_sct[0], 0));
+    SYZ_HIP(hipStreamWaitEvent(q, big ? c.ev_sct[0] : c.ev_psmall, 0));
+    hipStream_t pq2 = q;
     if (nd) {
       ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
       k_smin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], dsg, gslab, gebase, D, slabs,
@@ -764,10 +814,16 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
       SYZ_LAUNCHED();
     }
     if (np) {
-      ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
-      k_smin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
-                                                       elems, rank_of_member, gstart, sel8);
-      SYZ_LAUNCHED();
+      {
+        ProfScope pk("k_pmin_packed", pq2, 4 * item_pcs[big][PMODE_PACKED]);
+        k_smin_hash<true><<<(unsigned)np, 1024, 0, pq2>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D,
+                                                           slabs, elems, rank_of_member, gstart, sel8);
+        SYZ_LAUNCHED();
+      }
+      if (pq2 != q) {
+        SYZ_HIP(hipEventRecord(c.ev_msmall2, pq2));
+        SYZ_HIP(hipStreamWaitEvent(q, c.ev_msmall2, 0));
+      }
     }
   };
   if (!J.plan || J.plan_key != hstart) {
@@ -777,7 +833,6 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   }
   GosortPlan& P = *J.plan;
   P.may_bounce = J.may_bounce;
-  rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
   auto small_done = [&](hipStream_t q) {
     if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);
     run_m(q, 0);
@@ -786,19 +841,22 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     if (P.nbig) ranks_big(el, perm, P, members, rank_of_member, ent_of_rank, q);
     run_m(q, 1);
   };
+  ht.mark("launch_p_plan_sort");
   if (n) {
     gosort_run(el, perm, n, P, s, small_done, big_done);
   } else {
     small_done(s);
     big_done(s);
   }
+  ht.mark("gosort_run");
   SYZ_HIP(hipEventSynchronize(c.ev_cnt[0]));
+  ht.mark("wait_p");
   if (!J.done) SYZ_HIP(hipEventCreateWithFlags(&J.done, hipEventDisableTiming));
   SYZ_HIP(hipEventRecord(J.done, s));
   J.stats_total_pcs = total_pcs;
-  J.stats_items_direct = items[0][PMODE_DIRECT].size() + items[1][PMODE_DIRECT].size();
-  J.stats_items_hash = items[0][PMODE_HASH].size() + items[1][PMODE_HASH].size() + items[0][PMODE_PACKED].size() +
-                       items[1][PMODE_PACKED].size();
+  J.stats_items_direct = icount[0][PMODE_DIRECT] + icount[1][PMODE_DIRECT];
+  J.stats_items_hash = icount[0][PMODE_HASH] + icount[1][PMODE_HASH] + icount[0][PMODE_PACKED] +
+                       icount[1][PMODE_PACKED];
   if (herr[0] & 1) {
     if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
     return false;
@@ -884,8 +942,14 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     ProfScope ps("group_partition", s, (uint64_t)n * 28);
     group_partition_dev(a.group, a.off, n, G, gstart, members, el, err, s);
     if (n) {
-      k_span_sums<<<grid_for(n, 256, span_blocks()), 256, G * 8, s>>>(a.pcs, a.off, a.group, n, G, gpcs, span,
-                                                                          mlmax);
+      // whole covers: the per-group PCs are the member prefix's group differences (k_gpack), so the
+      // span pass takes no per-group atomics (a wider grid measured slower: its span atomics)
+      if (krange)
+        k_span_sums<<<grid_for(n, 256, span_blocks()), 256, G * 8, s>>>(a.pcs, a.off, a.group, n, G, gpcs, span,
+                                                                            mlmax);
+      else
+        k_span_sums<<<grid_for(n, 256, span_blocks()), 256, 0, s>>>(a.pcs, a.off, a.group, n, G, nullptr, span,
+                                                                       mlmax);
       SYZ_LAUNCHED();
       if (krange)
         k_slices<<<grid_for(n, 256, 4096), 256, 0, s>>>(a.pcs, a.off, members, el, a.group, n, krange, sbeg, mlen);
@@ -899,11 +963,17 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   }
   uint64_t* hbuf = c.pinned.get<uint64_t>(3 * (size_t)G + 8);
   SYZ_HIP(hipMemcpyAsync(hbuf, gpack, (3 * (size_t)G + 4) * 8, hipMemcpyDeviceToHost, s));
+  // work that needs no plan runs while the host plans: identity ranks, the slab tiles' prefix
+  rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
+  if (!pm_region()) slab_tiles(mlen, n, "pm", s);
+  HostTimer ht("begin");
   SYZ_HIP(hipStreamSynchronize(s));
+  ht.mark("wait_partition");
   J.may_bounce = hbuf[3 * G + 3] >= GS_U32_LEN_LIMIT;
   if (*reinterpret_cast<int*>(hbuf + 2 * G + 2)) fail(SYZGPU_EINVAL, "group id >= ngroups");
   std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
   const uint64_t* hsl = hbuf + 2 * G + 3;  // PCs this job reads per group (key parts: the slices)
+  if (!krange) hpcs.assign(hsl, hsl + G);  // (whole covers: the slices are the groups' PCs)
   uint32_t lo = reinterpret_cast<uint32_t*>(hbuf + 2 * G + 1)[0], hi = reinterpret_cast<uint32_t*>(hbuf + 2 * G + 1)[1];
   if (exact_span) {
     lo = exact_span[0];
@@ -915,6 +985,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   // ---- plan: window size per call group, blocks, chunk bound, work items ----
   std::vector<PGroup> hpg;
   plan_windows(spanw, hpcs.data(), hstart.data(), G, hpg);
+  ht.mark("plan_windows");
   if (!pm_region())
     return begin_slab(J, a, hstart, hpcs, hsl, hpg, lo, hi, exact_span, members, el, mlen, mpos, sbeg, err);
   std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
@@ -1159,7 +1230,6 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   }
   GosortPlan& P = *J.plan;
   P.may_bounce = J.may_bounce;
-  rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
   auto small_done = [&](hipStream_t q) {
     if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);
     run_m(q, 0);
@@ -1434,13 +1504,11 @@ int syzgpu_mz_end_prio_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist,
     std::lock_guard<std::recursive_mutex> hl_(J.mu);
     Context& c = ctx();
     hipStream_t s = (hipStream_t)stream;
-    // calcStaticPriorities depends on the usage matrix only: on the side stream (idle once the small
-    // call groups' Minimize is done), joined before CalculatePriorities
-    hipStream_t ss = c.side ? c.side : s;
-    if (ss != s) {
-      SYZ_HIP(hipEventRecord(c.ev_fork, s));
-      SYZ_HIP(hipStreamWaitEvent(ss, c.ev_fork, 0));
-    }
+    // calcStaticPriorities depends on the usage matrix only: on the transpose's stream, which is idle
+    // once P is done (the side stream would hold it behind the small groups' Minimize) and ordered
+    // after the job's begin on `stream` (uses must be ready there by then), joined before
+    // CalculatePriorities
+    hipStream_t ss = J.begun && c.part ? c.part : s;
     const uint32_t* dserr = static_priorities_enqueue(uses, nkeys, C, static_prios, ss);
     RawEndArgs e;
     e.C = C;
@@ -1453,8 +1521,8 @@ int syzgpu_mz_end_prio_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist,
     e.defer_check = true;
     minimize_raw_end(J, e);
     if (ss != s) {
-      SYZ_HIP(hipEventRecord(c.ev_join, ss));
-      SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
+      SYZ_HIP(hipEventRecord(c.ev_part1, ss));
+      SYZ_HIP(hipStreamWaitEvent(s, c.ev_part1, 0));
     }
     prio_choice_dev(static_prios, len_hist, nullptr, C, nullptr, prios, run, row_present, s);
     uint32_t* h = c.pinned.get<uint32_t>(8);

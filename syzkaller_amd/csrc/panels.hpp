@@ -39,7 +39,7 @@ struct SGroup {       // per call group, slab form
   uint32_t stride;    // D row length (>= the group's slabs)
   uint32_t memb;      // members per block: min(SL_MEMB, 2^(32 - S))
   uint32_t wbase;     // first per-window total (wtot, when P is asked for them)
-  uint32_t pad;
+  uint32_t pad;       // bit 0: a big call group (the Go sort's global rounds; P's second launch)
   uint64_t xbase;     // element slots of the padding of the groups before (a slab's runs are padded to
                       // 4 elements: it takes its PCs + 3 W + 4 slots at most)
 };
@@ -72,7 +72,9 @@ struct SlabJob {
 void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* hpcs, const std::vector<PGroup>& hpg,
                uint32_t G, bool want_wtot);
 void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint64_t* mpos, size_t nmem,
-                const uint64_t* gstart, hipStream_t s);
+                const uint64_t* gstart, hipStream_t s, bool tiles_done = false);
+// the members' tile prefix alone (slab_build's first step, which needs no plan): returns tpos
+uint64_t* slab_tiles(const uint32_t* mlen, size_t nmem, const char* prefix, hipStream_t s);
 
 struct RawMinArgs {
   const uint32_t* pcs;

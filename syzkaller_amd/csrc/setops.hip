@@ -510,7 +510,8 @@ __global__ void k_store_len(const uint64_t* pos, uint64_t n, uint64_t* out_len, 
 // Covers are classed on the device by length (wave-aggregated appends to five lists): <= 512 and
 // <= 1024 PCs take one wave each, in registers (k_canon_wave below; SYZGPU_CANON_LDS=1: the workgroup
 // LDS sorters instead), <= 2048 a 512-thread workgroup with an LDS bitonic sort, <= 16384 (kCoverSize)
-// a 1024-thread one; longer ones (not produced by kcov) go through the global network one by one.
+// a 1024-thread one, <= 32768 (raw kcov output with repeats) the same with 128 KB of LDS; longer ones
+// go through the global network one by one.
 // After the sort: unique with last = sentinel and the in-place store of the kept prefix
 // (cover.go:28-40), the new length to out_len.
 template <uint32_t PMAX, int BLOCK>
@@ -628,15 +629,16 @@ __global__ __launch_bounds__(256) void k_canon_wave(uint32_t* pcs, const uint64_
   }
 }
 
-// cls lists: [0] <= 512, [1] <= 1024, [2] <= 2048, [3] <= 16384, [4] longer; cnt[5]
-constexpr int CANON_NCLS = 5;
+// cls lists: [0] <= 512, [1] <= 1024, [2] <= 2048, [3] <= 16384, [4] <= 32768, [5] longer; cnt[6]
+constexpr int CANON_NCLS = 6;
+constexpr int CANON_LDS2 = 32768;  // a 1024-thread workgroup with 128 KB of LDS (raw kcov covers with repeats)
 __global__ void k_canon_class(const uint64_t* off, size_t ncov, uint32_t* lists, size_t cap, uint32_t* cnt) {
   for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < ncov; i0 += (size_t)gridDim.x * blockDim.x) {
     const size_t i = i0 + threadIdx.x;
     int c = -1;
     if (i < ncov) {
       const uint64_t n = off[i + 1] - off[i];
-      c = n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= (uint64_t)CANON_LDS ? 3 : 4;
+      c = n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= (uint64_t)CANON_LDS ? 3 : n <= (uint64_t)CANON_LDS2 ? 4 : 5;
     }
 #pragma unroll
     for (int k = 0; k < CANON_NCLS; k++) {
@@ -681,14 +683,16 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   SYZ_LAUNCHED();
   k_canon_cls<CANON_LDS, CANON_BLOCK><<<ncu * 2, CANON_BLOCK, 0, s>>>(pcs, off, lists + 3 * ncov, cnt + 3, out_len);
   SYZ_LAUNCHED();
+  k_canon_cls<CANON_LDS2, CANON_BLOCK><<<ncu, CANON_BLOCK, 0, s>>>(pcs, off, lists + 4 * ncov, cnt + 4, out_len);
+  SYZ_LAUNCHED();
   // longer covers: their list back to the host, then the global network one by one
   uint32_t* h = c.pinned.get<uint32_t>(CANON_NCLS);
   SYZ_HIP(hipMemcpyAsync(h, cnt, CANON_NCLS * 4, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
-  const uint32_t nbig = h[4];
+  const uint32_t nbig = h[5];
   if (!nbig) return;
   std::vector<uint32_t> big(nbig);
-  SYZ_HIP(hipMemcpyAsync(big.data(), lists + 4 * ncov, nbig * 4, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(big.data(), lists + 5 * ncov, nbig * 4, hipMemcpyDeviceToHost, s));
   std::vector<uint64_t> hoff(2);
   for (uint32_t seg : big) {
     SYZ_HIP(hipMemcpyAsync(hoff.data(), off + seg, 16, hipMemcpyDeviceToHost, s));

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const uint32_t* __restrict__ mlen, const uint64_t* __restrict__ tpos, const uint32_t* __restrict__ sbeg,
     const PSlab* __restrict__ slabs, const uint64_t* nslab, const SGroup* __restrict__ sg,
     const uint64_t* __restrict__ gebase, uint32_t lo, uint32_t* __restrict__ elems, uint32_t* __restrict__ D,
-    int* err, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int dbg = 0) {
+    int* err, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int dbg = 0, int cls = 0) {
   constexpr int WAVES = BLOCK / 64;
   static_assert((uint32_t)TPW * WAVES == SL_TILES, "slab tiles");
   __shared__ __align__(16) uint32_t obuf[SL_BUF];
@@ -145,6 +145,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   const unsigned lane = __lane_id();
   const PSlab sl = slabs[c];
   const SGroup gp = sg[sl.g];
+  // cls 1 / 2: only the slabs of small / big call groups (SGroup.pad bit 0), so the small groups' M
+  // can start while the big groups' slabs are still being cut
+  if (cls && (gp.pad & 1u) != (uint32_t)(cls - 1)) return;
   const uint32_t S = gp.S, W = gp.W, nt = sl.nt, nmem = sl.nmem;
   for (uint32_t i = threadIdx.x; i < nmem; i += BLOCK) {
     const uint64_t m = (uint64_t)sl.m0 + i;
