@@ -78,7 +78,7 @@ def parse():
 
 # the round's committed rocprofv3 kernel summary of this bench command (tools/gpu_final.sh): its top
 # kernel by total GPU time names the roofline kernel
-ROCPROF_STATS = os.path.join(ROOT, "profiles", "r03_kernel_stats.csv")
+ROCPROF_STATS = os.path.join(ROOT, "profiles", "r04_kernel_stats.csv")
 # rocprofv3 kernel name -> the library's profiling scope around that kernel
 ROCPROF_SCOPE = [("k_slab<", "k_slab"), ("k_smin_direct", "k_pmin_direct"), ("k_smin_hash<false>", "k_pmin_hash"),
                  ("k_smin_hash<true>", "k_pmin_packed"),
