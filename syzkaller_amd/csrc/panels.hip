@@ -328,57 +328,59 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #else
 #define SYZ_SMIN_OCC
 #endif
-__global__ __launch_bounds__(1024) SYZ_SMIN_OCC void k_smin_direct(const PItem* items, const SGroup* sg, const uint32_t* gslab,
-                                                      const uint64_t* gebase, const uint32_t* D,
-                                                      const PSlab* slabs, const uint32_t* __restrict__ elems,
-                                                      const uint32_t* __restrict__ rank_of_member,
-                                                      const uint64_t* gstart, uint8_t* sel8) {
-  __shared__ __align__(16) uint32_t tab[1u << DS];
-  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];
-  __shared__ uint64_t red64[1024 / 64 + 1];
-  const PItem it = items[blockIdx.x];
+// LDS of one M workgroup: the window's table (direct: 2^DS u32; hashed: keys + values or packed slots),
+// the walk's scratch (then the emit bitmap) and reductions
+struct SminLds {
+  __align__(16) uint32_t tabs[(1u << DS) > 2 * HS ? (1u << DS) : 2 * HS];
+  __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];
+  uint64_t red64[1024 / 64 + 1];
+  int full;
+};
+static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
+
+__device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, const uint32_t* gslab,
+                                            const uint64_t* gebase, const uint32_t* D, const PSlab* slabs,
+                                            const uint32_t* __restrict__ elems,
+                                            const uint32_t* __restrict__ rank_of_member, const uint64_t* gstart,
+                                            uint8_t* sel8, SminLds& L) {
+  uint32_t* tab = L.tabs;
   {
     uint4* t4 = reinterpret_cast<uint4*>(tab);
     const uint4 none4 = make_uint4(RANK_NONE, RANK_NONE, RANK_NONE, RANK_NONE);
     for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
   }
   __syncthreads();
-  for_slab_window<SYZ_SL_MU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, wsc, red64,
+  for_slab_window<SYZ_SL_MU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
                                     [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
   __syncthreads();
   const uint64_t gb = gstart[it.g];
-  emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, wsc, sel8);
+  emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, L.wsc, sel8);
 }
 
 #ifndef SYZ_SL_HU
 #define SYZ_SL_HU 1
 #endif
 template <bool PACKED>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_smin_hash(const PItem* items, const SGroup* sg, const uint32_t* gslab,
-                                                    const uint64_t* gebase, const uint32_t* D, const PSlab* slabs,
-                                                    const uint32_t* __restrict__ elems,
-                                                    const uint32_t* __restrict__ rank_of_member,
-                                                    const uint64_t* gstart, uint8_t* sel8) {
+__device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, const uint32_t* gslab,
+                                          const uint64_t* gebase, const uint32_t* D, const PSlab* slabs,
+                                          const uint32_t* __restrict__ elems,
+                                          const uint32_t* __restrict__ rank_of_member, const uint64_t* gstart,
+                                          uint8_t* sel8, SminLds& L) {
   constexpr uint32_t NS = PACKED ? PHS : HS;  // slots
   constexpr uint32_t CAP = PACKED ? PHCAP : HCAP;
-  __shared__ uint32_t tabs[2 * HS];
-  static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
-  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];  // the walk's scratch, then the emit bitmap
-  __shared__ uint64_t red64[1024 / 64 + 1];
-  __shared__ int full;
+  uint32_t* tabs = L.tabs;
   uint32_t* keys = tabs;  // PACKED: the slots
   uint32_t* vals = tabs + HS;
-  const PItem it = items[blockIdx.x];
   const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
-  const uint32_t E = slab_window_count<1024>(it, sg, gslab, D, reinterpret_cast<uint32_t*>(red64));
+  const uint32_t E = slab_window_count<1024>(it, sg, gslab, D, reinterpret_cast<uint32_t*>(L.red64));
   if (E == 0) return;
   uint32_t R = (E + CAP - 1) / CAP;
   for (uint32_t round = 0; round < R;) {
     for (uint32_t i = threadIdx.x; i < 2 * HS; i += 1024) tabs[i] = (PACKED || i < HS) ? 0xFFFFFFFFu : RANK_NONE;
-    if (threadIdx.x == 0) full = 0;
+    if (threadIdx.x == 0) L.full = 0;
     __syncthreads();
     const uint32_t RR = R, rr = round;
-    for_slab_window<SYZ_SL_HU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, wsc, red64,
+    for_slab_window<SYZ_SL_HU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
                                       [&](uint32_t o, uint32_t Rk) {
                                         if (Rk == RANK_NONE) return;  // a lane past the window
                                         if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
@@ -412,10 +414,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                                             h = (h + 1) & (HS - 1);
                                           }
                                         }
-                                        full = 1;
+                                        L.full = 1;
                                       });
     __syncthreads();
-    if (full) {
+    if (L.full) {
       R *= 2;
       round = 0;
       __syncthreads();
@@ -423,14 +425,35 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     }
     if constexpr (PACKED) {
       const uint32_t g32 = (uint32_t)gb;
-      emit_winner_bytes<PK_SCRATCH_WORDS>(keys, NS, gb, ng, wsc, sel8, [g32](uint32_t v) {
+      emit_winner_bytes<PK_SCRATCH_WORDS>(keys, NS, gb, ng, L.wsc, sel8, [g32](uint32_t v) {
         return v == 0xFFFFFFFFu ? RANK_NONE : g32 + (v & ((1u << PK_RBITS) - 1));
       });
     } else {
-      emit_winner_bytes<PK_SCRATCH_WORDS>(vals, HS, gb, ng, wsc, sel8);
+      emit_winner_bytes<PK_SCRATCH_WORDS>(vals, HS, gb, ng, L.wsc, sel8);
     }
     round++;
+    __syncthreads();  // the emit's bitmap and table reads are done before the next round clears them
   }
+}
+
+__global__ __launch_bounds__(1024) SYZ_SMIN_OCC void k_smin_direct(const PItem* items, const SGroup* sg,
+                                                                   const uint32_t* gslab, const uint64_t* gebase,
+                                                                   const uint32_t* D, const PSlab* slabs,
+                                                                   const uint32_t* __restrict__ elems,
+                                                                   const uint32_t* __restrict__ rank_of_member,
+                                                                   const uint64_t* gstart, uint8_t* sel8) {
+  __shared__ SminLds L;
+  smin_direct(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, sel8, L);
+}
+
+// (one launch for a class's three table kinds measured no better and spills: M is throughput-bound)
+template <bool PACKED>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_smin_hash(
+    const PItem* items, const SGroup* sg, const uint32_t* gslab, const uint64_t* gebase, const uint32_t* D,
+    const PSlab* slabs, const uint32_t* __restrict__ elems, const uint32_t* __restrict__ rank_of_member,
+    const uint64_t* gstart, uint8_t* sel8) {
+  __shared__ SminLds L;
+  smin_hash<PACKED>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, sel8, L);
 }
 
 // ---- outputs: the group-major kept list in selection order ----------------------------------------
@@ -800,7 +823,6 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     const size_t nd = icount[big][PMODE_DIRECT], nh = icount[big][PMODE_HASH], np = icount[big][PMODE_PACKED];
     if (!nd && !nh && !np) return;
     SYZ_HIP(hipStreamWaitEvent(q, big ? c.ev_sct[0] : c.ev_psmall, 0));
-    hipStream_t pq2 = q;
     if (nd) {
       ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
       k_smin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], dsg, gslab, gebase, D, slabs,
@@ -814,16 +836,10 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
       SYZ_LAUNCHED();
     }
     if (np) {
-      {
-        ProfScope pk("k_pmin_packed", pq2, 4 * item_pcs[big][PMODE_PACKED]);
-        k_smin_hash<true><<<(unsigned)np, 1024, 0, pq2>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D,
-                                                           slabs, elems, rank_of_member, gstart, sel8);
-        SYZ_LAUNCHED();
-      }
-      if (pq2 != q) {
-        SYZ_HIP(hipEventRecord(c.ev_msmall2, pq2));
-        SYZ_HIP(hipStreamWaitEvent(q, c.ev_msmall2, 0));
-      }
+      ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
+      k_smin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
+                                                       elems, rank_of_member, gstart, sel8);
+      SYZ_LAUNCHED();
     }
   };
   if (!J.plan || J.plan_key != hstart) {

@@ -133,31 +133,6 @@ __global__ void k_so_tpair(const uint64_t* tstart, uint32_t npairs, uint32_t* tp
     for (uint64_t t = tstart[p]; t < tstart[p + 1]; t++) tpair[t] = p;
 }
 
-// merge path over global memory by one wave: 64 candidates per round (the predicate a[i] <= b[d-i-1]
-// is true, then false), so a range of 2^12 takes two rounds of dependent loads, not twelve
-__device__ __forceinline__ uint32_t merge_path_wave(const uint32_t* A, uint32_t la, const uint32_t* B, uint32_t lb,
-                                                    uint32_t d) {
-  uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;  // answer in [lo, hi]
-  const unsigned lane = __lane_id();
-  while (hi > lo) {
-    const uint32_t n = hi - lo;
-    const uint32_t step = (n + 63) / 64;
-    const uint32_t i = lo + lane * step;
-    const bool t = i < hi && A[i] <= B[d - i - 1];
-    const uint64_t bt = __ballot(t);
-    // the predicate holds on lanes [0, k): the answer is in (lo + (k - 1) step, lo + k step]
-    const uint32_t k = (uint32_t)__popcll(bt);
-    if (k == 0) {
-      hi = lo;
-    } else {
-      const uint32_t nlo = lo + (k - 1) * step + 1;
-      hi = min(hi, lo + k * step);
-      lo = nlo;
-    }
-  }
-  return lo;
-}
-
 // merge path: the number of a-elements among the first d merged ones (a first on ties)
 template <class RA, class RB>
 __device__ __forceinline__ uint32_t merge_path(RA A, uint32_t la, RB B, uint32_t lb, uint32_t d) {
@@ -172,125 +147,223 @@ __device__ __forceinline__ uint32_t merge_path(RA A, uint32_t la, RB B, uint32_t
   return lo;
 }
 
-// COUNT: tcnt[tile] = outputs of the tile; flags bit 0 = a repeated value, err = descending
-// EMIT: the tile's outputs at out[tout[tile]..]
-template <bool EMIT>
-__global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __restrict__ a,
-                                                      const uint64_t* __restrict__ aoff,
-                                                      const uint32_t* __restrict__ b,
-                                                      const uint64_t* __restrict__ boff, uint32_t npairs,
-                                                      const uint64_t* __restrict__ tstart,
-                                                      const uint32_t* __restrict__ tpair, uint32_t* tcnt,
-                                                      const uint64_t* __restrict__ tout, uint32_t* out,
-                                                      int* flags, int* err) {
-  __shared__ uint32_t As[SO_T + 2], Bs[SO_T + 2];  // As[0]: a before the tile; Bs[nb]: b after it
-  __shared__ uint32_t st[EMIT ? SO_T : 1];
-  __shared__ uint32_t red[SO_BLOCK / 64 + 1];
-  __shared__ uint32_t meta[6];
-  // a grid of a few workgroups per CU walks the tiles (one workgroup per tile made the launch's
-  // dispatch the bound: ~1M short workgroups per batch)
+// A tile's sub-lists a[a0, a0 + na) and b[b0, b0 + nb) and the two pairings that cross its edges:
+// SO_B0PAIRED (b[b0] equals the a taken just before the tile, a[a0 - 1]) and SO_ALASTPAIRED (a[a0 + na - 1]
+// equals the b taken just after it, b[b0 + nb]); for strictly increasing lists no other element of a tile
+// can pair across its edges. Built once per batch (which also checks the list order across tile edges),
+// so a tile walk needs no halo loads and its only dependent read is this 32-byte record.
+struct SoDesc {
+  uint64_t a0, b0;
+  uint32_t na, nb, fl, pad;
+};
+constexpr uint32_t SO_B0PAIRED = 1, SO_ALASTPAIRED = 2;
+
+// one thread per tile: its pair and merge-path diagonals (a one-tile pair needs no search)
+__global__ void k_so_tdesc(const uint32_t* __restrict__ a, const uint64_t* __restrict__ aoff,
+                           const uint32_t* __restrict__ b, const uint64_t* __restrict__ boff,
+                           const uint64_t* __restrict__ tstart, const uint32_t* __restrict__ tpair, uint32_t npairs,
+                           SoDesc* __restrict__ desc, int* flags, int* err) {
   const uint64_t ntiles = tstart[npairs];
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-  if (threadIdx.x < 64) {  // wave 0: the tile's diagonals (a one-tile pair needs no search)
-    const uint32_t p = tpair[tile];
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < ntiles; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = tpair[t];
     const uint64_t a0 = aoff[p], b0 = boff[p];
     const uint32_t la = (uint32_t)(aoff[p + 1] - a0), lb = (uint32_t)(boff[p + 1] - b0);
-    const uint32_t d0 = (uint32_t)(tile - tstart[p]) * SO_T, d1 = min(d0 + SO_T, la + lb);
-    const uint32_t* A = a + a0;
-    const uint32_t* B = b + b0;
-    const uint32_t i0 = d0 == 0 ? 0u : merge_path_wave(A, la, B, lb, d0);
-    const uint32_t i1 = d1 == la + lb ? la : merge_path_wave(A, la, B, lb, d1);
-    if (threadIdx.x == 0) {
-      meta[0] = p;
-      meta[1] = i0;
-      meta[2] = i1;
-      meta[3] = d0 - i0;  // j0
-      meta[4] = d1 - i1;  // j1
-      meta[5] = 0;
-    }
-  }
-  __syncthreads();
-  const uint32_t p = meta[0], i0 = meta[1], i1 = meta[2], j0 = meta[3], j1 = meta[4];
-  const uint64_t a0 = aoff[p], b0 = boff[p];
-  const uint32_t la = (uint32_t)(aoff[p + 1] - a0), lb = (uint32_t)(boff[p + 1] - b0);
-  const uint32_t na = i1 - i0, nb = j1 - j0;
-  // halo: the a before the tile (none: a value no b equals... the walk's "previous a" does not exist,
-  // marked by NOPREV), the b after it (the pointer past the pair: NONEXT)
-  for (uint32_t k = threadIdx.x; k < na; k += SO_BLOCK) As[k + 1] = a[a0 + i0 + k];
-  for (uint32_t k = threadIdx.x; k < nb; k += SO_BLOCK) Bs[k] = b[b0 + j0 + k];
-  if (threadIdx.x == 0) As[0] = i0 > 0 ? a[a0 + i0 - 1] : 0u;
-  if (threadIdx.x == 1) Bs[nb] = j1 < lb ? b[b0 + j1] : 0u;
-  // one element past the tile's a run (the order check across tiles)
-  const uint32_t anext = i1 < la ? a[a0 + i1] : 0xFFFFFFFFu;
-  __syncthreads();
-  const bool hasprev = i0 > 0, hasnext = j1 < lb;
-  // order checks: strictly increasing inside the tile and against the next tile's first element
-  if (!EMIT) {
+    const uint32_t d0 = (uint32_t)(t - tstart[p]) * SO_T, d1 = min(d0 + SO_T, la + lb);
+    auto ga = [&](uint32_t i) { return a[a0 + i]; };
+    auto gb = [&](uint32_t j) { return b[b0 + j]; };
+    const uint32_t i0 = d0 == 0 ? 0u : merge_path(ga, la, gb, lb, d0);
+    const uint32_t i1 = d1 == la + lb ? la : merge_path(ga, la, gb, lb, d1);
+    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
+    uint32_t fl = 0;
+    if (i0 > 0 && j0 < j1 && a[a0 + i0 - 1] == b[b0 + j0]) fl |= SO_B0PAIRED;
+    if (i0 < i1 && j1 < lb && a[a0 + i1 - 1] == b[b0 + j1]) fl |= SO_ALASTPAIRED;
+    // the order of the neighbours this tile's end separates
     int f = 0, e = 0;
-    for (uint32_t k = threadIdx.x; k < na; k += SO_BLOCK) {
-      const uint32_t x = As[k + 1];
-      const uint32_t nx = k + 1 < na ? As[k + 2] : (i1 < la ? anext : 0xFFFFFFFFu);
-      if (k + 1 < na || i1 < la) {
-        if (nx < x) e = 1;
-        if (nx == x) f = 1;
-      }
+    if (i1 > 0 && i1 < la) {
+      const uint32_t x = a[a0 + i1 - 1], y = a[a0 + i1];
+      f |= x == y;
+      e |= y < x;
     }
-    for (uint32_t k = threadIdx.x; k < nb; k += SO_BLOCK) {
-      const uint32_t x = Bs[k];
-      if (k + 1 < nb || j1 < lb) {
-        const uint32_t nx = Bs[k + 1];  // (Bs[nb] is the halo)
-        if (nx < x) e = 1;
-        if (nx == x) f = 1;
-      }
+    if (j1 > 0 && j1 < lb) {
+      const uint32_t x = b[b0 + j1 - 1], y = b[b0 + j1];
+      f |= x == y;
+      e |= y < x;
     }
     if (f) atomicOr(flags, 1);
     if (e) atomicOr(err, 1);
+    SoDesc d;
+    d.a0 = a0 + i0;
+    d.b0 = b0 + j0;
+    d.na = i1 - i0;
+    d.nb = j1 - j0;
+    d.fl = fl;
+    d.pad = 0;
+    desc[t] = d;
   }
-  // this thread's merged range [t * VT, (t + 1) * VT) of the tile
-  const uint32_t dt0 = min((uint32_t)threadIdx.x * SO_VT, na + nb), dt1 = min(dt0 + SO_VT, na + nb);
-  auto la_ = [&](uint32_t i) { return As[i + 1]; };
-  auto lb_ = [&](uint32_t j) { return Bs[j]; };
-  uint32_t i = merge_path(la_, na, lb_, nb, dt0), j = dt0 - i;
-  uint32_t outv[SO_VT];
-  uint32_t c = 0;
-  for (uint32_t d = dt0; d < dt1; d++) {
-    const bool take_a = j >= nb || (i < na && As[i + 1] <= Bs[j]);
-    uint32_t v;
-    bool paired, isa;
-    if (take_a) {
-      v = As[i + 1];
-      paired = (j < nb || hasnext) && Bs[j] == v;  // the b at the walk's pointer
-      isa = true;
-      i++;
-    } else {
-      v = Bs[j];
-      paired = (i > 0 || hasprev) && As[i] == v;  // the a taken just before
-      isa = false;
-      j++;
+}
+
+constexpr int SO_RSRC_FLAGS = 0x00020000;
+
+// COUNT: tcnt[tile] = outputs of the tile; flags bit 0 = a repeated value, err = descending
+// EMIT: the tile's outputs at out[tout[tile]..]
+// A grid of a few workgroups per CU walks the tiles (one workgroup per tile made the launch's dispatch
+// the bound: ~1M short workgroups per batch). The walk is software-pipelined: while tile k merges out of
+// LDS, tile k+1's elements and tile k+2's record are in flight into registers. Every global access is a
+// buffer op whose descriptor range is the tile's own (out-of-range loads return 0, stores are dropped),
+// so the loop has no data-dependent branches around memory and the only wait before staging a tile is
+// for its own loads (issued a merge earlier), not for the stores behind them.
+template <bool EMIT>
+__global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __restrict__ a,
+                                                      const uint32_t* __restrict__ b,
+                                                      const SoDesc* __restrict__ desc,
+                                                      const uint64_t* __restrict__ ntiles_dev, uint32_t* tcnt,
+                                                      const uint64_t* __restrict__ tout, uint32_t* out, int* flags,
+                                                      int* err) {
+  __shared__ uint32_t As[SO_T], Bs[SO_T];
+  __shared__ uint32_t st[EMIT ? SO_T : 1];
+  __shared__ uint32_t red[SO_BLOCK / 64 + 1];
+  const uint64_t ntiles = *ntiles_dev;
+  uint64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  const uint32_t lane = __lane_id();
+  // a tile's record (lanes 0..7, one word each) and, for EMIT, its output offset (lanes 0..1)
+  auto rec_load = [&](uint64_t t) {
+    const bool ok = t < ntiles;
+    const auto r = __builtin_amdgcn_make_buffer_rsrc((void*)(desc + (ok ? t : 0)), 0, ok ? 32 : 0, SO_RSRC_FLAGS);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (lane & 7) * 4, 0, 0);
+  };
+  auto tout_load = [&](uint64_t t) {
+    const bool ok = EMIT && t < ntiles;
+    const auto r = __builtin_amdgcn_make_buffer_rsrc((void*)(tout + (ok ? t : 0)), 0, ok ? 8 : 0, SO_RSRC_FLAGS);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (lane & 1) * 4, 0, 0);
+  };
+  uint32_t ra[SO_VT], rb[SO_VT];
+  auto fetch = [&](uint64_t a0, uint32_t na, uint64_t b0, uint32_t nb) {
+    const auto rsa = __builtin_amdgcn_make_buffer_rsrc((void*)(a + a0), 0, na * 4, SO_RSRC_FLAGS);
+    const auto rsb = __builtin_amdgcn_make_buffer_rsrc((void*)(b + b0), 0, nb * 4, SO_RSRC_FLAGS);
+#pragma unroll
+    for (int r = 0; r < SO_VT; r++) {
+      ra[r] = __builtin_amdgcn_raw_buffer_load_b32(rsa, (threadIdx.x + r * SO_BLOCK) * 4, 0, 0);
+      rb[r] = __builtin_amdgcn_raw_buffer_load_b32(rsb, (threadIdx.x + r * SO_BLOCK) * 4, 0, 0);
     }
-    bool emit;
-    switch (op) {
-      case SYZGPU_DIFFERENCE: emit = isa && !paired; break;
-      case SYZGPU_INTERSECTION: emit = isa && paired; break;
-      case SYZGPU_UNION: emit = isa || !paired; break;
-      default: emit = !paired; break;  // symmetric difference
-    }
-    emit = emit && v != SENT;
-    if (EMIT && emit) outv[c] = v;
-    c += emit ? 1u : 0u;
+  };
+  auto field = [](uint32_t w, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)w, k); };
+  auto a0_of = [&](uint32_t w) { return (uint64_t)field(w, 0) | (uint64_t)field(w, 1) << 32; };
+  auto b0_of = [&](uint32_t w) { return (uint64_t)field(w, 2) | (uint64_t)field(w, 3) << 32; };
+  // prologue: tile k's record (waited for), its elements, tile k+1's record and tile k's output offset
+  uint32_t dw = rec_load(tile);
+  uint32_t na = field(dw, 4), nb = field(dw, 5), fl = field(dw, 6);
+  fetch(a0_of(dw), na, b0_of(dw), nb);
+  dw = rec_load(tile + gridDim.x);
+  uint32_t tw = tout_load(tile);
+  {
+    // as many (empty-range, dropped) stores as an iteration ends with, so the loop head's wait for the
+    // loads above is the same counted vmcnt on entry as on the back edge (else the merge makes it vmcnt(0),
+    // a wait for the previous tile's stores)
+    const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)(EMIT ? out : tcnt), 0, 0, SO_RSRC_FLAGS);
+#pragma unroll
+    for (int r = 0; r < (EMIT ? SO_VT : 1); r++)
+      __builtin_amdgcn_raw_buffer_store_b32(0u, rz, (threadIdx.x + r * SO_BLOCK) * 4, 0, 0);
   }
-  uint32_t tot;
-  const uint32_t pre = block_excl_scan<SO_BLOCK>(c, red, &tot);
-  if (!EMIT) {
-    if (threadIdx.x == 0) tcnt[tile] = tot;
-  } else {
-    for (uint32_t k = 0; k < c; k++) st[pre + k] = outv[k];
+  int f = 0, e = 0;  // a repeated value / a descending neighbour, over all of this thread's tiles
+  for (;;) {
+#pragma unroll
+    for (int r = 0; r < SO_VT; r++) {
+      As[threadIdx.x + r * SO_BLOCK] = ra[r];
+      Bs[threadIdx.x + r * SO_BLOCK] = rb[r];
+    }
+    const uint64_t obase = EMIT ? (uint64_t)field(tw, 0) | (uint64_t)field(tw, 1) << 32 : 0;
+    const uint32_t cna = na, cnb = nb, cfl = fl;
+    const uint64_t next = tile + gridDim.x;
     __syncthreads();
-    uint32_t* o = out + tout[tile];
-    for (uint32_t k = threadIdx.x; k < tot; k += SO_BLOCK) o[k] = st[k];
+    // tile k+1: its elements in flight during this merge (a past-the-end tile loads nothing)
+    {
+      const bool ok = next < ntiles;
+      na = ok ? field(dw, 4) : 0;
+      nb = ok ? field(dw, 5) : 0;
+      fl = field(dw, 6);
+      fetch(ok ? a0_of(dw) : 0, na, ok ? b0_of(dw) : 0, nb);
+      dw = rec_load(next + gridDim.x);
+      tw = tout_load(next);
+    }
+    // order checks inside the tile (its edges are the record builder's)
+#pragma unroll
+    for (int r = 0; r < SO_VT; r++) {
+      const uint32_t k = threadIdx.x + r * SO_BLOCK;
+      if (k + 1 < cna) {
+        const uint32_t x = As[k], y = As[k + 1];
+        f |= x == y;
+        e |= y < x;
+      }
+      if (k + 1 < cnb) {
+        const uint32_t x = Bs[k], y = Bs[k + 1];
+        f |= x == y;
+        e |= y < x;
+      }
+    }
+    // this thread's merged range [t * VT, (t + 1) * VT) of the tile
+    const uint32_t dt0 = min((uint32_t)threadIdx.x * SO_VT, cna + cnb), dt1 = min(dt0 + SO_VT, cna + cnb);
+    auto la_ = [&](uint32_t i) { return As[i]; };
+    auto lb_ = [&](uint32_t j) { return Bs[j]; };
+    uint32_t i = merge_path(la_, cna, lb_, cnb, dt0), j = dt0 - i;
+    uint32_t outv[SO_VT];
+    uint32_t c = 0, em = 0;  // em bit r: merged element dt0 + r is an output
+#pragma unroll
+    for (int r = 0; r < SO_VT; r++) {
+      if (dt0 + r >= dt1) break;
+      const bool take_a = j >= cnb || (i < cna && As[i] <= Bs[j]);
+      uint32_t v;
+      bool paired, isa;
+      if (take_a) {
+        v = As[i];
+        paired = j < cnb ? Bs[j] == v : (i + 1 == cna && (cfl & SO_ALASTPAIRED));  // the b at the walk's pointer
+        isa = true;
+        i++;
+      } else {
+        v = Bs[j];
+        paired = i > 0 ? As[i - 1] == v : (j == 0 && (cfl & SO_B0PAIRED));  // the a taken just before
+        isa = false;
+        j++;
+      }
+      bool emit;
+      switch (op) {
+        case SYZGPU_DIFFERENCE: emit = isa && !paired; break;
+        case SYZGPU_INTERSECTION: emit = isa && paired; break;
+        case SYZGPU_UNION: emit = isa || !paired; break;
+        default: emit = !paired; break;  // symmetric difference
+      }
+      emit = emit && v != SENT;
+      outv[r] = v;
+      em |= emit ? 1u << r : 0u;
+      c += emit ? 1u : 0u;
+    }
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<SO_BLOCK>(c, red, &tot);
+    if (!EMIT) {
+      const auto rc = __builtin_amdgcn_make_buffer_rsrc((void*)(tcnt + tile), 0, 4, SO_RSRC_FLAGS);
+      __builtin_amdgcn_raw_buffer_store_b32(tot, rc, threadIdx.x * 4, 0, 0);  // thread 0's store is the one in range
+    } else {
+#pragma unroll
+      for (int r = 0; r < SO_VT; r++)
+        if (em >> r & 1) st[pre + __popc(em & ((1u << r) - 1))] = outv[r];
+      __syncthreads();
+      const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + obase), 0, tot * 4, SO_RSRC_FLAGS);
+#pragma unroll
+      for (int r = 0; r < SO_VT; r++) {
+        const uint32_t k = threadIdx.x + r * SO_BLOCK;
+        __builtin_amdgcn_raw_buffer_store_b32(st[k], ro, k * 4, 0, 0);
+      }
+    }
+    __syncthreads();  // the tile's LDS is free for the next one
+    if (next >= ntiles) break;
+    tile = next;
   }
-  __syncthreads();  // the tile's LDS is free for the next one
-  }  // tiles
+  if (__ballot(f)) {
+    if (lane == 0) atomicOr(flags, 1);
+  }
+  if (__ballot(e)) {
+    if (lane == 0) atomicOr(err, 1);
+  }
 }
 
 // workgroups of a tile walk: enough to fill the CUs several times over (env SYZGPU_SO_GRID for A/B)
@@ -325,15 +398,18 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
   int* fl = c.scratch.get<int>("so_fl", 2);
   SYZ_HIP(hipMemsetAsync(fl, 0, 2 * sizeof(int), s));
   uint32_t* tpair = c.scratch.get<uint32_t>("so_tpair", tbound + 1);
+  SoDesc* desc = c.scratch.get<SoDesc>("so_desc", tbound + 1);
   k_so_ntiles<<<grid_for(npairs, 256, 4096), 256, 0, s>>>(aoff, boff, npairs, ntile);
   SYZ_LAUNCHED();
   exclusive_scan_u32(ntile, tstart, npairs, s);
   k_so_tpair<<<grid_for(npairs, 256, 4096), 256, 0, s>>>(tstart, npairs, tpair);
   SYZ_LAUNCHED();
+  k_so_tdesc<<<grid_for(tbound, 256, 8192), 256, 0, s>>>(a, aoff, b, boff, tstart, tpair, npairs, desc, fl, fl + 1);
+  SYZ_LAUNCHED();
   {
     ProfScope ps("setop_count", s, 4 * (na + nb) + 16 * (uint64_t)npairs);
-    k_so_tile<false><<<so_grid(tbound), SO_BLOCK, 0, s>>>(op, a, aoff, b, boff, npairs, tstart, tpair, tcnt, nullptr,
-                                                           nullptr, fl, fl + 1);
+    k_so_tile<false><<<so_grid(tbound), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, tcnt, nullptr, nullptr,
+                                                           fl, fl + 1);
     SYZ_LAUNCHED();
   }
   uint64_t* hnt = c.pinned.get<uint64_t>(2);
@@ -355,8 +431,8 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
   if (total > out_cap) fail(SYZGPU_ECAPACITY, "set operation output capacity too small");
   if (ntiles) {
     ProfScope ps("setop_emit", s, 4 * (na + nb) + 4 * total + 8 * (uint64_t)npairs);
-    k_so_tile<true><<<so_grid(ntiles), SO_BLOCK, 0, s>>>(op, a, aoff, b, boff, npairs, tstart, tpair, nullptr, tout, out,
-                                                         nullptr, nullptr);
+    k_so_tile<true><<<so_grid(ntiles), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, nullptr, tout, out, nullptr,
+                                                         nullptr);
     SYZ_LAUNCHED();
   }
   return total;
