@@ -116,9 +116,11 @@ __global__ __launch_bounds__(256) void k_setop_scatter(int side, const uint32_t*
 // of the counts, stages them in LDS and stores the tile's run coalesced (emit). A pair with a repeated
 // value (allowed by Go, never produced by the executor's sort + unique) sends the batch to the
 // per-element rank path above; a descending neighbour is the Go panic (EINVAL).
-constexpr int SO_BLOCK = 256;
-constexpr int SO_VT = 4;
+constexpr int SO_BLOCK = 128;
+constexpr int SO_VT = 8;
 constexpr uint32_t SO_T = SO_BLOCK * SO_VT;  // merged elements per tile
+constexpr int SO_LOG_T = 10;
+static_assert(SO_T == 1u << SO_LOG_T, "tile size");
 
 __global__ void k_so_ntiles(const uint64_t* aoff, const uint64_t* boff, uint32_t npairs, uint32_t* nt) {
   for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += gridDim.x * blockDim.x) {
@@ -147,16 +149,17 @@ __device__ __forceinline__ uint32_t merge_path(RA A, uint32_t la, RB B, uint32_t
   return lo;
 }
 
-// A tile's sub-lists a[a0, a0 + na) and b[b0, b0 + nb) and the two pairings that cross its edges:
-// SO_B0PAIRED (b[b0] equals the a taken just before the tile, a[a0 - 1]) and SO_ALASTPAIRED (a[a0 + na - 1]
-// equals the b taken just after it, b[b0 + nb]); for strictly increasing lists no other element of a tile
-// can pair across its edges. Built once per batch (which also checks the list order across tile edges),
-// so a tile walk needs no halo loads and its only dependent read is this 32-byte record.
+// A tile's sub-lists a[a0, a0 + na) and b[b0, b0 + nb) (n = na | nb << 16) and its halo values: aprev, the a
+// taken just before the tile (a[a0 - 1]; without one, b[b0] - 1, which pairs with no b of the tile but a
+// sentinel); anext / bnext, the a / b taken after it (0xFFFFFFFF past the pair's end: the sentinel is never
+// an output). With them a tile's merge is closed: an exhausted list reads its halo, which orders after
+// everything the other list still has in the tile (the merge-path property), and a pairing across a tile
+// edge is a compare against a halo. Built once per batch (which also checks the list order across tile
+// edges), so a tile walk's only dependent read is this 32-byte record.
 struct SoDesc {
   uint64_t a0, b0;
-  uint32_t na, nb, fl, pad;
+  uint32_t n, aprev, anext, bnext;
 };
-constexpr uint32_t SO_B0PAIRED = 1, SO_ALASTPAIRED = 2;
 
 // one thread per tile: its pair and merge-path diagonals (a one-tile pair needs no search)
 __global__ void k_so_tdesc(const uint32_t* __restrict__ a, const uint64_t* __restrict__ aoff,
@@ -174,9 +177,6 @@ __global__ void k_so_tdesc(const uint32_t* __restrict__ a, const uint64_t* __res
     const uint32_t i0 = d0 == 0 ? 0u : merge_path(ga, la, gb, lb, d0);
     const uint32_t i1 = d1 == la + lb ? la : merge_path(ga, la, gb, lb, d1);
     const uint32_t j0 = d0 - i0, j1 = d1 - i1;
-    uint32_t fl = 0;
-    if (i0 > 0 && j0 < j1 && a[a0 + i0 - 1] == b[b0 + j0]) fl |= SO_B0PAIRED;
-    if (i0 < i1 && j1 < lb && a[a0 + i1 - 1] == b[b0 + j1]) fl |= SO_ALASTPAIRED;
     // the order of the neighbours this tile's end separates
     int f = 0, e = 0;
     if (i1 > 0 && i1 < la) {
@@ -194,34 +194,43 @@ __global__ void k_so_tdesc(const uint32_t* __restrict__ a, const uint64_t* __res
     SoDesc d;
     d.a0 = a0 + i0;
     d.b0 = b0 + j0;
-    d.na = i1 - i0;
-    d.nb = j1 - j0;
-    d.fl = fl;
-    d.pad = 0;
+    d.n = (i1 - i0) | (j1 - j0) << 16;
+    d.aprev = i0 > 0 ? a[a0 + i0 - 1] : j0 < j1 ? b[b0 + j0] - 1u : 0u;
+    d.anext = i1 < la ? a[a0 + i1] : 0xFFFFFFFFu;
+    d.bnext = j1 < lb ? b[b0 + j1] : 0xFFFFFFFFu;
     desc[t] = d;
   }
 }
 
 constexpr int SO_RSRC_FLAGS = 0x00020000;
 
-// COUNT: tcnt[tile] = outputs of the tile; flags bit 0 = a repeated value, err = descending
-// EMIT: the tile's outputs at out[tout[tile]..]
+// SO_COUNT: tcnt[tile] = outputs of the tile; flags bit 0 = a repeated value, err = descending
+// SO_EMIT: the tile's outputs at out[tout[tile]..] (after a scan of the counts)
+// SO_GAP: both in one pass, the outputs at out[a0 + b0..] (the tile's merged start: a gapped image of the
+// result in a scratch of na + nb words, which k_so_compact closes up after the scan)
 // A grid of a few workgroups per CU walks the tiles (one workgroup per tile made the launch's dispatch
 // the bound: ~1M short workgroups per batch). The walk is software-pipelined: while tile k merges out of
 // LDS, tile k+1's elements and tile k+2's record are in flight into registers. Every global access is a
 // buffer op whose descriptor range is the tile's own (out-of-range loads return 0, stores are dropped),
 // so the loop has no data-dependent branches around memory and the only wait before staging a tile is
 // for its own loads (issued a merge earlier), not for the stores behind them.
-template <bool EMIT>
+constexpr int SO_COUNT = 0, SO_EMIT = 1, SO_GAP = 2;
+template <int MODE>
 __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __restrict__ a,
                                                       const uint32_t* __restrict__ b,
                                                       const SoDesc* __restrict__ desc,
                                                       const uint64_t* __restrict__ ntiles_dev, uint32_t* tcnt,
                                                       const uint64_t* __restrict__ tout, uint32_t* out, int* flags,
                                                       int* err) {
-  __shared__ uint32_t As[SO_T], Bs[SO_T];
-  __shared__ uint32_t st[EMIT ? SO_T : 1];
+  constexpr bool EMIT = MODE != SO_COUNT, CHECK = MODE != SO_EMIT, DIRECT = MODE == SO_EMIT;
+  // (+ SO_VT + 1: a walk that runs past a list's end reads on, ignored, instead of clamping its index)
+  __shared__ __attribute__((aligned(16))) uint32_t As[SO_T + SO_VT + 4], Bs[SO_T + SO_VT + 4];
+  __shared__ uint32_t st[EMIT ? SO_T + 1 : 1];
   __shared__ uint32_t red[SO_BLOCK / 64 + 1];
+  // the op's outputs (cover.go:81-102): a paired / a unpaired / b unpaired (a paired b is never one)
+  const bool eap = op == SYZGPU_INTERSECTION || op == SYZGPU_UNION;
+  const bool eau = op != SYZGPU_INTERSECTION;
+  const bool ebu = op == SYZGPU_UNION || op == SYZGPU_SYMMETRIC_DIFFERENCE;
   const uint64_t ntiles = *ntiles_dev;
   uint64_t tile = blockIdx.x;
   if (tile >= ntiles) return;
@@ -233,7 +242,7 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
     return __builtin_amdgcn_raw_buffer_load_b32(r, (lane & 7) * 4, 0, 0);
   };
   auto tout_load = [&](uint64_t t) {
-    const bool ok = EMIT && t < ntiles;
+    const bool ok = DIRECT && t < ntiles;
     const auto r = __builtin_amdgcn_make_buffer_rsrc((void*)(tout + (ok ? t : 0)), 0, ok ? 8 : 0, SO_RSRC_FLAGS);
     return __builtin_amdgcn_raw_buffer_load_b32(r, (lane & 1) * 4, 0, 0);
   };
@@ -252,7 +261,9 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
   auto b0_of = [&](uint32_t w) { return (uint64_t)field(w, 2) | (uint64_t)field(w, 3) << 32; };
   // prologue: tile k's record (waited for), its elements, tile k+1's record and tile k's output offset
   uint32_t dw = rec_load(tile);
-  uint32_t na = field(dw, 4), nb = field(dw, 5), fl = field(dw, 6);
+  uint32_t na = field(dw, 4) & 0xFFFFu, nb = field(dw, 4) >> 16;
+  uint32_t hp = field(dw, 5), ha = field(dw, 6), hb = field(dw, 7);
+  uint64_t gbase = a0_of(dw) + b0_of(dw);  // SO_GAP's output offset of the tile in flight
   fetch(a0_of(dw), na, b0_of(dw), nb);
   dw = rec_load(tile + gridDim.x);
   uint32_t tw = tout_load(tile);
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
     // a wait for the previous tile's stores)
     const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)(EMIT ? out : tcnt), 0, 0, SO_RSRC_FLAGS);
 #pragma unroll
-    for (int r = 0; r < (EMIT ? SO_VT : 1); r++)
+    for (int r = 0; r < (EMIT ? SO_VT : 0) + (CHECK ? 1 : 0); r++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, rz, (threadIdx.x + r * SO_BLOCK) * 4, 0, 0);
   }
   int f = 0, e = 0;  // a repeated value / a descending neighbour, over all of this thread's tiles
@@ -272,86 +283,95 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
       As[threadIdx.x + r * SO_BLOCK] = ra[r];
       Bs[threadIdx.x + r * SO_BLOCK] = rb[r];
     }
-    const uint64_t obase = EMIT ? (uint64_t)field(tw, 0) | (uint64_t)field(tw, 1) << 32 : 0;
-    const uint32_t cna = na, cnb = nb, cfl = fl;
+    const uint64_t obase = DIRECT ? (uint64_t)field(tw, 0) | (uint64_t)field(tw, 1) << 32 : gbase;
+    const uint32_t cna = na, cnb = nb, chp = hp, cha = ha, chb = hb;
     const uint64_t next = tile + gridDim.x;
     __syncthreads();
     // tile k+1: its elements in flight during this merge (a past-the-end tile loads nothing)
     {
       const bool ok = next < ntiles;
-      na = ok ? field(dw, 4) : 0;
-      nb = ok ? field(dw, 5) : 0;
-      fl = field(dw, 6);
+      na = ok ? field(dw, 4) & 0xFFFFu : 0;
+      nb = ok ? field(dw, 4) >> 16 : 0;
+      hp = field(dw, 5);
+      ha = field(dw, 6);
+      hb = field(dw, 7);
       fetch(ok ? a0_of(dw) : 0, na, ok ? b0_of(dw) : 0, nb);
+      gbase = ok ? a0_of(dw) + b0_of(dw) : 0;
       dw = rec_load(next + gridDim.x);
       tw = tout_load(next);
     }
-    // order checks inside the tile (its edges are the record builder's)
+    // this thread's merged range [t * VT, (t + 1) * VT) of the tile, from the merge path at its start by
+    // a fixed number of halvings
+    const uint32_t m = cna + cnb, dt0 = min((uint32_t)threadIdx.x * SO_VT, m);
+    uint32_t lo = dt0 > cnb ? dt0 - cnb : 0u, hi = min(dt0, cna);
 #pragma unroll
-    for (int r = 0; r < SO_VT; r++) {
-      const uint32_t k = threadIdx.x + r * SO_BLOCK;
-      if (k + 1 < cna) {
-        const uint32_t x = As[k], y = As[k + 1];
-        f |= x == y;
-        e |= y < x;
-      }
-      if (k + 1 < cnb) {
-        const uint32_t x = Bs[k], y = Bs[k + 1];
-        f |= x == y;
-        e |= y < x;
-      }
+    for (int it = 0; it < SO_LOG_T + 1; it++) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const bool le = As[mid & (SO_T - 1)] <= Bs[(dt0 - mid - 1) & (SO_T - 1)];
+      const bool live = lo < hi;
+      lo = (live & le) ? mid + 1 : lo;
+      hi = (live & !le) ? mid : hi;
     }
-    // this thread's merged range [t * VT, (t + 1) * VT) of the tile
-    const uint32_t dt0 = min((uint32_t)threadIdx.x * SO_VT, cna + cnb), dt1 = min(dt0 + SO_VT, cna + cnb);
-    auto la_ = [&](uint32_t i) { return As[i]; };
-    auto lb_ = [&](uint32_t j) { return Bs[j]; };
-    uint32_t i = merge_path(la_, cna, lb_, cnb, dt0), j = dt0 - i;
+    uint32_t i = lo, j = dt0 - lo;
+    const uint32_t pv = As[i > 0 ? i - 1 : 0];
+    uint32_t pa = i > 0 ? pv : chp;  // the a taken just before
     uint32_t outv[SO_VT];
     uint32_t c = 0, em = 0;  // em bit r: merged element dt0 + r is an output
 #pragma unroll
     for (int r = 0; r < SO_VT; r++) {
-      if (dt0 + r >= dt1) break;
-      const bool take_a = j >= cnb || (i < cna && As[i] <= Bs[j]);
-      uint32_t v;
-      bool paired, isa;
-      if (take_a) {
-        v = As[i];
-        paired = j < cnb ? Bs[j] == v : (i + 1 == cna && (cfl & SO_ALASTPAIRED));  // the b at the walk's pointer
-        isa = true;
-        i++;
-      } else {
-        v = Bs[j];
-        paired = i > 0 ? As[i - 1] == v : (j == 0 && (cfl & SO_B0PAIRED));  // the a taken just before
-        isa = false;
-        j++;
-      }
-      bool emit;
-      switch (op) {
-        case SYZGPU_DIFFERENCE: emit = isa && !paired; break;
-        case SYZGPU_INTERSECTION: emit = isa && paired; break;
-        case SYZGPU_UNION: emit = isa || !paired; break;
-        default: emit = !paired; break;  // symmetric difference
-      }
-      emit = emit && v != SENT;
+      const uint32_t av = As[i], bv = Bs[j];
+      const uint32_t ae = i < cna ? av : cha, be = j < cnb ? bv : chb;  // an exhausted list reads its halo
+      const bool take_a = ae <= be;
+      const uint32_t v = take_a ? ae : be;
+      // a: paired with the b at the walk's pointer; b: with the a taken just before it
+      const bool paired = (take_a ? be : pa) == v;
+      const bool out_a = paired ? eap : eau;
+      const bool emit = (dt0 + r < m) & (v != SENT) & (take_a ? out_a : (!paired & ebu));
       outv[r] = v;
       em |= emit ? 1u << r : 0u;
       c += emit ? 1u : 0u;
+      pa = take_a ? ae : pa;
+      i += take_a ? 1u : 0u;
+      j += take_a ? 0u : 1u;
     }
     uint32_t tot;
     const uint32_t pre = block_excl_scan<SO_BLOCK>(c, red, &tot);
-    if (!EMIT) {
+    tot = __builtin_amdgcn_readfirstlane(tot);  // (uniform: a store range from a VGPR is a waterfall loop)
+    if (CHECK) {
       const auto rc = __builtin_amdgcn_make_buffer_rsrc((void*)(tcnt + tile), 0, 4, SO_RSRC_FLAGS);
       __builtin_amdgcn_raw_buffer_store_b32(tot, rc, threadIdx.x * 4, 0, 0);  // thread 0's store is the one in range
-    } else {
+    }
+    if (EMIT) {
 #pragma unroll
       for (int r = 0; r < SO_VT; r++)
-        if (em >> r & 1) st[pre + __popc(em & ((1u << r) - 1))] = outv[r];
+        st[(em >> r & 1) ? pre + __popc(em & ((1u << r) - 1)) : SO_T] = outv[r];  // st[SO_T]: a dump slot
       __syncthreads();
       const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + obase), 0, tot * 4, SO_RSRC_FLAGS);
 #pragma unroll
       for (int r = 0; r < SO_VT; r++) {
         const uint32_t k = threadIdx.x + r * SO_BLOCK;
         __builtin_amdgcn_raw_buffer_store_b32(st[k], ro, k * 4, 0, 0);
+      }
+    }
+    // order checks inside the tile (its edges are the record builder's), after the merge so that their
+    // reads are not hoisted into it (register pressure); like the merge, branch-free
+    if (CHECK) {  // (the emit pass runs only on checked input)
+      const uint32_t k0 = threadIdx.x * SO_VT;  // this thread's VT neighbours of each list, read as b128s
+#pragma unroll
+      for (int side = 0; side < 2; side++) {
+        const uint32_t* S = side ? Bs : As;
+        const uint32_t n = side ? cnb : cna;
+#pragma unroll
+        for (int q = 0; q < SO_VT; q += 4) {  // a b128 and the element after it at a time (few live VGPRs)
+          const uint4 x = *reinterpret_cast<const uint4*>(S + k0 + q);
+          const uint32_t v[5] = {x.x, x.y, x.z, x.w, S[(k0 + q + 4) & (SO_T - 1)]};
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const bool ok = k0 + q + u + 1 < n;
+            f |= ok & (v[u] == v[u + 1]);  // (bitwise: && would become branches)
+            e |= ok & (v[u + 1] < v[u]);
+          }
+        }
       }
     }
     __syncthreads();  // the tile's LDS is free for the next one
@@ -366,9 +386,81 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
   }
 }
 
+// SO_GAP's gapped image closed up: tile t's tcnt[t] outputs from gap[a0 + b0..] to out[tout[t]..]. Each
+// WAVE walks its own tiles (no LDS, no barrier: more tiles in flight per CU for a walk that is all latency),
+// pipelined like k_so_tile: tile k+1's words and tile k+2's offsets are in flight while tile k is stored.
+constexpr int SC_VT = SO_T / 64;
+__global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restrict__ desc,
+                                                         const uint32_t* __restrict__ tcnt,
+                                                         const uint64_t* __restrict__ tout,
+                                                         const uint64_t* __restrict__ ntiles_dev,
+                                                         const uint32_t* __restrict__ gap, uint32_t* out) {
+  const uint64_t ntiles = *ntiles_dev;
+  const uint64_t stride = (uint64_t)gridDim.x * (SO_BLOCK / 64);
+  uint64_t tile = (uint64_t)blockIdx.x * (SO_BLOCK / 64) + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (tile >= ntiles) return;
+  const uint32_t lane = __lane_id();
+  // a tile's offsets, one word a lane: 0..3 the record's a0/b0, 4 its count, 5..6 its output offset
+  auto meta_load = [&](uint64_t t) {
+    const bool ok = t < ntiles;
+    const uint64_t tt = ok ? t : 0;
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(desc + tt), 0, ok ? 16 : 0, SO_RSRC_FLAGS);
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc((void*)(tcnt + tt), 0, ok ? 4 : 0, SO_RSRC_FLAGS);
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(tout + tt), 0, ok ? 8 : 0, SO_RSRC_FLAGS);
+    const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(rd, (lane & 3) * 4, 0, 0);
+    const uint32_t y = __builtin_amdgcn_raw_buffer_load_b32(rc, 0, 0, 0);
+    const uint32_t z = __builtin_amdgcn_raw_buffer_load_b32(ro, (lane & 1) * 4, 0, 0);
+    return lane < 4 ? x : lane == 4 ? y : z;  // (lanes 5, 6: z's words 1, 0; fixed below)
+  };
+  auto field = [](uint32_t w, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)w, k); };
+  auto src_of = [&](uint32_t w) {
+    return ((uint64_t)field(w, 0) | (uint64_t)field(w, 1) << 32) + ((uint64_t)field(w, 2) | (uint64_t)field(w, 3) << 32);
+  };
+  auto dst_of = [&](uint32_t w) { return (uint64_t)field(w, 6) | (uint64_t)field(w, 5) << 32; };  // lane 6: word 0
+  uint32_t cur[SC_VT], nxt[SC_VT];
+  auto fetch = [&](uint32_t w, bool ok, uint32_t* v) {
+    const uint32_t n = ok ? field(w, 4) : 0;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(gap + (ok ? src_of(w) : 0)), 0, n * 4, SO_RSRC_FLAGS);
+#pragma unroll
+    for (int r = 0; r < SC_VT; r++)
+      v[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, (lane + r * 64) * 4, 0, 0);
+  };
+  uint32_t mw = meta_load(tile);
+  uint32_t n = field(mw, 4);
+  uint64_t dst = dst_of(mw);
+  fetch(mw, true, cur);
+  mw = meta_load(tile + stride);
+  {
+    const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, 0, SO_RSRC_FLAGS);  // (see k_so_tile)
+#pragma unroll
+    for (int r = 0; r < SC_VT; r++)
+      __builtin_amdgcn_raw_buffer_store_b32(0u, rz, (lane + r * 64) * 4, 0, 0);
+  }
+  // one tile stored from cv while the next one loads into nv (two register sets, alternated, so the
+  // loads in flight are never copied, which would wait for them)
+  auto step = [&](uint32_t* cv, uint32_t* nv) {
+    const uint64_t next = tile + stride;
+    const bool ok = next < ntiles;
+    const uint32_t cn = n;
+    const uint64_t cdst = dst;
+    n = ok ? field(mw, 4) : 0;
+    dst = ok ? dst_of(mw) : 0;
+    fetch(mw, ok, nv);
+    mw = meta_load(next + stride);
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(out + cdst), 0, cn * 4, SO_RSRC_FLAGS);
+#pragma unroll
+    for (int r = 0; r < SC_VT; r++)
+      __builtin_amdgcn_raw_buffer_store_b32(cv[r], rd, (lane + r * 64) * 4, 0, 0);
+    tile = next;
+    return ok;
+  };
+  while (step(cur, nxt) && step(nxt, cur)) {
+  }
+}
+
 // workgroups of a tile walk: enough to fill the CUs several times over (env SYZGPU_SO_GRID for A/B)
 static unsigned so_grid(uint64_t tiles) {
-  static const unsigned cap = getenv("SYZGPU_SO_GRID") ? (unsigned)atoi(getenv("SYZGPU_SO_GRID")) : 8192u;
+  static const unsigned cap = getenv("SYZGPU_SO_GRID") ? (unsigned)atoi(getenv("SYZGPU_SO_GRID")) : 16384u;
   return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, cap));
 }
 
@@ -406,10 +498,19 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
   SYZ_LAUNCHED();
   k_so_tdesc<<<grid_for(tbound, 256, 8192), 256, 0, s>>>(a, aoff, b, boff, tstart, tpair, npairs, desc, fl, fl + 1);
   SYZ_LAUNCHED();
-  {
+  // one merge pass into a gapped image + a compaction (default), or count + scan + a second merge
+  // (SYZGPU_SO_TWOPASS=1, for A/B: the merge is VALU-bound, so running it once is what pays)
+  static const bool twopass = getenv("SYZGPU_SO_TWOPASS") && atoi(getenv("SYZGPU_SO_TWOPASS"));
+  uint32_t* gap = twopass ? nullptr : c.scratch.get<uint32_t>("so_gap", na + nb + 1);
+  if (twopass) {
     ProfScope ps("setop_count", s, 4 * (na + nb) + 16 * (uint64_t)npairs);
-    k_so_tile<false><<<so_grid(tbound), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, tcnt, nullptr, nullptr,
-                                                           fl, fl + 1);
+    k_so_tile<SO_COUNT><<<so_grid(tbound), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, tcnt, nullptr, nullptr,
+                                                              fl, fl + 1);
+    SYZ_LAUNCHED();
+  } else {
+    ProfScope ps("setop_merge", s, 4 * (na + nb) + 16 * (uint64_t)npairs);
+    k_so_tile<SO_GAP><<<so_grid(tbound), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, tcnt, nullptr, gap, fl,
+                                                            fl + 1);
     SYZ_LAUNCHED();
   }
   uint64_t* hnt = c.pinned.get<uint64_t>(2);
@@ -429,10 +530,14 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
     return setop_batch_rank(op, a, aoff, na, b, boff, nb, npairs, out, out_cap, out_off_dev, s);
   const uint64_t total = *htot;
   if (total > out_cap) fail(SYZGPU_ECAPACITY, "set operation output capacity too small");
-  if (ntiles) {
+  if (ntiles && twopass) {
     ProfScope ps("setop_emit", s, 4 * (na + nb) + 4 * total + 8 * (uint64_t)npairs);
-    k_so_tile<true><<<so_grid(ntiles), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, nullptr, tout, out, nullptr,
-                                                         nullptr);
+    k_so_tile<SO_EMIT><<<so_grid(ntiles), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, nullptr, tout, out,
+                                                             nullptr, nullptr);
+    SYZ_LAUNCHED();
+  } else if (ntiles) {
+    ProfScope ps("setop_compact", s, 8 * total + 32 * ntiles);
+    k_so_compact<<<so_grid((ntiles + SO_BLOCK / 64 - 1) / (SO_BLOCK / 64)), SO_BLOCK, 0, s>>>(desc, tcnt, tout, tstart + npairs, gap, out);
     SYZ_LAUNCHED();
   }
   return total;
