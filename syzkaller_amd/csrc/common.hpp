@@ -123,6 +123,13 @@ struct Context {
 
 // The lane held by the calling thread (inside SYZ_API_BODY); lazily init(0); throws ENODEV.
 Context& ctx();
+// The lane's side stream and its fork / join events, created on first use.
+inline void ensure_side(Context& c) {
+  if (c.side) return;
+  SYZ_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+  SYZ_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+  SYZ_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
+}
 // RAII: hold a lane for the calling thread (nested API calls reuse it).
 struct LaneGuard {
   LaneGuard();

@@ -1550,11 +1550,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   // while the main stream runs the global levels
   // (the big groups' rounds on a stream of the greatest priority measured no faster beside the
   // transpose: r04_t1, 2.988 vs 2.983 ms)
-  if (!c.side) {
-    SYZ_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
-  }
+  ensure_side(c);
   const bool fork = P.npacks && P.nbig && !getenv("SYZGPU_GS_NOFORK");
   hipStream_t ss = fork ? c.side : s;  // the small groups' stream
   hipStream_t bs = s;                  // the big groups'

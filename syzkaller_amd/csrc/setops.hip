@@ -688,11 +688,10 @@ __global__ void k_store_len(const uint64_t* pos, uint64_t n, uint64_t* out_len, 
 }
 
 // ---- Canonicalize on a device-resident CSR (no host copy of the offsets) --------------------------
-// Covers are classed on the device by length (wave-aggregated appends to five lists): <= 512 and
-// <= 1024 PCs take one wave each, in registers (k_canon_wave below; SYZGPU_CANON_LDS=1: the workgroup
-// LDS sorters instead), <= 2048 a 512-thread workgroup with an LDS bitonic sort, <= 16384 (kCoverSize)
-// a 1024-thread one, <= 32768 (raw kcov output with repeats) the same with 128 KB of LDS; longer ones
-// go through the global network one by one.
+// Covers are classed on the device by length (k_canon_class): <= 1024 PCs take one wave each, in
+// registers (k_canon_net), <= 16384 (kCoverSize) a workgroup of register-sorted 1024-slot chunks merged
+// through LDS (k_canon_mrg), <= 32768 (raw kcov output with repeats) a 1024-thread LDS bitonic sort with
+// 128 KB of LDS (k_canon_cls); longer ones go through the global network one by one.
 // After the sort: unique with last = sentinel and the in-place store of the kept prefix
 // (cover.go:28-40), the new length to out_len.
 template <uint32_t PMAX, int BLOCK>
@@ -743,15 +742,60 @@ __global__ __launch_bounds__(BLOCK) void k_canon_cls(uint32_t* pcs, const uint64
   }
 }
 
-// One WAVE per cover of <= 64 R PCs, the cover in registers (element e = r * 64 + lane: coalesced loads
-// and stores): a bitonic network over the next power of two >= its length (>= 64), compare-exchanges
-// across registers in place and across lanes by xor shuffles, no LDS and no barriers; then unique
-// (cover.go:28-40: a PC is kept iff it differs from the one before, the first against the sentinel)
-// and the kept PCs stored in place at their ballot ranks. Four independent waves per workgroup walk
-// the class list.
+// One WAVE per cover of <= 64 R PCs, the cover in registers in BLOCKED order (lane l holds elements
+// l R .. l R + R - 1): a bitonic network over 64 R slots (the class's covers are longer than 32 R, so at
+// most half of it is padding), fully unrolled so every compare-exchange's direction is a compile-time
+// or per-lane constant. Distances below R are register pairs (min/max), the others lane exchanges by
+// DPP (xor 1, 2), ds_swizzle (xor 4..16) or v_permlane32_swap (xor 32): no LDS traffic, no barriers,
+// no exec-mask loops. Then unique (cover.go:28-40: a PC is kept iff it differs from the one before,
+// the first against the sentinel) and the kept PCs stored in place after a wave scan of the per-lane
+// counts. Four independent waves per workgroup walk the class list.
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x, int m) {
+  switch (m) {  // (a compile-time m after unrolling)
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (4 << 10));
+    case 8: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (8 << 10));
+    case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (16 << 10));
+    default: {  // 32: the halves swapped (whichever way the two results come back, their xor with x is it)
+      const auto h = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+      return h[0] ^ h[1] ^ x;
+    }
+  }
+}
+
 template <int R>
-__global__ __launch_bounds__(256) void k_canon_wave(uint32_t* pcs, const uint64_t* off, const uint32_t* list,
-                                                    const uint32_t* nlist_dev, uint64_t* out_len) {
+__device__ __forceinline__ void canon_net(uint32_t (&x)[R], unsigned lane) {
+#pragma unroll
+  for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < R) {  // register pairs (r, r | j); descending where element bit k is set
+        const bool lane_desc = k >= R && (((uint32_t)lane * R) & k) != 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          if (r & j) continue;
+          const uint32_t lo = min(x[r], x[r | j]), hi = max(x[r], x[r | j]);
+          const bool desc = k < R ? (r & k) != 0 : lane_desc;
+          x[r] = desc ? hi : lo;
+          x[r | j] = desc ? lo : hi;
+        }
+      } else {  // lane pairs (l, l ^ j / R)
+        const int m = j / R;
+        const bool keepmin = (((uint32_t)lane & m) == 0) == ((((uint32_t)lane * R) & k) == 0);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const uint32_t y = xor_lane(x[r], m);
+          x[r] = keepmin ? min(x[r], y) : max(x[r], y);
+        }
+      }
+    }
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void k_canon_net(uint32_t* pcs, const uint64_t* off, const uint32_t* list,
+                                                   const uint32_t* nlist_dev, uint64_t* out_len) {
   const uint32_t nlist = *nlist_dev;
   const unsigned lane = __lane_id();
   const uint32_t waves = gridDim.x * (blockDim.x >> 6);
@@ -759,77 +803,162 @@ __global__ __launch_bounds__(256) void k_canon_wave(uint32_t* pcs, const uint64_
     const uint32_t seg = list[li];
     const uint64_t beg = off[seg];
     const uint32_t n = (uint32_t)(off[seg + 1] - beg);
-    uint32_t P = 64;
-    while (P < n) P <<= 1;
-    const uint32_t nr = P >> 6;  // registers in use (uniform)
     uint32_t x[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
-      const uint32_t e = (uint32_t)r * 64 + lane;
+      const uint32_t e = lane * R + r;
       x[r] = e < n ? pcs[beg + e] : SENT;
     }
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        if (j >= 64) {  // partner register r ^ (j / 64), same lane
-          const uint32_t jr = j >> 6;
-#pragma unroll
-          for (int r = 0; r < R; r++) {
-            if ((uint32_t)r >= nr || (r & jr)) continue;
-            const int r2 = r ^ (int)jr;
-            const uint32_t a = x[r], b = x[r2];
-            const bool up = (((uint32_t)r * 64 + lane) & k) == 0;
-            x[r] = up ? min(a, b) : max(a, b);
-            x[r2] = up ? max(a, b) : min(a, b);
-          }
-        } else {  // partner lane lane ^ j, same register
-          const bool lower = (lane & j) == 0;
-#pragma unroll
-          for (int r = 0; r < R; r++) {
-            if ((uint32_t)r >= nr) continue;
-            const uint32_t y = (uint32_t)__shfl_xor((int)x[r], (int)j, 64);
-            const bool up = (((uint32_t)r * 64 + lane) & k) == 0;
-            x[r] = (lower == up) ? min(x[r], y) : max(x[r], y);
-          }
-        }
-      }
-    }
-    uint32_t kept = 0;
+    canon_net<R>(x, lane);
+    const uint32_t pl = (uint32_t)__builtin_amdgcn_mov_dpp((int)x[R - 1], 0x138, 0xF, 0xF, false);  // lane - 1's last
+    uint32_t km = 0;  // bit r: element lane R + r is kept
 #pragma unroll
     for (int r = 0; r < R; r++) {
-      if ((uint32_t)r >= nr) continue;
-      const uint32_t e = (uint32_t)r * 64 + lane;
-      uint32_t prev = (uint32_t)__shfl_up((int)x[r], 1, 64);
-      const uint32_t last = r ? (uint32_t)__builtin_amdgcn_readlane((int)x[r > 0 ? r - 1 : 0], 63) : SENT;
-      if (lane == 0) prev = last;
-      const bool keep = e < n && x[r] != prev;
-      const uint64_t b = __ballot(keep);
-      if (keep) pcs[beg + kept + (uint32_t)__popcll(b & lanemask_lt())] = x[r];
-      kept += (uint32_t)__popcll(b);
+      const uint32_t prev = r ? x[r > 0 ? r - 1 : 0] : (lane ? pl : SENT);
+      km |= (lane * R + r < n && x[r] != prev) ? 1u << r : 0u;
     }
-    if (lane == 0) out_len[seg] = kept;
+    const uint32_t cnt = (uint32_t)__popc(km);
+    const uint32_t incl = wave_incl_scan(cnt);
+    uint32_t* dst = pcs + beg + (incl - cnt);
+    uint32_t q = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (km >> r & 1u) dst[q] = x[r];
+      q += km >> r & 1u;
+    }
+    if (lane == 63) out_len[seg] = incl;
   }
 }
 
-// cls lists: [0] <= 512, [1] <= 1024, [2] <= 2048, [3] <= 16384, [4] <= 32768, [5] longer; cnt[6]
-constexpr int CANON_NCLS = 6;
-constexpr int CANON_LDS2 = 32768;  // a 1024-thread workgroup with 128 KB of LDS (raw kcov covers with repeats)
-__global__ void k_canon_class(const uint64_t* off, size_t ncov, uint32_t* lists, size_t cap, uint32_t* cnt) {
-  for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < ncov; i0 += (size_t)gridDim.x * blockDim.x) {
-    const size_t i = i0 + threadIdx.x;
-    int c = -1;
-    if (i < ncov) {
-      const uint64_t n = off[i + 1] - off[i];
-      c = n <= 512 ? 0 : n <= 1024 ? 1 : n <= 2048 ? 2 : n <= (uint64_t)CANON_LDS ? 3 : n <= (uint64_t)CANON_LDS2 ? 4 : 5;
-    }
+// One WORKGROUP of P / 1024 waves per cover of P / 2 < n <= P PCs (P = 2048 .. 16384): each wave
+// sorts a 1024-slot chunk in registers (canon_net<16>), then log2(P / 1024) rounds of pairwise merges
+// through LDS (ping-pong buffers; each thread finds its 16 outputs' start by a merge-path search and
+// merges them), the last round's outputs straight into unique and the in-place store. Against the
+// all-LDS bitonic network (log2(P) (log2(P) + 1) / 2 barrier-separated stages) this is 55 register
+// stages and 2-4 merge rounds.
+template <int P>
+__global__ __launch_bounds__(P / 16) void k_canon_mrg(uint32_t* pcs, const uint64_t* off, const uint32_t* list,
+                                                     const uint32_t* nlist_dev, uint64_t* out_len) {
+  constexpr int BLOCK = P / 16, WAVES = BLOCK / 64;
+  __shared__ __attribute__((aligned(16))) uint32_t buf[2][P];
+  __shared__ uint32_t wl[WAVES];
+  __shared__ uint32_t red[WAVES + 1];
+  const uint32_t nlist = *nlist_dev;
+  const unsigned lane = __lane_id();
+  const uint32_t wv = threadIdx.x >> 6, o = threadIdx.x * 16;
+  for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
+    const uint32_t seg = list[li];
+    const uint64_t beg = off[seg];
+    const uint32_t n = (uint32_t)(off[seg + 1] - beg);
+    uint32_t x[16];
 #pragma unroll
-    for (int k = 0; k < CANON_NCLS; k++) {
-      const uint64_t m = __ballot(c == k);
-      if (!m) continue;
-      const unsigned leader = (unsigned)__ffsll((unsigned long long)m) - 1;
-      uint32_t base = 0;
-      if (__lane_id() == leader) base = atomicAdd(&cnt[k], (uint32_t)__popcll(m));
-      base = (uint32_t)__shfl((int)base, (int)leader, 64);
-      if (c == k) lists[k * cap + base + (uint32_t)__popcll(m & lanemask_lt())] = (uint32_t)i;
+    for (int r = 0; r < 16; r++) {
+      const uint32_t e = wv * 1024 + lane * 16 + r;
+      x[r] = e < n ? pcs[beg + e] : SENT;
+    }
+    canon_net<16>(x, lane);
+    int cur = 0;
+#pragma unroll
+    for (int r = 0; r < 16; r += 4)
+      *reinterpret_cast<uint4*>(&buf[0][o + r]) = make_uint4(x[r], x[r + 1], x[r + 2], x[r + 3]);
+    __syncthreads();
+#pragma unroll
+    for (int sl = 1024; sl < P; sl <<= 1) {
+      const uint32_t* src = buf[cur];
+      const uint32_t pb = o & ~(2u * sl - 1), d = o - pb;
+      const uint32_t* A = src + pb;
+      const uint32_t* B = src + pb + sl;
+      uint32_t lo = d > (uint32_t)sl ? d - sl : 0u, hi = min(d, (uint32_t)sl);
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (A[mid] <= B[d - mid - 1])
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      uint32_t i = lo, j = d - lo;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const uint32_t a = A[min(i, (uint32_t)sl - 1)], b = B[min(j, (uint32_t)sl - 1)];
+        const bool ta = (j >= (uint32_t)sl) | ((i < (uint32_t)sl) & (a <= b));
+        x[r] = ta ? a : b;
+        i += ta ? 1u : 0u;
+        j += ta ? 0u : 1u;
+      }
+      if (2 * sl < P) {  // not the last round: to the other buffer
+        uint32_t* dst = buf[cur ^ 1];
+#pragma unroll
+        for (int r = 0; r < 16; r += 4)
+          *reinterpret_cast<uint4*>(&dst[o + r]) = make_uint4(x[r], x[r + 1], x[r + 2], x[r + 3]);
+        __syncthreads();
+        cur ^= 1;
+      }
+    }
+    // x = merged elements o .. o + 15; unique against the element before (a lane's / a wave's neighbour)
+    if (lane == 63) wl[wv] = x[15];
+    __syncthreads();
+    const uint32_t pl = (uint32_t)__builtin_amdgcn_mov_dpp((int)x[15], 0x138, 0xF, 0xF, false);
+    uint32_t km = 0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const uint32_t prev = r ? x[r > 0 ? r - 1 : 0] : lane ? pl : wv ? wl[wv > 0 ? wv - 1 : 0] : SENT;
+      km |= (o + r < n && x[r] != prev) ? 1u << r : 0u;
+    }
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<BLOCK>((uint32_t)__popc(km), red, &tot);
+    uint32_t* dstg = pcs + beg + pre;
+    uint32_t q = 0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      if (km >> r & 1u) dstg[q] = x[r];
+      q += km >> r & 1u;
+    }
+    if (threadIdx.x == 0) out_len[seg] = tot;
+    __syncthreads();  // wl / buffers reused by the next cover
+  }
+}
+
+// cls lists: [0..4] <= 64 << c (one wave each, k_canon_net<1 << c>), [5..8] <= 2048 << (c - 5)
+// (k_canon_mrg), [9] <= 32768 (k_canon_cls), [10] longer
+constexpr int CANON_NCLS = 11;
+constexpr int CANON_LDS2 = 32768;  // a 1024-thread workgroup with 128 KB of LDS (raw kcov covers with repeats)
+// A workgroup classes CANON_CHUNK covers: wave-aggregated LDS counts, one global reservation per class
+// per workgroup (global atomics per wave on nine counters were the kernel's bound), then the list entries.
+constexpr int CANON_CHUNK = 4096;
+__device__ __forceinline__ int canon_class_of(uint64_t n) {
+  return n <= 64 ? 0 : n <= 128 ? 1 : n <= 256 ? 2 : n <= 512 ? 3 : n <= 1024 ? 4 : n <= 2048 ? 5
+       : n <= 4096 ? 6 : n <= 8192 ? 7 : n <= 16384 ? 8 : n <= (uint64_t)CANON_LDS2 ? 9 : 10;
+}
+__global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t ncov, uint32_t* lists, size_t cap,
+                                                     uint32_t* cnt) {
+  __shared__ uint32_t lc[CANON_NCLS], lb[CANON_NCLS];
+  const unsigned lane = __lane_id();
+  for (size_t c0 = (size_t)blockIdx.x * CANON_CHUNK; c0 < ncov; c0 += (size_t)gridDim.x * CANON_CHUNK) {
+    if (threadIdx.x < CANON_NCLS) lc[threadIdx.x] = 0;
+    __syncthreads();
+    for (int pass = 0; pass < 2; pass++) {  // 0: counts; 1: entries at the reserved bases
+      for (size_t i0 = c0; i0 < min(c0 + CANON_CHUNK, ncov); i0 += blockDim.x) {
+        const size_t i = i0 + threadIdx.x;
+        const int c = i < ncov ? canon_class_of(off[i + 1] - off[i]) : -1;
+#pragma unroll
+        for (int k = 0; k < CANON_NCLS; k++) {
+          const uint64_t m = __ballot(c == k);
+          if (!m) continue;
+          const unsigned leader = (unsigned)__ffsll((unsigned long long)m) - 1;
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(&lc[k], (uint32_t)__popcll(m));
+          if (pass) {
+            base = (uint32_t)__shfl((int)base, (int)leader, 64);
+            if (c == k) lists[k * cap + lb[k] + base + (uint32_t)__popcll(m & lanemask_lt())] = (uint32_t)i;
+          }
+        }
+      }
+      __syncthreads();
+      if (pass == 0 && threadIdx.x < CANON_NCLS) {
+        lb[threadIdx.x] = lc[threadIdx.x] ? atomicAdd(&cnt[threadIdx.x], lc[threadIdx.x]) : 0u;
+        lc[threadIdx.x] = 0;
+      }
+      __syncthreads();
     }
   }
 }
@@ -841,39 +970,45 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", CANON_NCLS * ncov);
   uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", CANON_NCLS);
   SYZ_HIP(hipMemsetAsync(cnt, 0, CANON_NCLS * 4, s));
-  k_canon_class<<<grid_for(ncov, 256, 8192), 256, 0, s>>>(off, ncov, lists, ncov, cnt);
+  k_canon_class<<<(unsigned)std::min<size_t>((ncov + CANON_CHUNK - 1) / CANON_CHUNK, 2048), 256, 0, s>>>(off, ncov, lists, ncov, cnt);
   SYZ_LAUNCHED();
   if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
   const unsigned ncu = (unsigned)std::max(1, c.ncu);
-  static const bool lds = getenv("SYZGPU_CANON_LDS") != nullptr;  // A/B: the workgroup LDS sorters
-  {
-    ProfScope ps("canon_small", s, 0);
-    if (lds) {
-      k_canon_cls<512, 256><<<ncu * 8, 256, 0, s>>>(pcs, off, lists, cnt, out_len);
-      SYZ_LAUNCHED();
-      k_canon_cls<2048, 512><<<ncu * 4, 512, 0, s>>>(pcs, off, lists + ncov, cnt + 1, out_len);
-      SYZ_LAUNCHED();
-    } else {
-      k_canon_wave<8><<<ncu * 8, 256, 0, s>>>(pcs, off, lists, cnt, out_len);
-      SYZ_LAUNCHED();
-      k_canon_wave<16><<<ncu * 6, 256, 0, s>>>(pcs, off, lists + ncov, cnt + 1, out_len);
-      SYZ_LAUNCHED();
-    }
-  }
-  k_canon_cls<2048, 512><<<ncu * 4, 512, 0, s>>>(pcs, off, lists + 2 * ncov, cnt + 2, out_len);
+  // the long classes (few covers, long per-cover chains: the 32768 class is one workgroup's bitonic
+  // network) on the side stream, started first, beside the short classes' persistent walks
+  ensure_side(c);
+  SYZ_HIP(hipEventRecord(c.ev_fork, s));
+  SYZ_HIP(hipStreamWaitEvent(c.side, c.ev_fork, 0));
+  k_canon_cls<CANON_LDS2, CANON_BLOCK><<<ncu, CANON_BLOCK, 0, c.side>>>(pcs, off, lists + 9 * ncov, cnt + 9, out_len);
   SYZ_LAUNCHED();
-  k_canon_cls<CANON_LDS, CANON_BLOCK><<<ncu * 2, CANON_BLOCK, 0, s>>>(pcs, off, lists + 3 * ncov, cnt + 3, out_len);
+  k_canon_mrg<16384><<<ncu, 1024, 0, c.side>>>(pcs, off, lists + 8 * ncov, cnt + 8, out_len);
   SYZ_LAUNCHED();
-  k_canon_cls<CANON_LDS2, CANON_BLOCK><<<ncu, CANON_BLOCK, 0, s>>>(pcs, off, lists + 4 * ncov, cnt + 4, out_len);
+  k_canon_mrg<8192><<<ncu * 2, 512, 0, c.side>>>(pcs, off, lists + 7 * ncov, cnt + 7, out_len);
   SYZ_LAUNCHED();
+  SYZ_HIP(hipEventRecord(c.ev_join, c.side));
+  k_canon_mrg<4096><<<ncu * 4, 256, 0, s>>>(pcs, off, lists + 6 * ncov, cnt + 6, out_len);
+  SYZ_LAUNCHED();
+  k_canon_mrg<2048><<<ncu * 8, 128, 0, s>>>(pcs, off, lists + 5 * ncov, cnt + 5, out_len);
+  SYZ_LAUNCHED();
+  k_canon_net<16><<<ncu * 8, 256, 0, s>>>(pcs, off, lists + 4 * ncov, cnt + 4, out_len);
+  SYZ_LAUNCHED();
+  k_canon_net<8><<<ncu * 8, 256, 0, s>>>(pcs, off, lists + 3 * ncov, cnt + 3, out_len);
+  SYZ_LAUNCHED();
+  k_canon_net<4><<<ncu * 8, 256, 0, s>>>(pcs, off, lists + 2 * ncov, cnt + 2, out_len);
+  SYZ_LAUNCHED();
+  k_canon_net<2><<<ncu * 8, 256, 0, s>>>(pcs, off, lists + ncov, cnt + 1, out_len);
+  SYZ_LAUNCHED();
+  k_canon_net<1><<<ncu * 8, 256, 0, s>>>(pcs, off, lists, cnt, out_len);
+  SYZ_LAUNCHED();
+  SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
   // longer covers: their list back to the host, then the global network one by one
   uint32_t* h = c.pinned.get<uint32_t>(CANON_NCLS);
   SYZ_HIP(hipMemcpyAsync(h, cnt, CANON_NCLS * 4, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
-  const uint32_t nbig = h[5];
+  const uint32_t nbig = h[CANON_NCLS - 1];
   if (!nbig) return;
   std::vector<uint32_t> big(nbig);
-  SYZ_HIP(hipMemcpyAsync(big.data(), lists + 5 * ncov, nbig * 4, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(big.data(), lists + (CANON_NCLS - 1) * ncov, nbig * 4, hipMemcpyDeviceToHost, s));
   std::vector<uint64_t> hoff(2);
   for (uint32_t seg : big) {
     SYZ_HIP(hipMemcpyAsync(hoff.data(), off + seg, 16, hipMemcpyDeviceToHost, s));

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 LEGS="--steps 3 --warmup 1 --cpu-baseline 0 --store 0 --text 0 --novelty 0 --hub 0 --analytics 0 --append 0 --cooccurrence 0"
-for e in "X=0" "SYZGPU_SO_TWOPASS=1"; do
+for e in "X=0"; do
   env $e timeout -k 10 300 python3 bench.py $LEGS > $OUT/bench_$e.json 2> $OUT/bench_$e.err || exit 1
   python3 -c "
 import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
