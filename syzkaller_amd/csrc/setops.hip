@@ -387,8 +387,8 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
 }
 
 // SO_GAP's gapped image closed up: tile t's tcnt[t] outputs from gap[a0 + b0..] to out[tout[t]..]. Each
-// WAVE walks its own tiles (no LDS, no barrier: more tiles in flight per CU for a walk that is all latency),
-// pipelined like k_so_tile: tile k+1's words and tile k+2's offsets are in flight while tile k is stored.
+// WAVE walks its own tiles (no LDS, no barrier: more tiles in flight per CU for a walk that is all
+// latency), two tiles deep (see step below).
 constexpr int SC_VT = SO_T / 64;
 __global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restrict__ desc,
                                                          const uint32_t* __restrict__ tcnt,
@@ -423,38 +423,41 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restric
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(gap + (ok ? src_of(w) : 0)), 0, n * 4, SO_RSRC_FLAGS);
 #pragma unroll
     for (int r = 0; r < SC_VT; r++)
-      v[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, (lane + r * 64) * 4, 0, 0);
+      if (r * 64 < (int)n) v[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, (lane + r * 64) * 4, 0, 0);
   };
-  uint32_t mw = meta_load(tile);
-  uint32_t n = field(mw, 4);
-  uint64_t dst = dst_of(mw);
-  fetch(mw, true, cur);
-  mw = meta_load(tile + stride);
+  // two tiles' words and two more tiles' offsets in flight per wave: tile k is stored from D[k % 2] while
+  // tile k+2's words load into it (its offsets were read two steps ago) and tile k+4's offsets into M[k % 2]
+  uint32_t D0[SC_VT], D1[SC_VT];
+  uint32_t m = meta_load(tile);
+  uint32_t n0 = field(m, 4);
+  uint64_t d0 = dst_of(m);
+  fetch(m, true, D0);
+  const bool ok1 = tile + stride < ntiles;
+  m = meta_load(tile + stride);
+  uint32_t n1 = ok1 ? field(m, 4) : 0;
+  uint64_t d1 = ok1 ? dst_of(m) : 0;
+  fetch(m, ok1, D1);
+  uint32_t M0 = meta_load(tile + 2 * stride), M1 = meta_load(tile + 3 * stride);
   {
     const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, 0, SO_RSRC_FLAGS);  // (see k_so_tile)
 #pragma unroll
     for (int r = 0; r < SC_VT; r++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, rz, (lane + r * 64) * 4, 0, 0);
   }
-  // one tile stored from cv while the next one loads into nv (two register sets, alternated, so the
-  // loads in flight are never copied, which would wait for them)
-  auto step = [&](uint32_t* cv, uint32_t* nv) {
-    const uint64_t next = tile + stride;
-    const bool ok = next < ntiles;
-    const uint32_t cn = n;
-    const uint64_t cdst = dst;
-    n = ok ? field(mw, 4) : 0;
-    dst = ok ? dst_of(mw) : 0;
-    fetch(mw, ok, nv);
-    mw = meta_load(next + stride);
-    const auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(out + cdst), 0, cn * 4, SO_RSRC_FLAGS);
+  auto step = [&](uint32_t* D, uint32_t& M, uint32_t& n, uint64_t& d) {
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(out + d), 0, n * 4, SO_RSRC_FLAGS);
 #pragma unroll
-    for (int r = 0; r < SC_VT; r++)
-      __builtin_amdgcn_raw_buffer_store_b32(cv[r], rd, (lane + r * 64) * 4, 0, 0);
-    tile = next;
-    return ok;
+    for (int r = 0; r < SC_VT; r++)  // (wave-uniform: a tile's empty slots issue nothing)
+      if (r * 64 < (int)n) __builtin_amdgcn_raw_buffer_store_b32(D[r], rd, (lane + r * 64) * 4, 0, 0);
+    const bool ok = tile + 2 * stride < ntiles;
+    n = ok ? field(M, 4) : 0;
+    d = ok ? dst_of(M) : 0;
+    fetch(M, ok, D);
+    M = meta_load(tile + 4 * stride);
+    tile += stride;
+    return tile < ntiles;
   };
-  while (step(cur, nxt) && step(nxt, cur)) {
+  while (step(D0, M0, n0, d0) && step(D1, M1, n1, d1)) {
   }
 }
 
