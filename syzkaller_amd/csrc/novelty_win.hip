@@ -172,7 +172,10 @@ __global__ __launch_bounds__(NwCfg<SB>::BLOCK) void k_nw_min(
   if (!(dbg & 1))
     for_slab_window<SYZ_NW_U, true>(it, sg, gslab, gebase, D, slabs, elems, nullptr, bm, red64,
                                     [&](uint32_t o, uint32_t R) {
-                                      if (R != RANK_NONE && atomicMin(&tab[nw_index<SB>(o)], R) == RANK_NONE)
+                                      // (a plain read first: an input that loses to the rank there
+                                      // issues no atomic; a slot below NONE is already present)
+                                      uint32_t* t = &tab[nw_index<SB>(o)];
+                                      if (R != RANK_NONE && *t > R && atomicMin(t, R) == RANK_NONE)
                                         atomicOr(&pres[o >> 5], 1u << (o & 31));
                                     });
   __syncthreads();
@@ -352,7 +355,7 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
           if (k == 0xFFFFFFFFu) k = o;
         }
         if (k == o) {
-          atomicMin(&vals[h], R);
+          if (vals[h] > R) atomicMin(&vals[h], R);
           return;
         }
         h = (h + 1) & (HS - 1);

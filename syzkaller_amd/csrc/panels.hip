@@ -190,10 +190,22 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 4))) vo
     if (acc == 0x9E3779B9u) sel8[0] = 1;
   } else if (dbg & 8) {  // timing only: no rank gathers
     for_region<SYZ_RG_U, true>(it, pg, gstart, rstart, rtot, elems, nullptr,
-                               [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
+                               [&](uint32_t o, uint32_t R) {
+                                      // a plain read first: most elements of a PC held by many inputs lose
+                                      // to the rank already there, and same-address reads broadcast where
+                                      // atomics serialize
+                                      uint32_t* t = &tab[tab_index(o)];
+                                      if (*t > R) atomicMin(t, R);
+                                    });
   } else {
     for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, rtot, elems, rank_of_member,
-                                [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
+                                [&](uint32_t o, uint32_t R) {
+                                      // a plain read first: most elements of a PC held by many inputs lose
+                                      // to the rank already there, and same-address reads broadcast where
+                                      // atomics serialize
+                                      uint32_t* t = &tab[tab_index(o)];
+                                      if (*t > R) atomicMin(t, R);
+                                    });
   }
   __syncthreads();
   if (dbg & 2) return;
@@ -291,7 +303,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                                                if (k == 0xFFFFFFFFu) k = o;
                                              }
                                              if (k == o) {
-                                               atomicMin(&vals[h], Rk);
+                                               if (vals[h] > Rk) atomicMin(&vals[h], Rk);
                                                return;
                                              }
                                              h = (h + 1) & (HS - 1);
@@ -351,7 +363,13 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
   }
   __syncthreads();
   for_slab_window<SYZ_SL_MU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
-                                    [&](uint32_t o, uint32_t R) { atomicMin(&tab[tab_index(o)], R); });
+                                    [&](uint32_t o, uint32_t R) {
+                                      // a plain read first: most elements of a PC held by many inputs lose
+                                      // to the rank already there, and same-address reads broadcast where
+                                      // atomics serialize
+                                      uint32_t* t = &tab[tab_index(o)];
+                                      if (*t > R) atomicMin(t, R);
+                                    });
   __syncthreads();
   const uint64_t gb = gstart[it.g];
   emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, L.wsc, sel8);
@@ -408,7 +426,7 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
                                               if (k == 0xFFFFFFFFu) k = o;
                                             }
                                             if (k == o) {
-                                              atomicMin(&vals[h], Rk);
+                                              if (vals[h] > Rk) atomicMin(&vals[h], Rk);
                                               return;
                                             }
                                             h = (h + 1) & (HS - 1);
