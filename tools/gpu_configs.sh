@@ -6,7 +6,7 @@ TAG=${1:-cfg}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-LEGS="--text 0 --novelty 0 --hub 0 --analytics 0 --append 0 --store 1 --cooccurrence 0 --setops 0"
+LEGS="--text 0 --novelty 0 --hub 0 --analytics 0 --append 0 --store 1 --cooccurrence 0 --setops 0 --canonicalize 0"
 run() {  # name, args...
   n=$1; shift
   timeout -k 10 600 python -u bench.py $LEGS "$@" > $OUT/$n.log 2>&1 || { echo "$n failed"; tail -5 $OUT/$n.log; exit 1; }
