@@ -11,7 +11,7 @@
 // rank is its position in that list, so the table is the group's smallest rank.
 //
 //   G  group partition (stable) + members + lengths (a trailing 0xFFFFFFFF dropped) + the PC span
-//   P  k_part3<NOV>: the members' PCs transposed into 2^DB-address windows (one HBM read per PC), every
+//   P  k_slab<NOV> (slab_dev.hpp): the members' PCs transposed into 2^DB-address windows (one HBM read per PC), every
 //      list checked strictly increasing on the way
 //   M  k_nw_min: a workgroup per (call, window): a direct min-rank table in LDS (and a presence bitmap
 //      the element that finds an entry empty sets), the LDS updates of 16 runs issued before one

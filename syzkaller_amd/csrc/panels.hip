@@ -1577,17 +1577,6 @@ int syzgpu_mz_fetch(syzgpu_mz* job, int64_t* out_idx, uint64_t* group_out_off) {
   })
 }
 
-#ifdef SYZ_STAMPS
-// diagnostic build only: the phase stamps of the last k_part4 (which = 0) / k_pmin_direct (1) launch
-int syzgpu_debug_stamps(int which, uint64_t* out, size_t cap) {
-  SYZ_API_BODY({
-    const size_t n = std::min<size_t>(cap, (size_t)STAMP_WG * 8);
-    SYZ_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), n * 8, (size_t)which * STAMP_WG * 8 * 8,
-                                hipMemcpyDeviceToHost));
-  })
-}
-#endif
-
 int syzgpu_mz_info(syzgpu_mz* job, uint64_t* info, size_t cap) {
   SYZ_API_BODY({
     if (!job || !info) fail(SYZGPU_EINVAL, "null pointer");

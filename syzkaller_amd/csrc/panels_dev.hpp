@@ -1,6 +1,7 @@
 // Device code shared by the raw-cover pipelines: minimizeCorpus (panels.hip) and the new-coverage
-// check on windows (novelty_win.hip). Chunks of <= PCAP PCs of <= 64 members of one call group are
-// transposed into PC windows (P, k_part3) and walked per (call, window) (M, for_window_elems).
+// check on windows (novelty_win.hip): window planning constants, the region form of the transpose
+// (k_region, the A/B alternative to slab_dev.hpp's k_slab) with its M walk (for_region), the packed
+// walk's scan and the min-table helpers. The default slab pipeline is slab_dev.hpp.
 #pragma once
 #include "panels.hpp"
 
@@ -58,18 +59,6 @@ constexpr uint32_t HTARGET = SYZ_HTARGET;  // PCs per window a sparse call's win
 constexpr uint32_t PHTARGET = 2 * HTARGET;  // the same for packed windows
 
 
-// Diagnostic build only (-DSYZ_STAMPS, tools/build_variant.sh): per-workgroup phase timestamps of the
-// transpose and the direct walk (thread 0, s_memtime), read back by syzgpu_debug_stamps.
-#ifdef SYZ_STAMPS
-constexpr uint32_t STAMP_WG = 1u << 15;
-static __device__ unsigned long long g_stamp[2][STAMP_WG][8];
-#define SYZ_STAMP(k, slot)                                                                  \
-  do {                                                                                      \
-    if (threadIdx.x == 0 && blockIdx.x < STAMP_WG) g_stamp[k][blockIdx.x][slot] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define SYZ_STAMP(k, slot)
-#endif
 
 // elements the element buffer needs for `pcs` PCs in at most `chunks` chunks (k_chunks' alignment)
 inline uint64_t elem_bound(uint64_t pcs, uint64_t chunks) { return pcs + 4 * chunks + 8; }
@@ -124,13 +113,9 @@ static __global__ __launch_bounds__(1024) void k_gchunk(const uint32_t* gblock, 
 
 constexpr uint32_t TMAX = PCAP / 64 + MEMB;  // tiles per chunk
 
-// ---- P, register form (k_part3): each PC read from HBM once ----------------------------------------
-// One workgroup per chunk, as k_part, but every wave loads all of its tiles' PCs into registers up
-// front (all of them in flight per lane), so the second pass needs no second read; and the LDS
-// atomics of both passes are taken once per RUN: the 64 lanes of a tile hold consecutive PCs of one
-// (sorted) cover, so neighbouring lanes mostly share a window; a run's head lane adds the run's
-// length to the window's count (pass 1) or reserves its slots (pass 2) and the run's lanes write
-// consecutive LDS words. 74 KB of LDS: two workgroups per CU.
+// ---- runs of equal windows in a tile (the region form's passes) ------------------------------------
+// The 64 lanes of a tile hold consecutive PCs of one (sorted) cover, so neighbouring lanes mostly share
+// a window; a run's head lane can take the run's slots with one LDS atomic.
 struct TileRun {
   uint32_t start, len;
   bool head;
@@ -162,365 +147,6 @@ struct NovSrc {
   uint32_t n1 = 0xFFFFFFFFu;
 };
 
-// BLOCK threads per chunk; each wave holds TPW tiles of PCs in registers. 512 threads x 40 tiles:
-// two workgroups (74 KB of LDS each) share a CU, so one's dependent metadata loads overlap the
-// other's passes.
-template <int BLOCK, int TPW, bool NOV = false>
-__global__ __launch_bounds__(BLOCK) void k_part3(
-    const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
-    const uint64_t* __restrict__ mpos, const uint32_t* __restrict__ sbeg, const PChunk* chunks,
-    const uint64_t* nchunks_dev, const PGroup* pg, const uint64_t* gchunk, const uint64_t* gdesc, uint32_t lo,
-    uint32_t* __restrict__ elems, uint16_t* __restrict__ desc, int* err, NovSrc ns = NovSrc{}) {
-  constexpr int WAVES = BLOCK / 64;
-  static_assert(TMAX <= (uint32_t)(TPW * WAVES), "k_part3: tiles per wave");
-  __shared__ uint32_t obuf[PCAP];
-  __shared__ uint32_t hist[WMAX + 1];
-  __shared__ uint32_t tpre[MEMB + 1];
-  __shared__ uint32_t mlo[MEMB], mhi[MEMB];
-  __shared__ uint64_t mraw[MEMB];  // byte address of the member's PC at block coordinate 0
-  __shared__ uint32_t red[WAVES + 1];
-  __shared__ uint4 tinfo[TMAX];
-  __shared__ uint32_t tlast[NOV ? TMAX : 1];  // NOV: the last PC of every tile
-  __shared__ uint8_t mtab[NOV ? MEMB : 1];    // NOV: the member is a table
-  const uint64_t c = blockIdx.x;
-  if (c >= *nchunks_dev) return;
-  const int wv = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  const PChunk ch = chunks[c];
-  const PGroup gp = pg[ch.g];
-  const uint32_t S = gp.S, W = gp.W;
-  const uint32_t cb = ch.sub, ce = ch.sub + ch.len;
-  int bad = 0;  // NOV: err bits of the lists this thread saw out of order
-  if (threadIdx.x < 64) {
-    const uint32_t m = threadIdx.x;
-    uint32_t nt = 0;
-    if (m < ch.nmem) {
-      const uint64_t p0 = mpos[ch.mb], a = mpos[ch.mb + m] - p0, b = mpos[ch.mb + m + 1] - p0;
-      const uint32_t x = (uint32_t)max<uint64_t>(a, cb), y = (uint32_t)min<uint64_t>(b, ce);
-      mlo[m] = x;
-      mhi[m] = y;
-      const uint32_t e = members[ch.mb + m];
-      const uint32_t* src;
-      if constexpr (NOV) {
-        src = e >= ns.n1 ? ns.mc + ns.mc_off[e - ns.n1] : pcs + off[e];
-        mtab[m] = e >= ns.n1;
-      } else
-        src = pcs + off[e] + (sbeg ? sbeg[ch.mb + m] : 0u);
-      mraw[m] = (uint64_t)(uintptr_t)src - a * 4;
-      nt = y > x ? (y - x + 63) / 64 : 0;
-      if constexpr (NOV) {
-        // the member began in an earlier chunk: its first PC here against the one before
-        if (x > a && y > x && src[x - a - 1] >= src[x - a]) bad |= e >= ns.n1 ? 1 : 4;
-      }
-    }
-    const uint32_t inc = wave_incl_scan<uint32_t>(nt);
-    tpre[m] = inc - nt;
-    if (m == 63) tpre[64] = inc;
-  }
-  for (uint32_t i = threadIdx.x; i <= W; i += BLOCK) hist[i] = 0;
-  __syncthreads();
-  const uint32_t ntiles = tpre[64];
-  for (uint32_t t = threadIdx.x; t < ntiles; t += BLOCK) {
-    uint32_t lo_m = 0, hi_m = ch.nmem;  // largest m < nmem with tpre[m] <= t
-    while (hi_m - lo_m > 1) {
-      const uint32_t mid = (lo_m + hi_m) >> 1;
-      if (tpre[mid] <= t)
-        lo_m = mid;
-      else
-        hi_m = mid;
-    }
-    const uint32_t m = lo_m;
-    const uint32_t q0 = mlo[m] + (t - tpre[m]) * 64;
-    const uint64_t base = mraw[m] + (uint64_t)q0 * 4;
-    uint32_t fl = 0;
-    if constexpr (NOV)  // bit 0: a table; bit 1: the member's previous tile is tile t - 1 of this chunk
-      fl = (mtab[m] ? 1u : 0u) | (t > tpre[m] ? 2u : 0u);
-    tinfo[t] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), min(64u, mhi[m] - q0) | (m << 8), fl);
-  }
-  __syncthreads();
-  // every tile of this wave: t = wv + WAVES k; its PCs into registers, all loads in flight
-  uint32_t v[TPW];
-#pragma unroll
-  for (int k = 0; k < TPW; k++) {
-    const uint32_t t = wv + WAVES * k;
-    v[k] = 0;
-    if (t < ntiles) {
-      const uint4 ti = tinfo[t];
-      if (lane < (ti.z & 0xFFu))
-        v[k] = reinterpret_cast<const uint32_t*>((uintptr_t)((((uint64_t)ti.y << 32) | ti.x) + 4ull * lane))[0];
-    }
-  }
-  // pass 1: window histogram, one LDS atomic per run
-#pragma unroll
-  for (int k = 0; k < TPW; k++) {
-    const uint32_t t = wv + WAVES * k;
-    if (t >= ntiles) break;  // wave-uniform
-    const uint32_t cnt = tinfo[t].z & 0xFFu;
-    const uint32_t w = (v[k] - lo) >> S;
-    const bool in = lane < cnt;
-    if constexpr (NOV) {
-      const uint32_t pv = __shfl_up(v[k], 1, 64);
-      const uint32_t eb = (tinfo[t].w & 1u) ? 1u : 4u;
-      if (in && (w >= W || (lane > 0 && pv >= v[k]))) bad |= eb;  // out of order (or outside every window)
-      if (lane + 1 == cnt) tlast[t] = v[k];
-    } else {
-      if (in && w >= W) atomicOr(err, 1);  // outside [lo, hi]: an unsorted cover; redone on exact bounds
-    }
-    const TileRun r = tile_run(w, in && w < W, lane);
-    if (r.head) atomicAdd(&hist[w], r.len);
-  }
-  __syncthreads();
-  // window starts (exclusive scan) -> desc row and cursors
-  uint16_t* drow = desc + gdesc[ch.g] + (c - gchunk[ch.g]) * (uint64_t)(W + 1);
-  {
-    uint32_t run = 0;
-    for (uint32_t b0 = 0; b0 <= W; b0 += BLOCK) {
-      const uint32_t i = b0 + threadIdx.x;
-      const uint32_t x = i < W ? hist[i] : 0;
-      uint32_t tot;
-      const uint32_t pre = block_excl_scan<BLOCK>(x, red, &tot) + run;
-      if (i <= W) {
-        drow[i] = (uint16_t)pre;
-        hist[i] = pre;
-      }
-      run += tot;
-    }
-  }
-  __syncthreads();
-  // pass 2: element = offset in window | member tag, window-major into obuf, a run's slots reserved
-  // by its head
-  const uint32_t omask = (1u << S) - 1;
-#pragma unroll
-  for (int k = 0; k < TPW; k++) {
-    const uint32_t t = wv + WAVES * k;
-    if (t >= ntiles) break;
-    const uint32_t z = tinfo[t].z;
-    const uint32_t d = v[k] - lo, w = d >> S;
-    const bool in = lane < (z & 0xFFu) && w < W;
-    if constexpr (NOV) {
-      const uint32_t f = tinfo[t].w;
-      if (lane == 0 && (f & 2u) && tlast[t - 1] >= v[k]) bad |= (f & 1u) ? 1 : 4;
-    }
-    const TileRun r = tile_run(w, in, lane);
-    uint32_t base = r.head ? atomicAdd(&hist[w], r.len) : 0u;
-    base = (uint32_t)__shfl((int)base, (int)r.start, 64);
-    if (in) obuf[base + (lane - r.start)] = (d & omask) | ((z >> 8) << S);
-  }
-  if constexpr (NOV) {
-    const uint64_t bm = __ballot(bad != 0);
-    if (bm) {
-      int all = bad;
-#pragma unroll
-      for (int dd = 32; dd >= 1; dd >>= 1) all |= __shfl_xor(all, dd, 64);
-      if (lane == (unsigned)(__ffsll((unsigned long long)bm) - 1)) atomicOr(err, all);
-    }
-  }
-  __syncthreads();
-  uint32_t* dst = elems + ch.elem;
-  for (uint32_t i = threadIdx.x; i < ch.len; i += BLOCK) dst[i] = obuf[i];
-}
-
-// ---- P, lean form (k_part4) ---------------------------------------------------------------------
-// The transpose of k_part3 with its per-tile instruction count cut: k_part3 issued ~89 VALU per 64-PC
-// tile (profiles/r03_pmin_base: 590M VALU for 6.6M tiles, ~1 ms of issue on 256 CUs for a 1.4 ms
-// kernel) on run detection, 64-bit tile addresses and per-lane tile-table loads. Here:
-//   * a tile's count, member tag and address are wave-uniform (readfirstlane into SGPRs), so its load
-//     is a saddr global load and its bookkeeping is scalar;
-//   * one LDS atomic per PC instead of run detection: covers are sparse against the windows (a
-//     256-PC median cover over 256 windows), so a tile's PCs rarely share a window and the atomics
-//     rarely collide; when they do (dense covers) the LDS serializes only those lanes;
-//   * the chunk leaves as aligned 16-byte vector stores (k_chunks aligns chunk starts).
-// Same inputs and outputs as k_part3 (elements in a window's run are in atomic order, which neither
-// consumer depends on).
-template <int BLOCK, int TPW, bool NOV = false>
-__global__ __launch_bounds__(BLOCK) void k_part4(
-    const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
-    const uint64_t* __restrict__ mpos, const uint32_t* __restrict__ sbeg, const PChunk* chunks,
-    const uint64_t* nchunks_dev, const PGroup* pg, const uint64_t* gchunk, const uint64_t* gdesc, uint32_t lo,
-    uint32_t* __restrict__ elems, uint16_t* __restrict__ desc, int* err, NovSrc ns = NovSrc{}) {
-  constexpr int WAVES = BLOCK / 64;
-  static_assert(TMAX <= (uint32_t)(TPW * WAVES), "k_part4: tiles per wave");
-  __shared__ __align__(16) uint32_t obuf[PCAP + 64];  // + a slot per lane for lanes with no element
-  __shared__ uint32_t hist[WMAX + 1 + 64];             // + a counter per lane for them
-  __shared__ uint32_t tpre[MEMB + 1];
-  __shared__ uint32_t mlo[MEMB], mhi[MEMB];
-  __shared__ uint64_t mraw[MEMB];
-  __shared__ uint32_t red[WAVES + 1];
-  __shared__ uint4 tinfo[TMAX];
-  __shared__ uint32_t tlast[NOV ? TMAX : 1];
-  __shared__ uint8_t mtab[NOV ? MEMB : 1];
-  const uint64_t c = blockIdx.x;
-  if (c >= *nchunks_dev) return;
-  const int wv = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  SYZ_STAMP(0, 0);
-  const PChunk ch = chunks[c];
-  const PGroup gp = pg[ch.g];
-  const uint32_t S = gp.S, W = gp.W;
-  const uint32_t cb = ch.sub, ce = ch.sub + ch.len;
-  int bad = 0;  // err bits this thread found (1: outside the windows / a table out of order, 4: a cover)
-  if (threadIdx.x < 64) {
-    const uint32_t m = threadIdx.x;
-    uint32_t nt = 0;
-    if (m < ch.nmem) {
-      const uint64_t p0 = mpos[ch.mb], a = mpos[ch.mb + m] - p0, b = mpos[ch.mb + m + 1] - p0;
-      const uint32_t x = (uint32_t)max<uint64_t>(a, cb), y = (uint32_t)min<uint64_t>(b, ce);
-      mlo[m] = x;
-      mhi[m] = y;
-      const uint32_t e = members[ch.mb + m];
-      const uint32_t* src;
-      if constexpr (NOV) {
-        src = e >= ns.n1 ? ns.mc + ns.mc_off[e - ns.n1] : pcs + off[e];
-        mtab[m] = e >= ns.n1;
-      } else
-        src = pcs + off[e] + (sbeg ? sbeg[ch.mb + m] : 0u);
-      mraw[m] = (uint64_t)(uintptr_t)src - a * 4;
-      nt = y > x ? (y - x + 63) / 64 : 0;
-      if constexpr (NOV) {
-        if (x > a && y > x && src[x - a - 1] >= src[x - a]) bad |= e >= ns.n1 ? 1 : 4;
-      }
-    }
-    const uint32_t inc = wave_incl_scan<uint32_t>(nt);
-    tpre[m] = inc - nt;
-    if (m == 63) tpre[64] = inc;
-  }
-  for (uint32_t i = threadIdx.x; i <= W; i += BLOCK) hist[i] = 0;
-  __syncthreads();
-  const uint32_t ntiles = tpre[64];
-  for (uint32_t t = threadIdx.x; t < ntiles; t += BLOCK) {
-    uint32_t lo_m = 0, hi_m = ch.nmem;  // largest m < nmem with tpre[m] <= t
-    while (hi_m - lo_m > 1) {
-      const uint32_t mid = (lo_m + hi_m) >> 1;
-      if (tpre[mid] <= t)
-        lo_m = mid;
-      else
-        hi_m = mid;
-    }
-    const uint32_t m = lo_m;
-    const uint32_t q0 = mlo[m] + (t - tpre[m]) * 64;
-    const uint64_t base = mraw[m] + (uint64_t)q0 * 4;
-    uint32_t fl = 0;
-    if constexpr (NOV) fl = (mtab[m] ? 1u : 0u) | (t > tpre[m] ? 2u : 0u);
-    tinfo[t] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), min(64u, mhi[m] - q0) | (m << 8), fl);
-  }
-  __syncthreads();
-  SYZ_STAMP(0, 1);
-  // this wave's tiles t = wv + WAVES k: PCs into registers, all loads in flight. Straight-line code
-  // (a lane past its tile re-reads the tile's last PC, a tile past the chunk re-reads the last tile
-  // with count 0), so the compiler counts its waits instead of draining at every branch join; a
-  // tile's count and member tag stay in SGPRs.
-  const uint32_t DUMMY = WMAX + 1 + lane;  // the histogram slot of a lane with no element (one per lane:
-                                          // a shared one serializes every idle lane's atomic)
-  static_assert(TPW <= 64, "a tile's count and tag per lane of one register");
-  // lane k of czv: count | tag << 8 of this wave's tile k (count 0 past the chunk); v_readlane per use
-  uint32_t czv = 0;
-  {
-    const uint32_t t = wv + WAVES * lane;
-    const uint32_t z = tinfo[min(t, ntiles - 1)].z;
-    czv = lane < (unsigned)TPW ? (t < ntiles ? z : (z & ~0xFFu)) : 0u;
-  }
-  auto cz = [&](int k) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)czv, k); };
-  uint32_t v[TPW];
-#pragma unroll
-  for (int k = 0; k < TPW; k++) {
-    const uint32_t t = wv + WAVES * k;
-    const uint4 ti = tinfo[min(t, ntiles - 1)];
-    const uint32_t z = (uint32_t)__builtin_amdgcn_readfirstlane((int)ti.z);
-    const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)ti.y) << 32) |
-                          (uint32_t)__builtin_amdgcn_readfirstlane((int)ti.x);
-    v[k] = reinterpret_cast<const uint32_t*>((uintptr_t)base)[min(lane, (z & 0xFFu) - 1)];
-    // tile-table reads in groups of 8: the scheduler would otherwise hoist all of them (and their
-    // addresses) ahead of the first load
-    if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-  }
-  // pass 1: window histogram, one LDS atomic per PC
-#pragma unroll
-  for (int k = 0; k < TPW; k++) {
-    const uint32_t t = wv + WAVES * k;
-    const uint32_t w = (v[k] - lo) >> S;
-    const bool in = lane < (cz(k) & 0xFFu);
-    if constexpr (NOV) {
-      if (t < ntiles) {
-        const uint32_t pv = __shfl_up(v[k], 1, 64);
-        const uint32_t eb = (tinfo[t].w & 1u) ? 1u : 4u;
-        if (in && (w >= W || (lane > 0 && pv >= v[k]))) bad |= eb;
-        if (lane + 1 == (cz(k) & 0xFFu)) tlast[t] = v[k];
-      }
-    } else {
-      bad |= (in && w >= W) ? 1 : 0;  // outside [lo, hi]: an unsorted cover; redone on exact bounds
-    }
-    atomicAdd(&hist[in && w < W ? w : DUMMY], 1u);
-    if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-  }
-  __syncthreads();
-  // window starts (exclusive scan) -> desc row and cursors
-  uint16_t* drow = desc + gdesc[ch.g] + (c - gchunk[ch.g]) * (uint64_t)(W + 1);
-  {
-    uint32_t run = 0;
-    for (uint32_t b0 = 0; b0 <= W; b0 += BLOCK) {
-      const uint32_t i = b0 + threadIdx.x;
-      const uint32_t x = i < W ? hist[i] : 0;
-      uint32_t tot;
-      const uint32_t pre = block_excl_scan<BLOCK>(x, red, &tot) + run;
-      if (i <= W) {
-        drow[i] = (uint16_t)pre;
-        hist[i] = pre;
-      }
-      run += tot;
-    }
-  }
-  __syncthreads();
-  SYZ_STAMP(0, 3);
-  // pass 2: element = offset in window | member tag, window-major into obuf through the cursors; the
-  // cursor atomics of PB tiles are issued before their stores wait on them
-  const uint32_t omask = (1u << S) - 1;
-  constexpr int PB = 8;
-#pragma unroll
-  for (int k0 = 0; k0 < TPW; k0 += PB) {
-    uint32_t pos[PB], el[PB];
-    bool ok[PB];
-#pragma unroll
-    for (int k = k0; k < k0 + PB && k < TPW; k++) {
-      const uint32_t d = v[k] - lo, w = d >> S;
-      ok[k - k0] = lane < (cz(k) & 0xFFu) && w < W;
-      el[k - k0] = (d & omask) | ((cz(k) >> 8) << S);
-      pos[k - k0] = atomicAdd(&hist[ok[k - k0] ? w : DUMMY], 1u);
-    }
-#pragma unroll
-    for (int k = k0; k < k0 + PB && k < TPW; k++) obuf[ok[k - k0] ? pos[k - k0] : PCAP + lane] = el[k - k0];
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if constexpr (NOV) {
-#pragma unroll
-    for (int k = 0; k < TPW; k++) {
-      const uint32_t t = wv + WAVES * k;
-      if (t < ntiles) {
-        const uint32_t f = tinfo[t].w;
-        if (lane == 0 && (f & 2u) && tlast[t - 1] >= v[k]) bad |= (f & 1u) ? 1 : 4;
-      }
-    }
-  }
-  {
-    const uint64_t bm = __ballot(bad != 0);
-    if (bm) {
-      int all = bad;
-#pragma unroll
-      for (int dd = 32; dd >= 1; dd >>= 1) all |= __shfl_xor(all, dd, 64);
-      if (lane == (unsigned)(__ffsll((unsigned long long)bm) - 1)) atomicOr(err, all);
-    }
-  }
-  __syncthreads();
-  SYZ_STAMP(0, 4);
-  // chunk starts are 16-byte aligned (k_chunks): vector stores, then the tail
-  uint32_t* dst = elems + ch.elem;
-  const uint32_t n4 = ch.len >> 2;
-  uint4* d4 = reinterpret_cast<uint4*>(dst);
-  const uint4* o4 = reinterpret_cast<const uint4*>(obuf);
-  for (uint32_t i = threadIdx.x; i < n4; i += BLOCK) d4[i] = o4[i];
-  for (uint32_t i = (n4 << 2) + threadIdx.x; i < ch.len; i += BLOCK) dst[i] = obuf[i];
-  SYZ_STAMP(0, 5);
-}
-
 // ---- P, region form: every (call group, member segment, window) contiguous in HBM -----------------
 // The element buffer is laid out by REGION r = pg[g].rb + s * W + w: all PCs of call group g's member
 // segment s (members [s << (32 - S), (s + 1) << (32 - S)) of the group, in partition order) that fall
@@ -536,7 +162,7 @@ __global__ __launch_bounds__(BLOCK) void k_part4(
 //             stored as one contiguous run per window at its place: runs of consecutive chunks land
 //             side by side, and no global atomics are taken.
 // NOV: the new-coverage check's second source (maxCover tables as members, lists checked strictly
-// increasing in the COUNT pass, as k_part3).
+// increasing in the COUNT pass).
 template <int BLOCK, int TPW, bool NOV = false, bool COUNT = false>
 __global__ __launch_bounds__(BLOCK) void k_region(
     const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
@@ -915,101 +541,9 @@ __device__ __forceinline__ void for_region(const PItem it, const PGroup* pg, con
 constexpr int P3_BLOCK = SYZ_P3_BLOCK;
 constexpr int P3_TPW = (int)((TMAX + P3_BLOCK / 64 - 1) / (P3_BLOCK / 64));
 
-// ---- M: min rank per key of one (call, window) ------------------------------------------------------
-// A wave takes the window's runs of 64 chunks at a time (one chunk's run per lane of metadata) and
-// then walks them RB runs at a time: for each run one coalesced 256-byte load brings the Go-sort
-// ranks of the run's 64-member block into a register (lane m = member m), and the run's elements are
-// loaded one per lane; an element's rank is then a register shuffle by its member tag. RB runs'
-// loads are in flight together.
-#ifndef SYZ_RB
-#define SYZ_RB 16
-#endif
-constexpr int RB = SYZ_RB;
-constexpr int TU = 4;  // slices in flight per long run
-// IDENT: the rank of a member is its position (the new-coverage check: batch order), no rank loads.
-template <int RBN = RB, bool IDENT = false, class F>
-__device__ __forceinline__ void for_window_elems(const PItem it, const PChunk* __restrict__ chunks,
-                                                 const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
-                                                 const uint16_t* __restrict__ desc, const uint32_t* __restrict__ elems,
-                                                 const uint32_t* __restrict__ rank_of_member, uint32_t nmem_total,
-                                                 int nwaves, F f) {
-  const uint32_t g = it.g, w = it.w;
-  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
-  const uint32_t W = pg[g].W, S = pg[g].S;
-  const uint32_t omask = (1u << S) - 1;
-  const uint16_t* d0 = desc + gdesc[g] + w;
-  const int wv = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  const uint32_t last_m = nmem_total ? nmem_total - 1 : 0;
-  // wave wv takes runs c0 + wv, c0 + wv + nwaves, ... (64 of them per batch), so a window with few
-  // chunks still spreads over every wave
-  const uint64_t nrun = c1 - c0;
-  for (uint64_t b0 = (uint64_t)wv; b0 < nrun; b0 += (uint64_t)nwaves * 64) {
-    const uint64_t c = c0 + b0 + (uint64_t)lane * nwaves;
-    uint32_t len = 0, mb = 0, stl = 0, sth = 0;
-    if (c < c1) {
-      const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
-      const uint32_t s0 = d[0], s1 = d[1];
-      len = s1 - s0;
-      const uint64_t st = chunks[c].elem + s0;
-      stl = (uint32_t)st;
-      sth = (uint32_t)(st >> 32);
-      mb = chunks[c].mb;
-    }
-    const uint32_t nr = (uint32_t)min<uint64_t>(64, (nrun - b0 + nwaves - 1) / nwaves);
-    for (uint32_t r0 = 0; r0 < nr; r0 += RBN) {
-      uint32_t rk[RBN], e0[RBN], e1[RBN], ln[RBN];
-      uint64_t sts[RBN];
-#pragma unroll
-      for (int r = 0; r < RBN; r++) {
-        const uint32_t j = r0 + r;
-        ln[r] = j < nr ? (uint32_t)__builtin_amdgcn_readlane((int)len, (int)j) : 0u;
-        const uint32_t mbj = (uint32_t)__builtin_amdgcn_readlane((int)mb, (int)j);
-        sts[r] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sth, (int)j) << 32) |
-                 (uint32_t)__builtin_amdgcn_readlane((int)stl, (int)j);
-        rk[r] = IDENT ? mbj : 0u;
-        e0[r] = 0;
-        e1[r] = 0;
-        if (ln[r]) {
-          if constexpr (!IDENT) rk[r] = rank_of_member[min(mbj + lane, last_m)];
-          if (lane < ln[r]) e0[r] = elems[sts[r] + lane];
-          if (lane + 64 < ln[r]) e1[r] = elems[sts[r] + 64 + lane];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < RBN; r++) {
-        if (!ln[r]) continue;
-        {
-          const uint32_t R = IDENT ? rk[r] + (e0[r] >> S) : (uint32_t)__shfl((int)rk[r], (int)(e0[r] >> S), 64);
-          if (lane < ln[r]) f(e0[r] & omask, R);
-        }
-        if (ln[r] > 64) {
-          const uint32_t R = IDENT ? rk[r] + (e1[r] >> S) : (uint32_t)__shfl((int)rk[r], (int)(e1[r] >> S), 64);
-          if (lane + 64 < ln[r]) f(e1[r] & omask, R);
-          for (uint32_t k = 128; k < ln[r]; k += 64 * TU) {  // long runs: TU 64-PC slices in flight
-            uint32_t x[TU];
-#pragma unroll
-            for (int u = 0; u < TU; u++) {
-              const uint32_t i = k + 64 * u + lane;
-              x[u] = i < ln[r] ? elems[sts[r] + i] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < TU; u++) {
-              const uint32_t R2 =
-                  IDENT ? rk[r] + (x[u] >> S) : (uint32_t)__shfl((int)rk[r], (int)(x[u] >> S), 64);
-              if (k + 64 * u + lane < ln[r]) f(x[u] & omask, R2);
-            }
-          }
-        }
-      }
-    }
-  }
-}
-
 // ---- M walk, packed form ------------------------------------------------------------------------------
-// for_window_elems spends one wave instruction per run: a run of ~50 elements leaves a quarter of the
-// lanes idle and pays ~47 VALU of per-run bookkeeping (profiles/r03_pmin_base: ~0.9 VALU wave
-// instructions per element). Here the workgroup takes up to PK_RUNS runs of the window at once (one per
+// A walk with one wave instruction per run leaves lanes idle on short runs and pays per-run bookkeeping
+// (profiles/r03_pmin_base: ~0.9 VALU wave instructions per element). Here the workgroup takes up to PK_RUNS runs of the window at once (one per
 // thread: desc pair, chunk start, member block), numbers their elements with one workgroup scan, and
 // the waves then stream the concatenation in 64-element blocks — every lane of every load holds an
 // element whichever run it belongs to, and every wave has blocks whether the window has thousands of
@@ -1056,113 +590,6 @@ __device__ __forceinline__ void pk_scan(uint32_t len, uint32_t* lds, uint32_t& p
   pre = inc - len + p;
   k = kin + q;
   T = tp;
-}
-
-template <int U, bool IDENT, class F>
-__device__ __forceinline__ void for_window_packed(const PItem it, const PChunk* __restrict__ chunks,
-                                                  const uint64_t* gchunk, const uint64_t* gdesc, const PGroup* pg,
-                                                  const uint16_t* __restrict__ desc,
-                                                  const uint32_t* __restrict__ elems,
-                                                  const uint32_t* __restrict__ rank_of_member, uint32_t* scratch,
-                                                  uint64_t* red64, F f) {
-  static_assert(PK_RUNS == 1024, "one run per thread");
-  const uint32_t g = it.g, w = it.w;
-  const uint64_t c0 = gchunk[g], c1 = gchunk[g + 1];
-  if (c1 == c0) return;
-  const uint32_t W = pg[g].W, S = pg[g].S;
-  const uint32_t omask = (1u << S) - 1;
-  const uint16_t* d0 = desc + gdesc[g] + w;
-  const uint64_t gbase = chunks[c0].elem;  // element offsets of the group fit 32 bits from here
-  const uint32_t* gel = elems + gbase;
-  uint32_t* rrel = scratch;                 // [PK_RUNS] element offset of run k's element 0 - its prefix
-  uint32_t* rmb = scratch + PK_RUNS;        // [PK_RUNS] first member of run k's chunk
-  uint32_t* bstart = scratch + 2 * PK_RUNS;  // [PK_NBLK] run holding block j's first element
-  uint32_t* bmask = bstart + PK_NBLK;        // [2 PK_NBLK] runs starting inside block j (bit = offset)
-  const int nwaves = blockDim.x >> 6, wv = threadIdx.x >> 6;
-  const unsigned lane = __lane_id();
-  // a thread's run of a batch: desc pair and chunk (loaded one batch ahead)
-  auto load_run = [&](uint64_t c, uint32_t& len, uint32_t& rel, uint32_t& mb) {
-    len = rel = mb = 0;
-    if (c < c1) {
-      const uint16_t* d = d0 + (c - c0) * (uint64_t)(W + 1);
-      const uint32_t s0 = d[0];
-      len = (uint32_t)d[1] - s0;
-      const PChunk ch = chunks[c];
-      rel = (uint32_t)(ch.elem - gbase) + s0;
-      mb = ch.mb;
-    }
-  };
-  uint32_t nlen, nrel, nmb;
-  load_run(c0 + threadIdx.x, nlen, nrel, nmb);
-  for (uint64_t rb = c0; rb < c1; rb += PK_RUNS) {
-    // ---- batch: one run per thread, non-empty runs compacted in element order ----
-    const uint32_t len = nlen, rel = nrel, mb = nmb;
-    uint32_t pre, k, T;
-    pk_scan(len, reinterpret_cast<uint32_t*>(red64), pre, k, T);
-    if (len) {
-      rrel[k] = rel - pre;  // (rel - pre + idx) mod 2^32 = rel + (idx - pre): the element's offset
-      rmb[k] = mb;
-    }
-    load_run(rb + PK_RUNS + threadIdx.x, nlen, nrel, nmb);  // the next batch's runs, in flight meanwhile
-    for (uint32_t ew = 0; ew < T; ew += PK_EW) {
-      const uint32_t te = min(T, ew + PK_EW);
-      for (uint32_t j = threadIdx.x; j < 2 * PK_NBLK; j += blockDim.x) bmask[j] = 0;
-      __syncthreads();
-      if (len && pre < te && pre + len > ew) {
-        // block starts inside [max(pre, ew), min(pre + len, te)) belong to run k
-        const uint32_t a = max(pre, ew) - ew, b = min(pre + len, te) - ew;
-        for (uint32_t j = (a + 63) >> 6; (j << 6) < b; j++) bstart[j] = k;
-        if (pre >= ew && (pre & 63)) {
-          const uint32_t o = pre - ew;
-          atomicOr(&bmask[2 * (o >> 6) + ((o >> 5) & 1)], 1u << (o & 31));
-        }
-      }
-      __syncthreads();
-      // ---- the waves stream the window's blocks, U at a time, straight-line (no per-lane branches,
-      // so the compiler's waits are counted, not vmcnt(0) at every join): a lane past the window
-      // reads its block's first element and applies RANK_NONE, a no-op for a min table ----
-      const uint32_t nblk = (te - ew + 63) >> 6;
-      const uint32_t step = (uint32_t)nwaves * U;
-      for (uint32_t j0 = wv; j0 < nblk; j0 += step) {
-        uint32_t r0[U], slo[U], shi[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const uint32_t jj = min(j0 + (uint32_t)nwaves * u, nblk - 1);
-          r0[u] = bstart[jj];
-          const uint32_t mlo = bmask[2 * jj], mhi = bmask[2 * jj + 1];
-          slo[u] = (mlo >> 1) | (mhi << 31);  // runs starting at offsets 1..lane: mbcnt of mask >> 1
-          shi[u] = mhi >> 1;
-        }
-        uint32_t rl[U], mbr[U], id[U];
-        bool ok[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const uint32_t j = j0 + (uint32_t)nwaves * u, jj = min(j, nblk - 1);
-          const uint32_t idx = ew + (j << 6) + lane;
-          ok[u] = j < nblk && idx < te;
-          const uint32_t r = r0[u] + __builtin_amdgcn_mbcnt_hi(shi[u], __builtin_amdgcn_mbcnt_lo(slo[u], 0u));
-          const uint32_t rr = ok[u] ? r : r0[u];
-          id[u] = ok[u] ? idx : ew + (jj << 6);  // the block's first element lies in run r0
-          rl[u] = rrel[rr];
-          mbr[u] = rmb[rr];
-        }
-        uint32_t e[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) e[u] = gel[rl[u] + id[u]];
-        uint32_t R[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          if constexpr (IDENT)
-            R[u] = mbr[u] + (e[u] >> S);
-          else
-            R[u] = rank_of_member[mbr[u] + (e[u] >> S)];
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) f(e[u] & omask, ok[u] ? R[u] : RANK_NONE);
-      }
-      __syncthreads();  // bstart / bmask are rebuilt for the next element window
-    }
-  }
 }
 
 }  // namespace syz

@@ -417,7 +417,6 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restric
     return ((uint64_t)field(w, 0) | (uint64_t)field(w, 1) << 32) + ((uint64_t)field(w, 2) | (uint64_t)field(w, 3) << 32);
   };
   auto dst_of = [&](uint32_t w) { return (uint64_t)field(w, 6) | (uint64_t)field(w, 5) << 32; };  // lane 6: word 0
-  uint32_t cur[SC_VT], nxt[SC_VT];
   auto fetch = [&](uint32_t w, bool ok, uint32_t* v) {
     const uint32_t n = ok ? field(w, 4) : 0;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(gap + (ok ? src_of(w) : 0)), 0, n * 4, SO_RSRC_FLAGS);
