@@ -752,47 +752,79 @@ __global__ __launch_bounds__(BLOCK) void k_canon_cls(uint32_t* pcs, const uint64
 // no exec-mask loops. Then unique (cover.go:28-40: a PC is kept iff it differs from the one before,
 // the first against the sentinel) and the kept PCs stored in place after a wave scan of the per-lane
 // counts. Four independent waves per workgroup walk the class list.
-__device__ __forceinline__ uint32_t xor_lane(uint32_t x, int m) {
-  switch (m) {  // (a compile-time m after unrolling)
-    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
-    case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (4 << 10));
-    case 8: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (8 << 10));
-    case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (16 << 10));
-    default: {  // 32: the halves swapped (whichever way the two results come back, their xor with x is it)
-      const auto h = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-      return h[0] ^ h[1] ^ x;
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
+  if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+  else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // 2,3,0,1
+  else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x1B, 0xF, 0xF, false);  // 3,2,1,0
+  else if constexpr (M == 7) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  else if constexpr (M == 15) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+  else if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (M << 10));  // 4, 8, 16, 31
+  else {  // 32, 63: the halves swapped (whichever way the two results come back, their xor with x is the
+          // other half's value), then for 63 the mirror inside each half
+    const auto h = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    const uint32_t y = h[0] ^ h[1] ^ x;
+    if constexpr (M == 63) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)y, 0x1F | (31 << 10));
+    else return y;
+  }
+}
+
+// The bitonic network in its direction-free form: the first stage of merge K pairs element e with
+// e ^ (K - 1) (the mirror), the later ones with e ^ J, and every comparator keeps the minimum at the
+// lower index. Pairs inside a lane's R registers are plain min/max; across lanes each lane keeps the
+// min or the max by one lane bit. Compile-time recursion (not unrolled loops), so every exchange is
+// resolved at compile time however long the network is.
+template <int R, int J>
+__device__ __forceinline__ void cn_half(uint32_t (&x)[R], unsigned lane) {
+  if constexpr (J > 0) {
+    if constexpr (J < R) {  // register pairs (r, r | J)
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (r & J) continue;
+        const uint32_t lo = min(x[r], x[r | J]), hi = max(x[r], x[r | J]);
+        x[r] = lo;
+        x[r | J] = hi;
+      }
+    } else {  // lane pairs (l, l ^ J / R)
+      const bool keepmin = ((uint32_t)lane & (uint32_t)(J / R)) == 0;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const uint32_t y = xor_lane<J / R>(x[r]);
+        x[r] = keepmin ? min(x[r], y) : max(x[r], y);
+      }
     }
+    cn_half<R, J / 2>(x, lane);
+  }
+}
+
+template <int R, int K>
+__device__ __forceinline__ void cn_merges(uint32_t (&x)[R], unsigned lane) {
+  if constexpr (K <= 64 * R) {
+    if constexpr (K <= R) {  // the mirror inside a lane: (r, r ^ (K - 1)) for r with bit K / 2 clear
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (r & (K >> 1)) continue;
+        const int q = r ^ (K - 1);
+        const uint32_t lo = min(x[r], x[q]), hi = max(x[r], x[q]);
+        x[r] = lo;
+        x[q] = hi;
+      }
+    } else {  // the mirror across lanes: lane ^ (K / R - 1), register R - 1 - r
+      const bool keepmin = ((uint32_t)lane & (uint32_t)(K / (2 * R))) == 0;
+      uint32_t y[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) y[r] = xor_lane<K / R - 1>(x[R - 1 - r]);
+#pragma unroll
+      for (int r = 0; r < R; r++) x[r] = keepmin ? min(x[r], y[r]) : max(x[r], y[r]);
+    }
+    cn_half<R, K / 4>(x, lane);
+    cn_merges<R, 2 * K>(x, lane);
   }
 }
 
 template <int R>
 __device__ __forceinline__ void canon_net(uint32_t (&x)[R], unsigned lane) {
-#pragma unroll
-  for (int k = 2; k <= 64 * R; k <<= 1) {
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j < R) {  // register pairs (r, r | j); descending where element bit k is set
-        const bool lane_desc = k >= R && (((uint32_t)lane * R) & k) != 0;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-          if (r & j) continue;
-          const uint32_t lo = min(x[r], x[r | j]), hi = max(x[r], x[r | j]);
-          const bool desc = k < R ? (r & k) != 0 : lane_desc;
-          x[r] = desc ? hi : lo;
-          x[r | j] = desc ? lo : hi;
-        }
-      } else {  // lane pairs (l, l ^ j / R)
-        const int m = j / R;
-        const bool keepmin = (((uint32_t)lane & m) == 0) == ((((uint32_t)lane * R) & k) == 0);
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-          const uint32_t y = xor_lane(x[r], m);
-          x[r] = keepmin ? min(x[r], y) : max(x[r], y);
-        }
-      }
-    }
-  }
+  cn_merges<R, 2>(x, lane);
 }
 
 template <int R>
