@@ -87,10 +87,26 @@ ROCPROF_SCOPE = [("k_slab<", "k_slab"), ("k_smin_direct", "k_pmin_direct"), ("k_
                  ("k_pmin_hash<true>", "k_pmin_packed"), ("k_colscan", "k_colscan")]
 
 
-def rocprof_top(path=ROCPROF_STATS):
+# the workload the committed rocprofv3 summary and PMC passes were taken on: the default bench line
+PROFILED_WORKLOAD = "config4-1M"
+
+
+def workload_key(args, world):
+    """Short key of the workload a line measures, to match committed profiles against: the default line
+    (config 4, 1M programs, 2M PCs, one GPU) is "config4-1M"."""
+    if world == 1 and not args.total_progs and not args.emulate and args.progs_per_gpu == 1_000_000 \
+            and args.npcs == 2_000_000 and args.ngroups == 289 and args.calls == 1159 and args.seed == 0x5EED0004:
+        return PROFILED_WORKLOAD
+    return "progs%d-pcs%d-groups%d-world%d%s" % (args.progs_per_gpu, args.npcs, args.ngroups, world,
+                                                "-total%d" % args.total_progs if args.total_progs else "")
+
+
+def rocprof_top(path=ROCPROF_STATS, workload=PROFILED_WORKLOAD):
     """(scope, kernel name) of the first row of the committed rocprofv3 --stats summary (rows are
-    sorted by total duration), or None."""
+    sorted by total duration), or None; None too when the line's workload is not the one profiled."""
     import csv
+    if workload != PROFILED_WORKLOAD:
+        return None
     try:
         rows = list(csv.DictReader(open(path)))
     except OSError:
@@ -104,7 +120,7 @@ def rocprof_top(path=ROCPROF_STATS):
     return None
 
 
-def dominant_kernel(kern):
+def dominant_kernel(kern, workload=PROFILED_WORKLOAD):
     """The step's dominant kernel: the top kernel of the committed rocprofv3 summary of this command
     (ROCPROF_STATS) when it maps to a byte-modelled scope; else the kernel scope with the most time in
     the untimed per-kernel pass among those carrying an algorithmic byte model (SURVEY.md
@@ -113,17 +129,18 @@ def dominant_kernel(kern):
     of the groups they walk. That pass runs the
     raw pipeline's passes one after another (syzgpu_profile_enable(2)), so each scope times its kernels
     alone. Phase scopes (gosort_*, m_big, group_partition) span several kernels and are not candidates."""
-    top = rocprof_top()
+    top = rocprof_top(workload=workload)
     if top and top[0] in kern and kern[top[0]]["bytes"] > 0:
         return top[0]
     rows = [(d["ms"], name) for name, d in kern.items() if name.startswith("k_") and d["bytes"] > 0]
     return max(rows)[1] if rows else None
 
 
-def roofline(name, ev, peak_gbs=None):
+def roofline(name, ev, peak_gbs=None, workload=PROFILED_WORKLOAD):
     """Roofline of one kernel from its HIP events in the timed region (on its launch stream): achieved =
     its recorded algorithmic bytes / its time; traffic = HBM bytes per launch from the committed PMC
-    passes (profiles/pmc_traffic.json, FETCH_SIZE doubled + WRITE_SIZE) when they name this kernel."""
+    passes (profiles/pmc_traffic.json, FETCH_SIZE doubled + WRITE_SIZE) when they name this kernel and
+    were taken on this line's workload (null otherwise)."""
     d = ev.get(name)
     if not d or not d["ms"]:
         return None
@@ -138,7 +155,7 @@ def roofline(name, ev, peak_gbs=None):
     if os.path.exists(tf):
         try:
             pm = json.load(open(tf))
-            if name in pm.get("kernels", {}) and pm.get("workload") == "config4-1M":
+            if name in pm.get("kernels", {}) and pm.get("workload") == workload:
                 out["traffic"] = pm["kernels"][name]["hbm_bytes_per_launch"]
         except Exception:
             pass
@@ -302,7 +319,8 @@ def main():
         torch.cuda.synchronize()
         kern = read_prof()
         L.syzgpu_profile_enable(0)
-    roof_kernel = dominant_kernel(kern) if kern else None
+    wkey = workload_key(args, world)
+    roof_kernel = dominant_kernel(kern, wkey) if kern else None
     # timed region: HIP events (on the launch stream) around the dominant kernel only
     if roof_kernel:
         L.syzgpu_profile_only(roof_kernel.encode())
@@ -341,11 +359,12 @@ def main():
     out = None
     if rank == 0:
         # roofline of the dominant kernel: algorithmic bytes over its measured time
-        roof = roofline(roof_kernel, roof_ev) if roof_kernel else None
+        roof = roofline(roof_kernel, roof_ev, workload=wkey) if roof_kernel else None
         if roof:
             roof["launches_per_step"] = round(roof_ev[roof_kernel]["launches"] / args.steps, 2)
             roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
-            top = rocprof_top()
+            roof["profiled_workload"] = wkey if wkey == PROFILED_WORKLOAD else None
+            top = rocprof_top(workload=wkey)
             roof["selection"] = (("the top kernel of the committed rocprofv3 summary %s (%s)"
                                   % (os.path.relpath(ROCPROF_STATS, ROOT), top[1][:60])) if top and top[0] == roof_kernel
                                  else "the byte-modelled kernel with the most time in the serialized per-kernel pass")
@@ -628,11 +647,15 @@ def analytics_leg(args, dev, L, read_prof, store, corp, sptr):
     if "cs_uniq" in ev:
         e = ev["cs_uniq"]
         ms = e["ms"] / e["launches"]
-        alg = 4 * int(corp.off[-1]) + 10 * n  # the covers once (4 B per PC) + offsets and call id
+        # what the kernel reads: the store's index-resident u16 id streams (2 B per PC; 16-B vectors of 8
+        # ids) and one u32 entry tag per vector, not the 4-B PCs of the raw covers
+        alg = 2 * int(corp.off[-1]) + 4 * (int(corp.off[-1]) // 8)
         res["roofline"] = {"bound": "hbm", "kernel": "cs_uniq", "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms, 4),
-                           "algorithmic_bytes_per_launch": alg}
+                           "algorithmic_bytes_per_launch": alg,
+                           "bytes": "index-resident u16 id streams (2 B per PC) + a u32 entry tag per 8 ids; the "
+                                    "index build (once per store, store_reuse) is outside this leg"}
     if args.cpu_baseline and args.analytics_cpu_sample > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle

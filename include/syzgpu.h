@@ -402,6 +402,11 @@ int syzgpu_profile_enable(int on);
 int syzgpu_profile_only(const char* name);
 size_t syzgpu_profile_read(char (*names)[48], float* ms, uint64_t* bytes, size_t cap);
 
+/* Test hook (no reference counterpart): the k-th growth of a corpus store's buffers from now fails
+ * with SYZGPU_ENOMEM, as a device allocation failure would (k <= 0: off). The failure-atomicity tests
+ * use it to check that a rejected append or NewInput leaves the store and corpusCover unchanged. */
+int syzgpu_debug_fail_grow(int k);
+
 #ifdef __cplusplus
 }
 #endif

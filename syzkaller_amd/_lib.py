@@ -102,6 +102,7 @@ SIGNATURES = {
     "syzgpu_profile_enable": (_c.c_int, [_c.c_int]),
     "syzgpu_profile_only": (_c.c_int, [_c.c_char_p]),
     "syzgpu_profile_read": (_sz, [_vp, _vp, _vp, _sz]),
+    "syzgpu_debug_fail_grow": (_c.c_int, [_c.c_int]),
 }
 
 

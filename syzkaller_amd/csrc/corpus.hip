@@ -118,6 +118,15 @@ static void index_follow(CorpusHandle& H, F f) {
   }
 }
 
+void append_reserve(CorpusHandle& H, size_t m, uint64_t Lm, hipStream_t s) {
+  const size_t n = H.n, nt = n + m;
+  if (nt >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
+  grow_keep(H.pcs, H.L, H.L + Lm + 1, s);
+  grow_keep(H.off, n + 1, nt + 1, s);
+  grow_keep(H.group, n, nt + 1, s);
+  grow_keep(H.prog_len, n, nt + 1, s);
+}
+
 // covers (device pointers) appended after H's current ones; prog_len may be null (zeros)
 void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                    const uint16_t* prog_len, size_t m, hipStream_t s, bool cc_update) {
@@ -141,15 +150,11 @@ void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, co
   if (Lm && !pcs) fail(SYZGPU_EINVAL, "null pointer");
   const size_t n = H.n, nt = n + m;
   const uint64_t L0 = H.L;
-  if (nt >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many corpus entries");
+  append_reserve(H, m, Lm, s);  // (before corpusCover changes: a failed growth leaves everything as it was)
   if (cc_update) cc_add(H, pcs, off, group, m, Lm, s);  // corpusCover follows every append
   index_follow(H, [&](Corpus& K) {  // a recorded keep first (the appends before it are applied by it)
     if (K.keep_pending) corpus_index_sync(K, H, s);
   });
-  grow_keep(H.pcs, H.L, H.L + Lm + 1, s);
-  grow_keep(H.off, n + 1, nt + 1, s);
-  grow_keep(H.group, n, nt + 1, s);
-  grow_keep(H.prog_len, n, nt + 1, s);
   if (Lm) SYZ_HIP(hipMemcpyAsync(H.pcs.p + H.L, pcs, Lm * 4, hipMemcpyDeviceToDevice, s));
   k_shift_off<<<grid_for(m + 1, 256, 4096), 256, 0, s>>>(off, m, H.L, H.off.p + n);
   SYZ_LAUNCHED();
@@ -180,7 +185,14 @@ static CorpusHandle* handle_create_dev(const uint32_t* pcs, const uint64_t* off,
 static void keep_entries(CorpusHandle& H, const int64_t* idx, size_t m, hipStream_t s, bool distinct = false) {
   if (m && !idx) fail(SYZGPU_EINVAL, "null pointer");
   // corpusCover holds every cover the store has held: taken before a keep that may drop a call's PCs
-  // (minimizeCorpus's keep without key parts cannot: Minimize keeps a first holder of every PC)
+  // (minimizeCorpus's keep without key parts cannot: Minimize keeps a first holder of every PC). The
+  // distinct form comes only from minimize_keep, whose begin and end run back to back on this store
+  // alone, so its selection covers every holder of every PC here; a multi-rank minimize (selections
+  // exchanged between begin_dev and end_dev, where a rank may drop all its local holders of a PC) keeps
+  // through syzgpu_corpus_keep[_dev], which is not distinct and builds corpusCover first.
+  // Deliberate difference from manager.go:121 (corpusCover starts empty there): the store seeds it from
+  // the covers it was created with, as if each had come through NewInput (manager.go:609-616), which is
+  // how the manager's corpus entries get there.
   if (!distinct || H.parts_set) cc_ensure(H, s);
   index_follow(H, [&](Corpus& K) { corpus_index_sync(K, H, s); });  // a recorded keep first
   Scratch& sc = ctx().scratch;

@@ -60,6 +60,9 @@ void corpus_index_sync(Corpus& K, const CorpusHandle& H, hipStream_t s);
 // (when built)
 void append_covers(CorpusHandle& H, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                    const uint16_t* prog_len, size_t m, hipStream_t s, bool cc_update = true);
+// room for m more entries and Lm more PCs, before anything changes (a gate that mutates corpusCover
+// first reserves, so the append after it cannot fail on capacity or the entry limit)
+void append_reserve(CorpusHandle& H, size_t m, uint64_t Lm, hipStream_t s);
 // corpus_cover.hip: corpusCover built from H's covers if it is not yet; the union of appended covers;
 // NewInput's gate over a batch (is_new: device bytes or null; returns the number appended)
 void cc_ensure(CorpusHandle& H, hipStream_t s);

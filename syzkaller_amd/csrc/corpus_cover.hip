@@ -475,22 +475,26 @@ uint64_t corpus_new_inputs(CorpusHandle& H, const uint32_t* pcs, const uint64_t*
   if (h[0] != 0) fail(SYZGPU_EINVAL, "CSR offsets must start at 0");
   const uint64_t Lm = h[1];
   if (Lm && !pcs) fail(SYZGPU_EINVAL, "null pointer");
+  // the append after the gate must not fail once the gate has put keys into corpusCover: the entry
+  // limit and the store's capacity for the worst case (every input accepted) are settled first
+  append_reserve(H, m, Lm, s);
   uint8_t* acc = is_new ? is_new : sc.get<uint8_t>("cc_acc", m + 1);
   uint64_t* apos = sc.get<uint64_t>("cc_apos", m + 1);
+  // the compaction's buffers too, at their worst-case sizes (every input accepted)
+  uint32_t* len = sc.get<uint32_t>("cc_len", m + 1);
+  uint64_t* lpos = sc.get<uint64_t>("cc_lpos", m + 1);
+  uint64_t* off2 = sc.get<uint64_t>("cc_off2", m + 1);
+  uint32_t* pcs2 = sc.get<uint32_t>("cc_pcs2", Lm + 1);
+  uint32_t* group2 = sc.get<uint32_t>("cc_grp2", m + 1);
+  uint16_t* pl2 = prog_len ? sc.get<uint16_t>("cc_pl2", m + 1) : nullptr;
   const uint64_t na = cc_gate(H.cc.h, pcs, off, group, m, Lm, H.G, acc, apos, s);
   pt.mark("gate", s);
   if (na == m) {
     append_covers(H, pcs, off, group, prog_len, m, s, false);
   } else if (na) {
-    uint32_t* len = sc.get<uint32_t>("cc_len", m + 1);
-    uint64_t* lpos = sc.get<uint64_t>("cc_lpos", m + 1);
-    uint64_t* off2 = sc.get<uint64_t>("cc_off2", na + 1);
     k_cc_lens<<<grid_for(m, 256, 4096), 256, 0, s>>>(off, acc, m, len);
     SYZ_LAUNCHED();
     exclusive_scan_u32(len, lpos, m, s);
-    uint32_t* pcs2 = sc.get<uint32_t>("cc_pcs2", Lm + 1);
-    uint32_t* group2 = sc.get<uint32_t>("cc_grp2", na + 1);
-    uint16_t* pl2 = prog_len ? sc.get<uint16_t>("cc_pl2", na + 1) : nullptr;
     k_cc_offs<<<grid_for(m + 1, 256, 4096), 256, 0, s>>>(acc, apos, lpos, m, off2);
     SYZ_LAUNCHED();
     k_cc_gather<<<wave_grid(m), 256, 0, s>>>(pcs, off, group, prog_len, acc, apos, m, off2, pcs2, group2, pl2);

@@ -332,6 +332,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 }
 
 // ---- M over slab runs (slab_dev.hpp): the same tables, the window's runs from every slab --------------
+#ifndef SYZ_SMIN_IDENT
+#define SYZ_SMIN_IDENT false  // timing experiment only (results wrong when true)
+#endif
 #ifndef SYZ_SL_MU
 #define SYZ_SL_MU 2
 #endif
@@ -362,7 +365,7 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
     for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
   }
   __syncthreads();
-  for_slab_window<SYZ_SL_MU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
+  for_slab_window<SYZ_SL_MU, SYZ_SMIN_IDENT>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
                                     [&](uint32_t o, uint32_t R) {
                                       // a plain read first: most elements of a PC held by many inputs lose
                                       // to the rank already there, and same-address reads broadcast where
@@ -398,7 +401,7 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
     if (threadIdx.x == 0) L.full = 0;
     __syncthreads();
     const uint32_t RR = R, rr = round;
-    for_slab_window<SYZ_SL_HU, false>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
+    for_slab_window<SYZ_SL_HU, SYZ_SMIN_IDENT>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
                                       [&](uint32_t o, uint32_t Rk) {
                                         if (Rk == RANK_NONE) return;  // a lane past the window
                                         if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;

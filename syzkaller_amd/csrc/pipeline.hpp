@@ -13,8 +13,8 @@ struct Seg {
 };
 
 // gosort.hip: the element at sorted position r of the groups' ranges is el[perm[r]]
-constexpr uint32_t GS_T_SEG = 8192;
-constexpr uint64_t GS_U32_LEN_LIMIT = 1ull << 19;  // cover lengths the packed u32 sort element holds  // call groups above this many entries start the global rounds
+constexpr uint32_t GS_T_SEG = 8192;                // call groups above this many entries start the global rounds
+constexpr uint64_t GS_U32_LEN_LIMIT = 1ull << 19;  // cover lengths the packed u32 sort element holds
 struct Pack;
 struct GosortPlan {
   size_t n = 0;

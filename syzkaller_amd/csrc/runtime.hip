@@ -4,6 +4,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "store.hpp"
 
 namespace syz {
 
@@ -331,6 +332,11 @@ int syzgpu_profile_enable(int on) {
   prof().on = on != 0;
   prof().serial = on == 2;
   prof().reset();
+  return SYZGPU_OK;
+}
+
+int syzgpu_debug_fail_grow(int k) {
+  syz::grow_fail_countdown() = k > 0 ? k : 0;
   return SYZGPU_OK;
 }
 

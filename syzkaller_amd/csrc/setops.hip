@@ -997,6 +997,14 @@ __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t
   }
 }
 
+// the bounds [off[seg], off[seg + 1]) of the listed covers
+static __global__ void k_canon_bigoff(const uint32_t* segs, uint32_t nseg, const uint64_t* off, uint64_t* out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nseg; i += gridDim.x * blockDim.x) {
+    out[2 * i] = off[segs[i]];
+    out[2 * i + 1] = off[segs[i] + 1];
+  }
+}
+
 void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, uint64_t* out_len, hipStream_t s) {
   Context& c = ctx();
   if (ncov == 0) return;
@@ -1041,18 +1049,28 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   SYZ_HIP(hipStreamSynchronize(s));
   const uint32_t nbig = h[CANON_NCLS - 1];
   if (!nbig) return;
+  // every long cover's bounds in one copy (one host wait for the whole batch, not one per cover)
+  uint64_t* dbo = c.scratch.get<uint64_t>("canon_bigoff", 2 * (size_t)nbig);
+  k_canon_bigoff<<<grid_for(nbig, 256, 1024), 256, 0, s>>>(lists + (CANON_NCLS - 1) * ncov, nbig, off, dbo);
+  SYZ_LAUNCHED();
   std::vector<uint32_t> big(nbig);
+  std::vector<uint64_t> hbo(2 * (size_t)nbig);
   SYZ_HIP(hipMemcpyAsync(big.data(), lists + (CANON_NCLS - 1) * ncov, nbig * 4, hipMemcpyDeviceToHost, s));
-  std::vector<uint64_t> hoff(2);
-  for (uint32_t seg : big) {
-    SYZ_HIP(hipMemcpyAsync(hoff.data(), off + seg, 16, hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
+  SYZ_HIP(hipMemcpyAsync(hbo.data(), dbo, 16 * (size_t)nbig, hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipStreamSynchronize(s));
+  uint64_t nmax = 0;
+  for (uint32_t i = 0; i < nbig; i++) nmax = std::max(nmax, hbo[2 * i + 1] - hbo[2 * i]);
+  uint64_t Pmax = 1;
+  while (Pmax < nmax) Pmax <<= 1;
+  uint32_t* tmp = c.scratch.get<uint32_t>("canon_big", Pmax);
+  uint8_t* keep = c.scratch.get<uint8_t>("canon_keep", nmax);
+  uint64_t* pos = c.scratch.get<uint64_t>("canon_pos", nmax + 1);
+  for (uint32_t i = 0; i < nbig; i++) {
+    const uint32_t seg = big[i];
+    const uint64_t hoff[2] = {hbo[2 * i], hbo[2 * i + 1]};
     const uint64_t n = hoff[1] - hoff[0];
     uint64_t P = 1;
     while (P < n) P <<= 1;
-    uint32_t* tmp = c.scratch.get<uint32_t>("canon_big", P);
-    uint8_t* keep = c.scratch.get<uint8_t>("canon_keep", n);
-    uint64_t* pos = c.scratch.get<uint64_t>("canon_pos", n + 1);
     const unsigned g = grid_for(P, 256, 65536);
     k_canon_pad<<<g, 256, 0, s>>>(pcs + hoff[0], n, tmp, P);
     SYZ_LAUNCHED();

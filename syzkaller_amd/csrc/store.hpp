@@ -181,9 +181,15 @@ void corpus_partition(Corpus& K, std::vector<uint64_t>& hpcs, hipStream_t s);
 void corpus_upload_work(Corpus& K, hipStream_t s);
 
 // Device buffer that keeps its first `used` elements when it grows (appends); 1.5x headroom.
+// test hook (syzgpu_debug_fail_grow): the k-th growth from now fails as an allocation failure would
+inline int& grow_fail_countdown() {
+  static int k = 0;
+  return k;
+}
 template <class T>
 void grow_keep(Grow<T>& g, size_t used, size_t need, hipStream_t s) {
   if (need <= g.cap && g.p) return;
+  if (int& k = grow_fail_countdown(); k > 0 && --k == 0) fail(SYZGPU_ENOMEM, "forced growth failure (test hook)");
   const size_t want = need + need / 2 + 16;
   T* p = nullptr;
   SYZ_HIP(hipMalloc(&p, want * sizeof(T)));

@@ -36,8 +36,34 @@ def test_dominant_kernel_follows_the_summary_else_the_serialized_pass(monkeypatc
     f = tmp_path / "stats.csv"
     f.write_text('"Name","Calls","TotalDurationNs"\n"void syz::k_region<512, 40, false, false>(int)",1,10\n')
     monkeypatch.setattr(bench, "ROCPROF_STATS", str(f))
-    monkeypatch.setattr(bench.rocprof_top, "__defaults__", (str(f),))
+    monkeypatch.setattr(bench.rocprof_top, "__defaults__", (str(f), bench.PROFILED_WORKLOAD))
     assert bench.dominant_kernel(kern) == "k_region"
-    monkeypatch.setattr(bench.rocprof_top, "__defaults__", (str(tmp_path / "missing.csv"),))
+    monkeypatch.setattr(bench.rocprof_top, "__defaults__", (str(tmp_path / "missing.csv"), bench.PROFILED_WORKLOAD))
     # phase scopes (no k_ prefix) and kernels without a byte model never name the roofline
     assert bench.dominant_kernel(kern) == "k_pmin_direct"
+
+
+def _args(**kw):
+    import types
+    d = dict(progs_per_gpu=1_000_000, npcs=2_000_000, ngroups=289, calls=1159, seed=0x5EED0004, total_progs=0,
+             emulate="")
+    d.update(kw)
+    return types.SimpleNamespace(**d)
+
+
+def test_profiles_apply_only_to_the_workload_they_were_taken_on(monkeypatch, tmp_path):
+    """A config-1 or config-2 line must not carry config 4's PMC traffic or rocprof selection."""
+    assert bench.workload_key(_args(), 1) == bench.PROFILED_WORKLOAD
+    small = bench.workload_key(_args(progs_per_gpu=10_000, npcs=50_000), 1)
+    assert small != bench.PROFILED_WORKLOAD
+    assert bench.workload_key(_args(), 8) != bench.PROFILED_WORKLOAD
+    assert bench.workload_key(_args(total_progs=1_000_000), 1) != bench.PROFILED_WORKLOAD
+    assert bench.rocprof_top(workload=small) is None
+    f = tmp_path / "pmc.json"
+    f.write_text('{"workload": "config4-1M", "kernels": {"k_slab": {"hbm_bytes_per_launch": 123}}}')
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    os.makedirs(tmp_path / "profiles")
+    os.replace(f, tmp_path / "profiles" / "pmc_traffic.json")
+    ev = {"k_slab": {"ms": 2.0, "launches": 2, "bytes": 2_000_000}}
+    assert bench.roofline("k_slab", ev, workload=bench.PROFILED_WORKLOAD)["traffic"] == 123
+    assert bench.roofline("k_slab", ev, workload=small)["traffic"] is None

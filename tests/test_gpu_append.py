@@ -347,11 +347,24 @@ def test_new_input_gate_vs_oracle_novelty(first):
     assert np.array_equal(is_new, want)
     assert 0 < want.sum() < want.size and not want[-4] and not want[-3] and want[-2] and not want[-1]
     _check_gate(st, model)
-    # 2: device pointers, a small batch (the one-workgroup path)
+    # 2a: the same edge cases through a small batch (under 4M PCs: the batch-table path with its
+    # atomicMin claims): a repeat of an earlier input of the batch, a sentinel-only cover, an empty one,
+    # and a new PC pair with the sentinel followed by the same pair without it
+    dup = b.pcs[int(b.off[20_005]):int(b.off[20_006])]
+    extra = [(dup, int(b.group[20_005])), (np.array([0xFFFFFFFF], np.uint32), 3), (np.zeros(0, np.uint32), 4),
+             (np.array([3, 4, 0xFFFFFFFF], np.uint32), 3), (np.array([3, 4], np.uint32), 3)]
+    pcs, off, grp, pl = _gate_batch(b, 20_000, 20_100, extra)
+    assert int(off[-1]) < (1 << 22)
+    is_new = st.NewInputs(pcs, off, grp, pl)
+    want = model.new_inputs(pcs, off, grp, pl)
+    assert np.array_equal(is_new, want)
+    assert not want[-5] and not want[-4] and not want[-3] and want[-2] and not want[-1]
+    _check_gate(st, model)
+    # 2b: device pointers, a small batch (the one-workgroup path)
     s = torch.cuda.current_stream().cuda_stream
-    pcs, off, grp, pl = _gate_batch(b, 20_000, 20_200)
-    d_new = torch.zeros(200, dtype=torch.uint8, device="cuda")
-    na = st.NewInputsDevice(*(_dev(x) for x in (pcs, off, grp, pl)), 200, d_new, s)
+    pcs, off, grp, pl = _gate_batch(b, 20_100, 20_200)
+    d_new = torch.zeros(100, dtype=torch.uint8, device="cuda")
+    na = st.NewInputsDevice(*(_dev(x) for x in (pcs, off, grp, pl)), 100, d_new, s)
     want = model.new_inputs(pcs, off, grp, pl)
     assert na == int(want.sum()) and np.array_equal(d_new.cpu().numpy().astype(bool), want)
     _check_gate(st, model)
@@ -395,4 +408,38 @@ def test_new_input_gate_rejects_bad_batches():
         with pytest.raises(Exception):
             st.NewInputs(pcs.astype(np.uint32), off.astype(np.uint64), np.array(grp, np.uint32))
         _check_gate(st, model)  # unchanged
+    st.close()
+
+
+def test_failed_growth_leaves_store_and_corpus_cover_unchanged():
+    """A NewInput batch or an append whose store growth fails (forced through the test hook
+    syzgpu_debug_fail_grow, as a device allocation failure) leaves the entries and corpusCover as they
+    were, so the same batch retried afterwards is gated exactly as the oracle gates it."""
+    from syzkaller_amd import _lib
+    G = 7
+    a = synth.corpus(0x5EED00C4, 3_000, G, 30_000)
+    b = synth.corpus(0x5EED00C5, 4_000, G, 60_000)  # more PCs than the store's headroom: it must grow
+    st = cover.CoverStore(a.pcs, a.off, a.group, G, a.prog_len)
+    hc = HostCorpus(a, 0, a.n)
+    model = GateModel(hc, G)
+    _check_gate(st, model)  # builds corpusCover
+    pcs, off, grp, pl = _gate_batch(b, 0, b.n)
+    lib = _lib.lib()
+    try:
+        lib.syzgpu_debug_fail_grow(1)
+        with pytest.raises(Exception):
+            st.NewInputs(pcs, off, grp, pl)
+        lib.syzgpu_debug_fail_grow(0)
+        _check_gate(st, model)  # unchanged: no key of the failed batch entered corpusCover
+        lib.syzgpu_debug_fail_grow(1)
+        with pytest.raises(Exception):
+            st.append(*_part(b, 0, b.n))
+        lib.syzgpu_debug_fail_grow(0)
+        _check_gate(st, model)
+    finally:
+        lib.syzgpu_debug_fail_grow(0)
+    want = model.new_inputs(pcs, off, grp, pl)
+    assert 0 < want.sum()
+    assert np.array_equal(st.NewInputs(pcs, off, grp, pl), want)  # the retry is gated as the first try
+    _check_gate(st, model)
     st.close()

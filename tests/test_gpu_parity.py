@@ -219,7 +219,7 @@ def test_canonicalize_batch_dev_classes_vs_oracle():
     import torch
     rnd = np.random.default_rng(23)
     sizes = [0, 1, 5, 63, 64, 65, 128, 129, 300, 511, 512, 513, 1000, 1024, 1025, 2048, 2049, 9000, 16384, 16385,
-             20000, 32768, 32769, 33000]
+             20000, 32768, 32769, 33000, 70000]
     sizes += list(rnd.integers(1, 1500, size=300))
     covs = [rnd.integers(0, max(2, int(sz)), size=int(sz), dtype=np.uint64).astype(np.uint32) for sz in sizes]
     covs.append(np.full(9, 0xFFFFFFFF, np.uint32))
