@@ -114,6 +114,7 @@ struct Context {
   hipEvent_t ev_part0 = nullptr, ev_part1 = nullptr;
   hipEvent_t ev_msmall = nullptr, ev_msmall2 = nullptr;  // the small groups' packed M on another stream
   hipEvent_t ev_psmall = nullptr;  // P's slabs of the small call groups are cut
+  hipEvent_t ev_spin = nullptr;    // stream_wait_spin's marker
   hipStream_t part2 = nullptr;  // its scatter passes, batch after batch beside the next batch's count
   std::vector<hipEvent_t> ev_cnt, ev_sct;  // per batch: count done, scatter done
   int ncu = 0;  // compute units of the device
@@ -206,6 +207,9 @@ struct HostTimer {
   }
 };
 void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s);
+// Waits for everything issued to s so far by polling an event (no blocking wait: the host turns around
+// in microseconds when the plan it waits for is short); falls back to a blocking wait after 50 ms.
+void stream_wait_spin(hipStream_t s);
 
 inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {
   size_t g = (n + block - 1) / block;

@@ -705,9 +705,8 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     ns.mc_off = d_mco;
     ns.n1 = (uint32_t)n;
     if (SJ.slab_bound) {
-      k_slab<SL_BLOCK, SL_TPW, true><<<(unsigned)SJ.slab_bound, SL_BLOCK, 0, s>>>(
-          d_pcs, d_off, cmem, mlen, SJ.tpos, nullptr, SJ.slabs, SJ.cstart + B, dsg, SJ.gebase, lo, SJ.elems, SJ.D, err,
-          SJ.wtot, ns);
+      launch_slab<true>(SJ.slab_bound, SJ.wmax, s, d_pcs, d_off, cmem, mlen, SJ.tpos, nullptr, SJ.slabs, SJ.cstart + B,
+                        dsg, SJ.gebase, lo, SJ.elems, SJ.D, err, SJ.wtot, ns, 0);
       SYZ_LAUNCHED();
     }
   }

@@ -332,9 +332,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 }
 
 // ---- M over slab runs (slab_dev.hpp): the same tables, the window's runs from every slab --------------
+#ifndef SYZ_SMIN_NOF
+#define SYZ_SMIN_NOF 0  // timing experiment only (results wrong when 1)
+#endif
 #ifndef SYZ_SMIN_IDENT
 #define SYZ_SMIN_IDENT false  // timing experiment only (results wrong when true)
 #endif
+#define SMIN_WALK(U, it, sg, gslab, gebase, D, slabs, elems, rom, wsc, red64, f) \
+  for_slab_window<U, SYZ_SMIN_IDENT>(it, sg, gslab, gebase, D, slabs, elems, rom, wsc, red64, f)
 #ifndef SYZ_SL_MU
 #define SYZ_SL_MU 2
 #endif
@@ -365,8 +370,12 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
     for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
   }
   __syncthreads();
-  for_slab_window<SYZ_SL_MU, SYZ_SMIN_IDENT>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
+  SMIN_WALK(SYZ_SL_MU, it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
                                     [&](uint32_t o, uint32_t R) {
+                                      if (SYZ_SMIN_NOF) {  // timing only: the walk without table updates
+                                        if ((o ^ R) == 0x7FFF1234u) tab[0] = 0;
+                                        return;
+                                      }
                                       // a plain read first: most elements of a PC held by many inputs lose
                                       // to the rank already there, and same-address reads broadcast where
                                       // atomics serialize
@@ -401,9 +410,13 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
     if (threadIdx.x == 0) L.full = 0;
     __syncthreads();
     const uint32_t RR = R, rr = round;
-    for_slab_window<SYZ_SL_HU, SYZ_SMIN_IDENT>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
+    SMIN_WALK(SYZ_SL_HU, it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
                                       [&](uint32_t o, uint32_t Rk) {
                                         if (Rk == RANK_NONE) return;  // a lane past the window
+                                        if (SYZ_SMIN_NOF) {  // timing only: the walk without table updates
+                                          if ((o ^ Rk) == 0x7FFF1234u) L.full = 1;
+                                          return;
+                                        }
                                         if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
                                         if constexpr (PACKED) {
                                           const uint32_t pk = (o << PK_RBITS) | (uint32_t)(Rk - gb);
@@ -619,6 +632,7 @@ void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* 
   J.hgblock.assign(G + 1, 0);
   J.hbgroup.clear();
   J.slab_bound = J.dtotal = J.wtotal = J.total_pcs = J.xtotal = 0;
+  J.wmax = 1;
   for (uint32_t g = 0; g < G; g++) {
     const uint64_t ng = hstart[g + 1] - hstart[g];
     const uint32_t S = hpg[g].S, W = hpg[g].W;
@@ -632,6 +646,7 @@ void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* 
     // a group's element offsets (D) are 32-bit
     if (hpcs[g] + stride * slab_pad(W) + 8 >= (1ull << 32)) fail(SYZGPU_EINVAL, "a call group with 2^32 or more PCs");
     J.hsg[g] = SGroup{J.dtotal, S, W, (uint32_t)stride, memb, (uint32_t)J.wtotal, 0, J.xtotal};
+    J.wmax = std::max(J.wmax, W);
     J.xtotal += stride * slab_pad(W);
     J.dtotal += (uint64_t)(W + 1) * stride;
     if (want_wtot) J.wtotal += W;
@@ -713,70 +728,83 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   // (hsl points into the lane's pinned buffer, which the plan's staging copy below reuses)
   const std::vector<uint64_t> hslv(hsl, hsl + G);
   hsl = hslv.data();
-  SlabJob SJ;
-  slab_plan(SJ, hstart, hsl, hpg, G, false);
-  ht.mark("slab_plan");
-  const uint64_t slab_bound = SJ.slab_bound, total_pcs = SJ.total_pcs;
-  const uint32_t B = SJ.B;
-  // work items: (call, window), class (big groups: sorted by the global rounds) and mode, largest
-  // expected window first; a key part only its windows
   const auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
-  std::vector<uint32_t> order(G);
-  std::iota(order.begin(), order.end(), 0u);
-  std::stable_sort(order.begin(), order.end(),
-                   [&](uint32_t x, uint32_t y) { return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W; });
-  // items counted per (class, mode) first, then written straight into the pinned staging copy
-  uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};
-  size_t icount[2][3] = {{0, 0, 0}, {0, 0, 0}};
-  std::vector<uint32_t> iw0(G, 0), iw1(G, 0);
-  for (uint32_t g : order) {
-    if (!hpcs[g]) continue;
-    uint32_t w0 = 0, w1 = hpg[g].W;
-    if (a.key_lo) {
-      const uint32_t klo = std::max(a.key_lo[g], lo), khi = std::min(a.key_hi[g], hi);
-      if (klo > khi) continue;
-      w0 = (klo - lo) >> hpg[g].S;
-      w1 = std::min<uint32_t>(hpg[g].W, ((khi - lo) >> hpg[g].S) + 1);
+  // The plan (slabs' layout, work items) is a pure function of the group sizes, the PCs each group
+  // reads, the span and the key ranges: a step on the same layout reuses the previous one's (host
+  // structures and the staged device copy owned by the job), so only the device work is redone.
+  std::vector<uint64_t> key(hstart);
+  key.insert(key.end(), hslv.begin(), hslv.end());
+  key.push_back(((uint64_t)lo << 32) | hi);
+  if (a.key_lo)
+    for (uint32_t g = 0; g < G; g++) key.push_back(((uint64_t)a.key_lo[g] << 32) | a.key_hi[g]);
+  if (!J.pcache || J.pcache->key != key) {
+    auto P = std::make_shared<SlabPlanCache>();
+    P->key = std::move(key);
+    SlabJob& SJ = P->SJ;
+    slab_plan(SJ, hstart, hsl, hpg, G, false);
+    const uint32_t B = SJ.B;
+    // work items: (call, window), class (big groups: sorted by the global rounds) and mode, largest
+    // expected window first; a key part only its windows
+    std::vector<uint32_t> order(G);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t x, uint32_t y) { return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W; });
+    std::vector<uint32_t> iw0(G, 0), iw1(G, 0);
+    for (uint32_t g : order) {
+      if (!hpcs[g]) continue;
+      uint32_t w0 = 0, w1 = hpg[g].W;
+      if (a.key_lo) {
+        const uint32_t klo = std::max(a.key_lo[g], lo), khi = std::min(a.key_hi[g], hi);
+        if (klo > khi) continue;
+        w0 = (klo - lo) >> hpg[g].S;
+        w1 = std::min<uint32_t>(hpg[g].W, ((khi - lo) >> hpg[g].S) + 1);
+      }
+      iw0[g] = w0;
+      iw1[g] = w1;
+      P->icount[is_big(g) ? 1 : 0][hpg[g].mode] += w1 - w0;
+      P->item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
     }
-    iw0[g] = w0;
-    iw1[g] = w1;
-    icount[is_big(g) ? 1 : 0][hpg[g].mode] += w1 - w0;
-    item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
-  }
-  std::array<std::array<size_t, 3>, 2> ifirst{};
-  size_t nitems = 0;
-  for (int big = 0; big < 2; big++)
-    for (int m = 0; m < 3; m++) {
-      ifirst[big][m] = nitems;
-      nitems += icount[big][m];
-    }
-  // the plan goes over in one copy: SGroup[G], gblock[G + 1], bgroup[B + 1], items[nitems + 1]
-  auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
-  const size_t o_gb = al16((G + 1) * sizeof(SGroup)), o_bg = o_gb + al16((G + 1) * 4),
-               o_it = o_bg + al16(((size_t)B + 1) * 4), stage_bytes = o_it + al16((nitems + 1) * sizeof(PItem));
-  uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
-  uint8_t* dstage = sc.get<uint8_t>("pm_stage", stage_bytes + 64);
-  SGroup* dsg = reinterpret_cast<SGroup*>(dstage);
-  uint32_t* dgblock = reinterpret_cast<uint32_t*>(dstage + o_gb);
-  uint32_t* dbgroup = reinterpret_cast<uint32_t*>(dstage + o_bg);
-  PItem* ditems = reinterpret_cast<PItem*>(dstage + o_it);
-  for (uint32_t g = 0; g < G; g++) SJ.hsg[g].pad = is_big(g) ? 1u : 0u;
-  {
+    size_t nitems = 0;
+    for (int big = 0; big < 2; big++)
+      for (int m = 0; m < 3; m++) {
+        P->ifirst[big][m] = nitems;
+        nitems += P->icount[big][m];
+      }
+    // the plan goes over in one copy: SGroup[G], gblock[G + 1], bgroup[B + 1], items[nitems + 1]
+    auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
+    P->o_gb = al16((G + 1) * sizeof(SGroup));
+    P->o_bg = P->o_gb + al16((G + 1) * 4);
+    P->o_it = P->o_bg + al16(((size_t)B + 1) * 4);
+    const size_t stage_bytes = P->o_it + al16((nitems + 1) * sizeof(PItem));
+    uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
+    P->dstage.ensure(stage_bytes + 64);
+    for (uint32_t g = 0; g < G; g++) SJ.hsg[g].pad = is_big(g) ? 1u : 0u;
     std::memcpy(stage, SJ.hsg.data(), G * sizeof(SGroup));
-    std::memcpy(stage + o_gb, SJ.hgblock.data(), (G + 1) * 4);
-    if (B) std::memcpy(stage + o_bg, SJ.hbgroup.data(), (size_t)B * 4);
-    PItem* hit = reinterpret_cast<PItem*>(stage + o_it);
-    std::array<std::array<size_t, 3>, 2> at = ifirst;
+    std::memcpy(stage + P->o_gb, SJ.hgblock.data(), (G + 1) * 4);
+    if (B) std::memcpy(stage + P->o_bg, SJ.hbgroup.data(), (size_t)B * 4);
+    PItem* hit = reinterpret_cast<PItem*>(stage + P->o_it);
+    std::array<std::array<size_t, 3>, 2> at = P->ifirst;
     for (uint32_t g : order) {
       size_t& k = at[is_big(g) ? 1 : 0][hpg[g].mode];
       for (uint32_t w = iw0[g]; w < iw1[g]; w++) hit[k++] = PItem{g, w};
     }
-    SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(P->dstage.p, stage, stage_bytes, hipMemcpyHostToDevice, s));
+    SJ.dsg = reinterpret_cast<SGroup*>(P->dstage.p);
+    SJ.dgblock = reinterpret_cast<uint32_t*>(P->dstage.p + P->o_gb);
+    SJ.dbgroup = reinterpret_cast<uint32_t*>(P->dstage.p + P->o_bg);
+    J.pcache = P;
   }
+  const SlabPlanCache& PC = *J.pcache;
+  SlabJob SJ = PC.SJ;  // (the device members below are this step's)
+  const auto& icount = PC.icount;
+  const auto& ifirst = PC.ifirst;
+  const auto& item_pcs = PC.item_pcs;
+  const uint64_t slab_bound = SJ.slab_bound, total_pcs = SJ.total_pcs;
+  const uint32_t B = SJ.B;
+  uint8_t* dstage = PC.dstage.p;
+  const SGroup* dsg = SJ.dsg;
+  const PItem* ditems = reinterpret_cast<const PItem*>(dstage + PC.o_it);
   ht.mark("items_stage");
-  SJ.dsg = dsg;
-  SJ.dgblock = dgblock;
-  SJ.dbgroup = dbgroup;
   slab_build(SJ, "pm", mlen, mpos, n, gstart, s, true);
   ht.mark("slab_build");
   const PSlab* slabs = SJ.slabs;
@@ -822,9 +850,8 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     for (int cls = split ? 1 : 0; cls <= (split ? 2 : 0); cls++) {
       const uint64_t bytes = cls ? cpcs[cls - 1] * 4 + cent[cls - 1] * 10 : total_pcs * 4 + (uint64_t)n * 10;
       ProfScope ps("k_slab", pq, bytes);
-      k_slab<SL_BLOCK, SL_TPW><<<(unsigned)slab_bound, SL_BLOCK, 0, pq>>>(
-          a.pcs, a.off, members, mlen, SJ.tpos, sbeg, slabs, SJ.cstart + B, dsg, gebase, lo, elems, SJ.D, err,
-          nullptr, NovSrc{}, rg_dbg(), cls);
+      launch_slab<false>(slab_bound, SJ.wmax, pq, a.pcs, a.off, members, mlen, SJ.tpos, sbeg, slabs, SJ.cstart + B,
+                         dsg, gebase, lo, elems, SJ.D, err, nullptr, NovSrc{}, cls);
       SYZ_LAUNCHED();
       if (cls == 1) SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
     }
@@ -1004,7 +1031,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
   if (!pm_region()) slab_tiles(mlen, n, "pm", s);
   HostTimer ht("begin");
-  SYZ_HIP(hipStreamSynchronize(s));
+  stream_wait_spin(s);
   ht.mark("wait_partition");
   J.may_bounce = hbuf[3 * G + 3] >= GS_U32_LEN_LIMIT;
   if (*reinterpret_cast<int*>(hbuf + 2 * G + 2)) fail(SYZGPU_EINVAL, "group id >= ngroups");

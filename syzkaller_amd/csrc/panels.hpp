@@ -1,5 +1,6 @@
 // The raw-cover Minimize pipeline (panels.hip) and the pieces of minimize.hip it shares.
 #pragma once
+#include <array>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -53,6 +54,7 @@ __host__ __device__ inline uint64_t slab_pad(uint32_t W) { return 3ull * W + 4; 
 // first slab and element; then k_slab (P) and for_slab_window (M).
 struct SlabJob {
   uint32_t G = 0, B = 0;
+  uint32_t wmax = 1;  // the widest call's windows (P's LDS staging is sized for it)
   uint64_t slab_bound = 0, dtotal = 0, wtotal = 0, total_pcs = 0, xtotal = 0;
   std::vector<SGroup> hsg;
   std::vector<uint32_t> hgblock, hbgroup;
@@ -101,6 +103,17 @@ struct RawEndArgs {
 // One minimizeCorpus job (the raw path): its selection lives here between begin and end, so a
 // multi-GPU step can exchange the selection of split call groups in between, and concurrent callers
 // with their own jobs never see each other's state.
+// begin_slab's plan for one layout (the key), kept by the job for the next step on the same layout
+struct SlabPlanCache {
+  std::vector<uint64_t> key;
+  SlabJob SJ;  // host parts; dsg / dgblock / dbgroup point into dstage
+  size_t icount[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  std::array<std::array<size_t, 3>, 2> ifirst{};
+  uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  size_t o_gb = 0, o_bg = 0, o_it = 0;
+  Grow<uint8_t> dstage;  // SGroup[G], gblock[G + 1], bgroup[B + 1], items
+};
+
 struct MinJob {
   std::recursive_mutex mu;
   size_t n = 0;
@@ -116,6 +129,7 @@ struct MinJob {
   Grow<uint8_t> count_hist;
   std::vector<uint64_t> hstart, xkey;
   std::shared_ptr<GosortPlan> plan;  // Go-sort plan of the last layout (keeps its rounds hint)
+  std::shared_ptr<SlabPlanCache> pcache;  // begin_slab's plan of the last layout
   std::vector<uint64_t> plan_key;
   uint64_t stats_total_pcs = 0;
   size_t stats_items_direct = 0, stats_items_hash = 0;

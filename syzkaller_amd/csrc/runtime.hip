@@ -1,3 +1,4 @@
+#include <chrono>
 // Context, error state, scratch memory, profiling and the device-wide scans.
 #include <condition_variable>
 #include <cstdio>
@@ -272,6 +273,21 @@ void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s
 void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s, const char* tag) {
   scan_impl<uint32_t>(in, out, n, s, 0, tag);
 }
+void stream_wait_spin(hipStream_t s) {
+  Context& c = ctx();
+  if (!c.ev_spin) SYZ_HIP(hipEventCreateWithFlags(&c.ev_spin, hipEventDisableTiming));
+  SYZ_HIP(hipEventRecord(c.ev_spin, s));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t r = hipEventQuery(c.ev_spin);
+    if (r == hipSuccess) return;
+    if (r != hipErrorNotReady) SYZ_HIP(r);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+    __builtin_ia32_pause();
+  }
+  SYZ_HIP(hipEventSynchronize(c.ev_spin));
+}
+
 void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) {
   scan_impl<uint64_t>(in, out, n, s, 0);
 }

@@ -116,11 +116,17 @@ __global__ __launch_bounds__(256) void k_setop_scatter(int side, const uint32_t*
 // of the counts, stages them in LDS and stores the tile's run coalesced (emit). A pair with a repeated
 // value (allowed by Go, never produced by the executor's sort + unique) sends the batch to the
 // per-element rank path above; a descending neighbour is the Go panic (EINVAL).
-constexpr int SO_BLOCK = 128;
-constexpr int SO_VT = 8;
+#ifndef SYZ_SO_BLOCK
+#define SYZ_SO_BLOCK 128
+#endif
+#ifndef SYZ_SO_VT
+#define SYZ_SO_VT 8
+#endif
+constexpr int SO_BLOCK = SYZ_SO_BLOCK;
+constexpr int SO_VT = SYZ_SO_VT;
 constexpr uint32_t SO_T = SO_BLOCK * SO_VT;  // merged elements per tile
-constexpr int SO_LOG_T = 10;
-static_assert(SO_T == 1u << SO_LOG_T, "tile size");
+constexpr int SO_LOG_T = SO_T == 512 ? 9 : SO_T == 1024 ? 10 : SO_T == 2048 ? 11 : SO_T == 4096 ? 12 : -1;
+static_assert(SO_LOG_T > 0 && SO_T == 1u << SO_LOG_T, "tile size");
 
 __global__ void k_so_ntiles(const uint64_t* aoff, const uint64_t* boff, uint32_t npairs, uint32_t* nt) {
   for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += gridDim.x * blockDim.x) {
@@ -390,6 +396,10 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_tile(int op, const uint32_t* __
 // WAVE walks its own tiles (no LDS, no barrier: more tiles in flight per CU for a walk that is all
 // latency), two tiles deep (see step below).
 constexpr int SC_VT = SO_T / 64;
+#ifndef SYZ_SC_DEPTH
+#define SYZ_SC_DEPTH 2
+#endif
+constexpr int SC_DEPTH = SYZ_SC_DEPTH;  // tiles in flight per compaction wave
 __global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restrict__ desc,
                                                          const uint32_t* __restrict__ tcnt,
                                                          const uint64_t* __restrict__ tout,
@@ -424,39 +434,46 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restric
     for (int r = 0; r < SC_VT; r++)
       if (r * 64 < (int)n) v[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, (lane + r * 64) * 4, 0, 0);
   };
-  // two tiles' words and two more tiles' offsets in flight per wave: tile k is stored from D[k % 2] while
-  // tile k+2's words load into it (its offsets were read two steps ago) and tile k+4's offsets into M[k % 2]
-  uint32_t D0[SC_VT], D1[SC_VT];
-  uint32_t m = meta_load(tile);
-  uint32_t n0 = field(m, 4);
-  uint64_t d0 = dst_of(m);
-  fetch(m, true, D0);
-  const bool ok1 = tile + stride < ntiles;
-  m = meta_load(tile + stride);
-  uint32_t n1 = ok1 ? field(m, 4) : 0;
-  uint64_t d1 = ok1 ? dst_of(m) : 0;
-  fetch(m, ok1, D1);
-  uint32_t M0 = meta_load(tile + 2 * stride), M1 = meta_load(tile + 3 * stride);
+  // SC_DEPTH tiles' words and SC_DEPTH more tiles' offsets in flight per wave: tile k is stored from
+  // D[k % SC_DEPTH] while tile k + SC_DEPTH's words load into it (its offsets were read SC_DEPTH steps ago)
+  // and tile k + 2 SC_DEPTH's offsets into M[k % SC_DEPTH]
+  uint32_t D[SC_DEPTH][SC_VT], M[SC_DEPTH], nn[SC_DEPTH];
+  uint64_t dd[SC_DEPTH];
+#pragma unroll
+  for (int q = 0; q < SC_DEPTH; q++) {
+    const bool ok = tile + q * stride < ntiles;
+    const uint32_t m = meta_load(tile + q * stride);
+    nn[q] = ok ? field(m, 4) : 0;
+    dd[q] = ok ? dst_of(m) : 0;
+    fetch(m, ok, D[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < SC_DEPTH; q++) M[q] = meta_load(tile + (SC_DEPTH + q) * stride);
   {
     const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, 0, SO_RSRC_FLAGS);  // (see k_so_tile)
 #pragma unroll
     for (int r = 0; r < SC_VT; r++)
       __builtin_amdgcn_raw_buffer_store_b32(0u, rz, (lane + r * 64) * 4, 0, 0);
   }
-  auto step = [&](uint32_t* D, uint32_t& M, uint32_t& n, uint64_t& d) {
+  auto step = [&](uint32_t* Dq, uint32_t& Mq, uint32_t& n, uint64_t& d) {
     const auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(out + d), 0, n * 4, SO_RSRC_FLAGS);
 #pragma unroll
     for (int r = 0; r < SC_VT; r++)  // (wave-uniform: a tile's empty slots issue nothing)
-      if (r * 64 < (int)n) __builtin_amdgcn_raw_buffer_store_b32(D[r], rd, (lane + r * 64) * 4, 0, 0);
-    const bool ok = tile + 2 * stride < ntiles;
-    n = ok ? field(M, 4) : 0;
-    d = ok ? dst_of(M) : 0;
-    fetch(M, ok, D);
-    M = meta_load(tile + 4 * stride);
+      if (r * 64 < (int)n) __builtin_amdgcn_raw_buffer_store_b32(Dq[r], rd, (lane + r * 64) * 4, 0, 0);
+    const bool ok = tile + SC_DEPTH * stride < ntiles;
+    n = ok ? field(Mq, 4) : 0;
+    d = ok ? dst_of(Mq) : 0;
+    fetch(Mq, ok, Dq);
+    Mq = meta_load(tile + 2 * SC_DEPTH * stride);
     tile += stride;
     return tile < ntiles;
   };
-  while (step(D0, M0, n0, d0) && step(D1, M1, n1, d1)) {
+  for (;;) {
+    bool more = true;
+#pragma unroll
+    for (int q = 0; q < SC_DEPTH; q++)
+      if (more) more = step(D[q], M[q], nn[q], dd[q]);
+    if (!more) break;
   }
 }
 
@@ -964,7 +981,7 @@ __device__ __forceinline__ int canon_class_of(uint64_t n) {
        : n <= 4096 ? 6 : n <= 8192 ? 7 : n <= 16384 ? 8 : n <= (uint64_t)CANON_LDS2 ? 9 : 10;
 }
 __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t ncov, uint32_t* lists, size_t cap,
-                                                     uint32_t* cnt) {
+                                                     uint32_t* cnt, const uint8_t* done = nullptr) {
   __shared__ uint32_t lc[CANON_NCLS], lb[CANON_NCLS];
   const unsigned lane = __lane_id();
   for (size_t c0 = (size_t)blockIdx.x * CANON_CHUNK; c0 < ncov; c0 += (size_t)gridDim.x * CANON_CHUNK) {
@@ -973,7 +990,7 @@ __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t
     for (int pass = 0; pass < 2; pass++) {  // 0: counts; 1: entries at the reserved bases
       for (size_t i0 = c0; i0 < min(c0 + CANON_CHUNK, ncov); i0 += blockDim.x) {
         const size_t i = i0 + threadIdx.x;
-        const int c = i < ncov ? canon_class_of(off[i + 1] - off[i]) : -1;
+        const int c = i < ncov && !(done && done[i]) ? canon_class_of(off[i + 1] - off[i]) : -1;
 #pragma unroll
         for (int k = 0; k < CANON_NCLS; k++) {
           const uint64_t m = __ballot(c == k);
@@ -997,6 +1014,48 @@ __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t
   }
 }
 
+// Already-canonical covers (the executor's dedup on, executor.cc:565-585 -> fuzzer.go:355): one wave
+// per cover streams it once, 4 x 64 PCs per step with lane i of load k at PC 64 k + i, and checks it
+// strictly increasing (each PC against the one before it: the lane before, the last lane of the load
+// before, the previous step's last PC), stopping at the first violation. Such a cover is its own
+// Canonicalize (sorted, no repeat; a 0xFFFFFFFF can only be its last PC, kept unless it is the only
+// one): its length goes to out_len and its flag keeps it out of the classes. Others: flag 0.
+constexpr int CANON_SCAN_U = 4;
+__global__ __launch_bounds__(256) void k_canon_sorted(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
+                                                      size_t ncov, uint8_t* __restrict__ done,
+                                                      uint64_t* __restrict__ out_len) {
+  const unsigned lane = __lane_id();
+  const size_t nw = (size_t)gridDim.x * (blockDim.x >> 6);
+  for (size_t i = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < ncov; i += nw) {
+    const uint64_t b = off[i], n = off[i + 1] - b;
+    const uint32_t* x = pcs + b;
+    bool bad = false;
+    uint32_t last = 0;  // the PC before this step's first (none at the start)
+    for (uint64_t j0 = 0; j0 < n && !bad; j0 += 64 * CANON_SCAN_U) {
+      uint32_t v[CANON_SCAN_U];
+#pragma unroll
+      for (int k = 0; k < CANON_SCAN_U; k++) {
+        const uint64_t j = j0 + 64 * k + lane;
+        v[k] = j < n ? x[j] : 0xFFFFFFFFu;
+      }
+      bool b2 = false;
+#pragma unroll
+      for (int k = 0; k < CANON_SCAN_U; k++) {
+        const uint64_t j = j0 + 64 * k + lane;
+        uint32_t prev = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k], 0x138, 0xF, 0xF, false);  // lane - 1
+        if (lane == 0) prev = last;
+        if (j < n && j > 0 && prev >= v[k]) b2 = true;
+        last = (uint32_t)__builtin_amdgcn_readlane((int)v[k], 63);
+      }
+      bad = __ballot(b2) != 0;
+    }
+    if (lane == 0) {
+      done[i] = !bad;
+      if (!bad) out_len[i] = (n == 1 && x[0] == 0xFFFFFFFFu) ? 0 : n;
+    }
+  }
+}
+
 // the bounds [off[seg], off[seg + 1]) of the listed covers
 static __global__ void k_canon_bigoff(const uint32_t* segs, uint32_t nseg, const uint64_t* off, uint64_t* out) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nseg; i += gridDim.x * blockDim.x) {
@@ -1012,7 +1071,11 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", CANON_NCLS * ncov);
   uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", CANON_NCLS);
   SYZ_HIP(hipMemsetAsync(cnt, 0, CANON_NCLS * 4, s));
-  k_canon_class<<<(unsigned)std::min<size_t>((ncov + CANON_CHUNK - 1) / CANON_CHUNK, 2048), 256, 0, s>>>(off, ncov, lists, ncov, cnt);
+  // covers that are canonical already are done by the check (no network); the rest are classed
+  uint8_t* done = c.scratch.get<uint8_t>("cd_done", ncov);
+  k_canon_sorted<<<(unsigned)std::min<size_t>((ncov + 3) / 4, 8192), 256, 0, s>>>(pcs, off, ncov, done, out_len);
+  SYZ_LAUNCHED();
+  k_canon_class<<<(unsigned)std::min<size_t>((ncov + CANON_CHUNK - 1) / CANON_CHUNK, 2048), 256, 0, s>>>(off, ncov, lists, ncov, cnt, done);
   SYZ_LAUNCHED();
   if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
   const unsigned ncu = (unsigned)std::max(1, c.ncu);

@@ -18,6 +18,8 @@
 // M (for_slab_window) then walks one run per slab: a window's runs are ~SL_TILES * 64 / W elements long
 // (128 for a dense call of 256 windows: 512-byte runs, against round 2's 64-element chunk runs).
 #pragma once
+#include <atomic>
+
 #include "panels_dev.hpp"
 
 namespace syz {
@@ -26,22 +28,13 @@ namespace syz {
 #define SYZ_SL_BLOCK 512
 #endif
 #ifndef SYZ_SL_TPW
-#define SYZ_SL_TPW 64
-#endif
-#ifndef SYZ_SL_SKIP
-#define SYZ_SL_SKIP 0  // A/B knob: skip tile groups outside a pass (measured with register spills)
-#endif
-#ifndef SYZ_SL_BUF_BITS
-#define SYZ_SL_BUF_BITS 14
+#define SYZ_SL_TPW 32
 #endif
 constexpr int SL_BLOCK = SYZ_SL_BLOCK;
 constexpr int SL_WAVES = SL_BLOCK / 64;
 constexpr int SL_TPW = SYZ_SL_TPW;
 constexpr uint32_t SL_TILES = (uint32_t)SL_TPW * SL_WAVES;  // tiles per slab (<= 64 PCs each)
-constexpr uint32_t SL_BUF_BITS = SYZ_SL_BUF_BITS;
-constexpr uint32_t SL_BUF = 1u << SL_BUF_BITS;                 // LDS staging elements per pass
 constexpr uint32_t SL_MEMB = 512;                              // members per slab at most
-constexpr uint32_t SL_PMAX = (SL_TILES * 64 + SL_BUF - 1) / SL_BUF + 1;  // passes at most
 static_assert(SL_TPW <= 64, "a wave's tile table is one register per lane");
 constexpr uint32_t SL_NONE = 0xFFFFFFFFu;  // a padding slot: no element (no member has the all-ones tag)
 
@@ -112,41 +105,52 @@ static __global__ void k_sl_groups(const uint32_t* gblock, uint32_t G, const uin
   }
 }
 
-// ---- P: one slab per workgroup ---------------------------------------------------------------------
-// (see the file comment). err bit 1: a PC outside [lo, lo + W << S) (an unsorted cover: the job is redone
-// on exact bounds).
+// ---- P: one slab per workgroup, one pass ------------------------------------------------------------
+// (see the file comment). The whole slab (<= 64 SL_TILES elements + 3 W padding slots) is staged in LDS
+// (dynamic: slab_lds_bytes(Wmax) for the widest call of the launch), so every element is placed once:
+// histogram by LDS atomics, a scan to the padded window starts (D rows), one returning atomic per
+// element for its place, the padding slots filled, and the slab leaves as one run of 16-byte stores.
+// err bit 1: a PC outside [lo, lo + W << S) (an unsorted cover: the job is redone on exact bounds).
 // NOV: the new-coverage check's second source (members with an entry id >= ns.n1 are maxCover tables),
 // every list checked strictly increasing as it is read (err 1 for a table, 4 for a cover: lane
 // neighbours, and a tile's first PC against the member's PC before it); wtot (optional): per (call,
 // window) element totals, added up over the slabs.
+__host__ __device__ constexpr uint32_t slab_obuf_words(uint32_t Wmax) { return (64 * SL_TILES + 3 * Wmax + 4 + 3) & ~3u; }
+__host__ __device__ constexpr uint32_t slab_hist_words(uint32_t Wmax) { return (Wmax + 1 + 64 + 3) & ~3u; }
+__host__ __device__ constexpr size_t slab_lds_bytes(uint32_t Wmax) {
+  return 4ull * (slab_obuf_words(Wmax) + 2 * slab_hist_words(Wmax) + 16);
+}
+static_assert(5 * SL_MEMB + SL_MEMB / 4 <= 64 * SL_TILES, "the member table lives in the staging buffer's space");
+
 template <int BLOCK, int TPW, bool NOV = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_slab(
     const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off, const uint32_t* __restrict__ members,
     const uint32_t* __restrict__ mlen, const uint64_t* __restrict__ tpos, const uint32_t* __restrict__ sbeg,
     const PSlab* __restrict__ slabs, const uint64_t* nslab, const SGroup* __restrict__ sg,
     const uint64_t* __restrict__ gebase, uint32_t lo, uint32_t* __restrict__ elems, uint32_t* __restrict__ D,
-    int* err, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int dbg = 0, int cls = 0) {
+    int* err, uint32_t Wmax, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int cls = 0) {
   constexpr int WAVES = BLOCK / 64;
   static_assert((uint32_t)TPW * WAVES == SL_TILES, "slab tiles");
-  __shared__ __align__(16) uint32_t obuf[SL_BUF];
-  __shared__ uint32_t hist[WMAX + 1 + 64];  // counts, then cursors; + a dummy slot per lane
-  __shared__ int32_t mrel[SL_MEMB];         // member i's tile 0 as a slab tile index (< 0: began earlier)
-  __shared__ uint32_t mtp[SL_MEMB];         // the search keys: mrel clipped to [0, nt]
-  __shared__ uint32_t mlo[SL_MEMB], mhi[SL_MEMB], mln[SL_MEMB];
-  __shared__ uint8_t mtab[NOV ? SL_MEMB : 1];  // NOV: member i is a table
-  __shared__ uint32_t red[WAVES + 1];
-  __shared__ uint32_t pw[SL_PMAX + 2];      // first window of each pass
-  __shared__ uint32_t pa[SL_PMAX + 1];      // its start (read before any pass moves the cursors)
-  // one slab per workgroup (a persistent loop over slabs made the compiler keep per-slab values across
-  // iterations and spill)
+  extern __shared__ __align__(16) uint32_t slds[];
+  uint32_t* obuf = slds;                                  // the slab's elements, window-major
+  uint32_t* hist = obuf + slab_obuf_words(Wmax);          // counts, then cursors; + a dummy slot per lane
+  uint32_t* pst = hist + slab_hist_words(Wmax);           // padded window starts
+  uint32_t* red = pst + slab_hist_words(Wmax);            // block scan
+  // the member table, in the staging buffer's space (dead once the tiles are resolved)
+  int32_t* mrel = reinterpret_cast<int32_t*>(obuf);       // member i's tile 0 as a slab tile index (< 0: began earlier)
+  uint32_t* mtp = obuf + SL_MEMB;                         // the search keys: mrel clipped to [0, nt]
+  uint32_t* mlo = obuf + 2 * SL_MEMB;
+  uint32_t* mhi = obuf + 3 * SL_MEMB;
+  uint32_t* mln = obuf + 4 * SL_MEMB;
+  uint8_t* mtab = reinterpret_cast<uint8_t*>(obuf + 5 * SL_MEMB);  // NOV: member i is a table
   const uint64_t nsl = *nslab;
-  if (uint64_t c = blockIdx.x; c < nsl) {
+  const uint64_t c = blockIdx.x;
+  if (c >= nsl) return;
   const int wv = threadIdx.x >> 6;
   const unsigned lane = __lane_id();
   const PSlab sl = slabs[c];
   const SGroup gp = sg[sl.g];
-  // cls 1 / 2: only the slabs of small / big call groups (SGroup.pad bit 0), so the small groups' M
-  // can start while the big groups' slabs are still being cut
+  // cls 1 / 2: only the slabs of small / big call groups (SGroup.pad bit 0)
   if (cls && (gp.pad & 1u) != (uint32_t)(cls - 1)) return;
   const uint32_t S = gp.S, W = gp.W, nt = sl.nt, nmem = sl.nmem;
   for (uint32_t i = threadIdx.x; i < nmem; i += BLOCK) {
@@ -167,8 +171,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     mhi[i] = (uint32_t)(a >> 32);
     mln[i] = mlen[m];
   }
-  for (uint32_t i = threadIdx.x; i <= W; i += BLOCK) hist[i] = 0;
-  for (uint32_t i = threadIdx.x; i < SL_PMAX + 2; i += BLOCK) pw[i] = W;
+  for (uint32_t i = threadIdx.x; i < W + 1 + 64; i += BLOCK) hist[i] = 0;
   __syncthreads();
   // lane k of this wave: tile t = wv + WAVES k (its member by a search of the tile prefix)
   uint32_t alo, ahi, cz;
@@ -204,11 +207,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     v[k] = reinterpret_cast<const uint32_t*>((uintptr_t)base)[lane < cnt ? lane : 0u];
     if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
   }
-  // every wave has read its tiles' member entries (its loads' addresses depend on them): the member
-  // table's space takes the tiles' window ranges (a plain barrier: the loads stay in flight)
-  if (SYZ_SL_SKIP) __builtin_amdgcn_s_barrier();
-  uint32_t* trng = reinterpret_cast<uint32_t*>(mrel);  // a tile's windows: min | max << 16
-  static_assert(SL_TILES <= SL_MEMB, "tile windows in the member table's space");
   int bad = 0;  // err bits this lane saw
   if constexpr (NOV) {
     // strictly increasing: lane neighbours inside a tile; a tile's first PC against the PC before it
@@ -226,16 +224,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       }
     }
   }
-  if (dbg & 16) {  // timing only: the loads alone
-    uint32_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < TPW; k++) acc += v[k];
-    if (acc == 0x9E3779B9u) err[1] = 1;
-    return;
-  }
   // from here on v holds the PC's offset from lo: window = v >> S, offset in it = v & omask
-  // window histogram
-  const uint32_t DUMMY = WMAX + 1 + lane;
+  // window histogram (lanes outside the tile count into a dummy slot of their own)
+  const uint32_t DUMMY = W + 1 + lane;
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
     const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, k);
@@ -243,11 +234,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     v[k] -= lo;
     const uint32_t w = v[k] >> S;
     const bool in = lane < cnt;
-    if (SYZ_SL_SKIP) {  // the tile's window range (min and max over its lanes: covers may be unsorted)
-      const uint32_t wc = in ? min(w, 0xFFFFu) : 0xFFFFu;
-      const uint32_t wlo = wave_min(wc), whi = (uint32_t)wave_incl_max(in ? (int32_t)min(w, 0xFFFFu) : -1);
-      if (lane == 63) trng[wv + WAVES * k] = wlo | (min(whi, 0xFFFFu) << 16);
-    }
     // outside the windows: an unsorted cover (Minimize: redone on exact bounds; NOV: out of order)
     bad |= (in && w >= W) ? (NOV ? ((z & 0x100u) ? 1 : 4) : 1) : 0;
     atomicAdd(&hist[in && w < W ? w : DUMMY], 1u);
@@ -266,7 +252,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   if (wtot)
     for (uint32_t i = threadIdx.x; i < W; i += BLOCK)
       if (hist[i]) atomicAdd(&wtot[gp.wbase + i], hist[i]);
-  // window starts -> cursors, D rows, pass boundaries
+  // padded window starts -> cursors (hist), pst, D rows
   uint32_t total;
   {
     uint32_t run = 0;
@@ -279,6 +265,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       const uint32_t pre = block_excl_scan<BLOCK>(x, red, &tot) + run;
       if (i <= W) {
         hist[i] = pre;
+        pst[i] = pre;
         D[dcol + (uint64_t)i * gp.stride] = erel + pre;
       }
       run += tot;
@@ -286,96 +273,63 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     total = run;
   }
   __syncthreads();
-  // pw[k] = first window i with wst[i] >= k * BUF (window i's start is hist[i] now; hist[W] = total):
-  // the i with wst[i - 1] < k * BUF <= wst[i]
-  for (uint32_t i = threadIdx.x; i <= W; i += BLOCK) {
-    const uint32_t s1 = hist[i];
-    const uint32_t k1 = s1 >> SL_BUF_BITS;
-    const uint32_t k0 = i ? (hist[i - 1] >> SL_BUF_BITS) + 1u : 0u;
-    for (uint32_t k = k0; k <= k1 && k < SL_PMAX + 2; k++) pw[k] = i;
-  }
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k <= SL_PMAX; k += BLOCK) pa[k] = pw[k] < W ? hist[pw[k]] : total;
-  if (dbg & 32) return;  // timing only: loads, histogram, scan
-  __syncthreads();
-  const uint32_t npass = (total + SL_BUF - 1) >> SL_BUF_BITS;
+  // each element's place from its window's cursor (lanes outside the tile or the windows issue nothing)
   const uint32_t omask = (1u << S) - 1;
-  uint32_t* gel = elems + sl.elem;
-  for (uint32_t k = 0; k < npass; k++) {
-    const uint32_t wl = pw[k], wh = pw[k + 1];
-    const uint32_t base = k << SL_BUF_BITS, lim = base + SL_BUF;
-    const uint32_t a0 = pa[k];  // the pass's first element: window wl's start
-    // the buffer's padding slots (a run's last vector) hold the no-element value
-    {
-      uint4* o4 = reinterpret_cast<uint4*>(obuf);
-      const uint4 none4 = make_uint4(SL_NONE, SL_NONE, SL_NONE, SL_NONE);
-      for (uint32_t i = threadIdx.x; i < SL_BUF / 4; i += BLOCK) o4[i] = none4;
-    }
-    __syncthreads();
-    // opaque per pass, so the compiler does not hoist 64 tiles' elements out of the pass loop (VGPRs)
-    uint32_t Sp = S, om = omask;
-    asm volatile("" : "+s"(Sp), "+s"(om));
+  {
     constexpr int PB = 8;
 #pragma unroll
     for (int k0 = 0; k0 < TPW; k0 += PB) {
-      if (SYZ_SL_SKIP) {  // a group of tiles with no window in this pass is skipped whole
-        bool any = false;
-#pragma unroll
-        for (int q = 0; q < PB; q++) {
-          const uint32_t r = (uint32_t)__builtin_amdgcn_readfirstlane((int)trng[wv + WAVES * (k0 + q)]);
-          any |= (r >> 16) >= wl && (r & 0xFFFFu) < wh && (r & 0xFFFFu) <= (r >> 16);
-        }
-        if (!any) continue;  // wave-uniform
-      }
       uint32_t pos[PB], el[PB];
       bool ok[PB];
 #pragma unroll
-        for (int q = 0; q < PB; q++) {
-          const int kk = k0 + q;
-          const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, kk);
-          const uint32_t d = v[kk], w = d >> Sp;
-          ok[q] = lane < (z & 0x7Fu) && (w - wl) < (wh - wl);
-          el[q] = (d & om) | ((z >> 9) << Sp);
-          pos[q] = 0;
-          if (ok[q]) pos[q] = atomicAdd(&hist[w], 1u);  // lanes outside the pass issue nothing
-        }
-#pragma unroll
       for (int q = 0; q < PB; q++) {
-        if (ok[q]) {
-          if (pos[q] < lim)
-            obuf[pos[q] - base] = el[q];
-          else
-            gel[pos[q]] = el[q];  // a window running past the buffer
-        }
+        const int kk = k0 + q;
+        const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)cz, kk);
+        const uint32_t d = v[kk], w = d >> S;
+        ok[q] = lane < (z & 0x7Fu) && w < W;
+        el[q] = (d & omask) | ((z >> 9) << S);
+        pos[q] = 0;
+        if (ok[q]) pos[q] = atomicAdd(&hist[w], 1u);
       }
-    }
-    __syncthreads();
-    // a last window running past the buffer: its padding slots are stored directly
-    if (wh > wl && threadIdx.x < 3) {
-      const uint32_t e = hist[wh - 1] + threadIdx.x;
-      if (e >= lim && (e & 3u)) gel[e] = SL_NONE;
-    }
-    // the pass leaves as [a0, e0): hist[wh - 1] is the end of its last window now (+ its padding)
-    const uint32_t e0 = wh > wl ? min((hist[wh - 1] + 3u) & ~3u, lim) : a0;
-    if (e0 > a0) {
-      const uint64_t A = sl.elem + a0, E = sl.elem + e0;
-      const uint64_t q0 = A >> 2, q1 = (E + 3) >> 2;
-      uint4* g4 = reinterpret_cast<uint4*>(elems);
-      for (uint64_t q = q0 + threadIdx.x; q < q1; q += BLOCK) {
-        const uint64_t e = q << 2;
-        const uint32_t lb = (uint32_t)(e - sl.elem) - base;  // LDS index of the vector's first element
-        if (e >= A && e + 4 <= E) {
-          g4[q] = *reinterpret_cast<const uint4*>(&obuf[lb]);
-        } else {
 #pragma unroll
-          for (int u = 0; u < 4; u++)
-            if (e + u >= A && e + u < E) elems[e + u] = obuf[lb + u];
-        }
-      }
+      for (int q = 0; q < PB; q++)
+        if (ok[q]) obuf[pos[q]] = el[q];
     }
-    __syncthreads();
   }
-  }  // slabs
+  __syncthreads();
+  // the padding slots of each run hold the no-element value: [cursor, next padded start)
+  for (uint32_t i = threadIdx.x; i < W; i += BLOCK)
+    for (uint32_t e = hist[i]; e < pst[i + 1]; e++) obuf[e] = SL_NONE;
+  __syncthreads();
+  // the slab leaves as one run of 16-byte stores (sl.elem and total are multiples of 4)
+  {
+    uint4* g4 = reinterpret_cast<uint4*>(elems + sl.elem);
+    const uint4* o4 = reinterpret_cast<const uint4*>(obuf);
+    for (uint32_t q = threadIdx.x; q < total / 4; q += BLOCK) g4[q] = o4[q];
+  }
+}
+
+// P's launch: one workgroup per slab (a bound; slabs past nslab return), the staging sized for the
+// launch's widest call (the attribute raised once per instantiation for the largest size asked)
+template <bool NOV>
+inline void launch_slab(uint64_t nslabs, uint32_t Wmax, hipStream_t s, const uint32_t* pcs, const uint64_t* off,
+                        const uint32_t* members, const uint32_t* mlen, const uint64_t* tpos, const uint32_t* sbeg,
+                        const PSlab* slabs, const uint64_t* nslab, const SGroup* sg, const uint64_t* gebase,
+                        uint32_t lo, uint32_t* elems, uint32_t* D, int* err, uint32_t* wtot, NovSrc ns, int cls) {
+  if (!nslabs) return;
+  const size_t bytes = slab_lds_bytes(Wmax);
+  static std::atomic<size_t> raised{0};
+  if (bytes > raised.load()) {
+    SYZ_HIP(hipFuncSetAttribute((const void*)k_slab<SL_BLOCK, SL_TPW, NOV>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    size_t cur = raised.load();
+    while (bytes > cur && !raised.compare_exchange_weak(cur, bytes)) {
+    }
+  }
+  k_slab<SL_BLOCK, SL_TPW, NOV><<<(unsigned)nslabs, SL_BLOCK, bytes, s>>>(pcs, off, members, mlen, tpos, sbeg, slabs,
+                                                                         nslab, sg, gebase, lo, elems, D, err, Wmax,
+                                                                         wtot, ns, cls);
+  SYZ_LAUNCHED();
 }
 
 // ---- M walk over a window's slab runs ---------------------------------------------------------------

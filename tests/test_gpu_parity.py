@@ -236,6 +236,45 @@ def test_canonicalize_batch_dev_classes_vs_oracle():
         assert np.array_equal(work[int(off[i]):int(off[i]) + int(lens[i])], want), i
 
 
+def test_canonicalize_batch_dev_canonical_fast_path_vs_oracle():
+    # covers that are canonical already (the executor's dedup on) skip the sort: sorted + unique of
+    # every length class, the sentinel alone (-> empty) or last (kept), empty covers; mixed with covers
+    # that are one step from canonical (a repeat or an inversion at the very end of a long sorted run,
+    # or at the start) and must take the full path
+    import torch
+    rnd = np.random.default_rng(29)
+    S = 0xFFFFFFFF
+    covs = []
+    for sz in [0, 1, 2, 63, 64, 65, 255, 256, 257, 1000, 1024, 5000, 16384, 20000, 40000]:
+        base = np.sort(rnd.choice(1 << 31, size=sz, replace=False)).astype(np.uint32)
+        covs.append(base)
+        if sz >= 2:
+            rep = base.copy()
+            rep[-1] = rep[-2]                       # a repeat at the end
+            covs.append(rep)
+            inv = base.copy()
+            inv[-2], inv[-1] = inv[-1], inv[-2]     # an inversion at the end
+            covs.append(inv)
+            head = base.copy()
+            head[0], head[1] = head[1], head[0]     # an inversion at the start
+            covs.append(head)
+    covs += [np.array([S], np.uint32), np.array([7, S], np.uint32), np.array([S, S], np.uint32),
+             np.array([3, 9, S], np.uint32), np.zeros(0, np.uint32)]
+    covs += [np.sort(rnd.choice(1 << 20, size=int(k), replace=False)).astype(np.uint32)
+             for k in rnd.integers(1, 3000, size=200)]
+    pcs, off = cover.to_csr(covs)
+    d_pcs = torch.from_numpy(pcs.view(np.int32).copy()).to("cuda:0")
+    d_off = torch.from_numpy(off.view(np.int64).copy()).to("cuda:0")
+    d_len = torch.zeros(len(covs), dtype=torch.int64, device="cuda:0")
+    cover.CanonicalizeBatchDev(d_pcs, d_off, len(covs), d_len)
+    work = d_pcs.cpu().numpy().view(np.uint32)
+    lens = d_len.cpu().numpy()
+    for i, c in enumerate(covs):
+        want = oracle.canonicalize(c)
+        assert int(lens[i]) == want.size, i
+        assert np.array_equal(work[int(off[i]):int(off[i]) + int(lens[i])], want), i
+
+
 # ---- Minimize -----------------------------------------------------------------------------------------
 @pytest.mark.parametrize("seed", range(4))
 def test_minimize_random_property(seed):

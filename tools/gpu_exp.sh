@@ -14,8 +14,8 @@ for E in "$@"; do
   LIB=$GRAFT_REPO_ROOT/syzkaller_amd/libsyzgpu.so; [ "$LT" != "base" ] && LIB=$GRAFT_REPO_ROOT/syzkaller_amd/libsyzgpu_$LT.so
   for ser in 1 0; do
     echo "== $i [$E] serial=$ser" >> $OUT/pm.log
-    env SYZGPU_LIB=$LIB $ENVS SYZGPU_PM_SERIAL=$ser timeout -k 10 150 python3 tools/pm_time.py > $OUT/pm$i_$ser.log 2>&1
-    rc=$?; grep step_ms $OUT/pm$i_$ser.log | cut -c1-600 >> $OUT/pm.log; [ $rc -eq 0 ] || { tail -5 $OUT/pm$i_$ser.log; exit $rc; }
+    env SYZGPU_LIB=$LIB $ENVS SYZGPU_PM_SERIAL=$ser timeout -k 10 150 python3 tools/pm_time.py > $OUT/pm${i}_${ser}.log 2>&1
+    rc=$?; grep step_ms $OUT/pm${i}_${ser}.log | cut -c1-600 >> $OUT/pm.log; [ $rc -eq 0 ] || { tail -5 $OUT/pm${i}_${ser}.log; exit $rc; }
   done
 done
 cat $OUT/pm.log
