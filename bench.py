@@ -381,7 +381,7 @@ def main():
         nov = novelty_leg(args, dev, L, read_prof) if args.novelty and solo else None
         cooc = cooccurrence_leg(args, dev, L, read_prof, corp, C) if args.cooccurrence and solo else None
         sops = setops_leg(args, dev, L, read_prof) if args.setops and solo else None
-        canon = canonicalize_leg(args, dev, L) if args.canonicalize and solo else None
+        canon = canonicalize_leg(args, dev, L, read_prof) if args.canonicalize and solo else None
         hubr = hub_leg(args, dev, L, read_prof, corp, sptr) if args.hub and solo else None
         ana = analytics_leg(args, dev, L, read_prof, store, corp, sptr) if args.analytics and solo else None
         app = append_leg(args, dev, store, sptr, C, d_hist) if args.append and solo else None  # last: replaces
@@ -923,7 +923,7 @@ def novelty_leg(args, dev, L, read_prof):
     return res
 
 
-def canonicalize_leg(args, dev, L):
+def canonicalize_leg(args, dev, L, read_prof=None):
     """cover.Canonicalize over a batch (cover/cover.go:28-40; its caller syz-fuzzer/fuzzer.go:355 runs it
     on every input's cover): config 3's 1M fresh covers as kcov returns them when the executor's
     dedup flag is off (executor.cc:565-585), each cover's PCs in random order with ~20 % of them
@@ -987,9 +987,18 @@ def canonicalize_leg(args, dev, L):
             tot2 += time.perf_counter() - t0
     ms2 = tot2 / steps * 1e3
     ok2 = bool(torch.equal(work2, canon)) and int(out_len.sum().item()) == int(c.off[-1])
+    kms2 = None
+    if read_prof is not None:  # one more pass with HIP events around the phases (not timed)
+        L.syzgpu_profile_only(None)
+        L.syzgpu_profile_enable(1)
+        work2.copy_(canon)
+        cover.CanonicalizeBatchDev(work2, coff, n, out_len, sptr)
+        kms2 = {k: round(e["ms"], 4) for k, e in read_prof().items()}
+        L.syzgpu_profile_enable(0)
     alg2 = 4 * int(c.off[-1]) + 8 * (n + 1) + 8 * n  # the PCs and offsets read, the lengths written
     res["sorted"] = {"workload": "the same 1M covers already canonical (executor dedup on): %d PCs" % int(c.off[-1]),
                      "ms_per_batch": round(ms2, 3), "covers_per_s": round(n / ms2 * 1e3, 1), "unchanged": ok2,
+                     "phases_ms": kms2,
                      "roofline": {"bound": "hbm", "achieved": round(alg2 / (ms2 * 1e-3) / 1e9, 1),
                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(alg2 / (ms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

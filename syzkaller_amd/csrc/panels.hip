@@ -162,176 +162,15 @@ __device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t 
 }
 
 
-// Dense windows: a 2^DS-entry direct min table in LDS (128 KB: one workgroup per CU), the window's
-// regions streamed (panels_dev.hpp for_region), then the winners as byte stores.
-#ifndef SYZ_RG_U
-#define SYZ_RG_U 2
-#endif
 // The direct table's index: the offset rotated right by 2 bits inside the window, so PCs on 4-byte
 // instruction boundaries (arm64, and the synthetic corpora) fill every LDS bank, not a quarter of them
 __device__ __forceinline__ uint32_t tab_index(uint32_t o) { return ((o >> 2) | (o << (DS - 2))) & ((1u << DS) - 1); }
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_pmin_direct(const PItem* items, const PGroup* pg, const uint64_t* rstart, const uint32_t* rtot,
-                                                      const uint32_t* elems,
-                                                      const uint32_t* __restrict__ rank_of_member,
-                                                      const uint64_t* gstart, uint8_t* sel8, int dbg) {
-  __shared__ __align__(16) uint32_t tab[1u << DS];
-  __shared__ uint32_t bm[PK_SCRATCH_WORDS];
-  const PItem it = items[blockIdx.x];
-  {
-    uint4* t4 = reinterpret_cast<uint4*>(tab);
-    const uint4 none4 = make_uint4(RANK_NONE, RANK_NONE, RANK_NONE, RANK_NONE);
-    for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
-  }
-  __syncthreads();
-  if (dbg & 1) {  // timing only: the walk without its table updates
-    uint32_t acc = 0;
-    for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, rtot, elems, rank_of_member,
-                                [&](uint32_t o, uint32_t R) { acc += o ^ R; });
-    if (acc == 0x9E3779B9u) sel8[0] = 1;
-  } else if (dbg & 8) {  // timing only: no rank gathers
-    for_region<SYZ_RG_U, true>(it, pg, gstart, rstart, rtot, elems, nullptr,
-                               [&](uint32_t o, uint32_t R) {
-                                      // a plain read first: most elements of a PC held by many inputs lose
-                                      // to the rank already there, and same-address reads broadcast where
-                                      // atomics serialize
-                                      uint32_t* t = &tab[tab_index(o)];
-                                      if (*t > R) atomicMin(t, R);
-                                    });
-  } else {
-    for_region<SYZ_RG_U, false>(it, pg, gstart, rstart, rtot, elems, rank_of_member,
-                                [&](uint32_t o, uint32_t R) {
-                                      // a plain read first: most elements of a PC held by many inputs lose
-                                      // to the rank already there, and same-address reads broadcast where
-                                      // atomics serialize
-                                      uint32_t* t = &tab[tab_index(o)];
-                                      if (*t > R) atomicMin(t, R);
-                                    });
-  }
-  __syncthreads();
-  if (dbg & 2) return;
-  const uint64_t gb = gstart[it.g];
-  emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, bm, sel8);
-}
-
-// PCs of one (call, window): the lengths of its segments' regions
-__device__ __forceinline__ uint32_t window_elem_count(const PItem it, const PGroup* pg, const uint64_t* gstart,
-                                                     const uint32_t* rtot) {
-  const PGroup p = pg[it.g];
-  const uint32_t sb = 32 - p.S;
-  const uint64_t ng = gstart[it.g + 1] - gstart[it.g];
-  const uint32_t nseg = (uint32_t)((ng + (1ull << sb) - 1) >> sb);
-  uint64_t e = 0;
-  for (uint32_t s = 0; s < nseg; s++) {
-    const uint32_t r = p.rb + s * p.W + it.w;
-    e += rtot[r];
-  }
-  return (uint32_t)e;
-}
-
 __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - HS_BITS); }
 
-// Sparse windows: open addressing keyed by the window offset, kept at most half full: a window with
-// more than HCAP PCs is done in R = ceil(PCs / HCAP) rounds, each taking the keys of one residue of
-// another hash (so each round holds at most about HCAP distinct keys). A probe run longer than
-// HPROBE means the table is full after all: every round is redone with twice as many; a winner
-// marked by a finished round stays valid (marks are idempotent stores of exact winners).
-// 72 KB of LDS at 8192 slots: two workgroups per CU (registers held to 64 per lane, 4 runs in
-// flight per wave), so one window's table init and emit overlap the other's loads
-#ifndef SYZ_PK_HU
-#define SYZ_PK_HU 1
-#endif
-// Sparse windows: open addressing keyed by the window offset, kept at most half full: a window with
-// more than HCAP PCs is done in R = ceil(PCs / HCAP) rounds, each taking the keys of one residue of
-// another hash (so each round holds at most about HCAP distinct keys). A probe run longer than
-// HPROBE means the table is full after all: every round is redone with twice as many; a winner
-// marked by a finished round stays valid (marks are idempotent stores of exact winners).
-// PACKED (call groups of < 2^13 entries, windows of <= 2^19 addresses): a slot is one u32,
-// offset << 13 | rank - the group's first rank, inserted by CAS and lowered by atomicMin (equal high
-// bits, so the min is the min rank), 16K slots in the 64 KB of the 8K key/value pairs.
-template <bool PACKED>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pmin_hash(const PItem* items, const PGroup* pg, const uint64_t* rstart, const uint32_t* rtot,
-                                                    const uint32_t* elems,
-                                                    const uint32_t* __restrict__ rank_of_member,
-                                                    const uint64_t* gstart, uint8_t* sel8, int dbg) {
-  constexpr uint32_t NS = PACKED ? PHS : HS;  // slots
-  constexpr uint32_t CAP = PACKED ? PHCAP : HCAP;
-  __shared__ uint32_t tabs[2 * HS];
-  static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
-  __shared__ __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];  // the emit bitmap
-  __shared__ int full;
-  uint32_t* keys = tabs;       // PACKED: the slots
-  uint32_t* vals = tabs + HS;
-  const PItem it = items[blockIdx.x];
-  const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
-  const uint32_t E = window_elem_count(it, pg, gstart, rtot);
-  if (E == 0) return;
-  uint32_t R = (E + CAP - 1) / CAP;
-  for (uint32_t round = 0; round < R;) {
-    for (uint32_t i = threadIdx.x; i < 2 * HS; i += 1024) tabs[i] = (PACKED || i < HS) ? 0xFFFFFFFFu : RANK_NONE;
-    if (threadIdx.x == 0) full = 0;
-    __syncthreads();
-    const uint32_t RR = R, rr = round;
-    uint32_t acc = 0;
-    for_region<SYZ_PK_HU, false>(it, pg, gstart, rstart, rtot, elems, rank_of_member, [&](uint32_t o, uint32_t Rk) {
-                                         if (Rk == RANK_NONE) return;  // a lane past the window
-                                         if (dbg & 64) {
-                                           acc ^= o * 31 + Rk;
-                                           return;
-                                         }
-                                         if (RR > 1 && (hash32(o) >> 5) % RR != rr) return;
-                                         if constexpr (PACKED) {
-                                           const uint32_t pk = (o << PK_RBITS) | (uint32_t)(Rk - gb);
-                                           uint32_t h = (o * 0x9E3779B1u) >> (32 - PHS_BITS);
-                                           for (uint32_t probes = 0; probes < HPROBE; probes++) {
-                                             uint32_t k = keys[h];
-                                             if (k == 0xFFFFFFFFu) {
-                                               k = atomicCAS(&keys[h], 0xFFFFFFFFu, pk);
-                                               if (k == 0xFFFFFFFFu) return;
-                                             }
-                                             if ((k >> PK_RBITS) == o) {
-                                               if (k > pk) atomicMin(&keys[h], pk);
-                                               return;
-                                             }
-                                             h = (h + 1) & (PHS - 1);
-                                           }
-                                         } else {
-                                           uint32_t h = hslot(o);
-                                           for (uint32_t probes = 0; probes < HPROBE; probes++) {
-                                             uint32_t k = keys[h];
-                                             if (k == 0xFFFFFFFFu) {
-                                               k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
-                                               if (k == 0xFFFFFFFFu) k = o;
-                                             }
-                                             if (k == o) {
-                                               if (vals[h] > Rk) atomicMin(&vals[h], Rk);
-                                               return;
-                                             }
-                                             h = (h + 1) & (HS - 1);
-                                           }
-                                         }
-                                         full = 1;
-                                       });
-    if (acc == 0x9E3779B9u) sel8[0] = 1;
-    __syncthreads();
-    if (full) {
-      R *= 2;
-      round = 0;
-      __syncthreads();
-      continue;
-    }
-    if constexpr (PACKED) {
-      const uint32_t g32 = (uint32_t)gb;  // ranks fit 32 bits (n < 2^32)
-      emit_winner_bytes<PK_SCRATCH_WORDS>(keys, NS, gb, ng, wsc, sel8, [g32](uint32_t v) {
-        return v == 0xFFFFFFFFu ? RANK_NONE : g32 + (v & ((1u << PK_RBITS) - 1));
-      });
-    } else {
-      emit_winner_bytes<PK_SCRATCH_WORDS>(vals, HS, gb, ng, wsc, sel8);
-    }
-    round++;
-  }
-}
-
 // ---- M over slab runs (slab_dev.hpp): the same tables, the window's runs from every slab --------------
+#ifndef SYZ_SMIN_NOEMIT
+#define SYZ_SMIN_NOEMIT 0  // timing experiment only (results wrong when 1)
+#endif
 #ifndef SYZ_SMIN_NOF
 #define SYZ_SMIN_NOF 0  // timing experiment only (results wrong when 1)
 #endif
@@ -350,12 +189,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #endif
 // LDS of one M workgroup: the window's table (direct: 2^DS u32; hashed: keys + values or packed slots),
 // the walk's scratch (then the emit bitmap) and reductions
-struct SminLds {
-  __align__(16) uint32_t tabs[(1u << DS) > 2 * HS ? (1u << DS) : 2 * HS];
-  __align__(16) uint32_t wsc[PK_SCRATCH_WORDS];
-  uint64_t red64[1024 / 64 + 1];
+template <int BLOCK, uint32_t TWORDS>
+struct SminLdsT {
+  __align__(16) uint32_t tabs[TWORDS];
+  __align__(16) uint32_t wsc[2 * BLOCK + 3 * PK_NBLK];
+  uint64_t red64[BLOCK / 64 + 1];
   int full;
+  static constexpr uint32_t WSC = 2 * BLOCK + 3 * PK_NBLK;
 };
+using SminLds = SminLdsT<1024, ((1u << DS) > 2 * HS ? (1u << DS) : 2 * HS)>;
+using SminPkLds = SminLdsT<PK_BLOCK, PHS>;  // packed windows: their slots only
 static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
 
 __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, const uint32_t* gslab,
@@ -383,6 +226,7 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
                                       if (*t > R) atomicMin(t, R);
                                     });
   __syncthreads();
+  if (SYZ_SMIN_NOEMIT) return;  // timing only
   const uint64_t gb = gstart[it.g];
   emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, L.wsc, sel8);
 }
@@ -390,23 +234,24 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
 #ifndef SYZ_SL_HU
 #define SYZ_SL_HU 1
 #endif
-template <bool PACKED>
+template <bool PACKED, int BLOCK, class LT>
 __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, const uint32_t* gslab,
                                           const uint64_t* gebase, const uint32_t* D, const PSlab* slabs,
                                           const uint32_t* __restrict__ elems,
                                           const uint32_t* __restrict__ rank_of_member, const uint64_t* gstart,
-                                          uint8_t* sel8, SminLds& L) {
+                                          uint8_t* sel8, LT& L) {
   constexpr uint32_t NS = PACKED ? PHS : HS;  // slots
   constexpr uint32_t CAP = PACKED ? PHCAP : HCAP;
+  constexpr uint32_t TW = PACKED ? PHS : 2 * HS;  // table words
   uint32_t* tabs = L.tabs;
   uint32_t* keys = tabs;  // PACKED: the slots
   uint32_t* vals = tabs + HS;
   const uint64_t gb = gstart[it.g], ng = gstart[it.g + 1] - gb;
-  const uint32_t E = slab_window_count<1024>(it, sg, gslab, D, reinterpret_cast<uint32_t*>(L.red64));
+  const uint32_t E = slab_window_count<BLOCK>(it, sg, gslab, D, reinterpret_cast<uint32_t*>(L.red64));
   if (E == 0) return;
   uint32_t R = (E + CAP - 1) / CAP;
   for (uint32_t round = 0; round < R;) {
-    for (uint32_t i = threadIdx.x; i < 2 * HS; i += 1024) tabs[i] = (PACKED || i < HS) ? 0xFFFFFFFFu : RANK_NONE;
+    for (uint32_t i = threadIdx.x; i < TW; i += BLOCK) tabs[i] = (PACKED || i < HS) ? 0xFFFFFFFFu : RANK_NONE;
     if (threadIdx.x == 0) L.full = 0;
     __syncthreads();
     const uint32_t RR = R, rr = round;
@@ -457,13 +302,18 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
       __syncthreads();
       continue;
     }
+    if (SYZ_SMIN_NOEMIT) {  // timing only
+      round++;
+      __syncthreads();
+      continue;
+    }
     if constexpr (PACKED) {
       const uint32_t g32 = (uint32_t)gb;
-      emit_winner_bytes<PK_SCRATCH_WORDS>(keys, NS, gb, ng, L.wsc, sel8, [g32](uint32_t v) {
+      emit_winner_bytes<LT::WSC>(keys, NS, gb, ng, L.wsc, sel8, [g32](uint32_t v) {
         return v == 0xFFFFFFFFu ? RANK_NONE : g32 + (v & ((1u << PK_RBITS) - 1));
       });
     } else {
-      emit_winner_bytes<PK_SCRATCH_WORDS>(vals, HS, gb, ng, L.wsc, sel8);
+      emit_winner_bytes<LT::WSC>(vals, HS, gb, ng, L.wsc, sel8);
     }
     round++;
     __syncthreads();  // the emit's bitmap and table reads are done before the next round clears them
@@ -481,13 +331,19 @@ __global__ __launch_bounds__(1024) SYZ_SMIN_OCC void k_smin_direct(const PItem* 
 }
 
 // (one launch for a class's three table kinds measured no better and spills: M is throughput-bound)
+// PACKED: PK_BLOCK threads with a PHS-slot table (SminPkLds); otherwise 1024 threads, keys + values
 template <bool PACKED>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_smin_hash(
+__global__ __launch_bounds__(PACKED ? PK_BLOCK : 1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_smin_hash(
     const PItem* items, const SGroup* sg, const uint32_t* gslab, const uint64_t* gebase, const uint32_t* D,
     const PSlab* slabs, const uint32_t* __restrict__ elems, const uint32_t* __restrict__ rank_of_member,
     const uint64_t* gstart, uint8_t* sel8) {
-  __shared__ SminLds L;
-  smin_hash<PACKED>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, sel8, L);
+  if constexpr (PACKED) {
+    __shared__ SminPkLds L;
+    smin_hash<true, PK_BLOCK>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, sel8, L);
+  } else {
+    __shared__ SminLds L;
+    smin_hash<false, 1024>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, sel8, L);
+  }
 }
 
 // ---- outputs: the group-major kept list in selection order ----------------------------------------
@@ -584,28 +440,12 @@ void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, u
 
 static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span);
 
-// diagnostic switches (SYZGPU_PM_DBG, timing experiments only; results are wrong when set):
-// 1 = direct walk without table updates, 2 = no winner emit (direct windows), 4 = no open-addressing
-// windows, 8 = direct walk without rank gathers, 64 = sparse windows walked but
-// not probed
-
 static bool pm_serial() {
   static const bool v = getenv("SYZGPU_PM_SERIAL") && atoi(getenv("SYZGPU_PM_SERIAL")) != 0;
   return v || (prof().on && prof().serial);
 }
 
-// SYZGPU_RG_DBG (timing only, results wrong): 16 = P loads only, 32 = scatter without pass 2, 64 = no stores
-static int rg_dbg() {
-  static const int v = getenv("SYZGPU_RG_DBG") ? atoi(getenv("SYZGPU_RG_DBG")) : 0;
-  return v;
-}
 
-// SYZGPU_PM_BATCHES: batches of call groups the raw pipeline is cut into (default 1: more batches
-// were measured slower, the overlapping passes compete for the same CUs and slow the Go sort)
-static uint32_t pm_batches() {
-  static const uint32_t v = getenv("SYZGPU_PM_BATCHES") ? (uint32_t)std::max(1, atoi(getenv("SYZGPU_PM_BATCHES"))) : 1u;
-  return v;
-}
 
 // SYZGPU_PM_PSPLIT=1 (A/B): P as two launches, the small call groups' slabs first, so their M starts
 // beside the big groups' slabs (measured slower: the big groups' LDS sort then waits for CUs behind
@@ -615,15 +455,7 @@ static bool pm_psplit() {
   return v;
 }
 
-static bool pm_p2() {
-  static const bool v = getenv("SYZGPU_PM_P2") && atoi(getenv("SYZGPU_PM_P2")) != 0;
-  return v;
-}
 
-static int pm_dbg() {
-  static const int v = getenv("SYZGPU_PM_DBG") ? atoi(getenv("SYZGPU_PM_DBG")) : 0;
-  return v;
-}
 
 void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* hpcs, const std::vector<PGroup>& hpg,
                uint32_t G, bool want_wtot) {
@@ -703,11 +535,6 @@ void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint
   SYZ_LAUNCHED();
 }
 
-// SYZGPU_PM_REGION=1 (A/B): round 3's region form (count pass, column scan, scatter) instead of slabs
-static bool pm_region() {
-  static const bool v = getenv("SYZGPU_PM_REGION") && atoi(getenv("SYZGPU_PM_REGION")) != 0;
-  return v;
-}
 
 // The slab form (slab_dev.hpp): one read of the covers. Inputs from begin_once's common part: the
 // group partition (members, el, mlen, mpos), the per-group PC counts and read slices, the windows.
@@ -885,7 +712,7 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     }
     if (np) {
       ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
-      k_smin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
+      k_smin_hash<true><<<(unsigned)np, PK_BLOCK, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
                                                        elems, rank_of_member, gstart, sel8);
       SYZ_LAUNCHED();
     }
@@ -976,7 +803,6 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint64_t* gstart = J.gstart.p;
   uint32_t* rank_of_member = J.rank_of_member.p;
   uint32_t* ent_of_rank = J.ent_of_rank.p;
-  uint8_t* sel8 = J.sel8.p;
   // ---- group partition (stable), sort keys, per-group PCs, span, member slices and offsets ----
   uint32_t* members = sc.get<uint32_t>("mz_members", n + 1);
   uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
@@ -1004,17 +830,24 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   }
   {
     ProfScope ps("group_partition", s, (uint64_t)n * 28);
-    group_partition_dev(a.group, a.off, n, G, gstart, members, el, err, s);
+    // the span pass reads only the covers: on the side stream, beside the partition
+    ensure_side(c);
     if (n) {
+      SYZ_HIP(hipEventRecord(c.ev_fork, s));
+      SYZ_HIP(hipStreamWaitEvent(c.side, c.ev_fork, 0));
       // whole covers: the per-group PCs are the member prefix's group differences (k_gpack), so the
       // span pass takes no per-group atomics (a wider grid measured slower: its span atomics)
       if (krange)
-        k_span_sums<<<grid_for(n, 256, span_blocks()), 256, G * 8, s>>>(a.pcs, a.off, a.group, n, G, gpcs, span,
-                                                                            mlmax);
+        k_span_sums<<<grid_for(n, 256, span_blocks()), 256, G * 8, c.side>>>(a.pcs, a.off, a.group, n, G, gpcs, span,
+                                                                                 mlmax);
       else
-        k_span_sums<<<grid_for(n, 256, span_blocks()), 256, 0, s>>>(a.pcs, a.off, a.group, n, G, nullptr, span,
-                                                                       mlmax);
+        k_span_sums<<<grid_for(n, 256, span_blocks()), 256, 0, c.side>>>(a.pcs, a.off, a.group, n, G, nullptr, span,
+                                                                            mlmax);
       SYZ_LAUNCHED();
+      SYZ_HIP(hipEventRecord(c.ev_join, c.side));
+    }
+    group_partition_dev(a.group, a.off, n, G, gstart, members, el, err, s);
+    if (n) {
       if (krange)
         k_slices<<<grid_for(n, 256, 4096), 256, 0, s>>>(a.pcs, a.off, members, el, a.group, n, krange, sbeg, mlen);
       else
@@ -1022,6 +855,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       SYZ_LAUNCHED();
     }
     exclusive_scan_u32(mlen, mpos, n, s);
+    if (n) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
     k_gpack<<<grid_for(3 * (size_t)G + 4, 256, 64), 256, 0, s>>>(gstart, gpcs, span, err, mpos, G, mlmax, gpack);
     SYZ_LAUNCHED();
   }
@@ -1029,7 +863,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_HIP(hipMemcpyAsync(hbuf, gpack, (3 * (size_t)G + 4) * 8, hipMemcpyDeviceToHost, s));
   // work that needs no plan runs while the host plans: identity ranks, the slab tiles' prefix
   rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
-  if (!pm_region()) slab_tiles(mlen, n, "pm", s);
+  slab_tiles(mlen, n, "pm", s);
   HostTimer ht("begin");
   stream_wait_spin(s);
   ht.mark("wait_partition");
@@ -1050,283 +884,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   std::vector<PGroup> hpg;
   plan_windows(spanw, hpcs.data(), hstart.data(), G, hpg);
   ht.mark("plan_windows");
-  if (!pm_region())
-    return begin_slab(J, a, hstart, hpcs, hsl, hpg, lo, hi, exact_span, members, el, mlen, mpos, sbeg, err);
-  std::vector<uint32_t> hgblock(G + 1, 0), hbgroup;
-  std::vector<uint64_t> hgel(G + 1, 0), hcb(G, 0);  // a group's first element; its chunk bound
-  std::vector<size_t> hcolg(G + 1, 0);              // a group's first column-scan item
-  uint64_t chunk_bound = 0, total_pcs = 0, nreg = 0, desc_bound = 0;
-  std::vector<ColItem> hcol;  // column-scan items: (group, segment, 64 windows)
-  for (uint32_t g = 0; g < G; g++) {
-    const uint64_t ng = hstart[g + 1] - hstart[g];
-    const uint32_t nb = (uint32_t)((ng + MEMB - 1) / MEMB);
-    hgblock[g + 1] = hgblock[g] + nb;
-    hbgroup.insert(hbgroup.end(), nb, g);
-    const uint64_t cb = nb + (hpcs[g] + PCAP - 1) / PCAP;  // a key part holds at most the whole group
-    hcb[g] = cb;
-    chunk_bound += cb;
-    desc_bound += cb * (hpg[g].W + 1);
-    hgel[g] = total_pcs;
-    total_pcs += hsl[g];
-    // regions: one per (member segment, window); a group's PCs must fit 32-bit places
-    if (hpcs[g] >= (1ull << 32)) fail(SYZGPU_EINVAL, "a call group with 2^32 or more PCs");
-    const uint32_t sb = 32 - hpg[g].S;
-    const uint32_t nseg = (uint32_t)((ng + (1ull << sb) - 1) >> sb);
-    hpg[g].rb = (uint32_t)nreg;
-    nreg += (uint64_t)nseg * hpg[g].W;
-    if (nreg >= (1ull << 31)) fail(SYZGPU_EINVAL, "too many PC regions");
-    hcolg[g] = hcol.size();
-    for (uint32_t sg = 0; sg < nseg; sg++)
-      for (uint32_t w0 = 0; w0 < hpg[g].W; w0 += 64) hcol.push_back(ColItem{g, sg, w0, 0});
-  }
-  hgel[G] = total_pcs;
-  hcolg[G] = hcol.size();
-  const uint32_t B = hgblock[G];
-  // batches: contiguous ranges of call groups of similar size (no group split), taken from the last
-  // group to the first; each batch's P (count, column scan, region starts, scatter) and M run as soon
-  // as their inputs are ready, so one batch's scatter overlaps the next one's count and the previous
-  // one's M
-  struct Batch {
-    uint32_t g0, g1;
-    uint64_t cb;
-  };
-  std::vector<Batch> batches;
-  {
-    const uint64_t target = std::max<uint64_t>(1, (chunk_bound + pm_batches() - 1) / pm_batches());
-    uint32_t g1 = G;
-    uint64_t acc = 0;
-    for (uint32_t g = G; g-- > 0;) {
-      acc += hcb[g];
-      if (acc >= target || g == 0) {
-        batches.push_back(Batch{g, g1, acc});
-        g1 = g;
-        acc = 0;
-      }
-    }
-  }
-  const size_t NB = batches.size();
-  std::vector<uint32_t> gbatch(G, 0);
-  for (size_t b = 0; b < NB; b++)
-    for (uint32_t g = batches[b].g0; g < batches[b].g1; g++) gbatch[g] = (uint32_t)b;
-  // work items: (call, window) per batch, class (big groups: sorted by the global rounds) and mode,
-  // largest expected window first so the tail of the grid is short; a key part only its windows
-  const auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
-  std::vector<uint32_t> order(G);
-  std::iota(order.begin(), order.end(), 0u);
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
-    return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W;
-  });
-  std::vector<std::array<std::array<std::vector<PItem>, 3>, 2>> items(NB);  // [batch][big][mode]
-  uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};  // PCs the items of each class walk (the M byte models)
-  for (uint32_t g : order) {
-    if (!hpcs[g]) continue;
-    uint32_t w0 = 0, w1 = hpg[g].W;
-    if (a.key_lo) {
-      const uint32_t klo = std::max(a.key_lo[g], lo), khi = std::min(a.key_hi[g], hi);
-      if (klo > khi) continue;
-      w0 = (klo - lo) >> hpg[g].S;
-      w1 = std::min<uint32_t>(hpg[g].W, ((khi - lo) >> hpg[g].S) + 1);
-    }
-    auto& v = items[gbatch[g]][is_big(g) ? 1 : 0][hpg[g].mode];
-    for (uint32_t w = w0; w < w1; w++) v.push_back(PItem{g, w});
-    item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
-  }
-  size_t nitems = 0;
-  for (auto& bi : items)
-    for (auto& r : bi)
-      for (auto& v : r) nitems += v.size();
-  // the plan goes over in one copy: PGroup[G + 1], gblock[G + 1], bgroup[B + 1], gel0[G + 1],
-  // items[nitems + 1], column-scan items (16-byte aligned parts)
-  auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
-  const size_t o_gb = al16((G + 1) * sizeof(PGroup)), o_bg = o_gb + al16((G + 1) * 4),
-               o_ge = o_bg + al16(((size_t)B + 1) * 4), o_it = o_ge + al16((G + 1) * 8),
-               o_co = o_it + al16((nitems + 1) * sizeof(PItem)),
-               stage_bytes = o_co + al16((hcol.size() + 1) * sizeof(ColItem));
-  uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
-  uint8_t* dstage = sc.get<uint8_t>("pm_stage", stage_bytes + 64);
-  PGroup* dpg = reinterpret_cast<PGroup*>(dstage);
-  uint32_t* dgblock = reinterpret_cast<uint32_t*>(dstage + o_gb);
-  uint32_t* dbgroup = reinterpret_cast<uint32_t*>(dstage + o_bg);
-  uint64_t* dgel = reinterpret_cast<uint64_t*>(dstage + o_ge);
-  PItem* ditems = reinterpret_cast<PItem*>(dstage + o_it);
-  ColItem* dcol = reinterpret_cast<ColItem*>(dstage + o_co);
-  std::vector<std::array<std::array<size_t, 3>, 2>> ifirst(NB);  // first item of [batch][big][mode]
-  {
-    std::memcpy(stage, hpg.data(), G * sizeof(PGroup));
-    std::memcpy(stage + o_gb, hgblock.data(), (G + 1) * 4);
-    if (B) std::memcpy(stage + o_bg, hbgroup.data(), (size_t)B * 4);
-    std::memcpy(stage + o_ge, hgel.data(), (G + 1) * 8);
-    size_t k = 0;
-    for (size_t b = 0; b < NB; b++)
-      for (int big = 0; big < 2; big++)
-        for (int m = 0; m < 3; m++) {
-          const auto& v = items[b][big][m];
-          ifirst[b][big][m] = k;
-          if (!v.empty()) std::memcpy(stage + o_it + k * sizeof(PItem), v.data(), v.size() * sizeof(PItem));
-          k += v.size();
-        }
-    if (!hcol.empty()) std::memcpy(stage + o_co, hcol.data(), hcol.size() * sizeof(ColItem));
-    SYZ_HIP(hipMemcpyAsync(dstage, stage, stage_bytes, hipMemcpyHostToDevice, s));
-  }
-  // ---- blocks -> chunks ----
-  uint32_t* nsub = sc.get<uint32_t>("pm_nsub", (size_t)B + 1);
-  uint64_t* cstart = sc.get<uint64_t>("pm_cstart", (size_t)B + 1);
-  PChunk* chunks = sc.get<PChunk>("pm_chunks", chunk_bound + 1);
-  uint64_t* gchunk = sc.get<uint64_t>("pm_gchunk", G + 1);
-  uint64_t* gdesc = sc.get<uint64_t>("pm_gdesc", G + 1);
-  uint16_t* cnt = sc.get<uint16_t>("pm_cnt", desc_bound + 1);
-  uint32_t* colpre = sc.get<uint32_t>("pm_colpre", desc_bound + 1);
-  uint32_t* elems = sc.get<uint32_t>("pm_elems", total_pcs + 8);
-  uint32_t* rtot = sc.get<uint32_t>("pm_rtot", nreg + 1);
-  uint64_t* rstart = sc.get<uint64_t>("pm_rstart", nreg + 2);
-  if (B) {
-    k_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, gstart, mpos, nsub);
-    SYZ_LAUNCHED();
-  }
-  exclusive_scan_u32(nsub, cstart, B, s);
-  if (B) {
-    k_chunks<<<grid_for(B, 256, 4096), 256, 0, s>>>(dbgroup, B, dgblock, gstart, mpos, cstart, chunks);
-    SYZ_LAUNCHED();
-  }
-  k_gchunk<<<1, 1024, 0, s>>>(dgblock, G, cstart, dpg, gchunk, gdesc);
-  SYZ_LAUNCHED();
-  // ---- P on two streams of their own (count, scatter), beside the Go sort ----
-  if (!c.part) {
-    int least = 0, greatest = 0;
-    SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
-    // (a fourth stream costs the Go sort its hardware-queue share even while idle: only when asked for)
-    if (pm_p2()) SYZ_HIP(hipStreamCreateWithPriority(&c.part2, hipStreamNonBlocking, least));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
-  }
-  while (c.ev_cnt.size() < NB) {
-    hipEvent_t e1, e2;
-    SYZ_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
-    c.ev_cnt.push_back(e1);
-    c.ev_sct.push_back(e2);
-  }
-  // SYZGPU_PM_SERIAL=1 (timing experiments): P on the main stream, before the sort
-  // SYZGPU_PM_P2=1: the scatter passes on a second stream (a fourth hardware queue: measured slower,
-  // the Go sort's latency-bound rounds lose their queue share)
-  hipStream_t pq = pm_serial() ? s : c.part, pq2 = pm_serial() ? s : (pm_p2() ? c.part2 : c.part);
-  int* herr = c.pinned.get<int>(4);
-  SYZ_HIP(hipEventRecord(c.ev_part0, s));
-  SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
-  if (c.part2) SYZ_HIP(hipStreamWaitEvent(c.part2, c.ev_part0, 0));
-  for (size_t b = 0; b < NB; b++) {
-    const Batch bt = batches[b];
-    const uint64_t bpcs = hgel[bt.g1] - hgel[bt.g0], bn = hstart[bt.g1] - hstart[bt.g0];
-    // byte model: every PC read twice (count, scatter) and written once as a 4-byte element, plus 24 B
-    // of member metadata per entry per pass (members, mpos, off, slice)
-    if (bt.cb) {
-      ProfScope ps("k_region_count", pq, bpcs * 4 + bn * 24);
-      k_region<P3_BLOCK, P3_TPW, false, true><<<(unsigned)bt.cb, P3_BLOCK, 0, pq>>>(
-          a.pcs, a.off, members, mpos, sbeg, chunks, bt.g0, bt.g1, dpg, gstart, gchunk, gdesc, lo, cnt, nullptr,
-          nullptr, nullptr, err, NovSrc{}, rg_dbg());
-      SYZ_LAUNCHED();
-    }
-    {
-      const size_t ncol = hcolg[bt.g1] - hcolg[bt.g0];
-      ProfScope ps("k_colscan", pq, 0);
-      if (ncol) {
-        k_colscan<<<(unsigned)ncol, CS_BLOCK, 0, pq>>>(dcol + hcolg[bt.g0], dpg, gstart, dgblock, cstart, gchunk,
-                                                       gdesc, cnt, colpre, rtot);
-        SYZ_LAUNCHED();
-      }
-      k_rstart<<<bt.g1 - bt.g0, RS_BLOCK, 0, pq>>>(bt.g0, dpg, gstart, dgel, rtot, rstart);
-      SYZ_LAUNCHED();
-    }
-    if (b + 1 == NB) {  // the count passes' error word, as soon as the last one is done
-      SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, pq));
-      SYZ_HIP(hipEventRecord(c.ev_cnt[b], pq));
-    }
-    if (pq2 != pq) {
-      if (b + 1 != NB) SYZ_HIP(hipEventRecord(c.ev_cnt[b], pq));
-      SYZ_HIP(hipStreamWaitEvent(pq2, c.ev_cnt[b], 0));
-    }
-    if (bt.cb) {
-      ProfScope ps("k_region", pq2, bpcs * 8 + bn * 24);
-      k_region<P3_BLOCK, P3_TPW, false, false><<<(unsigned)bt.cb, P3_BLOCK, 0, pq2>>>(
-          a.pcs, a.off, members, mpos, sbeg, chunks, bt.g0, bt.g1, dpg, gstart, gchunk, gdesc, lo, cnt, colpre,
-          rstart, elems, err, NovSrc{}, rg_dbg());
-      SYZ_LAUNCHED();
-    }
-    SYZ_HIP(hipEventRecord(c.ev_sct[b], pq2));
-  }
-  SYZ_HIP(hipEventRecord(c.ev_part1, pq2));
-  // ---- Go-sort ranks, then M per class and batch as soon as its own sort and scatter are done ----
-  uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
-  SYZ_HIP(hipMemsetAsync(sel8, 0, (n + 31) / 32 * 32 + 64, s));
-  // byte model of M: every element read once (4 B per PC of the class's groups)
-  auto run_m = [&](hipStream_t q, int big) {
-    ProfScope ps(big ? "m_big" : "m_small", q, 0);
-    for (size_t b = 0; b < NB; b++) {
-      const auto& it = items[b][big];
-      const size_t nd = it[PMODE_DIRECT].size(), nh = it[PMODE_HASH].size(), np = it[PMODE_PACKED].size();
-      if (!nd && !nh && !np) continue;
-      SYZ_HIP(hipStreamWaitEvent(q, c.ev_sct[b], 0));
-      if (nd) {
-        ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
-        k_pmin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[b][big][PMODE_DIRECT], dpg, rstart, rtot, elems,
-                                                     rank_of_member, gstart, sel8, pm_dbg());
-        SYZ_LAUNCHED();
-      }
-      if (nh && !(pm_dbg() & 4)) {
-        ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
-        k_pmin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[b][big][PMODE_HASH], dpg, rstart, rtot,
-                                                          elems, rank_of_member, gstart, sel8, pm_dbg());
-        SYZ_LAUNCHED();
-      }
-      if (np && !(pm_dbg() & 4)) {
-        ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
-        k_pmin_hash<true><<<(unsigned)np, 1024, 0, q>>>(ditems + ifirst[b][big][PMODE_PACKED], dpg, rstart, rtot,
-                                                         elems, rank_of_member, gstart, sel8, pm_dbg());
-        SYZ_LAUNCHED();
-      }
-    }
-  };
-  if (!J.plan || J.plan_key != hstart) {
-    J.plan = std::make_shared<GosortPlan>();
-    gosort_plan(*J.plan, hstart, G, s);
-    J.plan_key = hstart;
-  }
-  GosortPlan& P = *J.plan;
-  P.may_bounce = J.may_bounce;
-  auto small_done = [&](hipStream_t q) {
-    if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);
-    run_m(q, 0);
-  };
-  auto big_done = [&](hipStream_t q) {
-    if (P.nbig) ranks_big(el, perm, P, members, rank_of_member, ent_of_rank, q);
-    run_m(q, 1);
-  };
-  if (n) {
-    gosort_run(el, perm, n, P, s, small_done, big_done);
-  } else {
-    small_done(s);
-    big_done(s);
-  }
-  // the only error the passes report (a PC outside the planned windows) comes from the count passes:
-  // wait for their error word, not for the scatter and M (end() and the exchange queue behind M on
-  // their streams)
-  SYZ_HIP(hipEventSynchronize(c.ev_cnt[NB - 1]));
-  if (!J.done) SYZ_HIP(hipEventCreateWithFlags(&J.done, hipEventDisableTiming));
-  SYZ_HIP(hipEventRecord(J.done, s));  // (s has joined the small class's M)
-  J.stats_total_pcs = total_pcs;
-  J.stats_items_direct = J.stats_items_hash = 0;
-  for (const auto& bi : items)
-    for (int big = 0; big < 2; big++) {
-      J.stats_items_direct += bi[big][PMODE_DIRECT].size();
-      J.stats_items_hash += bi[big][PMODE_HASH].size() + bi[big][PMODE_PACKED].size();
-    }
-  if (herr[0] & 1) {
-    if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
-    return false;
-  }
-  J.begun = true;
-  return true;
+  return begin_slab(J, a, hstart, hpcs, hsl, hpg, lo, hi, exact_span, members, el, mlen, mpos, sbeg, err);
 }
 
 __global__ void k_job_xchg(uint8_t* sel8, const uint64_t* gstart, const uint32_t* groups, const uint64_t* boff,

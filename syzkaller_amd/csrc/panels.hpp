@@ -19,12 +19,6 @@ struct PGroup {          // per call group: window bits, windows, table kind
 struct PItem {           // one (call group, window) min-rank table
   uint32_t g, w;
 };
-struct PChunk {          // <= PCAP consecutive PCs of one 64-member block, in member order
-  uint64_t elem;         // first element (= position in the group-major concatenation of covers)
-  uint32_t len, mb;      // PCs; first member of the block
-  uint32_t nmem, sub;    // members in the block; offset of this chunk inside the block's PCs
-  uint32_t g, pad;
-};
 
 struct PSlab {
   uint64_t elem;      // first element (4-aligned: the slab's passes leave as 16-byte vectors)

@@ -980,19 +980,56 @@ __device__ __forceinline__ int canon_class_of(uint64_t n) {
   return n <= 64 ? 0 : n <= 128 ? 1 : n <= 256 ? 2 : n <= 512 ? 3 : n <= 1024 ? 4 : n <= 2048 ? 5
        : n <= 4096 ? 6 : n <= 8192 ? 7 : n <= 16384 ? 8 : n <= (uint64_t)CANON_LDS2 ? 9 : 10;
 }
+// The first CANON_PRE = 8 PCs of every cover, eight covers per wave (lane 8 c + e reads PC e of cover
+// c: one coalesced load for eight covers): cand[i] = 1 when they increase strictly (a candidate for the
+// canonical-cover check, k_canon_sorted), so a raw cover costs the check one 4-byte read per PC of its
+// prefix.
+constexpr int CANON_PRE = 8;  // lanes per cover: 64 / CANON_PRE covers per load
+static_assert(CANON_PRE == 8, "k_canon_prefix's lane groups");
+__global__ __launch_bounds__(256) void k_canon_prefix(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
+                                                      size_t ncov, uint8_t* __restrict__ cand) {
+  const unsigned lane = __lane_id();
+  const size_t nw = (size_t)gridDim.x * (blockDim.x >> 6);
+  for (size_t c0 = ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8; c0 < ncov; c0 += nw * 8) {
+    const size_t i = c0 + (lane >> 3);
+    const uint32_t e = lane & 7;
+    uint64_t b = 0, n = 0;
+    if (i < ncov) {
+      b = off[i];
+      n = off[i + 1] - b;
+    }
+    const uint32_t x = e < n ? pcs[b + e] : 0u;
+    const uint32_t prev = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x138, 0xF, 0xF, false);  // lane - 1
+    const bool bad = e > 0 && e < n && prev >= x;
+    const uint64_t m = __ballot(bad);
+    if (e == 0 && i < ncov) cand[i] = ((m >> (lane & ~7u)) & 0xFFu) == 0;
+  }
+}
+
+// Classes by length; a cover flagged in cand (its prefix increases) goes to the extra class CANON_NCLS
+// instead, for the canonical-cover check.
 __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t ncov, uint32_t* lists, size_t cap,
-                                                     uint32_t* cnt, const uint8_t* done = nullptr) {
-  __shared__ uint32_t lc[CANON_NCLS], lb[CANON_NCLS];
+                                                     uint32_t* cnt, const uint8_t* cand = nullptr) {
+  constexpr int NC = CANON_NCLS + 1;
+  __shared__ uint32_t lc[NC], lb[NC];
   const unsigned lane = __lane_id();
   for (size_t c0 = (size_t)blockIdx.x * CANON_CHUNK; c0 < ncov; c0 += (size_t)gridDim.x * CANON_CHUNK) {
-    if (threadIdx.x < CANON_NCLS) lc[threadIdx.x] = 0;
+    if (threadIdx.x < NC) lc[threadIdx.x] = 0;
     __syncthreads();
-    for (int pass = 0; pass < 2; pass++) {  // 0: counts; 1: entries at the reserved bases
-      for (size_t i0 = c0; i0 < min(c0 + CANON_CHUNK, ncov); i0 += blockDim.x) {
-        const size_t i = i0 + threadIdx.x;
-        const int c = i < ncov && !(done && done[i]) ? canon_class_of(off[i + 1] - off[i]) : -1;
+    constexpr int PER = CANON_CHUNK / 256;
+    int cls[PER];
 #pragma unroll
-        for (int k = 0; k < CANON_NCLS; k++) {
+    for (int q = 0; q < PER; q++) {
+      const size_t i = c0 + (size_t)q * blockDim.x + threadIdx.x;
+      cls[q] = i >= ncov ? -1 : (cand && cand[i]) ? CANON_NCLS : canon_class_of(off[i + 1] - off[i]);
+    }
+    for (int pass = 0; pass < 2; pass++) {  // 0: counts; 1: entries at the reserved bases
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const size_t i = c0 + (size_t)q * blockDim.x + threadIdx.x;
+        const int c = cls[q];
+#pragma unroll
+        for (int k = 0; k < NC; k++) {
           const uint64_t m = __ballot(c == k);
           if (!m) continue;
           const unsigned leader = (unsigned)__ffsll((unsigned long long)m) - 1;
@@ -1005,7 +1042,7 @@ __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t
         }
       }
       __syncthreads();
-      if (pass == 0 && threadIdx.x < CANON_NCLS) {
+      if (pass == 0 && threadIdx.x < NC) {
         lb[threadIdx.x] = lc[threadIdx.x] ? atomicAdd(&cnt[threadIdx.x], lc[threadIdx.x]) : 0u;
         lc[threadIdx.x] = 0;
       }
@@ -1014,20 +1051,43 @@ __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t
   }
 }
 
-// Already-canonical covers (the executor's dedup on, executor.cc:565-585 -> fuzzer.go:355): one wave
-// per cover streams it once, 4 x 64 PCs per step with lane i of load k at PC 64 k + i, and checks it
-// strictly increasing (each PC against the one before it: the lane before, the last lane of the load
-// before, the previous step's last PC), stopping at the first violation. Such a cover is its own
-// Canonicalize (sorted, no repeat; a 0xFFFFFFFF can only be its last PC, kept unless it is the only
-// one): its length goes to out_len and its flag keeps it out of the classes. Others: flag 0.
-constexpr int CANON_SCAN_U = 4;
+// Already-canonical covers (the executor's dedup on, executor.cc:565-585 -> fuzzer.go:355): the class
+// kernel lists the covers whose first CANON_PRE PCs increase; one wave per such candidate streams the
+// whole cover once, CANON_SCAN_U x 64 PCs a step (lane i of load k at PC 64 k + i), and checks every PC
+// against the one before it (the lane before, the last lane of the load before, the previous step's
+// last PC), stopping at the first violation. A strictly increasing cover is its own Canonicalize
+// (sorted, no repeat; a 0xFFFFFFFF can only be its last PC, kept unless it is the only one): its length
+// goes to out_len and no network touches it. A candidate that fails joins its length class.
+#ifndef SYZ_CANON_SCAN_U
+#define SYZ_CANON_SCAN_U 8
+#endif
+constexpr int CANON_SCAN_U = SYZ_CANON_SCAN_U;
 __global__ __launch_bounds__(256) void k_canon_sorted(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
-                                                      size_t ncov, uint8_t* __restrict__ done,
+                                                      const uint32_t* __restrict__ cand, const uint32_t* ncand_dev,
+                                                      uint32_t* __restrict__ lists, size_t cap, uint32_t* cnt,
                                                       uint64_t* __restrict__ out_len) {
   const unsigned lane = __lane_id();
-  const size_t nw = (size_t)gridDim.x * (blockDim.x >> 6);
-  for (size_t i = (size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < ncov; i += nw) {
-    const uint64_t b = off[i], n = off[i + 1] - b;
+  const uint32_t ncand = *ncand_dev;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  uint32_t ci = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // the wave's next candidate and its bounds are read one cover ahead (lane 0: index, lanes 1, 2: the
+  // offsets), so a cover's loads wait only for its own data
+  auto meta = [&](uint32_t c) -> uint64_t {
+    uint64_t x = 0;
+    if (c < ncand) {
+      const uint32_t i = cand[c];
+      x = lane == 0 ? i : lane == 1 ? off[i] : lane == 2 ? off[i + 1] : 0;
+    }
+    return x;
+  };
+  uint64_t m = meta(ci);
+  for (; ci < ncand; ci += nw) {
+    const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, 0);
+    const uint64_t b = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), 1) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, 1);
+    const uint64_t e = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), 2) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, 2);
+    const uint64_t n = e - b;
     const uint32_t* x = pcs + b;
     bool bad = false;
     uint32_t last = 0;  // the PC before this step's first (none at the start)
@@ -1038,6 +1098,7 @@ __global__ __launch_bounds__(256) void k_canon_sorted(const uint32_t* __restrict
         const uint64_t j = j0 + 64 * k + lane;
         v[k] = j < n ? x[j] : 0xFFFFFFFFu;
       }
+      if (j0 == 0) m = meta(ci + nw);  // (issued behind this cover's first loads)
       bool b2 = false;
 #pragma unroll
       for (int k = 0; k < CANON_SCAN_U; k++) {
@@ -1049,9 +1110,14 @@ __global__ __launch_bounds__(256) void k_canon_sorted(const uint32_t* __restrict
       }
       bad = __ballot(b2) != 0;
     }
+    if (n == 0) m = meta(ci + nw);
     if (lane == 0) {
-      done[i] = !bad;
-      if (!bad) out_len[i] = (n == 1 && x[0] == 0xFFFFFFFFu) ? 0 : n;
+      if (!bad) {
+        out_len[i] = (n == 1 && x[0] == 0xFFFFFFFFu) ? 0 : n;
+      } else {  // not canonical after all: the network of its length class
+        const int k = canon_class_of(n);
+        lists[(size_t)k * cap + atomicAdd(&cnt[k], 1u)] = i;
+      }
     }
   }
 }
@@ -1068,15 +1134,27 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   Context& c = ctx();
   if (ncov == 0) return;
   if (ncov >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many covers");
-  uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", CANON_NCLS * ncov);
-  uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", CANON_NCLS);
-  SYZ_HIP(hipMemsetAsync(cnt, 0, CANON_NCLS * 4, s));
-  // covers that are canonical already are done by the check (no network); the rest are classed
-  uint8_t* done = c.scratch.get<uint8_t>("cd_done", ncov);
-  k_canon_sorted<<<(unsigned)std::min<size_t>((ncov + 3) / 4, 8192), 256, 0, s>>>(pcs, off, ncov, done, out_len);
-  SYZ_LAUNCHED();
-  k_canon_class<<<(unsigned)std::min<size_t>((ncov + CANON_CHUNK - 1) / CANON_CHUNK, 2048), 256, 0, s>>>(off, ncov, lists, ncov, cnt, done);
-  SYZ_LAUNCHED();
+  uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", (CANON_NCLS + 1) * ncov);
+  uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", CANON_NCLS + 1);
+  SYZ_HIP(hipMemsetAsync(cnt, 0, (CANON_NCLS + 1) * 4, s));
+  // classes by length; covers with an increasing prefix are checked whole first: canonical ones are
+  // done (no network), the others join their class before the class kernels run
+  uint8_t* cand = c.scratch.get<uint8_t>("cd_cand", ncov + 1);
+  {
+    ProfScope ps("canon_classes", s, 0);
+    k_canon_prefix<<<(unsigned)std::min<size_t>((ncov + 31) / 32, 8192), 256, 0, s>>>(pcs, off, ncov, cand);
+    SYZ_LAUNCHED();
+    k_canon_class<<<(unsigned)std::min<size_t>((ncov + CANON_CHUNK - 1) / CANON_CHUNK, 2048), 256, 0, s>>>(
+        off, ncov, lists, ncov, cnt, cand);
+    SYZ_LAUNCHED();
+  }
+  {
+    ProfScope ps("canon_check", s, 0);
+    k_canon_sorted<<<(unsigned)std::min<size_t>((ncov + 3) / 4, 8192), 256, 0, s>>>(pcs, off, lists + CANON_NCLS * ncov,
+                                                                                    cnt + CANON_NCLS, lists, ncov, cnt,
+                                                                                    out_len);
+    SYZ_LAUNCHED();
+  }
   if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
   const unsigned ncu = (unsigned)std::max(1, c.ncu);
   // the long classes (few covers, long per-cover chains: the 32768 class is one workgroup's bitonic

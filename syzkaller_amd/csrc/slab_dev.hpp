@@ -1,22 +1,22 @@
 // Slab form of the raw Minimize pipeline's transpose (P) and window walk (M): the covers are read from
-// HBM once (round 3's region form read them twice, a count pass then the scatter).
+// HBM once.
 //
-// A SLAB is up to SL_TILES tiles of one call group's members (a tile = <= 64 consecutive PCs of one
-// member's sorted cover), i.e. <= 32K PCs, cut from the group's member sequence (partition order) in
-// blocks of at most SL_MEMB (and 2^(32 - S)) members so a member's tag fits the element. One workgroup
-// per slab:
-//   * member table in LDS, each lane resolves one tile of its wave (address, count, tag) by a search,
-//     the wave's tiles are loaded with wave-uniform (scalar) addresses, all of them in flight;
-//   * window histogram by LDS atomics, an exclusive scan -> window starts inside the slab;
-//   * the slab's window-major element sequence is produced in PASSES over a 16K-element LDS buffer:
-//     pass k takes the windows that START in [k * 16K, (k + 1) * 16K) (a contiguous window range), each
-//     element's place comes from the window's LDS cursor, and the pass leaves as one contiguous run of
-//     16-byte stores; the few elements of a window running past the buffer are stored directly;
+// A SLAB is up to SL_TILES = 256 tiles of one call group's members (a tile = <= 64 consecutive PCs of
+// one member's sorted cover), i.e. <= 16K PCs, cut from the group's member sequence (partition order)
+// in blocks of at most SL_MEMB (and 2^(32 - S)) members so a member's tag fits the element. One
+// workgroup per slab, ONE pass (the whole slab is staged in LDS):
+//   * member table in LDS (in the staging buffer's space), each lane resolves one tile of its wave
+//     (address, count, tag) by a search; the wave's 32 tiles are loaded with wave-uniform (scalar)
+//     addresses, all of them in flight;
+//   * window histogram by LDS atomics, an exclusive scan -> padded window starts inside the slab;
+//   * one returning LDS atomic per element for its place in the staging buffer, the padding slots
+//     filled, and the slab leaves as one contiguous run of 16-byte stores;
 //   * the window starts go out WINDOW-MAJOR per call group: D[dbase + w * stride + j] = element offset
 //     (from the group's first element) of window w of the group's slab j, so M reads, for its window,
 //     two contiguous rows (starts, and the next window's starts = ends).
-// M (for_slab_window) then walks one run per slab: a window's runs are ~SL_TILES * 64 / W elements long
-// (128 for a dense call of 256 windows: 512-byte runs, against round 2's 64-element chunk runs).
+// Round 4's form (512-tile slabs through a 16K-element buffer in up to three passes, each pass walking
+// every tile again) took 1.27 ms against this form's 1.13 ms at config 4 (serialized).
+// M (for_slab_window) then walks one run per slab: a window's runs are ~SL_TILES * 64 / W elements long.
 #pragma once
 #include <atomic>
 

@@ -35,7 +35,7 @@ def read_prof():
 if leg == "setops":
     res = bench.setops_leg(args, dev, L, read_prof)
 elif leg == "canonicalize":
-    res = bench.canonicalize_leg(args, dev, L)
+    res = bench.canonicalize_leg(args, dev, L, read_prof)
 elif leg == "novelty":
     res = bench.novelty_leg(args, dev, L, read_prof)
 else:
