@@ -166,12 +166,16 @@ def workload_label(args, world):
     """The BASELINE.json config the line measures: configs[3] (1M programs; strong scaling over N GPUs
     with --total-progs) or, weak scaling at N > 1, configs[4]'s hub-merge shape (N managers' corpora of
     --progs-per-gpu programs each)."""
-    tail = "2M-PC space, 289 calls, C=1159"
+    tail = "%s-PC space, %d calls, C=%d" % (("%gM" % (args.npcs / 1e6)) if args.npcs >= 1_000_000 else
+                                           ("%gk" % (args.npcs / 1e3)), args.ngroups, args.calls)
     if args.total_progs:
         return "config4-%dk over %d GPU%s (strong scaling): %s" % (args.total_progs // 1000, world,
                                                                   "s" if world > 1 else "", tail)
     if world == 1:
-        return "config4-1M: %d programs on 1 GPU, %s" % (args.progs_per_gpu, tail)
+        # BASELINE.json configs[0] / [1] / [3] by their (programs, PC space); other shapes by their numbers
+        name = {(10_000, 50_000): "config1-10k", (100_000, 500_000): "config2-100k",
+                (1_000_000, 2_000_000): "config4-1M"}.get((args.progs_per_gpu, args.npcs), "custom")
+        return "%s: %d programs on 1 GPU, %s" % (name, args.progs_per_gpu, tail)
     return ("config5-shape: %d managers' corpora of %d programs (%d programs, weak scaling: %d per GPU), %s"
             % (world, args.progs_per_gpu, args.progs_per_gpu * world, args.progs_per_gpu, tail))
 

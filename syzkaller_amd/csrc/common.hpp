@@ -14,6 +14,7 @@
 #include <thread>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/syzgpu.h"
@@ -114,10 +115,13 @@ struct Context {
   hipEvent_t ev_part0 = nullptr, ev_part1 = nullptr;
   hipEvent_t ev_msmall = nullptr, ev_msmall2 = nullptr;  // the small groups' packed M on another stream
   hipEvent_t ev_psmall = nullptr;  // P's slabs of the small call groups are cut
+  hipEvent_t ev_spec = nullptr;    // the end of a speculative P (panels.hip begin_once)
   hipEvent_t ev_spin = nullptr;    // stream_wait_spin's marker
   hipStream_t part2 = nullptr;  // its scatter passes, batch after batch beside the next batch's count
   std::vector<hipEvent_t> ev_cnt, ev_sct;  // per batch: count done, scatter done
   int ncu = 0;  // compute units of the device
+  // single-pass scans (scan.hpp): per tag and stream, the flag buffer, the tiles it was cleared for, the epoch
+  std::unordered_map<std::string, std::pair<void*, std::pair<size_t, uint32_t>>> scan_epoch;
   std::shared_ptr<struct GosortPlan> raw_plan;  // Go-sort plan of the last raw corpus layout
   std::vector<uint64_t> raw_plan_key;
 };
@@ -210,6 +214,7 @@ void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t
 // Waits for everything issued to s so far by polling an event (no blocking wait: the host turns around
 // in microseconds when the plan it waits for is short); falls back to a blocking wait after 50 ms.
 void stream_wait_spin(hipStream_t s);
+void event_wait_spin(hipEvent_t e);  // the same on an event already recorded
 
 inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 20) {
   size_t g = (n + block - 1) / block;

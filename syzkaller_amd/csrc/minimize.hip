@@ -76,14 +76,19 @@ __global__ __launch_bounds__(256) void k_grp_sumlen(const uint32_t* group, const
 }
 
 // Stable placement: each wave walks its chunk in order; lanes of one group inside a 64-entry round
-// are ranked with a ballot, the per-group running slot is kept in LDS.
+// are ranked with a ballot, the per-group running slot is kept in LDS. Also (PartOut, each optional):
+// the group starts, the identity ranks (rank_of_member[m] = m, ent_of_rank[m] = members[m]: groups of
+// one entry are never sorted) and the member lengths, so the step needs no pass of its own for them.
 __global__ __launch_bounds__(256) void k_grp_scatter(const uint32_t* group, const uint64_t* off, size_t n,
                                                      uint32_t G, uint32_t nchunks, uint32_t pw,
                                                      const uint64_t* cnt_scan,
-                                                     uint32_t* members, uint64_t* el) {
+                                                     uint32_t* members, uint64_t* el, PartOut po) {
   extern __shared__ uint32_t run[];  // [4][G]
   const int w = threadIdx.x >> 6;
   uint32_t* mine = run + (size_t)w * G;
+  if (po.gstart)
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x)
+      po.gstart[g] = g < G ? cnt_scan[(size_t)g * nchunks] : (uint64_t)n;
   const uint32_t chunk = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (chunk >= nchunks) return;
   for (uint32_t g = __lane_id(); g < G; g += 64) mine[g] = (uint32_t)cnt_scan[(size_t)g * nchunks + chunk];
@@ -109,6 +114,11 @@ __global__ __launch_bounds__(256) void k_grp_scatter(const uint32_t* group, cons
         const uint32_t pos = b0 + __popcll(mask & lanemask_lt());
         members[pos] = (uint32_t)i;
         el[pos] = (len << 32) | pos;
+        if (po.rank_of_member) {
+          po.rank_of_member[pos] = pos;
+          po.ent_of_rank[pos] = (uint32_t)i;
+        }
+        if (po.mlen) po.mlen[pos] = (uint32_t)len;
       }
       wave_sync();
       if (__lane_id() == (unsigned)leader) mine[gl] = b0 + __popcll(mask);
@@ -277,23 +287,24 @@ __global__ void k_order_out(const uint64_t* el, const uint32_t* perm, const uint
 }
 
 void group_partition_dev(const uint32_t* group, const uint64_t* off, size_t n, uint32_t G, uint64_t* gstart,
-                         uint32_t* members, uint64_t* el, int* err, hipStream_t s) {
+                         uint32_t* members, uint64_t* el, int* err, hipStream_t s, PartOut po) {
   Scratch& sc = ctx().scratch;
   const uint32_t pw = grp_pw(n, G);
   const uint32_t nchunks = (uint32_t)((n + pw - 1) / pw);
   uint32_t* cnt = sc.get<uint32_t>("mz_cnt", (size_t)G * nchunks + 1);
   uint64_t* cnt_scan = sc.get<uint64_t>("mz_cnt_scan", (size_t)G * nchunks + 1);
-  SYZ_HIP(hipMemsetAsync(cnt, 0, ((size_t)G * nchunks + 1) * 4, s));
   const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
-  if (n) {
+  if (n) {  // (k_grp_count writes every count the scan reads: no clearing)
     k_grp_count<<<wg, 256, 4 * G * 4, s>>>(group, n, G, nchunks, pw, cnt, err);
     SYZ_LAUNCHED();
   }
   exclusive_scan_u32(cnt, cnt_scan, (size_t)G * nchunks, s);
-  k_grp_starts<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(cnt_scan, G, nchunks, n, gstart);
-  SYZ_LAUNCHED();
   if (n) {
-    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, pw, cnt_scan, members, el);
+    po.gstart = gstart;
+    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, pw, cnt_scan, members, el, po);
+    SYZ_LAUNCHED();
+  } else {
+    k_grp_starts<<<grid_for(G + 1, 256, 1024), 256, 0, s>>>(cnt_scan, G, nchunks, n, gstart);
     SYZ_LAUNCHED();
   }
 }
@@ -928,7 +939,7 @@ Corpus* corpus_create_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   SYZ_LAUNCHED();
   if (n) {
     const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
-    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, pw, cnt_scan, K.members.p, el);
+    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(group, off, n, G, nchunks, pw, cnt_scan, K.members.p, el, PartOut{});
     SYZ_LAUNCHED();
   }
   K.member_of.alloc(n);
@@ -1167,7 +1178,8 @@ void corpus_partition(Corpus& K, std::vector<uint64_t>& hpcs, hipStream_t s) {
   SYZ_LAUNCHED();
   if (n) {
     const unsigned wg = (unsigned)(((size_t)nchunks * 64 + 255) / 256);
-    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(K.group.p, K.off.p, n, G, nchunks, pw, cnt_scan, K.members.p, K.el0.p);
+    k_grp_scatter<<<wg, 256, 4 * G * 4, s>>>(K.group.p, K.off.p, n, G, nchunks, pw, cnt_scan, K.members.p, K.el0.p,
+                                                PartOut{});
     SYZ_LAUNCHED();
     k_invert<<<grid_for(n, 256, 4096), 256, 0, s>>>(K.members.p, n, K.member_of.p);
     SYZ_LAUNCHED();

@@ -569,10 +569,11 @@ static int nwh_dbg() {
   return v | (so && atoi(so) ? 16 : 0);
 }
 
-// SYZGPU_NW_BITS=14|15: direct window bits (default: 14 while the span fits 1024 such windows, else 15)
+// SYZGPU_NW_BITS=14|15: direct window bits (default: 14 while the span fits 1024 such windows, else 15;
+// 13-bit windows measured slower, r05: 5.83 vs 4.61 ms at config 3)
 static uint32_t nw_bits_forced() {
   static const uint32_t v = getenv("SYZGPU_NW_BITS") ? (uint32_t)atoi(getenv("SYZGPU_NW_BITS")) : 0u;
-  return v == 13 || v == 14 || v == 15 ? v : 0u;
+  return v == 14 || v == 15 ? v : 0u;
 }
 
 __global__ void k_nw_gpcs(const uint64_t* mpos, const uint64_t* cstart, uint32_t G, uint64_t* gpcs) {
@@ -706,7 +707,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     ns.n1 = (uint32_t)n;
     if (SJ.slab_bound) {
       launch_slab<true>(SJ.slab_bound, SJ.wmax, s, d_pcs, d_off, cmem, mlen, SJ.tpos, nullptr, SJ.slabs, SJ.cstart + B,
-                        dsg, SJ.gebase, lo, SJ.elems, SJ.D, err, SJ.wtot, ns, 0);
+                        dsg, SJ.gebase, lo, SJ.elems, SJ.ecap, SJ.D, err, SJ.wtot, ns, 0);
       SYZ_LAUNCHED();
     }
   }
@@ -738,11 +739,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     k_nw_fstart<<<grid_for(WD + 1, 256, 64), 256, 0, s>>>(d_fl, nfl, lo, WD, DB, fstart);
     SYZ_LAUNCHED();
     if (nitems) {
-      if (DB == 13)
-        k_nw_min<13><<<(unsigned)nitems, NwCfg<13>::BLOCK, 0, s>>>(dorder, WD, dsg, gslab, gebase, D, slabs, elems,
-                                                                   cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
-                                                                   upd, nw_dbg());
-      else if (DB == 14)
+      if (DB == 14)
         k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, dsg, gslab, gebase, D, slabs, elems,
                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
                                                                    upd, nw_dbg());

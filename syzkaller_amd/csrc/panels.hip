@@ -84,13 +84,14 @@ __global__ __launch_bounds__(256) void k_minmax(const uint32_t* pcs, size_t L, u
 }
 
 // the job's per-step state: error word, per-group PC sums, the PC span
-__global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span) {
+__global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span, uint32_t* mlmax) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x) {
     gpcs[g] = 0;
     if (g < 2) {
       err[g] = 0;
       span[g] = g ? 0u : 0xFFFFFFFFu;
     }
+    if (g == 0) *mlmax = 0;
   }
 }
 
@@ -117,11 +118,6 @@ __global__ void k_gpack(const uint64_t* gstart, const uint64_t* gpcs, const uint
     }
     out[i] = v;
   }
-}
-
-__global__ void k_mlen(const uint64_t* el, size_t n, uint32_t* mlen) {
-  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x)
-    mlen[m] = (uint32_t)(el[m] >> 32);
 }
 
 // Winners of a window table -> sel8[rank] = 1 with plain byte stores (no atomics: a byte written by
@@ -455,6 +451,12 @@ static bool pm_psplit() {
   return v;
 }
 
+// SYZGPU_PM_SPEC=0 (A/B): no speculative P on the last step's plan (begin_once)
+static bool pm_spec() {
+  static const bool v = !getenv("SYZGPU_PM_SPEC") || atoi(getenv("SYZGPU_PM_SPEC")) != 0;
+  return v;
+}
+
 
 
 void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* hpcs, const std::vector<PGroup>& hpg,
@@ -489,16 +491,10 @@ void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* 
   J.B = J.hgblock[G];
 }
 
-// the members' tile counts and their prefix (tpos): needs no plan, so it can run before the host's
+// the members' tile prefix (tpos): needs no plan, so it can run before the host's
 uint64_t* slab_tiles(const uint32_t* mlen, size_t nmem, const char* prefix, hipStream_t s) {
-  Scratch& sc = ctx().scratch;
-  uint32_t* mtile = sc.get<uint32_t>((std::string(prefix) + "_sl_mtile").c_str(), nmem + 1);
-  uint64_t* tpos = sc.get<uint64_t>((std::string(prefix) + "_sl_tpos").c_str(), nmem + 2);
-  if (nmem) {
-    k_sl_tiles<<<grid_for(nmem, 256, 4096), 256, 0, s>>>(mlen, nmem, mtile);
-    SYZ_LAUNCHED();
-  }
-  exclusive_scan_u32(mtile, tpos, nmem, s);
+  uint64_t* tpos = ctx().scratch.get<uint64_t>((std::string(prefix) + "_sl_tpos").c_str(), nmem + 2);
+  scan_f<1>(TilesFn{mlen}, nmem, tpos, nullptr, s, prefix);
   return tpos;
 }
 
@@ -507,34 +503,73 @@ void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint
   Scratch& sc = ctx().scratch;
   auto nm = [&](const char* x) { return std::string(prefix) + x; };
   const uint32_t B = J.B, G = J.G;
-  uint32_t* nsub = sc.get<uint32_t>(nm("_sl_nsub").c_str(), (size_t)B + 1);
   J.tpos = tiles_done ? sc.get<uint64_t>(nm("_sl_tpos").c_str(), nmem + 2) : slab_tiles(mlen, nmem, prefix, s);
   J.cstart = sc.get<uint64_t>(nm("_sl_cstart").c_str(), (size_t)B + 2);
   J.slabs = sc.get<PSlab>(nm("_sl_slabs").c_str(), J.slab_bound + 1);
   J.gslab = sc.get<uint32_t>(nm("_sl_gslab").c_str(), G + 1);
   J.gebase = sc.get<uint64_t>(nm("_sl_gebase").c_str(), G + 1);
   J.D = sc.get<uint32_t>(nm("_sl_D").c_str(), J.dtotal + 1);
-  J.elems = sc.get<uint32_t>("pm_elems", J.total_pcs + J.xtotal + 16);
+  J.ecap = J.total_pcs + J.xtotal + 16;
+  J.elems = sc.get<uint32_t>("pm_elems", J.ecap);
   J.wtot = nullptr;
   ProfScope ps("slab_plan", s, 0);
   if (J.wtotal) {
     J.wtot = sc.get<uint32_t>(nm("_sl_wtot").c_str(), J.wtotal + 1);
     SYZ_HIP(hipMemsetAsync(J.wtot, 0, J.wtotal * 4, s));
   }
-  if (B) {
-    k_sl_blocks<<<grid_for(B, 256, 4096), 256, 0, s>>>(J.dbgroup, B, J.dgblock, gstart, J.dsg, J.tpos, nsub);
-    SYZ_LAUNCHED();
-  }
-  exclusive_scan_u32(nsub, J.cstart, B, s);
-  if (J.slab_bound) {
-    k_sl_slabs<<<grid_for(J.slab_bound, 256, 8192), 256, 0, s>>>(J.dbgroup, B, J.dgblock, gstart, J.dsg, J.tpos, mpos,
-                                                                  J.cstart, J.slab_bound, J.slabs);
-    SYZ_LAUNCHED();
-  }
-  k_sl_groups<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(J.dgblock, G, J.cstart, J.slabs, J.gslab, J.gebase);
+  scan_f<1>(BlockSlabsFn{J.dbgroup, J.dgblock, gstart, J.dsg, J.tpos}, B, J.cstart, nullptr, s, prefix);
+  k_sl_slabs<<<grid_for(std::max<uint64_t>(J.slab_bound, G + 1), 256, 8192), 256, 0, s>>>(
+      J.dbgroup, B, J.dgblock, gstart, J.dsg, J.tpos, mpos, J.cstart, J.slab_bound, J.slabs, G, J.gslab, J.gebase);
   SYZ_LAUNCHED();
 }
 
+
+// P for one plan: the plan's slab table (slab_build on s), then the transpose on the part stream
+// (pm_serial: on s); SYZGPU_PM_PSPLIT=1: the small call groups' slabs as a launch of their own first.
+// ev_psmall marks the small groups' slabs, the caller records the rest.
+static hipStream_t launch_p(const RawMinArgs& a, const SlabPlanCache& PC, SlabJob& SJ, const uint32_t* members,
+                            const uint32_t* mlen, const uint64_t* mpos, const uint64_t* gstart, const uint32_t* sbeg,
+                            int* err) {
+  Context& c = ctx();
+  hipStream_t s = a.s;
+  slab_build(SJ, "pm", mlen, mpos, a.n, gstart, s, true);
+  if (!c.part) {
+    int least = 0, greatest = 0;
+    SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_spec, hipEventDisableTiming));
+  }
+  if (!c.ev_msmall) {
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall2, hipEventDisableTiming));
+    SYZ_HIP(hipEventCreateWithFlags(&c.ev_psmall, hipEventDisableTiming));
+  }
+  hipStream_t pq = pm_serial() ? s : c.part;
+  SYZ_HIP(hipEventRecord(c.ev_part0, s));
+  SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
+  if (!SJ.slab_bound) {
+    SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
+    return pq;
+  }
+  // byte model: the algorithm's input this pass reads, 4 B per PC + 10 B per entry
+  // (offset, group id); the element buffer it writes is intermediate traffic, not algorithmic bytes
+  const auto& icount = PC.icount;
+  const bool split = pm_psplit() && !pm_serial() && icount[0][0] + icount[0][1] + icount[0][2] > 0;
+  for (int cls = split ? 1 : 0; cls <= (split ? 2 : 0); cls++) {
+    const uint64_t bytes = cls ? PC.cpcs[cls - 1] * 4 + PC.cent[cls - 1] * 10
+                               : (PC.cpcs[0] + PC.cpcs[1]) * 4 + (uint64_t)a.n * 10;
+    ProfScope ps("k_slab", pq, bytes);
+    launch_slab<false>(SJ.slab_bound, SJ.wmax, pq, a.pcs, a.off, members, mlen, SJ.tpos, sbeg, SJ.slabs,
+                       SJ.cstart + SJ.B, SJ.dsg, SJ.gebase, PC.lo, SJ.elems, SJ.ecap, SJ.D, err, nullptr, NovSrc{},
+                       cls);
+    SYZ_LAUNCHED();
+    if (cls == 1) SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
+  }
+  if (!split) SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
+  return pq;
+}
 
 // The slab form (slab_dev.hpp): one read of the covers. Inputs from begin_once's common part: the
 // group partition (members, el, mlen, mpos), the per-group PC counts and read slices, the windows.
@@ -564,6 +599,15 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   key.push_back(((uint64_t)lo << 32) | hi);
   if (a.key_lo)
     for (uint32_t g = 0; g < G; g++) key.push_back(((uint64_t)a.key_lo[g] << 32) | a.key_hi[g]);
+  // a speculative P (begin_once) ran on the cached plan: kept when this layout is the cached one;
+  // otherwise the slab table is rebuilt once that P is done, and its flags cleared (the partition's
+  // own were read back already)
+  const bool spec_hit = J.spec && J.pcache && J.pcache->key == key;
+  if (J.spec && !spec_hit) {
+    SYZ_HIP(hipStreamWaitEvent(s, c.ev_spec, 0));
+    SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
+  }
+  J.spec = false;
   if (!J.pcache || J.pcache->key != key) {
     auto P = std::make_shared<SlabPlanCache>();
     P->key = std::move(key);
@@ -619,6 +663,12 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     SJ.dsg = reinterpret_cast<SGroup*>(P->dstage.p);
     SJ.dgblock = reinterpret_cast<uint32_t*>(P->dstage.p + P->o_gb);
     SJ.dbgroup = reinterpret_cast<uint32_t*>(P->dstage.p + P->o_bg);
+    for (uint32_t g = 0; g < G; g++) {
+      P->cpcs[is_big(g) ? 1 : 0] += hsl[g];
+      P->cent[is_big(g) ? 1 : 0] += hstart[g + 1] - hstart[g];
+    }
+    P->lo = lo;
+    P->n = n;
     J.pcache = P;
   }
   const SlabPlanCache& PC = *J.pcache;
@@ -626,32 +676,19 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   const auto& icount = PC.icount;
   const auto& ifirst = PC.ifirst;
   const auto& item_pcs = PC.item_pcs;
-  const uint64_t slab_bound = SJ.slab_bound, total_pcs = SJ.total_pcs;
-  const uint32_t B = SJ.B;
+  const uint64_t total_pcs = SJ.total_pcs;
   uint8_t* dstage = PC.dstage.p;
   const SGroup* dsg = SJ.dsg;
   const PItem* ditems = reinterpret_cast<const PItem*>(dstage + PC.o_it);
   ht.mark("items_stage");
-  slab_build(SJ, "pm", mlen, mpos, n, gstart, s, true);
+  hipStream_t pq = spec_hit ? (pm_serial() ? s : c.part) : launch_p(a, PC, SJ, members, mlen, mpos, gstart, sbeg, err);
+  if (spec_hit) SJ = J.spec_sj;
   ht.mark("slab_build");
   const PSlab* slabs = SJ.slabs;
   const uint32_t* gslab = SJ.gslab;
   const uint64_t* gebase = SJ.gebase;
   const uint32_t* D = SJ.D;
   uint32_t* elems = SJ.elems;
-  // ---- P on its own stream, beside the Go sort ----
-  if (!c.part) {
-    int least = 0, greatest = 0;
-    SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
-  }
-  if (!c.ev_msmall) {
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall2, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_psmall, hipEventDisableTiming));
-  }
   while (c.ev_cnt.size() < 1) {
     hipEvent_t e1, e2;
     SYZ_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
@@ -659,33 +696,7 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     c.ev_cnt.push_back(e1);
     c.ev_sct.push_back(e2);
   }
-  hipStream_t pq = pm_serial() ? s : c.part;
   int* herr = c.pinned.get<int>(4);
-  SYZ_HIP(hipEventRecord(c.ev_part0, s));
-  SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
-  if (slab_bound) {
-    // byte model: the algorithm's input this pass reads, 4 B per PC + 10 B per entry
-    // (offset, group id); the element buffer it writes is intermediate traffic, not algorithmic bytes
-    // two launches: the small call groups' slabs first (their M starts once they and the small groups'
-    // sort are done, beside the big groups' slabs), then the big groups'; SYZGPU_PM_PSPLIT=0: one launch
-    const bool split = pm_psplit() && !pm_serial() && icount[0][0] + icount[0][1] + icount[0][2] > 0;
-    uint64_t cpcs[2] = {0, 0}, cent[2] = {0, 0};  // each launch's share of the byte model
-    for (uint32_t g = 0; g < G; g++) {
-      cpcs[is_big(g) ? 1 : 0] += hsl[g];
-      cent[is_big(g) ? 1 : 0] += hstart[g + 1] - hstart[g];
-    }
-    for (int cls = split ? 1 : 0; cls <= (split ? 2 : 0); cls++) {
-      const uint64_t bytes = cls ? cpcs[cls - 1] * 4 + cent[cls - 1] * 10 : total_pcs * 4 + (uint64_t)n * 10;
-      ProfScope ps("k_slab", pq, bytes);
-      launch_slab<false>(slab_bound, SJ.wmax, pq, a.pcs, a.off, members, mlen, SJ.tpos, sbeg, slabs, SJ.cstart + B,
-                         dsg, gebase, lo, elems, SJ.D, err, nullptr, NovSrc{}, cls);
-      SYZ_LAUNCHED();
-      if (cls == 1) SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
-    }
-    if (!split) SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
-  } else {
-    SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
-  }
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, pq));
   SYZ_HIP(hipEventRecord(c.ev_cnt[0], pq));
   SYZ_HIP(hipEventRecord(c.ev_sct[0], pq));
@@ -748,6 +759,7 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
   J.stats_items_direct = icount[0][PMODE_DIRECT] + icount[1][PMODE_DIRECT];
   J.stats_items_hash = icount[0][PMODE_HASH] + icount[1][PMODE_HASH] + icount[0][PMODE_PACKED] +
                        icount[1][PMODE_PACKED];
+  if (herr[0] & 64) fail(SYZGPU_EINTERNAL, "minimize: slab plan does not fit the layout");
   if (herr[0] & 1) {
     if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
     return false;
@@ -814,8 +826,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint64_t* mpos = sc.get<uint64_t>("pm_mpos", n + 1);
   uint64_t* gpack = sc.get<uint64_t>("pm_gpack", 3 * (size_t)G + 4);
   uint32_t* mlmax = sc.get<uint32_t>("pm_mlmax", 1);
-  SYZ_HIP(hipMemsetAsync(mlmax, 0, 4, s));
-  k_pm_init<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(err, gpcs, G, span);
+  k_pm_init<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(err, gpcs, G, span, mlmax);
   SYZ_LAUNCHED();
   uint32_t* krange = nullptr;
   if (a.key_lo) {
@@ -846,26 +857,39 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
       SYZ_LAUNCHED();
       SYZ_HIP(hipEventRecord(c.ev_join, c.side));
     }
-    group_partition_dev(a.group, a.off, n, G, gstart, members, el, err, s);
-    if (n) {
-      if (krange)
-        k_slices<<<grid_for(n, 256, 4096), 256, 0, s>>>(a.pcs, a.off, members, el, a.group, n, krange, sbeg, mlen);
-      else
-        k_mlen<<<grid_for(n, 256, 4096), 256, 0, s>>>(el, n, mlen);
+    // (the partition also writes the identity ranks and, for whole covers, the member lengths)
+    PartOut po;
+    po.rank_of_member = rank_of_member;
+    po.ent_of_rank = ent_of_rank;
+    po.mlen = krange ? nullptr : mlen;
+    group_partition_dev(a.group, a.off, n, G, gstart, members, el, err, s, po);
+    if (n && krange) {
+      k_slices<<<grid_for(n, 256, 4096), 256, 0, s>>>(a.pcs, a.off, members, el, a.group, n, krange, sbeg, mlen);
       SYZ_LAUNCHED();
     }
-    exclusive_scan_u32(mlen, mpos, n, s);
+    // the member slices' prefix (mpos) and the slab tiles' (tpos) in one scan
+    uint64_t* tpos = sc.get<uint64_t>("pm_sl_tpos", n + 2);
+    scan_f<2>(LenTilesFn{mlen}, n, mpos, tpos, s, "pm_mt");
     if (n) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
     k_gpack<<<grid_for(3 * (size_t)G + 4, 256, 64), 256, 0, s>>>(gstart, gpcs, span, err, mpos, G, mlmax, gpack);
     SYZ_LAUNCHED();
   }
   uint64_t* hbuf = c.pinned.get<uint64_t>(3 * (size_t)G + 8);
   SYZ_HIP(hipMemcpyAsync(hbuf, gpack, (3 * (size_t)G + 4) * 8, hipMemcpyDeviceToHost, s));
-  // work that needs no plan runs while the host plans: identity ranks, the slab tiles' prefix
-  rank_init_dev(members, n, rank_of_member, ent_of_rank, s);
-  slab_tiles(mlen, n, "pm", s);
+  if (!c.ev_spin) SYZ_HIP(hipEventCreateWithFlags(&c.ev_spin, hipEventDisableTiming));
+  SYZ_HIP(hipEventRecord(c.ev_spin, s));
+  // when the last step's plan is at hand, P on that plan runs while the host plans (a step on the same
+  // layout, the common case: begin_slab keeps it when the layout read back matches; P's guards keep a
+  // stale plan's slabs inside their buffers, err 64)
+  J.spec = false;
+  if (J.pcache && !exact_span && pm_spec() && J.pcache->n == n && J.pcache->SJ.G == G) {
+    J.spec_sj = J.pcache->SJ;
+    const hipStream_t pq = launch_p(a, *J.pcache, J.spec_sj, members, mlen, mpos, gstart, sbeg, err);
+    SYZ_HIP(hipEventRecord(c.ev_spec, pq));
+    J.spec = true;
+  }
   HostTimer ht("begin");
-  stream_wait_spin(s);
+  event_wait_spin(c.ev_spin);
   ht.mark("wait_partition");
   J.may_bounce = hbuf[3 * G + 3] >= GS_U32_LEN_LIMIT;
   if (*reinterpret_cast<int*>(hbuf + 2 * G + 2)) fail(SYZGPU_EINVAL, "group id >= ngroups");

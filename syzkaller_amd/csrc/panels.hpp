@@ -62,6 +62,7 @@ struct SlabJob {
   uint64_t* gebase = nullptr;
   uint32_t* D = nullptr;
   uint32_t* elems = nullptr;
+  uint64_t ecap = 0;         // elements the buffer holds
   uint32_t* wtot = nullptr;  // per (call, window) totals, when asked for
 };
 // hpcs: PCs each call group's members hold (their slices); S, W from hpg
@@ -105,6 +106,9 @@ struct SlabPlanCache {
   std::array<std::array<size_t, 3>, 2> ifirst{};
   uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};
   size_t o_gb = 0, o_bg = 0, o_it = 0;
+  uint64_t cpcs[2] = {0, 0}, cent[2] = {0, 0};  // PCs / entries of the small and big call groups
+  uint32_t lo = 0;
+  size_t n = 0;
   Grow<uint8_t> dstage;  // SGroup[G], gblock[G + 1], bgroup[B + 1], items
 };
 
@@ -124,6 +128,8 @@ struct MinJob {
   std::vector<uint64_t> hstart, xkey;
   std::shared_ptr<GosortPlan> plan;  // Go-sort plan of the last layout (keeps its rounds hint)
   std::shared_ptr<SlabPlanCache> pcache;  // begin_slab's plan of the last layout
+  bool spec = false;                      // this step's P was launched on pcache before the layout was read
+  SlabJob spec_sj;                        // (its device buffers)
   std::vector<uint64_t> plan_key;
   uint64_t stats_total_pcs = 0;
   size_t stats_items_direct = 0, stats_items_hash = 0;
@@ -145,8 +151,15 @@ void sel_compact_dev(const uint8_t* sel8, const uint32_t* ent_of_rank, const uin
                      int64_t* out_idx, uint64_t* group_out_off, hipStream_t s);
 
 // minimize.hip
+// group_partition_dev's optional extra outputs (k_grp_scatter)
+struct PartOut {
+  uint64_t* gstart = nullptr;          // (set by group_partition_dev)
+  uint32_t* rank_of_member = nullptr;  // identity ranks: rank_of_member[m] = m, ent_of_rank[m] = members[m]
+  uint32_t* ent_of_rank = nullptr;
+  uint32_t* mlen = nullptr;            // member lengths (whole covers)
+};
 void group_partition_dev(const uint32_t* group, const uint64_t* off, size_t n, uint32_t G, uint64_t* gstart,
-                         uint32_t* members, uint64_t* el, int* err, hipStream_t s);
+                         uint32_t* members, uint64_t* el, int* err, hipStream_t s, PartOut po = PartOut{});
 void rank_init_dev(const uint32_t* members, size_t n, uint32_t* rank_of_member, uint32_t* ent_of_rank, hipStream_t s);
 void ranks_packs(const uint64_t* el, const uint32_t* perm, const GosortPlan& P, const uint32_t* members,
                  uint32_t* rank_of_member, uint32_t* ent_of_rank, hipStream_t q);

@@ -5,6 +5,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "scan.hpp"
 #include "store.hpp"
 
 namespace syz {
@@ -158,7 +159,8 @@ static void free_lane(Context* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->part) (void)hipStreamDestroy(c->part);
   if (c->cap) (void)hipStreamDestroy(c->cap);
-  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_part0, c->ev_part1, c->ev_msmall, c->ev_msmall2, c->ev_psmall})
+  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_part0, c->ev_part1, c->ev_msmall, c->ev_msmall2, c->ev_psmall,
+                       c->ev_spec, c->ev_spin})
     if (e) (void)hipEventDestroy(e);
   for (auto& row : c->gl_exec)
     for (auto& g : row)
@@ -200,96 +202,64 @@ void Prof::end(size_t rec, hipStream_t s) {
   SYZ_HIP(hipEventRecord(recs[rec].b, s));
 }
 
-// ---- device-wide exclusive scan: reduce tiles, scan tile sums (recursively), add back ----------
-constexpr int SCAN_BLOCK = 256;
-constexpr int SCAN_ITEMS = 16;
-constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+// ---- device-wide exclusive scans (scan.hpp) ------------------------------------------------------------
+__global__ void k_scan_zero(uint64_t* out0, uint64_t* out1) {
+  out0[0] = 0;
+  if (out1) out1[0] = 0;
+}
 
-template <class T>
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const T* in, size_t n, uint64_t* sums) {
-  __shared__ uint64_t lds[SCAN_BLOCK / 64 + 1];
-  const size_t base = (size_t)blockIdx.x * SCAN_TILE;
-  uint64_t s = 0;
-#pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; k++) {
-    size_t i = base + (size_t)k * SCAN_BLOCK + threadIdx.x;
-    if (i < n) s += (uint64_t)in[i];
+ScanState scan_state(const char* tag, size_t tiles, int nv, hipStream_t s) {
+  if (tiles >= 0xFFFFFFFFull) fail(SYZGPU_EINVAL, "scan too long");
+  Context& c = ctx();
+  // per tag and stream: scans on other streams never share a ticket or words
+  char sk[32];
+  snprintf(sk, sizeof sk, "_%p", (void*)s);
+  const std::string key = std::string("scan1_") + tag + sk;
+  const size_t words = 32 + tiles * nv;  // [0, 32): the ticket's line
+  uint64_t* buf = c.scratch.get<uint64_t>(key, words);
+  auto& ep = c.scan_epoch[key];
+  // a new or grown buffer (its memory may hold anything, the ticket too), or the epochs ran out: cleared
+  if (ep.first != buf || ep.second.first < words || ep.second.second >= 63) {
+    SYZ_HIP(hipMemsetAsync(buf, 0, words * 8, s));
+    ep = {buf, {words, 0u}};
   }
-  uint64_t tot = block_sum<SCAN_BLOCK>(s, lds);
-  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+  ep.second.second++;
+  return ScanState{buf + 32, reinterpret_cast<uint32_t*>(buf), ep.second.second};
 }
 
 template <class T>
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const T* in, size_t n, const uint64_t* offs,
-                                                           uint64_t* out, int write_total) {
-  __shared__ uint64_t lds[SCAN_BLOCK / 64 + 1];
-  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
-  uint64_t v[SCAN_ITEMS];
-  uint64_t s = 0;
-#pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; k++) {
-    size_t i = base + k;
-    v[k] = i < n ? (uint64_t)in[i] : 0;
-    s += v[k];
-  }
-  uint64_t tot;
-  uint64_t pre = block_excl_scan<SCAN_BLOCK>(s, lds, &tot) + offs[blockIdx.x];
-#pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; k++) {
-    size_t i = base + k;
-    if (i < n) out[i] = pre;
-    pre += v[k];
-  }
-  if (write_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) out[n] = pre;
-}
-
-__global__ void k_zero_total(uint64_t* out) { out[0] = 0; }
-
-template <class T>
-static void scan_impl(const T* in, uint64_t* out, size_t n, hipStream_t s, int depth, const char* tag = "") {
-  if (n == 0) {
-    k_zero_total<<<1, 1, 0, s>>>(out);
-    SYZ_LAUNCHED();
-    return;
-  }
-  const size_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  Scratch& sc = ctx().scratch;
-  uint64_t* sums = sc.get<uint64_t>(std::string("scan_sums") + tag + std::to_string(depth), tiles + 1);
-  uint64_t* offs = sc.get<uint64_t>(std::string("scan_offs") + tag + std::to_string(depth), tiles + 1);
-  if (tiles == 1) {
-    SYZ_HIP(hipMemsetAsync(offs, 0, sizeof(uint64_t), s));
-  } else {
-    k_scan_reduce<T><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, sums);
-    SYZ_LAUNCHED();
-    scan_impl<uint64_t>(sums, offs, tiles, s, depth + 1, tag);
-  }
-  k_scan_apply<T><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(in, n, offs, out, 1);
-  SYZ_LAUNCHED();
-}
+struct LoadFn {
+  const T* in;
+  __device__ void operator()(size_t i, uint64_t* v) const { v[0] = (uint64_t)in[i]; }
+};
 
 void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s) {
-  scan_impl<uint8_t>(in, out, n, s, 0);
+  scan_f<1>(LoadFn<uint8_t>{in}, n, out, nullptr, s, "u8");
 }
 void exclusive_scan_u32(const uint32_t* in, uint64_t* out, size_t n, hipStream_t s, const char* tag) {
-  scan_impl<uint32_t>(in, out, n, s, 0, tag);
+  scan_f<1>(LoadFn<uint32_t>{in}, n, out, nullptr, s, tag);
 }
 void stream_wait_spin(hipStream_t s) {
   Context& c = ctx();
   if (!c.ev_spin) SYZ_HIP(hipEventCreateWithFlags(&c.ev_spin, hipEventDisableTiming));
   SYZ_HIP(hipEventRecord(c.ev_spin, s));
+  event_wait_spin(c.ev_spin);
+}
+
+void event_wait_spin(hipEvent_t e) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    const hipError_t r = hipEventQuery(c.ev_spin);
+    const hipError_t r = hipEventQuery(e);
     if (r == hipSuccess) return;
     if (r != hipErrorNotReady) SYZ_HIP(r);
     if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
     __builtin_ia32_pause();
   }
-  SYZ_HIP(hipEventSynchronize(c.ev_spin));
+  SYZ_HIP(hipEventSynchronize(e));
 }
 
 void exclusive_scan_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s) {
-  scan_impl<uint64_t>(in, out, n, s, 0);
+  scan_f<1>(LoadFn<uint64_t>{in}, n, out, nullptr, s, "u64");
 }
 
 }  // namespace syz

@@ -1006,11 +1006,11 @@ __global__ __launch_bounds__(256) void k_canon_prefix(const uint32_t* __restrict
   }
 }
 
-// Classes by length; a cover flagged in cand (its prefix increases) goes to the extra class CANON_NCLS
-// instead, for the canonical-cover check.
+// Classes by length; a cover flagged in cand (its prefix increases) is left to the canonical-cover check
+// (k_canon_runs), which lists it in its class only if it fails.
 __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t ncov, uint32_t* lists, size_t cap,
                                                      uint32_t* cnt, const uint8_t* cand = nullptr) {
-  constexpr int NC = CANON_NCLS + 1;
+  constexpr int NC = CANON_NCLS;
   __shared__ uint32_t lc[NC], lb[NC];
   const unsigned lane = __lane_id();
   for (size_t c0 = (size_t)blockIdx.x * CANON_CHUNK; c0 < ncov; c0 += (size_t)gridDim.x * CANON_CHUNK) {
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t
 #pragma unroll
     for (int q = 0; q < PER; q++) {
       const size_t i = c0 + (size_t)q * blockDim.x + threadIdx.x;
-      cls[q] = i >= ncov ? -1 : (cand && cand[i]) ? CANON_NCLS : canon_class_of(off[i + 1] - off[i]);
+      cls[q] = (i >= ncov || (cand && cand[i])) ? -1 : canon_class_of(off[i + 1] - off[i]);
     }
     for (int pass = 0; pass < 2; pass++) {  // 0: counts; 1: entries at the reserved bases
 #pragma unroll
@@ -1051,72 +1051,77 @@ __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t
   }
 }
 
-// Already-canonical covers (the executor's dedup on, executor.cc:565-585 -> fuzzer.go:355): the class
-// kernel lists the covers whose first CANON_PRE PCs increase; one wave per such candidate streams the
-// whole cover once, CANON_SCAN_U x 64 PCs a step (lane i of load k at PC 64 k + i), and checks every PC
-// against the one before it (the lane before, the last lane of the load before, the previous step's
-// last PC), stopping at the first violation. A strictly increasing cover is its own Canonicalize
-// (sorted, no repeat; a 0xFFFFFFFF can only be its last PC, kept unless it is the only one): its length
-// goes to out_len and no network touches it. A candidate that fails joins its length class.
+// Already-canonical covers (the executor's dedup on, executor.cc:565-585 -> fuzzer.go:355): k_canon_prefix
+// flags the covers whose first CANON_PRE PCs increase (candidates); here one wave takes 64 consecutive
+// covers and streams each maximal run of consecutive candidates as ONE contiguous range of PCs
+// (CANON_SCAN_U x 64 PCs a step, lane i of load k at PC 64 k + i), checking every PC against the one
+// before it. A break inside the run is either a cover start (the next cover's first PC) or a violation:
+// the wave resolves it by a ballot over its covers' start offsets (one per lane) and flags the cover. A
+// strictly increasing cover is its own Canonicalize (sorted, no repeat; a 0xFFFFFFFF can only be its
+// last PC, kept unless it is the only one): its length goes to out_len and no network touches it. A
+// flagged candidate joins its length class. With every cover a candidate (the sorted batch) the pass is
+// one coalesced stream over the PCs.
 #ifndef SYZ_CANON_SCAN_U
 #define SYZ_CANON_SCAN_U 8
 #endif
 constexpr int CANON_SCAN_U = SYZ_CANON_SCAN_U;
-__global__ __launch_bounds__(256) void k_canon_sorted(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ cand, const uint32_t* ncand_dev,
-                                                      uint32_t* __restrict__ lists, size_t cap, uint32_t* cnt,
-                                                      uint64_t* __restrict__ out_len) {
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+}
+__global__ __launch_bounds__(256) void k_canon_runs(const uint32_t* __restrict__ pcs, const uint64_t* __restrict__ off,
+                                                    size_t ncov, const uint8_t* __restrict__ cand,
+                                                    uint32_t* __restrict__ lists, size_t cap, uint32_t* cnt,
+                                                    uint64_t* __restrict__ out_len) {
   const unsigned lane = __lane_id();
-  const uint32_t ncand = *ncand_dev;
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  uint32_t ci = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  // the wave's next candidate and its bounds are read one cover ahead (lane 0: index, lanes 1, 2: the
-  // offsets), so a cover's loads wait only for its own data
-  auto meta = [&](uint32_t c) -> uint64_t {
-    uint64_t x = 0;
-    if (c < ncand) {
-      const uint32_t i = cand[c];
-      x = lane == 0 ? i : lane == 1 ? off[i] : lane == 2 ? off[i + 1] : 0;
-    }
-    return x;
-  };
-  uint64_t m = meta(ci);
-  for (; ci < ncand; ci += nw) {
-    const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, 0);
-    const uint64_t b = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), 1) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, 1);
-    const uint64_t e = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), 2) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, 2);
-    const uint64_t n = e - b;
-    const uint32_t* x = pcs + b;
-    bool bad = false;
-    uint32_t last = 0;  // the PC before this step's first (none at the start)
-    for (uint64_t j0 = 0; j0 < n && !bad; j0 += 64 * CANON_SCAN_U) {
-      uint32_t v[CANON_SCAN_U];
+  const size_t nw = (size_t)gridDim.x * (blockDim.x >> 6);
+  for (size_t c0 = ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; c0 < ncov; c0 += nw * 64) {
+    const size_t c = c0 + lane;
+    const bool has = c < ncov;
+    const uint64_t ob = off[has ? c : ncov], oe = has ? off[c + 1] : ob;
+    const bool ca = has && cand[c];
+    uint64_t cm = __ballot(ca);
+    bool mybad = false;
+    while (cm) {
+      const int s = __ffsll((unsigned long long)cm) - 1;
+      const uint64_t inv = ~cm & (~0ull << s);  // lanes at or after s that are not candidates
+      const int e = inv ? __ffsll((unsigned long long)inv) - 1 : 64;
+      cm = e >= 64 ? 0 : (cm & (~0ull << e));
+      const uint64_t jb = readlane64(ob, s), je = readlane64(oe, e - 1);
+      const bool inrun = (int)lane >= s && (int)lane < e;
+      const uint32_t* x = pcs;
+      uint32_t last = 0;
+      for (uint64_t j0 = jb; j0 < je; j0 += 64 * CANON_SCAN_U) {
+        uint32_t v[CANON_SCAN_U];
 #pragma unroll
-      for (int k = 0; k < CANON_SCAN_U; k++) {
-        const uint64_t j = j0 + 64 * k + lane;
-        v[k] = j < n ? x[j] : 0xFFFFFFFFu;
-      }
-      if (j0 == 0) m = meta(ci + nw);  // (issued behind this cover's first loads)
-      bool b2 = false;
+        for (int k = 0; k < CANON_SCAN_U; k++) {
+          const uint64_t j = j0 + 64 * k + lane;
+          v[k] = j < je ? x[j] : 0xFFFFFFFFu;
+        }
 #pragma unroll
-      for (int k = 0; k < CANON_SCAN_U; k++) {
-        const uint64_t j = j0 + 64 * k + lane;
-        uint32_t prev = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k], 0x138, 0xF, 0xF, false);  // lane - 1
-        if (lane == 0) prev = last;
-        if (j < n && j > 0 && prev >= v[k]) b2 = true;
-        last = (uint32_t)__builtin_amdgcn_readlane((int)v[k], 63);
+        for (int k = 0; k < CANON_SCAN_U; k++) {
+          const uint64_t j = j0 + 64 * k + lane;
+          uint32_t prev = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k], 0x138, 0xF, 0xF, false);  // lane - 1
+          if (lane == 0) prev = k == 0 ? last : (uint32_t)__builtin_amdgcn_readlane((int)v[k - 1], 63);
+          uint64_t vm = __ballot(j < je && j > jb && prev >= v[k]);
+          while (vm) {  // a cover start or a violation: the cover holding PC jj
+            const int bl = __ffsll((unsigned long long)vm) - 1;
+            vm &= vm - 1;
+            const uint64_t jj = j0 + 64 * k + bl;
+            const int L = s + __popcll(__ballot(inrun && ob <= jj)) - 1;
+            if (readlane64(ob, L) != jj && (int)lane == L) mybad = true;
+          }
+        }
+        last = (uint32_t)__builtin_amdgcn_readlane((int)v[CANON_SCAN_U - 1], 63);
       }
-      bad = __ballot(b2) != 0;
     }
-    if (n == 0) m = meta(ci + nw);
-    if (lane == 0) {
-      if (!bad) {
-        out_len[i] = (n == 1 && x[0] == 0xFFFFFFFFu) ? 0 : n;
+    if (ca) {
+      const uint64_t n = oe - ob;
+      if (!mybad) {
+        out_len[c] = (n == 1 && pcs[ob] == 0xFFFFFFFFu) ? 0 : n;
       } else {  // not canonical after all: the network of its length class
         const int k = canon_class_of(n);
-        lists[(size_t)k * cap + atomicAdd(&cnt[k], 1u)] = i;
+        lists[(size_t)k * cap + atomicAdd(&cnt[k], 1u)] = (uint32_t)c;
       }
     }
   }
@@ -1134,9 +1139,9 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   Context& c = ctx();
   if (ncov == 0) return;
   if (ncov >= 0xFFFFFFF0ull) fail(SYZGPU_EINVAL, "too many covers");
-  uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", (CANON_NCLS + 1) * ncov);
-  uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", CANON_NCLS + 1);
-  SYZ_HIP(hipMemsetAsync(cnt, 0, (CANON_NCLS + 1) * 4, s));
+  uint32_t* lists = c.scratch.get<uint32_t>("cd_lists", CANON_NCLS * ncov);
+  uint32_t* cnt = c.scratch.get<uint32_t>("cd_cnt", CANON_NCLS);
+  SYZ_HIP(hipMemsetAsync(cnt, 0, CANON_NCLS * 4, s));
   // classes by length; covers with an increasing prefix are checked whole first: canonical ones are
   // done (no network), the others join their class before the class kernels run
   uint8_t* cand = c.scratch.get<uint8_t>("cd_cand", ncov + 1);
@@ -1150,9 +1155,8 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   }
   {
     ProfScope ps("canon_check", s, 0);
-    k_canon_sorted<<<(unsigned)std::min<size_t>((ncov + 3) / 4, 8192), 256, 0, s>>>(pcs, off, lists + CANON_NCLS * ncov,
-                                                                                    cnt + CANON_NCLS, lists, ncov, cnt,
-                                                                                    out_len);
+    k_canon_runs<<<(unsigned)std::min<size_t>((ncov + 255) / 256, 8192), 256, 0, s>>>(pcs, off, ncov, cand, lists,
+                                                                                      ncov, cnt, out_len);
     SYZ_LAUNCHED();
   }
   if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));

@@ -21,6 +21,7 @@
 #include <atomic>
 
 #include "panels_dev.hpp"
+#include "scan.hpp"
 
 namespace syz {
 
@@ -45,63 +46,82 @@ __device__ __forceinline__ uint32_t lane_prev(uint32_t x) {
 }
 
 // ---- slab planning on the device ------------------------------------------------------------------
-static __global__ void k_sl_tiles(const uint32_t* mlen, size_t n, uint32_t* mtile) {
-  for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x)
-    mtile[m] = (mlen[m] + 63) >> 6;
-}
+// tiles per member, and the member lengths with them (one scan gives mpos and tpos)
+struct TilesFn {
+  const uint32_t* mlen;
+  __device__ void operator()(size_t m, uint64_t* v) const { v[0] = (mlen[m] + 63) >> 6; }
+};
+struct LenTilesFn {
+  const uint32_t* mlen;
+  __device__ void operator()(size_t m, uint64_t* v) const {
+    const uint32_t l = mlen[m];
+    v[0] = l;
+    v[1] = (l + 63) >> 6;
+  }
+};
 
-// slabs per block of memb members
-static __global__ void k_sl_blocks(const uint32_t* bgroup, uint32_t B, const uint32_t* gblock, const uint64_t* gstart,
-                            const SGroup* sg, const uint64_t* tpos, uint32_t* nsub) {
-  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) {
+// slabs per block of memb members (the scan's input: cstart = its prefix)
+struct BlockSlabsFn {
+  const uint32_t* bgroup;
+  const uint32_t* gblock;
+  const uint64_t* gstart;
+  const SGroup* sg;
+  const uint64_t* tpos;
+  __device__ void operator()(size_t b, uint64_t* v) const {
     const uint32_t g = bgroup[b];
     const uint32_t mb_ = sg[g].memb;
-    const uint64_t mb = gstart[g] + (uint64_t)(b - gblock[g]) * mb_;
+    // (clamped: a plan run speculatively on another layout may hold more blocks than the group needs)
+    const uint64_t mb = min<uint64_t>(gstart[g] + (uint64_t)(b - gblock[g]) * mb_, gstart[g + 1]);
     const uint64_t me = min<uint64_t>(mb + mb_, gstart[g + 1]);
-    nsub[b] = (uint32_t)((tpos[me] - tpos[mb] + SL_TILES - 1) / SL_TILES);
+    v[0] = (tpos[me] - tpos[mb] + SL_TILES - 1) / SL_TILES;
   }
+};
+
+// slab c of block b (cstart[b] <= c < cstart[b + 1])
+__device__ __forceinline__ PSlab slab_at(uint64_t c, uint32_t b, const uint32_t* bgroup, const uint32_t* gblock,
+                                         const uint64_t* gstart, const SGroup* sg, const uint64_t* tpos,
+                                         const uint64_t* mpos, const uint64_t* cstart) {
+  const uint32_t g = bgroup[b];
+  const uint32_t mb_ = sg[g].memb;
+  const uint64_t mb = min<uint64_t>(gstart[g] + (uint64_t)(b - gblock[g]) * mb_, gstart[g + 1]);
+  const uint64_t me = min<uint64_t>(mb + mb_, gstart[g + 1]);
+  const uint64_t T0 = tpos[mb] + (c - cstart[b]) * SL_TILES;
+  const uint64_t T1 = min<uint64_t>(T0 + SL_TILES, tpos[me]);
+  // the member holding tile T0: the first m with tpos[m + 1] > T0; the one holding T1 - 1 likewise
+  const uint64_t m0 = upper_bound_dev<uint64_t>(tpos, mb + 1, me + 1, T0) - 1;
+  const uint64_t m1 = upper_bound_dev<uint64_t>(tpos, m0 + 1, me + 1, T1 - 1) - 1;
+  const uint64_t pcpos = mpos[m0] + 64 * (T0 - tpos[m0]);  // the slab's first PC in the slices' order
+  PSlab s;
+  // PCs before it + the padding slots of every slab before it (at most slab_pad(W) each), 4-aligned
+  const SGroup gp = sg[g];
+  s.elem = (pcpos + gp.xbase + (c - cstart[gblock[g]]) * slab_pad(gp.W) + 3) & ~3ull;
+  s.t0 = T0;
+  s.m0 = (uint32_t)m0;
+  s.nmem = (uint32_t)(m1 - m0 + 1);
+  s.nt = (uint32_t)(T1 - T0);
+  s.g = g;
+  s.j = (uint32_t)(c - cstart[gblock[g]]);
+  s.pad = 0;
+  return s;
 }
 
-// one thread per slab (grid over a bound; cstart[B] = the slabs there are)
+// one thread per slab (grid over a bound; cstart[B] = the slabs there are); the first G + 1 threads
+// also write gslab[g] = the group's first slab (gslab[G] = all of them) and gebase[g] = its first element
 static __global__ void k_sl_slabs(const uint32_t* bgroup, uint32_t B, const uint32_t* gblock, const uint64_t* gstart,
-                           const SGroup* sg, const uint64_t* tpos, const uint64_t* mpos, const uint64_t* cstart,
-                           uint64_t bound, PSlab* slabs) {
+                                  const SGroup* sg, const uint64_t* tpos, const uint64_t* mpos, const uint64_t* cstart,
+                                  uint64_t bound, PSlab* slabs, uint32_t G, uint32_t* gslab, uint64_t* gebase) {
   const uint64_t ns = cstart[B];
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < min(ns, bound);
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t b = (uint32_t)upper_bound_dev<uint64_t>(cstart, 0, B + 1, c) - 1;  // cstart[b] <= c < cstart[b+1]
-    const uint32_t g = bgroup[b];
-    const uint32_t mb_ = sg[g].memb;
-    const uint64_t mb = gstart[g] + (uint64_t)(b - gblock[g]) * mb_;
-    const uint64_t me = min<uint64_t>(mb + mb_, gstart[g + 1]);
-    const uint64_t T0 = tpos[mb] + (c - cstart[b]) * SL_TILES;
-    const uint64_t T1 = min<uint64_t>(T0 + SL_TILES, tpos[me]);
-    // the member holding tile T0: the first m with tpos[m + 1] > T0; the one holding T1 - 1 likewise
-    const uint64_t m0 = upper_bound_dev<uint64_t>(tpos, mb + 1, me + 1, T0) - 1;
-    const uint64_t m1 = upper_bound_dev<uint64_t>(tpos, m0 + 1, me + 1, T1 - 1) - 1;
-    const uint64_t pcpos = mpos[m0] + 64 * (T0 - tpos[m0]);  // the slab's first PC in the slices' order
-    PSlab s;
-    // PCs before it + the padding slots of every slab before it (at most slab_pad(W) each), 4-aligned
-    const SGroup gp = sg[g];
-    s.elem = (pcpos + gp.xbase + (c - cstart[gblock[g]]) * slab_pad(gp.W) + 3) & ~3ull;
-    s.t0 = T0;
-    s.m0 = (uint32_t)m0;
-    s.nmem = (uint32_t)(m1 - m0 + 1);
-    s.nt = (uint32_t)(T1 - T0);
-    s.g = g;
-    s.j = (uint32_t)(c - cstart[gblock[g]]);
-    s.pad = 0;
-    slabs[c] = s;
-  }
-}
-
-// gslab[g] = the group's first slab (gslab[G] = all of them), gebase[g] = its first element
-static __global__ void k_sl_groups(const uint32_t* gblock, uint32_t G, const uint64_t* cstart, const PSlab* slabs,
-                            uint32_t* gslab, uint64_t* gebase) {
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x) {
-    const uint64_t c = cstart[gblock[g]];
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t g = i0; g <= G; g += step) {
+    const uint32_t b = gblock[g];
+    const uint64_t c = cstart[b];
     gslab[g] = (uint32_t)c;
-    if (g < G) gebase[g] = c < cstart[gblock[g + 1]] ? slabs[c].elem : 0;
+    if (g < G) gebase[g] = c < cstart[gblock[g + 1]] && c < bound ? slab_at(c, b, bgroup, gblock, gstart, sg, tpos, mpos,
+                                                                           cstart).elem : 0;
+  }
+  for (uint64_t c = i0; c < min(ns, bound); c += step) {
+    const uint32_t b = (uint32_t)upper_bound_dev<uint64_t>(cstart, 0, B + 1, c) - 1;  // cstart[b] <= c < cstart[b+1]
+    slabs[c] = slab_at(c, b, bgroup, gblock, gstart, sg, tpos, mpos, cstart);
   }
 }
 
@@ -128,7 +148,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const uint32_t* __restrict__ mlen, const uint64_t* __restrict__ tpos, const uint32_t* __restrict__ sbeg,
     const PSlab* __restrict__ slabs, const uint64_t* nslab, const SGroup* __restrict__ sg,
     const uint64_t* __restrict__ gebase, uint32_t lo, uint32_t* __restrict__ elems, uint32_t* __restrict__ D,
-    int* err, uint32_t Wmax, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int cls = 0) {
+    int* err, uint32_t Wmax, uint64_t ecap, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int cls = 0) {
   constexpr int WAVES = BLOCK / 64;
   static_assert((uint32_t)TPW * WAVES == SL_TILES, "slab tiles");
   extern __shared__ __align__(16) uint32_t slds[];
@@ -153,6 +173,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   // cls 1 / 2: only the slabs of small / big call groups (SGroup.pad bit 0)
   if (cls && (gp.pad & 1u) != (uint32_t)(cls - 1)) return;
   const uint32_t S = gp.S, W = gp.W, nt = sl.nt, nmem = sl.nmem;
+  // a plan that does not fit this layout (run speculatively before the layout was read back): the
+  // slab's D column, staging or elements (checked at the store) would fall outside their buffers;
+  // flagged (err 64) and redone
+  if (sl.j >= gp.stride || W > Wmax) {
+    if (threadIdx.x == 0) atomicOr(err, 64);
+    return;
+  }
   for (uint32_t i = threadIdx.x; i < nmem; i += BLOCK) {
     const uint64_t m = (uint64_t)sl.m0 + i;
     const int64_t r = (int64_t)tpos[m] - (int64_t)sl.t0;
@@ -302,6 +329,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     for (uint32_t e = hist[i]; e < pst[i + 1]; e++) obuf[e] = SL_NONE;
   __syncthreads();
   // the slab leaves as one run of 16-byte stores (sl.elem and total are multiples of 4)
+  if (sl.elem + total > ecap) {
+    if (threadIdx.x == 0) atomicOr(err, 64);
+    return;
+  }
   {
     uint4* g4 = reinterpret_cast<uint4*>(elems + sl.elem);
     const uint4* o4 = reinterpret_cast<const uint4*>(obuf);
@@ -315,7 +346,8 @@ template <bool NOV>
 inline void launch_slab(uint64_t nslabs, uint32_t Wmax, hipStream_t s, const uint32_t* pcs, const uint64_t* off,
                         const uint32_t* members, const uint32_t* mlen, const uint64_t* tpos, const uint32_t* sbeg,
                         const PSlab* slabs, const uint64_t* nslab, const SGroup* sg, const uint64_t* gebase,
-                        uint32_t lo, uint32_t* elems, uint32_t* D, int* err, uint32_t* wtot, NovSrc ns, int cls) {
+                        uint32_t lo, uint32_t* elems, uint64_t ecap, uint32_t* D, int* err, uint32_t* wtot,
+                        NovSrc ns, int cls) {
   if (!nslabs) return;
   const size_t bytes = slab_lds_bytes(Wmax);
   static std::atomic<size_t> raised{0};
@@ -328,7 +360,7 @@ inline void launch_slab(uint64_t nslabs, uint32_t Wmax, hipStream_t s, const uin
   }
   k_slab<SL_BLOCK, SL_TPW, NOV><<<(unsigned)nslabs, SL_BLOCK, bytes, s>>>(pcs, off, members, mlen, tpos, sbeg, slabs,
                                                                          nslab, sg, gebase, lo, elems, D, err, Wmax,
-                                                                         wtot, ns, cls);
+                                                                         ecap, wtot, ns, cls);
   SYZ_LAUNCHED();
 }
 

@@ -6,6 +6,7 @@ Go's per-op float32 rounding, so the test demands identical bits). Layout mirror
 cover/cover_test.go: the known-answer tables first, then seeded random/property cases, then the
 BASELINE.json configs at sizes the oracle finishes in seconds.
 """
+import copy
 import os
 import sys
 
@@ -340,6 +341,36 @@ def test_minimize_corpus_few_big_groups():
     c = synth.corpus(77, 60_000, 3, 3000, len_median=3.0, len_sigma=0.5)
     c.pcs[c.off[1:-1][::97].astype(np.int64) - 1] = 0xFFFFFFFF  # last PC of some covers
     _grouped_parity(c)
+
+
+def _mirror_covers(c):
+    # the same layout (entries, groups, cover lengths, PC span) with different PCs: each cover mapped by
+    # pc -> lo + hi - pc and reversed, so it stays strictly increasing
+    lo, hi = int(c.pcs.min()), int(c.pcs.max())
+    lens = np.diff(c.off).astype(np.int64)
+    ent = np.repeat(np.arange(c.n), lens)
+    j = np.arange(len(c.pcs), dtype=np.int64)
+    src = c.off[ent].astype(np.int64) + c.off[ent + 1].astype(np.int64) - 1 - j
+    m = copy.copy(c)
+    m.pcs = (np.uint64(lo + hi) - c.pcs[src].astype(np.uint64)).astype(np.uint32)
+    return m
+
+
+def test_minimize_speculative_plan_reuse():
+    # minimize launches P on the last step's plan before it reads the layout back (panels.hip
+    # begin_once): same layout (kept), same layout with other PCs (kept: the plan is a function of the
+    # layout only), and another layout of the same size (the stale plan's P is discarded), alternating
+    a = synth.corpus(0x5EED0011, 20_000, 289, 100_000)
+    b = synth.corpus(0x5EED0012, 20_000, 289, 100_000)
+    am = _mirror_covers(a)
+    want = {}
+    for name, c in (("a", a), ("b", b), ("am", am)):
+        want[name] = oracle.minimize_grouped(c.pcs, c.off, c.group, c.ngroups)
+    for name in ["a", "a", "am", "b", "a", "am", "am", "b", "b", "a"]:
+        c = {"a": a, "b": b, "am": am}[name]
+        got, goff = cover.MinimizeCorpus(c.pcs, c.off, c.group, c.ngroups)
+        assert np.array_equal(want[name][1], goff), name
+        assert np.array_equal(want[name][0], got), name
 
 
 def test_minimize_corpus_property_full_size():
