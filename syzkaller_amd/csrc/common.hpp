@@ -97,6 +97,7 @@ struct Context {
   hipStream_t stream = nullptr;  // library-owned stream for host-pointer entry points
   Scratch scratch;
   Pinned pinned;
+  Pinned pinned_err;  // the raw Minimize's P flags (panels.hip launch_step)
   // the last minimize of this lane (for syzgpu_minimize_grouped_fetch): which thread ran it, on
   // which job; fetch on another thread or after the lane served someone else reports EINVAL
   std::thread::id last_thread;
@@ -115,7 +116,6 @@ struct Context {
   hipEvent_t ev_part0 = nullptr, ev_part1 = nullptr;
   hipEvent_t ev_msmall = nullptr, ev_msmall2 = nullptr;  // the small groups' packed M on another stream
   hipEvent_t ev_psmall = nullptr;  // P's slabs of the small call groups are cut
-  hipEvent_t ev_spec = nullptr;    // the end of a speculative P (panels.hip begin_once)
   hipEvent_t ev_spin = nullptr;    // stream_wait_spin's marker
   hipStream_t part2 = nullptr;  // its scatter passes, batch after batch beside the next batch's count
   std::vector<hipEvent_t> ev_cnt, ev_sct;  // per batch: count done, scatter done

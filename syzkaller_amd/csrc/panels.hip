@@ -451,7 +451,7 @@ static bool pm_psplit() {
   return v;
 }
 
-// SYZGPU_PM_SPEC=0 (A/B): no speculative P on the last step's plan (begin_once)
+// SYZGPU_PM_SPEC=0 (A/B): no speculative step on the last step's plans (begin_once)
 static bool pm_spec() {
   static const bool v = !getenv("SYZGPU_PM_SPEC") || atoi(getenv("SYZGPU_PM_SPEC")) != 0;
   return v;
@@ -524,22 +524,21 @@ void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint
 }
 
 
-// P for one plan: the plan's slab table (slab_build on s), then the transpose on the part stream
-// (pm_serial: on s); SYZGPU_PM_PSPLIT=1: the small call groups' slabs as a launch of their own first.
-// ev_psmall marks the small groups' slabs, the caller records the rest.
+// P for one plan on the part stream (pm_serial: on s): the plan's slab table (slab_build), then the
+// transpose, so the main stream goes from the partition straight into the Go sort (the step's critical
+// path); SYZGPU_PM_PSPLIT=1: the small call groups' slabs as a launch of their own first. ev_psmall
+// marks the small groups' slabs, the caller records the rest.
 static hipStream_t launch_p(const RawMinArgs& a, const SlabPlanCache& PC, SlabJob& SJ, const uint32_t* members,
                             const uint32_t* mlen, const uint64_t* mpos, const uint64_t* gstart, const uint32_t* sbeg,
                             int* err) {
   Context& c = ctx();
   hipStream_t s = a.s;
-  slab_build(SJ, "pm", mlen, mpos, a.n, gstart, s, true);
   if (!c.part) {
     int least = 0, greatest = 0;
     SYZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
     SYZ_HIP(hipStreamCreateWithPriority(&c.part, hipStreamNonBlocking, least));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_spec, hipEventDisableTiming));
   }
   if (!c.ev_msmall) {
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall, hipEventDisableTiming));
@@ -549,6 +548,7 @@ static hipStream_t launch_p(const RawMinArgs& a, const SlabPlanCache& PC, SlabJo
   hipStream_t pq = pm_serial() ? s : c.part;
   SYZ_HIP(hipEventRecord(c.ev_part0, s));
   SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
+  slab_build(SJ, "pm", mlen, mpos, a.n, gstart, pq, true);
   if (!SJ.slab_bound) {
     SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
     return pq;
@@ -571,43 +571,33 @@ static hipStream_t launch_p(const RawMinArgs& a, const SlabPlanCache& PC, SlabJo
   return pq;
 }
 
-// The slab form (slab_dev.hpp): one read of the covers. Inputs from begin_once's common part: the
-// group partition (members, el, mlen, mpos), the per-group PC counts and read slices, the windows.
-static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_t>& hstart,
-                       const std::vector<uint64_t>& hpcs, const uint64_t* hsl, const std::vector<PGroup>& hpg,
-                       uint32_t lo, uint32_t hi, const uint32_t* exact_span, const uint32_t* members, uint64_t* el,
-                       const uint32_t* mlen, const uint64_t* mpos, const uint32_t* sbeg, int* err) {
+// The plan of a layout: the slabs' layout and the M work items, a pure function of the group sizes, the
+// PCs each group reads, the span and the key ranges (plan_key). A step on the same layout reuses the
+// previous one's (host structures and the staged device copy owned by the job).
+static std::vector<uint64_t> plan_key(const RawMinArgs& a, const std::vector<uint64_t>& hstart, const uint64_t* hsl,
+                                      uint32_t lo, uint32_t hi, bool may_bounce) {
+  const uint32_t G = a.G;
+  std::vector<uint64_t> key(hstart);
+  key.insert(key.end(), hsl, hsl + G);
+  key.push_back(((uint64_t)lo << 32) | hi);
+  key.push_back(may_bounce);
+  if (a.key_lo)
+    for (uint32_t g = 0; g < G; g++) key.push_back(((uint64_t)a.key_lo[g] << 32) | a.key_hi[g]);
+  return key;
+}
+
+static void plan_layout(MinJob& J, const RawMinArgs& a, const std::vector<uint64_t>& hstart,
+                        const std::vector<uint64_t>& hpcs, const uint64_t* hsl_in, const std::vector<PGroup>& hpg,
+                        uint32_t lo, uint32_t hi) {
   Context& c = ctx();
-  Scratch& sc = c.scratch;
   const size_t n = a.n;
   const uint32_t G = a.G;
   hipStream_t s = a.s;
-  uint64_t* gstart = J.gstart.p;
-  uint32_t* rank_of_member = J.rank_of_member.p;
-  uint32_t* ent_of_rank = J.ent_of_rank.p;
-  uint8_t* sel8 = J.sel8.p;
-  HostTimer ht("begin_slab");
   // (hsl points into the lane's pinned buffer, which the plan's staging copy below reuses)
-  const std::vector<uint64_t> hslv(hsl, hsl + G);
-  hsl = hslv.data();
+  const std::vector<uint64_t> hslv(hsl_in, hsl_in + G);
+  const uint64_t* hsl = hslv.data();
   const auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
-  // The plan (slabs' layout, work items) is a pure function of the group sizes, the PCs each group
-  // reads, the span and the key ranges: a step on the same layout reuses the previous one's (host
-  // structures and the staged device copy owned by the job), so only the device work is redone.
-  std::vector<uint64_t> key(hstart);
-  key.insert(key.end(), hslv.begin(), hslv.end());
-  key.push_back(((uint64_t)lo << 32) | hi);
-  if (a.key_lo)
-    for (uint32_t g = 0; g < G; g++) key.push_back(((uint64_t)a.key_lo[g] << 32) | a.key_hi[g]);
-  // a speculative P (begin_once) ran on the cached plan: kept when this layout is the cached one;
-  // otherwise the slab table is rebuilt once that P is done, and its flags cleared (the partition's
-  // own were read back already)
-  const bool spec_hit = J.spec && J.pcache && J.pcache->key == key;
-  if (J.spec && !spec_hit) {
-    SYZ_HIP(hipStreamWaitEvent(s, c.ev_spec, 0));
-    SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
-  }
-  J.spec = false;
+  std::vector<uint64_t> key = plan_key(a, hstart, hsl, lo, hi, J.may_bounce);
   if (!J.pcache || J.pcache->key != key) {
     auto P = std::make_shared<SlabPlanCache>();
     P->key = std::move(key);
@@ -669,20 +659,36 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     }
     P->lo = lo;
     P->n = n;
+    P->hi = hi;
     J.pcache = P;
   }
+}
+
+// The step's device work on the job's plan (J.pcache) and Go-sort plan: P on its own stream beside the
+// Go sort, then M per class as soon as its own sort and P are done. Nothing here waits for the device.
+static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members, uint64_t* el, const uint32_t* mlen,
+                        const uint64_t* mpos, const uint32_t* sbeg, int* err) {
+  Context& c = ctx();
+  Scratch& sc = c.scratch;
+  const size_t n = a.n;
+  const uint32_t G = a.G;
+  hipStream_t s = a.s;
+  uint64_t* gstart = J.gstart.p;
+  uint32_t* rank_of_member = J.rank_of_member.p;
+  uint32_t* ent_of_rank = J.ent_of_rank.p;
+  uint8_t* sel8 = J.sel8.p;
+  const std::vector<uint64_t>& hstart = J.hstart;
+  HostTimer ht("launch_step");
   const SlabPlanCache& PC = *J.pcache;
   SlabJob SJ = PC.SJ;  // (the device members below are this step's)
   const auto& icount = PC.icount;
   const auto& ifirst = PC.ifirst;
   const auto& item_pcs = PC.item_pcs;
-  const uint64_t total_pcs = SJ.total_pcs;
   uint8_t* dstage = PC.dstage.p;
   const SGroup* dsg = SJ.dsg;
   const PItem* ditems = reinterpret_cast<const PItem*>(dstage + PC.o_it);
-  ht.mark("items_stage");
-  hipStream_t pq = spec_hit ? (pm_serial() ? s : c.part) : launch_p(a, PC, SJ, members, mlen, mpos, gstart, sbeg, err);
-  if (spec_hit) SJ = J.spec_sj;
+  (void)G;
+  hipStream_t pq = launch_p(a, PC, SJ, members, mlen, mpos, gstart, sbeg, err);
   ht.mark("slab_build");
   const PSlab* slabs = SJ.slabs;
   const uint32_t* gslab = SJ.gslab;
@@ -696,7 +702,7 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     c.ev_cnt.push_back(e1);
     c.ev_sct.push_back(e2);
   }
-  int* herr = c.pinned.get<int>(4);
+  int* herr = c.pinned_err.get<int>(4);  // (not the lane's pinned buffer: the read-back may still be read)
   SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, pq));
   SYZ_HIP(hipEventRecord(c.ev_cnt[0], pq));
   SYZ_HIP(hipEventRecord(c.ev_sct[0], pq));
@@ -751,14 +757,21 @@ static bool begin_slab(MinJob& J, const RawMinArgs& a, const std::vector<uint64_
     big_done(s);
   }
   ht.mark("gosort_run");
-  SYZ_HIP(hipEventSynchronize(c.ev_cnt[0]));
-  ht.mark("wait_p");
   if (!J.done) SYZ_HIP(hipEventCreateWithFlags(&J.done, hipEventDisableTiming));
   SYZ_HIP(hipEventRecord(J.done, s));
-  J.stats_total_pcs = total_pcs;
-  J.stats_items_direct = icount[0][PMODE_DIRECT] + icount[1][PMODE_DIRECT];
-  J.stats_items_hash = icount[0][PMODE_HASH] + icount[1][PMODE_HASH] + icount[0][PMODE_PACKED] +
-                       icount[1][PMODE_PACKED];
+}
+
+// After launch_step: P's flags (herr, copied back behind P). false: a PC outside the windows (an
+// unsorted cover): the caller redoes the job on exact bounds.
+static bool finish_step(MinJob& J, const uint32_t* exact_span) {
+  Context& c = ctx();
+  const SlabPlanCache& PC = *J.pcache;
+  int* herr = c.pinned_err.get<int>(4);
+  SYZ_HIP(hipEventSynchronize(c.ev_cnt[0]));
+  J.stats_total_pcs = PC.SJ.total_pcs;
+  J.stats_items_direct = PC.icount[0][PMODE_DIRECT] + PC.icount[1][PMODE_DIRECT];
+  J.stats_items_hash = PC.icount[0][PMODE_HASH] + PC.icount[1][PMODE_HASH] + PC.icount[0][PMODE_PACKED] +
+                       PC.icount[1][PMODE_PACKED];
   if (herr[0] & 64) fail(SYZGPU_EINTERNAL, "minimize: slab plan does not fit the layout");
   if (herr[0] & 1) {
     if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
@@ -878,23 +891,23 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   SYZ_HIP(hipMemcpyAsync(hbuf, gpack, (3 * (size_t)G + 4) * 8, hipMemcpyDeviceToHost, s));
   if (!c.ev_spin) SYZ_HIP(hipEventCreateWithFlags(&c.ev_spin, hipEventDisableTiming));
   SYZ_HIP(hipEventRecord(c.ev_spin, s));
-  // when the last step's plan is at hand, P on that plan runs while the host plans (a step on the same
-  // layout, the common case: begin_slab keeps it when the layout read back matches; P's guards keep a
-  // stale plan's slabs inside their buffers, err 64)
-  J.spec = false;
-  if (J.pcache && !exact_span && pm_spec() && J.pcache->n == n && J.pcache->SJ.G == G) {
-    J.spec_sj = J.pcache->SJ;
-    const hipStream_t pq = launch_p(a, *J.pcache, J.spec_sj, members, mlen, mpos, gstart, sbeg, err);
-    SYZ_HIP(hipEventRecord(c.ev_spec, pq));
-    J.spec = true;
-  }
+  // Speculation: with the last step's plans at hand (a step on the same layout: the common case), the
+  // whole step goes out on them before the layout is read back, so the host's read-back and planning
+  // leave the device's critical path. It is kept when the layout read back is the one planned (the
+  // group starts and plan_key); otherwise it is waited for and the step redone without. P's guards
+  // keep a stale plan's slabs inside their buffers (err 64). SYZGPU_PM_SPEC=0: no speculation.
+  const bool spec = !J.nospec && J.pcache && J.plan && !exact_span && pm_spec() && J.pcache->n == n &&
+                    J.pcache->SJ.G == G && J.hstart == J.plan_key && J.plan_key.size() == (size_t)G + 1;
+  J.nospec = false;
+  if (spec) launch_step(J, a, members, el, mlen, mpos, sbeg, err);
   HostTimer ht("begin");
   event_wait_spin(c.ev_spin);
   ht.mark("wait_partition");
-  J.may_bounce = hbuf[3 * G + 3] >= GS_U32_LEN_LIMIT;
-  if (*reinterpret_cast<int*>(hbuf + 2 * G + 2)) fail(SYZGPU_EINVAL, "group id >= ngroups");
+  const bool may_bounce = hbuf[3 * G + 3] >= GS_U32_LEN_LIMIT;
+  const bool bad_group = *reinterpret_cast<int*>(hbuf + 2 * G + 2) != 0;
   std::vector<uint64_t> hstart(hbuf, hbuf + G + 1), hpcs(hbuf + G + 1, hbuf + 2 * G + 1);
-  const uint64_t* hsl = hbuf + 2 * G + 3;  // PCs this job reads per group (key parts: the slices)
+  const std::vector<uint64_t> hslv(hbuf + 2 * G + 3, hbuf + 3 * G + 3);  // PCs this job reads per group
+  const uint64_t* hsl = hslv.data();                                     // (key parts: the slices)
   if (!krange) hpcs.assign(hsl, hsl + G);  // (whole covers: the slices are the groups' PCs)
   uint32_t lo = reinterpret_cast<uint32_t*>(hbuf + 2 * G + 1)[0], hi = reinterpret_cast<uint32_t*>(hbuf + 2 * G + 1)[1];
   if (exact_span) {
@@ -902,13 +915,29 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     hi = exact_span[1];
   }
   if (lo > hi) lo = hi = 0;  // no PCs at all
+  if (spec) {
+    if (!bad_group && hstart == J.plan_key && plan_key(a, hstart, hsl, lo, hi, may_bounce) == J.pcache->key) {
+      ht.mark("spec_kept");
+      return finish_step(J, exact_span);
+    }
+    SYZ_HIP(hipEventSynchronize(J.done));  // the speculative step is done with every buffer
+    if (!bad_group) {
+      J.nospec = true;
+      return begin_once(J, a, exact_span);  // the partition again, then planned as below
+    }
+  }
+  if (bad_group) fail(SYZGPU_EINVAL, "group id >= ngroups");
+  J.may_bounce = may_bounce;
   J.hstart = hstart;
   const uint64_t spanw = (uint64_t)hi - lo + 1;
   // ---- plan: window size per call group, blocks, chunk bound, work items ----
   std::vector<PGroup> hpg;
   plan_windows(spanw, hpcs.data(), hstart.data(), G, hpg);
   ht.mark("plan_windows");
-  return begin_slab(J, a, hstart, hpcs, hsl, hpg, lo, hi, exact_span, members, el, mlen, mpos, sbeg, err);
+  plan_layout(J, a, hstart, hpcs, hsl, hpg, lo, hi);
+  ht.mark("plan_layout");
+  launch_step(J, a, members, el, mlen, mpos, sbeg, err);
+  return finish_step(J, exact_span);
 }
 
 __global__ void k_job_xchg(uint8_t* sel8, const uint64_t* gstart, const uint32_t* groups, const uint64_t* boff,

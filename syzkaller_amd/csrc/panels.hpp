@@ -98,7 +98,7 @@ struct RawEndArgs {
 // One minimizeCorpus job (the raw path): its selection lives here between begin and end, so a
 // multi-GPU step can exchange the selection of split call groups in between, and concurrent callers
 // with their own jobs never see each other's state.
-// begin_slab's plan for one layout (the key), kept by the job for the next step on the same layout
+// plan_layout's plan for one layout (the key), kept by the job for the next step on the same layout
 struct SlabPlanCache {
   std::vector<uint64_t> key;
   SlabJob SJ;  // host parts; dsg / dgblock / dbgroup point into dstage
@@ -107,7 +107,7 @@ struct SlabPlanCache {
   uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};
   size_t o_gb = 0, o_bg = 0, o_it = 0;
   uint64_t cpcs[2] = {0, 0}, cent[2] = {0, 0};  // PCs / entries of the small and big call groups
-  uint32_t lo = 0;
+  uint32_t lo = 0, hi = 0;
   size_t n = 0;
   Grow<uint8_t> dstage;  // SGroup[G], gblock[G + 1], bgroup[B + 1], items
 };
@@ -127,9 +127,8 @@ struct MinJob {
   Grow<uint8_t> count_hist;
   std::vector<uint64_t> hstart, xkey;
   std::shared_ptr<GosortPlan> plan;  // Go-sort plan of the last layout (keeps its rounds hint)
-  std::shared_ptr<SlabPlanCache> pcache;  // begin_slab's plan of the last layout
-  bool spec = false;                      // this step's P was launched on pcache before the layout was read
-  SlabJob spec_sj;                        // (its device buffers)
+  std::shared_ptr<SlabPlanCache> pcache;  // plan_layout's plan of the last layout
+  bool nospec = false;                    // begin_once: this call redoes a speculation that missed
   std::vector<uint64_t> plan_key;
   uint64_t stats_total_pcs = 0;
   size_t stats_items_direct = 0, stats_items_hash = 0;

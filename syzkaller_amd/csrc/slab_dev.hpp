@@ -107,7 +107,7 @@ __device__ __forceinline__ PSlab slab_at(uint64_t c, uint32_t b, const uint32_t*
 
 // one thread per slab (grid over a bound; cstart[B] = the slabs there are); the first G + 1 threads
 // also write gslab[g] = the group's first slab (gslab[G] = all of them) and gebase[g] = its first element
-static __global__ void k_sl_slabs(const uint32_t* bgroup, uint32_t B, const uint32_t* gblock, const uint64_t* gstart,
+[[maybe_unused]] static __global__ void k_sl_slabs(const uint32_t* bgroup, uint32_t B, const uint32_t* gblock, const uint64_t* gstart,
                                   const SGroup* sg, const uint64_t* tpos, const uint64_t* mpos, const uint64_t* cstart,
                                   uint64_t bound, PSlab* slabs, uint32_t G, uint32_t* gslab, uint64_t* gebase) {
   const uint64_t ns = cstart[B];
@@ -141,6 +141,30 @@ __host__ __device__ constexpr size_t slab_lds_bytes(uint32_t Wmax) {
   return 4ull * (slab_obuf_words(Wmax) + 2 * slab_hist_words(Wmax) + 16);
 }
 static_assert(5 * SL_MEMB + SL_MEMB / 4 <= 64 * SL_TILES, "the member table lives in the staging buffer's space");
+
+#ifndef SYZ_SL_RUNS
+#define SYZ_SL_RUNS 1
+#endif
+constexpr bool SL_RUNS = SYZ_SL_RUNS != 0;
+// A wave's lanes with window w, ok: the maximal runs of consecutive ok lanes with one window. head: the
+// lane starts a run (len: its length); hd: the head of the lane's run.
+struct WinRun {
+  bool head;
+  uint32_t len, hd;
+};
+__device__ __forceinline__ WinRun win_run(uint32_t w, bool ok, unsigned lane) {
+  const uint32_t wp = lane_prev(w);
+  const bool head = ok && (lane == 0 || wp != w);
+  const uint64_t hm = __ballot(head), okm = __ballot(ok);
+  const uint64_t upto = (2ull << lane) - 1;  // lanes <= this one (lane 63: all)
+  const uint64_t ends = (hm | ~okm) & ~upto;  // run boundaries after this lane
+  const uint64_t mine = hm & upto;
+  WinRun r;
+  r.head = head;
+  r.len = (ends ? (uint32_t)__builtin_ctzll(ends) : 64u) - lane;
+  r.hd = mine ? 63u - (uint32_t)__builtin_clzll(mine) : lane;
+  return r;
+}
 
 template <int BLOCK, int TPW, bool NOV = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_slab(
@@ -252,7 +276,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
   }
   // from here on v holds the PC's offset from lo: window = v >> S, offset in it = v & omask
-  // window histogram (lanes outside the tile count into a dummy slot of their own)
+  // window histogram. A tile's PCs are sorted, so its lanes' windows come in runs: one LDS atomic per
+  // run (its head lane adds the run's length), not one per element (SYZ_SL_RUNS=0: per element, lanes
+  // outside the tile counting into a dummy slot of their own)
   const uint32_t DUMMY = W + 1 + lane;
 #pragma unroll
   for (int k = 0; k < TPW; k++) {
@@ -263,7 +289,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const bool in = lane < cnt;
     // outside the windows: an unsorted cover (Minimize: redone on exact bounds; NOV: out of order)
     bad |= (in && w >= W) ? (NOV ? ((z & 0x100u) ? 1 : 4) : 1) : 0;
-    atomicAdd(&hist[in && w < W ? w : DUMMY], 1u);
+    if (SL_RUNS) {
+      const WinRun r = win_run(w, in && w < W, lane);
+      if (r.head) atomicAdd(&hist[w], r.len);
+    } else {
+      atomicAdd(&hist[in && w < W ? w : DUMMY], 1u);
+    }
     if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
   }
   {
@@ -316,7 +347,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
         ok[q] = lane < (z & 0x7Fu) && w < W;
         el[q] = (d & omask) | ((z >> 9) << S);
         pos[q] = 0;
-        if (ok[q]) pos[q] = atomicAdd(&hist[w], 1u);
+        if (SL_RUNS) {  // the run's head takes the run's places; its lanes follow it
+          const WinRun r = win_run(w, ok[q], lane);
+          const uint32_t b = r.head ? atomicAdd(&hist[w], r.len) : 0u;
+          pos[q] = (uint32_t)__shfl((int)b, (int)r.hd, 64) + (lane - r.hd);
+        } else if (ok[q]) {
+          pos[q] = atomicAdd(&hist[w], 1u);
+        }
       }
 #pragma unroll
       for (int q = 0; q < PB; q++)

@@ -21,7 +21,8 @@ for _ in range(int(os.environ.get("PM_W", "3"))):
     step()
 torch.cuda.synchronize()
 L.syzgpu_profile_only(None)
-L.syzgpu_profile_enable(1)
+if os.environ.get("PM_PROF", "1") == "1":
+    L.syzgpu_profile_enable(1)
 K = int(os.environ.get("PM_K", "5"))
 t0 = time.perf_counter()
 for _ in range(K):
