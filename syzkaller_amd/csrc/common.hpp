@@ -114,10 +114,8 @@ struct Context {
   uint32_t gr_resident = 0;  // workgroups of k_gr_persist resident at once (occupancy x CUs)
   hipStream_t part = nullptr;  // the raw Minimize's transpose pass, beside the Go sort
   hipEvent_t ev_part0 = nullptr, ev_part1 = nullptr;
-  hipEvent_t ev_msmall = nullptr, ev_msmall2 = nullptr;  // the small groups' packed M on another stream
   hipEvent_t ev_psmall = nullptr;  // P's slabs of the small call groups are cut
   hipEvent_t ev_spin = nullptr;    // stream_wait_spin's marker
-  hipStream_t part2 = nullptr;  // its scatter passes, batch after batch beside the next batch's count
   std::vector<hipEvent_t> ev_cnt, ev_sct;  // per batch: count done, scatter done
   int ncu = 0;  // compute units of the device
   // single-pass scans (scan.hpp): per tag and stream, the flag buffer, the tiles it was cleared for, the epoch

@@ -344,14 +344,16 @@ __global__ __launch_bounds__(PACKED ? PK_BLOCK : 1024) __attribute__((amdgpu_wav
 
 // ---- outputs: the group-major kept list in selection order ----------------------------------------
 // kept inputs per 32 ranks (bytes are 0/1)
-__global__ void k_sel_wpop(const uint8_t* sel8, size_t nw, uint32_t* cnt) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x) {
+// kept flags per 32-rank word (sel8 bytes are 0 / 1): the compaction scan's input
+struct SelWordsFn {
+  const uint8_t* sel8;
+  __device__ void operator()(size_t i, uint64_t* v) const {
     const uint4* q = reinterpret_cast<const uint4*>(sel8 + 32 * i);
     const uint4 a = q[0], b = q[1];
-    cnt[i] = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(b.x) + __popc(b.y) + __popc(b.z) +
-             __popc(b.w);
+    v[0] = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(b.x) + __popc(b.y) + __popc(b.z) +
+           __popc(b.w);
   }
-}
+};
 
 __device__ __forceinline__ uint64_t sel_pos(const uint8_t* sel8, const uint64_t* wpos, uint64_t r) {
   uint64_t p = wpos[r >> 5];
@@ -540,11 +542,7 @@ static hipStream_t launch_p(const RawMinArgs& a, const SlabPlanCache& PC, SlabJo
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part0, hipEventDisableTiming));
     SYZ_HIP(hipEventCreateWithFlags(&c.ev_part1, hipEventDisableTiming));
   }
-  if (!c.ev_msmall) {
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_msmall2, hipEventDisableTiming));
-    SYZ_HIP(hipEventCreateWithFlags(&c.ev_psmall, hipEventDisableTiming));
-  }
+  if (!c.ev_psmall) SYZ_HIP(hipEventCreateWithFlags(&c.ev_psmall, hipEventDisableTiming));
   hipStream_t pq = pm_serial() ? s : c.part;
   SYZ_HIP(hipEventRecord(c.ev_part0, s));
   SYZ_HIP(hipStreamWaitEvent(c.part, c.ev_part0, 0));
@@ -727,7 +725,7 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
                                                         elems, rank_of_member, gstart, sel8);
       SYZ_LAUNCHED();
     }
-    if (np) {
+    if (np) {  // (on a stream of their own beside the others: slower, the process has 4 hardware queues)
       ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
       k_smin_hash<true><<<(unsigned)np, PK_BLOCK, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
                                                        elems, rank_of_member, gstart, sel8);
@@ -1013,13 +1011,8 @@ void sel_compact_dev(const uint8_t* sel8, const uint32_t* ent_of_rank, const uin
                      int64_t* out_idx, uint64_t* group_out_off, hipStream_t s) {
   Scratch& sc = ctx().scratch;
   const size_t nw = (n + 31) / 32;
-  uint32_t* wcnt = sc.get<uint32_t>("pm_wcnt", nw + 1);
   uint64_t* wpos = sc.get<uint64_t>("pm_wpos", nw + 2);
-  if (nw) {
-    k_sel_wpop<<<grid_for(nw, 256, 4096), 256, 0, s>>>(sel8, nw, wcnt);
-    SYZ_LAUNCHED();
-  }
-  exclusive_scan_u32(wcnt, wpos, nw, s);
+  scan_f<1>(SelWordsFn{sel8}, nw, wpos, nullptr, s, "sel");
   if (out_idx && n) {
     k_sel_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(sel8, wpos, ent_of_rank, n, out_idx);
     SYZ_LAUNCHED();
@@ -1038,9 +1031,9 @@ void minimize_raw_end(MinJob& J, const RawEndArgs& e) {
   const size_t n = J.n;
   const uint32_t G = J.G;
   hipStream_t s = e.s;
+  // (err holds no bit here: begin fails or redoes the job on any of its own)
   int* err = sc.get<int>("mz_err", 2);
   SYZ_HIP(hipStreamWaitEvent(s, J.done, 0));
-  SYZ_HIP(hipMemsetAsync(err, 0, 2 * sizeof(int), s));
   const uint8_t* dcount = nullptr;
   if (e.count_hist) {
     J.count_hist.ensure(G);

@@ -159,8 +159,7 @@ static void free_lane(Context* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->part) (void)hipStreamDestroy(c->part);
   if (c->cap) (void)hipStreamDestroy(c->cap);
-  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_part0, c->ev_part1, c->ev_msmall, c->ev_msmall2, c->ev_psmall,
-                       c->ev_spin})
+  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_part0, c->ev_part1, c->ev_psmall, c->ev_spin})
     if (e) (void)hipEventDestroy(e);
   for (auto& row : c->gl_exec)
     for (auto& g : row)

@@ -21,8 +21,9 @@
 //   K1 k_st_classes  distinct non-zero weights (at most ST_KMAX) into a small table (atomicCAS)
 //   K2 k_st_prep     one thread: classes sorted ascending, the float32 products of every class pair
 //   K3 k_st_pack     indicator matrices X[a][c][k] = (W[k][c] == w_a), int8, 32-padded
-//   K4 k_st_gram     one wave per 32x32 tile of calls: MFMA over keys for every class pair, float64
-//                    combination, the C x C float32 sums (diagonal 0)
+//   K4 k_st_gram     one 4-wave workgroup per 32x32 tile of calls: MFMA over keys per class pair,
+//                    counts through LDS, float64 combination in (a, b) order, the C x C float32 sums
+//                    (diagonal 0)
 //   K5 k_prio_row    (prio.hip, mode 2) diagonal := row max, normalizePrio, in place
 #include <cmath>
 
@@ -112,40 +113,74 @@ __global__ __launch_bounds__(256) void k_st_pack(const float* __restrict__ uses,
   }
 }
 
-// One wave per 32x32 tile (rows c0.., columns c1..). Operands: lane l holds 16 consecutive keys
-// [16 (l >> 5), +16) of call (l & 31) of the tile, for A (rows, class a) and B (columns, class b)
-// alike, so whatever order the instruction gives the 32 keys of a step inside its K, A and B agree
-// on it and the step sums the 32 keys. Result registers: column l & 31, row
-// (r & 3) + 8 (r >> 2) + 4 (l >> 5) (the gfx950 32x32 C/D map).
-__global__ __launch_bounds__(64) void k_st_gram(const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t Kp,
-                                                const StClasses* __restrict__ cl, float* __restrict__ prios) {
+// One 4-wave workgroup per 32x32 tile (rows c0.., columns c1..). The class pairs (a, b) go in groups
+// of 16, four per wave, two MFMA chains interleaved; a pair's integer counts n_ab land in LDS, then every
+// thread adds n_ab * w_a w_b for its four entries of the tile over the group's pairs in (a, b) order
+// (float64, exact products), so the sum is the one-pair-at-a-time sum in that fixed order.
+// Operands: lane l holds 16 consecutive keys [16 (l >> 5), +16) of call (l & 31) of the tile, for A
+// (rows, class a) and B (columns, class b) alike, so whatever order the instruction gives the 32 keys
+// of a step inside its K, A and B agree on it and the step sums the 32 keys. Result registers: column
+// l & 31, row (r & 3) + 8 (r >> 2) + 4 (l >> 5) (the gfx950 32x32 C/D map).
+// (One wave per tile doing every pair one after another took 75 us at config 1: load latency, chain
+// after chain.)
+constexpr int ST_GP = 16;  // pairs per LDS group
+__global__ __launch_bounds__(256) void k_st_gram(const int8_t* __restrict__ X, int32_t C, uint32_t Cp, uint32_t Kp,
+                                                 const StClasses* __restrict__ cl, float* __restrict__ prios) {
+  __shared__ int32_t cnt[ST_GP][32 * 32];
   const uint32_t c0 = blockIdx.y * 32, c1 = blockIdx.x * 32;
   const unsigned lane = __lane_id();
-  const uint32_t nk = cl->nk;
-  double acc[16];
-#pragma unroll
-  for (int r = 0; r < 16; r++) acc[r] = 0.0;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t nk = cl->nk, np = nk * nk;
   const size_t koff = 16 * (lane >> 5);
-  for (uint32_t a = 0; a < nk; a++) {
-    const int8_t* xa = X + ((size_t)a * Cp + c0 + (lane & 31)) * Kp + koff;
-    for (uint32_t b = 0; b < nk; b++) {
-      const int8_t* xb = X + ((size_t)b * Cp + c1 + (lane & 31)) * Kp + koff;
-      v16i n = {};
-      for (uint32_t k = 0; k < Kp; k += 32) {
-        const v4i va = *reinterpret_cast<const v4i*>(xa + k);
-        const v4i vb = *reinterpret_cast<const v4i*>(xb + k);
-        n = __builtin_amdgcn_mfma_i32_32x32x32_i8(va, vb, n, 0, 0, 0);
-      }
-      const double p = cl->prod[a][b];
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[r] += (double)n[r] * p;  // exact product, fixed (a, b) order
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};  // entries threadIdx.x + 256 e of the tile
+  auto chain2 = [&](uint32_t p0, uint32_t p1, v16i& n0, v16i& n1) {
+    const int8_t* xa0 = X + ((size_t)(p0 / nk) * Cp + c0 + (lane & 31)) * Kp + koff;
+    const int8_t* xb0 = X + ((size_t)(p0 % nk) * Cp + c1 + (lane & 31)) * Kp + koff;
+    const uint32_t q1 = p1 < np ? p1 : p0;
+    const int8_t* xa1 = X + ((size_t)(q1 / nk) * Cp + c0 + (lane & 31)) * Kp + koff;
+    const int8_t* xb1 = X + ((size_t)(q1 % nk) * Cp + c1 + (lane & 31)) * Kp + koff;
+    n0 = v16i{};
+    n1 = v16i{};
+#pragma unroll 4
+    for (uint32_t k = 0; k < Kp; k += 32) {
+      const v4i a0 = *reinterpret_cast<const v4i*>(xa0 + k);
+      const v4i b0 = *reinterpret_cast<const v4i*>(xb0 + k);
+      const v4i a1 = *reinterpret_cast<const v4i*>(xa1 + k);
+      const v4i b1 = *reinterpret_cast<const v4i*>(xb1 + k);
+      n0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, n0, 0, 0, 0);
+      n1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, n1, 0, 0, 0);
     }
-  }
-  const uint32_t col = c1 + (lane & 31);
+  };
+  auto put = [&](uint32_t slot, const v16i& n) {
 #pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const uint32_t row = c0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if ((int32_t)row < C && (int32_t)col < C) prios[(size_t)row * C + col] = row == col ? 0.0f : (float)acc[r];
+    for (int r = 0; r < 16; r++) {
+      const uint32_t row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      cnt[slot][row * 32 + (lane & 31)] = n[r];
+    }
+  };
+  for (uint32_t g0 = 0; g0 < np; g0 += ST_GP) {
+    for (uint32_t q = 0; q < 4; q += 2) {
+      const uint32_t p0 = g0 + 4 * wv + q;
+      if (p0 >= np) break;
+      v16i n0, n1;
+      chain2(p0, p0 + 1, n0, n1);
+      put(4 * wv + q, n0);
+      if (p0 + 1 < np) put(4 * wv + q + 1, n1);
+    }
+    __syncthreads();
+    const uint32_t gn = min<uint32_t>(ST_GP, np - g0);
+    for (uint32_t j = 0; j < gn; j++) {  // (a, b) order
+      const double pr = cl->prod[(g0 + j) / nk][(g0 + j) % nk];
+#pragma unroll
+      for (int e = 0; e < 4; e++) acc[e] += (double)cnt[j][threadIdx.x + 256 * e] * pr;  // exact product
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const uint32_t i = threadIdx.x + 256 * e;
+    const uint32_t row = c0 + i / 32, col = c1 + i % 32;
+    if ((int32_t)row < C && (int32_t)col < C) prios[(size_t)row * C + col] = row == col ? 0.0f : (float)acc[e];
   }
 }
 
@@ -176,7 +211,7 @@ const uint32_t* static_priorities_enqueue(const float* uses, size_t nkeys, int32
   const uint64_t packs = (uint64_t)ST_KMAX * Cp * (Kp / 16);  // an upper bound (nk <= ST_KMAX)
   k_st_pack<<<grid_for(packs, 256, 8192), 256, 0, s>>>(uses, (uint32_t)nkeys, C, Cp, Kp, cl, X);
   SYZ_LAUNCHED();
-  k_st_gram<<<dim3(Cp / 32, Cp / 32), 64, 0, s>>>(X, C, Cp, Kp, cl, prios);
+  k_st_gram<<<dim3(Cp / 32, Cp / 32), 256, 0, s>>>(X, C, Cp, Kp, cl, prios);
   SYZ_LAUNCHED();
   static_prio_rows_dev(prios, C, s);
   return &cl->err;
