@@ -271,9 +271,7 @@ static void handle_end(CorpusHandle& H, int32_t C, uint8_t* selected, int64_t* l
     Corpus& K = *H.index;
     corpus_minimize_end(K, C, selected, len_hist, s);
     if (out_idx || group_out_off) {
-      uint8_t* s8 = ctx().scratch.get<uint8_t>("mz_sel8", (K.n + 31) / 32 * 32 + 64);
-      sel_bits_bytes_dev(K.sel_bits.p, K.n, s8, s);
-      sel_compact_dev(s8, K.eor.p, K.gstart.p, K.n, K.G, out_idx, group_out_off, s);
+      sel_compact_dev(K.sel_bits.p, K.eor.p, K.gstart.p, K.n, K.G, out_idx, group_out_off, s);
     }
   } else if (H.path == 2) {
     RawEndArgs e;

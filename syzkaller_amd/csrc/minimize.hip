@@ -309,11 +309,6 @@ void group_partition_dev(const uint32_t* group, const uint64_t* off, size_t n, u
   }
 }
 
-__global__ void k_bits_bytes(const uint32_t* bits, size_t n, uint8_t* out) {
-  for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x)
-    out[r] = (uint8_t)((bits[r >> 5] >> (r & 31)) & 1u);
-}
-
 // groups of one entry are not sorted (no pack or round touches them): their rank is their position
 __global__ void k_rank_init(const uint32_t* members, size_t n, uint32_t* rank_of_member, uint32_t* ent_of_rank) {
   for (size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x) {
@@ -1334,15 +1329,6 @@ void corpus_minimize_end(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
     k_select_store<<<grid_for(n, 256, 512), 256, len_hist ? (size_t)(C + 1) * 8 : 0, s>>>(
         sel_bits, rank_of_entry, n, len_hist ? K.prog_len.p : nullptr, K.group.p,
         K.has_count_hist ? K.count_hist.p : nullptr, C, selected, len_hist, err);
-    SYZ_LAUNCHED();
-  }
-}
-
-// rank bitmap -> one byte per rank (sel_compact_dev's input)
-void sel_bits_bytes_dev(const uint32_t* bits, size_t n, uint8_t* out, hipStream_t s) {
-  SYZ_HIP(hipMemsetAsync(out, 0, (n + 31) / 32 * 32 + 64, s));
-  if (n) {
-    k_bits_bytes<<<grid_for(n, 256, 4096), 256, 0, s>>>(bits, n, out);
     SYZ_LAUNCHED();
   }
 }

@@ -120,40 +120,36 @@ __global__ void k_gpack(const uint64_t* gstart, const uint64_t* gpcs, const uint
   }
 }
 
-// Winners of a window table -> sel8[rank] = 1 with plain byte stores (no atomics: a byte written by
-// several tables is written with the same value). Ranks of call g lie in [gbase, gbase + ng); the
-// first BMW*32 of them are deduplicated through an LDS bitmap first, so each kept input costs one
-// store per table, not one per key it wins.
+// Winners of a window table -> the job's rank bitmap (bit r of selbits: rank r kept). A window's winners
+// are deduplicated through an LDS bitmap aligned to the global words (the group's first BMW * 32 ranks
+// from its first word), which leaves as one atomicOr per nonzero word; a winner past it goes straight to
+// its global word. The atomics return nothing, so no wave waits for them (a read of the word first, to
+// skip an atomic that is not needed, cost more than it saved: the read is waited for).
 struct RankIdentity {
   __device__ uint32_t operator()(uint32_t v) const { return v; }
 };
+__device__ __forceinline__ void set_bits(uint32_t* w, uint32_t bits) { atomicOr(w, bits); }
 template <uint32_t BMW, class D = RankIdentity>
-__device__ __forceinline__ void emit_winner_bytes(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
-                                                  uint32_t* bm, uint8_t* sel8, D decode = D{}) {
-  const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)BMW * 32, ng);
-  const uint32_t words = (span + 31) / 32;
+__device__ __forceinline__ void emit_winner_bits(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
+                                                 uint32_t* bm, uint32_t* selbits, D decode = D{}) {
+  const uint64_t base = gbase & ~31ull;  // rank of bitmap word 0, bit 0
+  const uint32_t words = (uint32_t)min<uint64_t>(BMW, (gbase + ng - base + 31) / 32);
   for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nids; i += blockDim.x) {
     const uint32_t r = decode(tab[i]);
     if (r == RANK_NONE) continue;
-    const uint64_t lr = (uint64_t)r - gbase;
-    if (lr < span) {
-      const uint32_t bit = 1u << (lr & 31);
+    const uint64_t lr = (uint64_t)r - base;
+    const uint32_t bit = 1u << (r & 31);
+    if (lr < 32ull * words) {
       if (!(bm[lr >> 5] & bit)) atomicOr(&bm[lr >> 5], bit);
     } else {
-      sel8[r] = 1;
+      set_bits(&selbits[r >> 5], bit);
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
-    uint32_t wv = bm[i];
-    while (wv) {
-      const uint32_t b = __ffs(wv) - 1;
-      sel8[gbase + 32ull * i + b] = 1;
-      wv &= wv - 1;
-    }
-  }
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+    if (const uint32_t v = bm[i]) set_bits(&selbits[(base >> 5) + i], v);
   __syncthreads();
 }
 
@@ -201,7 +197,7 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
                                             const uint64_t* gebase, const uint32_t* D, const PSlab* slabs,
                                             const uint32_t* __restrict__ elems,
                                             const uint32_t* __restrict__ rank_of_member, const uint64_t* gstart,
-                                            uint8_t* sel8, SminLds& L) {
+                                            uint32_t* selbits, SminLds& L) {
   uint32_t* tab = L.tabs;
   {
     uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -224,7 +220,7 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
   __syncthreads();
   if (SYZ_SMIN_NOEMIT) return;  // timing only
   const uint64_t gb = gstart[it.g];
-  emit_winner_bytes<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, L.wsc, sel8);
+  emit_winner_bits<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, L.wsc, selbits);
 }
 
 #ifndef SYZ_SL_HU
@@ -235,7 +231,7 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
                                           const uint64_t* gebase, const uint32_t* D, const PSlab* slabs,
                                           const uint32_t* __restrict__ elems,
                                           const uint32_t* __restrict__ rank_of_member, const uint64_t* gstart,
-                                          uint8_t* sel8, LT& L) {
+                                          uint32_t* selbits, LT& L) {
   constexpr uint32_t NS = PACKED ? PHS : HS;  // slots
   constexpr uint32_t CAP = PACKED ? PHCAP : HCAP;
   constexpr uint32_t TW = PACKED ? PHS : 2 * HS;  // table words
@@ -305,11 +301,11 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
     }
     if constexpr (PACKED) {
       const uint32_t g32 = (uint32_t)gb;
-      emit_winner_bytes<LT::WSC>(keys, NS, gb, ng, L.wsc, sel8, [g32](uint32_t v) {
+      emit_winner_bits<LT::WSC>(keys, NS, gb, ng, L.wsc, selbits, [g32](uint32_t v) {
         return v == 0xFFFFFFFFu ? RANK_NONE : g32 + (v & ((1u << PK_RBITS) - 1));
       });
     } else {
-      emit_winner_bytes<LT::WSC>(vals, HS, gb, ng, L.wsc, sel8);
+      emit_winner_bits<LT::WSC>(vals, HS, gb, ng, L.wsc, selbits);
     }
     round++;
     __syncthreads();  // the emit's bitmap and table reads are done before the next round clears them
@@ -321,9 +317,9 @@ __global__ __launch_bounds__(1024) SYZ_SMIN_OCC void k_smin_direct(const PItem* 
                                                                    const uint32_t* D, const PSlab* slabs,
                                                                    const uint32_t* __restrict__ elems,
                                                                    const uint32_t* __restrict__ rank_of_member,
-                                                                   const uint64_t* gstart, uint8_t* sel8) {
+                                                                   const uint64_t* gstart, uint32_t* selbits) {
   __shared__ SminLds L;
-  smin_direct(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, sel8, L);
+  smin_direct(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, L);
 }
 
 // (one launch for a class's three table kinds measured no better and spills: M is throughput-bound)
@@ -332,41 +328,36 @@ template <bool PACKED>
 __global__ __launch_bounds__(PACKED ? PK_BLOCK : 1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_smin_hash(
     const PItem* items, const SGroup* sg, const uint32_t* gslab, const uint64_t* gebase, const uint32_t* D,
     const PSlab* slabs, const uint32_t* __restrict__ elems, const uint32_t* __restrict__ rank_of_member,
-    const uint64_t* gstart, uint8_t* sel8) {
+    const uint64_t* gstart, uint32_t* selbits) {
   if constexpr (PACKED) {
     __shared__ SminPkLds L;
-    smin_hash<true, PK_BLOCK>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, sel8, L);
+    smin_hash<true, PK_BLOCK>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits,
+                              L);
   } else {
     __shared__ SminLds L;
-    smin_hash<false, 1024>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, sel8, L);
+    smin_hash<false, 1024>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, L);
   }
 }
 
 // ---- outputs: the group-major kept list in selection order ----------------------------------------
 // kept inputs per 32 ranks (bytes are 0/1)
-// kept flags per 32-rank word (sel8 bytes are 0 / 1): the compaction scan's input
+// kept ranks per 32-rank word: the compaction scan's input
 struct SelWordsFn {
-  const uint8_t* sel8;
-  __device__ void operator()(size_t i, uint64_t* v) const {
-    const uint4* q = reinterpret_cast<const uint4*>(sel8 + 32 * i);
-    const uint4 a = q[0], b = q[1];
-    v[0] = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(b.x) + __popc(b.y) + __popc(b.z) +
-           __popc(b.w);
-  }
+  const uint32_t* selbits;
+  __device__ void operator()(size_t i, uint64_t* v) const { v[0] = __popc(selbits[i]); }
 };
 
-__device__ __forceinline__ uint64_t sel_pos(const uint8_t* sel8, const uint64_t* wpos, uint64_t r) {
-  uint64_t p = wpos[r >> 5];
-  for (uint64_t k = r & ~31ull; k < r; k++) p += sel8[k];
-  return p;
+__device__ __forceinline__ uint64_t sel_pos(const uint32_t* selbits, const uint64_t* wpos, uint64_t r) {
+  return wpos[r >> 5] + __popc(selbits[r >> 5] & ((1u << (r & 31)) - 1u));
 }
+__device__ __forceinline__ bool sel_bit(const uint32_t* selbits, uint64_t r) { return (selbits[r >> 5] >> (r & 31)) & 1u; }
 
-__global__ void k_sel_compact(const uint8_t* sel8, const uint64_t* wpos, const uint32_t* ent_of_rank, size_t n,
+__global__ void k_sel_compact(const uint32_t* selbits, const uint64_t* wpos, const uint32_t* ent_of_rank, size_t n,
                               int64_t* out) {
   // one wave per 64 ranks: positions by a ballot prefix
   for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r - __lane_id() < n;
        r += (size_t)gridDim.x * blockDim.x) {
-    const bool s = r < n && sel8[r];
+    const bool s = r < n && sel_bit(selbits, r);
     const uint64_t bal = __ballot(s);
     if (s) {
       const uint64_t base = r - __lane_id();
@@ -377,10 +368,10 @@ __global__ void k_sel_compact(const uint8_t* sel8, const uint64_t* wpos, const u
   }
 }
 
-__global__ void k_sel_goff(const uint8_t* sel8, const uint64_t* wpos, const uint64_t* gstart, uint32_t G,
+__global__ void k_sel_goff(const uint32_t* selbits, const uint64_t* wpos, const uint64_t* gstart, uint32_t G,
                            uint64_t* goff) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x)
-    goff[g] = sel_pos(sel8, wpos, gstart[g]);
+    goff[g] = sel_pos(selbits, wpos, gstart[g]);
 }
 
 // ---- key parts: a call group restricted to a PC range (multi-GPU) --------------------
@@ -674,7 +665,7 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
   uint64_t* gstart = J.gstart.p;
   uint32_t* rank_of_member = J.rank_of_member.p;
   uint32_t* ent_of_rank = J.ent_of_rank.p;
-  uint8_t* sel8 = J.sel8.p;
+  uint32_t* selbits = J.selbits.p;
   const std::vector<uint64_t>& hstart = J.hstart;
   HostTimer ht("launch_step");
   const SlabPlanCache& PC = *J.pcache;
@@ -707,7 +698,7 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
   SYZ_HIP(hipEventRecord(c.ev_part1, pq));
   // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
   uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
-  SYZ_HIP(hipMemsetAsync(sel8, 0, (n + 31) / 32 * 32 + 64, s));
+  SYZ_HIP(hipMemsetAsync(selbits, 0, (n / 32 + 2) * 4, s));
   auto run_m = [&](hipStream_t q, int big) {
     ProfScope ps(big ? "m_big" : "m_small", q, 0);
     const size_t nd = icount[big][PMODE_DIRECT], nh = icount[big][PMODE_HASH], np = icount[big][PMODE_PACKED];
@@ -716,19 +707,19 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
     if (nd) {
       ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
       k_smin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], dsg, gslab, gebase, D, slabs,
-                                                   elems, rank_of_member, gstart, sel8);
+                                                   elems, rank_of_member, gstart, selbits);
       SYZ_LAUNCHED();
     }
     if (nh) {
       ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
       k_smin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[big][PMODE_HASH], dsg, gslab, gebase, D, slabs,
-                                                        elems, rank_of_member, gstart, sel8);
+                                                        elems, rank_of_member, gstart, selbits);
       SYZ_LAUNCHED();
     }
     if (np) {  // (on a stream of their own beside the others: slower, the process has 4 hardware queues)
       ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
       k_smin_hash<true><<<(unsigned)np, PK_BLOCK, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
-                                                       elems, rank_of_member, gstart, sel8);
+                                                       elems, rank_of_member, gstart, selbits);
       SYZ_LAUNCHED();
     }
   };
@@ -820,7 +811,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   J.group = a.group;
   J.prog_len = a.prog_len;
   J.gstart.ensure(G + 1);
-  J.sel8.ensure((n + 31) / 32 * 32 + 64);
+  J.selbits.ensure(n / 32 + 2);
   J.ent_of_rank.ensure(n + 1);
   J.rank_of_member.ensure(n + 1);
   uint64_t* gstart = J.gstart.p;
@@ -938,15 +929,15 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   return finish_step(J, exact_span);
 }
 
-__global__ void k_job_xchg(uint8_t* sel8, const uint64_t* gstart, const uint32_t* groups, const uint64_t* boff,
+__global__ void k_job_xchg(uint32_t* selbits, const uint64_t* gstart, const uint32_t* groups, const uint64_t* boff,
                            uint8_t* buf, int import) {
   const uint32_t g = groups[blockIdx.y];
   const uint64_t gb = gstart[g], ng = gstart[g + 1] - gb, o = boff[blockIdx.y];
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < ng; r += (uint64_t)gridDim.x * blockDim.x) {
     if (import) {
-      if (buf[o + r]) sel8[gb + r] = 1;
+      if (buf[o + r]) set_bits(&selbits[(gb + r) >> 5], 1u << ((gb + r) & 31));
     } else {
-      buf[o + r] = sel8[gb + r];
+      buf[o + r] = (uint8_t)sel_bit(selbits, gb + r);
     }
   }
 }
@@ -973,11 +964,11 @@ void minimize_raw_xchg(MinJob& J, const uint32_t* groups, const uint64_t* offset
   }
   SYZ_HIP(hipStreamWaitEvent(s, J.done, 0));
   const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>(1, (maxn + 1023) / 1024), 1024);
-  k_job_xchg<<<dim3(gx, ng), 256, 0, s>>>(J.sel8.p, J.gstart.p, J.xg.p, J.xo.p, buf, import);
+  k_job_xchg<<<dim3(gx, ng), 256, 0, s>>>(J.selbits.p, J.gstart.p, J.xg.p, J.xo.p, buf, import);
   SYZ_LAUNCHED();
 }
 
-__global__ __launch_bounds__(256) void k_sel_flags(const uint8_t* sel8, const uint32_t* ent_of_rank, size_t n,
+__global__ __launch_bounds__(256) void k_sel_flags(const uint32_t* selbits, const uint32_t* ent_of_rank, size_t n,
                                                    const uint16_t* prog_len, const uint32_t* group,
                                                    const uint8_t* count_hist, int32_t C, uint8_t* selected,
                                                    int64_t* hist, int* err) {
@@ -989,7 +980,7 @@ __global__ __launch_bounds__(256) void k_sel_flags(const uint8_t* sel8, const ui
   }
   for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
     const uint32_t e = ent_of_rank[r];
-    const uint32_t s = sel8[r];
+    const uint32_t s = sel_bit(selbits, r);
     if (selected) selected[e] = (uint8_t)s;
     if (do_hist && s && (!count_hist || count_hist[group[e]])) {
       const uint32_t L = prog_len[e];
@@ -1006,19 +997,19 @@ __global__ __launch_bounds__(256) void k_sel_flags(const uint8_t* sel8, const ui
   }
 }
 
-// sel8 must hold 32 * ceil(n / 32) + 64 bytes, zero past n
-void sel_compact_dev(const uint8_t* sel8, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
+// selbits: the rank bitmap, n / 32 + 1 words at least, zero past n
+void sel_compact_dev(const uint32_t* selbits, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
                      int64_t* out_idx, uint64_t* group_out_off, hipStream_t s) {
   Scratch& sc = ctx().scratch;
   const size_t nw = (n + 31) / 32;
   uint64_t* wpos = sc.get<uint64_t>("pm_wpos", nw + 2);
-  scan_f<1>(SelWordsFn{sel8}, nw, wpos, nullptr, s, "sel");
+  scan_f<1>(SelWordsFn{selbits}, nw, wpos, nullptr, s, "sel");
   if (out_idx && n) {
-    k_sel_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(sel8, wpos, ent_of_rank, n, out_idx);
+    k_sel_compact<<<grid_for(n, 256, 8192), 256, 0, s>>>(selbits, wpos, ent_of_rank, n, out_idx);
     SYZ_LAUNCHED();
   }
   if (group_out_off) {
-    k_sel_goff<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(sel8, wpos, gstart, G, group_out_off);
+    k_sel_goff<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(selbits, wpos, gstart, G, group_out_off);
     SYZ_LAUNCHED();
   }
 }
@@ -1044,11 +1035,12 @@ void minimize_raw_end(MinJob& J, const RawEndArgs& e) {
   if (e.len_hist) SYZ_HIP(hipMemsetAsync(e.len_hist, 0, (size_t)(e.C + 1) * 8, s));
   if (n) {
     k_sel_flags<<<grid_for(n, 256, 512), 256, e.len_hist ? (size_t)(e.C + 1) * 8 : 0, s>>>(
-        J.sel8.p, J.ent_of_rank.p, n, e.len_hist ? J.prog_len : nullptr, J.group, dcount, e.C, e.selected,
+        J.selbits.p, J.ent_of_rank.p, n, e.len_hist ? J.prog_len : nullptr, J.group, dcount, e.C, e.selected,
         e.len_hist, err);
     SYZ_LAUNCHED();
   }
-  if (e.out_idx || e.group_out_off) sel_compact_dev(J.sel8.p, J.ent_of_rank.p, J.gstart.p, n, G, e.out_idx, e.group_out_off, s);
+  if (e.out_idx || e.group_out_off)
+    sel_compact_dev(J.selbits.p, J.ent_of_rank.p, J.gstart.p, n, G, e.out_idx, e.group_out_off, s);
   if (e.len_hist && !e.defer_check) {  // len(p.Calls) > C is Go's index-out-of-range panic (prio.go:148)
     int* herr = c.pinned.get<int>(4);
     SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, s));

@@ -121,7 +121,7 @@ struct MinJob {
   const uint32_t* group = nullptr;     // caller's device buffers (valid from begin to end)
   const uint16_t* prog_len = nullptr;
   Grow<uint64_t> gstart;
-  Grow<uint8_t> sel8;  // kept flag per global rank (Go-sort position), zero-padded to 32 * k + 64
+  Grow<uint32_t> selbits;  // kept bit per global rank (Go-sort position), n / 32 + 2 words
   Grow<uint32_t> ent_of_rank, rank_of_member, xg;
   Grow<uint64_t> xo;
   Grow<uint8_t> count_hist;
@@ -146,7 +146,7 @@ void minimize_raw_end_check(int err);  // the deferred check of end's device err
 void minimize_raw_fetch(MinJob& J, int64_t* out_idx, uint64_t* group_out_off);
 void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, uint32_t G, std::vector<PGroup>& pg);
 // group-major kept list (device) from a rank bitmap
-void sel_compact_dev(const uint8_t* sel8, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
+void sel_compact_dev(const uint32_t* selbits, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
                      int64_t* out_idx, uint64_t* group_out_off, hipStream_t s);
 
 // minimize.hip

@@ -176,7 +176,6 @@ void corpus_minimize_end(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_h
 void corpus_minimize_dev(Corpus& K, int32_t C, uint8_t* selected, int64_t* len_hist, hipStream_t s);
 void corpus_sel_xchg(Corpus& K, const uint32_t* groups, const uint64_t* offsets, uint32_t ng, uint8_t* buf,
                      int import, hipStream_t s);
-void sel_bits_bytes_dev(const uint32_t* bits, size_t n, uint8_t* out, hipStream_t s);
 void corpus_partition(Corpus& K, std::vector<uint64_t>& hpcs, hipStream_t s);
 void corpus_upload_work(Corpus& K, hipStream_t s);
 

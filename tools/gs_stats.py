@@ -13,7 +13,7 @@ import numpy as np  # noqa: E402
 from syzkaller_amd import _lib, cover, synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-p = synth.params(0x5EED0004, n, 289, 2_000_000)
+p = synth.params(int(os.environ.get("GS_SEED", "0x5EED0004"), 0), n, 289, int(os.environ.get("GS_NPCS", "2000000")))
 group, off, plen = synth.layout(p)
 order = np.argsort(group, kind="stable")
 lens = np.diff(off)[order].astype(np.uint64)
