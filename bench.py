@@ -76,15 +76,13 @@ def parse():
     return ap.parse_args()
 
 
-# the round's committed rocprofv3 kernel summary of this bench command (tools/gpu_final.sh): its top
+# the round's committed rocprofv3 kernel summary of this bench command (tools/gpu_final5.sh): its top
 # kernel by total GPU time names the roofline kernel
-ROCPROF_STATS = os.path.join(ROOT, "profiles", "r04_kernel_stats.csv")
-# rocprofv3 kernel name -> the library's profiling scope around that kernel
+ROCPROF_STATS = os.path.join(ROOT, "profiles", "r05_kernel_stats.csv")
+# rocprofv3 kernel name -> the library's profiling scope around that kernel; the same
+# names key profiles/pmc_traffic.json (tools/pmc_traffic.py)
 ROCPROF_SCOPE = [("k_slab<", "k_slab"), ("k_smin_direct", "k_pmin_direct"), ("k_smin_hash<false>", "k_pmin_hash"),
-                 ("k_smin_hash<true>", "k_pmin_packed"),
-                 ("k_region<512, 40, false, false>", "k_region"), ("k_region<512, 40, false, true>", "k_region_count"),
-                 ("k_pmin_direct", "k_pmin_direct"), ("k_pmin_hash<false>", "k_pmin_hash"),
-                 ("k_pmin_hash<true>", "k_pmin_packed"), ("k_colscan", "k_colscan")]
+                 ("k_smin_hash<true>", "k_pmin_packed")]
 
 
 # the workload the committed rocprofv3 summary and PMC passes were taken on: the default bench line

@@ -14,15 +14,21 @@ import os
 import sys
 
 
+# kernel name -> the bench's profiling scope around it (bench.py ROCPROF_SCOPE)
+SCOPES = [("k_slab<", "k_slab"), ("k_smin_direct", "k_pmin_direct"), ("k_smin_hash<false>", "k_pmin_hash"),
+          ("k_smin_hash<true>", "k_pmin_packed")]
+
+
 def short(name, grid):
-    """The kernel's base name (`void syz::k_part4<512, 40, false>(...)` -> `k_part4`): the names the
-    bench's per-kernel scopes use."""
+    """The bench scope of a kernel (k_smin_direct -> k_pmin_direct), else its base name
+    (`void syz::k_gr_swap<true>(...)` -> `k_gr_swap`)."""
+    for pat, scope in SCOPES:
+        if pat in name:
+            return scope
     head = name.split("(")[0]
     base = head.split("<")[0].split("::")[-1].strip()
     if base.startswith("void "):
         base = base[5:]
-    if base == "k_region" and head.replace(" ", "").endswith(",true>"):
-        base = "k_region_count"  # the count pass (bench scope name), k_region<.., COUNT = true>
     return base or None
 
 
