@@ -14,14 +14,14 @@ def test_rocprof_top_of_the_committed_summary():
     assert top is not None
     scope, name = top
     assert scope in dict((s, s) for _, s in bench.ROCPROF_SCOPE)
-    assert name.split("(")[0].split("::")[-1].startswith(scope.replace("_count", ""))
+    assert any(pat in name and s == scope for pat, s in bench.ROCPROF_SCOPE)
 
 
-def test_rocprof_scope_names_the_count_and_scatter_apart(tmp_path):
-    for kernel, scope in (("void syz::k_region<512, 40, false, false>(unsigned int const*)", "k_region"),
-                          ("void syz::k_region<512, 40, false, true>(unsigned int const*)", "k_region_count"),
-                          ("syz::k_pmin_direct(syz::PItem const*)", "k_pmin_direct"),
-                          ("void syz::k_pmin_hash<true>(syz::PItem const*)", "k_pmin_packed")):
+def test_rocprof_scope_names_the_table_kinds_apart(tmp_path):
+    for kernel, scope in (("void syz::k_slab<512, 32, false>(unsigned int const*)", "k_slab"),
+                          ("syz::k_smin_direct(syz::PItem const*)", "k_pmin_direct"),
+                          ("void syz::k_smin_hash<false>(syz::PItem const*)", "k_pmin_hash"),
+                          ("void syz::k_smin_hash<true>(syz::PItem const*)", "k_pmin_packed")):
         f = tmp_path / "stats.csv"
         f.write_text('"Name","Calls","TotalDurationNs"\n"%s",1,10\n' % kernel)
         assert bench.rocprof_top(str(f))[0] == scope
@@ -31,13 +31,13 @@ def test_rocprof_scope_names_the_count_and_scatter_apart(tmp_path):
 
 
 def test_dominant_kernel_follows_the_summary_else_the_serialized_pass(monkeypatch, tmp_path):
-    kern = {"k_region": {"ms": 1.3, "bytes": 3}, "k_pmin_direct": {"ms": 1.4, "bytes": 2},
+    kern = {"k_slab": {"ms": 1.3, "bytes": 3}, "k_pmin_direct": {"ms": 1.4, "bytes": 2},
             "gosort_level": {"ms": 9.0, "bytes": 0}, "m_big": {"ms": 5.0, "bytes": 7}}
     f = tmp_path / "stats.csv"
-    f.write_text('"Name","Calls","TotalDurationNs"\n"void syz::k_region<512, 40, false, false>(int)",1,10\n')
+    f.write_text('"Name","Calls","TotalDurationNs"\n"void syz::k_slab<512, 32, false>(int)",1,10\n')
     monkeypatch.setattr(bench, "ROCPROF_STATS", str(f))
     monkeypatch.setattr(bench.rocprof_top, "__defaults__", (str(f), bench.PROFILED_WORKLOAD))
-    assert bench.dominant_kernel(kern) == "k_region"
+    assert bench.dominant_kernel(kern) == "k_slab"
     monkeypatch.setattr(bench.rocprof_top, "__defaults__", (str(tmp_path / "missing.csv"), bench.PROFILED_WORKLOAD))
     # phase scopes (no k_ prefix) and kernels without a byte model never name the roofline
     assert bench.dominant_kernel(kern) == "k_pmin_direct"
