@@ -33,6 +33,68 @@ struct ScanState {
 ScanState scan_state(const char* tag, size_t tiles, int nv, hipStream_t s);  // runtime.hip
 constexpr uint64_t SCAN_VMASK = (1ull << 56) - 1;
 
+// Tile t's exclusive prefix by decoupled look-back, run by ONE whole wave: publishes t's sums tot
+// (flag 1), reads 64 predecessors' words at once (the nearest inclusive prefix ends it, else the
+// window's sums are added and it moves 64 tiles back), publishes t's inclusive prefix (flag 2) and
+// returns the exclusive one in excl on every lane. Tiles must be taken in ticket order (st.ticket), so
+// every predecessor belongs to a running workgroup.
+template <int NV>
+__device__ __forceinline__ void scan_lookback(const ScanState& st, uint32_t t, const uint64_t* tot, uint64_t* excl) {
+  const unsigned lane = __lane_id();
+  const uint64_t ep = (uint64_t)st.epoch << 56, f_agg = (1ull << 62) | ep, f_inc = (2ull << 62) | ep;
+  auto put = [&](uint64_t f, const uint64_t* x) {
+#pragma unroll
+    for (int q = 0; q < NV; q++)
+      __hip_atomic_store(&st.words[(size_t)t * NV + q], f | (x[q] & SCAN_VMASK), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  };
+#pragma unroll
+  for (int q = 0; q < NV; q++) excl[q] = 0;
+  if (t > 0) {
+    if (lane == 0) put(f_agg, tot);
+    uint32_t spins = 0;
+    for (int64_t w0 = (int64_t)t - 1; w0 >= 0;) {  // window: tiles w0, w0 - 1, ..., w0 - 63
+      const int64_t i = w0 - (int64_t)lane;
+      uint64_t w[NV];
+      bool ready = true, inc = false;
+      if (i >= 0) {
+#pragma unroll
+        for (int q = 0; q < NV; q++)
+          w[q] = __hip_atomic_load(&st.words[(size_t)i * NV + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t h = w[0] & ~SCAN_VMASK;
+        ready = h == f_agg || h == f_inc;
+#pragma unroll
+        for (int q = 1; q < NV; q++) ready = ready && (w[q] & ~SCAN_VMASK) == h;  // (both words one state)
+        inc = ready && h == f_inc;
+      } else {
+#pragma unroll
+        for (int q = 0; q < NV; q++) w[q] = 0;
+      }
+      const uint64_t incm = __ballot(inc);
+      // lanes up to the nearest inclusive prefix must all be ready
+      const int last = incm ? __ffsll((unsigned long long)incm) - 1 : 63;
+      const uint64_t need = last >= 63 ? ~0ull : ((2ull << last) - 1);
+      if ((__ballot(ready) & need) != need) {
+        // (a predecessor that never publishes is a bug: left, not waited for forever; the output is
+        // then wrong and the parity tests say so)
+        if (++spins == (1u << 24)) break;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+#pragma unroll
+      for (int q = 0; q < NV; q++) excl[q] += wave_sum_u64((int)lane <= last ? (w[q] & SCAN_VMASK) : 0ull);
+      if (incm || w0 < 64) break;
+      w0 -= 64;
+    }
+  }
+  if (lane == 0) {
+    uint64_t inc[NV];
+#pragma unroll
+    for (int q = 0; q < NV; q++) inc[q] = excl[q] + tot[q];
+    put(f_inc, inc);
+  }
+}
+
 // f(i, v): the NV values of element i (i < n). out_k[i] = the sum of sequence k before i; out_k[n] =
 // its total.
 template <int NV, class F>
@@ -67,66 +129,12 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_f(F f, size_t n, uint64_t* 
     for (int k = 0; k < SCAN_ITEMS; k++) s += v[q][k];
     pre[q] = block_excl_scan<SCAN_BLOCK>(s, lds, &tot[q]);
   }
-  // the look-back, by wave 0: its lanes read 64 predecessors' words at once; the nearest inclusive
-  // prefix ends it, else the window's sums are added and it moves 64 tiles back
   if (threadIdx.x < 64) {
-    const unsigned lane = threadIdx.x;
-    const uint64_t ep = (uint64_t)st.epoch << 56, f_agg = (1ull << 62) | ep, f_inc = (2ull << 62) | ep;
-    auto put = [&](uint64_t f, const uint64_t* x) {
-#pragma unroll
-      for (int q = 0; q < NV; q++)
-        __hip_atomic_store(&st.words[(size_t)t * NV + q], f | (x[q] & SCAN_VMASK), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    };
     uint64_t excl[NV];
+    scan_lookback<NV>(st, t, tot, excl);
+    if (threadIdx.x == 0)
 #pragma unroll
-    for (int q = 0; q < NV; q++) excl[q] = 0;
-    if (t > 0) {
-      if (lane == 0) put(f_agg, tot);
-      uint32_t spins = 0;
-      for (int64_t w0 = (int64_t)t - 1; w0 >= 0;) {  // window: tiles w0, w0 - 1, ..., w0 - 63
-        const int64_t i = w0 - (int64_t)lane;
-        uint64_t w[NV];
-        bool ready = true, inc = false;
-        if (i >= 0) {
-#pragma unroll
-          for (int q = 0; q < NV; q++)
-            w[q] = __hip_atomic_load(&st.words[(size_t)i * NV + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint64_t h = w[0] & ~SCAN_VMASK;
-          ready = h == f_agg || h == f_inc;
-#pragma unroll
-          for (int q = 1; q < NV; q++) ready = ready && (w[q] & ~SCAN_VMASK) == h;  // (both words one state)
-          inc = ready && h == f_inc;
-        } else {
-#pragma unroll
-          for (int q = 0; q < NV; q++) w[q] = 0;
-        }
-        const uint64_t incm = __ballot(inc);
-        // lanes up to the nearest inclusive prefix must all be ready
-        const int last = incm ? __ffsll((unsigned long long)incm) - 1 : 63;
-        const uint64_t need = last >= 63 ? ~0ull : ((2ull << last) - 1);
-        if ((__ballot(ready) & need) != need) {
-          // (a predecessor that never publishes is a bug: left, not waited for forever; the scan's output
-          // is then wrong and the parity tests say so)
-          if (++spins == (1u << 24)) break;
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-#pragma unroll
-        for (int q = 0; q < NV; q++) excl[q] += wave_sum_u64((int)lane <= last ? (w[q] & SCAN_VMASK) : 0ull);
-        if (incm || w0 < 64) break;
-        w0 -= 64;
-      }
-    }
-    if (lane == 0) {
-      uint64_t inc[NV];
-#pragma unroll
-      for (int q = 0; q < NV; q++) {
-        inc[q] = excl[q] + tot[q];
-        excl_s[q] = excl[q];
-      }
-      put(f_inc, inc);
-    }
+      for (int q = 0; q < NV; q++) excl_s[q] = excl[q];
   }
   __syncthreads();
 #pragma unroll
