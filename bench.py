@@ -966,10 +966,19 @@ def canonicalize_leg(args, dev, L, read_prof=None):
     ms = tot / steps * 1e3
     nin, nout = int(raw.numel()), int(out_len.sum().item())
     ok = nout == int(c.off[-1])  # the raw batch canonicalizes back to the distinct PCs of each cover
+    kms = None
+    if read_prof is not None:  # one more pass with HIP events around the phases (not timed)
+        L.syzgpu_profile_only(None)
+        L.syzgpu_profile_enable(1)
+        work.copy_(raw)
+        cover.CanonicalizeBatchDev(work, off, n, out_len, sptr)
+        kms = {k: round(e["ms"], 4) for k, e in read_prof().items()}
+        L.syzgpu_profile_enable(0)
     alg = 4 * nin + 4 * nout + 8 * (n + 1) + 8 * n
     res = {"workload": "config3's 1M covers as raw kcov output: %d PCs (random order, ~20%% repeated) -> %d"
                        % (nin, nout),
            "ms_per_batch": round(ms, 3), "covers_per_s": round(n / ms * 1e3, 1), "canonical_pcs_match": ok,
+           "phases_ms": kms,
            "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "algorithmic_bytes": int(alg)}}

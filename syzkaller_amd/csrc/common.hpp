@@ -169,12 +169,14 @@ struct ProfScope {
   ProfScope(const char* name, hipStream_t st, uint64_t bytes) : s(st), on(prof().on && prof().match(name)) {
     if (on) rec = prof().begin(name, s, bytes);
   }
-  ~ProfScope() {
+  void end() {  // (early, before the scope closes)
     if (on) prof().end(rec, s);
+    on = false;
   }
+  ~ProfScope() { end(); }
 };
 
-// ---- device-wide scans (scan.hip) ----------------------------------------------------------
+// ---- device-wide scans (scan.hpp, runtime.hip) ----------------------------------------------------------
 // out[i] = sum(in[0..i)), out[n] = total. in may be uint8_t / uint32_t / uint64_t.
 void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s);
 // tag: a distinct scratch name for scans that may run on another stream at the same time

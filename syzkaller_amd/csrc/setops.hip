@@ -1056,7 +1056,9 @@ __global__ __launch_bounds__(256) void k_canon_class(const uint64_t* off, size_t
 // covers and streams each maximal run of consecutive candidates as ONE contiguous range of PCs
 // (CANON_SCAN_U x 64 PCs a step, lane i of load k at PC 64 k + i), checking every PC against the one
 // before it. A break inside the run is either a cover start (the next cover's first PC) or a violation:
-// the wave resolves it by a ballot over its covers' start offsets (one per lane) and flags the cover. A
+// the wave resolves it by a ballot over its covers' start offsets (one per lane) and flags the cover;
+// the rest of a flagged cover's breaks in that load are skipped, and a run whose covers are all flagged
+// stops streaming (a raw cover with an increasing prefix: one step). A
 // strictly increasing cover is its own Canonicalize (sorted, no repeat; a 0xFFFFFFFF can only be its
 // last PC, kept unless it is the only one): its length goes to out_len and no network touches it. A
 // flagged candidate joins its length class. With every cover a candidate (the sorted batch) the pass is
@@ -1081,17 +1083,18 @@ __global__ __launch_bounds__(256) void k_canon_runs(const uint32_t* __restrict__
     const uint64_t ob = off[has ? c : ncov], oe = has ? off[c + 1] : ob;
     const bool ca = has && cand[c];
     uint64_t cm = __ballot(ca);
-    bool mybad = false;
+    uint64_t badm = 0;  // (wave-uniform) covers found not increasing
     while (cm) {
       const int s = __ffsll((unsigned long long)cm) - 1;
       const uint64_t inv = ~cm & (~0ull << s);  // lanes at or after s that are not candidates
       const int e = inv ? __ffsll((unsigned long long)inv) - 1 : 64;
       cm = e >= 64 ? 0 : (cm & (~0ull << e));
+      const uint64_t runm = (e >= 64 ? ~0ull : ((1ull << e) - 1)) & (~0ull << s);
       const uint64_t jb = readlane64(ob, s), je = readlane64(oe, e - 1);
       const bool inrun = (int)lane >= s && (int)lane < e;
       const uint32_t* x = pcs;
       uint32_t last = 0;
-      for (uint64_t j0 = jb; j0 < je; j0 += 64 * CANON_SCAN_U) {
+      for (uint64_t j0 = jb; j0 < je && (badm & runm) != runm; j0 += 64 * CANON_SCAN_U) {
         uint32_t v[CANON_SCAN_U];
 #pragma unroll
         for (int k = 0; k < CANON_SCAN_U; k++) {
@@ -1109,7 +1112,14 @@ __global__ __launch_bounds__(256) void k_canon_runs(const uint32_t* __restrict__
             vm &= vm - 1;
             const uint64_t jj = j0 + 64 * k + bl;
             const int L = s + __popcll(__ballot(inrun && ob <= jj)) - 1;
-            if (readlane64(ob, L) != jj && (int)lane == L) mybad = true;
+            if (readlane64(ob, L) != jj) {
+              badm |= 1ull << L;
+              // every cover of the run out of order (a raw cover with an increasing prefix): done
+              if ((badm & runm) == runm) break;
+              const uint64_t eL = readlane64(oe, L), p0 = j0 + 64 * k;  // cover L's other breaks here
+              const uint64_t eb = eL > p0 ? eL - p0 : 0;
+              vm &= eb >= 64 ? 0ull : ~((1ull << eb) - 1);
+            }
           }
         }
         last = (uint32_t)__builtin_amdgcn_readlane((int)v[CANON_SCAN_U - 1], 63);
@@ -1117,7 +1127,7 @@ __global__ __launch_bounds__(256) void k_canon_runs(const uint32_t* __restrict__
     }
     if (ca) {
       const uint64_t n = oe - ob;
-      if (!mybad) {
+      if (!((badm >> lane) & 1ull)) {
         out_len[c] = (n == 1 && pcs[ob] == 0xFFFFFFFFu) ? 0 : n;
       } else {  // not canonical after all: the network of its length class
         const int k = canon_class_of(n);
@@ -1164,6 +1174,7 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   // the long classes (few covers, long per-cover chains: the 32768 class is one workgroup's bitonic
   // network) on the side stream, started first, beside the short classes' persistent walks
   ensure_side(c);
+  ProfScope psn("canon_nets", s, 0);
   SYZ_HIP(hipEventRecord(c.ev_fork, s));
   SYZ_HIP(hipStreamWaitEvent(c.side, c.ev_fork, 0));
   k_canon_cls<CANON_LDS2, CANON_BLOCK><<<ncu, CANON_BLOCK, 0, c.side>>>(pcs, off, lists + 9 * ncov, cnt + 9, out_len);
@@ -1188,6 +1199,7 @@ void canonicalize_batch_dev2(uint32_t* pcs, const uint64_t* off, size_t ncov, ui
   k_canon_net<1><<<ncu * 8, 256, 0, s>>>(pcs, off, lists, cnt, out_len);
   SYZ_LAUNCHED();
   SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
+  psn.end();
   // longer covers: their list back to the host, then the global network one by one
   uint32_t* h = c.pinned.get<uint32_t>(CANON_NCLS);
   SYZ_HIP(hipMemcpyAsync(h, cnt, CANON_NCLS * 4, hipMemcpyDeviceToHost, s));
