@@ -226,6 +226,12 @@ ScanState scan_state(const char* tag, size_t tiles, int nv, hipStream_t s) {
   return ScanState{buf + 32, reinterpret_cast<uint32_t*>(buf), ep.second.second};
 }
 
+uint64_t* scan_scratch(const char* tag, int depth, size_t words) {
+  char k[96];
+  snprintf(k, sizeof k, "scan2_%s.%d", tag, depth);
+  return ctx().scratch.get<uint64_t>(k, words);
+}
+
 template <class T>
 struct LoadFn {
   const T* in;

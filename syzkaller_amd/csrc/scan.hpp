@@ -152,16 +152,102 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_f(F f, size_t n, uint64_t* 
 
 __global__ void k_scan_zero(uint64_t* out0, uint64_t* out1);  // runtime.hip: the totals of an empty scan
 
+// Long scans (more tiles than SCAN_LB_MAX): reduce-then-scan instead, since every tile of a long
+// single-pass scan is in flight at once and its look-back walks back far before it meets an inclusive
+// prefix (a 9M-element scan measured slower than three launches). Tile sums, a scan of them, then the
+// tiles again with their offsets.
+constexpr size_t SCAN_LB_MAX = 512;
+template <int NV, class F>
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums_f(F f, size_t n, uint64_t* sums, uint32_t tiles) {
+  __shared__ uint64_t lds[SCAN_BLOCK / 64 + 1];
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+  uint64_t acc[NV];
+#pragma unroll
+  for (int q = 0; q < NV; q++) acc[q] = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    uint64_t x[NV];
+#pragma unroll
+    for (int q = 0; q < NV; q++) x[q] = 0;
+    if (base + k < n) f(base + k, x);
+#pragma unroll
+    for (int q = 0; q < NV; q++) acc[q] += x[q];
+  }
+#pragma unroll
+  for (int q = 0; q < NV; q++) {
+    uint64_t tot;
+    block_excl_scan<SCAN_BLOCK>(acc[q], lds, &tot);
+    if (threadIdx.x == 0) sums[(size_t)q * tiles + blockIdx.x] = tot;
+  }
+}
+template <int NV, class F>
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply_f(F f, size_t n, const uint64_t* offs0, const uint64_t* offs1,
+                                                             uint64_t* out0, uint64_t* out1, uint32_t tiles) {
+  __shared__ uint64_t lds[SCAN_BLOCK / 64 + 1];
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+  uint64_t v[NV][SCAN_ITEMS];
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    uint64_t x[NV];
+#pragma unroll
+    for (int q = 0; q < NV; q++) x[q] = 0;
+    if (base + k < n) f(base + k, x);
+#pragma unroll
+    for (int q = 0; q < NV; q++) v[q][k] = x[q];
+  }
+#pragma unroll
+  for (int q = 0; q < NV; q++) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) s += v[q][k];
+    uint64_t tot;
+    uint64_t p = block_excl_scan<SCAN_BLOCK>(s, lds, &tot) + (q == 0 ? offs0 : offs1)[blockIdx.x];
+    uint64_t* out = q == 0 ? out0 : out1;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+      if (base + k < n) out[base + k] = p;
+      p += v[q][k];
+    }
+    if (blockIdx.x == tiles - 1 && threadIdx.x == SCAN_BLOCK - 1) out[n] = p;
+  }
+}
+template <int NV>
+struct ScanSumsFn {
+  const uint64_t* sums;
+  uint32_t tiles;
+  __device__ void operator()(size_t i, uint64_t* v) const {
+#pragma unroll
+    for (int q = 0; q < NV; q++) v[q] = sums[(size_t)q * tiles + i];
+  }
+};
+uint64_t* scan_scratch(const char* tag, int depth, size_t words);  // runtime.hip
+
 // tag: scans that may run at the same time (other streams) take different tags
 template <int NV, class F>
-void scan_f(F f, size_t n, uint64_t* out0, uint64_t* out1, hipStream_t s, const char* tag) {
+void scan_f(F f, size_t n, uint64_t* out0, uint64_t* out1, hipStream_t s, const char* tag, int depth = 0) {
   if (n == 0) {
     k_scan_zero<<<1, 1, 0, s>>>(out0, NV > 1 ? out1 : nullptr);
     SYZ_LAUNCHED();
     return;
   }
   const size_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  const ScanState st = scan_state(tag, tiles, NV, s);
+  if (tiles > SCAN_LB_MAX) {
+    if (tiles >= 0xFFFFFFFFull) fail(SYZGPU_EINVAL, "scan too long");
+    uint64_t* buf = scan_scratch(tag, depth, (NV + NV) * (tiles + 1));
+    uint64_t* sums = buf;
+    uint64_t* offs = buf + NV * (tiles + 1);
+    k_scan_sums_f<NV, F><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(f, n, sums, (uint32_t)tiles);
+    SYZ_LAUNCHED();
+    scan_f<NV>(ScanSumsFn<NV>{sums, (uint32_t)tiles}, tiles, offs, NV > 1 ? offs + (tiles + 1) : nullptr, s, tag,
+               depth + 1);
+    k_scan_apply_f<NV, F><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(f, n, offs, NV > 1 ? offs + (tiles + 1) : nullptr,
+                                                                  out0, out1, (uint32_t)tiles);
+    SYZ_LAUNCHED();
+    return;
+  }
+  char t2[64];
+  snprintf(t2, sizeof t2, "%s.%d", tag, depth);
+  const ScanState st = scan_state(depth ? t2 : tag, tiles, NV, s);
   k_scan_f<NV, F><<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(f, n, out0, out1, st, (uint32_t)tiles);
   SYZ_LAUNCHED();
 }
