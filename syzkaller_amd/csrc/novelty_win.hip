@@ -26,8 +26,10 @@
 // windows (2^15 x 1024 = 32M addresses); a wider span takes hashed windows (k_nw_hash: a window size
 // per call, an open-addressing LDS table, the kept keys sorted per address sub-range and stored as a
 // list), up to the whole u32 space. Only G > 4096 falls back to the keyed table (novelty.hip).
-// Measured and dropped (profiles/r02_ab/novelty_ab.md): hashed windows for the calls with few PCs per
-// window inside a narrow span, persistent workgroups with the next item prefetched, branch-free batches.
+// Inside a narrow span the calls with few PCs per direct window take hashed windows too (NW_HSPARSE;
+// measured slower in round 2, before the slab transpose, and faster since: 4.30 -> 3.92 ms at config
+// 3). Measured and dropped (profiles/r02_ab/novelty_ab.md): persistent workgroups with the next item
+// prefetched, branch-free batches.
 #include <algorithm>
 #include <cstdlib>
 #include <numeric>
@@ -281,7 +283,7 @@ __global__ void k_nw_hcap(const NwGroup* ng_, const SGroup* sg, const uint32_t* 
   for (uint64_t sl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; sl < slots; sl += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t g = nw_slot_group(ng_, G, sl);
     const uint32_t w = (uint32_t)(sl - ng_[g].sbase);
-    hcap[sl] = w < sg[g].W ? wtot[sg[g].wbase + w] : 0u;
+    hcap[sl] = w < sg[g].W && sg[g].wbase != SG_NO_WTOT ? wtot[sg[g].wbase + w] : 0u;  // (direct windows: none)
   }
 }
 
@@ -523,7 +525,7 @@ __global__ __launch_bounds__(NE_BLOCK) void k_nw_emit(const uint32_t* __restrict
     if (threadIdx.x == 0) out[p0] = SENT;
     return;
   }
-  if (hbase) {
+  if (hbase && pg[g].mode == PMODE_HASH) {
     const uint32_t wlo = lo + (w << S);
     const uint32_t* src = hkeys + hbase[slot];
     for (uint64_t i = threadIdx.x; i < c; i += NE_BLOCK) out[p0 + i] = wlo + src[i];
@@ -571,6 +573,17 @@ static int nwh_dbg() {
 
 // SYZGPU_NW_BITS=14|15: direct window bits (default: 14 while the span fits 1024 such windows, else 15;
 // 13-bit windows measured slower, r05: 5.83 vs 4.61 ms at config 3)
+// Inside a span that fits direct windows, the calls with fewer than NW_HSPARSE PCs per direct window
+// take hashed windows: a direct window's fixed costs (its 64 KB table cleared and scanned, a 2 KB
+// bitmap out, one run per slab of the call) outweigh its few elements there. Config 3 (r05_novmix2):
+// 4.30 ms all direct; 256 4.35, 512 4.09, 1024 3.92 ms. SYZGPU_NW_HSPARSE=t overrides (0: all direct).
+constexpr uint64_t NW_HSPARSE = 1024;
+static uint64_t nw_hsparse() {
+  static const uint64_t v =
+      getenv("SYZGPU_NW_HSPARSE") ? (uint64_t)atoll(getenv("SYZGPU_NW_HSPARSE")) : NW_HSPARSE;
+  return v;
+}
+
 static uint32_t nw_bits_forced() {
   static const uint32_t v = getenv("SYZGPU_NW_BITS") ? (uint32_t)atoi(getenv("SYZGPU_NW_BITS")) : 0u;
   return v == 14 || v == 15 ? v : 0u;
@@ -635,41 +648,54 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   auto nwin = [&](uint32_t sb) { return (((uint64_t)hi - lo) >> sb) + 1; };
   uint32_t DB = nw_bits_forced();
   if (!DB) DB = nwin(14) <= WMAX ? 14 : 15;
-  const bool hashed = force_hash || nwin(DB) > WMAX;
+  const bool hashed = force_hash || nwin(DB) > WMAX;  // every call on hashed windows
   uint32_t smin = 15;  // hashed windows: the narrowest size whose windows fit WMAX
   while (nwin(smin) > WMAX) smin++;
   const uint32_t WD = hashed ? 0u : (uint32_t)nwin(DB);
-  // ---- plan: direct — every call on WD windows of 2^DB addresses; hashed — a window size per call
-  // (about NW_HTARGET PCs per window); regions, blocks, work items ----
+  const uint64_t hsparse = nw_hsparse();
+  // ---- plan: direct — a call on WD windows of 2^DB addresses; hashed — a window size per call (about
+  // NW_HTARGET PCs per window): every call when the span is too wide for direct windows, else the calls
+  // with fewer than hsparse PCs per direct window (SYZGPU_NW_HSPARSE); regions, blocks, work items ----
   std::vector<PGroup> hpg(G);
   std::vector<NwGroup> hng(G + 1);
   uint64_t kw = 0, slots = 0;
+  bool any_hash = false, any_direct = false;
   for (uint32_t g = 0; g < G; g++) {
     uint32_t S = DB, W = WD;
-    if (hashed) {
+    const bool hg = hashed || hpcs[g] < hsparse * WD;
+    any_hash |= hg;
+    any_direct |= !hg;
+    if (hg) {
       const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(WMAX, (hpcs[g] + NW_HTARGET - 1) / NW_HTARGET));
       S = smin;
       while (S < SMAX && nwin(S + 1) >= want) S++;
       W = (uint32_t)nwin(S);
     }
-    hpg[g] = PGroup{S, W, (uint32_t)(hashed ? PMODE_HASH : PMODE_DIRECT), 0};
+    hpg[g] = PGroup{S, W, (uint32_t)(hg ? PMODE_HASH : PMODE_DIRECT), 0};
     hng[g] = NwGroup{kw, slots};
-    if (!hashed) kw += (uint64_t)W << (S - 5);
+    if (!hg) kw += (uint64_t)W << (S - 5);
     slots += W + 1;
   }
   hng[G] = NwGroup{kw, slots};
   // slabs of the combined members (slab_dev.hpp); hashed windows need their per-window totals
   SlabJob SJ;
-  slab_plan(SJ, hstart, hpcs.data(), hpg, G, hashed);
+  slab_plan(SJ, hstart, hpcs.data(), hpg, G, any_hash);
   const uint32_t B = SJ.B;
   // items (call, window), larger calls first (their windows are the long ones) so the grid's tail is
-  // short: item i is window i % WD of call order[i / WD], generated on the device
+  // short. order = the direct calls (Gd), then the hashed ones (Gh); direct item i is window i % WD of
+  // call order[i / WD]; hashed item i is window i - iofs[j] of call order[Gd + j]
   std::vector<uint32_t> order(G);
   std::iota(order.begin(), order.end(), 0u);
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hpcs[x] > hpcs[y]; });
-  std::vector<uint32_t> iofs(G + 1, 0);  // hashed: the items of order[j] are [iofs[j], iofs[j + 1])
-  for (uint32_t j = 0; j < G; j++) iofs[j + 1] = iofs[j] + hpg[order[j]].W;
-  const size_t nitems = hashed ? (size_t)iofs[G] : (size_t)G * WD;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+    const bool hx = hpg[x].mode == PMODE_HASH, hy = hpg[y].mode == PMODE_HASH;
+    return hx != hy ? hy : hpcs[x] > hpcs[y];
+  });
+  uint32_t Gd = 0;
+  while (Gd < G && hpg[order[Gd]].mode == PMODE_DIRECT) Gd++;
+  const uint32_t Gh = G - Gd;
+  std::vector<uint32_t> iofs(G + 1, 0);  // hashed: the items of order[Gd + j] are [iofs[j], iofs[j + 1])
+  for (uint32_t j = 0; j < Gh; j++) iofs[j + 1] = iofs[j] + hpg[order[Gd + j]].W;
+  const size_t nitems_d = (size_t)Gd * WD, nitems_h = iofs[Gh];
   // one staging copy: PGroup[G+1], NwGroup[G+1], SGroup[G+1], gblock[G+1], bgroup[B+1], order[G+1], iofs[G+1]
   auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
   const size_t o_ng = al16((G + 1) * sizeof(PGroup)), o_sg = o_ng + al16((G + 1) * sizeof(NwGroup));
@@ -718,7 +744,7 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   const uint32_t* elems = SJ.elems;
   uint64_t* hbase = nullptr;
   uint32_t* hkeys = nullptr;
-  if (hashed) {
+  if (any_hash) {
     ProfScope ps("novelty_min_hash", s, total * 8 + slots * 20);
     uint32_t* hcap = sc.get<uint32_t>("nw_hcap", slots + 1);
     hbase = sc.get<uint64_t>("nw_hbase", slots + 1);
@@ -726,25 +752,25 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
     k_nw_hcap<<<grid_for(slots, 256, 4096), 256, 0, s>>>(dng, dsg, SJ.wtot, G, slots, hcap);
     SYZ_LAUNCHED();
     exclusive_scan_u32(hcap, hbase, slots, s);
-    if (nitems) {
-      k_nw_hash<<<(unsigned)nitems, NH_BLOCK, 0, s>>>(dorder, diofs, G, dsg, gslab, gebase, D, slabs, SJ.wtot, elems,
+    if (nitems_h) {
+      k_nw_hash<<<(unsigned)nitems_h, NH_BLOCK, 0, s>>>(dorder + Gd, diofs, Gh, dsg, gslab, gebase, D, slabs, SJ.wtot, elems,
                                                       cstart, lo, d_fl, nfl, dng, hbase, hkeys, wcount, sel8, upd, err,
                                                       nwh_dbg());
       SYZ_LAUNCHED();
     }
   }
   uint32_t* fstart = sc.get<uint32_t>("nw_fstart", (size_t)WD + 2);
-  if (!hashed) {
+  if (any_direct) {
     ProfScope ps("novelty_min", s, total * 4 + kw * 4);
     k_nw_fstart<<<grid_for(WD + 1, 256, 64), 256, 0, s>>>(d_fl, nfl, lo, WD, DB, fstart);
     SYZ_LAUNCHED();
-    if (nitems) {
+    if (nitems_d) {
       if (DB == 14)
-        k_nw_min<14><<<(unsigned)nitems, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, dsg, gslab, gebase, D, slabs, elems,
+        k_nw_min<14><<<(unsigned)nitems_d, NwCfg<14>::BLOCK, 0, s>>>(dorder, WD, dsg, gslab, gebase, D, slabs, elems,
                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
                                                                    upd, nw_dbg());
       else
-        k_nw_min<15><<<(unsigned)nitems, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, dsg, gslab, gebase, D, slabs, elems,
+        k_nw_min<15><<<(unsigned)nitems_d, NwCfg<15>::BLOCK, 0, s>>>(dorder, WD, dsg, gslab, gebase, D, slabs, elems,
                                                                    cstart, lo, d_fl, fstart, dng, kbits, wcount, sel8,
                                                                    upd, nw_dbg());
       SYZ_LAUNCHED();

@@ -472,11 +472,13 @@ void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* 
     const uint64_t stride = (hpcs[g] / 64 + ng) / SL_TILES + nb + 1;
     // a group's element offsets (D) are 32-bit
     if (hpcs[g] + stride * slab_pad(W) + 8 >= (1ull << 32)) fail(SYZGPU_EINVAL, "a call group with 2^32 or more PCs");
-    J.hsg[g] = SGroup{J.dtotal, S, W, (uint32_t)stride, memb, (uint32_t)J.wtotal, 0, J.xtotal};
+    // per-window totals (wtot) only for the hashed groups of a job that asks for them
+    const bool wt = want_wtot && hpg[g].mode == PMODE_HASH;
+    J.hsg[g] = SGroup{J.dtotal, S, W, (uint32_t)stride, memb, wt ? (uint32_t)J.wtotal : SG_NO_WTOT, 0, J.xtotal};
     J.wmax = std::max(J.wmax, W);
     J.xtotal += stride * slab_pad(W);
     J.dtotal += (uint64_t)(W + 1) * stride;
-    if (want_wtot) J.wtotal += W;
+    if (wt) J.wtotal += W;
     J.slab_bound += stride;
     J.total_pcs += hpcs[g];
   }

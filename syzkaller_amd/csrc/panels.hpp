@@ -28,12 +28,13 @@ struct PSlab {
   uint32_t j, pad;    // slab index inside its call group
 };
 
+constexpr uint32_t SG_NO_WTOT = 0xFFFFFFFFu;  // SGroup.wbase of a group without per-window totals
 struct SGroup {       // per call group, slab form
   uint64_t dbase;     // first D entry
   uint32_t S, W;      // window bits, windows
   uint32_t stride;    // D row length (>= the group's slabs)
   uint32_t memb;      // members per block: min(SL_MEMB, 2^(32 - S))
-  uint32_t wbase;     // first per-window total (wtot, when P is asked for them)
+  uint32_t wbase;     // first per-window total (wtot, when P is asked for them), else SG_NO_WTOT
   uint32_t pad;       // bit 0: a big call group (the Go sort's global rounds; P's second launch)
   uint64_t xbase;     // element slots of the padding of the groups before (a slab's runs are padded to
                       // 4 elements: it takes its PCs + 3 W + 4 slots at most)

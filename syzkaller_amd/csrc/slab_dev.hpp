@@ -226,6 +226,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   __syncthreads();
   // lane k of this wave: tile t = wv + WAVES k (its member by a search of the tile prefix)
   uint32_t alo, ahi, cz;
+  uint32_t pprev = 0;  // NOV: the PC before the lane's tile in its member (a tile other than the first)
   {
     const uint32_t t = wv + WAVES * lane;
     const uint32_t tt = t < nt ? t : 0u;
@@ -244,7 +245,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const uint32_t cnt = (t < nt && lane < (unsigned)TPW) ? min(64u, mln[a] - 64 * ti) : 0u;
     // count | (not the member's first tile) << 7 | (a table) << 8 | member tag << 9
     uint32_t fl = 0;
-    if constexpr (NOV) fl = (ti > 0 ? 0x80u : 0u) | (mtab[a] ? 0x100u : 0u);
+    if constexpr (NOV) {
+      fl = (ti > 0 ? 0x80u : 0u) | (mtab[a] ? 0x100u : 0u);
+      // loaded here, beside the tiles' loads, so the order check below waits for none of them one by one
+      if (ti > 0 && cnt) pprev = reinterpret_cast<const uint32_t*>((uintptr_t)addr)[-1];
+    }
     cz = cnt | fl | (a << 9);
   }
   // every tile's PCs into registers, all loads in flight (a tile's address is wave-uniform)
@@ -268,11 +273,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       const int eb = (z & 0x100u) ? 1 : 4;
       const uint32_t pv = lane_prev(v[k]);
       if (lane > 0 && lane < cnt && pv >= v[k]) bad |= eb;
-      if ((z & 0x80u) && lane == 0 && cnt) {
-        const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ahi, k) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)alo, k);
-        if (reinterpret_cast<const uint32_t*>((uintptr_t)base)[-1] >= v[k]) bad |= eb;
-      }
+      if ((z & 0x80u) && lane == 0 && cnt && (uint32_t)__builtin_amdgcn_readlane((int)pprev, k) >= v[k]) bad |= eb;
     }
   }
   // from here on v holds the PC's offset from lo: window = v >> S, offset in it = v & omask
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
   }
   __syncthreads();
-  if (wtot)
+  if (wtot && gp.wbase != SG_NO_WTOT)
     for (uint32_t i = threadIdx.x; i < W; i += BLOCK)
       if (hist[i]) atomicAdd(&wtot[gp.wbase + i], hist[i]);
   // padded window starts -> cursors (hist), pst, D rows

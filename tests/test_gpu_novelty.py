@@ -167,6 +167,36 @@ def _with_extremes(mcp, mco):
     return out, mco
 
 
+def test_novelty_mixed_windows_vs_literal_oracle(strategy):
+    # a narrow span (4 direct windows) where one call is dense (direct windows) and the others hold
+    # fewer than NW_HSPARSE PCs per direct window (hashed windows): both kernels in one batch, the
+    # updated tables interleaved by call in the output, bit-exact against the literal oracle
+    if strategy != "windows":
+        pytest.skip("the default strategy's per-call window choice")
+    rnd = np.random.default_rng(51)
+    base = 0x81000000
+    pool = (base + 4 * np.arange(16_000)).astype(np.uint32)  # 64K addresses
+    G = 5
+    covs, grp = [], []
+    for _ in range(1_500):  # call 2: ~600K PCs, dense
+        covs.append(np.unique(rnd.choice(pool, size=400)))
+        grp.append(2)
+    for g in (0, 1, 3, 4):
+        for _ in range(int(rnd.integers(20, 60))):
+            covs.append(np.unique(rnd.choice(pool, size=int(rnd.integers(0, 40)))))
+            grp.append(g)
+    order = rnd.permutation(len(covs))
+    covs = [covs[i].astype(np.uint32) for i in order]
+    grp = np.array(grp, np.uint32)[order]
+    mc = [np.unique(rnd.choice(pool, size=int(rnd.integers(0, 1_000)))).astype(np.uint32) for _ in range(G)]
+    flakes = np.unique(rnd.choice(pool, size=200)).astype(np.uint32)
+    pcs, off = oracle.to_csr(covs)
+    mcp, mco = oracle.to_csr(mc)
+    new, sc = _scopes(lambda: _check(pcs, off, grp, G, mcp, mco, flakes))
+    assert "novelty_min" in sc and "novelty_min_hash" in sc
+    assert 0 < new.sum() < len(covs)
+
+
 @pytest.mark.parametrize("span", ["256M", "u32"])
 def test_novelty_wide_span_small_vs_literal_oracle(span, strategy):
     # configs[2]-shaped data spread over a 280M-address span (past the direct windows' 32M) and over

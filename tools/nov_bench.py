@@ -19,7 +19,8 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     covers = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
     args = argparse.Namespace(ngroups=289, npcs=2_000_000, seed=0x5EED0004, novelty_covers=covers, steps=2 * steps,
-                              cpu_baseline=0, novelty_cpu_sample=0, novelty_wide=1)
+                              cpu_baseline=0, novelty_cpu_sample=0,
+                              novelty_wide=int(os.environ.get("NOV_WIDE", "1")))
     dev = torch.device("cuda", 0)
     L = _lib.lib()
     _lib.check(L.syzgpu_init(0))
