@@ -256,7 +256,11 @@ __global__ void k_nw_sent(const uint8_t* has_sent, const uint8_t* upd, const NwG
 constexpr uint32_t NW_HTARGET = 8192;
 constexpr int NH_BLOCK = 512;             // two workgroups per CU (74 KB of LDS each)
 constexpr uint32_t NH_PER = HS / NH_BLOCK;  // table slots per thread at compaction
-constexpr uint32_t NH_FLK = 512;         // flakes of a window kept in LDS for the lookup
+constexpr uint32_t NH_FLK = 256;         // flakes of a window kept in LDS for the lookup (more: global)
+constexpr uint32_t NH_FHS = 2 * NH_FLK;  // ... as an open-addressing set of window offsets (half full at most;
+                                         // 2 KB: two workgroups per CU)
+__device__ __forceinline__ uint32_t nh_fslot(uint32_t o) { return (o * 0x9E3779B1u) >> (32 - 9); }
+static_assert(NH_FHS == 512, "nh_fslot");
 constexpr uint32_t NH_NB_BITS = 11;      // order buckets of a sub-range: 2048
 constexpr uint32_t NH_NB = 1u << NH_NB_BITS;
 constexpr uint32_t NH_BSCAN = 64;        // keys of a bucket placed by a scan of it; more: the sort
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
   __shared__ uint32_t tabs[2 * HS];  // keys, values; then the sub-range's kept-offset bitmap
   __shared__ uint32_t bm[HBM_WORDS];
   __shared__ uint32_t red[NH_BLOCK / 64 + 1];
-  __shared__ uint32_t flk[NH_FLK];  // the window's flakes (when they fit)
+  __shared__ uint32_t fhs[NH_FHS];  // the window's flakes as offsets (when they fit): a hash set
   __shared__ int full;
   constexpr uint32_t NH_WBLK = 128;  // the walk's element windows: 8K elements (its scratch fits beside)
   __shared__ uint32_t wsc[2 * NH_BLOCK + 3 * NH_WBLK];
@@ -324,7 +328,17 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
   const uint64_t f1 = whi > 0xFFFFFFFFull ? nfl : lower_bound_dev<uint32_t>(fl, f0, nfl, (uint32_t)whi);
   const bool flds = f1 - f0 <= NH_FLK;  // searched in LDS, else in the global list
   const uint32_t nf = flds ? (uint32_t)(f1 - f0) : 0u;
-  for (uint32_t i = threadIdx.x; i < nf; i += NH_BLOCK) flk[i] = fl[f0 + i];
+  // (a set, not a sorted list searched per key: most keys of a batch are new, and each one's binary
+  // search was a chain of dependent LDS reads)
+  for (uint32_t i = threadIdx.x; i < NH_FHS; i += NH_BLOCK) fhs[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nf; i += NH_BLOCK) {
+    const uint32_t o = fl[f0 + i] - wlo;  // < 2^S <= 2^26: never the empty mark
+    for (uint32_t h = nh_fslot(o);; h = (h + 1) & (NH_FHS - 1)) {
+      const uint32_t prev = atomicCAS(&fhs[h], 0xFFFFFFFFu, o);
+      if (prev == 0xFFFFFFFFu || prev == o) break;
+    }
+  }
   const uint32_t span = (uint32_t)min<uint64_t>((uint64_t)HBM_WORDS * 32, ng);
   const uint32_t words = (span + 31) / 32;
   for (uint32_t i = threadIdx.x; i < words; i += NH_BLOCK) bm[i] = 0;
@@ -391,8 +405,13 @@ __global__ __launch_bounds__(NH_BLOCK) void k_nw_hash(const uint32_t* order, con
       if (!old && f1 > f0) {  // a flake no table holds: never new, never kept
         const uint32_t pc = wlo + kk[q];
         if (flds) {
-          const uint32_t x = (uint32_t)lower_bound_dev<uint32_t>(flk, 0, nf, pc);
-          if (x < nf && flk[x] == pc) continue;
+          bool isf = false;
+          for (uint32_t h = nh_fslot(kk[q]);; h = (h + 1) & (NH_FHS - 1)) {
+            const uint32_t x = fhs[h];
+            if (x == kk[q]) isf = true;
+            if (x == kk[q] || x == 0xFFFFFFFFu) break;
+          }
+          if (isf) continue;
         } else {
           const uint64_t x = lower_bound_dev<uint32_t>(fl, f0, f1, pc);
           if (x < f1 && fl[x] == pc) continue;
