@@ -743,8 +743,9 @@ bool novelty_windows(const uint32_t* d_pcs, const uint64_t* d_off, const uint32_
   uint32_t* wcount = sc.get<uint32_t>("nw_wcount", slots + 1);
   uint64_t* wpos = sc.get<uint64_t>("nw_wpos", slots + 1);
   {
-    // byte model: every PC read once and written once as an element, 48 B of member metadata
-    ProfScope ps("novelty_part", s, total * 8 + (uint64_t)nm * 48);
+    // byte model (as the Minimize transpose's): every PC read once + 10 B per member
+    // (offset, group id); the element buffer it writes is intermediate traffic, not algorithmic bytes
+    ProfScope ps("novelty_part", s, total * 4 + (uint64_t)nm * 10);
     slab_build(SJ, "nw", mlen, mpos, nm, cstart, s);
     NovSrc ns;
     ns.mc = d_mc;
