@@ -155,6 +155,36 @@ __device__ __forceinline__ uint32_t merge_path(RA A, uint32_t la, RB B, uint32_t
   return lo;
 }
 
+// the same search with three probes a step (a quarter of the range left each time): half the chain of
+// dependent loads of merge_path when the lists are in HBM (the probes' loads are in flight together)
+template <class RA, class RB>
+__device__ __forceinline__ uint32_t merge_path4(RA A, uint32_t la, RB B, uint32_t lb, uint32_t d) {
+  uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;
+  while (hi - lo >= 4) {  // every probe i in [lo, hi): A(i) and B(d - i - 1) exist
+    const uint32_t n = hi - lo, m1 = lo + n / 4, m2 = lo + n / 2, m3 = lo + 3 * (n / 4);
+    const uint32_t a1 = A(m1), b1 = B(d - m1 - 1), a2 = A(m2), b2 = B(d - m2 - 1), a3 = A(m3), b3 = B(d - m3 - 1);
+    if (!(a1 <= b1)) {
+      hi = m1;
+    } else if (!(a2 <= b2)) {
+      lo = m1 + 1;
+      hi = m2;
+    } else if (!(a3 <= b3)) {
+      lo = m2 + 1;
+      hi = m3;
+    } else {
+      lo = m3 + 1;
+    }
+  }
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (A(mid) <= B(d - mid - 1))
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
 // A tile's sub-lists a[a0, a0 + na) and b[b0, b0 + nb) (n = na | nb << 16) and its halo values: aprev, the a
 // taken just before the tile (a[a0 - 1]; without one, b[b0] - 1, which pairs with no b of the tile but a
 // sentinel); anext / bnext, the a / b taken after it (0xFFFFFFFF past the pair's end: the sentinel is never
@@ -173,15 +203,22 @@ __global__ void k_so_tdesc(const uint32_t* __restrict__ a, const uint64_t* __res
                            const uint64_t* __restrict__ tstart, const uint32_t* __restrict__ tpair, uint32_t npairs,
                            SoDesc* __restrict__ desc, int* flags, int* err) {
   const uint64_t ntiles = tstart[npairs];
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < ntiles; t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = tpair[t];
-    const uint64_t a0 = aoff[p], b0 = boff[p];
-    const uint32_t la = (uint32_t)(aoff[p + 1] - a0), lb = (uint32_t)(boff[p + 1] - b0);
-    const uint32_t d0 = (uint32_t)(t - tstart[p]) * SO_T, d1 = min(d0 + SO_T, la + lb);
+  // (block-uniform loop: the lanes of a wave exchange their diagonals)
+  for (uint64_t tb = blockIdx.x * (uint64_t)blockDim.x; tb < ntiles; tb += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t t = tb + threadIdx.x;
+    const bool ok = t < ntiles;
+    const uint32_t p = ok ? tpair[t] : 0u;
+    const uint64_t a0 = ok ? aoff[p] : 0, b0 = ok ? boff[p] : 0;
+    const uint32_t la = ok ? (uint32_t)(aoff[p + 1] - a0) : 0u, lb = ok ? (uint32_t)(boff[p + 1] - b0) : 0u;
+    const uint32_t d0 = ok ? (uint32_t)(t - tstart[p]) * SO_T : 0u, d1 = min(d0 + SO_T, la + lb);
     auto ga = [&](uint32_t i) { return a[a0 + i]; };
     auto gb = [&](uint32_t j) { return b[b0 + j]; };
-    const uint32_t i0 = d0 == 0 ? 0u : merge_path(ga, la, gb, lb, d0);
-    const uint32_t i1 = d1 == la + lb ? la : merge_path(ga, la, gb, lb, d1);
+    const uint32_t i1 = d1 == la + lb ? la : merge_path4(ga, la, gb, lb, d1);
+    // a tile's start diagonal is the end of the tile before it: the lane before's, when it holds it
+    const uint32_t i1p = (uint32_t)__shfl_up((int)i1, 1, 64), pp = (uint32_t)__shfl_up((int)p, 1, 64);
+    const bool nb = __lane_id() > 0 && pp == p;
+    const uint32_t i0 = d0 == 0 ? 0u : nb ? i1p : merge_path4(ga, la, gb, lb, d0);
+    if (!ok) continue;
     const uint32_t j0 = d0 - i0, j1 = d1 - i1;
     // the order of the neighbours this tile's end separates
     int f = 0, e = 0;
