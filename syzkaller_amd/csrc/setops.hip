@@ -441,7 +441,8 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restric
                                                          const uint32_t* __restrict__ tcnt,
                                                          const uint64_t* __restrict__ tout,
                                                          const uint64_t* __restrict__ ntiles_dev,
-                                                         const uint32_t* __restrict__ gap, uint32_t* out) {
+                                                         const uint32_t* __restrict__ gap, uint32_t* out,
+                                                         uint64_t out_cap) {
   const uint64_t ntiles = *ntiles_dev;
   const uint64_t stride = (uint64_t)gridDim.x * (SO_BLOCK / 64);
   uint64_t tile = (uint64_t)blockIdx.x * (SO_BLOCK / 64) + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -493,7 +494,9 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restric
       __builtin_amdgcn_raw_buffer_store_b32(0u, rz, (lane + r * 64) * 4, 0, 0);
   }
   auto step = [&](uint32_t* Dq, uint32_t& Mq, uint32_t& n, uint64_t& d) {
-    const auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(out + d), 0, n * 4, SO_RSRC_FLAGS);
+    // (launched before the host has checked the total against out_cap: stores past it are dropped)
+    const uint32_t nc = d < out_cap ? (uint32_t)min<uint64_t>(n, out_cap - d) : 0u;
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(out + d), 0, nc * 4, SO_RSRC_FLAGS);
 #pragma unroll
     for (int r = 0; r < SC_VT; r++)  // (wave-uniform: a tile's empty slots issue nothing)
       if (r * 64 < (int)n) __builtin_amdgcn_raw_buffer_store_b32(Dq[r], rd, (lane + r * 64) * 4, 0, 0);
@@ -564,38 +567,59 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
                                                               fl, fl + 1);
     SYZ_LAUNCHED();
   } else {
+    SYZ_HIP(hipMemsetAsync(tcnt, 0, (tbound + 1) * 4, s));  // the scan runs over the bound
     ProfScope ps("setop_merge", s, 4 * (na + nb) + 16 * (uint64_t)npairs);
     k_so_tile<SO_GAP><<<so_grid(tbound), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, tcnt, nullptr, gap, fl,
                                                             fl + 1);
     SYZ_LAUNCHED();
   }
-  uint64_t* hnt = c.pinned.get<uint64_t>(2);
-  SYZ_HIP(hipMemcpyAsync(hnt, tstart + npairs, 8, hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipStreamSynchronize(s));
-  const uint64_t ntiles = *hnt;
-  exclusive_scan_u32(tcnt, tout, ntiles, s);
-  k_so_pairoff<<<grid_for(npairs + 1, 256, 4096), 256, 0, s>>>(tstart, tout, npairs, out_off_dev);
-  SYZ_LAUNCHED();
   int* herr = c.pinned.get<int>(4);
   uint64_t* htot = reinterpret_cast<uint64_t*>(herr + 2);
+  if (twopass) {
+    uint64_t* hnt = c.pinned.get<uint64_t>(2);
+    SYZ_HIP(hipMemcpyAsync(hnt, tstart + npairs, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    const uint64_t ntiles = *hnt;
+    exclusive_scan_u32(tcnt, tout, ntiles, s);
+    k_so_pairoff<<<grid_for(npairs + 1, 256, 4096), 256, 0, s>>>(tstart, tout, npairs, out_off_dev);
+    SYZ_LAUNCHED();
+    SYZ_HIP(hipMemcpyAsync(herr, fl, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipMemcpyAsync(htot, tout + ntiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (herr[1]) fail(SYZGPU_EINVAL, "set operation input is not sorted ascending");
+    if (herr[0])  // a repeated value: the multiset rank path
+      return setop_batch_rank(op, a, aoff, na, b, boff, nb, npairs, out, out_cap, out_off_dev, s);
+    const uint64_t total = *htot;
+    if (total > out_cap) fail(SYZGPU_ECAPACITY, "set operation output capacity too small");
+    if (ntiles) {
+      ProfScope ps("setop_emit", s, 4 * (na + nb) + 4 * total + 8 * (uint64_t)npairs);
+      k_so_tile<SO_EMIT><<<so_grid(ntiles), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, nullptr, tout, out,
+                                                               nullptr, nullptr);
+      SYZ_LAUNCHED();
+    }
+    return total;
+  }
+  // one pass: the scan over the tile bound (the counts past the last tile were zeroed before the
+  // merge), the pair offsets and the compaction (its stores clamped to out_cap) go out without a wait;
+  // one read-back of the flags and the total at the end
+  exclusive_scan_u32(tcnt, tout, tbound, s);
+  k_so_pairoff<<<grid_for(npairs + 1, 256, 4096), 256, 0, s>>>(tstart, tout, npairs, out_off_dev);
+  SYZ_LAUNCHED();
+  {
+    ProfScope ps("setop_compact", s, 0);  // (its bytes, 8 per output, are not known at launch)
+    k_so_compact<<<so_grid((tbound + SO_BLOCK / 64 - 1) / (SO_BLOCK / 64)), SO_BLOCK, 0, s>>>(desc, tcnt, tout,
+                                                                                           tstart + npairs, gap, out,
+                                                                                           out_cap);
+    SYZ_LAUNCHED();
+  }
   SYZ_HIP(hipMemcpyAsync(herr, fl, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
-  SYZ_HIP(hipMemcpyAsync(htot, tout + ntiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  SYZ_HIP(hipMemcpyAsync(htot, tout + tbound, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
   if (herr[1]) fail(SYZGPU_EINVAL, "set operation input is not sorted ascending");
-  if (herr[0])  // a repeated value: the multiset rank path
+  if (herr[0])  // a repeated value: the multiset rank path (rewrites out and the offsets)
     return setop_batch_rank(op, a, aoff, na, b, boff, nb, npairs, out, out_cap, out_off_dev, s);
   const uint64_t total = *htot;
   if (total > out_cap) fail(SYZGPU_ECAPACITY, "set operation output capacity too small");
-  if (ntiles && twopass) {
-    ProfScope ps("setop_emit", s, 4 * (na + nb) + 4 * total + 8 * (uint64_t)npairs);
-    k_so_tile<SO_EMIT><<<so_grid(ntiles), SO_BLOCK, 0, s>>>(op, a, b, desc, tstart + npairs, nullptr, tout, out,
-                                                             nullptr, nullptr);
-    SYZ_LAUNCHED();
-  } else if (ntiles) {
-    ProfScope ps("setop_compact", s, 8 * total + 32 * ntiles);
-    k_so_compact<<<so_grid((ntiles + SO_BLOCK / 64 - 1) / (SO_BLOCK / 64)), SO_BLOCK, 0, s>>>(desc, tcnt, tout, tstart + npairs, gap, out);
-    SYZ_LAUNCHED();
-  }
   return total;
 }
 
