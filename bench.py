@@ -63,6 +63,10 @@ def parse():
     ap.add_argument("--append", type=int, default=10_000,
                     help="also time a NewInput append of this many programs to the store at N=1 (0: off)")
     ap.add_argument("--novelty-cpu-sample", type=int, default=20_000)
+    ap.add_argument("--layout-change", type=int, default=1000,
+                    help="also time minimizeCorpus when every step's corpus has this many more programs than the "
+                         "step before (the manager's NewInputs between minimizes: a new group layout every call; "
+                         "0: off)")
     ap.add_argument("--cooccurrence", type=int, default=1,
                     help="also time the call-ID co-occurrence X^T X on int8 MFMA (SURVEY.md F1/K9) at N=1")
     ap.add_argument("--split-largest", type=int, default=0,
@@ -358,6 +362,12 @@ def main():
         except Exception as e:  # noqa: BLE001
             nov_sh = {"error": "%s: %s" % (type(e).__name__, e)}
 
+    # the same step on a layout that changes every call (rank 0 at N = 1 only; never `value`)
+    lchg = None
+    if world == 1 and not args.emulate and args.layout_change:
+        lchg = layout_change_leg(args, dev, corp, d_pcs, d_off, d_grp, d_len, G, C, uses, d_uses, d_static,
+                                 d_prios, d_run, d_sel, d_hist, d_out, d_goff, d_pres, sptr, ms_step)
+
     out = None
     if rank == 0:
         # roofline of the dominant kernel: algorithmic bytes over its measured time
@@ -423,10 +433,63 @@ def main():
             "cover_analytics": ana,
             "hub_ingest_config5": hubr,
             "manager_cycle": app,
+            "layout_change": lchg,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def layout_change_leg(args, dev, corp, d_pcs, d_off, d_grp, d_len, G, C, uses, d_uses, d_static, d_prios, d_run,
+                      d_sel, d_hist, d_out, d_goff, d_pres, sptr, ms_headline):
+    """Side leg (never `value`): minimizeCorpus + CalculatePriorities + BuildChoiceTable as in the headline
+    step, but every step's corpus is the step before's plus --layout-change fresh programs, as when the
+    manager's NewInputs (manager.go:599-616) land between the Connect-driven minimizes (manager.go:569): the
+    call groups' sizes and PCs differ on every call, so the job's cached plans never match the layout. One
+    corpus of 1M + (warmup + steps) x batch programs is resident; step i minimizes its first 1M + i x batch
+    entries. Reports ms per step beside the headline's."""
+    import torch
+    from syzkaller_amd import cover, synth
+    batch = args.layout_change
+    nsteps = max(1, args.steps)
+    extra_n = batch * (args.warmup + nsteps + 1)
+    ex = synth.corpus(args.seed + 0x51, extra_n, args.ngroups, args.npcs)
+
+    def dt(a):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64, np.dtype(np.uint16): np.int16}
+        return torch.from_numpy(a.view(view.get(a.dtype, a.dtype))).to(dev)
+
+    n0 = corp.n
+    a_pcs = torch.cat([d_pcs[:int(corp.off[-1])], dt(ex.pcs)])
+    a_off = torch.cat([d_off, dt(ex.off[1:] + np.uint64(corp.off[-1]))])
+    a_grp = torch.cat([d_grp, dt(ex.group)])
+    a_len = torch.cat([d_len, dt(ex.prog_len)])
+    sel = torch.zeros(n0 + extra_n, dtype=torch.uint8, device=dev)
+    out_idx = torch.zeros(n0 + extra_n, dtype=torch.int64, device=dev)
+    job = cover.MinimizeJob()
+    k = [0]
+
+    def step():
+        k[0] += 1
+        n = n0 + k[0] * batch
+        job.begin(a_pcs, a_off, a_grp, n, G, a_len, None, None, sptr)
+        job.end_prio(C, d_uses, uses.shape[0], d_static, d_prios, d_run, None, sel, d_hist, out_idx, d_goff,
+                     d_pres, sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(nsteps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / nsteps * 1e3
+    job.close()
+    return {"what": "the headline step on a corpus that grows by %d programs per step (a new call-group layout "
+                    "every call, so the cached plans never match)" % batch,
+            "programs_first_timed": n0 + (args.warmup + 1) * batch, "steps": nsteps,
+            "ms_per_step": round(ms, 4), "headline_ms_per_step": round(ms_headline, 4),
+            "over_headline_ms": round(ms - ms_headline, 4)}
 
 
 def store_leg(args, L, corp, d_pcs, d_off, d_grp, d_len, d_sel, d_hist, C, G, sptr):

@@ -91,7 +91,9 @@ int syzgpu_setop_batch(int op, const uint32_t* a, const uint64_t* a_off, const u
                        uint64_t* out_off);
 /* The same on device-resident CSRs (a_off[0] = b_off[0] = 0; na = a_off[npairs], nb = b_off[npairs]
  * from the caller): out / out_off device arrays, *total (host, may be NULL) = out_off[npairs]. Returns
- * after the stream has drained. The triage users: fuzzer.go:374-375, 389-406. */
+ * after the stream has drained. The triage users: fuzzer.go:374-375, 389-406.
+ * On SYZGPU_ECAPACITY or SYZGPU_EINVAL the contents of out[0, out_cap) are undefined (the compaction is
+ * launched before the total is read back); out_off and *total are then not meaningful either. */
 int syzgpu_setop_batch_dev(int op, const uint32_t* a, const uint64_t* a_off, uint64_t na, const uint32_t* b,
                            const uint64_t* b_off, uint64_t nb, size_t npairs, uint32_t* out, size_t out_cap,
                            uint64_t* out_off, void* stream, uint64_t* total);
@@ -233,7 +235,38 @@ int syzgpu_mz_end_prio_dev(syzgpu_mz* job, int32_t C, const uint8_t* count_hist,
                            size_t nkeys, float* static_prios, float* prios, int64_t* run, uint8_t* row_present,
                            void* stream);
 int syzgpu_mz_fetch(syzgpu_mz* job, int64_t* out_idx, uint64_t* group_out_off);
+/* info[0..cap): entries, groups, PCs, direct windows, hashed windows of the last begin; speculative steps
+ * kept, speculative steps redone (a layout that changed since the call before). */
 int syzgpu_mz_info(syzgpu_mz* job, uint64_t* info, size_t cap);
+
+/* ---- minimizeCorpus over several GPUs of one node, inside the library ------------
+ * One process, one sub-job per entry of devices[] (a device may repeat). The library plans the split
+ * (call groups whole; a group heavier than a sub-job's share split by PC-value ranges, the cost model of
+ * syzkaller_amd/sharding.py plan_parts), uploads each sub-job's covers at load, and on every minimize runs
+ * the sub-jobs on threads of their own: begin on every device, the split groups' selections exchanged
+ * by peer copies (xGMI) and MAX-folded on each device, end, the kept-length histograms summed on
+ * devices[0], which also computes calcStaticPriorities + CalculatePriorities + BuildChoiceTable.
+ * Outputs (host): the kept corpus ids group-major in Go's selection order and group_out_off[ngroups+1]
+ * (as syzgpu_minimize_grouped), len_hist[C+1], and, when prios/run are given, prios[C*C], run[C*C],
+ * row_present[C] (may be NULL). Covers must be canonical (key parts need sorted covers). */
+typedef struct syzgpu_mgz syzgpu_mgz;
+int syzgpu_mgz_create(const int* devices, int ndev, syzgpu_mgz** out);
+int syzgpu_mgz_destroy(syzgpu_mgz* job);
+/* split_largest > 1: the largest group is split into that many parts (rehearsals, tests); 0: the plan */
+int syzgpu_mgz_load(syzgpu_mgz* job, const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
+                    const uint16_t* prog_len, size_t n, uint32_t ngroups, uint32_t split_largest);
+int syzgpu_mgz_minimize_prio(syzgpu_mgz* job, int32_t C, const float* uses, size_t nkeys, int64_t* out_idx,
+                             uint64_t* group_out_off, int64_t* len_hist, float* prios, int64_t* run,
+                             uint8_t* row_present);
+/* info: sub-jobs, groups, entries, split groups, exchange bytes, then each sub-job's entries */
+int syzgpu_mgz_info(syzgpu_mgz* job, uint64_t* info, size_t cap);
+/* The plan alone (host only, no device needed): ranks_out[g * nranks + j] = the sub-job holding part j of
+ * group g (-1 past its parts); cost_out[nranks] (may be NULL) = the modelled step per sub-job, us. */
+int syzgpu_plan_parts(const int64_t* entries, const double* pcs, uint32_t ngroups, int nranks, uint32_t split_largest,
+                      int32_t* ranks_out, double* cost_out);
+/* The PC bounds of group g's k parts (host only): bounds_out[k + 1], 0 .. 2^32 */
+int syzgpu_plan_split_bounds(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n, uint32_t g,
+                             uint32_t k, uint64_t* bounds_out);
 
 /* Dynamic prio from a length histogram, normalize, multiply by static, and the ChoiceTable:
  * prog/prio.go:29-38, 137-192, 202-228 fused. enabled may be NULL. */

@@ -62,6 +62,13 @@ SIGNATURES = {
                                           _vp]),
     "syzgpu_mz_fetch": (_c.c_int, [_vp, _vp, _vp]),
     "syzgpu_mz_info": (_c.c_int, [_vp, _vp, _sz]),
+    "syzgpu_mgz_create": (_c.c_int, [_vp, _c.c_int, _vp]),
+    "syzgpu_mgz_destroy": (_c.c_int, [_vp]),
+    "syzgpu_mgz_load": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _sz, _c.c_uint32, _c.c_uint32]),
+    "syzgpu_mgz_minimize_prio": (_c.c_int, [_vp, _c.c_int32, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "syzgpu_mgz_info": (_c.c_int, [_vp, _vp, _sz]),
+    "syzgpu_plan_parts": (_c.c_int, [_vp, _vp, _c.c_uint32, _c.c_int, _c.c_uint32, _vp, _vp]),
+    "syzgpu_plan_split_bounds": (_c.c_int, [_vp, _vp, _vp, _sz, _c.c_uint32, _c.c_uint32, _vp]),
     "syzgpu_prio_choice_dev": (_c.c_int, [_vp, _vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_minimize_grouped_fetch": (_c.c_int, [_vp, _vp, _sz, _c.c_uint32]),
     "syzgpu_corpus_create": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp]),

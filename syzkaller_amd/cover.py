@@ -112,6 +112,87 @@ def MinimizeCorpusDev(d_pcs, d_off, d_group, n, ngroups, d_prog_len=None, C=0, d
                                                     ptr(d_group_out_off), stream))
 
 
+class MultiMinimizeJob:
+    """minimizeCorpus over several GPUs of one node inside the library (syzgpu_mgz_*): the library plans
+    the split (call groups whole, the heaviest split by PC ranges), uploads each device's share at load,
+    and runs every sub-job on a thread of its own with the exchange (peer copies + MAX) and the
+    histogram sum inside. devices may repeat (two sub-jobs on device 0 exercise the exchange on one GPU)."""
+
+    def __init__(self, devices):
+        d = np.ascontiguousarray(devices, np.int32)
+        h = np.zeros(1, np.uint64)
+        check(lib().syzgpu_mgz_create(ptr(d), d.size, ptr(h)))
+        self._h = int(h[0])
+        self.ngroups = 0
+        self.n = 0
+
+    def load(self, pcs, off, group, prog_len, ngroups, split_largest=0):
+        pcs = np.ascontiguousarray(pcs, np.uint32)
+        off = np.ascontiguousarray(off, np.uint64)
+        group = np.ascontiguousarray(group, np.uint32)
+        prog_len = np.ascontiguousarray(prog_len, np.uint16)
+        self.n = off.size - 1
+        self.ngroups = ngroups
+        check(lib().syzgpu_mgz_load(self._h, ptr(pcs), ptr(off), ptr(group), ptr(prog_len), self.n, ngroups,
+                                    split_largest))
+
+    def minimize_prio(self, C, uses=None):
+        """(kept ids group-major, group offsets, len_hist, prios, run, row_present); prios/run/row_present
+        are None without a usage matrix."""
+        out = np.zeros(max(self.n, 1), np.int64)
+        goff = np.zeros(self.ngroups + 1, np.uint64)
+        hist = np.zeros(C + 1, np.int64)
+        prios = run = rowp = None
+        nkeys = 0
+        if uses is not None:
+            uses = np.ascontiguousarray(uses, np.float32)
+            nkeys = uses.shape[0]
+            prios = np.zeros((C, C), np.float32)
+            run = np.zeros((C, C), np.int64)
+            rowp = np.zeros(C, np.uint8)
+        check(lib().syzgpu_mgz_minimize_prio(self._h, C, ptr(uses), nkeys, ptr(out), ptr(goff), ptr(hist),
+                                             ptr(prios), ptr(run), ptr(rowp)))
+        return out[:int(goff[-1])].copy(), goff, hist, prios, run, rowp
+
+    def info(self):
+        v = np.zeros(5 + 64, np.uint64)
+        check(lib().syzgpu_mgz_info(self._h, ptr(v), v.size))
+        nd = int(v[0])
+        return {"subjobs": nd, "groups": int(v[1]), "entries": int(v[2]), "split_groups": int(v[3]),
+                "exchange_bytes": int(v[4]), "subjob_entries": [int(x) for x in v[5:5 + nd]]}
+
+    def close(self):
+        if self._h:
+            lib().syzgpu_mgz_destroy(self._h)
+            self._h = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def plan_parts(entries, pcs, nranks, split_largest=0):
+    """The library's key-space plan (host only, no device): (ranks per group, modelled cost per rank)."""
+    e = np.ascontiguousarray(entries, np.int64)
+    p = np.ascontiguousarray(pcs, np.float64)
+    ranks = np.full((e.size, nranks), -1, np.int32)
+    cost = np.zeros(nranks, np.float64)
+    check(lib().syzgpu_plan_parts(ptr(e), ptr(p), e.size, nranks, split_largest, ptr(ranks), ptr(cost)))
+    return [tuple(int(x) for x in row if x >= 0) for row in ranks], cost
+
+
+def plan_split_bounds(pcs, off, group, g, k):
+    """The library's PC bounds of group g's k parts (host only)."""
+    pcs = np.ascontiguousarray(pcs, np.uint32)
+    off = np.ascontiguousarray(off, np.uint64)
+    group = np.ascontiguousarray(group, np.uint32)
+    b = np.zeros(k + 1, np.uint64)
+    check(lib().syzgpu_plan_split_bounds(ptr(pcs), ptr(off), ptr(group), off.size - 1, g, k, ptr(b)))
+    return b
+
+
 class MinimizeJob:
     """minimizeCorpus as a job on device-resident covers (syzgpu_mz_*): begin, an optional exchange of
     split groups' selections, end. key_lo/key_hi (per group, numpy u32) restrict this rank to a PC
@@ -162,9 +243,10 @@ class MinimizeJob:
         return out[: int(goff[-1])].copy(), goff
 
     def info(self):
-        v = np.zeros(5, np.uint64)
-        check(lib().syzgpu_mz_info(self._h, ptr(v), 5))
-        return dict(zip(["entries", "groups", "pcs", "direct_windows", "hash_windows"], (int(x) for x in v)))
+        v = np.zeros(7, np.uint64)
+        check(lib().syzgpu_mz_info(self._h, ptr(v), 7))
+        return dict(zip(["entries", "groups", "pcs", "direct_windows", "hash_windows", "spec_hits", "spec_misses"],
+                        (int(x) for x in v)))
 
     def close(self):
         if self._h:

@@ -98,6 +98,8 @@ struct Context {
   Scratch scratch;
   Pinned pinned;
   Pinned pinned_err;  // the raw Minimize's P flags (panels.hip launch_step)
+  Pinned pinned_plan;          // the Go sort's plan staging (gosort_plan)
+  hipEvent_t ev_plan = nullptr;  // its copies are done
   // the last minimize of this lane (for syzgpu_minimize_grouped_fetch): which thread ran it, on
   // which job; fetch on another thread or after the lane served someone else reports EINVAL
   std::thread::id last_thread;
@@ -124,7 +126,9 @@ struct Context {
   std::vector<uint64_t> raw_plan_key;
 };
 
-// The lane held by the calling thread (inside SYZ_API_BODY); lazily init(0); throws ENODEV.
+// The lane held by the calling thread (inside SYZ_API_BODY); lazily init(0); throws ENODEV. Lanes belong
+// to one device each: the process's device by default, another one for the sub-jobs of a multi-device
+// job (multi.hip), each run on a thread of its own holding a lane of its device.
 Context& ctx();
 // The lane's side stream and its fork / join events, created on first use.
 inline void ensure_side(Context& c) {
@@ -135,7 +139,7 @@ inline void ensure_side(Context& c) {
 }
 // RAII: hold a lane for the calling thread (nested API calls reuse it).
 struct LaneGuard {
-  LaneGuard();
+  explicit LaneGuard(int device = -1);  // -1: the process's device (syzgpu_init); else a lane of that device
   ~LaneGuard();
   LaneGuard(const LaneGuard&) = delete;
   LaneGuard& operator=(const LaneGuard&) = delete;
@@ -176,6 +180,28 @@ struct ProfScope {
   ~ProfScope() { end(); }
 };
 
+// Developer switches (A/B variants that lost, timing-only debug modes, some of which give wrong results):
+// read from the environment only in the variant and dbg builds (-DSYZ_DEV_KNOBS, Makefile `variant` /
+// `dbg`). The production library always takes the default, so a manager that inherits one of these
+// variables gets the shipped behaviour. The runtime options the production library reads are listed in
+// INTEGRATION.md ("Environment"); none of them changes a result.
+inline const char* dev_env(const char* name) {
+#ifdef SYZ_DEV_KNOBS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
+// The process's device fault word: host-mapped, so a kernel that detects an internal failure it has no
+// other way to report (scan.hpp's look-back timeout or 2^56 overflow) sets a bit that the host reads
+// without a device wait. Every entry point checks it on return (SYZ_API_BODY); once set, calls fail
+// with SYZGPU_EINTERNAL (sticky, like a device error).
+constexpr uint32_t FAULT_SCAN_WAIT = 1, FAULT_SCAN_RANGE = 2;
+uint32_t* fault_word_dev();  // its device address (allocated on first use)
+void check_faults();         // fail(SYZGPU_EINTERNAL) when a bit is set
+
 // ---- device-wide scans (scan.hpp, runtime.hip) ----------------------------------------------------------
 // out[i] = sum(in[0..i)), out[n] = total. in may be uint8_t / uint32_t / uint64_t.
 void exclusive_scan_u8(const uint8_t* in, uint64_t* out, size_t n, hipStream_t s);
@@ -188,7 +214,7 @@ struct PhaseTimer {
   bool on;
   const char* what;
   std::chrono::steady_clock::time_point t;
-  explicit PhaseTimer(const char* w) : on(getenv("SYZGPU_PHASE_TIMING") != nullptr), what(w), t(std::chrono::steady_clock::now()) {}
+  explicit PhaseTimer(const char* w) : on(dev_env("SYZGPU_PHASE_TIMING") != nullptr), what(w), t(std::chrono::steady_clock::now()) {}
   void mark(const char* name, hipStream_t s) {
     if (!on) return;
     (void)hipStreamSynchronize(s);
@@ -202,7 +228,7 @@ struct HostTimer {
   bool on;
   const char* what;
   std::chrono::steady_clock::time_point t;
-  explicit HostTimer(const char* w) : on(getenv("SYZGPU_HOST_TIMING") != nullptr), what(w), t(std::chrono::steady_clock::now()) {}
+  explicit HostTimer(const char* w) : on(dev_env("SYZGPU_HOST_TIMING") != nullptr), what(w), t(std::chrono::steady_clock::now()) {}
   void mark(const char* name) {
     if (!on) return;
     const auto n = std::chrono::steady_clock::now();
@@ -419,6 +445,7 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
     ::syz::Context& C_ = ::syz::ctx();                                                           \
     (void)C_;                                                                                    \
     __VA_ARGS__;                                                                                 \
+    ::syz::check_faults();                                                                       \
     return SYZGPU_OK;                                                                            \
   } catch (const ::syz::Error& e) {                                                              \
     ::syz::set_last_error(e.msg);                                                                \

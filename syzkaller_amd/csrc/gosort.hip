@@ -23,6 +23,7 @@
 // Elements are (len << 32) | position in HBM and (len << SH) | local index in LDS (u32 when every
 // length of the pack fits, otherwise a u64 instantiation); Less only compares the length field.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -67,7 +68,7 @@ __constant__ uint32_t g_t_child = T_SEG;
 static uint32_t t_child_host() {
   static const uint32_t v = [] {
     uint32_t x = GS_T_CHILD_DEFAULT;
-    if (const char* e = getenv("SYZGPU_GS_T_CHILD")) x = (uint32_t)atoi(e);
+    if (const char* e = dev_env("SYZGPU_GS_T_CHILD")) x = (uint32_t)atoi(e);
     if (x < 64) x = 64;
     if (x > T_SEG) x = T_SEG;
     SYZ_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_t_child), &x, sizeof(x)));
@@ -1441,11 +1442,13 @@ template <int SH, class E>
 static void launch_ls(const uint64_t* el, uint32_t* perm, const Pack* packs, uint32_t npacks_host,
                       const uint32_t* npacks_dev, unsigned grid, const Seg* segs, uint32_t* bounce_cnt, Pack* bounce,
                       hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<bool> attr[64];  // per device
+  int dev = 0;
+  SYZ_HIP(hipGetDevice(&dev));
+  if (!attr[dev & 63].load()) {
     SYZ_HIP(hipFuncSetAttribute((const void*)k_ls_sort<SH, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sizeof(LsLds<E>)));
-    attr = true;
+    attr[dev & 63] = true;
   }
   if (grid == 0) return;
   k_ls_sort<SH, E><<<grid, LS_BLOCK, sizeof(LsLds<E>), s>>>(el, perm, packs, npacks_host, npacks_dev, segs,
@@ -1462,15 +1465,10 @@ GosortPlan::~GosortPlan() {
 }
 
 void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ngroups, hipStream_t s) {
-  // a plan may be re-made for a new layout (the incremental corpus index): the old arrays go first
-  // (their last users ran on s), the learned round count stays as a hint
-  if (P.small || P.packs || P.big) SYZ_HIP(hipStreamSynchronize(s));
-  if (P.small) (void)hipFree(P.small);
-  if (P.packs) (void)hipFree(P.packs);
-  if (P.big) (void)hipFree(P.big);
-  P.small = nullptr;
-  P.packs = nullptr;
-  P.big = nullptr;
+  // a plan may be re-made for a new layout (a corpus that grew since the last minimize, the incremental
+  // corpus index): its device arrays are grow-only (a hipFree would wait for the whole device, the
+  // transpose included), overwritten on s after their last users there; the learned round count stays
+  // as a hint
   P.big_max = 0;
   std::vector<Seg> big, small;
   std::vector<Pack> packs;
@@ -1523,16 +1521,31 @@ void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ng
     P.big_total += sg.hi - sg.lo;
     P.big_max = std::max<uint64_t>(P.big_max, sg.hi - sg.lo);
   }
-  SYZ_HIP(hipMalloc(&P.small, (small.size() + 1) * sizeof(Seg)));
-  SYZ_HIP(hipMalloc(&P.packs, (packs.size() + 1) * sizeof(Pack)));
-  SYZ_HIP(hipMalloc(&P.big, (big.size() + 1) * sizeof(Seg)));
-  // on the caller's stream, never the legacy one: another thread's graph capture may be running
-  if (!small.empty())
-    SYZ_HIP(hipMemcpyAsync(P.small, small.data(), small.size() * sizeof(Seg), hipMemcpyHostToDevice, s));
-  if (!packs.empty())
-    SYZ_HIP(hipMemcpyAsync(P.packs, packs.data(), packs.size() * sizeof(Pack), hipMemcpyHostToDevice, s));
-  if (!big.empty()) SYZ_HIP(hipMemcpyAsync(P.big, big.data(), big.size() * sizeof(Seg), hipMemcpyHostToDevice, s));
-  SYZ_HIP(hipStreamSynchronize(s));  // the host vectors are temporaries
+  auto grow = [](auto*& p, size_t& cap, size_t need) {
+    if (p && cap >= need) return;
+    if (p) SYZ_HIP(hipFree(p));
+    p = nullptr;
+    cap = need + need / 4 + 16;
+    SYZ_HIP(hipMalloc(&p, cap * sizeof(*p)));
+  };
+  grow(P.small, P.cap_small, small.size() + 1);
+  grow(P.packs, P.cap_packs, packs.size() + 1);
+  grow(P.big, P.cap_big, big.size() + 1);
+  // on the caller's stream, never the legacy one: another thread's graph capture may be running; from
+  // the lane's plan staging (pinned), so the host goes on without waiting for the copies: the staging is
+  // rewritten only once the previous plan's copies are done (ev_plan)
+  Context& c = ctx();
+  if (!c.ev_plan) SYZ_HIP(hipEventCreateWithFlags(&c.ev_plan, hipEventDisableTiming));
+  else SYZ_HIP(hipEventSynchronize(c.ev_plan));
+  const size_t bs = small.size() * sizeof(Seg), bp = packs.size() * sizeof(Pack), bb = big.size() * sizeof(Seg);
+  uint8_t* h = c.pinned_plan.get<uint8_t>(bs + bp + bb + 16);
+  std::memcpy(h, small.data(), bs);
+  std::memcpy(h + bs, packs.data(), bp);
+  std::memcpy(h + bs + bp, big.data(), bb);
+  if (bs) SYZ_HIP(hipMemcpyAsync(P.small, h, bs, hipMemcpyHostToDevice, s));
+  if (bp) SYZ_HIP(hipMemcpyAsync(P.packs, h + bs, bp, hipMemcpyHostToDevice, s));
+  if (bb) SYZ_HIP(hipMemcpyAsync(P.big, h + bs + bp, bb, hipMemcpyHostToDevice, s));
+  SYZ_HIP(hipEventRecord(c.ev_plan, s));
 }
 
 void gosort_groups(uint64_t* el, uint32_t* perm, size_t n, const std::vector<uint64_t>& hstart, uint32_t ngroups,
@@ -1579,7 +1592,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   // (the big groups' rounds on a stream of the greatest priority measured no faster beside the
   // transpose: r04_t1, 2.988 vs 2.983 ms)
   ensure_side(c);
-  const bool fork = P.npacks && P.nbig && !getenv("SYZGPU_GS_NOFORK");
+  const bool fork = P.npacks && P.nbig && !dev_env("SYZGPU_GS_NOFORK");
   hipStream_t ss = fork ? c.side : s;  // the small groups' stream
   hipStream_t bs = s;                  // the big groups'
   if (fork) {
@@ -1637,7 +1650,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     // 0.74 ms at 64-256 workgroups vs 0.45 ms as graphs): a barrier's per-workgroup L2 write-back and
     // invalidate costs more than the launch gap it replaces.
     const char* pe = getenv("SYZGPU_GR_PERSIST");
-    const bool wt = !getenv("SYZGPU_GR_FENCE");  // A/B switch: write-through swaps vs release fence
+    const bool wt = !dev_env("SYZGPU_GR_FENCE");  // A/B switch: write-through swaps vs release fence
     if (pe && !strcmp(pe, "1")) {
       if (!c.gr_resident) {  // workgroups the device holds at once: the persistent grid never exceeds it
         int per_cu = 0, cus = 0;
@@ -1659,7 +1672,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
       else
         k_gr_persist<false><<<pgrid, GL_BLOCK, 0, bs>>>(el, lvl[0], lvl[1], tcnt, A, B, VA, VB, ctl, dlds, heap, bar, MAXR);
       SYZ_LAUNCHED();
-      if (getenv("SYZGPU_GS_DEBUG")) {
+      if (dev_env("SYZGPU_GS_DEBUG")) {
         GCtl h;
         SYZ_HIP(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, bs));
         SYZ_HIP(hipStreamSynchronize(bs));
@@ -1754,7 +1767,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
         __builtin_ia32_pause();
       }
       P.rounds_hint = last_rounds;
-      if (getenv("SYZGPU_GS_DEBUG")) {
+      if (dev_env("SYZGPU_GS_DEBUG")) {
         SYZ_HIP(hipStreamSynchronize(bs));
         fprintf(stderr, "gosort: %u rounds issued, %u with segments\n", issued, last_rounds);
       }

@@ -27,7 +27,7 @@ namespace syz {
 // placement more waves (measured at config 4: 1024 -> 256 entries takes it from 0.23 to 0.17 ms), as
 // long as the G x chunks counter table stays small (<= 8M counters); SYZGPU_GRP_PW overrides (A/B)
 static uint32_t grp_pw(size_t n, uint32_t G) {
-  const char* e = getenv("SYZGPU_GRP_PW");
+  const char* e = dev_env("SYZGPU_GRP_PW");
   if (e && *e) return (uint32_t)std::min(8192, std::max(64, atoi(e))) / 64 * 64;
   uint32_t pw = 256;
   while (pw < 8192 && (uint64_t)G * ((n + pw - 1) / pw) > (1ull << 23)) pw *= 2;
@@ -1231,7 +1231,7 @@ void corpus_minimize_begin(Corpus& K, hipStream_t s) {
   const GosortPlan& P = K.gsplan;
   // the small class runs beside the big class's latency-bound global rounds: it is held to part of
   // the chip (its workgroups fill a CU's LDS), so the rounds keep CUs to run on
-  static const unsigned side_cus = getenv("SYZGPU_SIDE_CUS") ? (unsigned)atoi(getenv("SYZGPU_SIDE_CUS")) : 128u;
+  static const unsigned side_cus = dev_env("SYZGPU_SIDE_CUS") ? (unsigned)atoi(dev_env("SYZGPU_SIDE_CUS")) : 128u;
   auto vec_min = [&](hipStream_t q, size_t first, size_t count, bool side) {
     if (!count) return;
     const unsigned grid = (unsigned)std::min<size_t>(count, side ? side_cus : (1u << 20));

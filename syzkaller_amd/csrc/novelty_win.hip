@@ -576,7 +576,7 @@ __global__ void k_nw_isnew(const uint32_t* cmem, const uint8_t* sel8, size_t nm,
 
 // timing experiments only (results are wrong when set): SYZGPU_NW_DBG 1 = tables not walked, 2 = no emit
 static int nw_dbg() {
-  static const int v = getenv("SYZGPU_NW_DBG") ? atoi(getenv("SYZGPU_NW_DBG")) : 0;
+  static const int v = dev_env("SYZGPU_NW_DBG") ? atoi(dev_env("SYZGPU_NW_DBG")) : 0;
   return v;
 }
 
@@ -584,7 +584,7 @@ static int nw_dbg() {
 // without table updates, 2 = tables built, nothing after, 4 = no new-cover marks, 8 = no ordered
 // output
 static int nwh_dbg() {
-  static const int v = getenv("SYZGPU_NWH_DBG") ? atoi(getenv("SYZGPU_NWH_DBG")) : 0;
+  static const int v = dev_env("SYZGPU_NWH_DBG") ? atoi(dev_env("SYZGPU_NWH_DBG")) : 0;
   // SYZGPU_NWH_SORT=1 (read per call; results unchanged): every sub-range ordered by the sort
   const char* so = getenv("SYZGPU_NWH_SORT");
   return v | (so && atoi(so) ? 16 : 0);
@@ -599,12 +599,12 @@ static int nwh_dbg() {
 constexpr uint64_t NW_HSPARSE = 1024;
 static uint64_t nw_hsparse() {
   static const uint64_t v =
-      getenv("SYZGPU_NW_HSPARSE") ? (uint64_t)atoll(getenv("SYZGPU_NW_HSPARSE")) : NW_HSPARSE;
+      dev_env("SYZGPU_NW_HSPARSE") ? (uint64_t)atoll(dev_env("SYZGPU_NW_HSPARSE")) : NW_HSPARSE;
   return v;
 }
 
 static uint32_t nw_bits_forced() {
-  static const uint32_t v = getenv("SYZGPU_NW_BITS") ? (uint32_t)atoi(getenv("SYZGPU_NW_BITS")) : 0u;
+  static const uint32_t v = dev_env("SYZGPU_NW_BITS") ? (uint32_t)atoi(dev_env("SYZGPU_NW_BITS")) : 0u;
   return v == 14 || v == 15 ? v : 0u;
 }
 

@@ -35,7 +35,7 @@ namespace syz {
 // workgroups of k_span_sums: each adds its G per-group sums to gpcs with global atomics, G x blocks
 // of them on G addresses; SYZGPU_SPAN_BLOCKS overrides (A/B)
 static unsigned span_blocks() {
-  const char* e = getenv("SYZGPU_SPAN_BLOCKS");
+  const char* e = dev_env("SYZGPU_SPAN_BLOCKS");
   return e && *e ? (unsigned)std::max(1, atoi(e)) : 512u;
 }
 
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_minmax(const uint32_t* pcs, size_t L, u
   block_span_update<256>(lo, hi, span);
 }
 
-// the job's per-step state: error word, per-group PC sums, the PC span
+// the job's per-step state: error word, speculation gate (err[2]), per-group PC sums, the PC span
 __global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span, uint32_t* mlmax) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x) {
     gpcs[g] = 0;
@@ -91,6 +91,7 @@ __global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span, 
       err[g] = 0;
       span[g] = g ? 0u : 0xFFFFFFFFu;
     }
+    if (g == 0) err[2] = 0;  // the speculation gate (k_gpack)
     if (g == 0) *mlmax = 0;
   }
 }
@@ -98,8 +99,13 @@ __global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span, 
 // What the host plans the windows from, in one buffer (one copy back): gstart[G + 1], the PCs of each
 // call group gpcs[G], the span, the error word, and the PCs of each call group this job reads (its
 // members' slices: the exact byte model of the kernels) gsl[G]
+// exp (a step speculated on a cached plan): the words the plan was made from, in the same places
+// (the per-group PC sums at [G + 1, 2G] are not part of the plan's key; exp[2G + 2] = 0, exp[3G + 3] =
+// may_bounce); any difference sets *gate, and the speculated P and M kernels then return at once (a
+// stale plan's M could read D rows past their length), so a miss costs the Go sort's rounds, not a step.
 __global__ void k_gpack(const uint64_t* gstart, const uint64_t* gpcs, const uint32_t* span, const int* err,
-                        const uint64_t* mpos, uint32_t G, const uint32_t* mlmax, uint64_t* out) {
+                        const uint64_t* mpos, uint32_t G, const uint32_t* mlmax, uint64_t* out,
+                        const uint64_t* exp, int* gate) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * G + 4; i += gridDim.x * blockDim.x) {
     uint64_t v;
     if (i == 3 * G + 3)
@@ -117,6 +123,11 @@ __global__ void k_gpack(const uint64_t* gstart, const uint64_t* gpcs, const uint
       v = mpos[gstart[g + 1]] - mpos[gstart[g]];
     }
     out[i] = v;
+    if (exp && (i <= G || i > 2 * G)) {
+      const uint64_t want = exp[i];
+      const uint64_t got = i == 3 * G + 3 ? (uint64_t)(v >= GS_U32_LEN_LIMIT) : v;
+      if (got != want) atomicOr(gate, 1);
+    }
   }
 }
 
@@ -317,7 +328,9 @@ __global__ __launch_bounds__(1024) SYZ_SMIN_OCC void k_smin_direct(const PItem* 
                                                                    const uint32_t* D, const PSlab* slabs,
                                                                    const uint32_t* __restrict__ elems,
                                                                    const uint32_t* __restrict__ rank_of_member,
-                                                                   const uint64_t* gstart, uint32_t* selbits) {
+                                                                   const uint64_t* gstart, uint32_t* selbits,
+                                                                   const int* gate) {
+  if (*gate) return;  // a speculated step on a plan that does not fit this layout (k_gpack)
   __shared__ SminLds L;
   smin_direct(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, L);
 }
@@ -328,7 +341,8 @@ template <bool PACKED>
 __global__ __launch_bounds__(PACKED ? PK_BLOCK : 1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_smin_hash(
     const PItem* items, const SGroup* sg, const uint32_t* gslab, const uint64_t* gebase, const uint32_t* D,
     const PSlab* slabs, const uint32_t* __restrict__ elems, const uint32_t* __restrict__ rank_of_member,
-    const uint64_t* gstart, uint32_t* selbits) {
+    const uint64_t* gstart, uint32_t* selbits, const int* gate) {
+  if (*gate) return;  // (see k_smin_direct)
   if constexpr (PACKED) {
     __shared__ SminPkLds L;
     smin_hash<true, PK_BLOCK>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits,
@@ -429,6 +443,17 @@ void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, u
 
 static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span);
 
+// the key parts (host arguments) of this call are those the cached plan was made for
+static bool spec_parts_match(const MinJob& J, const RawMinArgs& a) {
+  const std::vector<uint64_t>& k = J.pcache->key;
+  const size_t G = a.G, tail = (size_t)2 * G + 3;  // hstart (G + 1), hsl (G), span, may_bounce
+  if (!a.key_lo) return k.size() == tail;
+  if (k.size() != tail + G) return false;
+  for (size_t g = 0; g < G; g++)
+    if (k[tail + g] != (((uint64_t)a.key_lo[g] << 32) | a.key_hi[g])) return false;
+  return true;
+}
+
 static bool pm_serial() {
   static const bool v = getenv("SYZGPU_PM_SERIAL") && atoi(getenv("SYZGPU_PM_SERIAL")) != 0;
   return v || (prof().on && prof().serial);
@@ -440,7 +465,7 @@ static bool pm_serial() {
 // beside the big groups' slabs (measured slower: the big groups' LDS sort then waits for CUs behind
 // both, r04_q3 3.04 vs 2.96 ms)
 static bool pm_psplit() {
-  static const bool v = getenv("SYZGPU_PM_PSPLIT") && atoi(getenv("SYZGPU_PM_PSPLIT")) != 0;
+  static const bool v = dev_env("SYZGPU_PM_PSPLIT") && atoi(dev_env("SYZGPU_PM_PSPLIT")) != 0;
   return v;
 }
 
@@ -554,7 +579,7 @@ static hipStream_t launch_p(const RawMinArgs& a, const SlabPlanCache& PC, SlabJo
     ProfScope ps("k_slab", pq, bytes);
     launch_slab<false>(SJ.slab_bound, SJ.wmax, pq, a.pcs, a.off, members, mlen, SJ.tpos, sbeg, SJ.slabs,
                        SJ.cstart + SJ.B, SJ.dsg, SJ.gebase, PC.lo, SJ.elems, SJ.ecap, SJ.D, err, nullptr, NovSrc{},
-                       cls);
+                       cls, err + 2);
     SYZ_LAUNCHED();
     if (cls == 1) SYZ_HIP(hipEventRecord(c.ev_psmall, pq));
   }
@@ -579,7 +604,7 @@ static std::vector<uint64_t> plan_key(const RawMinArgs& a, const std::vector<uin
 
 static void plan_layout(MinJob& J, const RawMinArgs& a, const std::vector<uint64_t>& hstart,
                         const std::vector<uint64_t>& hpcs, const uint64_t* hsl_in, const std::vector<PGroup>& hpg,
-                        uint32_t lo, uint32_t hi) {
+                        uint32_t lo, uint32_t hi, uint64_t span_raw) {
   Context& c = ctx();
   const size_t n = a.n;
   const uint32_t G = a.G;
@@ -589,8 +614,13 @@ static void plan_layout(MinJob& J, const RawMinArgs& a, const std::vector<uint64
   const uint64_t* hsl = hslv.data();
   const auto is_big = [&](uint32_t g) { return hstart[g + 1] - hstart[g] > GS_T_SEG; };
   std::vector<uint64_t> key = plan_key(a, hstart, hsl, lo, hi, J.may_bounce);
+  J.spec_ok = J.pcache && J.pcache->key == key;  // the layout repeated: the next call may speculate
   if (!J.pcache || J.pcache->key != key) {
     auto P = std::make_shared<SlabPlanCache>();
+    if (J.pcache) {  // the device staging of the last plan is reused (grow-only): no hipMalloc / hipFree
+      std::swap(P->dstage.p, J.pcache->dstage.p);
+      std::swap(P->dstage.cap, J.pcache->dstage.cap);
+    }
     P->key = std::move(key);
     SlabJob& SJ = P->SJ;
     slab_plan(SJ, hstart, hsl, hpg, G, false);
@@ -627,7 +657,8 @@ static void plan_layout(MinJob& J, const RawMinArgs& a, const std::vector<uint64
     P->o_gb = al16((G + 1) * sizeof(SGroup));
     P->o_bg = P->o_gb + al16((G + 1) * 4);
     P->o_it = P->o_bg + al16(((size_t)B + 1) * 4);
-    const size_t stage_bytes = P->o_it + al16((nitems + 1) * sizeof(PItem));
+    P->o_exp = P->o_it + al16((nitems + 1) * sizeof(PItem));
+    const size_t stage_bytes = P->o_exp + al16((3 * (size_t)G + 4) * 8);
     uint8_t* stage = c.pinned.get<uint8_t>(stage_bytes + 64);
     P->dstage.ensure(stage_bytes + 64);
     for (uint32_t g = 0; g < G; g++) SJ.hsg[g].pad = is_big(g) ? 1u : 0u;
@@ -640,6 +671,13 @@ static void plan_layout(MinJob& J, const RawMinArgs& a, const std::vector<uint64
       size_t& k = at[is_big(g) ? 1 : 0][hpg[g].mode];
       for (uint32_t w = iw0[g]; w < iw1[g]; w++) hit[k++] = PItem{g, w};
     }
+    // the words a step speculated on this plan must read back (k_gpack's gate)
+    uint64_t* ex = reinterpret_cast<uint64_t*>(stage + P->o_exp);
+    std::memset(ex, 0, (3 * (size_t)G + 4) * 8);
+    for (uint32_t g = 0; g <= G; g++) ex[g] = hstart[g];
+    ex[2 * G + 1] = span_raw;
+    for (uint32_t g = 0; g < G; g++) ex[2 * G + 3 + g] = hsl[g];
+    ex[3 * G + 3] = J.may_bounce ? 1 : 0;
     SYZ_HIP(hipMemcpyAsync(P->dstage.p, stage, stage_bytes, hipMemcpyHostToDevice, s));
     SJ.dsg = reinterpret_cast<SGroup*>(P->dstage.p);
     SJ.dgblock = reinterpret_cast<uint32_t*>(P->dstage.p + P->o_gb);
@@ -679,8 +717,16 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
   const SGroup* dsg = SJ.dsg;
   const PItem* ditems = reinterpret_cast<const PItem*>(dstage + PC.o_it);
   (void)G;
+  // the Go sort's plan of a new layout first, while the device is idle (re-planned in place: grow-only
+  // device arrays, the learned round count kept)
+  if (!J.plan || J.plan_key != hstart) {
+    if (!J.plan) J.plan = std::make_shared<GosortPlan>();
+    gosort_plan(*J.plan, hstart, G, s);
+    J.plan_key = hstart;
+  }
   hipStream_t pq = launch_p(a, PC, SJ, members, mlen, mpos, gstart, sbeg, err);
   ht.mark("slab_build");
+  const int* gate = err + 2;
   const PSlab* slabs = SJ.slabs;
   const uint32_t* gslab = SJ.gslab;
   const uint64_t* gebase = SJ.gebase;
@@ -694,7 +740,7 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
     c.ev_sct.push_back(e2);
   }
   int* herr = c.pinned_err.get<int>(4);  // (not the lane's pinned buffer: the read-back may still be read)
-  SYZ_HIP(hipMemcpyAsync(herr, err, 8, hipMemcpyDeviceToHost, pq));
+  SYZ_HIP(hipMemcpyAsync(herr, err, 12, hipMemcpyDeviceToHost, pq));  // P's flags, the partition's, the gate
   SYZ_HIP(hipEventRecord(c.ev_cnt[0], pq));
   SYZ_HIP(hipEventRecord(c.ev_sct[0], pq));
   SYZ_HIP(hipEventRecord(c.ev_part1, pq));
@@ -709,27 +755,22 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
     if (nd) {
       ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
       k_smin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], dsg, gslab, gebase, D, slabs,
-                                                   elems, rank_of_member, gstart, selbits);
+                                                   elems, rank_of_member, gstart, selbits, gate);
       SYZ_LAUNCHED();
     }
     if (nh) {
       ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
       k_smin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[big][PMODE_HASH], dsg, gslab, gebase, D, slabs,
-                                                        elems, rank_of_member, gstart, selbits);
+                                                        elems, rank_of_member, gstart, selbits, gate);
       SYZ_LAUNCHED();
     }
     if (np) {  // (on a stream of their own beside the others: slower, the process has 4 hardware queues)
       ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
       k_smin_hash<true><<<(unsigned)np, PK_BLOCK, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
-                                                       elems, rank_of_member, gstart, selbits);
+                                                       elems, rank_of_member, gstart, selbits, gate);
       SYZ_LAUNCHED();
     }
   };
-  if (!J.plan || J.plan_key != hstart) {
-    J.plan = std::make_shared<GosortPlan>();
-    gosort_plan(*J.plan, hstart, G, s);
-    J.plan_key = hstart;
-  }
   GosortPlan& P = *J.plan;
   P.may_bounce = J.may_bounce;
   auto small_done = [&](hipStream_t q) {
@@ -764,6 +805,8 @@ static bool finish_step(MinJob& J, const uint32_t* exact_span) {
   J.stats_items_hash = PC.icount[0][PMODE_HASH] + PC.icount[1][PMODE_HASH] + PC.icount[0][PMODE_PACKED] +
                        PC.icount[1][PMODE_PACKED];
   if (herr[0] & 64) fail(SYZGPU_EINTERNAL, "minimize: slab plan does not fit the layout");
+  // a kept step whose gate closed would have skipped P and M: the host's and the device's key checks agree
+  if (herr[2]) fail(SYZGPU_EINTERNAL, "minimize: speculation gate closed on a kept step");
   if (herr[0] & 1) {
     if (exact_span) fail(SYZGPU_EINTERNAL, "minimize: PC outside the exact span");
     return false;
@@ -824,12 +867,20 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   uint64_t* el = sc.get<uint64_t>("mz_el", n + 1);
   uint64_t* gpcs = sc.get<uint64_t>("mz_gpcs", G + 1);
   uint32_t* span = sc.get<uint32_t>("pm_span", 4);
-  int* err = sc.get<int>("mz_err", 2);
+  int* err = sc.get<int>("mz_err", 4);  // [0] P's flags, [1] the partition's, [2] the speculation gate
   uint32_t* mlen = sc.get<uint32_t>("pm_mlen", n + 1);
   uint32_t* sbeg = a.key_lo ? sc.get<uint32_t>("pm_sbeg", n + 1) : nullptr;
   uint64_t* mpos = sc.get<uint64_t>("pm_mpos", n + 1);
   uint64_t* gpack = sc.get<uint64_t>("pm_gpack", 3 * (size_t)G + 4);
   uint32_t* mlmax = sc.get<uint32_t>("pm_mlmax", 1);
+  // Only while layouts repeat: after a miss (a corpus that changed since the last call, e.g. NewInputs
+  // between the manager's minimizes) the job plans on the read-back layout until a step finds its plan
+  // cached again, so a layout that changes on every call pays one miss, not one per call.
+  const bool spec = J.spec_ok && !J.nospec && J.pcache && J.plan && !exact_span && pm_spec() && J.pcache->n == n &&
+                    J.pcache->SJ.G == G && J.hstart == J.plan_key && J.plan_key.size() == (size_t)G + 1 &&
+                    spec_parts_match(J, a);
+  J.nospec = false;
+  const uint64_t* exp = spec ? reinterpret_cast<const uint64_t*>(J.pcache->dstage.p + J.pcache->o_exp) : nullptr;
   k_pm_init<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(err, gpcs, G, span, mlmax);
   SYZ_LAUNCHED();
   uint32_t* krange = nullptr;
@@ -875,7 +926,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
     uint64_t* tpos = sc.get<uint64_t>("pm_sl_tpos", n + 2);
     scan_f<2>(LenTilesFn{mlen}, n, mpos, tpos, s, "pm_mt");
     if (n) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
-    k_gpack<<<grid_for(3 * (size_t)G + 4, 256, 64), 256, 0, s>>>(gstart, gpcs, span, err, mpos, G, mlmax, gpack);
+    k_gpack<<<grid_for(3 * (size_t)G + 4, 256, 64), 256, 0, s>>>(gstart, gpcs, span, err, mpos, G, mlmax, gpack, exp,
+                                                                 err + 2);
     SYZ_LAUNCHED();
   }
   uint64_t* hbuf = c.pinned.get<uint64_t>(3 * (size_t)G + 8);
@@ -887,9 +939,6 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   // leave the device's critical path. It is kept when the layout read back is the one planned (the
   // group starts and plan_key); otherwise it is waited for and the step redone without. P's guards
   // keep a stale plan's slabs inside their buffers (err 64). SYZGPU_PM_SPEC=0: no speculation.
-  const bool spec = !J.nospec && J.pcache && J.plan && !exact_span && pm_spec() && J.pcache->n == n &&
-                    J.pcache->SJ.G == G && J.hstart == J.plan_key && J.plan_key.size() == (size_t)G + 1;
-  J.nospec = false;
   if (spec) launch_step(J, a, members, el, mlen, mpos, sbeg, err);
   HostTimer ht("begin");
   event_wait_spin(c.ev_spin);
@@ -909,9 +958,12 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   if (spec) {
     if (!bad_group && hstart == J.plan_key && plan_key(a, hstart, hsl, lo, hi, may_bounce) == J.pcache->key) {
       ht.mark("spec_kept");
+      J.spec_hits++;
       return finish_step(J, exact_span);
     }
     SYZ_HIP(hipEventSynchronize(J.done));  // the speculative step is done with every buffer
+    J.spec_ok = false;
+    J.spec_misses++;
     if (!bad_group) {
       J.nospec = true;
       return begin_once(J, a, exact_span);  // the partition again, then planned as below
@@ -925,7 +977,7 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
   std::vector<PGroup> hpg;
   plan_windows(spanw, hpcs.data(), hstart.data(), G, hpg);
   ht.mark("plan_windows");
-  plan_layout(J, a, hstart, hpcs, hsl, hpg, lo, hi);
+  plan_layout(J, a, hstart, hpcs, hsl, hpg, lo, hi, hbuf[2 * G + 1]);
   ht.mark("plan_layout");
   launch_step(J, a, members, el, mlen, mpos, sbeg, err);
   return finish_step(J, exact_span);
@@ -1210,8 +1262,9 @@ int syzgpu_mz_info(syzgpu_mz* job, uint64_t* info, size_t cap) {
     if (!job || !info) fail(SYZGPU_EINVAL, "null pointer");
     MinJob& J = *reinterpret_cast<MinJob*>(job);
     std::lock_guard<std::recursive_mutex> hl_(J.mu);
-    const uint64_t v[5] = {J.n, J.G, J.stats_total_pcs, J.stats_items_direct, J.stats_items_hash};
-    for (size_t i = 0; i < cap && i < 5; i++) info[i] = v[i];
+    const uint64_t v[7] = {J.n, J.G, J.stats_total_pcs, J.stats_items_direct, J.stats_items_hash, J.spec_hits,
+                           J.spec_misses};
+    for (size_t i = 0; i < cap && i < 7; i++) info[i] = v[i];
   })
 }
 

@@ -106,11 +106,11 @@ struct SlabPlanCache {
   size_t icount[2][3] = {{0, 0, 0}, {0, 0, 0}};
   std::array<std::array<size_t, 3>, 2> ifirst{};
   uint64_t item_pcs[2][3] = {{0, 0, 0}, {0, 0, 0}};
-  size_t o_gb = 0, o_bg = 0, o_it = 0;
+  size_t o_gb = 0, o_bg = 0, o_it = 0, o_exp = 0;  // staging offsets (o_exp: k_gpack's expected words)
   uint64_t cpcs[2] = {0, 0}, cent[2] = {0, 0};  // PCs / entries of the small and big call groups
   uint32_t lo = 0, hi = 0;
   size_t n = 0;
-  Grow<uint8_t> dstage;  // SGroup[G], gblock[G + 1], bgroup[B + 1], items
+  Grow<uint8_t> dstage;  // SGroup[G], gblock[G + 1], bgroup[B + 1], items, expected words
 };
 
 struct MinJob {
@@ -130,6 +130,8 @@ struct MinJob {
   std::shared_ptr<GosortPlan> plan;  // Go-sort plan of the last layout (keeps its rounds hint)
   std::shared_ptr<SlabPlanCache> pcache;  // plan_layout's plan of the last layout
   bool nospec = false;                    // begin_once: this call redoes a speculation that missed
+  bool spec_ok = false;                   // the last planned layout was the cached one: speculate next call
+  uint64_t spec_hits = 0, spec_misses = 0;
   std::vector<uint64_t> plan_key;
   uint64_t stats_total_pcs = 0;
   size_t stats_items_direct = 0, stats_items_hash = 0;

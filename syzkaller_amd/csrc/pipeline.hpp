@@ -26,6 +26,7 @@ struct GosortPlan {
   Seg* small = nullptr;
   Pack* packs = nullptr;
   Seg* big = nullptr;
+  size_t cap_small = 0, cap_packs = 0, cap_big = 0;  // (grow-only across re-plans)
   GosortPlan() = default;
   GosortPlan(const GosortPlan&) = delete;
   GosortPlan& operator=(const GosortPlan&) = delete;

@@ -220,7 +220,7 @@ void prio_choice_dev(const float* static_prios, const int64_t* len_hist, const f
     return;
   }
   // SYZGPU_PRIO_SUFFIX=1: the suffix sums as their own launch (A/B reference)
-  static const bool sep = getenv("SYZGPU_PRIO_SUFFIX") != nullptr;
+  static const bool sep = dev_env("SYZGPU_PRIO_SUFFIX") != nullptr;
   float* Hf = nullptr;
   if (sep) {
     Hf = ctx().scratch.get<float>("pr_H", C + 1);

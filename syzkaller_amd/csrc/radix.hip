@@ -170,7 +170,7 @@ static void radix_sort_pairs_t(KT*& keys, uint32_t*& vals, KT*& ktmp, uint32_t*&
   unsigned long long* h_bits = ctx().pinned.get<unsigned long long>(2);
   SYZ_HIP(hipMemcpyAsync(h_bits, d_bits, 16, hipMemcpyDeviceToHost, s));
   SYZ_HIP(hipStreamSynchronize(s));
-  const unsigned long long differ = getenv("SYZGPU_RS_ALL_PASSES") ? ~0ull : (h_bits[0] ^ h_bits[1]);
+  const unsigned long long differ = dev_env("SYZGPU_RS_ALL_PASSES") ? ~0ull : (h_bits[0] ^ h_bits[1]);
   for (int shift = 0; shift < end_bit; shift += RADIX_BITS) {
     if (!((differ >> shift) & (RS_RADIX - 1))) continue;
     k_rs_hist<KT><<<(unsigned)ntiles, RS_BLOCK, 0, s>>>(keys, n, shift, (uint32_t)ntiles, counts);

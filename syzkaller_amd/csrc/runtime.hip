@@ -69,7 +69,7 @@ static thread_local int t_depth = 0;
 static thread_local Context* t_last = nullptr;   // affinity: the lane this thread used last
 static thread_local uint64_t t_last_gen = 0;
 
-static size_t max_lanes() {
+static size_t max_lanes() {  // per device
   static const size_t v = [] {
     const char* e = getenv("SYZGPU_LANES");
     const long x = e ? atol(e) : 8;
@@ -78,7 +78,11 @@ static size_t max_lanes() {
   return v;
 }
 
-static void pick_device(int dev) {  // g_mu held
+static std::vector<int> g_checked;  // devices found to be gfx950 (g_mu held)
+
+static void check_device(int dev) {  // g_mu held
+  for (int d : g_checked)
+    if (d == dev) return;
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n <= 0) fail(SYZGPU_ENODEV, "no HIP device available");
@@ -87,13 +91,19 @@ static void pick_device(int dev) {  // g_mu held
   SYZ_HIP(hipGetDeviceProperties(&prop, dev));
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     fail(SYZGPU_ENODEV, std::string("libsyzgpu is built for gfx950 only, found ") + prop.gcnArchName);
+  g_checked.push_back(dev);
+}
+
+static void pick_device(int dev) {  // g_mu held
+  check_device(dev);
   g_device = dev;
 }
 
-static Context* new_lane() {  // g_mu held
-  SYZ_HIP(hipSetDevice(g_device));
+static Context* new_lane(int dev) {  // g_mu held
+  check_device(dev);
+  SYZ_HIP(hipSetDevice(dev));
   std::unique_ptr<Context> c(new Context());
-  c->device = g_device;
+  c->device = dev;
   c->gen = g_gen;
   SYZ_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   g_lanes.push_back(c.get());
@@ -101,23 +111,33 @@ static Context* new_lane() {  // g_mu held
   return c.release();
 }
 
-LaneGuard::LaneGuard() {
-  if (t_depth++ > 0) return;
+LaneGuard::LaneGuard(int device) {
+  if (t_depth++ > 0) {
+    if (device >= 0 && t_lane && t_lane->device != device) {
+      t_depth--;
+      fail(SYZGPU_EINTERNAL, "nested call on another device");
+    }
+    return;
+  }
   std::unique_lock<std::mutex> lk(g_mu);
   try {
-    if (g_device < 0) pick_device(0);
+    if (g_device < 0) pick_device(device >= 0 ? device : 0);
+    const int dev = device >= 0 ? device : g_device;
     for (;;) {
-      size_t pick = g_lanes.size();
+      size_t pick = g_lanes.size(), mine = 0;
       for (size_t i = 0; i < g_lanes.size(); i++)
-        if (!g_busy[i] && g_lanes[i] == t_last && t_last_gen == g_gen) pick = i;
+        if (g_lanes[i]->device == dev) {
+          mine++;
+          if (!g_busy[i] && g_lanes[i] == t_last && t_last_gen == g_gen) pick = i;
+        }
       if (pick == g_lanes.size())
         for (size_t i = 0; i < g_lanes.size(); i++)
-          if (!g_busy[i]) {
+          if (!g_busy[i] && g_lanes[i]->device == dev) {
             pick = i;
             break;
           }
-      if (pick == g_lanes.size() && g_lanes.size() < max_lanes()) {
-        new_lane();
+      if (pick == g_lanes.size() && mine < max_lanes()) {
+        new_lane(dev);
         pick = g_lanes.size() - 1;
       }
       if (pick < g_lanes.size()) {
@@ -142,7 +162,7 @@ LaneGuard::~LaneGuard() {
   for (size_t i = 0; i < g_lanes.size(); i++)
     if (g_lanes[i] == t_lane) g_busy[i] = false;
   t_lane = nullptr;
-  g_cv.notify_one();
+  g_cv.notify_all();  // (waiters may want lanes of different devices)
 }
 
 Context& ctx() {
@@ -159,7 +179,7 @@ static void free_lane(Context* c) {
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->part) (void)hipStreamDestroy(c->part);
   if (c->cap) (void)hipStreamDestroy(c->cap);
-  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_part0, c->ev_part1, c->ev_psmall, c->ev_spin})
+  for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_part0, c->ev_part1, c->ev_psmall, c->ev_spin, c->ev_plan})
     if (e) (void)hipEventDestroy(e);
   for (auto& row : c->gl_exec)
     for (auto& g : row)
@@ -201,6 +221,33 @@ void Prof::end(size_t rec, hipStream_t s) {
   SYZ_HIP(hipEventRecord(recs[rec].b, s));
 }
 
+// ---- the device fault word (common.hpp) -----------------------------------------------------------------
+static std::mutex g_fault_mu;
+static uint32_t* g_fault_host = nullptr;
+static uint32_t* g_fault_dev = nullptr;
+
+uint32_t* fault_word_dev() {
+  std::lock_guard<std::mutex> lk(g_fault_mu);
+  if (!g_fault_dev) {
+    void* h = nullptr;
+    SYZ_HIP(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+    std::memset(h, 0, 64);
+    void* d = nullptr;
+    SYZ_HIP(hipHostGetDevicePointer(&d, h, 0));
+    g_fault_host = static_cast<uint32_t*>(h);
+    g_fault_dev = static_cast<uint32_t*>(d);
+  }
+  return g_fault_dev;
+}
+
+void check_faults() {
+  const uint32_t* h = g_fault_host;
+  if (!h) return;
+  const uint32_t f = __atomic_load_n(h, __ATOMIC_RELAXED);
+  if (f & FAULT_SCAN_WAIT) fail(SYZGPU_EINTERNAL, "device scan: a look-back never completed (results void)");
+  if (f & FAULT_SCAN_RANGE) fail(SYZGPU_EINTERNAL, "device scan: a prefix reached 2^56 (results void)");
+}
+
 // ---- device-wide exclusive scans (scan.hpp) ------------------------------------------------------------
 __global__ void k_scan_zero(uint64_t* out0, uint64_t* out1) {
   out0[0] = 0;
@@ -223,7 +270,7 @@ ScanState scan_state(const char* tag, size_t tiles, int nv, hipStream_t s) {
     ep = {buf, {words, 0u}};
   }
   ep.second.second++;
-  return ScanState{buf + 32, reinterpret_cast<uint32_t*>(buf), ep.second.second};
+  return ScanState{buf + 32, reinterpret_cast<uint32_t*>(buf), ep.second.second, fault_word_dev()};
 }
 
 uint64_t* scan_scratch(const char* tag, int depth, size_t words) {
@@ -251,14 +298,20 @@ void stream_wait_spin(hipStream_t s) {
   event_wait_spin(c.ev_spin);
 }
 
+// Spins for 200 us (the step's short read-backs come back within it), then polls with the thread
+// yielding its core to the manager's other threads for up to 5 ms, then blocks.
 void event_wait_spin(hipEvent_t e) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t r = hipEventQuery(e);
     if (r == hipSuccess) return;
     if (r != hipErrorNotReady) SYZ_HIP(r);
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
-    __builtin_ia32_pause();
+    const auto dt = std::chrono::steady_clock::now() - t0;
+    if (dt > std::chrono::milliseconds(5)) break;
+    if (dt > std::chrono::microseconds(200))
+      std::this_thread::yield();
+    else
+      __builtin_ia32_pause();
   }
   SYZ_HIP(hipEventSynchronize(e));
 }
@@ -327,7 +380,7 @@ int syzgpu_profile_enable(int on) {
 }
 
 int syzgpu_debug_fail_grow(int k) {
-  syz::grow_fail_countdown() = k > 0 ? k : 0;
+  syz::grow_fail_countdown().store(k > 0 ? k : 0);
   return SYZGPU_OK;
 }
 

@@ -8,7 +8,12 @@
 // writes back / invalidates the L2: measured 75 us for a 276-tile scan). The epoch lets the words go
 // uncleared for 63 scans; the tile that takes the last ticket resets the counter. One launch per scan:
 // the reduce / scan-of-sums / apply form took three or four, ~6 us each at the step's small sizes.
-// Values: sums below 2^56.
+// Values: sums below 2^56 (a tile whose inclusive prefix reaches 2^56 sets the fault word, below).
+// A look-back that waits 2^24 polls for a predecessor that never publishes (a bug: every predecessor
+// holds a ticket taken before, so it is resident or done) stops waiting and sets the fault word too; the
+// process's entry points then fail with SYZGPU_EINTERNAL (check_faults) rather than return its output.
+// scan_f must not be captured into a HIP graph: each launch takes the next epoch on the host, which a
+// replayed capture would reuse.
 #pragma once
 #include "common.hpp"
 
@@ -28,7 +33,8 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t x) {
 struct ScanState {
   uint64_t* words;
   uint32_t* ticket;
-  uint32_t epoch;  // 1..63
+  uint32_t epoch;   // 1..63
+  uint32_t* fault;  // the process's fault word (host-mapped, fault_word_dev)
 };
 ScanState scan_state(const char* tag, size_t tiles, int nv, hipStream_t s);  // runtime.hip
 constexpr uint64_t SCAN_VMASK = (1ull << 56) - 1;
@@ -77,7 +83,10 @@ __device__ __forceinline__ void scan_lookback(const ScanState& st, uint32_t t, c
       if ((__ballot(ready) & need) != need) {
         // (a predecessor that never publishes is a bug: left, not waited for forever; the output is
         // then wrong and the parity tests say so)
-        if (++spins == (1u << 24)) break;
+        if (++spins == (1u << 24)) {
+          if (lane == 0) __hip_atomic_fetch_or(st.fault, FAULT_SCAN_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
@@ -90,7 +99,10 @@ __device__ __forceinline__ void scan_lookback(const ScanState& st, uint32_t t, c
   if (lane == 0) {
     uint64_t inc[NV];
 #pragma unroll
-    for (int q = 0; q < NV; q++) inc[q] = excl[q] + tot[q];
+    for (int q = 0; q < NV; q++) {
+      inc[q] = excl[q] + tot[q];
+      if (inc[q] > SCAN_VMASK) __hip_atomic_fetch_or(st.fault, FAULT_SCAN_RANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     put(f_inc, inc);
   }
 }

@@ -519,7 +519,7 @@ __global__ __launch_bounds__(SO_BLOCK) void k_so_compact(const SoDesc* __restric
 
 // workgroups of a tile walk: enough to fill the CUs several times over (env SYZGPU_SO_GRID for A/B)
 static unsigned so_grid(uint64_t tiles) {
-  static const unsigned cap = getenv("SYZGPU_SO_GRID") ? (unsigned)atoi(getenv("SYZGPU_SO_GRID")) : 16384u;
+  static const unsigned cap = dev_env("SYZGPU_SO_GRID") ? (unsigned)atoi(dev_env("SYZGPU_SO_GRID")) : 16384u;
   return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, cap));
 }
 
@@ -539,7 +539,7 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
                          const uint64_t* boff, uint64_t nb, uint32_t npairs, uint32_t* out, uint64_t out_cap,
                          uint64_t* out_off_dev, hipStream_t s) {
   Context& c = ctx();
-  if (getenv("SYZGPU_SETOP_RANK") && atoi(getenv("SYZGPU_SETOP_RANK")))
+  if (dev_env("SYZGPU_SETOP_RANK") && atoi(dev_env("SYZGPU_SETOP_RANK")))
     return setop_batch_rank(op, a, aoff, na, b, boff, nb, npairs, out, out_cap, out_off_dev, s);
   const uint64_t tbound = npairs + (na + nb) / SO_T + 1;
   uint32_t* ntile = c.scratch.get<uint32_t>("so_ntile", npairs + 1);
@@ -559,7 +559,7 @@ uint64_t setop_batch_dev(int op, const uint32_t* a, const uint64_t* aoff, uint64
   SYZ_LAUNCHED();
   // one merge pass into a gapped image + a compaction (default), or count + scan + a second merge
   // (SYZGPU_SO_TWOPASS=1, for A/B: the merge is VALU-bound, so running it once is what pays)
-  static const bool twopass = getenv("SYZGPU_SO_TWOPASS") && atoi(getenv("SYZGPU_SO_TWOPASS"));
+  static const bool twopass = dev_env("SYZGPU_SO_TWOPASS") && atoi(dev_env("SYZGPU_SO_TWOPASS"));
   uint32_t* gap = twopass ? nullptr : c.scratch.get<uint32_t>("so_gap", na + nb + 1);
   if (twopass) {
     ProfScope ps("setop_count", s, 4 * (na + nb) + 16 * (uint64_t)npairs);

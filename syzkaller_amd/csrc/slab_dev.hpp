@@ -172,7 +172,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const uint32_t* __restrict__ mlen, const uint64_t* __restrict__ tpos, const uint32_t* __restrict__ sbeg,
     const PSlab* __restrict__ slabs, const uint64_t* nslab, const SGroup* __restrict__ sg,
     const uint64_t* __restrict__ gebase, uint32_t lo, uint32_t* __restrict__ elems, uint32_t* __restrict__ D,
-    int* err, uint32_t Wmax, uint64_t ecap, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int cls = 0) {
+    int* err, uint32_t Wmax, uint64_t ecap, uint32_t* wtot = nullptr, NovSrc ns = NovSrc{}, int cls = 0,
+    const int* gate = nullptr) {
   constexpr int WAVES = BLOCK / 64;
   static_assert((uint32_t)TPW * WAVES == SL_TILES, "slab tiles");
   extern __shared__ __align__(16) uint32_t slds[];
@@ -187,6 +188,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   uint32_t* mhi = obuf + 3 * SL_MEMB;
   uint32_t* mln = obuf + 4 * SL_MEMB;
   uint8_t* mtab = reinterpret_cast<uint8_t*>(obuf + 5 * SL_MEMB);  // NOV: member i is a table
+  // a step speculated on a plan that does not fit the layout read back (panels.hip k_gpack)
+  if (gate && *gate) return;
   const uint64_t nsl = *nslab;
   const uint64_t c = blockIdx.x;
   if (c >= nsl) return;
@@ -385,20 +388,24 @@ inline void launch_slab(uint64_t nslabs, uint32_t Wmax, hipStream_t s, const uin
                         const uint32_t* members, const uint32_t* mlen, const uint64_t* tpos, const uint32_t* sbeg,
                         const PSlab* slabs, const uint64_t* nslab, const SGroup* sg, const uint64_t* gebase,
                         uint32_t lo, uint32_t* elems, uint64_t ecap, uint32_t* D, int* err, uint32_t* wtot,
-                        NovSrc ns, int cls) {
+                        NovSrc ns, int cls, const int* gate = nullptr) {
   if (!nslabs) return;
   const size_t bytes = slab_lds_bytes(Wmax);
-  static std::atomic<size_t> raised{0};
-  if (bytes > raised.load()) {
+  // (per device: the attribute is a property of the device's copy of the kernel)
+  static std::atomic<size_t> raised[64];
+  int dev = 0;
+  SYZ_HIP(hipGetDevice(&dev));
+  std::atomic<size_t>& rd = raised[dev & 63];
+  if (bytes > rd.load()) {
     SYZ_HIP(hipFuncSetAttribute((const void*)k_slab<SL_BLOCK, SL_TPW, NOV>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-    size_t cur = raised.load();
-    while (bytes > cur && !raised.compare_exchange_weak(cur, bytes)) {
+    size_t cur = rd.load();
+    while (bytes > cur && !rd.compare_exchange_weak(cur, bytes)) {
     }
   }
   k_slab<SL_BLOCK, SL_TPW, NOV><<<(unsigned)nslabs, SL_BLOCK, bytes, s>>>(pcs, off, members, mlen, tpos, sbeg, slabs,
                                                                          nslab, sg, gebase, lo, elems, D, err, Wmax,
-                                                                         ecap, wtot, ns, cls);
+                                                                         ecap, wtot, ns, cls, gate);
   SYZ_LAUNCHED();
 }
 

@@ -1,6 +1,7 @@
 // The resident corpus store (the device analog of syz-manager's mgr.corpus, manager.go:52-65),
 // shared by Minimize (minimize.hip) and the manager's cover analytics (analytics.hip).
 #pragma once
+#include <atomic>
 #include <map>
 #include <vector>
 
@@ -181,14 +182,20 @@ void corpus_upload_work(Corpus& K, hipStream_t s);
 
 // Device buffer that keeps its first `used` elements when it grows (appends); 1.5x headroom.
 // test hook (syzgpu_debug_fail_grow): the k-th growth from now fails as an allocation failure would
-inline int& grow_fail_countdown() {
-  static int k = 0;
+// (atomic: lanes on other threads grow their buffers at the same time)
+inline std::atomic<int>& grow_fail_countdown() {
+  static std::atomic<int> k{0};
   return k;
 }
 template <class T>
 void grow_keep(Grow<T>& g, size_t used, size_t need, hipStream_t s) {
   if (need <= g.cap && g.p) return;
-  if (int& k = grow_fail_countdown(); k > 0 && --k == 0) fail(SYZGPU_ENOMEM, "forced growth failure (test hook)");
+  if (std::atomic<int>& k = grow_fail_countdown(); k.load(std::memory_order_relaxed) > 0) {
+    int cur = k.load(std::memory_order_relaxed);
+    while (cur > 0 && !k.compare_exchange_weak(cur, cur - 1)) {
+    }
+    if (cur == 1) fail(SYZGPU_ENOMEM, "forced growth failure (test hook)");
+  }
   const size_t want = need + need / 2 + 16;
   T* p = nullptr;
   SYZ_HIP(hipMalloc(&p, want * sizeof(T)));

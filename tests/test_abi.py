@@ -65,3 +65,34 @@ def test_synth_is_deterministic_and_canonical():
         c = a.cover(i)
         assert c.size >= 1 and np.all(c[1:] > c[:-1])
     assert a.prog_len.min() >= 1 and a.prog_len.max() <= 40
+
+
+# The runtime options the production library reads (INTEGRATION.md "Environment"): each selects a
+# strategy or a schedule and none changes a result (the -m gpu tests run the alternatives against the
+# oracle). Developer switches (timing-only modes, A/B variants) are read only in the variant / dbg
+# builds (dev_env, syzkaller_amd/csrc/common.hpp).
+RUNTIME_OPTIONS = {
+    "SYZGPU_LANES", "SYZGPU_NOVELTY", "SYZGPU_NO_INC_INDEX", "SYZGPU_NWH_SORT", "SYZGPU_PM_SERIAL",
+    "SYZGPU_PM_SPEC", "SYZGPU_CHUNK_VECS", "SYZGPU_CO_FORM", "SYZGPU_CO_KS", "SYZGPU_GR_PERSIST",
+    "SYZGPU_GR_PGRID",
+}
+
+
+def test_production_library_reads_only_documented_options():
+    data = open(os.path.join(ROOT, "syzkaller_amd", "libsyzgpu.so"), "rb").read()
+    names = set(m.decode() for m in re.findall(rb"SYZGPU_[A-Z0-9_]+", data))
+    assert names <= RUNTIME_OPTIONS, sorted(names - RUNTIME_OPTIONS)
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert all(n in doc for n in RUNTIME_OPTIONS), [n for n in RUNTIME_OPTIONS if n not in doc]
+    # the wrong-result timing switches in particular
+    for n in ("SYZGPU_NW_DBG", "SYZGPU_NWH_DBG", "SYZGPU_PM_PSPLIT", "SYZGPU_SO_TWOPASS"):
+        assert n.encode() not in data, n
+
+
+def test_every_getenv_in_sources_is_documented_or_dev_only():
+    src = os.path.join(ROOT, "syzkaller_amd", "csrc")
+    seen = set()
+    for f in os.listdir(src):
+        text = open(os.path.join(src, f), errors="ignore").read()
+        seen |= set(re.findall(r'\bgetenv\("(SYZGPU_[A-Z0-9_]+)"\)', text))
+    assert seen <= RUNTIME_OPTIONS, sorted(seen - RUNTIME_OPTIONS)

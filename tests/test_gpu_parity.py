@@ -373,6 +373,51 @@ def test_minimize_speculative_plan_reuse():
         assert np.array_equal(want[name][0], got), name
 
 
+def test_minimize_speculation_miss_after_miss():
+    # the job speculates only once its layout repeated (panels.hip begin_once): a layout that changes on
+    # every call pays at most one miss (a miss after a miss cannot happen), a corpus that grows between
+    # calls (NewInputs between minimizes, manager.go:599-616) never speculates, and every call's result
+    # matches the oracle through misses, re-plans and hits
+    import torch
+    a = synth.corpus(0x5EED0013, 20_000, 289, 100_000)
+    b = synth.corpus(0x5EED0014, 20_000, 289, 100_000)
+    g = synth.corpus(0x5EED0015, 22_000, 289, 100_000)
+    dev = torch.device("cuda", 0)
+
+    def t(x):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64, np.dtype(np.uint16): np.int16}
+        return torch.from_numpy(x.view(view.get(x.dtype, x.dtype))).to(dev)
+
+    src = {k: (c, [t(c.pcs), t(c.off), t(c.group), t(c.prog_len)]) for k, c in (("a", a), ("b", b), ("g", g))}
+    job = cover.MinimizeJob()
+    s = torch.cuda.current_stream().cuda_stream
+    want = {}
+    seq = [("a", 20_000)] * 3 + [("b", 20_000)] * 3 + [("a", 20_000), ("b", 20_000), ("a", 20_000),
+                                                      ("b", 20_000)] \
+        + [("g", n) for n in (20_000, 20_500, 21_000, 21_500, 22_000)] + [("g", 22_000)] * 2
+    hist = []
+    for name, n in seq:
+        c, d = src[name]
+        if (name, n) not in want:
+            want[name, n] = oracle.minimize_grouped(c.pcs[:int(c.off[n])], c.off[:n + 1], c.group[:n], c.ngroups)
+        job.begin(d[0], d[1], d[2], n, c.ngroups, d[3], stream=s)
+        got, goff = job.fetch(n, c.ngroups)
+        assert np.array_equal(want[name, n][1], goff), (name, n)
+        assert np.array_equal(want[name, n][0], got), (name, n)
+        inf = job.info()
+        hist.append((inf["spec_hits"], inf["spec_misses"]))
+    hits = [h for h, _ in hist]
+    misses = [m for _, m in hist]
+    assert hits[2] == 1 and misses[2] == 0   # the third call on one layout kept its speculation
+    assert misses[3] == 1                    # another layout of the same size: one miss
+    assert hits[5] == 2 and misses[5] == 1   # ... then planned, then speculated again once it repeated
+    assert misses[6] == 2                    # back to a: a miss
+    assert misses[9] == 2 and hits[9] == 2   # alternating after a miss: planned steps, no miss after a miss
+    assert misses[14] == 2 and hits[14] == 2  # a growing corpus: never speculated
+    assert hits[-1] == 3                     # the grown corpus repeated: speculating again
+    job.close()
+
+
 def test_minimize_corpus_property_full_size():
     # size-independent property at the bench scale: per group, union(kept) == union(all)
     c = synth.corpus(0x5EED0004, 300_000, 289, 2_000_000)
