@@ -46,10 +46,7 @@ __device__ unsigned long long g_gs_stats[24];
 #endif
 
 constexpr uint32_t T_SEG = GS_T_SEG;  // largest segment sorted in LDS
-#ifndef SYZ_GS_PACK_DIV
-#define SYZ_GS_PACK_DIV 1024
-#endif
-constexpr uint64_t GS_PACK_DIV = SYZ_GS_PACK_DIV;  // pack size cap: n / GS_PACK_DIV elements (gosort_plan)
+// (GS_PACK_DIV, the pack size cap n / GS_PACK_DIV, and the packs themselves: plan_host.cpp gosort_segments)
 #ifndef GS_T_CHILD_DEFAULT
 #define GS_T_CHILD_DEFAULT T_SEG
 #endif
@@ -355,19 +352,12 @@ __device__ void seq_terminal(P d, uint32_t lo, uint32_t hi, int32_t depth) {
   }
 }
 
-__host__ __device__ inline int32_t go_max_depth(uint64_t n) {
-  int32_t depth = 0;
-  for (uint64_t i = n; i > 0; i >>= 1) depth++;
-  return depth * 2;
-}
+// (go_max_depth: plan_host.hpp)
 
 // =====================================================================================================
 // LDS level-synchronous sorter: one workgroup per pack.
 // =====================================================================================================
-struct Pack {
-  uint32_t plo, phi;    // element range in el[] (whole segments)
-  uint32_t sbeg, send;  // its segments in the segment array
-};
+// (Pack: plan_host.hpp)
 
 // LDS view of the pack's elements with one pad word per chunk: a thread's contiguous LS_ITEMS-element
 // chunk then starts on its own bank, so chunk walks are conflict-free (a plain array is 8-way).
@@ -1472,46 +1462,7 @@ void gosort_plan(GosortPlan& P, const std::vector<uint64_t>& hstart, uint32_t ng
   P.big_max = 0;
   std::vector<Seg> big, small;
   std::vector<Pack> packs;
-  // Packs of consecutive small call groups: at most T_SEG elements (the LDS sorter's capacity), and at
-  // most n / GS_PACK_DIV so that a small corpus still spreads over many workgroups (config 1's 10k
-  // entries in one T_SEG pack: one workgroup, 184 us). The packs and the big groups tile [0, n): the
-  // entries of one-entry groups between them belong to a pack's range (or to a pack of no segments),
-  // so the pack ranks pass gives them their rank (their position) too.
-  const uint64_t n_all = hstart[ngroups];
-  const uint64_t pack_cap = std::min<uint64_t>(T_SEG, std::max<uint64_t>(64, n_all / GS_PACK_DIV));
-  uint64_t cov = 0;  // [0, cov) is covered by a pack or a big group
-  auto cover_to = [&](uint64_t x) {  // one-entry groups' entries [cov, x)
-    if (cov >= x) return;
-    if (!packs.empty() && packs.back().phi == cov && x - packs.back().plo <= T_SEG) {
-      packs.back().phi = (uint32_t)x;
-    } else {
-      for (; cov < x; cov = std::min<uint64_t>(x, cov + T_SEG))
-        packs.push_back(Pack{(uint32_t)cov, (uint32_t)std::min<uint64_t>(x, cov + T_SEG), (uint32_t)small.size(),
-                             (uint32_t)small.size()});
-    }
-    cov = x;
-  };
-  for (uint32_t g = 0; g < ngroups; g++) {
-    const uint32_t lo = (uint32_t)hstart[g], hi = (uint32_t)hstart[g + 1];
-    if (hi - lo <= 1) continue;
-    const Seg sg{lo, hi, go_max_depth(hi - lo), 0};
-    if (hi - lo > T_SEG) {
-      cover_to(lo);
-      big.push_back(sg);
-      cov = hi;
-      continue;
-    }
-    if (!packs.empty() && packs.back().phi == cov && hi - packs.back().plo <= pack_cap) {
-      packs.back().phi = hi;
-      packs.back().send++;
-    } else {
-      if (hi - cov > T_SEG) cover_to(lo);
-      packs.push_back(Pack{(uint32_t)cov, hi, (uint32_t)small.size(), (uint32_t)small.size() + 1});
-    }
-    small.push_back(sg);
-    cov = hi;
-  }
-  cover_to(n_all);
+  gosort_segments(hstart, ngroups, small, packs, big);
   P.n = hstart[ngroups];
   P.nsmall = (uint32_t)small.size();
   P.npacks = (uint32_t)packs.size();

@@ -30,131 +30,7 @@
 
 namespace syz {
 
-// ---- the key-space plan: syzkaller_amd/sharding.py plan_parts / _assign / split_bounds, restated ------
-// (the same cost model and tie-breaking, so the Python rehearsals and the library agree;
-// tests/test_multi.py compares the two)
-namespace kp {
-constexpr int64_t SMALL_GROUP = 8192;
-constexpr double LAT_REF_US = 290.0;   // the Go sort's dependent rounds once a rank holds a big group
-constexpr double US_PER_PC = 4.26e-6;  // per streamed PC (transpose + first-occurrence tables)
-constexpr double US_PER_ENTRY = 1.24e-3;
-constexpr double SMALL_PC_FRACTION = 0.3;
-
-inline double sort_latency_us(int64_t n) { return n <= SMALL_GROUP ? 0.0 : LAT_REF_US; }
-
-struct Plan {
-  std::vector<std::vector<int>> ranks;  // ranks[g]: holders of group g's parts, the primary first
-  std::vector<double> cost;             // modelled step per rank (µs)
-};
-
-static Plan assign(const std::vector<int64_t>& E, const std::vector<double>& P, const std::vector<int64_t>& k, int R) {
-  const size_t G = E.size();
-  std::vector<double> lat(G), w(G);
-  for (size_t g = 0; g < G; g++) {
-    lat[g] = sort_latency_us(E[g]);
-    const double f = E[g] > SMALL_GROUP ? 1.0 : SMALL_PC_FRACTION;
-    w[g] = US_PER_PC * P[g] * f / (double)std::max<int64_t>(k[g], 1) + US_PER_ENTRY * (double)E[g];
-  }
-  struct Item {
-    double c;
-    uint32_t g, j;
-  };
-  std::vector<Item> items;
-  for (size_t g = 0; g < G; g++)
-    if (E[g] > 0)
-      for (int64_t j = 0; j < k[g]; j++) items.push_back(Item{lat[g] + w[g], (uint32_t)g, (uint32_t)j});
-  std::sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
-    if (a.c != b.c) return a.c > b.c;
-    if (a.g != b.g) return a.g < b.g;
-    return a.j < b.j;
-  });
-  std::vector<double> cl(R, 0.0), cw(R, 0.0);
-  Plan p;
-  p.ranks.assign(G, {});
-  for (const Item& it : items) {
-    int best = -1;
-    double bc = 0;
-    for (int r = 0; r < R; r++) {
-      const auto& h = p.ranks[it.g];
-      if (std::find(h.begin(), h.end(), r) != h.end()) continue;
-      const double c = std::max(cl[r], lat[it.g]) + cw[r] + w[it.g];
-      if (best < 0 || c < bc - 1e-9) {
-        best = r;
-        bc = c;
-      }
-    }
-    p.ranks[it.g].push_back(best);
-    cl[best] = std::max(cl[best], lat[it.g]);
-    cw[best] += w[it.g];
-  }
-  p.cost.resize(R);
-  for (int r = 0; r < R; r++) p.cost[r] = cl[r] + cw[r];
-  return p;
-}
-
-// start with whole groups, then double the part count of the heaviest group on the bottleneck rank
-// while the modelled step (max over ranks) improves; split_largest > 1 forces the largest group
-// into that many parts instead (rehearsals and tests)
-static Plan plan_parts(const std::vector<int64_t>& E, const std::vector<double>& P, int R, uint32_t split_largest = 0,
-                       int max_rounds = 24) {
-  const size_t G = E.size();
-  std::vector<int64_t> k(G, 1);
-  if (split_largest > 1 && G) {
-    const size_t g = (size_t)(std::max_element(E.begin(), E.end()) - E.begin());
-    k[g] = std::min<int64_t>(split_largest, R);
-    return assign(E, P, k, R);
-  }
-  Plan cur = assign(E, P, k, R);
-  for (int round = 0; round < max_rounds; round++) {
-    const int r = (int)(std::max_element(cur.cost.begin(), cur.cost.end()) - cur.cost.begin());
-    int64_t pick = -1;
-    double pv = 0;
-    for (size_t g = 0; g < G; g++) {
-      const auto& h = cur.ranks[g];
-      if (std::find(h.begin(), h.end(), r) == h.end() || k[g] >= R || E[g] <= SMALL_GROUP) continue;
-      const double v = sort_latency_us(E[g]) + US_PER_PC * P[g] / (double)k[g];
-      if (pick < 0 || v > pv) {  // (ties: the smaller group id, as max(key=(v, -g)))
-        pick = (int64_t)g;
-        pv = v;
-      }
-    }
-    if (pick < 0) break;
-    std::vector<int64_t> k2(k);
-    k2[pick] = std::min<int64_t>(R, k[pick] * 2);
-    Plan nxt = assign(E, P, k2, R);
-    if (*std::max_element(nxt.cost.begin(), nxt.cost.end()) >=
-        *std::max_element(cur.cost.begin(), cur.cost.end()) - 1e-6)
-      break;
-    k = k2;
-    cur = nxt;
-  }
-  return cur;
-}
-
-// PC-value bounds of a split group's k parts: k + 1 values [0, ..., 2^32] at equal-count quantiles of a
-// sample of the group's PCs (every 16th entry of the group in corpus order), a pure function of the
-// group's covers (sharding.py split_bounds)
-static std::vector<uint64_t> split_bounds(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, size_t n,
-                                          uint32_t g, size_t k) {
-  std::vector<uint64_t> sample;
-  size_t seen = 0;
-  for (size_t e = 0; e < n; e++) {
-    if (group[e] != g) continue;
-    if (seen++ % 16) continue;
-    sample.insert(sample.end(), pcs + off[e], pcs + off[e + 1]);
-  }
-  std::vector<uint64_t> b{0};
-  if (!sample.empty()) {
-    std::sort(sample.begin(), sample.end());
-    for (size_t j = 1; j < k; j++)
-      b.push_back(std::max<uint64_t>(b.back() + 1, sample[std::min(sample.size() - 1, sample.size() * j / k)]));
-  } else {
-    for (size_t j = 1; j < k; j++) b.push_back((1ull << 32) * j / k);
-  }
-  b.push_back(1ull << 32);
-  return b;
-}
-}  // namespace kp
+// (the key-space plan, kp::plan_parts / kp::split_bounds: plan_host.cpp)
 
 // ---- device helpers -----------------------------------------------------------------------------------
 __global__ void k_mg_max_u8(uint8_t* dst, const uint8_t* src, uint64_t bytes, uint32_t nsrc) {

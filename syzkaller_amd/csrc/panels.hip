@@ -210,12 +210,14 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
                                             const uint32_t* __restrict__ rank_of_member, const uint64_t* gstart,
                                             uint32_t* selbits, SminLds& L) {
   uint32_t* tab = L.tabs;
+  [[maybe_unused]] const uint64_t t0 = SM_T();
   {
     uint4* t4 = reinterpret_cast<uint4*>(tab);
     const uint4 none4 = make_uint4(RANK_NONE, RANK_NONE, RANK_NONE, RANK_NONE);
     for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
   }
   __syncthreads();
+  [[maybe_unused]] const uint64_t t1 = SM_T();
   SMIN_WALK(SYZ_SL_MU, it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
                                     [&](uint32_t o, uint32_t R) {
                                       if (SYZ_SMIN_NOF) {  // timing only: the walk without table updates
@@ -229,9 +231,16 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
                                       if (*t > R) atomicMin(t, R);
                                     });
   __syncthreads();
+  [[maybe_unused]] const uint64_t t2 = SM_T();
   if (SYZ_SMIN_NOEMIT) return;  // timing only
   const uint64_t gb = gstart[it.g];
   emit_winner_bits<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, L.wsc, selbits);
+  [[maybe_unused]] const uint64_t t3 = SM_T();
+  SM_STAT_ADD(0, 1);
+  SM_STAT_ADD(1, t3 - t0);
+  SM_STAT_ADD(2, t1 - t0);
+  SM_STAT_ADD(3, t2 - t1);
+  SM_STAT_ADD(4, t3 - t2);
 }
 
 #ifndef SYZ_SL_HU
@@ -411,35 +420,7 @@ __global__ void k_slices(const uint32_t* pcs, const uint64_t* off, const uint32_
 
 // ---- host orchestration ---------------------------------------------------------------------------------
 
-void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, uint32_t G, std::vector<PGroup>& pg) {
-  pg.assign(G, PGroup{});
-  auto nwin = [&](uint32_t S) { return (span + (1ull << S) - 1) >> S; };
-  uint32_t smin = DS;
-  while (smin < 32 && nwin(smin) > WMAX) smin++;
-  const uint64_t w15 = nwin(DS);
-  for (uint32_t g = 0; g < G; g++) {
-    const uint64_t E = gpcs[g];
-    PGroup& p = pg[g];
-    if (smin == DS && E >= (uint64_t)DENSE * w15) {
-      p.S = DS;
-      p.W = (uint32_t)w15;
-      p.mode = PMODE_DIRECT;
-      continue;
-    }
-    // sparse: the widest window (<= 2^SMAX addresses) that still gives about HTARGET PCs per window;
-    // a group of < 2^13 entries whose windows fit 2^19 addresses takes the packed table (2x the PCs)
-    const bool small = gstart[g + 1] - gstart[g] < (1u << PK_RBITS);
-    const uint64_t tgt = small ? PHTARGET : HTARGET;
-    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(WMAX, (E + tgt - 1) / tgt));
-    uint32_t S = std::max(smin, DS);
-    while (S < SMAX && nwin(S + 1) >= want) S++;
-    if (S > SMAX) S = SMAX;
-    if (small && S > PSMAX && nwin(PSMAX) <= WMAX) S = PSMAX;
-    p.S = S;
-    p.W = (uint32_t)std::max<uint64_t>(1, nwin(S));
-    p.mode = small && S <= PSMAX ? PMODE_PACKED : PMODE_HASH;
-  }
-}
+// (plan_windows, slab_plan, plan_items: plan_host.cpp)
 
 static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_span);
 
@@ -476,40 +457,6 @@ static bool pm_spec() {
 }
 
 
-
-void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* hpcs, const std::vector<PGroup>& hpg,
-               uint32_t G, bool want_wtot) {
-  J.G = G;
-  J.hsg.assign(G, SGroup{});
-  J.hgblock.assign(G + 1, 0);
-  J.hbgroup.clear();
-  J.slab_bound = J.dtotal = J.wtotal = J.total_pcs = J.xtotal = 0;
-  J.wmax = 1;
-  for (uint32_t g = 0; g < G; g++) {
-    const uint64_t ng = hstart[g + 1] - hstart[g];
-    const uint32_t S = hpg[g].S, W = hpg[g].W;
-    // a member's tag fits 32 - S bits, and the all-ones tag is never a member's (SL_NONE: padding)
-    const uint32_t memb = S <= 23 ? SL_MEMB : (1u << (32 - S)) - 1;
-    const uint64_t nb = (ng + memb - 1) / memb;
-    J.hgblock[g + 1] = J.hgblock[g] + (uint32_t)nb;
-    J.hbgroup.insert(J.hbgroup.end(), nb, g);
-    // slabs of a block: ceil(tiles / SL_TILES); tiles <= PCs / 64 + members
-    const uint64_t stride = (hpcs[g] / 64 + ng) / SL_TILES + nb + 1;
-    // a group's element offsets (D) are 32-bit
-    if (hpcs[g] + stride * slab_pad(W) + 8 >= (1ull << 32)) fail(SYZGPU_EINVAL, "a call group with 2^32 or more PCs");
-    // per-window totals (wtot) only for the hashed groups of a job that asks for them
-    const bool wt = want_wtot && hpg[g].mode == PMODE_HASH;
-    J.hsg[g] = SGroup{J.dtotal, S, W, (uint32_t)stride, memb, wt ? (uint32_t)J.wtotal : SG_NO_WTOT, 0, J.xtotal};
-    J.wmax = std::max(J.wmax, W);
-    J.xtotal += stride * slab_pad(W);
-    J.dtotal += (uint64_t)(W + 1) * stride;
-    if (wt) J.wtotal += W;
-    J.slab_bound += stride;
-    J.total_pcs += hpcs[g];
-  }
-  if (J.wtotal >= (1ull << 32) || J.slab_bound >= (1ull << 31)) fail(SYZGPU_EINVAL, "too many slabs");
-  J.B = J.hgblock[G];
-}
 
 // the members' tile prefix (tpos): needs no plan, so it can run before the host's
 uint64_t* slab_tiles(const uint32_t* mlen, size_t nmem, const char* prefix, hipStream_t s) {
@@ -625,33 +572,14 @@ static void plan_layout(MinJob& J, const RawMinArgs& a, const std::vector<uint64
     SlabJob& SJ = P->SJ;
     slab_plan(SJ, hstart, hsl, hpg, G, false);
     const uint32_t B = SJ.B;
-    // work items: (call, window), class (big groups: sorted by the global rounds) and mode, largest
-    // expected window first; a key part only its windows
-    std::vector<uint32_t> order(G);
-    std::iota(order.begin(), order.end(), 0u);
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint32_t x, uint32_t y) { return hpcs[x] / hpg[x].W > hpcs[y] / hpg[y].W; });
-    std::vector<uint32_t> iw0(G, 0), iw1(G, 0);
-    for (uint32_t g : order) {
-      if (!hpcs[g]) continue;
-      uint32_t w0 = 0, w1 = hpg[g].W;
-      if (a.key_lo) {
-        const uint32_t klo = std::max(a.key_lo[g], lo), khi = std::min(a.key_hi[g], hi);
-        if (klo > khi) continue;
-        w0 = (klo - lo) >> hpg[g].S;
-        w1 = std::min<uint32_t>(hpg[g].W, ((khi - lo) >> hpg[g].S) + 1);
-      }
-      iw0[g] = w0;
-      iw1[g] = w1;
-      P->icount[is_big(g) ? 1 : 0][hpg[g].mode] += w1 - w0;
-      P->item_pcs[is_big(g) ? 1 : 0][hpg[g].mode] += hsl[g];
-    }
-    size_t nitems = 0;
-    for (int big = 0; big < 2; big++)
-      for (int m = 0; m < 3; m++) {
-        P->ifirst[big][m] = nitems;
-        nitems += P->icount[big][m];
-      }
+    ItemPlan ip;
+    plan_items(hstart, hpcs, hsl, hpg, G, a.key_lo, a.key_hi, lo, hi, ip);
+    const size_t nitems = ip.items.size();
+    std::memcpy(P->icount, ip.icount, sizeof(P->icount));
+    std::memcpy(P->item_pcs, ip.item_pcs, sizeof(P->item_pcs));
+    std::memcpy(P->cpcs, ip.cpcs, sizeof(P->cpcs));
+    std::memcpy(P->cent, ip.cent, sizeof(P->cent));
+    P->ifirst = ip.ifirst;
     // the plan goes over in one copy: SGroup[G], gblock[G + 1], bgroup[B + 1], items[nitems + 1]
     auto al16 = [](size_t x) { return (x + 15) & ~size_t(15); };
     P->o_gb = al16((G + 1) * sizeof(SGroup));
@@ -665,12 +593,7 @@ static void plan_layout(MinJob& J, const RawMinArgs& a, const std::vector<uint64
     std::memcpy(stage, SJ.hsg.data(), G * sizeof(SGroup));
     std::memcpy(stage + P->o_gb, SJ.hgblock.data(), (G + 1) * 4);
     if (B) std::memcpy(stage + P->o_bg, SJ.hbgroup.data(), (size_t)B * 4);
-    PItem* hit = reinterpret_cast<PItem*>(stage + P->o_it);
-    std::array<std::array<size_t, 3>, 2> at = P->ifirst;
-    for (uint32_t g : order) {
-      size_t& k = at[is_big(g) ? 1 : 0][hpg[g].mode];
-      for (uint32_t w = iw0[g]; w < iw1[g]; w++) hit[k++] = PItem{g, w};
-    }
+    if (nitems) std::memcpy(stage + P->o_it, ip.items.data(), nitems * sizeof(PItem));
     // the words a step speculated on this plan must read back (k_gpack's gate)
     uint64_t* ex = reinterpret_cast<uint64_t*>(stage + P->o_exp);
     std::memset(ex, 0, (3 * (size_t)G + 4) * 8);
@@ -682,10 +605,6 @@ static void plan_layout(MinJob& J, const RawMinArgs& a, const std::vector<uint64
     SJ.dsg = reinterpret_cast<SGroup*>(P->dstage.p);
     SJ.dgblock = reinterpret_cast<uint32_t*>(P->dstage.p + P->o_gb);
     SJ.dbgroup = reinterpret_cast<uint32_t*>(P->dstage.p + P->o_bg);
-    for (uint32_t g = 0; g < G; g++) {
-      P->cpcs[is_big(g) ? 1 : 0] += hsl[g];
-      P->cent[is_big(g) ? 1 : 0] += hstart[g + 1] - hstart[g];
-    }
     P->lo = lo;
     P->n = n;
     P->hi = hi;
@@ -1131,6 +1050,18 @@ void minimize_raw_fetch(MinJob& J, int64_t* out_idx, uint64_t* group_out_off) {
 using namespace syz;
 
 extern "C" {
+
+#ifdef SYZ_SMIN_STATS
+int syzgpu_debug_smin_stats(unsigned long long* out, int reset) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sm_stats), sizeof(unsigned long long) * 16);
+  if (reset) {
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sm_stats), z, sizeof(z));
+  }
+  return 0;
+}
+#endif
 
 int syzgpu_mz_create(syzgpu_mz** out) {
   SYZ_API_BODY({

@@ -5,20 +5,13 @@
 #include <mutex>
 #include <vector>
 
+#include "plan_host.hpp"
 #include "store.hpp"
 
 namespace syz {
 
 constexpr uint32_t MAX_GROUPS_PM = 4096;
 
-enum { PMODE_DIRECT = 0, PMODE_HASH = 1, PMODE_PACKED = 2 };
-
-struct PGroup {          // per call group: window bits, windows, table kind
-  uint32_t S, W, mode, rb;  // rb: first region of the group (region form: rb + segment * W + window)
-};
-struct PItem {           // one (call group, window) min-rank table
-  uint32_t g, w;
-};
 
 struct PSlab {
   uint64_t elem;      // first element (4-aligned: the slab's passes leave as 16-byte vectors)
@@ -28,31 +21,11 @@ struct PSlab {
   uint32_t j, pad;    // slab index inside its call group
 };
 
-constexpr uint32_t SG_NO_WTOT = 0xFFFFFFFFu;  // SGroup.wbase of a group without per-window totals
-struct SGroup {       // per call group, slab form
-  uint64_t dbase;     // first D entry
-  uint32_t S, W;      // window bits, windows
-  uint32_t stride;    // D row length (>= the group's slabs)
-  uint32_t memb;      // members per block: min(SL_MEMB, 2^(32 - S))
-  uint32_t wbase;     // first per-window total (wtot, when P is asked for them), else SG_NO_WTOT
-  uint32_t pad;       // bit 0: a big call group (the Go sort's global rounds; P's second launch)
-  uint64_t xbase;     // element slots of the padding of the groups before (a slab's runs are padded to
-                      // 4 elements: it takes its PCs + 3 W + 4 slots at most)
-};
-
-// slots of padding a slab of a call with W windows may take (k_sl_slabs' spacing)
-__host__ __device__ inline uint64_t slab_pad(uint32_t W) { return 3ull * W + 4; }
-
 // The slab form's layout of one job (slab_dev.hpp), device arrays in the lane's scratch under a name
 // prefix. slab_plan (host): blocks, slab bounds, D rows; the caller stages hsg / hgblock / hbgroup to the
 // device and sets dsg / dgblock / dbgroup; slab_build (device): tiles, their prefix, the slabs, per-group
 // first slab and element; then k_slab (P) and for_slab_window (M).
-struct SlabJob {
-  uint32_t G = 0, B = 0;
-  uint32_t wmax = 1;  // the widest call's windows (P's LDS staging is sized for it)
-  uint64_t slab_bound = 0, dtotal = 0, wtotal = 0, total_pcs = 0, xtotal = 0;
-  std::vector<SGroup> hsg;
-  std::vector<uint32_t> hgblock, hbgroup;
+struct SlabJob : SlabPlan {  // the host plan (plan_host.hpp slab_plan) and its device arrays
   const SGroup* dsg = nullptr;
   const uint32_t* dgblock = nullptr;
   const uint32_t* dbgroup = nullptr;
@@ -66,9 +39,6 @@ struct SlabJob {
   uint64_t ecap = 0;         // elements the buffer holds
   uint32_t* wtot = nullptr;  // per (call, window) totals, when asked for
 };
-// hpcs: PCs each call group's members hold (their slices); S, W from hpg
-void slab_plan(SlabJob& J, const std::vector<uint64_t>& hstart, const uint64_t* hpcs, const std::vector<PGroup>& hpg,
-               uint32_t G, bool want_wtot);
 void slab_build(SlabJob& J, const char* prefix, const uint32_t* mlen, const uint64_t* mpos, size_t nmem,
                 const uint64_t* gstart, hipStream_t s, bool tiles_done = false);
 // the members' tile prefix alone (slab_build's first step, which needs no plan): returns tpos
@@ -147,7 +117,6 @@ void minimize_raw_xchg(MinJob& J, const uint32_t* groups, const uint64_t* offset
 void minimize_raw_end(MinJob& J, const RawEndArgs& e);
 void minimize_raw_end_check(int err);  // the deferred check of end's device error word (mz_err)
 void minimize_raw_fetch(MinJob& J, int64_t* out_idx, uint64_t* group_out_off);
-void plan_windows(uint64_t span, const uint64_t* gpcs, const uint64_t* gstart, uint32_t G, std::vector<PGroup>& pg);
 // group-major kept list (device) from a rank bitmap
 void sel_compact_dev(const uint32_t* selbits, const uint32_t* ent_of_rank, const uint64_t* gstart, size_t n, uint32_t G,
                      int64_t* out_idx, uint64_t* group_out_off, hipStream_t s);

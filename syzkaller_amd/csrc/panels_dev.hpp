@@ -6,10 +6,6 @@
 
 namespace syz {
 
-constexpr uint32_t WMAX = 1024;   // windows per call group
-#ifndef SYZ_DS
-#define SYZ_DS 14
-#endif
 #ifndef SYZ_PBM_WORDS
 #define SYZ_PBM_WORDS 6144
 #endif
@@ -19,9 +15,8 @@ constexpr uint32_t WMAX = 1024;   // windows per call group
 #ifndef SYZ_DIRECT_WPE
 #define SYZ_DIRECT_WPE 1
 #endif
-constexpr uint32_t DS = SYZ_DS;  // direct-mode window bits: a 2^DS-entry u32 min table
 constexpr uint32_t PBM_WORDS = SYZ_PBM_WORDS;  // LDS winner bitmap of the direct kernel
-constexpr uint32_t SMAX = 26;     // 32 - 6 tag bits
+// (WMAX, DS, SMAX, DENSE, HTARGET, PK_RBITS, PSMAX, PHS, PHTARGET: plan_host.hpp)
 constexpr int PP_BLOCK = 1024;
 constexpr int PP_WAVES = PP_BLOCK / 64;
 constexpr int PP_U = 4;     // 64-PC tiles per wave in flight in k_part's passes
@@ -33,31 +28,18 @@ constexpr uint32_t HS = 1u << HS_BITS;  // open-addressing slots of a sparse-win
 #ifndef SYZ_HCAP
 #define SYZ_HCAP 16384
 #endif
-#ifndef SYZ_HTARGET
-#define SYZ_HTARGET 8192
-#endif
 constexpr uint32_t HCAP = SYZ_HCAP;  // PCs per round of a sparse window: twice the slots, i.e. the table
                                      // fills only if no PC repeats (then the probe limit redoes the
                                      // window in more rounds); a tighter cap reads most windows twice
 constexpr uint32_t HPROBE = 128; // a longer probe run means the table is full after all
 constexpr uint32_t HBM_WORDS = 2048;  // LDS winner bitmap of the sparse kernel (65536 ranks per pass)
 // packed sparse windows (call groups of < 8192 entries): one u32 per slot, offset << 13 | rank in the
-// group, 16K slots in the same 64 KB, so twice the PCs per window (half the workgroups)
-constexpr uint32_t PK_RBITS = 13;
-constexpr uint32_t PSMAX = 32 - PK_RBITS;  // window bits a packed slot holds
-#ifndef SYZ_PK_BITS
-#define SYZ_PK_BITS 13
-#endif
+// group (PK_RBITS, PHS_BITS: plan_host.hpp)
 #ifndef SYZ_PK_BLOCK
 #define SYZ_PK_BLOCK 512
 #endif
-constexpr uint32_t PHS_BITS = SYZ_PK_BITS;  // 13: 32 KB tables in 512-thread workgroups, four per CU
-constexpr int PK_BLOCK = SYZ_PK_BLOCK;
-constexpr uint32_t PHS = 1u << PHS_BITS;
+constexpr int PK_BLOCK = SYZ_PK_BLOCK;     // 32 KB packed tables in 512-thread workgroups, four per CU
 constexpr uint32_t PHCAP = 2 * PHS;       // PCs per round of a packed window
-constexpr uint32_t DENSE = 8192u >> (15 - DS);  // PCs per window (per 32K addresses: 8192) above which a call is direct-mode
-constexpr uint32_t HTARGET = SYZ_HTARGET;  // PCs per window a sparse call's window size aims at
-constexpr uint32_t PHTARGET = PHS;  // the same for packed windows: as many PCs as the table's slots
 
 
 

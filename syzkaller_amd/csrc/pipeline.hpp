@@ -3,19 +3,13 @@
 #include <functional>
 
 #include "common.hpp"
+#include "plan_host.hpp"
 
 namespace syz {
 
-struct Seg {
-  uint32_t lo, hi;
-  int32_t depth;  // remaining sort.Sort maxDepth budget at this recursion node
-  uint32_t pad;
-};
 
 // gosort.hip: the element at sorted position r of the groups' ranges is el[perm[r]]
-constexpr uint32_t GS_T_SEG = 8192;                // call groups above this many entries start the global rounds
-constexpr uint64_t GS_U32_LEN_LIMIT = 1ull << 19;  // cover lengths the packed u32 sort element holds
-struct Pack;
+// (GS_T_SEG, GS_U32_LEN_LIMIT, Seg, Pack, gosort_segments: plan_host.hpp)
 struct GosortPlan {
   size_t n = 0;
   uint32_t nsmall = 0, npacks = 0, nbig = 0;

@@ -48,8 +48,11 @@ void* Pinned::get(size_t bytes) {
   if (bytes_ >= bytes && p_) return p_;
   if (p_) (void)hipHostFree(p_);
   p_ = nullptr;
-  SYZ_HIP(hipHostMalloc(&p_, bytes, hipHostMallocDefault));
-  bytes_ = bytes;
+  // headroom: a plan staged every call grows by a few bytes as the corpus grows, and each regrowth is a
+  // free + pinned allocation (hundreds of microseconds on the step's critical path)
+  const size_t want = bytes + bytes / 2 + 256;
+  SYZ_HIP(hipHostMalloc(&p_, want, hipHostMallocDefault));
+  bytes_ = want;
   return p_;
 }
 

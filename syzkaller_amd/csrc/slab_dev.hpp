@@ -25,17 +25,22 @@
 
 namespace syz {
 
-#ifndef SYZ_SL_BLOCK
-#define SYZ_SL_BLOCK 512
+// Diagnostic build only (-DSYZ_SMIN_STATS, tools/smin_stats.py): where a direct-window M workgroup's cycles
+// go. [0] workgroups [1] cycles [2] table init [3] walk [4] emit [5] batches [6] element windows
+// [7] wave-0 steps [8] batch set-up cycles (scan, run maps) [9] step-loop cycles [10] vectors [11] runs
+#ifdef SYZ_SMIN_STATS
+static __device__ unsigned long long g_sm_stats[16];
+#define SM_STAT_ADD(i, v) \
+  do {                    \
+    if (threadIdx.x == 0) atomicAdd(&g_sm_stats[i], (unsigned long long)(v)); \
+  } while (0)
+#define SM_T() __builtin_amdgcn_s_memtime()
+#else
+#define SM_STAT_ADD(i, v)
+#define SM_T() 0ull
 #endif
-#ifndef SYZ_SL_TPW
-#define SYZ_SL_TPW 32
-#endif
-constexpr int SL_BLOCK = SYZ_SL_BLOCK;
-constexpr int SL_WAVES = SL_BLOCK / 64;
-constexpr int SL_TPW = SYZ_SL_TPW;
-constexpr uint32_t SL_TILES = (uint32_t)SL_TPW * SL_WAVES;  // tiles per slab (<= 64 PCs each)
-constexpr uint32_t SL_MEMB = 512;                              // members per slab at most
+
+// (SL_BLOCK, SL_TPW, SL_TILES, SL_MEMB: plan_host.hpp)
 static_assert(SL_TPW <= 64, "a wave's tile table is one register per lane");
 constexpr uint32_t SL_NONE = 0xFFFFFFFFu;  // a padding slot: no element (no member has the all-ones tag)
 
@@ -452,7 +457,10 @@ __device__ __forceinline__ void for_slab_window(const PItem it, const SGroup* __
   };
   uint32_t nlen, nrel, nmb;
   load_run(threadIdx.x, nlen, nrel, nmb);
+  SM_STAT_ADD(11, ns);
   for (uint32_t rb = 0; rb < ns; rb += BD) {
+    [[maybe_unused]] uint64_t tb = SM_T();
+    SM_STAT_ADD(5, 1);
     const uint32_t len = nlen, rel = nrel, mb = nmb;
     uint32_t pre, k, T;
     pk_scan(len, reinterpret_cast<uint32_t*>(red64), pre, k, T);
@@ -461,7 +469,9 @@ __device__ __forceinline__ void for_slab_window(const PItem it, const SGroup* __
       rmb[k] = mb;
     }
     load_run(rb + BD + threadIdx.x, nlen, nrel, nmb);
+    SM_STAT_ADD(10, T / 4);
     for (uint32_t ew = 0; ew < T; ew += 64 * NBLK) {
+      SM_STAT_ADD(6, 1);
       const uint32_t te = min(T, ew + 64 * NBLK);
       for (uint32_t j = threadIdx.x; j < 2 * NBLK; j += blockDim.x) bmask[j] = 0;
       __syncthreads();
@@ -474,6 +484,8 @@ __device__ __forceinline__ void for_slab_window(const PItem it, const SGroup* __
         }
       }
       __syncthreads();
+      [[maybe_unused]] const uint64_t ts = SM_T();
+      SM_STAT_ADD(8, ts - tb);
       const uint32_t nblk = (te - ew + 63) >> 6;
       const uint32_t step = (uint32_t)nwaves * U;
       // a step's runs (LDS) and vector loads; a lane past the window reads its block's first vector
@@ -500,6 +512,7 @@ __device__ __forceinline__ void for_slab_window(const PItem it, const SGroup* __
       };
       if ((uint32_t)wv < nblk) prep_load(wv, mbr, ok);
       for (uint32_t j0 = wv; j0 < nblk; j0 += step) {
+        SM_STAT_ADD(7, 1);
         // this step's ranks (gathers) and offsets; then the next step's loads into the same registers
         // (this step's elements are dead by then); then the updates, which wait only for the gathers
         uint32_t R[4 * U], o[4 * U];
@@ -531,6 +544,8 @@ __device__ __forceinline__ void for_slab_window(const PItem it, const SGroup* __
         }
       }
       __syncthreads();
+      SM_STAT_ADD(9, SM_T() - ts);
+      tb = SM_T();
     }
   }
 }
