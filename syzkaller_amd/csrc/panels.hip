@@ -182,6 +182,16 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 #endif
 #define SMIN_WALK(U, it, sg, gslab, gebase, D, slabs, elems, rom, wsc, red64, f) \
   for_slab_window<U, SYZ_SMIN_IDENT>(it, sg, gslab, gebase, D, slabs, elems, rom, wsc, red64, f)
+// the direct tables' walk: every wave on its own runs (slab_dev.hpp for_slab_window_w); SYZ_SMIN_WW=0: the
+// workgroup form
+#ifndef SYZ_SMIN_WW
+#define SYZ_SMIN_WW 1
+#endif
+#ifndef SYZ_SMIN_NBW
+#define SYZ_SMIN_NBW 16
+#endif
+constexpr uint32_t SMIN_NBW = SYZ_SMIN_NBW;
+static_assert(16 * (128 + 3 * SMIN_NBW) <= 2 * 1024 + 3 * PK_NBLK, "the wave walk's maps in the walk scratch");
 #ifndef SYZ_SL_MU
 #define SYZ_SL_MU 2
 #endif
@@ -192,17 +202,50 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 #endif
 // LDS of one M workgroup: the window's table (direct: 2^DS u32; hashed: keys + values or packed slots),
 // the walk's scratch (then the emit bitmap) and reductions
-template <int BLOCK, uint32_t TWORDS>
+template <int BLOCK, uint32_t TWORDS, uint32_t TOUCH = 1>
 struct SminLdsT {
   __align__(16) uint32_t tabs[TWORDS];
   __align__(16) uint32_t wsc[2 * BLOCK + 3 * PK_NBLK];
+  uint32_t touched[TOUCH];  // direct tables: a bit per entry some element wrote (the emit walks only those)
   uint64_t red64[BLOCK / 64 + 1];
   int full;
   static constexpr uint32_t WSC = 2 * BLOCK + 3 * PK_NBLK;
 };
-using SminLds = SminLdsT<1024, ((1u << DS) > 2 * HS ? (1u << DS) : 2 * HS)>;
+using SminLds = SminLdsT<1024, ((1u << DS) > 2 * HS ? (1u << DS) : 2 * HS), (1u << DS) / 32>;
 using SminPkLds = SminLdsT<PK_BLOCK, PHS>;  // packed windows: their slots only
+static_assert(sizeof(SminLds) <= 80 * 1024, "two direct-table workgroups per CU");
 static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
+
+// The direct table's winners -> the job's rank bitmap, like emit_winner_bits but over the touched entries
+// only: a window holds a few thousand keys in 2^DS slots, so walking the 512 words of the touched bitmap
+// and their set bits replaces a scan of every slot (r06: the full scan was 16 % of the kernel's cycles)
+template <uint32_t BMW>
+__device__ __forceinline__ void emit_touched(const uint32_t* tab, const uint32_t* touched, uint32_t ntw, uint64_t gbase,
+                                             uint64_t ng, uint32_t* bm, uint32_t* selbits) {
+  const uint64_t base = gbase & ~31ull;  // rank of bitmap word 0, bit 0
+  const uint32_t words = (uint32_t)min<uint64_t>(BMW, (gbase + ng - base + 31) / 32);
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
+  __syncthreads();
+  for (uint32_t wi = threadIdx.x; wi < ntw; wi += blockDim.x) {
+    uint32_t m = touched[wi];
+    while (m) {
+      const uint32_t b = __builtin_ctz(m);
+      m &= m - 1;
+      const uint32_t r = tab[wi * 32 + b];
+      const uint64_t lr = (uint64_t)r - base;
+      const uint32_t bit = 1u << (r & 31);
+      if (lr < 32ull * words) {
+        if (!(bm[lr >> 5] & bit)) atomicOr(&bm[lr >> 5], bit);
+      } else {
+        set_bits(&selbits[r >> 5], bit);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+    if (const uint32_t v = bm[i]) set_bits(&selbits[(base >> 5) + i], v);
+  __syncthreads();
+}
 
 __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, const uint32_t* gslab,
                                             const uint64_t* gebase, const uint32_t* D, const PSlab* slabs,
@@ -215,11 +258,11 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
     uint4* t4 = reinterpret_cast<uint4*>(tab);
     const uint4 none4 = make_uint4(RANK_NONE, RANK_NONE, RANK_NONE, RANK_NONE);
     for (uint32_t i = threadIdx.x; i < (1u << DS) / 4; i += 1024) t4[i] = none4;
+    for (uint32_t i = threadIdx.x; i < (1u << DS) / 32; i += 1024) L.touched[i] = 0;
   }
   __syncthreads();
   [[maybe_unused]] const uint64_t t1 = SM_T();
-  SMIN_WALK(SYZ_SL_MU, it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
-                                    [&](uint32_t o, uint32_t R) {
+  auto upd = [&](uint32_t o, uint32_t R) {
                                       if (SYZ_SMIN_NOF) {  // timing only: the walk without table updates
                                         if ((o ^ R) == 0x7FFF1234u) tab[0] = 0;
                                         return;
@@ -227,14 +270,25 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
                                       // a plain read first: most elements of a PC held by many inputs lose
                                       // to the rank already there, and same-address reads broadcast where
                                       // atomics serialize
-                                      uint32_t* t = &tab[tab_index(o)];
-                                      if (*t > R) atomicMin(t, R);
-                                    });
+                                      const uint32_t ix = tab_index(o);
+                                      uint32_t* t = &tab[ix];
+                                      const uint32_t cur = *t;
+                                      if (cur > R) {
+                                        atomicMin(t, R);
+                                        // the first writer of an entry saw it empty (and so did any racing
+                                        // one): every written entry is marked
+                                        if (cur == RANK_NONE) atomicOr(&L.touched[ix >> 5], 1u << (ix & 31));
+                                      }
+                                    };
+  if (SYZ_SMIN_WW)
+    for_slab_window_w<SYZ_SL_MU, SMIN_NBW>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, upd);
+  else
+    SMIN_WALK(SYZ_SL_MU, it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64, upd);
   __syncthreads();
   [[maybe_unused]] const uint64_t t2 = SM_T();
   if (SYZ_SMIN_NOEMIT) return;  // timing only
   const uint64_t gb = gstart[it.g];
-  emit_winner_bits<PK_SCRATCH_WORDS>(tab, 1u << DS, gb, gstart[it.g + 1] - gb, L.wsc, selbits);
+  emit_touched<PK_SCRATCH_WORDS>(tab, L.touched, (1u << DS) / 32, gb, gstart[it.g + 1] - gb, L.wsc, selbits);
   [[maybe_unused]] const uint64_t t3 = SM_T();
   SM_STAT_ADD(0, 1);
   SM_STAT_ADD(1, t3 - t0);
@@ -670,6 +724,7 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
     ProfScope ps(big ? "m_big" : "m_small", q, 0);
     const size_t nd = icount[big][PMODE_DIRECT], nh = icount[big][PMODE_HASH], np = icount[big][PMODE_PACKED];
     if (!nd && !nh && !np) return;
+    if (SYZ_SL_NOD) return;  // (timing variant without D rows: M would walk garbage)
     SYZ_HIP(hipStreamWaitEvent(q, big ? c.ev_sct[0] : c.ev_psmall, 0));
     if (nd) {
       ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
@@ -1055,9 +1110,11 @@ extern "C" {
 int syzgpu_debug_smin_stats(unsigned long long* out, int reset) {
   (void)hipDeviceSynchronize();
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sm_stats), sizeof(unsigned long long) * 16);
+  (void)hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_sl_stats), sizeof(unsigned long long) * 8);
   if (reset) {
     unsigned long long z[16] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sm_stats), z, sizeof(z));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sl_stats), z, sizeof(unsigned long long) * 8);
   }
   return 0;
 }

@@ -28,8 +28,15 @@ namespace syz {
 // Diagnostic build only (-DSYZ_SMIN_STATS, tools/smin_stats.py): where a direct-window M workgroup's cycles
 // go. [0] workgroups [1] cycles [2] table init [3] walk [4] emit [5] batches [6] element windows
 // [7] wave-0 steps [8] batch set-up cycles (scan, run maps) [9] step-loop cycles [10] vectors [11] runs
+// P's phases in the same build: g_sl_stats [0] slabs [1] cycles [2] member table + tile resolution
+// [3] tile loads waited + histogram [4] scan + D rows [5] placement [6] padding [7] stores
 #ifdef SYZ_SMIN_STATS
 static __device__ unsigned long long g_sm_stats[16];
+static __device__ unsigned long long g_sl_stats[8];
+#define SL_STAT_ADD(i, v) \
+  do {                    \
+    if (threadIdx.x == 0) atomicAdd(&g_sl_stats[i], (unsigned long long)(v)); \
+  } while (0)
 #define SM_STAT_ADD(i, v) \
   do {                    \
     if (threadIdx.x == 0) atomicAdd(&g_sm_stats[i], (unsigned long long)(v)); \
@@ -37,6 +44,7 @@ static __device__ unsigned long long g_sm_stats[16];
 #define SM_T() __builtin_amdgcn_s_memtime()
 #else
 #define SM_STAT_ADD(i, v)
+#define SL_STAT_ADD(i, v)
 #define SM_T() 0ull
 #endif
 
@@ -151,6 +159,9 @@ static_assert(5 * SL_MEMB + SL_MEMB / 4 <= 64 * SL_TILES, "the member table live
 #define SYZ_SL_RUNS 1
 #endif
 constexpr bool SL_RUNS = SYZ_SL_RUNS != 0;
+#ifndef SYZ_SL_NOD
+#define SYZ_SL_NOD 0  // timing experiment only (results wrong when 1): P without its D-row stores
+#endif
 // A wave's lanes with window w, ok: the maximal runs of consecutive ok lanes with one window. head: the
 // lane starts a run (len: its length); hd: the head of the lane's run.
 struct WinRun {
@@ -212,6 +223,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     if (threadIdx.x == 0) atomicOr(err, 64);
     return;
   }
+  [[maybe_unused]] const uint64_t q0 = SM_T();
   for (uint32_t i = threadIdx.x; i < nmem; i += BLOCK) {
     const uint64_t m = (uint64_t)sl.m0 + i;
     const int64_t r = (int64_t)tpos[m] - (int64_t)sl.t0;
@@ -260,6 +272,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
     cz = cnt | fl | (a << 9);
   }
+  [[maybe_unused]] const uint64_t q1 = SM_T();
   // every tile's PCs into registers, all loads in flight (a tile's address is wave-uniform)
   uint32_t v[TPW];
 #pragma unroll
@@ -316,6 +329,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
   }
   __syncthreads();
+  [[maybe_unused]] const uint64_t q2 = SM_T();
   if (wtot && gp.wbase != SG_NO_WTOT)
     for (uint32_t i = threadIdx.x; i < W; i += BLOCK)
       if (hist[i]) atomicAdd(&wtot[gp.wbase + i], hist[i]);
@@ -333,13 +347,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       if (i <= W) {
         hist[i] = pre;
         pst[i] = pre;
-        D[dcol + (uint64_t)i * gp.stride] = erel + pre;
+        if (!SYZ_SL_NOD) D[dcol + (uint64_t)i * gp.stride] = erel + pre;
       }
       run += tot;
     }
     total = run;
   }
   __syncthreads();
+  [[maybe_unused]] const uint64_t q3 = SM_T();
   // each element's place from its window's cursor (lanes outside the tile or the windows issue nothing)
   const uint32_t omask = (1u << S) - 1;
   {
@@ -370,10 +385,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     }
   }
   __syncthreads();
+  [[maybe_unused]] const uint64_t q4 = SM_T();
   // the padding slots of each run hold the no-element value: [cursor, next padded start)
   for (uint32_t i = threadIdx.x; i < W; i += BLOCK)
     for (uint32_t e = hist[i]; e < pst[i + 1]; e++) obuf[e] = SL_NONE;
   __syncthreads();
+  [[maybe_unused]] const uint64_t q5 = SM_T();
   // the slab leaves as one run of 16-byte stores (sl.elem and total are multiples of 4)
   if (sl.elem + total > ecap) {
     if (threadIdx.x == 0) atomicOr(err, 64);
@@ -384,6 +401,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const uint4* o4 = reinterpret_cast<const uint4*>(obuf);
     for (uint32_t q = threadIdx.x; q < total / 4; q += BLOCK) g4[q] = o4[q];
   }
+  [[maybe_unused]] const uint64_t q6 = SM_T();
+  SL_STAT_ADD(0, 1);
+  SL_STAT_ADD(1, q6 - q0);
+  SL_STAT_ADD(2, q1 - q0);
+  SL_STAT_ADD(3, q2 - q1);
+  SL_STAT_ADD(4, q3 - q2);
+  SL_STAT_ADD(5, q4 - q3);
+  SL_STAT_ADD(6, q5 - q4);
+  SL_STAT_ADD(7, q6 - q5);
 }
 
 // P's launch: one workgroup per slab (a bound; slabs past nslab return), the staging sized for the
@@ -546,6 +572,130 @@ __device__ __forceinline__ void for_slab_window(const PItem it, const SGroup* __
       __syncthreads();
       SM_STAT_ADD(9, SM_T() - ts);
       tb = SM_T();
+    }
+  }
+}
+
+// The same walk with every WAVE on its own runs (the direct tables' form): the window's runs are dealt to
+// the waves (run j to wave j mod waves, 64 runs a wave-batch, one per lane), each wave numbers its
+// wave-batch's vectors with a DPP scan and builds its run maps in its own LDS slice, then streams its
+// vectors in blocks of 64 with U blocks in flight. No workgroup barrier between the table's clear and its
+// emit: a wave waiting on its loads or rank gathers leaves the SIMD to the other waves of the workgroup
+// (the workgroup form above stops all 16 waves at five barriers per batch of runs, and a batch holds ~3
+// load round trips per wave). wsc: WW_WORDS(NBW) words per wave; NBW: blocks per element window of a
+// wave-batch. f(offset, rank) as above.
+__host__ __device__ constexpr uint32_t ww_words(uint32_t nbw) { return 128 + 3 * nbw; }
+template <int U, uint32_t NBW, class F>
+__device__ __forceinline__ void for_slab_window_w(const PItem it, const SGroup* __restrict__ sg,
+                                                  const uint32_t* __restrict__ gslab, const uint64_t* __restrict__ gebase,
+                                                  const uint32_t* __restrict__ D, const PSlab* __restrict__ slabs,
+                                                  const uint32_t* __restrict__ elems,
+                                                  const uint32_t* __restrict__ rank_of_member, uint32_t* wsc, F f) {
+  const uint32_t g = it.g, w = it.w;
+  const uint32_t c0 = gslab[g], ns = gslab[g + 1] - c0;
+  if (ns == 0) return;
+  const SGroup p = sg[g];
+  const uint32_t S = p.S, omask = (1u << S) - 1;
+  const uint32_t* Dw = D + p.dbase + (uint64_t)w * p.stride;
+  const uint32_t* Dw1 = Dw + p.stride;
+  const uint4* gel4 = reinterpret_cast<const uint4*>(elems + gebase[g]);
+  const uint32_t nwaves = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  const unsigned lane = __lane_id();
+  uint32_t* rrel = wsc + wv * ww_words(NBW);  // [64] vector offset of run k's vector 0 - its prefix
+  uint32_t* rmb = rrel + 64;                  // [64] first member of run k's slab
+  uint32_t* bstart = rmb + 64;                // [NBW] run holding block j's first vector
+  uint32_t* bmask = bstart + NBW;             // [2 NBW] runs starting inside block j (bit = offset)
+  // wave-batch b of this wave: runs wv + nwaves * (64 b + lane)
+  auto load_run = [&](uint32_t b, uint32_t& len, uint32_t& rel, uint32_t& mb) {
+    len = rel = mb = 0;
+    const uint32_t j = wv + nwaves * (64 * b + lane);
+    if (j < ns) {
+      const uint32_t a = Dw[j];
+      rel = a >> 2;
+      len = (Dw1[j] - a) >> 2;
+      mb = slabs[c0 + j].m0;
+    }
+  };
+  const uint32_t nb = (ns + 64 * nwaves - 1) / (64 * nwaves);  // wave-batches (every wave the same count)
+  uint32_t nlen, nrel, nmb;
+  load_run(0, nlen, nrel, nmb);
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint32_t len = nlen, rel = nrel, mb = nmb;
+    if (b + 1 < nb) load_run(b + 1, nlen, nrel, nmb);  // the next wave-batch's runs in flight
+    // this wave's vectors: an exclusive DPP scan of the run lengths; k: non-empty runs before this one
+    const uint32_t inc = wave_incl_scan<uint32_t>(len);
+    const uint32_t pre = inc - len;
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    if (T == 0) continue;  // (wave-uniform)
+    const uint64_t bal = __ballot(len != 0);
+    const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    wave_sync();  // (the previous wave-batch's map reads are done)
+    if (len) {
+      rrel[k] = rel - pre;
+      rmb[k] = mb;
+    }
+    for (uint32_t ew = 0; ew < T; ew += 64 * NBW) {
+      const uint32_t te = min(T, ew + 64 * NBW);
+      for (uint32_t j = lane; j < 2 * NBW; j += 64) bmask[j] = 0;
+      wave_sync();
+      if (len && pre < te && pre + len > ew) {
+        const uint32_t a = max(pre, ew) - ew, e = min(pre + len, te) - ew;
+        for (uint32_t j = (a + 63) >> 6; (j << 6) < e; j++) bstart[j] = k;
+        if (pre >= ew && (pre & 63)) {
+          const uint32_t o = pre - ew;
+          atomicOr(&bmask[2 * (o >> 6) + ((o >> 5) & 1)], 1u << (o & 31));
+        }
+      }
+      wave_sync();
+      const uint32_t nblk = (te - ew + 63) >> 6;
+      uint32_t mbr[U], mbn[U];
+      bool ok[U], okn[U];
+      uint4 ev[U];
+      auto prep_load = [&](uint32_t j0, uint32_t* mb_, bool* ok_) {
+        uint32_t vi[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t j = j0 + (uint32_t)u, jj = min(j, nblk - 1);
+          const uint32_t r0 = bstart[jj];
+          const uint32_t mlo_ = bmask[2 * jj], mhi_ = bmask[2 * jj + 1];
+          const uint32_t slo = (mlo_ >> 1) | (mhi_ << 31), shi = mhi_ >> 1;
+          const uint32_t idx = ew + (j << 6) + lane;
+          ok_[u] = j < nblk && idx < te;
+          const uint32_t r = r0 + __builtin_amdgcn_mbcnt_hi(shi, __builtin_amdgcn_mbcnt_lo(slo, 0u));
+          const uint32_t rr = ok_[u] ? r : r0;
+          vi[u] = rrel[rr] + (ok_[u] ? idx : ew + (jj << 6));
+          mb_[u] = rmb[rr];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) ev[u] = gel4[vi[u]];
+      };
+      prep_load(0, mbr, ok);
+      for (uint32_t j0 = 0; j0 < nblk; j0 += U) {
+        uint32_t R[4 * U], o[4 * U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t q[4] = {ev[u].x, ev[u].y, ev[u].z, ev[u].w};
+#pragma unroll
+          for (int t = 0; t < 4; t++) {
+            const bool val = ok[u] && q[t] != SL_NONE;
+            R[4 * u + t] = rank_of_member[mbr[u] + (val ? (q[t] >> S) : 0u)];
+            o[4 * u + t] = val ? (q[t] & omask) : 0xFFFFFFFFu;
+          }
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const bool more = j0 + U < nblk;  // wave-uniform
+        if (more) prep_load(j0 + U, mbn, okn);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4 * U; q++) f(o[q] & omask, o[q] == 0xFFFFFFFFu ? RANK_NONE : R[q]);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          mbr[u] = mbn[u];
+          ok[u] = okn[u];
+        }
+      }
     }
   }
 }

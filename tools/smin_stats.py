@@ -26,7 +26,7 @@ def dt(a):
 d = [dt(c.pcs), dt(c.off), dt(c.group), dt(c.prog_len)]
 job = cover.MinimizeJob()
 s = torch.cuda.current_stream().cuda_stream
-st = np.zeros(16, np.uint64)
+st = np.zeros(24, np.uint64)
 names = ["wgs", "cycles", "init", "walk", "emit", "batches", "ewins", "w0_steps", "batch_setup", "step_loop",
          "vectors", "runs"]
 for it in range(4):
@@ -40,3 +40,7 @@ for it in range(4):
           "setup %.0f steploop %.0f vectors %.0f runs %.0f | cycles/step %.0f" %
           (st[1] / w, st[2] / w, st[3] / w, st[4] / w, st[5] / w, st[6] / w, st[7] / w, st[8] / w, st[9] / w,
            st[10] / w, st[11] / w, st[9] / max(1, st[7])), flush=True)
+    q = st[16:24]
+    k = max(1, int(q[0]))
+    print("  P per slab (%d): cycles %.0f | members+tiles %.0f loads+hist %.0f scan+D %.0f place %.0f pad %.0f store %.0f"
+          % (k, q[1] / k, q[2] / k, q[3] / k, q[4] / k, q[5] / k, q[6] / k, q[7] / k), flush=True)
