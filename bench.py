@@ -176,7 +176,9 @@ def workload_label(args, world):
     if world == 1:
         # BASELINE.json configs[0] / [1] / [3] by their (programs, PC space); other shapes by their numbers
         name = {(10_000, 50_000): "config1-10k", (100_000, 500_000): "config2-100k",
-                (1_000_000, 2_000_000): "config4-1M"}.get((args.progs_per_gpu, args.npcs), "custom")
+                (1_000_000, 2_000_000): "config4-1M",
+                (8_000_000, 2_000_000): "config5-8M (hub merge of 8 managers' corpora, on 1 GPU)"}.get(
+                    (args.progs_per_gpu, args.npcs), "custom")
         return "%s: %d programs on 1 GPU, %s" % (name, args.progs_per_gpu, tail)
     return ("config5-shape: %d managers' corpora of %d programs (%d programs, weak scaling: %d per GPU), %s"
             % (world, args.progs_per_gpu, args.progs_per_gpu * world, args.progs_per_gpu, tail))
@@ -374,6 +376,8 @@ def main():
         roof = roofline(roof_kernel, roof_ev, workload=wkey) if roof_kernel else None
         if roof:
             roof["launches_per_step"] = round(roof_ev[roof_kernel]["launches"] / args.steps, 2)
+            # the rocprofv3 kernel the library's profiling scope times (ROCPROF_SCOPE)
+            roof["rocprof_kernel"] = next((pat.rstrip("<") for pat, sc in ROCPROF_SCOPE if sc == roof_kernel), None)
             roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
             roof["profiled_workload"] = wkey if wkey == PROFILED_WORKLOAD else None
             top = rocprof_top(workload=wkey)

@@ -84,8 +84,10 @@ __global__ __launch_bounds__(256) void k_minmax(const uint32_t* pcs, size_t L, u
 }
 
 // the job's per-step state: error word, speculation gate (err[2]), per-group PC sums, the PC span
-__global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span, uint32_t* mlmax) {
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= G; g += gridDim.x * blockDim.x) {
+__global__ void k_pm_init(int* err, uint64_t* gpcs, uint32_t G, uint32_t* span, uint32_t* mlmax, uint32_t* mctr) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g <= max(G, 15u); g += gridDim.x * blockDim.x) {
+    if (g < 16) mctr[g] = 0;  // M's item counters (m_items)
+    if (g > G) continue;
     gpcs[g] = 0;
     if (g < 2) {
       err[g] = 0;
@@ -139,7 +141,18 @@ __global__ void k_gpack(const uint64_t* gstart, const uint64_t* gpcs, const uint
 struct RankIdentity {
   __device__ uint32_t operator()(uint32_t v) const { return v; }
 };
-__device__ __forceinline__ void set_bits(uint32_t* w, uint32_t bits) { atomicOr(w, bits); }
+#ifndef SYZ_EMIT_RFIRST
+#define SYZ_EMIT_RFIRST 0
+#endif
+#ifndef SYZ_SMIN_NOATOM
+#define SYZ_SMIN_NOATOM 0  // timing experiment only (results wrong when 1): plain stores for the winner bits
+#endif
+__device__ __forceinline__ void set_bits(uint32_t* w, uint32_t bits) {
+  if (SYZ_SMIN_NOATOM)
+    *w = bits;
+  else
+    atomicOr(w, bits);
+}
 template <uint32_t BMW, class D = RankIdentity>
 __device__ __forceinline__ void emit_winner_bits(const uint32_t* tab, uint32_t nids, uint64_t gbase, uint64_t ng,
                                                  uint32_t* bm, uint32_t* selbits, D decode = D{}) {
@@ -190,6 +203,9 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 #ifndef SYZ_SMIN_NBW
 #define SYZ_SMIN_NBW 16
 #endif
+#ifndef SYZ_SMIN_WWP
+#define SYZ_SMIN_WWP 0  // the packed tables' walk in the wave form too
+#endif
 constexpr uint32_t SMIN_NBW = SYZ_SMIN_NBW;
 static_assert(16 * (128 + 3 * SMIN_NBW) <= 2 * 1024 + 3 * PK_NBLK, "the wave walk's maps in the walk scratch");
 #ifndef SYZ_SL_MU
@@ -202,36 +218,48 @@ static_assert(16 * (128 + 3 * SMIN_NBW) <= 2 * 1024 + 3 * PK_NBLK, "the wave wal
 #endif
 // LDS of one M workgroup: the window's table (direct: 2^DS u32; hashed: keys + values or packed slots),
 // the walk's scratch (then the emit bitmap) and reductions
-template <int BLOCK, uint32_t TWORDS, uint32_t TOUCH = 1>
+template <int BLOCK, uint32_t TWORDS, uint32_t TOUCH, uint32_t NB>
 struct SminLdsT {
   __align__(16) uint32_t tabs[TWORDS];
-  __align__(16) uint32_t wsc[2 * BLOCK + 3 * PK_NBLK];
-  uint32_t touched[TOUCH];  // direct tables: a bit per entry some element wrote (the emit walks only those)
+  __align__(16) uint32_t wsc[2 * BLOCK + 3 * NB];
+  uint32_t touched[TOUCH];  // a bit per table entry / slot some element wrote (the emit walks only those)
   uint64_t red64[BLOCK / 64 + 1];
   int full;
-  static constexpr uint32_t WSC = 2 * BLOCK + 3 * PK_NBLK;
+  static constexpr uint32_t WSC = 2 * BLOCK + 3 * NB;
+  static constexpr uint32_t NBLK = NB;  // the workgroup walk's blocks per element window
 };
-using SminLds = SminLdsT<1024, ((1u << DS) > 2 * HS ? (1u << DS) : 2 * HS), (1u << DS) / 32>;
-using SminPkLds = SminLdsT<PK_BLOCK, PHS>;  // packed windows: their slots only
+using SminLds = SminLdsT<1024, ((1u << DS) > 2 * HS ? (1u << DS) : 2 * HS), (1u << DS) / 32, PK_NBLK>;
+// packed windows: their slots only; a 128-block walk window keeps four workgroups per CU
+using SminPkLds = SminLdsT<PK_BLOCK, PHS, PHS / 32, 128>;
 static_assert(sizeof(SminLds) <= 80 * 1024, "two direct-table workgroups per CU");
+static_assert(sizeof(SminPkLds) + 16 <= 40 * 1024, "four packed-table workgroups per CU");
+static_assert(HS / 32 <= (1u << DS) / 32, "the hashed table's touched bits in the direct table's");
 static_assert(PHS <= 2 * HS, "packed slots in the key/value space");
 
 // The direct table's winners -> the job's rank bitmap, like emit_winner_bits but over the touched entries
 // only: a window holds a few thousand keys in 2^DS slots, so walking the 512 words of the touched bitmap
 // and their set bits replaces a scan of every slot (r06: the full scan was 16 % of the kernel's cycles)
-template <uint32_t BMW>
+template <uint32_t BMW, class Dec = RankIdentity>
 __device__ __forceinline__ void emit_touched(const uint32_t* tab, const uint32_t* touched, uint32_t ntw, uint64_t gbase,
-                                             uint64_t ng, uint32_t* bm, uint32_t* selbits) {
+                                             uint64_t ng, uint32_t* bm, uint32_t* selbits, Dec decode = Dec{}) {
   const uint64_t base = gbase & ~31ull;  // rank of bitmap word 0, bit 0
+  // The LDS bitmap over the group's first BMW rank words merges the winners of a word before the global
+  // ORs. It must stay: the winners of every window of a call concentrate on its lowest ranks (the longest
+  // covers), and one global atomic per winner put all of a call's windows on the same few words (r06: 4.8
+  // instead of 1.0 ms for the direct tables)
   const uint32_t words = (uint32_t)min<uint64_t>(BMW, (gbase + ng - base + 31) / 32);
+  constexpr bool dedupe = true;
   for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bm[i] = 0;
   __syncthreads();
-  for (uint32_t wi = threadIdx.x; wi < ntw; wi += blockDim.x) {
-    uint32_t m = touched[wi];
+  // two threads per touched word (16 bits each): the walk over set bits is a chain of LDS reads
+  for (uint32_t hw = threadIdx.x; hw < 2 * ntw; hw += blockDim.x) {
+    const uint32_t wi = hw >> 1;
+    uint32_t m = (touched[wi] >> (16 * (hw & 1))) & 0xFFFFu;
     while (m) {
-      const uint32_t b = __builtin_ctz(m);
+      const uint32_t b = __builtin_ctz(m) + 16 * (hw & 1);
       m &= m - 1;
-      const uint32_t r = tab[wi * 32 + b];
+      const uint32_t r = decode(tab[wi * 32 + b]);
+      if (r == RANK_NONE) continue;
       const uint64_t lr = (uint64_t)r - base;
       const uint32_t bit = 1u << (r & 31);
       if (lr < 32ull * words) {
@@ -241,9 +269,16 @@ __device__ __forceinline__ void emit_touched(const uint32_t* tab, const uint32_t
       }
     }
   }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
-    if (const uint32_t v = bm[i]) set_bits(&selbits[(base >> 5) + i], v);
+  if (dedupe) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+      if (const uint32_t v = bm[i]) {
+        uint32_t* gw = &selbits[(base >> 5) + i];
+        // SYZ_EMIT_RFIRST: skip the OR when a plain read already shows the bits (a stale copy can only lack
+        // bits: they are set, never cleared, during the step)
+        if (!SYZ_EMIT_RFIRST || (*gw & v) != v) set_bits(gw, v);
+      }
+  }
   __syncthreads();
 }
 
@@ -263,6 +298,7 @@ __device__ __forceinline__ void smin_direct(const PItem it, const SGroup* sg, co
   __syncthreads();
   [[maybe_unused]] const uint64_t t1 = SM_T();
   auto upd = [&](uint32_t o, uint32_t R) {
+                                      if (R == RANK_NONE) return;  // padding or a lane past the window
                                       if (SYZ_SMIN_NOF) {  // timing only: the walk without table updates
                                         if ((o ^ R) == 0x7FFF1234u) tab[0] = 0;
                                         return;
@@ -316,13 +352,15 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
   const uint32_t E = slab_window_count<BLOCK>(it, sg, gslab, D, reinterpret_cast<uint32_t*>(L.red64));
   if (E == 0) return;
   uint32_t R = (E + CAP - 1) / CAP;
+  uint32_t* touched = L.touched;
+  auto touch = [&](uint32_t h) { atomicOr(&touched[h >> 5], 1u << (h & 31)); };
   for (uint32_t round = 0; round < R;) {
     for (uint32_t i = threadIdx.x; i < TW; i += BLOCK) tabs[i] = (PACKED || i < HS) ? 0xFFFFFFFFu : RANK_NONE;
+    for (uint32_t i = threadIdx.x; i < NS / 32; i += BLOCK) touched[i] = 0;
     if (threadIdx.x == 0) L.full = 0;
     __syncthreads();
     const uint32_t RR = R, rr = round;
-    SMIN_WALK(SYZ_SL_HU, it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, L.red64,
-                                      [&](uint32_t o, uint32_t Rk) {
+    auto upd = [&](uint32_t o, uint32_t Rk) {
                                         if (Rk == RANK_NONE) return;  // a lane past the window
                                         if (SYZ_SMIN_NOF) {  // timing only: the walk without table updates
                                           if ((o ^ Rk) == 0x7FFF1234u) L.full = 1;
@@ -336,7 +374,10 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
                                             uint32_t k = keys[h];
                                             if (k == 0xFFFFFFFFu) {
                                               k = atomicCAS(&keys[h], 0xFFFFFFFFu, pk);
-                                              if (k == 0xFFFFFFFFu) return;
+                                              if (k == 0xFFFFFFFFu) {
+                                                touch(h);
+                                                return;
+                                              }
                                             }
                                             if ((k >> PK_RBITS) == o) {
                                               if (k > pk) atomicMin(&keys[h], pk);
@@ -350,7 +391,10 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
                                             uint32_t k = keys[h];
                                             if (k == 0xFFFFFFFFu) {
                                               k = atomicCAS(&keys[h], 0xFFFFFFFFu, o);
-                                              if (k == 0xFFFFFFFFu) k = o;
+                                              if (k == 0xFFFFFFFFu) {
+                                                k = o;
+                                                touch(h);
+                                              }
                                             }
                                             if (k == o) {
                                               if (vals[h] > Rk) atomicMin(&vals[h], Rk);
@@ -360,7 +404,12 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
                                           }
                                         }
                                         L.full = 1;
-                                      });
+                                      };
+    if (PACKED && SYZ_SMIN_WWP)
+      for_slab_window_w<SYZ_SL_HU, 16>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member, L.wsc, upd);
+    else
+      for_slab_window<SYZ_SL_HU, SYZ_SMIN_IDENT, LT::NBLK>(it, sg, gslab, gebase, D, slabs, elems, rank_of_member,
+                                                           L.wsc, L.red64, upd);
     __syncthreads();
     if (L.full) {
       R *= 2;
@@ -375,14 +424,48 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
     }
     if constexpr (PACKED) {
       const uint32_t g32 = (uint32_t)gb;
-      emit_winner_bits<LT::WSC>(keys, NS, gb, ng, L.wsc, selbits, [g32](uint32_t v) {
+      emit_touched<LT::WSC>(keys, touched, NS / 32, gb, ng, L.wsc, selbits, [g32](uint32_t v) {
         return v == 0xFFFFFFFFu ? RANK_NONE : g32 + (v & ((1u << PK_RBITS) - 1));
       });
     } else {
-      emit_winner_bits<LT::WSC>(vals, HS, gb, ng, L.wsc, selbits);
+      emit_touched<LT::WSC>(vals, touched, NS / 32, gb, ng, L.wsc, selbits);
     }
     round++;
     __syncthreads();  // the emit's bitmap and table reads are done before the next round clears them
+  }
+}
+
+// The items of an M launch: a workgroup per item (ctr null: items blockIdx.x, + gridDim.x, ...), or a grid
+// of resident workgroups that take the next item from a counter when they finish one (ctr: zeroed by
+// k_pm_init), so no slot waits for a workgroup launch between items and the largest items still go first
+#if defined(SYZ_SMIN_DYN) || defined(SYZ_SMIN_PERSIST) || defined(SYZ_SMIN_IPW_D) || defined(SYZ_SMIN_IPW_H) || \
+    defined(SYZ_SMIN_IPW_P)
+#define SYZ_SMIN_LOOP 1
+#else
+#define SYZ_SMIN_LOOP 0  // one item per workgroup: no item loop in the kernels (the loop costs registers)
+#endif
+template <class Fn>
+__device__ __forceinline__ void m_items(uint32_t nitems, uint32_t* ctr, Fn fn) {
+  if (!SYZ_SMIN_LOOP) {
+    (void)ctr;
+    if (blockIdx.x < nitems) fn(blockIdx.x);
+    return;
+  }
+  if (!ctr) {
+    for (uint32_t i = blockIdx.x; i < nitems; i += gridDim.x) {
+      fn(i);
+      __syncthreads();
+    }
+    return;
+  }
+  __shared__ uint32_t next;
+  for (;;) {
+    if (threadIdx.x == 0) next = atomicAdd(ctr, 1u);
+    __syncthreads();
+    const uint32_t i = next;
+    if (i >= nitems) break;
+    fn(i);
+    __syncthreads();  // (and every thread has read `next` before thread 0 writes it again)
   }
 }
 
@@ -392,10 +475,12 @@ __global__ __launch_bounds__(1024) SYZ_SMIN_OCC void k_smin_direct(const PItem* 
                                                                    const uint32_t* __restrict__ elems,
                                                                    const uint32_t* __restrict__ rank_of_member,
                                                                    const uint64_t* gstart, uint32_t* selbits,
-                                                                   const int* gate) {
+                                                                   const int* gate, uint32_t nitems, uint32_t* ctr) {
   if (*gate) return;  // a speculated step on a plan that does not fit this layout (k_gpack)
   __shared__ SminLds L;
-  smin_direct(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, L);
+  m_items(nitems, ctr, [&](uint32_t i) {
+    smin_direct(items[i], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, L);
+  });
 }
 
 // (one launch for a class's three table kinds measured no better and spills: M is throughput-bound)
@@ -404,16 +489,57 @@ template <bool PACKED>
 __global__ __launch_bounds__(PACKED ? PK_BLOCK : 1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_smin_hash(
     const PItem* items, const SGroup* sg, const uint32_t* gslab, const uint64_t* gebase, const uint32_t* D,
     const PSlab* slabs, const uint32_t* __restrict__ elems, const uint32_t* __restrict__ rank_of_member,
-    const uint64_t* gstart, uint32_t* selbits, const int* gate) {
+    const uint64_t* gstart, uint32_t* selbits, const int* gate, uint32_t nitems, uint32_t* ctr) {
   if (*gate) return;  // (see k_smin_direct)
   if constexpr (PACKED) {
     __shared__ SminPkLds L;
-    smin_hash<true, PK_BLOCK>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits,
-                              L);
+    m_items(nitems, ctr, [&](uint32_t i) {
+      smin_hash<true, PK_BLOCK>(items[i], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, L);
+    });
   } else {
     __shared__ SminLds L;
-    smin_hash<false, 1024>(items[blockIdx.x], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, L);
+    m_items(nitems, ctr, [&](uint32_t i) {
+      smin_hash<false, 1024>(items[i], sg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, L);
+    });
   }
+}
+
+// Items per workgroup of the M kernels: a workgroup takes items i, i + grid, i + 2 grid, ... so the
+// launch dispatches nitems / IPW workgroups (a 1024-thread, 79 KB-LDS workgroup per item made the direct
+// kernel's dispatch its bound, r06). SYZ_SMIN_PERSIST=1: a grid of resident workgroups instead (per CU:
+// two direct / hashed, four packed), which starves the kernels beside it.
+#ifndef SYZ_SMIN_PERSIST
+#define SYZ_SMIN_PERSIST 0
+#endif
+#ifndef SYZ_SMIN_IPW_D
+#define SYZ_SMIN_IPW_D 1
+#endif
+#ifndef SYZ_SMIN_IPW_H
+#define SYZ_SMIN_IPW_H 1
+#endif
+#ifndef SYZ_SMIN_IPW_P
+#define SYZ_SMIN_IPW_P 1
+#endif
+static unsigned m_grid(size_t nitems, unsigned per_cu, unsigned ipw) {
+  Context& c = ctx();
+  if (SYZ_SMIN_PERSIST && !c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+  const unsigned cap = SYZ_SMIN_PERSIST ? (unsigned)std::max(1, c.ncu) * per_cu : 0xFFFFFFFFu;
+  return (unsigned)std::min<size_t>((nitems + ipw - 1) / ipw, cap);
+}
+// SYZ_SMIN_DYN: the launches that take their items from a counter (bit 0 / 1: direct small / big, 2 / 3:
+// packed small / big, 4 / 5: hashed small / big), on SYZ_SMIN_DYN_CU resident workgroups per CU x their
+// per-CU capacity
+#ifndef SYZ_SMIN_DYN
+#define SYZ_SMIN_DYN 0
+#endif
+#ifndef SYZ_SMIN_DYN_CU
+#define SYZ_SMIN_DYN_CU 1.0
+#endif
+static unsigned m_dyn_grid(size_t nitems, unsigned per_cu) {
+  Context& c = ctx();
+  if (!c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+  const unsigned cap = std::max(1u, (unsigned)(SYZ_SMIN_DYN_CU * per_cu * std::max(1, c.ncu)));
+  return (unsigned)std::min<size_t>(nitems, cap);
 }
 
 // ---- outputs: the group-major kept list in selection order ----------------------------------------
@@ -700,6 +826,7 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
   hipStream_t pq = launch_p(a, PC, SJ, members, mlen, mpos, gstart, sbeg, err);
   ht.mark("slab_build");
   const int* gate = err + 2;
+  uint32_t* mctr = sc.get<uint32_t>("pm_mctr", 16);
   const PSlab* slabs = SJ.slabs;
   const uint32_t* gslab = SJ.gslab;
   const uint64_t* gebase = SJ.gebase;
@@ -726,22 +853,27 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
     if (!nd && !nh && !np) return;
     if (SYZ_SL_NOD) return;  // (timing variant without D rows: M would walk garbage)
     SYZ_HIP(hipStreamWaitEvent(q, big ? c.ev_sct[0] : c.ev_psmall, 0));
+    const bool dd = (SYZ_SMIN_DYN >> big) & 1, dp = (SYZ_SMIN_DYN >> (2 + big)) & 1,
+               dh = (SYZ_SMIN_DYN >> (4 + big)) & 1;
     if (nd) {
       ProfScope pk("k_pmin_direct", q, 4 * item_pcs[big][PMODE_DIRECT]);
-      k_smin_direct<<<(unsigned)nd, 1024, 0, q>>>(ditems + ifirst[big][PMODE_DIRECT], dsg, gslab, gebase, D, slabs,
-                                                   elems, rank_of_member, gstart, selbits, gate);
+      k_smin_direct<<<dd ? m_dyn_grid(nd, 2) : m_grid(nd, 2, SYZ_SMIN_IPW_D), 1024, 0, q>>>(
+          ditems + ifirst[big][PMODE_DIRECT], dsg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, gate,
+          (uint32_t)nd, dd ? mctr + 2 * big : nullptr);
       SYZ_LAUNCHED();
     }
     if (nh) {
       ProfScope pk("k_pmin_hash", q, 4 * item_pcs[big][PMODE_HASH]);
-      k_smin_hash<false><<<(unsigned)nh, 1024, 0, q>>>(ditems + ifirst[big][PMODE_HASH], dsg, gslab, gebase, D, slabs,
-                                                        elems, rank_of_member, gstart, selbits, gate);
+      k_smin_hash<false><<<dh ? m_dyn_grid(nh, 2) : m_grid(nh, 2, SYZ_SMIN_IPW_H), 1024, 0, q>>>(
+          ditems + ifirst[big][PMODE_HASH], dsg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits, gate,
+          (uint32_t)nh, dh ? mctr + 4 + 2 * big : nullptr);
       SYZ_LAUNCHED();
     }
     if (np) {  // (on a stream of their own beside the others: slower, the process has 4 hardware queues)
       ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
-      k_smin_hash<true><<<(unsigned)np, PK_BLOCK, 0, q>>>(ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs,
-                                                       elems, rank_of_member, gstart, selbits, gate);
+      k_smin_hash<true><<<dp ? m_dyn_grid(np, 4) : m_grid(np, 4, SYZ_SMIN_IPW_P), PK_BLOCK, 0, q>>>(
+          ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits,
+          gate, (uint32_t)np, dp ? mctr + 8 + 2 * big : nullptr);
       SYZ_LAUNCHED();
     }
   };
@@ -855,7 +987,8 @@ static bool begin_once(MinJob& J, const RawMinArgs& a, const uint32_t* exact_spa
                     spec_parts_match(J, a);
   J.nospec = false;
   const uint64_t* exp = spec ? reinterpret_cast<const uint64_t*>(J.pcache->dstage.p + J.pcache->o_exp) : nullptr;
-  k_pm_init<<<grid_for(G + 1, 256, 64), 256, 0, s>>>(err, gpcs, G, span, mlmax);
+  k_pm_init<<<grid_for(std::max<uint32_t>(G + 1, 16), 256, 64), 256, 0, s>>>(err, gpcs, G, span, mlmax,
+                                                                             sc.get<uint32_t>("pm_mctr", 16));
   SYZ_LAUNCHED();
   uint32_t* krange = nullptr;
   if (a.key_lo) {

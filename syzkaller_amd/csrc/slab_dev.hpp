@@ -159,6 +159,12 @@ static_assert(5 * SL_MEMB + SL_MEMB / 4 <= 64 * SL_TILES, "the member table live
 #define SYZ_SL_RUNS 1
 #endif
 constexpr bool SL_RUNS = SYZ_SL_RUNS != 0;
+#ifndef SYZ_SL_SPW
+#define SYZ_SL_SPW 1  // slabs per P workgroup (c, c + grid, ...): fewer workgroups to dispatch
+#endif
+#ifndef SYZ_SL_PERSIST
+#define SYZ_SL_PERSIST 0  // P as a grid of resident workgroups (two per CU) walking the slabs
+#endif
 #ifndef SYZ_SL_NOD
 #define SYZ_SL_NOD 0  // timing experiment only (results wrong when 1): P without its D-row stores
 #endif
@@ -207,8 +213,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   // a step speculated on a plan that does not fit the layout read back (panels.hip k_gpack)
   if (gate && *gate) return;
   const uint64_t nsl = *nslab;
-  const uint64_t c = blockIdx.x;
-  if (c >= nsl) return;
+  // one slab per workgroup, or (SYZ_SL_PERSIST) a grid of resident workgroups walking the slabs
+#if SYZ_SL_PERSIST
+  for (uint64_t c = blockIdx.x; c < nsl; c += gridDim.x) {
+#else
+  // SYZ_SL_SPW slabs per workgroup, as straight-line copies of the body (a loop spills, r06)
+#pragma unroll
+  for (uint32_t q_ = 0; q_ < SYZ_SL_SPW; q_++) {
+    const uint64_t c = (uint64_t)blockIdx.x + (uint64_t)q_ * gridDim.x;
+    if (c >= nsl) return;
+    if (q_) __syncthreads();  // the staging buffer is free for the next slab
+#endif
+  [&]() {  // (a `return` below ends this slab)
   const int wv = threadIdx.x >> 6;
   const unsigned lane = __lane_id();
   const PSlab sl = slabs[c];
@@ -410,6 +426,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   SL_STAT_ADD(5, q4 - q3);
   SL_STAT_ADD(6, q5 - q4);
   SL_STAT_ADD(7, q6 - q5);
+  }();
+#if SYZ_SL_PERSIST
+  __syncthreads();  // the staging buffer is free for the next slab
+#endif
+  }
 }
 
 // P's launch: one workgroup per slab (a bound; slabs past nslab return), the staging sized for the
@@ -434,7 +455,15 @@ inline void launch_slab(uint64_t nslabs, uint32_t Wmax, hipStream_t s, const uin
     while (bytes > cur && !rd.compare_exchange_weak(cur, bytes)) {
     }
   }
-  k_slab<SL_BLOCK, SL_TPW, NOV><<<(unsigned)nslabs, SL_BLOCK, bytes, s>>>(pcs, off, members, mlen, tpos, sbeg, slabs,
+  unsigned grid = (unsigned)((nslabs + SYZ_SL_SPW - 1) / SYZ_SL_SPW);
+#if SYZ_SL_PERSIST
+  {
+    int ncu = 0;
+    SYZ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    grid = (unsigned)std::min<uint64_t>(nslabs, 2ull * (uint64_t)std::max(1, ncu));
+  }
+#endif
+  k_slab<SL_BLOCK, SL_TPW, NOV><<<grid, SL_BLOCK, bytes, s>>>(pcs, off, members, mlen, tpos, sbeg, slabs,
                                                                          nslab, sg, gebase, lo, elems, D, err, Wmax,
                                                                          ecap, wtot, ns, cls, gate);
   SYZ_LAUNCHED();

@@ -12,7 +12,7 @@ cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d $OUT/$C -o run -- \
     python3 $R/bench.py --steps 3 --warmup 1 --cpu-baseline 0 --profile 0 --novelty 0 --text 0 \
-      --hub 0 --analytics 0 --append 0 --store 0 --cooccurrence 0 --setops 0 --canonicalize 0 > $OUT/$C.log 2>&1
+      --hub 0 --analytics 0 --append 0 --store 0 --cooccurrence 0 --setops 0 --canonicalize 0 --layout-change 0 > $OUT/$C.log 2>&1
   rc=$?; echo "$C rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python3 $R/tools/pmc_traffic.py $OUT $OUT/pmc_traffic.json
