@@ -188,6 +188,43 @@ def test_setop_batch_repeated_values_take_rank_path():
             assert np.array_equal(got[op][i], oracle.setop(op, a, b)), (op, i)
 
 
+def test_setop_batch_many_tiles_and_capacity():
+    # ~40K merge tiles in one batch (the tiles' output offsets come from a look-back over all of them),
+    # repeated twice (the look-back words are reused across calls), then the same batch with an output
+    # capacity one short of the total: ECAPACITY, and no store past the buffer (a guard word after it)
+    import torch
+    c = synth.corpus(0x5EED00C7, 60_000, 31, 400_000)
+    rnd = np.random.default_rng(9)
+    a_list = [c.cover(i) for i in range(c.n)]
+    b_list = [x[rnd.random(x.size) > 0.3] for x in a_list]
+    a, aoff = cover.to_csr(a_list)
+    b, boff = cover.to_csr(b_list)
+    assert (a.size + b.size) // 1024 > 20_000
+
+    def t(x):
+        view = {np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+        return torch.from_numpy(np.ascontiguousarray(x).view(view.get(x.dtype, x.dtype))).to("cuda:0")
+    da, dao, db, dbo = t(a), t(aoff), t(b), t(boff)
+    aoff64, boff64 = aoff.astype(np.int64), boff.astype(np.int64)
+    for op in SETOPS:
+        for _ in range(2):
+            cap = a.size + b.size
+            out = torch.zeros(cap + 1, dtype=torch.int32, device="cuda:0")
+            ooff = torch.zeros(c.n + 1, dtype=torch.int64, device="cuda:0")
+            tot = cover.SetOpBatchDev(op, da, dao, a.size, db, dbo, b.size, c.n, out, cap, ooff)
+            o = out.cpu().numpy().view(np.uint32)
+            oo = ooff.cpu().numpy().view(np.uint64)
+            want = [oracle.setop(op, a[aoff64[i]:aoff64[i + 1]], b[boff64[i]:boff64[i + 1]]) for i in range(c.n)]
+            assert tot == sum(w.size for w in want) == int(oo[-1])
+            assert np.array_equal(o[:tot], np.concatenate(want)), op
+        guard = torch.full((tot + 8,), -7, dtype=torch.int32, device="cuda:0")
+        with pytest.raises(_lib.SyzGpuError) as e:
+            cover.SetOpBatchDev(op, da, dao, a.size, db, dbo, b.size, c.n, guard, tot - 1, ooff)
+        assert e.value.code == _lib.ECAPACITY
+        g = guard.cpu().numpy()
+        assert (g[tot - 1:] == -7).all(), op
+
+
 def test_setop_rejects_unsorted():
     with pytest.raises(_lib.SyzGpuError) as e:
         cover.Union([3, 1], [2])
