@@ -80,9 +80,9 @@ def parse():
     return ap.parse_args()
 
 
-# the round's committed rocprofv3 kernel summary of this bench command (tools/gpu_final5.sh): its top
-# kernel by total GPU time names the roofline kernel
-ROCPROF_STATS = os.path.join(ROOT, "profiles", "r05_kernel_stats.csv")
+# the round's committed rocprofv3 kernel summary of this bench command (tools/gpu_final6.sh): its top
+# byte-modelled kernel by total GPU time names the roofline kernel
+ROCPROF_STATS = os.path.join(ROOT, "profiles", "r06_kernel_stats.csv")
 # rocprofv3 kernel name -> the library's profiling scope around that kernel; the same
 # names key profiles/pmc_traffic.json (tools/pmc_traffic.py)
 ROCPROF_SCOPE = [("k_slab<", "k_slab"), ("k_smin_direct", "k_pmin_direct"), ("k_smin_hash<false>", "k_pmin_hash"),
@@ -105,7 +105,9 @@ def workload_key(args, world):
 
 def rocprof_top(path=ROCPROF_STATS, workload=PROFILED_WORKLOAD):
     """(scope, kernel name) of the first row of the committed rocprofv3 --stats summary (rows are
-    sorted by total duration), or None; None too when the line's workload is not the one profiled."""
+    sorted by total duration) that is a byte-modelled kernel (ROCPROF_SCOPE), or None; None too when the
+    line's workload is not the one profiled. Rows above it are latency-bound kernels without a byte model
+    (round 6: the Go sort's LDS sorter, whose launches last long beside the transpose)."""
     import csv
     if workload != PROFILED_WORKLOAD:
         return None
@@ -115,10 +117,11 @@ def rocprof_top(path=ROCPROF_STATS, workload=PROFILED_WORKLOAD):
         return None
     if not rows:
         return None
-    top = rows[0]["Name"]
-    for pat, scope in ROCPROF_SCOPE:
-        if pat in top:
-            return scope, top
+    for row in rows:
+        top = row["Name"]
+        for pat, scope in ROCPROF_SCOPE:
+            if pat in top:
+                return scope, top
     return None
 
 
@@ -381,7 +384,7 @@ def main():
             roof["dominant_kernel_overall"] = max(kern.items(), key=lambda kv: kv[1]["ms"])[0]
             roof["profiled_workload"] = wkey if wkey == PROFILED_WORKLOAD else None
             top = rocprof_top(workload=wkey)
-            roof["selection"] = (("the top kernel of the committed rocprofv3 summary %s (%s)"
+            roof["selection"] = (("the top byte-modelled kernel of the committed rocprofv3 summary %s (%s)"
                                   % (os.path.relpath(ROCPROF_STATS, ROOT), top[1][:60])) if top and top[0] == roof_kernel
                                  else "the byte-modelled kernel with the most time in the serialized per-kernel pass")
             roof["selection"] += "; achieved from its HIP events in the (concurrent) timed region"
