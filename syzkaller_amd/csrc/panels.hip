@@ -195,10 +195,11 @@ __device__ __forceinline__ uint32_t hslot(uint32_t o) { return (o * 0x9E3779B1u)
 #endif
 #define SMIN_WALK(U, it, sg, gslab, gebase, D, slabs, elems, rom, wsc, red64, f) \
   for_slab_window<U, SYZ_SMIN_IDENT>(it, sg, gslab, gebase, D, slabs, elems, rom, wsc, red64, f)
-// the direct tables' walk: every wave on its own runs (slab_dev.hpp for_slab_window_w); SYZ_SMIN_WW=0: the
-// workgroup form
+// the direct tables' walk: the workgroup form (for_slab_window); SYZ_SMIN_WW=1: every wave on its own
+// runs (slab_dev.hpp for_slab_window_w) — fewer cycles per workgroup, the same time at config 4 (2.559
+// vs 2.535 ms) and 1 ms slower at config 5 (17.80 vs 16.76 ms, profiles/r06_ab/r06_ww5_pm.log): off
 #ifndef SYZ_SMIN_WW
-#define SYZ_SMIN_WW 1
+#define SYZ_SMIN_WW 0
 #endif
 #ifndef SYZ_SMIN_NBW
 #define SYZ_SMIN_NBW 16
