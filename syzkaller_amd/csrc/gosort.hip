@@ -50,9 +50,12 @@ constexpr uint32_t T_SEG = GS_T_SEG;  // largest segment sorted in LDS
 #ifndef GS_T_CHILD_DEFAULT
 #define GS_T_CHILD_DEFAULT T_SEG
 #endif
-constexpr int LS_BLOCK = 1024;     // LDS workgroup (16 waves: the wave sorter runs 16 segments at once)
+#ifndef SYZ_LS_BLOCK
+#define SYZ_LS_BLOCK 1024
+#endif
+constexpr int LS_BLOCK = SYZ_LS_BLOCK;  // LDS workgroup (1024: 16 waves, the wave sorter runs 16 segments at once)
 constexpr int LS_ITEMS = T_SEG / LS_BLOCK;  // elements per thread chunk
-constexpr int LS_ISH = 3;                   // log2(LS_ITEMS)
+constexpr int LS_ISH = LS_ITEMS == 8 ? 3 : LS_ITEMS == 16 ? 4 : -1;  // log2(LS_ITEMS)
 static_assert((1 << LS_ISH) == LS_ITEMS, "LS_ISH");
 constexpr int LS_SH = 13;  // local index bits of the packed u32 LDS element (T_SEG = 2^13)
 static_assert((1u << LS_SH) == T_SEG, "LS_SH");
