@@ -58,6 +58,44 @@ __device__ __forceinline__ uint32_t lane_prev(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x138, 0xF, 0xF, false);
 }
 
+// Once-read streams with the non-temporal cache policy, so they do not push the data that is re-read
+// (the Go sort's keys, M's rank array and D rows) out of L2: P's cover loads and element stores
+// (SYZ_SL_NTL / SYZ_SL_NTS, on: `k_slab` 1.03 -> 1.00 ms alone, step 2.54-2.55 -> 2.52 ms); M's element
+// loads (SYZ_M_NT, off: M direct 0.96 -> 1.01 ms, step 2.61 ms), profiles/r06_ab/r06_nt_pm.log
+#ifndef SYZ_SL_NTL
+#define SYZ_SL_NTL 1
+#endif
+#ifndef SYZ_SL_NTS
+#define SYZ_SL_NTS 1
+#endif
+#ifndef SYZ_M_NT
+#define SYZ_M_NT 0
+#endif
+typedef unsigned syz_v4u __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint32_t ld_once(const uint32_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ uint4 ld_once4(const uint4* p) {
+  if constexpr (NT) {
+    const syz_v4u v = __builtin_nontemporal_load(reinterpret_cast<const syz_v4u*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st_once4(uint4* p, uint4 x) {
+  if constexpr (NT) {
+    syz_v4u v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<syz_v4u*>(p));
+  } else {
+    *p = x;
+  }
+}
+
 // ---- slab planning on the device ------------------------------------------------------------------
 // tiles per member, and the member lengths with them (one scan gives mpos and tpos)
 struct TilesFn {
@@ -297,7 +335,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)ahi, k) << 32) |
                           (uint32_t)__builtin_amdgcn_readlane((int)alo, k);
     const uint32_t cnt = z & 0x7Fu;
-    v[k] = reinterpret_cast<const uint32_t*>((uintptr_t)base)[lane < cnt ? lane : 0u];
+    v[k] = ld_once<SYZ_SL_NTL != 0>(reinterpret_cast<const uint32_t*>((uintptr_t)base) + (lane < cnt ? lane : 0u));
     if ((k & 7) == 7) __builtin_amdgcn_sched_barrier(0);
   }
   int bad = 0;  // err bits this lane saw
@@ -415,7 +453,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   {
     uint4* g4 = reinterpret_cast<uint4*>(elems + sl.elem);
     const uint4* o4 = reinterpret_cast<const uint4*>(obuf);
-    for (uint32_t q = threadIdx.x; q < total / 4; q += BLOCK) g4[q] = o4[q];
+    for (uint32_t q = threadIdx.x; q < total / 4; q += BLOCK) st_once4<SYZ_SL_NTS != 0>(g4 + q, o4[q]);
   }
   [[maybe_unused]] const uint64_t q6 = SM_T();
   SL_STAT_ADD(0, 1);
@@ -563,7 +601,7 @@ __device__ __forceinline__ void for_slab_window(const PItem it, const SGroup* __
           mb_[u] = rmb[rr];
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) ev[u] = gel4[vi[u]];
+        for (int u = 0; u < U; u++) ev[u] = ld_once4<SYZ_M_NT != 0>(gel4 + vi[u]);
       };
       if ((uint32_t)wv < nblk) prep_load(wv, mbr, ok);
       for (uint32_t j0 = wv; j0 < nblk; j0 += step) {
@@ -696,7 +734,7 @@ __device__ __forceinline__ void for_slab_window_w(const PItem it, const SGroup* 
           mb_[u] = rmb[rr];
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) ev[u] = gel4[vi[u]];
+        for (int u = 0; u < U; u++) ev[u] = ld_once4<SYZ_M_NT != 0>(gel4 + vi[u]);
       };
       prep_load(0, mbr, ok);
       for (uint32_t j0 = 0; j0 < nblk; j0 += U) {
