@@ -346,6 +346,10 @@ static MinJob& lane_job() {
   return *c.own_job;
 }
 
+// the lane of this thread's last one-call minimize (syzgpu_minimize_grouped_fetch runs there)
+static thread_local Context* t_min_lane = nullptr;
+static thread_local uint64_t t_min_gen = 0;
+
 // one call: begin + outputs on the lane's own job (remembered for syzgpu_minimize_grouped_fetch)
 void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32_t* group, const uint16_t* prog_len,
                           size_t n, uint32_t G, int32_t C, uint8_t* selected, int64_t* len_hist, int64_t* out_idx,
@@ -366,6 +370,8 @@ void minimize_grouped_dev(const uint32_t* pcs, const uint64_t* off, const uint32
   minimize_raw_end(J, e);
   c.last_job = &J;
   c.last_thread = std::this_thread::get_id();
+  t_min_lane = &c;
+  t_min_gen = c.gen;
 }
 
 void minimize_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n, uint32_t G) {
@@ -405,6 +411,7 @@ int syzgpu_minimize_grouped_ordered_dev(const uint32_t* pcs, const uint64_t* off
 }
 
 int syzgpu_minimize_grouped_fetch(int64_t* out_idx, uint64_t* group_out_off, size_t n, uint32_t ngroups) {
+  want_lane(t_min_lane, t_min_gen);
   SYZ_API_BODY({
     if (!group_out_off) fail(SYZGPU_EINVAL, "null pointer");
     minimize_fetch(out_idx, group_out_off, n, ngroups);

@@ -848,6 +848,7 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
   // ---- Go-sort ranks, then M per class as soon as its own sort and P are done ----
   uint32_t* perm = sc.get<uint32_t>("mz_perm", n + 1);
   SYZ_HIP(hipMemsetAsync(selbits, 0, (n / 32 + 2) * 4, s));
+  GosortPlan& P = *J.plan;
   auto run_m = [&](hipStream_t q, int big) {
     ProfScope ps(big ? "m_big" : "m_small", q, 0);
     const size_t nd = icount[big][PMODE_DIRECT], nh = icount[big][PMODE_HASH], np = icount[big][PMODE_PACKED];
@@ -870,15 +871,28 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
           (uint32_t)nh, dh ? mctr + 4 + 2 * big : nullptr);
       SYZ_LAUNCHED();
     }
-    if (np) {  // (on a stream of their own beside the others: slower, the process has 4 hardware queues)
-      ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
-      k_smin_hash<true><<<dp ? m_dyn_grid(np, 4) : m_grid(np, 4, SYZ_SMIN_IPW_P), PK_BLOCK, 0, q>>>(
+    // the packed tables on a stream of their own beside the others: slower when the big groups' M runs
+    // too (the process has 4 hardware queues), but with no big groups the side stream is idle and the
+    // two small launches overlap (config 1)
+    hipStream_t qp = q;
+    if (np && (nd || nh) && !P.nbig && !big) {
+      ensure_side(c);
+      qp = c.side;
+      SYZ_HIP(hipEventRecord(c.ev_mfork, q));
+      SYZ_HIP(hipStreamWaitEvent(qp, c.ev_mfork, 0));
+    }
+    if (np) {
+      ProfScope pk("k_pmin_packed", qp, 4 * item_pcs[big][PMODE_PACKED]);
+      k_smin_hash<true><<<dp ? m_dyn_grid(np, 4) : m_grid(np, 4, SYZ_SMIN_IPW_P), PK_BLOCK, 0, qp>>>(
           ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits,
           gate, (uint32_t)np, dp ? mctr + 8 + 2 * big : nullptr);
       SYZ_LAUNCHED();
     }
+    if (qp != q) {
+      SYZ_HIP(hipEventRecord(c.ev_mjoin, qp));
+      SYZ_HIP(hipStreamWaitEvent(q, c.ev_mjoin, 0));
+    }
   };
-  GosortPlan& P = *J.plan;
   P.may_bounce = J.may_bounce;
   auto small_done = [&](hipStream_t q) {
     if (P.npacks) ranks_packs(el, perm, P, members, rank_of_member, ent_of_rank, q);

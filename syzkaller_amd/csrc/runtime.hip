@@ -71,6 +71,13 @@ static thread_local Context* t_lane = nullptr;  // held for the current API call
 static thread_local int t_depth = 0;
 static thread_local Context* t_last = nullptr;   // affinity: the lane this thread used last
 static thread_local uint64_t t_last_gen = 0;
+static thread_local Context* t_want = nullptr;    // want_lane: the next call runs on this lane (waits for it)
+static thread_local uint64_t t_want_gen = 0;
+
+void want_lane(Context* c, uint64_t gen) {  // (c is not dereferenced: it may be gone)
+  t_want = c;
+  t_want_gen = gen;
+}
 
 static size_t max_lanes() {  // per device
   static const size_t v = [] {
@@ -126,13 +133,24 @@ LaneGuard::LaneGuard(int device) {
   try {
     if (g_device < 0) pick_device(device >= 0 ? device : 0);
     const int dev = device >= 0 ? device : g_device;
+    // a requested lane (want_lane) that still exists: wait for it, whatever else is free
+    Context* const want = t_want && t_want_gen == g_gen ? t_want : nullptr;
+    t_want = nullptr;
     for (;;) {
-      size_t pick = g_lanes.size(), mine = 0;
+      size_t pick = g_lanes.size(), mine = 0, wanted = g_lanes.size();
       for (size_t i = 0; i < g_lanes.size(); i++)
         if (g_lanes[i]->device == dev) {
           mine++;
           if (!g_busy[i] && g_lanes[i] == t_last && t_last_gen == g_gen) pick = i;
+          if (g_lanes[i] == want) wanted = i;
         }
+      if (wanted < g_lanes.size()) {
+        if (g_busy[wanted]) {
+          g_cv.wait(lk);
+          continue;
+        }
+        pick = wanted;
+      }
       if (pick == g_lanes.size())
         for (size_t i = 0; i < g_lanes.size(); i++)
           if (!g_busy[i] && g_lanes[i]->device == dev) {
