@@ -15,8 +15,9 @@
  * holds a lane (streams, scratch memory, captured graphs) for its duration; concurrent calls get
  * different lanes (up to SYZGPU_LANES, default 8; more callers wait) and run concurrently on the
  * device. Handles (stores, jobs, signature sets) serialise the calls made on the same handle.
- * syzgpu_minimize_grouped_fetch reads the calling thread's last syzgpu_minimize_grouped_dev; a
- * Go caller that cannot pin its goroutine to a thread (runtime.LockOSThread) uses a job handle or
+ * syzgpu_minimize_grouped_fetch reads the calling thread's last syzgpu_minimize_grouped_dev (it runs on
+ * the lane that minimize ran on, waiting for it while another call holds it; if another thread's
+ * minimize ran there in between, it returns SYZGPU_EINVAL); a Go caller that cannot pin its goroutine to a thread (runtime.LockOSThread) uses a job handle or
  * syzgpu_minimize_grouped_ordered_dev, which return everything per call.
  */
 #ifndef SYZGPU_H

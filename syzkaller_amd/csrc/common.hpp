@@ -107,7 +107,6 @@ struct Context {
   std::shared_ptr<MinJob> own_job;  // the lane's job for the one-call entry points
   hipStream_t side = nullptr;         // second stream: independent work overlapped with the main one
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_mfork = nullptr, ev_mjoin = nullptr;  // the raw Minimize's M split over two streams
   hipStream_t cap = nullptr;           // capture stream for the gosort round graph
   hipGraphExec_t gl_exec[2][4] = {};  // [start parity][rounds - 1]: global-round graphs
   std::vector<const void*> gl_key;
@@ -137,8 +136,6 @@ inline void ensure_side(Context& c) {
   SYZ_HIP(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
   SYZ_HIP(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
   SYZ_HIP(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
-  SYZ_HIP(hipEventCreateWithFlags(&c.ev_mfork, hipEventDisableTiming));
-  SYZ_HIP(hipEventCreateWithFlags(&c.ev_mjoin, hipEventDisableTiming));
 }
 // The calling thread's next (outermost) API call runs on lane c (of generation gen), waiting for it if another thread holds
 // it (a lane that no longer exists is ignored): for entries whose result lives on the lane of an earlier

@@ -871,26 +871,15 @@ static void launch_step(MinJob& J, const RawMinArgs& a, const uint32_t* members,
           (uint32_t)nh, dh ? mctr + 4 + 2 * big : nullptr);
       SYZ_LAUNCHED();
     }
-    // the packed tables on a stream of their own beside the others: slower when the big groups' M runs
-    // too (the process has 4 hardware queues), but with no big groups the side stream is idle and the
-    // two small launches overlap (config 1)
-    hipStream_t qp = q;
-    if (np && (nd || nh) && !P.nbig && !big) {
-      ensure_side(c);
-      qp = c.side;
-      SYZ_HIP(hipEventRecord(c.ev_mfork, q));
-      SYZ_HIP(hipStreamWaitEvent(qp, c.ev_mfork, 0));
-    }
+    // (the packed tables on a stream of their own beside the others: slower with the big groups' M
+    // running too, the process has 4 hardware queues; and with no big groups, config 1, 0.387 against
+    // 0.353 ms: the fork and join cost more than the two small launches overlap)
     if (np) {
-      ProfScope pk("k_pmin_packed", qp, 4 * item_pcs[big][PMODE_PACKED]);
-      k_smin_hash<true><<<dp ? m_dyn_grid(np, 4) : m_grid(np, 4, SYZ_SMIN_IPW_P), PK_BLOCK, 0, qp>>>(
+      ProfScope pk("k_pmin_packed", q, 4 * item_pcs[big][PMODE_PACKED]);
+      k_smin_hash<true><<<dp ? m_dyn_grid(np, 4) : m_grid(np, 4, SYZ_SMIN_IPW_P), PK_BLOCK, 0, q>>>(
           ditems + ifirst[big][PMODE_PACKED], dsg, gslab, gebase, D, slabs, elems, rank_of_member, gstart, selbits,
           gate, (uint32_t)np, dp ? mctr + 8 + 2 * big : nullptr);
       SYZ_LAUNCHED();
-    }
-    if (qp != q) {
-      SYZ_HIP(hipEventRecord(c.ev_mjoin, qp));
-      SYZ_HIP(hipStreamWaitEvent(q, c.ev_mjoin, 0));
     }
   };
   P.may_bounce = J.may_bounce;
