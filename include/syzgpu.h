@@ -106,6 +106,16 @@ int syzgpu_setop_batch_dev(int op, const uint32_t* a, const uint64_t* a_off, uin
 int syzgpu_minimize_grouped(const uint32_t* pcs, const uint64_t* off, const uint32_t* group,
                             size_t n, uint32_t ngroups, int64_t* out_idx, uint64_t* group_out_off);
 
+/* Minimize sorts each call group with Go's unstable sort.Sort (cover/cover.go:113), so equal cover
+ * lengths keep the tie order of the Go release the manager was built with. Two leaf forms of its
+ * quickSort are restated: 12 (`for b-a > 12`, then a gap-6 shell pass and insertionSort; the default)
+ * and 7 (`for b-a > 7`, then insertionSort alone). Which one the reference's Go release used is not
+ * pinned by anything in the reference (it asks for Go >= 1.7 and holds no tie of more than three equal
+ * lengths in its tests). Process-wide; takes effect at the next minimize. No device work: callable
+ * before syzgpu_init. SYZGPU_EINVAL for another value. */
+int syzgpu_set_go_sort_leaf(int leaf);
+int syzgpu_go_sort_leaf(void);  /* the current form: 12 or 7 */
+
 /* syz-fuzzer/fuzzer.go:446-470 execute (and syz-manager/manager.go:609-616 NewInput) over a batch:
  * covers are processed in order; cover k of group g is new iff (cov \ maxCover[g]) \ flakes != {},
  * and then maxCover[g] = Union(maxCover[g], that difference). mc/mc_off is the CSR of the ngroups

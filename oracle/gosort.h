@@ -11,6 +11,9 @@
  * Algorithm restated from the published Go sources of that era (sort/sort.go):
  *   quickSort(data, a, b, maxDepth):   while b-a > 12 { heapSort at depth 0; doPivot; recurse on the
  *                                      smaller side }  then a gap-6 shell pass + insertionSort.
+ *   Leaf form (gosort_leaf, oracle_set_go_sort_leaf): 12 as above (the default), or 7: `while b-a > 7`
+ *   and insertionSort alone. The reference pins neither (it asks for Go >= 1.7; its tests hold no tie of
+ *   more than three equal keys), so both are restated, as in the GPU sort (syzgpu_set_go_sort_leaf).
  *   doPivot: Tukey ninther for hi-lo > 40, medianOfThree(lo, m, hi-1), Hoare-style partition with
  *            the "protect" duplicate pass, pivot swapped into the middle.
  *   maxDepth(n) = 2 * ceil(lg(n+1)).
@@ -25,6 +28,8 @@
  */
 #ifndef SYZ_ORACLE_GOSORT_H
 #define SYZ_ORACLE_GOSORT_H
+
+static int gosort_leaf = 12; /* 12 or 7, see above */
 
 #define GOSORT_DEFINE(name, T, LESS)                                                             \
   static inline int name##_less(T* d, long i, long j) { return (LESS(d[i], d[j])); }            \
@@ -123,7 +128,7 @@
     *midhi = c;                                                                                 \
   }                                                                                             \
   static void name##_quick(T* d, long a, long b, int maxDepth) {                                \
-    while (b - a > 12) {                                                                        \
+    while (b - a > gosort_leaf) {                                                               \
       if (maxDepth == 0) {                                                                      \
         name##_heapsort(d, a, b);                                                               \
         return;                                                                                 \
@@ -140,8 +145,9 @@
       }                                                                                         \
     }                                                                                           \
     if (b - a > 1) {                                                                            \
-      for (long i = a + 6; i < b; i++)                                                          \
-        if (name##_less(d, i, i - 6)) name##_swap(d, i, i - 6);                                 \
+      if (gosort_leaf == 12)                                                                    \
+        for (long i = a + 6; i < b; i++)                                                        \
+          if (name##_less(d, i, i - 6)) name##_swap(d, i, i - 6);                               \
       name##_insertion(d, a, b);                                                                \
     }                                                                                           \
   }                                                                                             \

@@ -176,6 +176,13 @@ int oracle_minimize(const uint32_t* pcs, const uint64_t* off, size_t ncov, int64
   return rc;
 }
 
+/* the leaf form of the restated Go quickSort (gosort.h): 12 (default) or 7; -1 for another value */
+int oracle_set_go_sort_leaf(int leaf) {
+  if (leaf != 12 && leaf != 7) return -1;
+  gosort_leaf = leaf;
+  return 0;
+}
+
 int oracle_minimize_order(const uint64_t* lens, size_t n, int64_t* perm) {
   min_input* inputs = (min_input*)malloc((n ? n : 1) * sizeof(min_input));
   for (size_t i = 0; i < n; i++) {

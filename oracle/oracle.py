@@ -38,6 +38,7 @@ def lib():
         L.oracle_minimize_grouped.argtypes = [_u32p, _u64p, _u32p, ctypes.c_size_t, ctypes.c_uint32, _i64p,
                                               _u64p]
         L.oracle_minimize_order.argtypes = [_u64p, ctypes.c_size_t, _i64p]
+        L.oracle_set_go_sort_leaf.argtypes = [ctypes.c_int]
         L.oracle_dynamic_prio.argtypes = [_u16p, ctypes.c_size_t, ctypes.c_int32, _f32p]
         L.oracle_call_cooccurrence.argtypes = [_u16p, _u64p, ctypes.c_size_t, ctypes.c_int32,
                                                ctypes.POINTER(ctypes.c_int32)]
@@ -123,6 +124,12 @@ def minimize_grouped_mt(pcs, off, group, ngroups, nthreads):
     _check(f(_p(pcs, _u32p), _p(off, _u64p), _p(group, _u32p), n, ngroups, int(nthreads), _p(out, _i64p),
              _p(goff, _u64p)), "minimize_grouped_mt")
     return out[: int(goff[-1])].copy(), goff
+
+
+def set_go_sort_leaf(leaf):
+    """The leaf form of the restated Go quickSort: 12 (default) or 7 (gosort.h)."""
+    if lib().oracle_set_go_sort_leaf(int(leaf)) != 0:
+        raise ValueError("leaf form must be 12 or 7")
 
 
 def minimize_order(lens):

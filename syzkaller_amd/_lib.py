@@ -71,6 +71,8 @@ SIGNATURES = {
     "syzgpu_plan_split_bounds": (_c.c_int, [_vp, _vp, _vp, _sz, _c.c_uint32, _c.c_uint32, _vp]),
     "syzgpu_prio_choice_dev": (_c.c_int, [_vp, _vp, _c.c_int32, _vp, _vp, _vp, _vp, _vp]),
     "syzgpu_minimize_grouped_fetch": (_c.c_int, [_vp, _vp, _sz, _c.c_uint32]),
+    "syzgpu_set_go_sort_leaf": (_c.c_int, [_c.c_int]),
+    "syzgpu_go_sort_leaf": (_c.c_int, []),
     "syzgpu_corpus_create": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp]),
     "syzgpu_corpus_create_dev": (_c.c_int, [_vp, _vp, _vp, _vp, _sz, _c.c_uint32, _vp, _vp]),
     "syzgpu_corpus_keep": (_c.c_int, [_vp, _vp, _sz]),

@@ -81,6 +81,17 @@ def to_csr(covers):
     return np.ascontiguousarray(pcs, dtype=np.uint32), off
 
 
+def SetGoSortLeaf(leaf):
+    """The leaf form of the restated Go quickSort that Minimize's tie order follows (cover.go:113):
+    12 (the default: `for b-a > 12`, a gap-6 shell pass, insertionSort) or 7 (`for b-a > 7`,
+    insertionSort alone). Process-wide (syzgpu_set_go_sort_leaf)."""
+    check(lib().syzgpu_set_go_sort_leaf(int(leaf)))
+
+
+def GoSortLeaf():
+    return int(lib().syzgpu_go_sort_leaf())
+
+
 def Minimize(corpus):
     """cover.go:105 — corpus is a list of covers; returns the kept indices in Go's order."""
     pcs, off = to_csr(corpus)

@@ -59,7 +59,14 @@ constexpr int LS_ISH = LS_ITEMS == 8 ? 3 : LS_ITEMS == 16 ? 4 : -1;  // log2(LS_
 static_assert((1 << LS_ISH) == LS_ITEMS, "LS_ISH");
 constexpr int LS_SH = 13;  // local index bits of the packed u32 LDS element (T_SEG = 2^13)
 static_assert((1u << LS_SH) == T_SEG, "LS_SH");
-constexpr uint32_t LS_MAXS = T_SEG / 13 + 4;  // active segments (> 12 elements) per pack
+// Go's quickSort leaf form (gosort_leaf, syzgpu_set_go_sort_leaf): GO_LEAF12 = `for b-a > 12`, then a
+// gap-6 shell pass + insertionSort (the default); GO_LEAF7 = `for b-a > 7`, then insertionSort alone.
+// Which one the reference's Go release used is not pinned by anything in the reference.
+constexpr int GO_LEAF12 = 12, GO_LEAF7 = 7;
+template <int LEAF>
+constexpr uint32_t ls_maxs() {  // active segments (> LEAF elements) per pack
+  return T_SEG / (LEAF + 1) + 4;
+}
 // Children of the global rounds at most this long go to the LDS sorter; longer ones take another
 // global round. Below T_SEG this trades one more (latency-bound) round for a shorter post-round LDS
 // launch. Measured at config 4 (step ms): 8192 0.850, 4096 0.892, 2048 0.931 - the LDS launch barely
@@ -281,7 +288,7 @@ __device__ bool wave_probe(P d, uint32_t lo, uint32_t hi, uint32_t m, uint32_t b
   return protect;
 }
 
-// quickSort's tail for 2..12 elements: gap-6 shell pass, then insertionSort.
+// quickSort's tail for 2..12 elements (the LEAF 12 form): gap-6 shell pass, then insertionSort.
 template <int SH, class P>
 __device__ void seq_leaf(P d, uint32_t a, uint32_t b) {
   for (uint32_t i = a + 6; i < b; i++)
@@ -313,10 +320,11 @@ __device__ void heap_sort(P d, uint32_t a, uint32_t b) {
   }
 }
 
-// The same leaf in registers: the shell pass swaps the disjoint pairs (i-6, i), and insertionSort
-// only moves an element past strictly Less ones, so it is the STABLE sort by Less: the element at i
-// lands at #{j : Less(j, i)} + #{j < i : equal}. Loads and stores are independent (no LDS chains).
-template <int SH, class P>
+// The same leaf in registers: the shell pass (LEAF 12 only) swaps the disjoint pairs (i-6, i), and
+// insertionSort only moves an element past strictly Less ones, so it is the STABLE sort by Less: the
+// element at i lands at #{j : Less(j, i)} + #{j < i : equal}. Loads and stores are independent (no LDS
+// chains).
+template <int SH, int LEAF, class P>
 __device__ void reg_leaf(P d, uint32_t a, uint32_t n) {
   using E = typename std::remove_reference<decltype(d[0])>::type;
   E x[12];
@@ -324,7 +332,7 @@ __device__ void reg_leaf(P d, uint32_t a, uint32_t n) {
   for (uint32_t i = 0; i < 12; i++) x[i] = i < n ? d[a + i] : (E)0;
 #pragma unroll
   for (uint32_t i = 6; i < 12; i++)
-    if (i < n && LT<SH>(x[i], x[i - 6])) {
+    if (LEAF == GO_LEAF12 && i < n && LT<SH>(x[i], x[i - 6])) {
       const E t = x[i];
       x[i] = x[i - 6];
       x[i - 6] = t;
@@ -344,10 +352,10 @@ __device__ void reg_leaf(P d, uint32_t a, uint32_t n) {
 }
 
 // A node of quickSort(data, lo, hi, depth) that is not a doPivot: leaf or depth-exhausted heapSort.
-template <int SH, class P>
+template <int SH, int LEAF, class P>
 __device__ void seq_terminal(P d, uint32_t lo, uint32_t hi, int32_t depth) {
-  if (hi - lo <= 12) {
-    if (hi - lo > 1) reg_leaf<SH>(d, lo, hi - lo);
+  if (hi - lo <= LEAF) {
+    if (hi - lo > 1) reg_leaf<SH, LEAF>(d, lo, hi - lo);
   } else if (depth == 0) {
     GS_STAT_ADD(8, 1);
     GS_STAT_ADD(9, hi - lo);
@@ -370,8 +378,9 @@ struct PadRef {
   __device__ __forceinline__ E& operator[](uint32_t i) const { return v[i + (i >> LS_ISH)]; }
 };
 
-template <class E>
+template <class E, int LEAF>
 struct LsLds {
+  static constexpr uint32_t LS_MAXS = ls_maxs<LEAF>();
   E dv[T_SEG + T_SEG / LS_ITEMS];
   __device__ __forceinline__ PadRef<E> D() { return PadRef<E>{dv}; }
   uint16_t bl[T_SEG];               // misplaced-right positions, at lo + rank from the right
@@ -382,7 +391,7 @@ struct LsLds {
   uint32_t pl[LS_MAXS], cnt[LS_MAXS];  // cnt: T | (#left before the range << 16) of the pass
   uint16_t m[LS_MAXS], bnd[LS_MAXS], b[LS_MAXS], c[LS_MAXS];
   uint8_t prot[LS_MAXS];
-  uint32_t wl[LS_MAXS];  // segments of 13..WQ elements for the wave sorter: lo | hi << 16
+  uint32_t wl[LS_MAXS];  // segments of LEAF+1..WQ elements for the wave sorter: lo | hi << 16
   int8_t wd[LS_MAXS];    // and their depth budget
   uint32_t red[LS_BLOCK / 64 + 1];
   uint32_t na, tot, flag, anyprot, nw;
@@ -555,7 +564,7 @@ __device__ void ls_partition(L& S, int cur, uint32_t na, uint32_t n, int mode) {
   (void)tq1; (void)tq2; (void)tq3;
 }
 
-// ---- wave sorter: a segment of 13..WQ elements finished by one wave, one element per lane ----------
+// ---- wave sorter: a segment of LEAF+1..WQ elements finished by one wave, one element per lane ---------
 // Level-synchronous inside the wave: every lane knows its segment [s, e) (lane-relative) and depth,
 // all segments of the subtree advance one quickSort node per iteration, and doPivot's steps are
 // ballots (counts, ranks), shuffles (pivot-of-nine, probe, partner exchange) and two per-wave LDS
@@ -597,7 +606,7 @@ __device__ __forceinline__ uint32_t wv_pass(E& v, uint32_t lane, bool act, uint3
   return bnd;
 }
 
-template <int SH, class E, class L>
+template <int SH, int LEAF, class E, class L>
 __device__ void wave_qs(L& S, uint32_t lo, uint32_t hi, int32_t dep0, uint8_t* slL, uint8_t* slR, E* slV) {
   const uint32_t lane = __lane_id(), n = hi - lo;
   E v = lane < n ? S.D()[lo + lane] : (E)0;
@@ -605,14 +614,14 @@ __device__ void wave_qs(L& S, uint32_t lo, uint32_t hi, int32_t dep0, uint8_t* s
   int32_t d = dep0;
   for (;;) {
     const uint32_t len = e > s ? e - s : 0u;
-    const bool leaf = len >= 2 && len <= 12;
-    const bool hp = len > 12 && d <= 0;
-    const bool act = len > 12 && d > 0;
-    if (__ballot(leaf)) {  // quickSort's tail: gap-6 shell pass (disjoint pairs), then insertionSort,
-                           // which is the stable sort by Less
+    const bool leaf = len >= 2 && len <= LEAF;
+    const bool hp = len > LEAF && d <= 0;
+    const bool act = len > LEAF && d > 0;
+    if (__ballot(leaf)) {  // quickSort's tail: (LEAF 12) gap-6 shell pass (disjoint pairs), then
+                           // insertionSort, which is the stable sort by Less
       const E up = __shfl(v, (int)(lane >= 6 ? lane - 6 : lane));
       const E dn = __shfl(v, (int)(lane + 6 < 64 ? lane + 6 : lane));
-      if (leaf) {
+      if (LEAF == GO_LEAF12 && leaf) {
         if (lane >= s + 6) {
           if (LT<SH>(v, up)) v = up;
         } else if (lane + 6 < e) {
@@ -742,13 +751,13 @@ __device__ __forceinline__ void ls_wave_push(L& S, uint32_t lo, uint32_t hi, int
   S.wd[i] = (int8_t)dep;
 }
 
-template <int SH, class E>
+template <int SH, class E, int LEAF>
 __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict__ el, uint32_t* __restrict__ perm,
                                                       const Pack* __restrict__ packs, uint32_t npacks_host,
                                                       const uint32_t* npacks_dev, const Seg* __restrict__ segs,
                                                       uint32_t* bounce_cnt, Pack* bounce) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  LsLds<E>& S = *reinterpret_cast<LsLds<E>*>(smem);
+  LsLds<E, LEAF>& S = *reinterpret_cast<LsLds<E, LEAF>*>(smem);
   constexpr uint64_t LEN_LIMIT = SH >= 32 ? ~0ull : (1ull << (sizeof(E) * 8 - SH));
   // packs == nullptr: the items are single segments segs[range[0] .. range[1]) (children of the global
   // levels, npacks_dev points at that range)
@@ -801,10 +810,10 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
           S.hi[0][o] = (uint16_t)hi;
           S.dep[0][o] = (int8_t)sg.depth;
           o++;
-        } else if (hi - lo > 12 && sg.depth > 0) {
+        } else if (hi - lo > LEAF && sg.depth > 0) {
           ls_wave_push(S, lo, hi, sg.depth);
         } else {
-          seq_terminal<SH>(S.D(), lo, hi, sg.depth);
+          seq_terminal<SH, LEAF>(S.D(), lo, hi, sg.depth);
         }
       }
       if (threadIdx.x == 0) S.na = tot;
@@ -861,11 +870,11 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
         swp(S.D(), lo, b - 1);
         S.b[s] = (uint16_t)mlo;  // reuse: child boundaries
         if (mlo - lo > WQ && dep > 0) cntA++;
-        else if (mlo - lo > 12 && dep > 0) ls_wave_push(S, lo, mlo, dep);
-        else seq_terminal<SH>(S.D(), lo, mlo, dep);
+        else if (mlo - lo > LEAF && dep > 0) ls_wave_push(S, lo, mlo, dep);
+        else seq_terminal<SH, LEAF>(S.D(), lo, mlo, dep);
         if (hi - mhi > WQ && dep > 0) cntA++;
-        else if (hi - mhi > 12 && dep > 0) ls_wave_push(S, mhi, hi, dep);
-        else seq_terminal<SH>(S.D(), mhi, hi, dep);
+        else if (hi - mhi > LEAF && dep > 0) ls_wave_push(S, mhi, hi, dep);
+        else seq_terminal<SH, LEAF>(S.D(), mhi, hi, dep);
       }
       uint32_t tot;
       uint32_t o = block_excl_scan<LS_BLOCK>(cntA, S.red, &tot);
@@ -906,7 +915,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_ls_sort(const uint64_t* __restrict
       uint8_t* scr = reinterpret_cast<uint8_t*>(S.bl) + w * (128 + 64 * sizeof(E));
       for (uint32_t it = w; it < nw; it += LS_BLOCK / 64) {
         const uint32_t x = S.wl[it];
-        wave_qs<SH, E>(S, x & 0xFFFFu, x >> 16, S.wd[it], scr, scr + 64, reinterpret_cast<E*>(scr + 128));
+        wave_qs<SH, LEAF, E>(S, x & 0xFFFFu, x >> 16, S.wd[it], scr, scr + 64, reinterpret_cast<E*>(scr + 128));
       }
       __syncthreads();
       if (threadIdx.x == 0) GS_STAT_ADD(11, nw);
@@ -1431,22 +1440,36 @@ __global__ void k_dyn_packs(const Seg* segs, const uint32_t* n, Pack* packs) {
 }
 
 // ---- host driver -------------------------------------------------------------------------------------
-template <int SH, class E>
-static void launch_ls(const uint64_t* el, uint32_t* perm, const Pack* packs, uint32_t npacks_host,
-                      const uint32_t* npacks_dev, unsigned grid, const Seg* segs, uint32_t* bounce_cnt, Pack* bounce,
-                      hipStream_t s) {
+template <int SH, class E, int LEAF>
+static void launch_ls_leaf(const uint64_t* el, uint32_t* perm, const Pack* packs, uint32_t npacks_host,
+                           const uint32_t* npacks_dev, unsigned grid, const Seg* segs, uint32_t* bounce_cnt,
+                           Pack* bounce, hipStream_t s) {
   static std::atomic<bool> attr[64];  // per device
   int dev = 0;
   SYZ_HIP(hipGetDevice(&dev));
   if (!attr[dev & 63].load()) {
-    SYZ_HIP(hipFuncSetAttribute((const void*)k_ls_sort<SH, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(LsLds<E>)));
+    SYZ_HIP(hipFuncSetAttribute((const void*)k_ls_sort<SH, E, LEAF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(LsLds<E, LEAF>)));
     attr[dev & 63] = true;
   }
   if (grid == 0) return;
-  k_ls_sort<SH, E><<<grid, LS_BLOCK, sizeof(LsLds<E>), s>>>(el, perm, packs, npacks_host, npacks_dev, segs,
-                                                            bounce_cnt, bounce);
+  k_ls_sort<SH, E, LEAF><<<grid, LS_BLOCK, sizeof(LsLds<E, LEAF>), s>>>(el, perm, packs, npacks_host, npacks_dev,
+                                                                        segs, bounce_cnt, bounce);
   SYZ_LAUNCHED();
+}
+
+// the process's leaf form (syzgpu_set_go_sort_leaf), read once per sort
+static std::atomic<int> g_go_leaf{GO_LEAF12};
+int gosort_leaf() { return g_go_leaf.load(); }
+
+template <int SH, class E>
+static void launch_ls(const uint64_t* el, uint32_t* perm, const Pack* packs, uint32_t npacks_host,
+                      const uint32_t* npacks_dev, unsigned grid, const Seg* segs, uint32_t* bounce_cnt, Pack* bounce,
+                      hipStream_t s, int leaf) {
+  if (leaf == GO_LEAF7)
+    launch_ls_leaf<SH, E, GO_LEAF7>(el, perm, packs, npacks_host, npacks_dev, grid, segs, bounce_cnt, bounce, s);
+  else
+    launch_ls_leaf<SH, E, GO_LEAF12>(el, perm, packs, npacks_host, npacks_dev, grid, segs, bounce_cnt, bounce, s);
 }
 
 // The static part of a sort over fixed call-group boundaries: which groups start the global levels,
@@ -1518,6 +1541,7 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
   Context& c = ctx();
   Scratch& sc = c.scratch;
   if (n >= 0xFFFFFFF0ull || n != P.n) fail(SYZGPU_EINVAL, "gosort: plan does not match the elements");
+  const int leaf = gosort_leaf();
   const uint32_t tch = t_child_host();
   const size_t maxseg = n / (tch / 2) + (size_t)P.nbig * 2 + 16;
   const size_t maxlds = n / 2 + 16;
@@ -1557,14 +1581,14 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     {
       ProfScope ps("gosort_lds_small", ss, (uint64_t)n * 12);
       launch_ls<LS_SH, uint32_t>(el, perm, d_packs, P.npacks, nullptr, std::min<uint32_t>(P.npacks, 65535), d_small,
-                              &ctl[2].nnext, bounceS, ss);
+                              &ctl[2].nnext, bounceS, ss, leaf);
     }
     // packs with a length that does not fit the u32 element (>= 2^19 PCs) were bounced: the u64
     // instantiation sorts them (a launch over an empty bounce list returns at once)
     // (skipped when no cover can bounce: even an empty launch of its 64 KB-LDS workgroups waits for whole
     // CUs while the transpose runs beside the sort)
     if (P.may_bounce)
-      launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, ss);
+      launch_ls<32, uint64_t>(el, perm, bounceS, 0, &ctl[2].nnext, 64, d_small, &ctl[3].nnext, bounceS, ss, leaf);
   }
   if (small_done) small_done(ss);
   if (fork) SYZ_HIP(hipEventRecord(c.ev_join, ss));
@@ -1734,15 +1758,23 @@ void gosort_run(uint64_t* el, uint32_t* perm, size_t n, const GosortPlan& P, hip
     // latency-bound level kernels need
     {
       ProfScope ps2("gosort_lds", bs, (uint64_t)n * 12);
-      launch_ls<LS_SH, uint32_t>(el, perm, nullptr, 0, &ctl[0].nnext, 1024, dlds, &ctl[2].nlds, bounceD, bs);
+      launch_ls<LS_SH, uint32_t>(el, perm, nullptr, 0, &ctl[0].nnext, 1024, dlds, &ctl[2].nlds, bounceD, bs, leaf);
     }
     if (P.may_bounce)
-      launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nlds, bounceD, bs);
+      launch_ls<32, uint64_t>(el, perm, bounceD, 0, &ctl[2].nlds, 64, dlds, &ctl[3].nlds, bounceD, bs, leaf);
   }
   if (big_done) big_done(bs);
   if (fork) SYZ_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
   (void)dpacks;
 }
+
+// (no device work and no lane: callable before syzgpu_init)
+extern "C" int syzgpu_set_go_sort_leaf(int leaf) {
+  if (leaf != GO_LEAF12 && leaf != GO_LEAF7) return SYZGPU_EINVAL;
+  g_go_leaf.store(leaf);
+  return SYZGPU_OK;
+}
+extern "C" int syzgpu_go_sort_leaf(void) { return g_go_leaf.load(); }
 
 #ifdef SYZ_GS_STATS
 extern "C" int syzgpu_debug_gosort_stats(unsigned long long* out, int reset) {

@@ -11,8 +11,10 @@ SENT = 0xFFFFFFFF
 
 # ---- Go sort.Sort over an index-addressed interface (less(i, j), swap(i, j)) -----------------
 class _Sorter:
-    def __init__(self, less, swap):
-        self.less, self.swap = less, swap
+    # leaf: the quickSort leaf form, 12 (`for b-a > 12`, gap-6 shell pass, insertionSort) or 7
+    # (`for b-a > 7`, insertionSort alone); see oracle/gosort.h
+    def __init__(self, less, swap, leaf=12):
+        self.less, self.swap, self.leaf = less, swap, leaf
 
     def insertion(self, a, b):
         for i in range(a + 1, b):
@@ -103,7 +105,7 @@ class _Sorter:
         return b - 1, c
 
     def quick_sort(self, a, b, max_depth):
-        while b - a > 12:
+        while b - a > self.leaf:
             if max_depth == 0:
                 self.heap_sort(a, b)
                 return
@@ -116,13 +118,14 @@ class _Sorter:
                 self.quick_sort(mhi, b, max_depth)
                 b = mlo
         if b - a > 1:
-            for i in range(a + 6, b):
-                if self.less(i, i - 6):
-                    self.swap(i, i - 6)
+            if self.leaf == 12:
+                for i in range(a + 6, b):
+                    if self.less(i, i - 6):
+                        self.swap(i, i - 6)
             self.insertion(a, b)
 
 
-def go_sort(data, less_key):
+def go_sort(data, less_key, leaf=12):
     def less(i, j):
         return less_key(data[i], data[j])
 
@@ -134,7 +137,7 @@ def go_sort(data, less_key):
     while i > 0:
         depth += 1
         i >>= 1
-    _Sorter(less, swap).quick_sort(0, n, depth * 2)
+    _Sorter(less, swap, leaf).quick_sort(0, n, depth * 2)
     return data
 
 
@@ -173,9 +176,9 @@ def setop(op, cov0, cov1):
     return res
 
 
-def minimize_order(lens):
+def minimize_order(lens, leaf=12):
     inputs = [(i, int(l)) for i, l in enumerate(lens)]
-    go_sort(inputs, lambda x, y: x[1] > y[1])
+    go_sort(inputs, lambda x, y: x[1] > y[1], leaf)
     return [i for i, _ in inputs]
 
 

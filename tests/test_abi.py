@@ -46,6 +46,19 @@ def test_library_reports_version_without_device():
     assert _lib.lib().syzgpu_version().startswith(b"syzgpu")
 
 
+def test_go_sort_leaf_setter_needs_no_device():
+    from syzkaller_amd import _lib
+    L = _lib.lib()
+    assert L.syzgpu_go_sort_leaf() == 12
+    assert L.syzgpu_set_go_sort_leaf(9) == _lib.EINVAL
+    assert L.syzgpu_go_sort_leaf() == 12
+    try:
+        assert L.syzgpu_set_go_sort_leaf(7) == 0
+        assert L.syzgpu_go_sort_leaf() == 7
+    finally:
+        assert L.syzgpu_set_go_sort_leaf(12) == 0
+
+
 def test_no_oracle_in_product_package():
     # the product package must never import or link the CPU oracle
     pkg = os.path.join(ROOT, "syzkaller_amd")

@@ -110,3 +110,45 @@ def test_order_persistent_rounds(kind, monkeypatch):
     monkeypatch.setenv("SYZGPU_GR_PGRID", "64")
     rnd = np.random.default_rng(13)
     _check_groups([_pattern(kind, 250_000, rnd), _pattern("saw", 40_000, rnd), _pattern(kind, 9000, rnd)])
+
+
+# ---- the other leaf form (syzgpu_set_go_sort_leaf(7): `for b-a > 7`, insertionSort alone) ----------
+@pytest.fixture
+def leaf7():
+    cover.SetGoSortLeaf(7)
+    oracle.set_go_sort_leaf(7)
+    try:
+        yield
+    finally:
+        cover.SetGoSortLeaf(12)
+        oracle.set_go_sort_leaf(12)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_order_leaf7_form(kind, leaf7):
+    # leaves of 2..7, the wave sorter from 8 elements, the LDS levels, the global levels' children
+    rnd = np.random.default_rng(17)
+    groups = [_pattern(kind, n, rnd) for n in [2, 7, 8, 9, 12, 13, 40, 41, 64, 65, 777, 4096, 9000, 65_537]]
+    _check_groups(groups)
+
+
+def test_minimize_corpus_leaf7_vs_oracle(leaf7):
+    # the raw minimizeCorpus pipeline with the leaf-7 tie order, bit-exact: three call groups above the
+    # LDS sorter's 8192 entries (global levels) and many small ones, cover lengths 1..6 (heavy ties)
+    rnd = np.random.default_rng(23)
+    sizes = [12_000, 9_500, 8_300] + [int(x) for x in rnd.integers(1, 300, size=40)]
+    group = np.concatenate([np.full(s, g, np.uint32) for g, s in enumerate(sizes)])
+    rnd.shuffle(group)
+    lens = rnd.integers(1, 7, size=group.size)
+    covs = [np.sort(rnd.choice(60, size=int(l), replace=False)).astype(np.uint32) + 1000 * np.uint32(g)
+            for l, g in zip(lens, group)]
+    pcs, off = cover.to_csr(covs)
+    got, goff = cover.MinimizeCorpus(pcs, off, group, len(sizes))
+    want, wgoff = oracle.minimize_grouped(pcs, off, group, len(sizes))
+    assert np.array_equal(goff, wgoff)
+    assert np.array_equal(got, want)
+    # the two forms differ on this corpus (else the test would not tell them apart)
+    cover.SetGoSortLeaf(12)
+    oracle.set_go_sort_leaf(12)
+    got12, _ = cover.MinimizeCorpus(pcs, off, group, len(sizes))
+    assert not np.array_equal(got12, got)

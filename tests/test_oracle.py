@@ -222,3 +222,23 @@ def test_oracle_call_cooccurrence_literal_pairs():
     np.cumsum([len(p) for p in progs], out=off[1:])
     calls = np.array([c for p in progs for c in p], np.uint16)
     assert np.array_equal(oracle.call_cooccurrence(calls, off, C), want)
+
+
+def test_go_sort_leaf_forms_oracle_vs_pyref():
+    # both leaf forms of the restated quickSort (oracle/gosort.h) against the pure-Python restatement,
+    # on tie-heavy lengths
+    rnd = np.random.default_rng(77)
+    try:
+        for leaf in (7, 12):
+            oracle.set_go_sort_leaf(leaf)
+            for n in [1, 2, 7, 8, 9, 12, 13, 20, 41, 200, 1500]:
+                for lenmax in [1, 2, 3, 6]:
+                    lens = rnd.integers(0, lenmax, size=n).astype(np.uint64)
+                    assert list(oracle.minimize_order(lens)) == pyref.minimize_order(list(lens), leaf=leaf), (leaf, n)
+        # the forms give different tie orders (8..12 elements with ties reach a doPivot under 7 only)
+        samples = [list(rnd.integers(0, 3, size=int(k))) for k in rnd.integers(8, 13, size=50)]
+        assert any(pyref.minimize_order(l, leaf=12) != pyref.minimize_order(l, leaf=7) for l in samples)
+        with pytest.raises(ValueError):
+            oracle.set_go_sort_leaf(9)
+    finally:
+        oracle.set_go_sort_leaf(12)
