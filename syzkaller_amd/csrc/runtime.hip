@@ -129,13 +129,16 @@ LaneGuard::LaneGuard(int device) {
     }
     return;
   }
+  // a requested lane (want_lane), for this call only
+  Context* const want_req = t_want;
+  const uint64_t want_gen = t_want_gen;
+  t_want = nullptr;
   std::unique_lock<std::mutex> lk(g_mu);
   try {
     if (g_device < 0) pick_device(device >= 0 ? device : 0);
     const int dev = device >= 0 ? device : g_device;
-    // a requested lane (want_lane) that still exists: wait for it, whatever else is free
-    Context* const want = t_want && t_want_gen == g_gen ? t_want : nullptr;
-    t_want = nullptr;
+    // the requested lane, when it still exists: wait for it, whatever else is free
+    Context* const want = want_req && want_gen == g_gen ? want_req : nullptr;
     for (;;) {
       size_t pick = g_lanes.size(), mine = 0, wanted = g_lanes.size();
       for (size_t i = 0; i < g_lanes.size(); i++)
