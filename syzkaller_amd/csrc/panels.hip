@@ -445,11 +445,25 @@ __device__ __forceinline__ void smin_hash(const PItem it, const SGroup* sg, cons
 #else
 #define SYZ_SMIN_LOOP 0  // one item per workgroup: no item loop in the kernels (the loop costs registers)
 #endif
+#ifndef SYZ_SMIN_XCD
+// > 0: M's items in XCD chunks of this many (m_items). 8: step 2.484-2.485 against 2.499-2.503 ms, 32:
+// 2.500-2.517 ms (profiles/r06_ab/r06_xcd_items_pm.log)
+#define SYZ_SMIN_XCD 8
+#endif
 template <class Fn>
 __device__ __forceinline__ void m_items(uint32_t nitems, uint32_t* ctr, Fn fn) {
   if (!SYZ_SMIN_LOOP) {
     (void)ctr;
-    if (blockIdx.x < nitems) fn(blockIdx.x);
+    uint32_t i = blockIdx.x;
+    if (SYZ_SMIN_XCD) {
+      // chunks of SYZ_SMIN_XCD consecutive items (windows of one call) on one XCD (blocks b and b + 8
+      // share one), chunk c on XCD c mod 8: the call's rank lines are re-read from that XCD's L2, and the
+      // heaviest items still go first on every XCD (the grid is a multiple of 8 chunks)
+      constexpr uint32_t K = SYZ_SMIN_XCD > 0 ? SYZ_SMIN_XCD : 1;
+      const uint32_t x = blockIdx.x & 7u, r = blockIdx.x >> 3;
+      i = ((r / K) * 8u + x) * K + r % K;
+    }
+    if (i < nitems) fn(i);
     return;
   }
   if (!ctr) {
@@ -525,6 +539,10 @@ static unsigned m_grid(size_t nitems, unsigned per_cu, unsigned ipw) {
   Context& c = ctx();
   if (SYZ_SMIN_PERSIST && !c.ncu) SYZ_HIP(hipDeviceGetAttribute(&c.ncu, hipDeviceAttributeMultiprocessorCount, c.device));
   const unsigned cap = SYZ_SMIN_PERSIST ? (unsigned)std::max(1, c.ncu) * per_cu : 0xFFFFFFFFu;
+  if (SYZ_SMIN_XCD && !SYZ_SMIN_LOOP) {  // (m_items: whole chunks on every XCD)
+    const size_t q = 8ull * (SYZ_SMIN_XCD > 0 ? SYZ_SMIN_XCD : 1);
+    return (unsigned)((nitems + q - 1) / q * q);
+  }
   return (unsigned)std::min<size_t>((nitems + ipw - 1) / ipw, cap);
 }
 // SYZ_SMIN_DYN: the launches that take their items from a counter (bit 0 / 1: direct small / big, 2 / 3:
