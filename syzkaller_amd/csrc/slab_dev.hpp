@@ -203,6 +203,13 @@ constexpr bool SL_RUNS = SYZ_SL_RUNS != 0;
 #ifndef SYZ_SL_PERSIST
 #define SYZ_SL_PERSIST 0  // P as a grid of resident workgroups (two per CU) walking the slabs
 #endif
+#ifndef SYZ_SL_XCDK
+// > 0: P's slabs in XCD chunks of this many, chunk k on XCD k mod 8 (blocks b and b + 8 share an XCD):
+// consecutive slabs' D words share lines, which then fill in one L2. 16: step 2.487-2.493 against
+// 2.521-2.532 ms; 64: 2.491-2.559 ms (profiles/r06_ab/r06_xcd_slab_chunks_pm.log). (All slabs of a launch
+// on one XCD each, consecutive, was slower: 2.62 vs 2.54 ms, r06_xcd_slabs_pm.log.)
+#define SYZ_SL_XCDK 16
+#endif
 #ifndef SYZ_SL_NOD
 #define SYZ_SL_NOD 0  // timing experiment only (results wrong when 1): P without its D-row stores
 #endif
@@ -258,7 +265,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   // SYZ_SL_SPW slabs per workgroup, as straight-line copies of the body (a loop spills, r06)
 #pragma unroll
   for (uint32_t q_ = 0; q_ < SYZ_SL_SPW; q_++) {
-    const uint64_t c = (uint64_t)blockIdx.x + (uint64_t)q_ * gridDim.x;
+    uint64_t c = (uint64_t)blockIdx.x + (uint64_t)q_ * gridDim.x;
+    if (SYZ_SL_XCDK) {  // chunks of SYZ_SL_XCDK consecutive slabs on one XCD, chunk k on XCD k mod 8
+      const uint32_t x = blockIdx.x & 7u, r = blockIdx.x >> 3;
+      c = ((uint64_t)(r / SYZ_SL_XCDK) * 8u + x) * SYZ_SL_XCDK + r % SYZ_SL_XCDK;
+    }
     if (c >= nsl) return;
     if (q_) __syncthreads();  // the staging buffer is free for the next slab
 #endif
@@ -494,6 +505,7 @@ inline void launch_slab(uint64_t nslabs, uint32_t Wmax, hipStream_t s, const uin
     }
   }
   unsigned grid = (unsigned)((nslabs + SYZ_SL_SPW - 1) / SYZ_SL_SPW);
+  if (SYZ_SL_XCDK) grid = (unsigned)((grid + 8u * SYZ_SL_XCDK - 1) / (8u * SYZ_SL_XCDK) * (8u * SYZ_SL_XCDK));
 #if SYZ_SL_PERSIST
   {
     int ncu = 0;
